@@ -1,0 +1,245 @@
+/*
+ * numamma_gpu.h -- C-ABI of the MI355X-native PEBS sample-analysis engine.
+ *
+ * Drop-in replacement for NumaMMa's offline buffer-processing loop:
+ *   - the body of mem_sampling_finalize()'s `while(samples)` loop
+ *     (src/mem_sampling.c:324-342) and everything it reaches
+ *     (__analyze_buffer :815-927, update_counters :517-592,
+ *      __match_sample :594-673, ma_find_mem_info_from_sample
+ *      src/mem_analyzer.c:249-306, ma_get_block :494-534,
+ *      ht_lower_key tools/hash.c:63-77);
+ *   - the report half of ma_finalize() (src/mem_analyzer.c:1813-1881:
+ *     update_call_sites, __print_counters, print_call_site_summary,
+ *     mem_sampling_statistics src/mem_sampling.c:357-361).
+ *
+ * Plain C, opaque handle, int status (0 = ok, < 0 = NMG_ERR_*), no exceptions
+ * and no HIP/torch types across the boundary.  The reference aborts on every
+ * error (e.g. mem_sampling.c:857-860); the engine returns a code instead and
+ * nmg_strerror() names it.
+ *
+ * Threading: one engine per calling thread; calls on one handle are not
+ * re-entrant.  The online/alarm path (SIGALRM, mem_sampling.c:130-139) must
+ * not call into the engine from a signal handler: enqueue there and call from
+ * a worker thread.
+ */
+#ifndef NUMAMMA_GPU_H
+#define NUMAMMA_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NMG_MAX_THREADS 1024 /* MAX_THREADS, src/numamma.h.in:9 */
+#define NMG_ACCESS_READ 0    /* enum access_type, src/mem_analyzer.h:43-47 */
+#define NMG_ACCESS_WRITE 1
+#define NMG_NB_BUCKETS 18 /* 9 hit + 9 miss levels of struct mem_counters */
+
+/* status codes */
+#define NMG_OK 0
+#define NMG_ERR_INVALID -1      /* bad argument / inconsistent table */
+#define NMG_ERR_HIP -2          /* HIP runtime failure (no GPU, OOM, ...) */
+#define NMG_ERR_NOMEM -3        /* host allocation failure */
+#define NMG_ERR_ZERO_SIZE -4    /* record with header.size == 0 (reference abort(), mem_sampling.c:857-860) */
+#define NMG_ERR_TRUNCATED -5    /* SAMPLE record running past the buffer end (reference reads out of bounds, :865-879) */
+#define NMG_ERR_STATE -6        /* call out of order (e.g. analyze before set_objects) */
+#define NMG_ERR_RANGE -7        /* thread rank >= nb_threads, buffer >= 4 GiB (unsigned cursors, :831-834) */
+#define NMG_ERR_CAPACITY -8     /* sparse page-histogram table full (raise nmg_options.sparse_capacity) */
+#define NMG_ERR_UNALIGNED -9    /* record size not a multiple of 8 (perf ABI guarantees 8-byte records) */
+#define NMG_ERR_IO -10          /* report file could not be written */
+
+/* engine flags */
+#define NMG_F_MATCH_SAMPLES 0x1  /* settings.match_samples (numamma.h.in:27) */
+#define NMG_F_PAGE_HIST 0x2      /* per-(object, page, thread) counts for callsite_counters_<id>.dat */
+#define NMG_F_OBJECT_LEVELS 0x4  /* per-object level buckets (count, sum) for callsite_summary_<id>.dat */
+#define NMG_F_DEFAULT (NMG_F_MATCH_SAMPLES | NMG_F_PAGE_HIST)
+
+/* struct count, src/mem_analyzer.h:10-15 */
+struct nmg_count {
+  uint64_t count, min_weight, max_weight, sum_weight;
+};
+
+/* struct mem_counters, src/mem_analyzer.h:17-41 (same 600-byte layout);
+ * b[0..8] = L1, L2, L3, LFB, local RAM, remote RAM, remote cache, IO,
+ * uncached hits; b[9..17] = the same levels' misses. */
+struct nmg_mem_counters {
+  uint64_t total_count, total_weight, na_miss_count;
+  struct nmg_count b[NMG_NB_BUCKETS];
+};
+
+/* One entry of the object table: the fields of struct memory_info
+ * (src/mem_analyzer.h:68-86) that sample attribution reads. */
+struct nmg_object {
+  uint64_t buffer_addr; /* current address (realloc rewrites it, quirk Q5) */
+  uint64_t buffer_size; /* size at free (ma_record_free, mem_analyzer.c:1287) */
+  uint64_t alloc_date;  /* 0 for globals / libs / [stack] */
+  uint64_t free_date;   /* after warn_non_freed_buffers (mem_analyzer.c:1751-1799) */
+};
+
+/* Host-only metadata of an entry, consumed by the call-site registry
+ * (find_call_site / new_call_site, mem_analyzer.c:1302-1378). */
+struct nmg_object_meta {
+  uint64_t initial_buffer_size;
+  uint64_t caller_rip;
+  const uint64_t *callstack; /* NULL == callstack_rip NULL */
+  int32_t callstack_size;
+  uint32_t mem_type; /* enum mem_type, mem_analyzer.h:58-64 (2 == stack) */
+  const char *caller; /* symbolised call site; NULL -> "???" for a NULL rip */
+  uint32_t id;
+  uint32_t reserved;
+};
+
+struct nmg_options {
+  int32_t device;            /* HIP device ordinal */
+  uint32_t flags;            /* NMG_F_* */
+  uint32_t nb_threads;       /* next_thread_rank: page-histogram columns (<= 1024) */
+  uint32_t reserved;
+  uint64_t hist_budget_bytes; /* dense page-histogram arena cap (0 = default 4 GiB) */
+  uint64_t sparse_capacity;   /* sparse (object, page, thread) slots (0 = default 1<<22) */
+};
+
+struct nmg_report_options {
+  const char *output_dir;  /* settings.output_dir; call_sites.log etc. land here */
+  int32_t dump_single_items; /* write callsite_counters_<id>.dat (default 1) */
+  int32_t reserved;
+};
+
+struct nmg_engine;
+typedef struct nmg_engine nmg_engine;
+
+const char *nmg_strerror(int status);
+int nmg_get_last_error_detail(nmg_engine *h, char *buf, size_t len);
+
+int nmg_create(nmg_engine **out, const struct nmg_options *opt);
+void nmg_destroy(nmg_engine *h);
+
+/*
+ * Object table snapshot: the AVL tree of mem_analyzer.c after
+ * warn_non_freed_buffers + ma_register_stack, flattened.  keys[] are the
+ * node keys in ascending order (unique); node i owns entries
+ * [entry_off[i], entry_off[i+1]) listed newest-first (the LIFO entry list of
+ * tools/hash.c:108-114).  Copied; the caller keeps ownership.
+ */
+int nmg_set_objects(nmg_engine *h, const uint64_t *keys, const uint32_t *entry_off,
+                    uint32_t nb_keys, const struct nmg_object *entries, uint32_t nb_entries);
+
+/*
+ * Append one captured buffer to the analysis list, in analysis order (the
+ * reference analyses `samples` head-first, i.e. newest capture first).
+ * nmg_submit_ring() linearises a perf ring segment [data_tail, data_head)
+ * exactly like __copy_buffer (mem_sampling.c:675-738); an empty segment is
+ * dropped, as the reference never pushes it.  Bytes are copied to pinned
+ * staging memory; the caller keeps ownership.
+ */
+int nmg_submit_ring(nmg_engine *h, const void *ring, uint64_t ring_size, uint64_t data_tail,
+                    uint64_t data_head, uint32_t thread_rank, uint32_t access_type);
+int nmg_submit_buffer(nmg_engine *h, const void *bytes, uint64_t len, uint32_t thread_rank,
+                      uint32_t access_type);
+
+/*
+ * Device-resident variant: linearised buffers already in HBM (caller-owned).
+ * offsets[] must be 16-byte aligned.  seq_base = analysis-order index of
+ * buffer 0 (non-zero when the buffer list is sharded over GPUs).  Replaces any
+ * previously submitted buffers.
+ */
+int nmg_set_device_buffers(nmg_engine *h, const void *d_data, const uint64_t *offsets,
+                           const uint64_t *lengths, const uint32_t *thread_ranks,
+                           const uint32_t *access_types, uint32_t nb_buffers, uint64_t seq_base);
+
+/* Enqueue attribution of every submitted buffer (stages host buffers H2D
+ * first).  Asynchronous; counters accumulate across calls. */
+int nmg_analyze(nmg_engine *h);
+int nmg_synchronize(nmg_engine *h);
+/* Zero every counter (global, per buffer, per object, page histogram). */
+int nmg_reset_counters(nmg_engine *h);
+/* Drop every submitted buffer (staging memory is kept for reuse). */
+int nmg_clear_buffers(nmg_engine *h);
+
+/* ---- results (synchronising, copied to host) ---- */
+int nmg_get_global_counters(nmg_engine *h, struct nmg_mem_counters out[2],
+                            uint64_t *nb_samples, uint64_t *nb_found);
+uint32_t nmg_get_nb_buffers(nmg_engine *h);
+/* per analysed buffer: SAMPLE records and matched samples */
+int nmg_get_buffer_counts(nmg_engine *h, uint32_t *nb_samples, uint32_t *nb_found);
+/* per entry: first-match ordinal ((analysis seq << 32) | byte offset,
+ * UINT64_MAX if never matched), and per access (count, weight) */
+int nmg_get_object_counters(nmg_engine *h, uint64_t *first_ordinal, uint64_t *count_weight /* [E][2][2] */);
+/* per entry and access: na_miss_count then 18 x (count, sum) [E][2][37] (NMG_F_OBJECT_LEVELS) */
+int nmg_get_object_levels(nmg_engine *h, uint64_t *levels);
+/* number of non-zero (entry, thread, page) cells */
+int64_t nmg_count_page_cells(nmg_engine *h);
+/* non-zero cells as (entry, thread, page, count) rows in (entry, thread, page) order */
+int nmg_get_page_cells(nmg_engine *h, uint32_t *rows /* [n][4] */, int64_t n);
+
+/* ---- multi-GPU merge (sharded buffer lists, one engine per rank) ----
+ * Arrays are exposed as flat u64 / u32 vectors so a caller can reduce them
+ * with RCCL (torch.distributed) over xGMI:
+ *   NMG_ARR_SUM64  : u64 sums   (global sums, per-object counts/weights/levels)
+ *   NMG_ARR_MIN64  : u64 mins   (global bucket mins, first-match ordinals, error word)
+ *   NMG_ARR_MAX64  : u64 maxes  (global bucket maxes)
+ *   NMG_ARR_HIST32 : u32 sums   (dense page histogram)
+ * nmg_export_array copies device -> device (dst is a device pointer),
+ * nmg_import_array copies back.  Sizes in elements. */
+#define NMG_ARR_SUM64 0
+#define NMG_ARR_MIN64 1
+#define NMG_ARR_MAX64 2
+#define NMG_ARR_HIST32 3
+uint64_t nmg_array_size(nmg_engine *h, int which);
+int nmg_export_array(nmg_engine *h, int which, void *d_dst);
+int nmg_import_array(nmg_engine *h, int which, const void *d_src);
+/* sparse (object, page, thread) cells: export as (key, count) pairs on host */
+int64_t nmg_sparse_count(nmg_engine *h);
+int nmg_sparse_export(nmg_engine *h, uint64_t *keys, uint32_t *counts, int64_t n);
+int nmg_sparse_import(nmg_engine *h, const uint64_t *keys, const uint32_t *counts, int64_t n);
+/* replace per-buffer counts with the whole job's (rank 0 before reporting) */
+int nmg_set_buffer_counts(nmg_engine *h, uint32_t nb_buffers, const uint32_t *nb_samples,
+                          const uint32_t *nb_found, const uint64_t *buffer_bytes);
+
+/* ---- device timing of the last nmg_analyze (HIP events on the engine stream) ---- */
+int nmg_last_analyze_ms(nmg_engine *h, float *ms);
+
+/*
+ * Report: the stdout text of mem_sampling_finalize + ma_finalize from
+ * "Analyzing %d sample buffers" to the final statistics line, written to
+ * stdout_path (NULL = process stdout), plus call_sites.log and
+ * callsite_counters_<id>.dat in opts->output_dir -- byte-identical formats
+ * (mem_analyzer.c:1438-1640, mem_sampling.c:321-361).
+ * meta[] parallels the entries passed to nmg_set_objects.
+ */
+int nmg_report(nmg_engine *h, const struct nmg_object_meta *meta,
+               const struct nmg_report_options *opts, const char *stdout_path);
+
+/*
+ * Host-only report from plain result arrays (no GPU needed): what rank 0 runs
+ * after a multi-GPU merge, and what nmg_report() calls internally.
+ * cells[] = (entry, thread, page, count) rows sorted by entry.
+ */
+struct nmg_host_results {
+  struct nmg_mem_counters global[2];
+  uint32_t nb_buffers;
+  uint32_t nb_entries;
+  const uint32_t *buf_samples; /* per analysed buffer (int in the reference) */
+  const uint32_t *buf_found;
+  const uint64_t *buf_bytes;
+  const uint64_t *buffer_size;   /* per entry: struct memory_info.buffer_size */
+  const uint64_t *first_ordinal; /* per entry, UINT64_MAX = never matched */
+  const uint64_t *count_weight;  /* [E][2][2] */
+  const uint32_t *cells;
+  int64_t nb_cells;
+  uint32_t nb_threads;    /* next_thread_rank */
+  uint32_t match_samples; /* settings.match_samples */
+};
+int nmg_report_host(const struct nmg_host_results *res, const struct nmg_object_meta *meta,
+                    const struct nmg_report_options *opts, const char *stdout_path);
+
+/* Convenience driver used by the nmg_replay CLI and the tests: load a replay
+ * file (DESIGN.md "Replay format"), analyse it on `device`, report. */
+int nmg_run_replay(const char *replay_path, const char *output_dir, const char *stdout_path,
+                   const char *raw_path, int device, uint32_t flags);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NUMAMMA_GPU_H */

@@ -1,0 +1,178 @@
+"""ctypes binding of the C-ABI in include/numamma_gpu.h.
+
+The shared library is built in-tree (numamma_amd/libnumamma_gpu.so, see
+numamma_amd/Makefile and __graft_entry__.build()).  There is no fallback: if
+the library is missing, importing this module raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libnumamma_gpu.so")
+HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "numamma_gpu.h")
+
+if not os.path.exists(LIB_PATH):
+    raise ImportError(
+        f"{LIB_PATH} is missing: build it with `make -C numamma_amd` or "
+        "`python -c 'import __graft_entry__ as g; g.build()'` (there is no CPU fallback)"
+    )
+lib = C.CDLL(LIB_PATH)
+
+NMG_OK = 0
+NMG_F_MATCH_SAMPLES = 0x1
+NMG_F_PAGE_HIST = 0x2
+NMG_F_OBJECT_LEVELS = 0x4
+NMG_F_DEFAULT = NMG_F_MATCH_SAMPLES | NMG_F_PAGE_HIST
+NMG_ARR_SUM64, NMG_ARR_MIN64, NMG_ARR_MAX64, NMG_ARR_HIST32 = range(4)
+ERRORS = {
+    -1: "NMG_ERR_INVALID",
+    -2: "NMG_ERR_HIP",
+    -3: "NMG_ERR_NOMEM",
+    -4: "NMG_ERR_ZERO_SIZE",
+    -5: "NMG_ERR_TRUNCATED",
+    -6: "NMG_ERR_STATE",
+    -7: "NMG_ERR_RANGE",
+    -8: "NMG_ERR_CAPACITY",
+    -9: "NMG_ERR_UNALIGNED",
+    -10: "NMG_ERR_IO",
+}
+
+
+class nmg_count(C.Structure):
+    _fields_ = [("count", C.c_uint64), ("min_weight", C.c_uint64), ("max_weight", C.c_uint64), ("sum_weight", C.c_uint64)]
+
+
+class nmg_mem_counters(C.Structure):
+    _fields_ = [
+        ("total_count", C.c_uint64),
+        ("total_weight", C.c_uint64),
+        ("na_miss_count", C.c_uint64),
+        ("b", nmg_count * 18),
+    ]
+
+
+class nmg_object(C.Structure):
+    _fields_ = [("buffer_addr", C.c_uint64), ("buffer_size", C.c_uint64), ("alloc_date", C.c_uint64), ("free_date", C.c_uint64)]
+
+
+class nmg_object_meta(C.Structure):
+    _fields_ = [
+        ("initial_buffer_size", C.c_uint64),
+        ("caller_rip", C.c_uint64),
+        ("callstack", C.POINTER(C.c_uint64)),
+        ("callstack_size", C.c_int32),
+        ("mem_type", C.c_uint32),
+        ("caller", C.c_char_p),
+        ("id", C.c_uint32),
+        ("reserved", C.c_uint32),
+    ]
+
+
+class nmg_options(C.Structure):
+    _fields_ = [
+        ("device", C.c_int32),
+        ("flags", C.c_uint32),
+        ("nb_threads", C.c_uint32),
+        ("reserved", C.c_uint32),
+        ("hist_budget_bytes", C.c_uint64),
+        ("sparse_capacity", C.c_uint64),
+    ]
+
+
+class nmg_report_options(C.Structure):
+    _fields_ = [("output_dir", C.c_char_p), ("dump_single_items", C.c_int32), ("reserved", C.c_int32)]
+
+
+class nmg_host_results(C.Structure):
+    _fields_ = [
+        ("global_", nmg_mem_counters * 2),
+        ("nb_buffers", C.c_uint32),
+        ("nb_entries", C.c_uint32),
+        ("buf_samples", C.POINTER(C.c_uint32)),
+        ("buf_found", C.POINTER(C.c_uint32)),
+        ("buf_bytes", C.POINTER(C.c_uint64)),
+        ("buffer_size", C.POINTER(C.c_uint64)),
+        ("first_ordinal", C.POINTER(C.c_uint64)),
+        ("count_weight", C.POINTER(C.c_uint64)),
+        ("cells", C.POINTER(C.c_uint32)),
+        ("nb_cells", C.c_int64),
+        ("nb_threads", C.c_uint32),
+        ("match_samples", C.c_uint32),
+    ]
+
+
+assert C.sizeof(nmg_mem_counters) == 600
+assert C.sizeof(nmg_object) == 32
+
+P = C.c_void_p
+u8p = C.POINTER(C.c_uint8)
+u32p = C.POINTER(C.c_uint32)
+u64p = C.POINTER(C.c_uint64)
+H = C.c_void_p  # nmg_engine*
+
+_SIGS = {
+    "nmg_strerror": (C.c_char_p, [C.c_int]),
+    "nmg_get_last_error_detail": (C.c_int, [H, C.c_char_p, C.c_size_t]),
+    "nmg_create": (C.c_int, [C.POINTER(H), C.POINTER(nmg_options)]),
+    "nmg_destroy": (None, [H]),
+    "nmg_set_objects": (C.c_int, [H, u64p, u32p, C.c_uint32, C.POINTER(nmg_object), C.c_uint32]),
+    "nmg_submit_ring": (C.c_int, [H, P, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32]),
+    "nmg_submit_buffer": (C.c_int, [H, P, C.c_uint64, C.c_uint32, C.c_uint32]),
+    "nmg_set_device_buffers": (C.c_int, [H, P, u64p, u64p, u32p, u32p, C.c_uint32, C.c_uint64]),
+    "nmg_analyze": (C.c_int, [H]),
+    "nmg_synchronize": (C.c_int, [H]),
+    "nmg_reset_counters": (C.c_int, [H]),
+    "nmg_clear_buffers": (C.c_int, [H]),
+    "nmg_get_global_counters": (C.c_int, [H, C.POINTER(nmg_mem_counters), u64p, u64p]),
+    "nmg_get_nb_buffers": (C.c_uint32, [H]),
+    "nmg_get_buffer_counts": (C.c_int, [H, u32p, u32p]),
+    "nmg_get_object_counters": (C.c_int, [H, u64p, u64p]),
+    "nmg_get_object_levels": (C.c_int, [H, u64p]),
+    "nmg_count_page_cells": (C.c_int64, [H]),
+    "nmg_get_page_cells": (C.c_int, [H, u32p, C.c_int64]),
+    "nmg_array_size": (C.c_uint64, [H, C.c_int]),
+    "nmg_export_array": (C.c_int, [H, C.c_int, P]),
+    "nmg_import_array": (C.c_int, [H, C.c_int, P]),
+    "nmg_sparse_count": (C.c_int64, [H]),
+    "nmg_sparse_export": (C.c_int, [H, u64p, u32p, C.c_int64]),
+    "nmg_sparse_import": (C.c_int, [H, u64p, u32p, C.c_int64]),
+    "nmg_set_buffer_counts": (C.c_int, [H, C.c_uint32, u32p, u32p, u64p]),
+    "nmg_last_analyze_ms": (C.c_int, [H, C.POINTER(C.c_float)]),
+    "nmg_report": (C.c_int, [H, C.POINTER(nmg_object_meta), C.POINTER(nmg_report_options), C.c_char_p]),
+    "nmg_report_host": (C.c_int, [C.POINTER(nmg_host_results), C.POINTER(nmg_object_meta), C.POINTER(nmg_report_options), C.c_char_p]),
+    "nmg_run_replay": (C.c_int, [C.c_char_p, C.c_char_p, C.c_char_p, C.c_char_p, C.c_int, C.c_uint32]),
+}
+
+for _name, (_res, _args) in _SIGS.items():
+    _fn = getattr(lib, _name)  # AttributeError == missing export: fail loudly
+    _fn.restype = _res
+    _fn.argtypes = _args
+
+
+def declared_symbols():
+    """Names of every function declared in include/numamma_gpu.h."""
+    import re
+
+    src = open(HEADER_PATH).read()
+    return sorted(set(re.findall(r"\b(nmg_[a-z_0-9]+)\s*\(", src)))
+
+
+class NmgError(RuntimeError):
+    def __init__(self, code: int, detail: str = ""):
+        self.code = code
+        name = ERRORS.get(code, str(code))
+        msg = lib.nmg_strerror(code).decode()
+        super().__init__(f"{name}: {msg}" + (f" ({detail})" if detail else ""))
+
+
+def check(rc: int, h=None) -> int:
+    if rc < 0:
+        detail = ""
+        if h:
+            buf = C.create_string_buffer(512)
+            lib.nmg_get_last_error_detail(h, buf, 512)
+            detail = buf.value.decode(errors="replace")
+        raise NmgError(rc, detail)
+    return rc

@@ -1,0 +1,1273 @@
+// nmg_engine.hip -- MI355X (gfx950) sample-attribution engine + C-ABI.
+//
+// Replaces NumaMMa's offline analysis loop (src/mem_sampling.c:311-346 ->
+// __analyze_buffer :815-927 -> update_counters :517-592 / __match_sample
+// :594-673 -> ma_find_mem_info_from_sample src/mem_analyzer.c:249-306 ->
+// ma_get_block :494-534).
+//
+// Kernel shape (DESIGN.md "Kernels"):
+//   * one workgroup owns one captured buffer at a time (persistent grid,
+//     round-robin over buffers) and walks it in 20 KiB LDS windows, so the
+//     record chain is followed exactly as the reference's byte cursor does
+//     (variable-size non-SAMPLE records, size==0 abort, truncation), while
+//     every HBM byte is read once with coalesced 16 B loads;
+//   * fast path: when every 40 B stride slot of a window is a 40 B record the
+//     whole window is decoded in parallel; otherwise lane 0 walks the headers
+//     in LDS and the window's SAMPLE offsets are processed in parallel;
+//   * global counters (mem_counters[2]) are privatised in LDS per buffer
+//     (wave-reduced sums, monotone min/max) and flushed once per buffer;
+//   * object lookup = LDS fence table -> binary search of the sorted key
+//     array in global (L2/MALL resident) -> LIFO entry scan with the
+//     inclusive timestamp window (quirks Q1-Q4);
+//   * per-object / per-page counters are u64/u32 atomics: integer adds,
+//     mins and maxes are order independent, so results are bit-exact.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "nmg_internal.h"
+
+namespace nmg {
+
+constexpr int kWG = 256;
+constexpr int kSegBytes = 20480;               // 512 x 40 B records per LDS window
+constexpr int kLdsBytes = kSegBytes + 64;      // + overlap: a record starting in the window has its 40 B
+constexpr int kMaxFences = 1024;               // LDS fence table (8 KiB)
+constexpr int kMaxList = kSegBytes / 8;        // slow path: record offsets of one window
+constexpr uint32_t kSampleType = 9;            // PERF_RECORD_SAMPLE
+constexpr uint32_t kRecBytes = 40;             // perf_event_header (8) + struct mem_sample (32)
+
+// PERF_MEM_LVL_* (/usr/include/linux/perf_event.h:1250-1263)
+constexpr uint32_t LVL_NA = 0x01, LVL_HIT = 0x02, LVL_MISS = 0x04;
+__constant__ uint32_t c_level_mask[9] = {0x08,  0x20,  0x40,  0x10,  0x80,
+                                         0x300, 0xC00, 0x1000, 0x2000};
+// order: L1, L2, L3, LFB, LOC_RAM, REM_RAM1|2, REM_CCE1|2, IO, UNC
+// (the bucket order of struct mem_counters, mem_analyzer.h:23-40)
+
+struct BufDesc {
+  uint64_t offset;  // byte offset in the data arena (16-aligned)
+  uint32_t len;     // linearised length (< 4 GiB, mem_sampling.c:831-834)
+  uint32_t thread_rank;
+  uint32_t access;
+  uint32_t pad;
+  uint64_t seq;  // analysis-order index (global across shards)
+};
+static_assert(sizeof(BufDesc) == 32, "BufDesc");
+
+struct DevEntry {
+  uint64_t addr;   // buffer_addr
+  uint64_t end;    // buffer_addr + buffer_size (mod 2^64, as the reference's void* sum)
+  uint64_t alloc;  // alloc_date
+  uint64_t free;   // free_date
+  uint64_t hist;   // dense histogram base cell, or kHistSparse
+  uint32_t sidx;   // sparse index (valid when hist == kHistSparse && sidx != ~0u)
+  uint32_t pad0;
+  uint64_t pad1[2];
+};
+static_assert(sizeof(DevEntry) == 64, "DevEntry");
+
+struct Params {
+  const uint8_t* data;
+  const BufDesc* bufs;
+  uint32_t nb_bufs;
+  uint32_t nb_keys;
+  const uint64_t* keys;
+  const uint32_t* entry_off;
+  const DevEntry* entries;
+  const uint64_t* fences;
+  uint32_t nb_fences;
+  uint32_t fence_step;
+  uint32_t nb_threads;
+  uint32_t flags;
+  uint32_t nb_entries;
+  uint32_t sparse_mask;  // capacity - 1 (power of two)
+  uint64_t* sum64;
+  uint64_t* min64;
+  uint64_t* max64;
+  uint32_t* hist;
+  uint32_t* bufcnt;  // [2][nb_bufs]: samples, found
+  uint64_t* sparse_keys;
+  uint32_t* sparse_vals;
+};
+
+// ---------------------------------------------------------------------------
+// device helpers
+
+__device__ __forceinline__ uint64_t wave_sum(uint64_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// Records are 8-byte multiples (sizes that are not are rejected), so every
+// record offset is 8-byte aligned in the 16-byte aligned LDS window.
+__device__ __forceinline__ uint64_t lds_u64(const uint8_t* s, uint32_t off) {
+  return *reinterpret_cast<const uint64_t*>(s + off);
+}
+
+__device__ __forceinline__ void set_error(Params& p, uint64_t seq, uint32_t off, uint32_t code) {
+  uint64_t w = (seq << 40) | (uint64_t(off) << 8) | code;
+  atomicMin(reinterpret_cast<unsigned long long*>(p.min64 + 36 + p.nb_entries),
+            (unsigned long long)w);
+}
+
+// Largest key <= addr (ht_lower_key, tools/hash.c:63-77): fence table in LDS,
+// then binary search of the fence's key bucket in global memory.
+__device__ __forceinline__ int64_t lower_key(const Params& p, const uint64_t* s_fences,
+                                             uint64_t addr) {
+  if (p.nb_fences == 0 || addr < s_fences[0]) return -1;
+  uint32_t lo = 0, hi = p.nb_fences - 1;
+  while (lo < hi) {
+    uint32_t mid = (lo + hi + 1) >> 1;
+    if (s_fences[mid] <= addr) lo = mid;
+    else hi = mid - 1;
+  }
+  if (p.fence_step == 1) return lo;
+  uint32_t klo = lo * p.fence_step;
+  uint32_t khi = min(klo + p.fence_step, p.nb_keys) - 1;
+  while (klo < khi) {
+    uint32_t mid = (klo + khi + 1) >> 1;
+    if (p.keys[mid] <= addr) klo = mid;
+    else khi = mid - 1;
+  }
+  return klo;
+}
+
+// __ma_find_mem_info_from_sample_generic (mem_analyzer.c:249-286) with
+// is_sample_in_buffer (:141-155): only the lower-bound node, newest entry first.
+__device__ __forceinline__ int64_t find_entry(const Params& p, const uint64_t* s_fences,
+                                              uint64_t addr, uint64_t ts, DevEntry* out) {
+  int64_t k = lower_key(p, s_fences, addr);
+  if (k < 0) return -1;
+  uint32_t e0 = p.entry_off[k], e1 = p.entry_off[k + 1];
+  for (uint32_t e = e0; e < e1; e++) {
+    const uint4* q = reinterpret_cast<const uint4*>(p.entries + e);
+    uint4 a = q[0], b = q[1];
+    uint64_t baddr = (uint64_t(a.y) << 32) | a.x;
+    uint64_t bend = (uint64_t(a.w) << 32) | a.z;
+    uint64_t alloc = (uint64_t(b.y) << 32) | b.x;
+    uint64_t fr = (uint64_t(b.w) << 32) | b.z;
+    if (baddr <= addr && addr < bend && alloc <= ts && ts <= fr) {
+      uint4 c = q[2];
+      out->addr = baddr;
+      out->hist = (uint64_t(c.y) << 32) | c.x;
+      out->sidx = c.z;
+      return e;
+    }
+  }
+  return -1;
+}
+
+__device__ __forceinline__ void sparse_add(Params& p, uint64_t key, uint64_t seq, uint32_t off) {
+  uint64_t h = (key * 0x9E3779B97F4A7C15ull) >> 20;
+  uint32_t slot = uint32_t(h) & p.sparse_mask;
+  for (uint32_t probe = 0; probe <= p.sparse_mask; probe++) {
+    unsigned long long prev = atomicCAS(reinterpret_cast<unsigned long long*>(p.sparse_keys + slot),
+                                        ~0ull, (unsigned long long)key);
+    if (prev == ~0ull || prev == key) {
+      atomicAdd(p.sparse_vals + slot, 1u);
+      return;
+    }
+    slot = (slot + 1) & p.sparse_mask;
+  }
+  set_error(p, seq, off, kErrCapacity);
+}
+
+// Per-workgroup privatised counters for the buffer being analysed.
+struct WgCounters {
+  unsigned long long sums[kGlobalSums];  // total_count, total_weight, na, 18 x (count, sum)
+  unsigned long long mins[18];
+  unsigned long long maxs[18];
+  unsigned int nb_samples, nb_found;
+};
+
+// Process one decoded record (`valid` = it is a SAMPLE).  Every lane of the
+// wave calls this together (wave-level reductions inside).
+__device__ __forceinline__ void process_sample(Params& p, WgCounters& wc, const uint64_t* s_fences,
+                                               bool valid, uint64_t ts, uint64_t addr,
+                                               uint64_t w, uint64_t dsrc, uint32_t access,
+                                               uint32_t th, uint64_t seq, uint32_t off) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t lvl = uint32_t(dsrc >> 5) & 0x3fff;  // data_src.mem_lvl
+  // ---- global counters: update_counters(global_counters, ...) (mem_sampling.c:882)
+  uint64_t vmask = __ballot(valid);
+  if (vmask == 0) return;
+  uint64_t wsum = wave_sum(valid ? w : 0);
+  uint64_t namask = __ballot(valid && (lvl & LVL_NA));
+  if (lane == 0) {
+    atomicAdd(&wc.sums[0], (unsigned long long)__popcll(vmask));
+    if (wsum) atomicAdd(&wc.sums[1], (unsigned long long)wsum);
+    if (namask) atomicAdd(&wc.sums[2], (unsigned long long)__popcll(namask));
+    atomicAdd(&wc.nb_samples, (unsigned)__popcll(vmask));
+  }
+#pragma unroll
+  for (int g = 0; g < 9; g++) {
+    bool has = valid && (lvl & c_level_mask[g]);
+    // HIT beats MISS; each level group is independent (quirk Q12)
+    int bucket = (lvl & LVL_HIT) ? g : ((lvl & LVL_MISS) ? 9 + g : -1);
+    bool in = has && bucket >= 0;
+    uint64_t m = __ballot(in);
+    if (m == 0) continue;
+    // buckets taken within a group differ only by HIT vs MISS
+    uint64_t mhit = __ballot(in && bucket == g);
+    uint64_t mmiss = m & ~mhit;
+    uint64_t shit = mhit ? wave_sum((in && bucket == g) ? w : 0) : 0;
+    uint64_t smiss = mmiss ? wave_sum((in && bucket != g) ? w : 0) : 0;
+    if (lane == 0) {
+      if (mhit) {
+        atomicAdd(&wc.sums[3 + 2 * g], (unsigned long long)__popcll(mhit));
+        if (shit) atomicAdd(&wc.sums[4 + 2 * g], (unsigned long long)shit);
+      }
+      if (mmiss) {
+        atomicAdd(&wc.sums[3 + 2 * (9 + g)], (unsigned long long)__popcll(mmiss));
+        if (smiss) atomicAdd(&wc.sums[4 + 2 * (9 + g)], (unsigned long long)smiss);
+      }
+    }
+    // min / max only move monotonically: read first, atomic only on improvement
+    if (in) {
+      if (w < wc.mins[bucket]) atomicMin(&wc.mins[bucket], (unsigned long long)w);
+      if (w > wc.maxs[bucket]) atomicMax(&wc.maxs[bucket], (unsigned long long)w);
+    }
+  }
+  if (!(p.flags & NMG_F_MATCH_SAMPLES)) return;
+
+  // ---- __match_sample (mem_sampling.c:594-673)
+  DevEntry ent;
+  int64_t e = valid ? find_entry(p, s_fences, addr, ts, &ent) : -1;
+  uint64_t fmask = __ballot(e >= 0);
+  if (lane == 0 && fmask) atomicAdd(&wc.nb_found, (unsigned)__popcll(fmask));
+  if (e < 0) return;
+  unsigned long long* cw = reinterpret_cast<unsigned long long*>(p.sum64 + objcw_index(e, access, 0));
+  atomicAdd(cw, 1ull);
+  if (w) atomicAdd(cw + 1, (unsigned long long)w);
+  // first match in analysis order -> call-site id order (quirk Q7)
+  uint64_t ord = (seq << 32) | off;
+  unsigned long long* fp = reinterpret_cast<unsigned long long*>(p.min64 + 36 + e);
+  if (ord < *fp) atomicMin(fp, (unsigned long long)ord);
+  if (p.flags & NMG_F_PAGE_HIST) {
+    // ma_get_block: page_no = (int)((addr - buffer_addr) / 4096) (mem_analyzer.c:530-531)
+    uint32_t page = uint32_t(int(uint64_t(addr - ent.addr) / kPageSize));
+    if (ent.hist != kHistSparse) {
+      atomicAdd(p.hist + ent.hist + uint64_t(page) * p.nb_threads + th, 1u);
+    } else if (ent.sidx != ~0u) {
+      sparse_add(p, sparse_key(ent.sidx, th, page), seq, off);
+    }
+  }
+  if (p.flags & NMG_F_OBJECT_LEVELS) {
+    unsigned long long* lv = reinterpret_cast<unsigned long long*>(
+        p.sum64 + 2 * kGlobalSums + uint64_t(p.nb_entries) * 4 + (uint64_t(e) * 2 + access) * kLevelWords);
+    if (lvl & LVL_NA) atomicAdd(lv, 1ull);
+    for (int g = 0; g < 9; g++) {
+      if (!(lvl & c_level_mask[g])) continue;
+      int bucket = (lvl & LVL_HIT) ? g : ((lvl & LVL_MISS) ? 9 + g : -1);
+      if (bucket < 0) continue;
+      atomicAdd(lv + 1 + 2 * bucket, 1ull);
+      if (w) atomicAdd(lv + 2 + 2 * bucket, (unsigned long long)w);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// the attribution kernel
+
+__global__ __launch_bounds__(kWG) void attribute_kernel(Params p) {
+  __shared__ __attribute__((aligned(16))) uint8_t s_data[kLdsBytes];
+  __shared__ uint64_t s_fences[kMaxFences];
+  __shared__ uint16_t s_list[kMaxList];
+  __shared__ WgCounters wc;
+  __shared__ uint32_t s_flag, s_nlist, s_next, s_err;
+
+  const int tid = threadIdx.x;
+  for (uint32_t i = tid; i < p.nb_fences; i += kWG) s_fences[i] = p.fences[i];
+
+  for (uint32_t b = blockIdx.x; b < p.nb_bufs; b += gridDim.x) {
+    const BufDesc d = p.bufs[b];
+    const uint8_t* base = p.data + d.offset;
+    const uint32_t len = d.len;
+    for (int i = tid; i < (int)kGlobalSums; i += kWG) wc.sums[i] = 0;
+    if (tid < 18) {
+      wc.mins[tid] = ~0ull;  // INIT_COUNTER: min = UINT64_MAX (mem_analyzer.c:415-420)
+      wc.maxs[tid] = 0;
+    }
+    if (tid == 0) {
+      wc.nb_samples = 0;
+      wc.nb_found = 0;
+      s_err = 0;
+    }
+    __syncthreads();
+
+    uint32_t cur = 0;  // byte cursor, as `cur_cpt` in __analyze_buffer
+    while (cur < len) {
+      const uint32_t win = cur & ~15u;
+      const uint32_t win_end = min(win + (uint32_t)kLdsBytes, (len + 15u) & ~15u);
+      // ---- stage the window into LDS: coalesced 16 B loads
+      const uint4* src = reinterpret_cast<const uint4*>(base + win);
+      uint4* dst = reinterpret_cast<uint4*>(s_data);
+      const uint32_t nchunks = (win_end - win) >> 4;
+      for (uint32_t c = tid; c < nchunks; c += kWG) dst[c] = src[c];
+      if (tid == 0) s_flag = 0;
+      __syncthreads();
+
+      const uint32_t seg_end = min(win + (uint32_t)kSegBytes, len);
+      const uint32_t n_cand = (seg_end - cur + kRecBytes - 1) / kRecBytes;
+      // ---- fast-path check: every 40 B stride slot holds a 40 B record
+      bool bad = (cur & 7) != 0;
+      for (uint32_t i = tid; i < n_cand && !bad; i += kWG) {
+        uint32_t pos = cur + i * kRecBytes;
+        uint64_t hdr = lds_u64(s_data, pos - win);
+        if ((hdr >> 48) != kRecBytes || pos + kRecBytes > len) bad = true;
+      }
+      if (bad) s_flag = 1;
+      __syncthreads();
+
+      if (s_flag == 0) {
+        // ---- fast path: decode all n_cand records in parallel
+        for (uint32_t i0 = 0; i0 < n_cand; i0 += kWG) {
+          uint32_t i = i0 + tid;
+          bool valid = false;
+          uint64_t ts = 0, addr = 0, w = 0, dsrc = 0;
+          uint32_t pos = cur + i * kRecBytes;
+          if (i < n_cand) {
+            uint32_t o = pos - win;
+            uint64_t hdr = lds_u64(s_data, o);
+            valid = uint32_t(hdr) == kSampleType;
+            ts = lds_u64(s_data, o + 8);
+            addr = lds_u64(s_data, o + 16);
+            w = lds_u64(s_data, o + 24);
+            dsrc = lds_u64(s_data, o + 32);
+          }
+          process_sample(p, wc, s_fences, valid, ts, addr, w, dsrc, d.access, d.thread_rank, d.seq, pos);
+        }
+        cur += n_cand * kRecBytes;
+      } else {
+        // ---- slow path: follow the header chain in LDS (lane 0), then
+        // process the window's SAMPLE records in parallel
+        if (tid == 0) {
+          uint32_t pos = cur, n = 0, err = 0;
+          while (pos < seg_end) {
+            if (uint64_t(pos) + 8 > len) { err = kErrTruncated; break; }
+            uint64_t hdr = lds_u64(s_data, pos - win);
+            uint32_t size = uint32_t(hdr >> 48);
+            if (size == 0) { err = kErrZeroSize; break; }  // mem_sampling.c:857-860
+            if (size & 7) { err = kErrUnaligned; break; }  // perf records are 8-byte multiples
+            if (uint32_t(hdr) == kSampleType) {
+              if (uint64_t(pos) + kRecBytes > len || uint64_t(pos) + size > len) {
+                err = kErrTruncated;
+                break;
+              }
+              s_list[n++] = uint16_t(pos - win);
+            }
+            pos += size;  // non-SAMPLE records are skipped by their size (:918)
+          }
+          if (err) {
+            set_error(p, d.seq, pos, err);
+            s_err = 1;
+          }
+          s_nlist = n;
+          s_next = pos;
+        }
+        __syncthreads();
+        const uint32_t n = s_nlist;
+        for (uint32_t i0 = 0; i0 < n; i0 += kWG) {
+          uint32_t i = i0 + tid;
+          bool valid = i < n;
+          uint64_t ts = 0, addr = 0, w = 0, dsrc = 0;
+          uint32_t o = valid ? s_list[i] : 0;
+          if (valid) {
+            ts = lds_u64(s_data, o + 8);
+            addr = lds_u64(s_data, o + 16);
+            w = lds_u64(s_data, o + 24);
+            dsrc = lds_u64(s_data, o + 32);
+          }
+          process_sample(p, wc, s_fences, valid, ts, addr, w, dsrc, d.access, d.thread_rank, d.seq,
+                         win + o);
+        }
+        cur = s_next;
+        if (s_err) break;  // the reference aborts here; stop this buffer
+      }
+      __syncthreads();  // LDS window is rewritten next iteration
+    }
+    __syncthreads();
+
+    // ---- flush the buffer's counters (one set per access type)
+    const uint32_t a = d.access;
+    for (int i = tid; i < (int)kGlobalSums; i += kWG)
+      if (wc.sums[i]) atomicAdd(reinterpret_cast<unsigned long long*>(p.sum64 + gsum_index(a, i)), wc.sums[i]);
+    if (tid < 18 && wc.sums[3 + 2 * tid]) {
+      atomicMin(reinterpret_cast<unsigned long long*>(p.min64 + a * 18 + tid), wc.mins[tid]);
+      atomicMax(reinterpret_cast<unsigned long long*>(p.max64 + a * 18 + tid), wc.maxs[tid]);
+    }
+    if (tid == 0) {
+      atomicAdd(p.bufcnt + b, wc.nb_samples);
+      atomicAdd(p.bufcnt + p.nb_bufs + b, wc.nb_found);
+    }
+    __syncthreads();
+  }
+}
+
+}  // namespace nmg
+
+// ===========================================================================
+// host side
+
+using namespace nmg;
+
+struct nmg_engine {
+  int device = 0;
+  uint32_t flags = NMG_F_DEFAULT;
+  uint32_t T = 1;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  int num_cus = 256;
+  bool launched = false;
+
+  // object table
+  bool have_table = false;
+  uint32_t K = 0, E = 0;
+  uint64_t* d_keys = nullptr;
+  uint32_t* d_entry_off = nullptr;
+  DevEntry* d_entries = nullptr;
+  uint64_t* d_fences = nullptr;
+  uint32_t nb_fences = 0, fence_step = 1;
+  std::vector<uint64_t> hist_base, npages, buffer_size;
+  std::vector<uint32_t> sparse_entries;
+  uint64_t hist_cells = 0;
+  uint64_t hist_budget = 4ull << 30;
+  uint64_t sparse_cap = 1u << 20;
+
+  // counters
+  uint64_t *d_sum64 = nullptr, *d_min64 = nullptr, *d_max64 = nullptr;
+  uint64_t n_sum64 = 0, n_min64 = 0, n_max64 = 0;
+  uint32_t* d_hist = nullptr;
+  uint64_t* d_sparse_keys = nullptr;
+  uint32_t* d_sparse_vals = nullptr;
+
+  // buffers
+  std::vector<BufDesc> descs;
+  std::vector<uint64_t> buf_bytes;
+  uint8_t* h_stage = nullptr;
+  size_t stage_cap = 0, stage_len = 0;
+  uint8_t* d_arena = nullptr;
+  size_t arena_cap = 0;
+  const uint8_t* d_data = nullptr;
+  bool external = false;
+  bool staged_dirty = false;
+  BufDesc* d_descs = nullptr;
+  size_t descs_cap = 0;
+  bool descs_dirty = false;
+  uint32_t* d_bufcnt = nullptr;
+  size_t bufcnt_cap = 0;
+
+  // multi-GPU override of per-buffer counts (rank 0 reporting)
+  bool counts_override = false;
+  std::vector<uint32_t> ov_samples, ov_found;
+  std::vector<uint64_t> ov_bytes;
+
+  std::string last_error;
+  float last_ms = 0.f;
+};
+
+#define HIP_TRY(h, expr)                                                        \
+  do {                                                                          \
+    hipError_t _e = (expr);                                                     \
+    if (_e != hipSuccess) {                                                     \
+      (h)->last_error = std::string(#expr) + ": " + hipGetErrorString(_e);      \
+      return NMG_ERR_HIP;                                                       \
+    }                                                                           \
+  } while (0)
+
+static int fail(nmg_engine* h, int code, const std::string& msg) {
+  if (h) h->last_error = msg;
+  return code;
+}
+
+namespace nmg {
+uint32_t engine_nb_threads(nmg_engine* h) { return h->T; }
+uint32_t engine_nb_entries(nmg_engine* h) { return h->E; }
+uint32_t engine_flags(nmg_engine* h) { return h->flags; }
+const std::vector<uint64_t>& engine_hist_base(nmg_engine* h) { return h->hist_base; }
+const std::vector<uint64_t>& engine_npages(nmg_engine* h) { return h->npages; }
+const std::vector<uint32_t>& engine_sparse_entries(nmg_engine* h) { return h->sparse_entries; }
+void engine_set_error(nmg_engine* h, const std::string& msg) { h->last_error = msg; }
+}  // namespace nmg
+
+extern "C" const char* nmg_strerror(int status) {
+  switch (status) {
+    case NMG_OK: return "ok";
+    case NMG_ERR_INVALID: return "invalid argument";
+    case NMG_ERR_HIP: return "HIP runtime error";
+    case NMG_ERR_NOMEM: return "out of host memory";
+    case NMG_ERR_ZERO_SIZE: return "record with size 0 (the reference aborts, mem_sampling.c:857-860)";
+    case NMG_ERR_TRUNCATED: return "SAMPLE record truncated at the end of its buffer";
+    case NMG_ERR_STATE: return "call out of order";
+    case NMG_ERR_RANGE: return "value out of range (thread rank, buffer size)";
+    case NMG_ERR_CAPACITY: return "sparse page-histogram table full";
+    case NMG_ERR_UNALIGNED: return "record size not a multiple of 8";
+    case NMG_ERR_IO: return "report file could not be written";
+    default: return "unknown error";
+  }
+}
+
+extern "C" int nmg_get_last_error_detail(nmg_engine* h, char* buf, size_t len) {
+  if (!h || !buf || !len) return NMG_ERR_INVALID;
+  snprintf(buf, len, "%s", h->last_error.c_str());
+  return NMG_OK;
+}
+
+static void free_counters(nmg_engine* h) {
+  (void)hipFree(h->d_sum64);
+  (void)hipFree(h->d_min64);
+  (void)hipFree(h->d_max64);
+  (void)hipFree(h->d_hist);
+  (void)hipFree(h->d_sparse_keys);
+  (void)hipFree(h->d_sparse_vals);
+  h->d_sum64 = h->d_min64 = h->d_max64 = nullptr;
+  h->d_hist = nullptr;
+  h->d_sparse_keys = nullptr;
+  h->d_sparse_vals = nullptr;
+}
+
+static void free_table(nmg_engine* h) {
+  (void)hipFree(h->d_keys);
+  (void)hipFree(h->d_entry_off);
+  (void)hipFree(h->d_entries);
+  (void)hipFree(h->d_fences);
+  h->d_keys = nullptr;
+  h->d_entry_off = nullptr;
+  h->d_entries = nullptr;
+  h->d_fences = nullptr;
+}
+
+extern "C" int nmg_create(nmg_engine** out, const nmg_options* opt) {
+  if (!out) return NMG_ERR_INVALID;
+  *out = nullptr;
+  nmg_engine* h = new (std::nothrow) nmg_engine();
+  if (!h) return NMG_ERR_NOMEM;
+  if (opt) {
+    h->device = opt->device;
+    h->flags = opt->flags;
+    h->T = opt->nb_threads ? opt->nb_threads : 1;
+    if (opt->hist_budget_bytes) h->hist_budget = opt->hist_budget_bytes;
+    if (opt->sparse_capacity) {
+      uint64_t c = 1;
+      while (c < opt->sparse_capacity) c <<= 1;
+      h->sparse_cap = c;
+    }
+  }
+  if (h->T > NMG_MAX_THREADS || h->sparse_cap > (1ull << 31)) {
+    delete h;
+    return NMG_ERR_RANGE;
+  }
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0 || h->device < 0 || h->device >= ndev) {
+    delete h;
+    return NMG_ERR_HIP;
+  }
+  if (hipSetDevice(h->device) != hipSuccess || hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreate(&h->ev0) != hipSuccess || hipEventCreate(&h->ev1) != hipSuccess) {
+    delete h;
+    return NMG_ERR_HIP;
+  }
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, h->device) == hipSuccess) h->num_cus = prop.multiProcessorCount;
+  *out = h;
+  return NMG_OK;
+}
+
+extern "C" void nmg_destroy(nmg_engine* h) {
+  if (!h) return;
+  (void)hipSetDevice(h->device);
+  if (h->stream) (void)hipStreamSynchronize(h->stream);
+  free_table(h);
+  free_counters(h);
+  (void)hipFree(h->d_arena);
+  (void)hipFree(h->d_descs);
+  (void)hipFree(h->d_bufcnt);
+  if (h->h_stage) (void)hipHostFree(h->h_stage);
+  if (h->ev0) (void)hipEventDestroy(h->ev0);
+  if (h->ev1) (void)hipEventDestroy(h->ev1);
+  if (h->stream) (void)hipStreamDestroy(h->stream);
+  delete h;
+}
+
+extern "C" int nmg_reset_counters(nmg_engine* h) {
+  if (!h) return NMG_ERR_INVALID;
+  if (!h->have_table) return fail(h, NMG_ERR_STATE, "nmg_reset_counters before nmg_set_objects");
+  HIP_TRY(h, hipSetDevice(h->device));
+  HIP_TRY(h, hipMemsetAsync(h->d_sum64, 0, h->n_sum64 * 8, h->stream));
+  HIP_TRY(h, hipMemsetAsync(h->d_min64, 0xff, h->n_min64 * 8, h->stream));
+  HIP_TRY(h, hipMemsetAsync(h->d_max64, 0, h->n_max64 * 8, h->stream));
+  if (h->hist_cells) HIP_TRY(h, hipMemsetAsync(h->d_hist, 0, h->hist_cells * 4, h->stream));
+  if (h->d_sparse_keys) {
+    HIP_TRY(h, hipMemsetAsync(h->d_sparse_keys, 0xff, h->sparse_cap * 8, h->stream));
+    HIP_TRY(h, hipMemsetAsync(h->d_sparse_vals, 0, h->sparse_cap * 4, h->stream));
+  }
+  // (a pending descriptor upload zeroes the per-buffer counts itself)
+  if (h->d_bufcnt && !h->descs_dirty && !h->descs.empty() && h->descs.size() <= h->descs_cap)
+    HIP_TRY(h, hipMemsetAsync(h->d_bufcnt, 0, h->descs.size() * 2 * 4, h->stream));
+  return NMG_OK;
+}
+
+extern "C" int nmg_set_objects(nmg_engine* h, const uint64_t* keys, const uint32_t* entry_off,
+                               uint32_t nb_keys, const nmg_object* entries, uint32_t nb_entries) {
+  if (!h || (nb_keys && (!keys || !entry_off)) || (nb_entries && !entries))
+    return NMG_ERR_INVALID;
+  if (entry_off && (entry_off[0] != 0 || entry_off[nb_keys] != nb_entries))
+    return fail(h, NMG_ERR_INVALID, "entry_off[0] must be 0 and entry_off[nb_keys] == nb_entries");
+  for (uint32_t i = 0; i < nb_keys; i++) {
+    if (entry_off[i + 1] <= entry_off[i]) return fail(h, NMG_ERR_INVALID, "every key needs >= 1 entry");
+    if (i && keys[i] <= keys[i - 1]) return fail(h, NMG_ERR_INVALID, "keys must be strictly ascending");
+  }
+  if (nb_entries >= (1u << 31)) return fail(h, NMG_ERR_RANGE, "too many entries");
+  HIP_TRY(h, hipSetDevice(h->device));
+  HIP_TRY(h, hipStreamSynchronize(h->stream));
+  free_table(h);
+  free_counters(h);
+  h->K = nb_keys;
+  h->E = nb_entries;
+
+  // page-histogram layout: dense [page][thread] block per entry within the
+  // budget, otherwise sparse hashed cells (e.g. the 412 GB [stack] range)
+  const uint64_t T = h->T;
+  const uint64_t max_cells_per_entry = 1ull << 24;
+  h->hist_base.assign(nb_entries, kHistSparse);
+  h->npages.resize(nb_entries);
+  h->buffer_size.resize(nb_entries);
+  h->sparse_entries.clear();
+  h->hist_cells = 0;
+  std::vector<DevEntry> dev(nb_entries);
+  const bool want_hist = (h->flags & NMG_F_PAGE_HIST) && (h->flags & NMG_F_MATCH_SAMPLES);
+  const uint64_t budget_cells = h->hist_budget / 4;
+  for (uint32_t e = 0; e < nb_entries; e++) {
+    const nmg_object& o = entries[e];
+    DevEntry& d = dev[e];
+    memset(&d, 0, sizeof(d));
+    d.addr = o.buffer_addr;
+    d.end = o.buffer_addr + o.buffer_size;
+    d.alloc = o.alloc_date;
+    d.free = o.free_date;
+    uint64_t np = o.buffer_size / kPageSize + 1;
+    h->npages[e] = np;
+    h->buffer_size[e] = o.buffer_size;
+    d.hist = kHistSparse;
+    d.sidx = ~0u;
+    if (!want_hist) continue;
+    uint64_t cells = np * T;
+    if (cells <= max_cells_per_entry && h->hist_cells + cells <= budget_cells) {
+      d.hist = h->hist_cells;
+      h->hist_base[e] = h->hist_cells;
+      h->hist_cells += cells;
+    } else {
+      if (h->sparse_entries.size() >= (1u << 22)) return fail(h, NMG_ERR_CAPACITY, "too many sparse entries");
+      d.sidx = (uint32_t)h->sparse_entries.size();
+      h->sparse_entries.push_back(e);
+    }
+  }
+  // LDS fence table: every fence_step-th key
+  h->fence_step = 1;
+  while ((uint64_t)nb_keys > (uint64_t)h->fence_step * kMaxFences) h->fence_step++;
+  h->nb_fences = nb_keys ? (nb_keys + h->fence_step - 1) / h->fence_step : 0;
+  std::vector<uint64_t> fences(h->nb_fences);
+  for (uint32_t f = 0; f < h->nb_fences; f++) fences[f] = keys[(uint64_t)f * h->fence_step];
+
+  auto alloc_copy = [&](void** dptr, const void* src, size_t bytes) -> hipError_t {
+    hipError_t e = hipMalloc(dptr, bytes ? bytes : 16);
+    if (e != hipSuccess) return e;
+    if (bytes) return hipMemcpyAsync(*dptr, src, bytes, hipMemcpyHostToDevice, h->stream);
+    return hipSuccess;
+  };
+  HIP_TRY(h, alloc_copy((void**)&h->d_keys, keys, (size_t)nb_keys * 8));
+  std::vector<uint32_t> off0;
+  if (!entry_off) off0.assign(1, 0);
+  HIP_TRY(h, alloc_copy((void**)&h->d_entry_off, entry_off ? entry_off : off0.data(), ((size_t)nb_keys + 1) * 4));
+  HIP_TRY(h, alloc_copy((void**)&h->d_entries, dev.data(), (size_t)nb_entries * sizeof(DevEntry)));
+  HIP_TRY(h, alloc_copy((void**)&h->d_fences, fences.data(), fences.size() * 8));
+
+  h->n_sum64 = 2 * kGlobalSums + (uint64_t)nb_entries * 4;
+  if (h->flags & NMG_F_OBJECT_LEVELS) h->n_sum64 += (uint64_t)nb_entries * 2 * kLevelWords;
+  h->n_min64 = 36 + (uint64_t)nb_entries + 1;
+  h->n_max64 = 36;
+  HIP_TRY(h, hipMalloc(&h->d_sum64, h->n_sum64 * 8));
+  HIP_TRY(h, hipMalloc(&h->d_min64, h->n_min64 * 8));
+  HIP_TRY(h, hipMalloc(&h->d_max64, h->n_max64 * 8));
+  if (h->hist_cells) HIP_TRY(h, hipMalloc(&h->d_hist, h->hist_cells * 4));
+  if (!h->sparse_entries.empty()) {
+    HIP_TRY(h, hipMalloc(&h->d_sparse_keys, h->sparse_cap * 8));
+    HIP_TRY(h, hipMalloc(&h->d_sparse_vals, h->sparse_cap * 4));
+  }
+  h->have_table = true;
+  HIP_TRY(h, hipStreamSynchronize(h->stream));
+  return nmg_reset_counters(h);
+}
+
+static int stage_reserve(nmg_engine* h, size_t need) {
+  if (need <= h->stage_cap) return NMG_OK;
+  size_t cap = std::max(need, h->stage_cap * 2 + (1u << 20));
+  uint8_t* p = nullptr;
+  HIP_TRY(h, hipHostMalloc((void**)&p, cap, hipHostMallocDefault));
+  if (h->stage_len) memcpy(p, h->h_stage, h->stage_len);
+  if (h->h_stage) {
+    HIP_TRY(h, hipStreamSynchronize(h->stream));
+    (void)hipHostFree(h->h_stage);
+  }
+  h->h_stage = p;
+  h->stage_cap = cap;
+  return NMG_OK;
+}
+
+static int append_desc(nmg_engine* h, uint64_t len, uint32_t thread_rank, uint32_t access) {
+  BufDesc d;
+  d.offset = h->stage_len;
+  d.len = (uint32_t)len;
+  d.thread_rank = thread_rank;
+  d.access = access;
+  d.pad = 0;
+  d.seq = h->descs.size();
+  h->descs.push_back(d);
+  h->buf_bytes.push_back(len);
+  h->stage_len = (h->stage_len + len + 15) & ~size_t(15);
+  h->staged_dirty = true;
+  h->descs_dirty = true;
+  return NMG_OK;
+}
+
+static int check_buffer_args(nmg_engine* h, uint64_t len, uint32_t thread_rank, uint32_t access) {
+  if (access > 1) return fail(h, NMG_ERR_INVALID, "access_type must be 0 (read) or 1 (write)");
+  if (thread_rank >= h->T)
+    return fail(h, NMG_ERR_RANGE, "thread_rank >= nb_threads (set nmg_options.nb_threads)");
+  if (len >= (1ull << 32)) return fail(h, NMG_ERR_RANGE, "buffer >= 4 GiB (unsigned cursors, mem_sampling.c:831-834)");
+  if (h->external) return fail(h, NMG_ERR_STATE, "device buffers are set; call nmg_clear_buffers first");
+  return NMG_OK;
+}
+
+extern "C" int nmg_submit_buffer(nmg_engine* h, const void* bytes, uint64_t len, uint32_t thread_rank,
+                                 uint32_t access_type) {
+  if (!h || (len && !bytes)) return NMG_ERR_INVALID;
+  int rc = check_buffer_args(h, len, thread_rank, access_type);
+  if (rc) return rc;
+  if (len == 0) return NMG_OK;  // __copy_buffer drops empty segments (mem_sampling.c:680-682)
+  rc = stage_reserve(h, h->stage_len + len + 16);
+  if (rc) return rc;
+  memcpy(h->h_stage + h->stage_len, bytes, len);
+  return append_desc(h, len, thread_rank, access_type);
+}
+
+extern "C" int nmg_submit_ring(nmg_engine* h, const void* ring, uint64_t ring_size, uint64_t data_tail,
+                               uint64_t data_head, uint32_t thread_rank, uint32_t access_type) {
+  if (!h || !ring || data_tail > ring_size || data_head > ring_size) return NMG_ERR_INVALID;
+  if (data_head == data_tail) return NMG_OK;  // nothing to do (mem_sampling.c:680-682)
+  uint64_t len = data_head - data_tail;
+  if (data_head < data_tail) len = ring_size - data_tail + data_head;  // :687-694
+  int rc = check_buffer_args(h, len, thread_rank, access_type);
+  if (rc) return rc;
+  rc = stage_reserve(h, h->stage_len + len + 16);
+  if (rc) return rc;
+  const uint8_t* r = (const uint8_t*)ring;
+  uint8_t* dst = h->h_stage + h->stage_len;
+  if (data_head < data_tail) {  // :704-713: two segments
+    uint64_t first = ring_size - data_tail;
+    memcpy(dst, r + data_tail, first);
+    memcpy(dst + first, r, data_head);
+  } else {
+    memcpy(dst, r + data_tail, len);
+  }
+  return append_desc(h, len, thread_rank, access_type);
+}
+
+extern "C" int nmg_set_device_buffers(nmg_engine* h, const void* d_data, const uint64_t* offsets,
+                                      const uint64_t* lengths, const uint32_t* thread_ranks,
+                                      const uint32_t* access_types, uint32_t nb_buffers, uint64_t seq_base) {
+  if (!h || (nb_buffers && (!d_data || !offsets || !lengths || !thread_ranks || !access_types)))
+    return NMG_ERR_INVALID;
+  std::vector<BufDesc> descs;
+  std::vector<uint64_t> bytes;
+  descs.reserve(nb_buffers);
+  for (uint32_t b = 0; b < nb_buffers; b++) {
+    if (offsets[b] & 15) return fail(h, NMG_ERR_INVALID, "device buffer offsets must be 16-byte aligned");
+    if (access_types[b] > 1) return fail(h, NMG_ERR_INVALID, "access_type must be 0 or 1");
+    if (thread_ranks[b] >= h->T) return fail(h, NMG_ERR_RANGE, "thread_rank >= nb_threads");
+    if (lengths[b] >= (1ull << 32)) return fail(h, NMG_ERR_RANGE, "buffer >= 4 GiB");
+    if (lengths[b] == 0) continue;
+    BufDesc d;
+    d.offset = offsets[b];
+    d.len = (uint32_t)lengths[b];
+    d.thread_rank = thread_ranks[b];
+    d.access = access_types[b];
+    d.pad = 0;
+    d.seq = seq_base + descs.size();
+    descs.push_back(d);
+    bytes.push_back(lengths[b]);
+  }
+  h->descs.swap(descs);
+  h->buf_bytes.swap(bytes);
+  h->d_data = (const uint8_t*)d_data;
+  h->external = true;
+  h->staged_dirty = false;
+  h->descs_dirty = true;
+  h->stage_len = 0;
+  return NMG_OK;
+}
+
+extern "C" int nmg_clear_buffers(nmg_engine* h) {
+  if (!h) return NMG_ERR_INVALID;
+  h->descs.clear();
+  h->buf_bytes.clear();
+  h->stage_len = 0;
+  h->external = false;
+  h->d_data = nullptr;
+  h->descs_dirty = true;
+  h->counts_override = false;
+  return NMG_OK;
+}
+
+static int upload_buffers(nmg_engine* h) {
+  if (!h->external && h->staged_dirty) {
+    if (h->stage_len + 64 > h->arena_cap) {
+      HIP_TRY(h, hipStreamSynchronize(h->stream));
+      (void)hipFree(h->d_arena);
+      h->d_arena = nullptr;
+      h->arena_cap = h->stage_len + 64;
+      HIP_TRY(h, hipMalloc(&h->d_arena, h->arena_cap));
+    }
+    if (h->stage_len) HIP_TRY(h, hipMemcpyAsync(h->d_arena, h->h_stage, h->stage_len, hipMemcpyHostToDevice, h->stream));
+    h->d_data = h->d_arena;
+    h->staged_dirty = false;
+  }
+  if (h->descs_dirty) {
+    size_t n = h->descs.size();
+    if (n > h->descs_cap) {
+      HIP_TRY(h, hipStreamSynchronize(h->stream));
+      (void)hipFree(h->d_descs);
+      (void)hipFree(h->d_bufcnt);
+      h->d_descs = nullptr;
+      h->d_bufcnt = nullptr;
+      h->descs_cap = n;
+      HIP_TRY(h, hipMalloc(&h->d_descs, n * sizeof(BufDesc)));
+      HIP_TRY(h, hipMalloc(&h->d_bufcnt, n * 2 * 4));
+    }
+    if (n) {
+      HIP_TRY(h, hipMemcpyAsync(h->d_descs, h->descs.data(), n * sizeof(BufDesc), hipMemcpyHostToDevice, h->stream));
+      HIP_TRY(h, hipMemsetAsync(h->d_bufcnt, 0, n * 2 * 4, h->stream));
+      HIP_TRY(h, hipStreamSynchronize(h->stream));  // descs come from pageable memory
+    }
+    h->descs_dirty = false;
+  }
+  return NMG_OK;
+}
+
+extern "C" int nmg_analyze(nmg_engine* h) {
+  if (!h) return NMG_ERR_INVALID;
+  if (!h->have_table) return fail(h, NMG_ERR_STATE, "nmg_analyze before nmg_set_objects");
+  HIP_TRY(h, hipSetDevice(h->device));
+  int rc = upload_buffers(h);
+  if (rc) return rc;
+  const uint32_t nb = (uint32_t)h->descs.size();
+  Params p;
+  memset(&p, 0, sizeof(p));
+  p.data = h->d_data;
+  p.bufs = h->d_descs;
+  p.nb_bufs = nb;
+  p.nb_keys = h->K;
+  p.keys = h->d_keys;
+  p.entry_off = h->d_entry_off;
+  p.entries = h->d_entries;
+  p.fences = h->d_fences;
+  p.nb_fences = h->nb_fences;
+  p.fence_step = h->fence_step;
+  p.nb_threads = h->T;
+  p.flags = h->flags;
+  p.nb_entries = h->E;
+  p.sparse_mask = (uint32_t)(h->sparse_cap - 1);
+  p.sum64 = h->d_sum64;
+  p.min64 = h->d_min64;
+  p.max64 = h->d_max64;
+  p.hist = h->d_hist;
+  p.bufcnt = h->d_bufcnt;
+  p.sparse_keys = h->d_sparse_keys;
+  p.sparse_vals = h->d_sparse_vals;
+  HIP_TRY(h, hipEventRecord(h->ev0, h->stream));
+  if (nb) {
+    uint32_t grid = std::min<uint32_t>(nb, (uint32_t)h->num_cus * 4);
+    hipLaunchKernelGGL(attribute_kernel, dim3(grid), dim3(kWG), 0, h->stream, p);
+    HIP_TRY(h, hipGetLastError());
+  }
+  HIP_TRY(h, hipEventRecord(h->ev1, h->stream));
+  h->launched = true;
+  return NMG_OK;
+}
+
+static int decode_error_word(nmg_engine* h, uint64_t w) {
+  if (w == ~0ull) return NMG_OK;
+  uint32_t code = w & 0xff;
+  uint64_t seq = w >> 40;
+  uint32_t off = (uint32_t)((w >> 8) & 0xffffffffu);
+  char msg[256];
+  snprintf(msg, sizeof(msg), "buffer %llu (analysis order), byte offset %u: ", (unsigned long long)seq, off);
+  switch (code) {
+    case kErrZeroSize: return fail(h, NMG_ERR_ZERO_SIZE, std::string(msg) + "invalid header size = 0");
+    case kErrTruncated: return fail(h, NMG_ERR_TRUNCATED, std::string(msg) + "truncated record");
+    case kErrUnaligned: return fail(h, NMG_ERR_UNALIGNED, std::string(msg) + "unaligned record");
+    case kErrCapacity: return fail(h, NMG_ERR_CAPACITY, std::string(msg) + "sparse table full");
+    default: return fail(h, NMG_ERR_RANGE, std::string(msg) + "range error");
+  }
+}
+
+extern "C" int nmg_synchronize(nmg_engine* h) {
+  if (!h) return NMG_ERR_INVALID;
+  HIP_TRY(h, hipSetDevice(h->device));
+  HIP_TRY(h, hipStreamSynchronize(h->stream));
+  if (h->launched) HIP_TRY(h, hipEventElapsedTime(&h->last_ms, h->ev0, h->ev1));
+  if (!h->have_table) return NMG_OK;
+  uint64_t w = ~0ull;
+  HIP_TRY(h, hipMemcpy(&w, h->d_min64 + 36 + h->E, 8, hipMemcpyDeviceToHost));
+  return decode_error_word(h, w);
+}
+
+extern "C" int nmg_last_analyze_ms(nmg_engine* h, float* ms) {
+  if (!h || !ms) return NMG_ERR_INVALID;
+  *ms = h->last_ms;
+  return NMG_OK;
+}
+
+extern "C" uint32_t nmg_get_nb_buffers(nmg_engine* h) {
+  if (!h) return 0;
+  return h->counts_override ? (uint32_t)h->ov_samples.size() : (uint32_t)h->descs.size();
+}
+
+namespace nmg {
+int engine_download(nmg_engine* h, HostResults& r) {
+  int rc = nmg_synchronize(h);
+  if (rc) return rc;
+  std::vector<uint64_t> sum(h->n_sum64), mn(h->n_min64), mx(h->n_max64);
+  HIP_TRY(h, hipMemcpy(sum.data(), h->d_sum64, h->n_sum64 * 8, hipMemcpyDeviceToHost));
+  HIP_TRY(h, hipMemcpy(mn.data(), h->d_min64, h->n_min64 * 8, hipMemcpyDeviceToHost));
+  HIP_TRY(h, hipMemcpy(mx.data(), h->d_max64, h->n_max64 * 8, hipMemcpyDeviceToHost));
+  for (int a = 0; a < 2; a++) {
+    nmg_mem_counters& c = r.global[a];
+    const uint64_t* s = sum.data() + gsum_index(a, 0);
+    c.total_count = s[0];
+    c.total_weight = s[1];
+    c.na_miss_count = s[2];
+    for (int k = 0; k < 18; k++) {
+      c.b[k].count = s[3 + 2 * k];
+      c.b[k].sum_weight = s[4 + 2 * k];
+      c.b[k].min_weight = mn[a * 18 + k];
+      c.b[k].max_weight = mx[a * 18 + k];
+    }
+  }
+  const uint64_t E = h->E;
+  r.first.assign(mn.begin() + 36, mn.begin() + 36 + E);
+  r.count_weight.assign(sum.begin() + 2 * kGlobalSums, sum.begin() + 2 * kGlobalSums + 4 * E);
+  if (h->flags & NMG_F_OBJECT_LEVELS)
+    r.levels.assign(sum.begin() + 2 * kGlobalSums + 4 * E, sum.end());
+  else
+    r.levels.clear();
+  if (h->counts_override) {
+    r.buf_samples = h->ov_samples;
+    r.buf_found = h->ov_found;
+    r.buf_bytes = h->ov_bytes;
+  } else {
+    size_t n = h->descs.size();
+    std::vector<uint32_t> cnt(2 * n);
+    if (n) HIP_TRY(h, hipMemcpy(cnt.data(), h->d_bufcnt, 2 * n * 4, hipMemcpyDeviceToHost));
+    r.buf_samples.assign(cnt.begin(), cnt.begin() + n);
+    r.buf_found.assign(cnt.begin() + n, cnt.end());
+    r.buf_bytes = h->buf_bytes;
+  }
+  // mem_sampling_finalize accumulates the per-buffer int counters (:334-335)
+  r.nb_samples_total = 0;
+  r.nb_found_total = 0;
+  for (size_t b = 0; b < r.buf_samples.size(); b++) {
+    r.nb_samples_total += (uint64_t)(int64_t)(int32_t)r.buf_samples[b];
+    r.nb_found_total += (uint64_t)(int64_t)(int32_t)r.buf_found[b];
+  }
+  return NMG_OK;
+}
+
+int engine_download_hist(nmg_engine* h, std::vector<uint32_t>& cells) {
+  int rc = nmg_synchronize(h);
+  if (rc) return rc;
+  cells.resize(h->hist_cells);
+  if (h->hist_cells) HIP_TRY(h, hipMemcpy(cells.data(), h->d_hist, h->hist_cells * 4, hipMemcpyDeviceToHost));
+  return NMG_OK;
+}
+}  // namespace nmg
+
+extern "C" int nmg_get_global_counters(nmg_engine* h, nmg_mem_counters out[2], uint64_t* nb_samples,
+                                       uint64_t* nb_found) {
+  if (!h || !out) return NMG_ERR_INVALID;
+  if (!h->have_table) return fail(h, NMG_ERR_STATE, "no object table");
+  HostResults r;
+  int rc = engine_download(h, r);
+  if (rc) return rc;
+  out[0] = r.global[0];
+  out[1] = r.global[1];
+  if (nb_samples) *nb_samples = r.nb_samples_total;
+  if (nb_found) *nb_found = r.nb_found_total;
+  return NMG_OK;
+}
+
+extern "C" int nmg_get_buffer_counts(nmg_engine* h, uint32_t* nb_samples, uint32_t* nb_found) {
+  if (!h) return NMG_ERR_INVALID;
+  if (!h->have_table) return fail(h, NMG_ERR_STATE, "no object table");
+  HostResults r;
+  int rc = engine_download(h, r);
+  if (rc) return rc;
+  if (nb_samples) memcpy(nb_samples, r.buf_samples.data(), r.buf_samples.size() * 4);
+  if (nb_found) memcpy(nb_found, r.buf_found.data(), r.buf_found.size() * 4);
+  return NMG_OK;
+}
+
+extern "C" int nmg_get_object_counters(nmg_engine* h, uint64_t* first_ordinal, uint64_t* count_weight) {
+  if (!h) return NMG_ERR_INVALID;
+  if (!h->have_table) return fail(h, NMG_ERR_STATE, "no object table");
+  int rc = nmg_synchronize(h);
+  if (rc) return rc;
+  if (first_ordinal && h->E)
+    HIP_TRY(h, hipMemcpy(first_ordinal, h->d_min64 + 36, (size_t)h->E * 8, hipMemcpyDeviceToHost));
+  if (count_weight && h->E)
+    HIP_TRY(h, hipMemcpy(count_weight, h->d_sum64 + 2 * kGlobalSums, (size_t)h->E * 32, hipMemcpyDeviceToHost));
+  return NMG_OK;
+}
+
+extern "C" int nmg_get_object_levels(nmg_engine* h, uint64_t* levels) {
+  if (!h || !levels) return NMG_ERR_INVALID;
+  if (!(h->flags & NMG_F_OBJECT_LEVELS)) return fail(h, NMG_ERR_STATE, "engine created without NMG_F_OBJECT_LEVELS");
+  int rc = nmg_synchronize(h);
+  if (rc) return rc;
+  if (h->E)
+    HIP_TRY(h, hipMemcpy(levels, h->d_sum64 + 2 * kGlobalSums + (uint64_t)h->E * 4,
+                         (size_t)h->E * 2 * kLevelWords * 8, hipMemcpyDeviceToHost));
+  return NMG_OK;
+}
+
+static int collect_page_cells(nmg_engine* h, std::vector<uint32_t>* rows, int64_t* count) {
+  std::vector<uint32_t> cells;
+  int rc = engine_download_hist(h, cells);
+  if (rc) return rc;
+  // sparse cells grouped per entry
+  std::vector<std::vector<std::pair<uint64_t, uint32_t>>> sparse(h->sparse_entries.size());
+  if (h->d_sparse_keys) {
+    std::vector<uint64_t> k(h->sparse_cap);
+    std::vector<uint32_t> v(h->sparse_cap);
+    HIP_TRY(h, hipMemcpy(k.data(), h->d_sparse_keys, h->sparse_cap * 8, hipMemcpyDeviceToHost));
+    HIP_TRY(h, hipMemcpy(v.data(), h->d_sparse_vals, h->sparse_cap * 4, hipMemcpyDeviceToHost));
+    for (size_t i = 0; i < k.size(); i++)
+      if (k[i] != ~0ull && v[i]) {
+        uint32_t s = sparse_key_idx(k[i]);
+        // order within an entry: (thread, page)
+        sparse[s].push_back({(uint64_t(sparse_key_thread(k[i])) << 32) | sparse_key_page(k[i]), v[i]});
+      }
+    for (auto& l : sparse) std::sort(l.begin(), l.end());
+  }
+  std::vector<int64_t> sidx_of(h->E, -1);
+  for (size_t s = 0; s < h->sparse_entries.size(); s++) sidx_of[h->sparse_entries[s]] = (int64_t)s;
+  int64_t n = 0;
+  const uint64_t T = h->T;
+  for (uint32_t e = 0; e < h->E; e++) {
+    if (h->hist_base[e] != kHistSparse) {
+      const uint32_t* c = cells.data() + h->hist_base[e];
+      for (uint32_t th = 0; th < T; th++)
+        for (uint64_t pg = 0; pg < h->npages[e]; pg++) {
+          uint32_t v = c[pg * T + th];
+          if (!v) continue;
+          if (rows) {
+            rows->push_back(e);
+            rows->push_back(th);
+            rows->push_back((uint32_t)pg);
+            rows->push_back(v);
+          }
+          n++;
+        }
+    } else if (sidx_of[e] >= 0) {
+      for (auto& kv : sparse[sidx_of[e]]) {
+        if (rows) {
+          rows->push_back(e);
+          rows->push_back((uint32_t)(kv.first >> 32));
+          rows->push_back((uint32_t)kv.first);
+          rows->push_back(kv.second);
+        }
+        n++;
+      }
+    }
+  }
+  *count = n;
+  return NMG_OK;
+}
+
+extern "C" int64_t nmg_count_page_cells(nmg_engine* h) {
+  if (!h || !h->have_table) return NMG_ERR_INVALID;
+  int64_t n = 0;
+  int rc = collect_page_cells(h, nullptr, &n);
+  return rc ? rc : n;
+}
+
+extern "C" int nmg_get_page_cells(nmg_engine* h, uint32_t* rows, int64_t n) {
+  if (!h || !h->have_table || (n && !rows)) return NMG_ERR_INVALID;
+  std::vector<uint32_t> r;
+  int64_t cnt = 0;
+  int rc = collect_page_cells(h, &r, &cnt);
+  if (rc) return rc;
+  if (cnt != n) return fail(h, NMG_ERR_INVALID, "row count mismatch");
+  if (n) memcpy(rows, r.data(), r.size() * 4);
+  return NMG_OK;
+}
+
+// ---- multi-GPU merge support
+
+extern "C" uint64_t nmg_array_size(nmg_engine* h, int which) {
+  if (!h || !h->have_table) return 0;
+  switch (which) {
+    case NMG_ARR_SUM64: return h->n_sum64;
+    case NMG_ARR_MIN64: return h->n_min64;
+    case NMG_ARR_MAX64: return h->n_max64;
+    case NMG_ARR_HIST32: return h->hist_cells;
+    default: return 0;
+  }
+}
+
+static void* array_ptr(nmg_engine* h, int which, size_t* bytes) {
+  switch (which) {
+    case NMG_ARR_SUM64: *bytes = h->n_sum64 * 8; return h->d_sum64;
+    case NMG_ARR_MIN64: *bytes = h->n_min64 * 8; return h->d_min64;
+    case NMG_ARR_MAX64: *bytes = h->n_max64 * 8; return h->d_max64;
+    case NMG_ARR_HIST32: *bytes = h->hist_cells * 4; return h->d_hist;
+    default: *bytes = 0; return nullptr;
+  }
+}
+
+extern "C" int nmg_export_array(nmg_engine* h, int which, void* d_dst) {
+  if (!h || !h->have_table) return NMG_ERR_INVALID;
+  size_t bytes = 0;
+  void* src = array_ptr(h, which, &bytes);
+  if (!bytes) return NMG_OK;
+  if (!src || !d_dst) return NMG_ERR_INVALID;
+  HIP_TRY(h, hipSetDevice(h->device));
+  HIP_TRY(h, hipMemcpyAsync(d_dst, src, bytes, hipMemcpyDeviceToDevice, h->stream));
+  HIP_TRY(h, hipStreamSynchronize(h->stream));
+  return NMG_OK;
+}
+
+extern "C" int nmg_import_array(nmg_engine* h, int which, const void* d_src) {
+  if (!h || !h->have_table) return NMG_ERR_INVALID;
+  size_t bytes = 0;
+  void* dst = array_ptr(h, which, &bytes);
+  if (!bytes) return NMG_OK;
+  if (!dst || !d_src) return NMG_ERR_INVALID;
+  HIP_TRY(h, hipSetDevice(h->device));
+  HIP_TRY(h, hipMemcpyAsync(dst, d_src, bytes, hipMemcpyDeviceToDevice, h->stream));
+  HIP_TRY(h, hipStreamSynchronize(h->stream));
+  return NMG_OK;
+}
+
+static int sparse_download(nmg_engine* h, std::vector<uint64_t>& k, std::vector<uint32_t>& v) {
+  int rc = nmg_synchronize(h);
+  if (rc) return rc;
+  if (!h->d_sparse_keys) {
+    k.clear();
+    v.clear();
+    return NMG_OK;
+  }
+  std::vector<uint64_t> kk(h->sparse_cap);
+  std::vector<uint32_t> vv(h->sparse_cap);
+  HIP_TRY(h, hipMemcpy(kk.data(), h->d_sparse_keys, h->sparse_cap * 8, hipMemcpyDeviceToHost));
+  HIP_TRY(h, hipMemcpy(vv.data(), h->d_sparse_vals, h->sparse_cap * 4, hipMemcpyDeviceToHost));
+  k.clear();
+  v.clear();
+  for (size_t i = 0; i < kk.size(); i++)
+    if (kk[i] != ~0ull && vv[i]) {
+      k.push_back(kk[i]);
+      v.push_back(vv[i]);
+    }
+  return NMG_OK;
+}
+
+extern "C" int64_t nmg_sparse_count(nmg_engine* h) {
+  if (!h || !h->have_table) return NMG_ERR_INVALID;
+  std::vector<uint64_t> k;
+  std::vector<uint32_t> v;
+  int rc = sparse_download(h, k, v);
+  return rc ? rc : (int64_t)k.size();
+}
+
+extern "C" int nmg_sparse_export(nmg_engine* h, uint64_t* keys, uint32_t* counts, int64_t n) {
+  if (!h || !h->have_table || (n && (!keys || !counts))) return NMG_ERR_INVALID;
+  std::vector<uint64_t> k;
+  std::vector<uint32_t> v;
+  int rc = sparse_download(h, k, v);
+  if (rc) return rc;
+  if ((int64_t)k.size() != n) return fail(h, NMG_ERR_INVALID, "sparse count mismatch");
+  memcpy(keys, k.data(), n * 8);
+  memcpy(counts, v.data(), n * 4);
+  return NMG_OK;
+}
+
+extern "C" int nmg_sparse_import(nmg_engine* h, const uint64_t* keys, const uint32_t* counts, int64_t n) {
+  // Re-inserts merged (key, count) pairs into an empty table on this rank.
+  if (!h || !h->have_table || (n && (!keys || !counts))) return NMG_ERR_INVALID;
+  if (!h->d_sparse_keys) return n ? fail(h, NMG_ERR_STATE, "no sparse table") : NMG_OK;
+  if ((uint64_t)n > h->sparse_cap) return fail(h, NMG_ERR_CAPACITY, "sparse table too small");
+  std::vector<uint64_t> k(h->sparse_cap, ~0ull);
+  std::vector<uint32_t> v(h->sparse_cap, 0);
+  for (int64_t i = 0; i < n; i++) {
+    uint64_t hh = (keys[i] * 0x9E3779B97F4A7C15ull) >> 20;
+    uint64_t slot = hh & (h->sparse_cap - 1);
+    while (k[slot] != ~0ull && k[slot] != keys[i]) slot = (slot + 1) & (h->sparse_cap - 1);
+    k[slot] = keys[i];
+    v[slot] += counts[i];
+  }
+  HIP_TRY(h, hipSetDevice(h->device));
+  HIP_TRY(h, hipMemcpy(h->d_sparse_keys, k.data(), h->sparse_cap * 8, hipMemcpyHostToDevice));
+  HIP_TRY(h, hipMemcpy(h->d_sparse_vals, v.data(), h->sparse_cap * 4, hipMemcpyHostToDevice));
+  return NMG_OK;
+}
+
+extern "C" int nmg_set_buffer_counts(nmg_engine* h, uint32_t nb_buffers, const uint32_t* nb_samples,
+                                     const uint32_t* nb_found, const uint64_t* buffer_bytes) {
+  if (!h || (nb_buffers && (!nb_samples || !nb_found || !buffer_bytes))) return NMG_ERR_INVALID;
+  h->counts_override = true;
+  h->ov_samples.assign(nb_samples, nb_samples + nb_buffers);
+  h->ov_found.assign(nb_found, nb_found + nb_buffers);
+  h->ov_bytes.assign(buffer_bytes, buffer_bytes + nb_buffers);
+  return NMG_OK;
+}
+
+extern "C" int nmg_report(nmg_engine* h, const nmg_object_meta* meta, const nmg_report_options* opts,
+                          const char* stdout_path) {
+  if (!h || (h->E && !meta)) return NMG_ERR_INVALID;
+  if (!h->have_table) return fail(h, NMG_ERR_STATE, "nmg_report before nmg_set_objects");
+  HostResults r;
+  int rc = engine_download(h, r);
+  if (rc) return rc;
+  std::vector<uint32_t> rows;
+  int64_t ncells = 0;
+  if ((h->flags & NMG_F_PAGE_HIST) && (!opts || opts->dump_single_items)) {
+    rc = collect_page_cells(h, &rows, &ncells);
+    if (rc) return rc;
+  }
+  nmg_host_results res;
+  memset(&res, 0, sizeof(res));
+  res.global[0] = r.global[0];
+  res.global[1] = r.global[1];
+  res.nb_buffers = (uint32_t)r.buf_samples.size();
+  res.nb_entries = h->E;
+  res.buf_samples = r.buf_samples.data();
+  res.buf_found = r.buf_found.data();
+  res.buf_bytes = r.buf_bytes.data();
+  res.buffer_size = h->buffer_size.data();
+  res.first_ordinal = r.first.data();
+  res.count_weight = r.count_weight.data();
+  res.cells = rows.data();
+  res.nb_cells = ncells;
+  res.nb_threads = h->T;
+  res.match_samples = (h->flags & NMG_F_MATCH_SAMPLES) ? 1 : 0;
+  std::string err;
+  rc = write_report(&res, meta, opts, stdout_path, err);
+  if (rc && !err.empty()) h->last_error = err;
+  return rc;
+}

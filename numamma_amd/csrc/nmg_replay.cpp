@@ -1,0 +1,248 @@
+// nmg_replay.cpp -- replay-file driver for the engine: the C++ stand-in for
+// the reference's LD_PRELOAD host while no live capture is available (no PMU
+// in the container, numap absent).  It plays the role of ma_finalize: hands
+// the object-table snapshot and every captured buffer (in `samples` order) to
+// the engine, then writes the reference's report.  Format: DESIGN.md
+// "Replay format".
+#include <cerrno>
+#include <cinttypes>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "nmg_internal.h"
+
+namespace {
+
+constexpr size_t kEntryBytes = 72;
+
+struct Replay {
+  std::vector<uint8_t> file;
+  uint32_t nb_threads = 0, nb_keys = 0, nb_entries = 0, nb_buffers = 0;
+  const uint64_t* keys = nullptr;
+  const uint32_t* entry_off = nullptr;
+  std::vector<nmg_object> objects;
+  std::vector<nmg_object_meta> meta;
+  struct Buf {
+    uint32_t rank, access;
+    uint64_t tail, head, ring;
+    const uint8_t* bytes;
+  };
+  std::vector<Buf> bufs;
+};
+
+template <class T>
+T get(const uint8_t* p) {
+  T v;
+  memcpy(&v, p, sizeof(T));
+  return v;
+}
+size_t pad8(size_t x) { return (x + 7) & ~size_t(7); }
+
+int load_replay(const char* path, Replay& r, std::string& err) {
+  FILE* f = fopen(path, "rb");
+  if (!f) {
+    err = std::string("cannot open ") + path + ": " + strerror(errno);
+    return NMG_ERR_IO;
+  }
+  fseek(f, 0, SEEK_END);
+  long sz = ftell(f);
+  fseek(f, 0, SEEK_SET);
+  r.file.resize(sz > 0 ? (size_t)sz : 0);
+  size_t got = fread(r.file.data(), 1, r.file.size(), f);
+  fclose(f);
+  if (got != r.file.size() || r.file.size() < 64) {
+    err = "short replay file";
+    return NMG_ERR_INVALID;
+  }
+  const uint8_t* p = r.file.data();
+  if (memcmp(p, "NMGRPLY1", 8) != 0 || get<uint32_t>(p + 8) != 1) {
+    err = "bad replay magic/version";
+    return NMG_ERR_INVALID;
+  }
+  r.nb_threads = get<uint32_t>(p + 12);
+  r.nb_keys = get<uint32_t>(p + 16);
+  r.nb_entries = get<uint32_t>(p + 20);
+  r.nb_buffers = get<uint32_t>(p + 24);
+  uint64_t cs_len = get<uint64_t>(p + 32), str_len = get<uint64_t>(p + 40);
+  size_t off = 64;
+  size_t need = off + 8ull * r.nb_keys + pad8(4ull * (r.nb_keys + 1)) + kEntryBytes * r.nb_entries + 8 * cs_len +
+                pad8(str_len);
+  if (need > r.file.size()) {
+    err = "truncated object table";
+    return NMG_ERR_INVALID;
+  }
+  r.keys = reinterpret_cast<const uint64_t*>(p + off);
+  off += 8ull * r.nb_keys;
+  r.entry_off = reinterpret_cast<const uint32_t*>(p + off);
+  off += pad8(4ull * (r.nb_keys + 1));
+  const uint8_t* ent = p + off;
+  off += kEntryBytes * r.nb_entries;
+  const uint64_t* cs_pool = reinterpret_cast<const uint64_t*>(p + off);
+  off += 8 * cs_len;
+  const char* str_pool = reinterpret_cast<const char*>(p + off);
+  off += pad8(str_len);
+  r.objects.resize(r.nb_entries);
+  r.meta.resize(r.nb_entries);
+  for (uint32_t e = 0; e < r.nb_entries; e++) {
+    const uint8_t* q = ent + kEntryBytes * e;
+    nmg_object& o = r.objects[e];
+    nmg_object_meta& m = r.meta[e];
+    o.buffer_addr = get<uint64_t>(q + 0);
+    o.buffer_size = get<uint64_t>(q + 8);
+    m.initial_buffer_size = get<uint64_t>(q + 16);
+    o.alloc_date = get<uint64_t>(q + 24);
+    o.free_date = get<uint64_t>(q + 32);
+    m.caller_rip = get<uint64_t>(q + 40);
+    m.mem_type = get<uint32_t>(q + 48);
+    m.id = get<uint32_t>(q + 52);
+    uint32_t cs_off = get<uint32_t>(q + 56);
+    m.callstack_size = get<int32_t>(q + 60);
+    uint32_t caller_off = get<uint32_t>(q + 64);
+    uint32_t has_cs = get<uint32_t>(q + 68);
+    if (has_cs) {
+      if (m.callstack_size < 0 || (uint64_t)cs_off + (uint64_t)m.callstack_size > cs_len) {
+        err = "callstack out of range";
+        return NMG_ERR_INVALID;
+      }
+      m.callstack = cs_pool + cs_off;
+    } else {
+      m.callstack = nullptr;
+    }
+    if (caller_off != 0xFFFFFFFFu) {
+      if (caller_off >= str_len) {
+        err = "caller string out of range";
+        return NMG_ERR_INVALID;
+      }
+      m.caller = str_pool + caller_off;
+    } else {
+      m.caller = nullptr;
+    }
+    m.reserved = 0;
+  }
+  for (uint32_t b = 0; b < r.nb_buffers; b++) {
+    if (off + 32 > r.file.size()) {
+      err = "truncated buffer header";
+      return NMG_ERR_INVALID;
+    }
+    Replay::Buf B;
+    B.rank = get<uint32_t>(p + off);
+    B.access = get<uint32_t>(p + off + 4);
+    B.tail = get<uint64_t>(p + off + 8);
+    B.head = get<uint64_t>(p + off + 16);
+    B.ring = get<uint64_t>(p + off + 24);
+    off += 32;
+    if (off + pad8(B.ring) > r.file.size()) {
+      err = "truncated ring";
+      return NMG_ERR_INVALID;
+    }
+    B.bytes = p + off;
+    off += pad8(B.ring);
+    r.bufs.push_back(B);
+  }
+  return NMG_OK;
+}
+
+int write_raw(nmg_engine* h, const Replay& r, const char* path) {
+  nmg::HostResults res;
+  int rc = nmg::engine_download(h, res);
+  if (rc) return rc;
+  const uint32_t E = r.nb_entries;
+  int64_t ncells = nmg_count_page_cells(h);
+  if (ncells < 0) return (int)ncells;
+  std::vector<uint32_t> rows(4 * (size_t)ncells);
+  rc = nmg_get_page_cells(h, rows.data(), ncells);
+  if (rc) return rc;
+  FILE* f = fopen(path, "wb");
+  if (!f) return NMG_ERR_IO;
+  fwrite("NMGRES01", 1, 8, f);
+  uint32_t hdr[4] = {E, (uint32_t)res.buf_samples.size(), nmg::engine_nb_threads(h), 0};
+  fwrite(hdr, 4, 4, f);
+  for (int a = 0; a < 2; a++) {
+    const nmg_mem_counters& c = res.global[a];
+    fwrite(&c.total_count, 8, 1, f);
+    fwrite(&c.total_weight, 8, 1, f);
+    fwrite(&c.na_miss_count, 8, 1, f);
+    for (int k = 0; k < 18; k++) fwrite(&c.b[k], 8, 4, f);
+  }
+  fwrite(&res.nb_samples_total, 8, 1, f);
+  fwrite(&res.nb_found_total, 8, 1, f);
+  fwrite(res.buf_samples.data(), 4, res.buf_samples.size(), f);
+  fwrite(res.buf_found.data(), 4, res.buf_found.size(), f);
+  const bool lv = !res.levels.empty();
+  for (uint32_t e = 0; e < E; e++) {
+    uint64_t rec[1 + 2 * 39] = {0};
+    rec[0] = res.first[e];
+    for (int a = 0; a < 2; a++) {
+      uint64_t* q = rec + 1 + 39 * a;
+      q[0] = res.count_weight[(uint64_t)e * 4 + a * 2 + 0];
+      q[1] = res.count_weight[(uint64_t)e * 4 + a * 2 + 1];
+      if (lv) {
+        const uint64_t* l = res.levels.data() + ((uint64_t)e * 2 + a) * nmg::kLevelWords;
+        q[2] = l[0];
+        for (int k = 0; k < 36; k++) q[3 + k] = l[1 + k];
+      }
+    }
+    fwrite(rec, 8, 1 + 2 * 39, f);
+  }
+  uint64_t n = (uint64_t)ncells;
+  fwrite(&n, 8, 1, f);
+  fwrite(rows.data(), 4, rows.size(), f);
+  fclose(f);
+  return NMG_OK;
+}
+
+}  // namespace
+
+extern "C" int nmg_run_replay(const char* replay_path, const char* output_dir, const char* stdout_path,
+                              const char* raw_path, int device, uint32_t flags) {
+  Replay r;
+  std::string err;
+  int rc = load_replay(replay_path, r, err);
+  if (rc) {
+    fprintf(stderr, "nmg_replay: %s\n", err.c_str());
+    return rc;
+  }
+  nmg_options opt;
+  memset(&opt, 0, sizeof(opt));
+  opt.device = device;
+  opt.flags = flags | (raw_path ? NMG_F_OBJECT_LEVELS : 0);
+  opt.nb_threads = r.nb_threads ? r.nb_threads : 1;
+  nmg_engine* h = nullptr;
+  rc = nmg_create(&h, &opt);
+  if (rc) {
+    fprintf(stderr, "nmg_replay: nmg_create: %s\n", nmg_strerror(rc));
+    return rc;
+  }
+  auto bail = [&](int code) {
+    char detail[512];
+    nmg_get_last_error_detail(h, detail, sizeof(detail));
+    fprintf(stderr, "nmg_replay: %s (%s)\n", nmg_strerror(code), detail);
+    nmg_destroy(h);
+    return code;
+  };
+  rc = nmg_set_objects(h, r.keys, r.entry_off, r.nb_keys, r.objects.data(), r.nb_entries);
+  if (rc) return bail(rc);
+  for (const auto& b : r.bufs) {
+    rc = nmg_submit_ring(h, b.bytes, b.ring, b.tail, b.head, b.rank, b.access);
+    if (rc) return bail(rc);
+  }
+  rc = nmg_analyze(h);
+  if (rc) return bail(rc);
+  rc = nmg_synchronize(h);
+  if (rc) return bail(rc);
+  nmg_report_options ro;
+  memset(&ro, 0, sizeof(ro));
+  ro.output_dir = output_dir;
+  ro.dump_single_items = 1;
+  rc = nmg_report(h, r.meta.data(), &ro, stdout_path);
+  if (rc) return bail(rc);
+  if (raw_path) {
+    rc = write_raw(h, r, raw_path);
+    if (rc) return bail(rc);
+  }
+  nmg_destroy(h);
+  return NMG_OK;
+}

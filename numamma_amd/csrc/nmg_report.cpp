@@ -1,0 +1,436 @@
+// nmg_report.cpp -- host half of the drop-in: the report part of ma_finalize
+// (src/mem_analyzer.c:1802-1884) fed by the engine's device results.
+//
+//  * call-site registry: sites are created in first-match order (the order
+//    __match_sample reaches new_call_site, mem_sampling.c:665-669), then every
+//    matched object is re-attached with find_call_site in FOREACH_HASH order
+//    (update_call_sites, mem_analyzer.c:1380-1436).  find_call_site's linear
+//    scan of the LIFO site list is replaced by two hash maps keyed exactly on
+//    its match predicate (callstack-keyed sites / caller_rip-keyed sites);
+//    "first in the list" == newest == highest id among the candidates.
+//  * __sort_sites (mem_analyzer.c:1531-1557) is reproduced exactly, including
+//    its int-truncated running minimum (quirk Q9): a plain sort when every
+//    key fits an int, otherwise an O(chain log S) segment-tree simulation of
+//    the selection passes.
+//  * printf formats are byte-identical to __print_counters (:1438-1487),
+//    print_call_site_summary (:1597-1640), __plot_counters (:1559-1583) and
+//    mem_sampling_statistics (mem_sampling.c:357-361).
+#include <sys/stat.h>
+
+#include <algorithm>
+#include <cinttypes>
+#include <cstdio>
+#include <cstring>
+#include <functional>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "nmg_internal.h"
+
+namespace nmg {
+namespace {
+
+constexpr uint32_t kMemTypeStack = 2;  // enum mem_type, mem_analyzer.h:58-64
+
+struct Site {
+  uint32_t id;
+  std::string caller;
+  uint64_t caller_rip;
+  const uint64_t* callstack;
+  int32_t callstack_size;
+  uint64_t buffer_size;            // initial_buffer_size of the creating object
+  uint32_t mem_type;               // site->mem_info.mem_type
+  uint64_t mem_info_buffer_size;   // site->mem_info.buffer_size (:1363)
+  uint32_t nb_mallocs = 0;
+  uint64_t read_count = 0, read_weight = 0, write_count = 0, write_weight = 0;
+  std::vector<uint32_t> objects;   // entries attached at finalize
+};
+
+struct CsKey {
+  uint64_t size;
+  int32_t cs_size;
+  std::vector<uint64_t> tail;  // callstack[3..cs_size)
+  bool operator==(const CsKey& o) const { return size == o.size && cs_size == o.cs_size && tail == o.tail; }
+};
+struct CsKeyHash {
+  size_t operator()(const CsKey& k) const {
+    uint64_t h = k.size * 0x9E3779B97F4A7C15ull ^ (uint64_t)(uint32_t)k.cs_size;
+    for (uint64_t v : k.tail) h = (h ^ v) * 0x100000001B3ull;
+    return (size_t)h;
+  }
+};
+struct RipKey {
+  uint64_t size, rip;
+  bool operator==(const RipKey& o) const { return size == o.size && rip == o.rip; }
+};
+struct RipKeyHash {
+  size_t operator()(const RipKey& k) const { return (size_t)(k.size * 0x9E3779B97F4A7C15ull ^ k.rip); }
+};
+
+class Registry {
+ public:
+  explicit Registry(const nmg_object_meta* meta) : meta_(meta) {}
+
+  // find_call_site (mem_analyzer.c:1302-1331)
+  int64_t find(uint32_t e) const {
+    const nmg_object_meta& m = meta_[e];
+    int64_t best = -1;
+    auto a = by_cs_.find(cs_key_of(m.initial_buffer_size, m.callstack, m.callstack_size));
+    if (a != by_cs_.end()) best = a->second;
+    auto b = by_rip_.find(RipKey{m.initial_buffer_size, m.caller_rip});
+    if (b != by_rip_.end() && b->second > best) best = b->second;
+    return best;  // sites are indexed by creation order == id - 1
+  }
+
+  // new_call_site (mem_analyzer.c:1333-1378)
+  int64_t create(uint32_t e, uint64_t npages) {
+    const nmg_object_meta& m = meta_[e];
+    Site s;
+    s.id = (uint32_t)sites.size() + 1;  // next_call_site_id starts at 1 (:1339-1340)
+    s.caller = caller_string(m);
+    s.caller_rip = m.caller_rip;
+    s.callstack = m.callstack;
+    s.callstack_size = m.callstack_size;
+    s.buffer_size = m.initial_buffer_size;
+    s.mem_type = m.mem_type;
+    // site->mem_info.buffer_size (:1363) is only ever used as buffer_size /
+    // 4096 + 1 rows (__plot_counters :1565), i.e. the entry's page count
+    s.mem_info_buffer_size = (npages - 1) * kPageSize;
+    int64_t idx = (int64_t)sites.size();
+    if (m.callstack)
+      by_cs_[cs_key_of(m.initial_buffer_size, m.callstack, m.callstack_size)] = idx;
+    else
+      by_rip_[RipKey{m.initial_buffer_size, m.caller_rip}] = idx;
+    sites.push_back(std::move(s));
+    return idx;
+  }
+
+  std::vector<Site> sites;  // creation order
+
+ private:
+  static CsKey cs_key_of(uint64_t size, const uint64_t* cs, int32_t cs_size) {
+    CsKey k{size, cs_size, {}};
+    if (cs && cs_size > 3) k.tail.assign(cs + 3, cs + cs_size);
+    return k;
+  }
+  // get_caller_function_from_rip (src/mem_tools.c:91-131): "???" for a NULL
+  // rip; replays carry the symbolised string; strings live in 1024-byte slots.
+  static std::string caller_string(const nmg_object_meta& m) {
+    char buf[1024];
+    if (m.caller)
+      snprintf(buf, sizeof(buf), "%s", m.caller);
+    else if (!m.caller_rip)
+      snprintf(buf, sizeof(buf), "???");
+    else
+      snprintf(buf, sizeof(buf), "[0x%" PRIx64 "]", m.caller_rip);
+    return buf;
+  }
+  const nmg_object_meta* meta_;
+  std::unordered_map<CsKey, int64_t, CsKeyHash> by_cs_;
+  std::unordered_map<RipKey, int64_t, RipKeyHash> by_rip_;
+};
+
+// (uint64_t)(int64_t)(int)x: the comparison in __sort_sites promotes the
+// int-truncated running minimum back to uint64_t (mem_analyzer.c:1544-1547)
+inline uint64_t trunc_key(uint64_t x) { return (uint64_t)(int64_t)(int32_t)(uint32_t)x; }
+
+// Returns the final list order (indices into sites), head first.
+std::vector<int64_t> sort_sites(const std::vector<Site>& sites) {
+  const int64_t n = (int64_t)sites.size();
+  std::vector<int64_t> out;
+  out.reserve(n);
+  bool small = true;
+  for (const Site& s : sites) small &= s.read_weight < (1ull << 31);
+  if (small) {
+    // selection of the first minimum in list order (list = id descending),
+    // pushed at the head: final = weight descending, ties by id ascending
+    for (int64_t i = 0; i < n; i++) out.push_back(i);
+    std::stable_sort(out.begin(), out.end(), [&](int64_t a, int64_t b) {
+      if (sites[a].read_weight != sites[b].read_weight) return sites[a].read_weight > sites[b].read_weight;
+      return a < b;
+    });
+    return out;
+  }
+  // general case: simulate the passes.  pos 0 = head of the LIFO list = newest.
+  int64_t sz = 1;
+  while (sz < n) sz <<= 1;
+  const uint64_t kDead = ~0ull;
+  std::vector<uint64_t> tree(2 * sz, kDead);
+  for (int64_t pos = 0; pos < n; pos++) tree[sz + pos] = sites[n - 1 - pos].read_weight;
+  for (int64_t i = sz - 1; i >= 1; i--) tree[i] = std::min(tree[2 * i], tree[2 * i + 1]);
+  auto remove = [&](int64_t pos) {
+    int64_t i = sz + pos;
+    tree[i] = kDead;
+    for (i >>= 1; i >= 1; i >>= 1) tree[i] = std::min(tree[2 * i], tree[2 * i + 1]);
+  };
+  // first position >= from whose value < m, or -1
+  std::function<int64_t(int64_t, int64_t, int64_t, int64_t, uint64_t)> first_below;
+  first_below = [&](int64_t node, int64_t lo, int64_t hi, int64_t from, uint64_t m) -> int64_t {
+    if (hi < from || tree[node] >= m) return -1;
+    if (lo == hi) return lo;
+    int64_t mid = (lo + hi) / 2;
+    int64_t r = first_below(2 * node, lo, mid, from, m);
+    if (r >= 0) return r;
+    return first_below(2 * node + 1, mid + 1, hi, from, m);
+  };
+  std::vector<int64_t> removal;
+  removal.reserve(n);
+  std::vector<char> alive(n, 1);
+  int64_t head = 0;
+  for (int64_t pass = 0; pass < n; pass++) {
+    while (!alive[head]) head++;
+    int64_t pick = head;
+    uint64_t m = trunc_key(sites[n - 1 - head].read_weight);
+    int64_t from = head;  // the head is compared against itself too
+    for (;;) {
+      int64_t q = first_below(1, 0, sz - 1, from, m);
+      if (q < 0) break;
+      pick = q;
+      m = trunc_key(sites[n - 1 - q].read_weight);
+      from = q + 1;
+    }
+    alive[pick] = 0;
+    remove(pick);
+    removal.push_back(n - 1 - pick);
+  }
+  for (int64_t i = n - 1; i >= 0; i--) out.push_back(removal[i]);
+  return out;
+}
+
+const char* kHitNames[9] = {"L1 Hit",         "L2 Hit",           "L3 Hit",
+                            "LFB Hit",        "Local RAM Hit",    "Remote RAM Hit",
+                            "Remote cache Hit", "IO memory Hit",  "Uncached memory Hit"};
+const char* kMissNames[9] = {nullptr,          nullptr,           nullptr,
+                             "LFB Miss",       "Local RAM Miss",  "Remote RAM Miss",
+                             "Remote cache Miss", "IO memory Miss", "Uncached memory Miss"};
+
+// __print_counters (mem_analyzer.c:1438-1487)
+void print_counters(FILE* f, const nmg_mem_counters* counters) {
+  for (int i = 0; i < 2; i++) {
+    const nmg_mem_counters& c = counters[i];
+    if (i == 0) {
+      fprintf(f, "\n");
+      fprintf(f, "# --------------------------------------\n");
+      fprintf(f, "# Summary of all the read memory access:\n");
+    } else {
+      fprintf(f, "# --------------------------------------\n");
+      fprintf(f, "# Summary of all the write memory access:\n");
+    }
+    fprintf(f, "# Total count          : \t %" PRIu64 "\n", c.total_count);
+    fprintf(f, "# Total weigh          : \t %" PRIu64 "\n", c.total_weight);
+    if (c.na_miss_count)
+      fprintf(f, "# N/A                  : \t %" PRIu64 " (%f %%)\n", c.na_miss_count,
+              100. * c.na_miss_count / c.total_count);
+    auto line = [&](int b, const char* name) {
+      const nmg_count& k = c.b[b];
+      if (!k.count) return;
+      double pct = 100. * k.count / c.total_count;
+      uint64_t avg = k.count ? k.sum_weight / k.count : 0;
+      double wpct = c.total_weight ? 100. * k.sum_weight / c.total_weight : 0;
+      fprintf(f,
+              "# %s\t: %ld (%f %%) \tmin: %" PRIu64 " cycles\tmax: %" PRIu64 " cycles\t avg: %" PRIu64
+              " cycles\ttotal weight: %" PRIu64 " (%f %%)\n",
+              name, (long)k.count, pct, k.min_weight, k.max_weight, avg, k.sum_weight, wpct);
+    };
+    for (int g = 0; g < 9; g++) line(g, kHitNames[g]);
+    fprintf(f, "\n");
+    for (int g = 3; g < 9; g++) line(9 + g, kMissNames[g]);
+  }
+}
+
+// Per-site page x thread matrix (__plot_counters input): dense unless huge.
+struct SiteHist {
+  uint64_t rows = 0;
+  uint32_t T = 0;
+  bool dense = true;
+  std::vector<uint32_t> cells;                    // [page][thread]
+  std::unordered_map<uint64_t, uint32_t> sparse;  // page * T + thread
+  void init(uint64_t r, uint32_t t) {
+    rows = r;
+    T = t;
+    dense = r * t <= (1ull << 26);
+    if (dense) cells.assign(r * t, 0);
+  }
+  void add(uint64_t page, uint32_t th, uint32_t v) {
+    if (page >= rows || th >= T) return;
+    if (dense) cells[page * T + th] += v;
+    else sparse[page * T + th] += v;
+  }
+  uint32_t get(uint64_t page, uint32_t th) const {
+    if (dense) return cells[page * T + th];
+    auto it = sparse.find(page * T + th);
+    return it == sparse.end() ? 0 : it->second;
+  }
+};
+
+}  // namespace
+
+int write_report(const nmg_host_results* r, const nmg_object_meta* meta, const nmg_report_options* opts,
+                 const char* stdout_path, std::string& err) {
+  const uint32_t E = r->nb_entries;
+  const uint32_t T = r->nb_threads;
+  FILE* out = stdout;
+  if (stdout_path) {
+    out = fopen(stdout_path, "w");
+    if (!out) {
+      err = std::string("cannot open ") + stdout_path;
+      return NMG_ERR_IO;
+    }
+  }
+  auto close_out = [&]() {
+    if (out != stdout) fclose(out);
+    else fflush(out);
+  };
+
+  // ---- mem_sampling_finalize's messages (mem_sampling.c:321-344)
+  const int nbuf = (int)r->nb_buffers;
+  fprintf(out, "Analyzing %d sample buffers\n", nbuf);
+  uint64_t so_far = 0, found_total = 0;
+  size_t total_bytes = 0;
+  for (int b = 0; b < nbuf; b++) {
+    if (b % 10 == 0)
+      fprintf(out, "\rAnalyzing sample buffer %d/%d. Total samples so far: %zu", b, nbuf, (size_t)so_far);
+    so_far += (uint64_t)(int64_t)(int32_t)r->buf_samples[b];  // int nb_samples (:325, :334)
+    found_total += (uint64_t)(int64_t)(int32_t)r->buf_found[b];
+    total_bytes += r->buf_bytes[b];
+  }
+  const uint64_t nb_samples_total = so_far;
+  fprintf(out, "\n");
+  fprintf(out, "%zu bytes processed\n", total_bytes);
+  fprintf(out, "---------------------------------\n");
+  fprintf(out, "         MEM ANALYZER\n");
+  fprintf(out, "---------------------------------\n");
+
+  // ---- call sites
+  Registry reg(meta);
+  std::vector<uint32_t> matched;
+  if (r->match_samples) {
+    for (uint32_t e = 0; e < E; e++)
+      if (r->first_ordinal[e] != ~0ull) matched.push_back(e);
+    for (uint32_t e : matched)
+      if (meta[e].callstack == nullptr && meta[e].callstack_size > 3) {
+        close_out();
+        err = "entry with NULL callstack and callstack_size > 3 (the reference dereferences NULL)";
+        return NMG_ERR_INVALID;
+      }
+    // creation: in the analysis order of each object's first matched sample
+    std::vector<uint32_t> order(matched);
+    std::sort(order.begin(), order.end(),
+              [&](uint32_t a, uint32_t b) { return r->first_ordinal[a] < r->first_ordinal[b]; });
+    for (uint32_t e : order)
+      if (reg.find(e) < 0) reg.create(e, r->buffer_size[e] / kPageSize + 1);
+    // update_call_sites in FOREACH_HASH order (= flattened order)
+    for (uint32_t e : matched) {
+      Site& site = reg.sites[reg.find(e)];
+      site.nb_mallocs++;
+      const uint64_t* cw = r->count_weight + (uint64_t)e * 4;
+      site.read_count += cw[0];
+      site.read_weight += cw[1];
+      site.write_count += cw[2];
+      site.write_weight += cw[3];
+      site.objects.push_back(e);
+    }
+  }
+  std::vector<Site>& sites = reg.sites;
+
+  // ---- ma_finalize prints (mem_analyzer.c:1877-1881)
+  print_counters(out, r->global);
+  fprintf(out, "Summary of the call sites:\n");
+  fprintf(out, "--------------------------\n");
+  fprintf(out, "Sorting call sites\n");
+  std::vector<int64_t> order = sort_sites(sites);
+
+  const char* dir = opts && opts->output_dir ? opts->output_dir : ".";
+  const bool dump_single = opts ? opts->dump_single_items != 0 : true;
+  mkdir(dir, S_IRWXU);  // get_log_dir (mem_intercept.c:402-409)
+  std::string cs_path = std::string(dir) + "/call_sites.log";
+  FILE* cf = fopen(cs_path.c_str(), "w");
+  if (!cf) {
+    close_out();
+    err = "cannot open " + cs_path;
+    return NMG_ERR_IO;
+  }
+  // per-entry ranges of the (entry, thread, page, count) rows
+  std::vector<int64_t> cell_begin;
+  auto index_cells = [&]() {
+    if (!cell_begin.empty()) return;
+    cell_begin.assign((size_t)E + 1, 0);
+    for (int64_t i = 0; i < r->nb_cells; i++) cell_begin[r->cells[4 * i] + 1]++;
+    for (uint32_t e = 0; e < E; e++) cell_begin[e + 1] += cell_begin[e];
+  };
+
+  int rc = NMG_OK;
+  std::string line;
+  char cell[16];
+  for (int64_t idx : order) {
+    const Site& s = sites[idx];
+    if (!(s.read_count || s.write_count)) continue;
+    double avg = 0;
+    if (s.read_count) avg = (double)s.read_weight / s.read_count;
+    for (int k = 0; k < 2; k++)
+      fprintf(k ? out : cf,
+              "%d\t%s (size=%zu) - %d buffers. %zu read access (total weight: %" PRIu64
+              ", avg weight: %f). %" PRIu64 " wr_access\n",
+              (int)s.id, s.caller.c_str(), (size_t)s.buffer_size, (int)s.nb_mallocs, (size_t)s.read_count,
+              s.read_weight, avg, s.write_count);
+    if (dump_single && s.mem_type != kMemTypeStack) {
+      // __plot_counters: (buffer_size / 4096 + 1) rows x next_thread_rank columns
+      index_cells();
+      SiteHist sh;
+      uint64_t rows = s.mem_info_buffer_size / kPageSize + 1;
+      sh.init(rows, T);
+      for (uint32_t e : s.objects)
+        for (int64_t i = cell_begin[e]; i < cell_begin[e + 1]; i++) {
+          const uint32_t* c = r->cells + 4 * i;
+          sh.add(c[2], c[1], c[3]);
+        }
+      char fn[4096];
+      snprintf(fn, sizeof(fn), "%s/callsite_counters_%d.dat", dir, (int)s.id);
+      FILE* df = fopen(fn, "w");
+      if (!df) {
+        rc = NMG_ERR_IO;
+        err = std::string("cannot open ") + fn;
+        break;
+      }
+      for (uint64_t i = 0; i < rows; i++) {
+        line.clear();
+        for (uint32_t th = 0; th < T; th++) {
+          int n = snprintf(cell, sizeof(cell), "\t%d", (int)sh.get(i, th));
+          line.append(cell, n);
+        }
+        line.push_back('\n');
+        fwrite(line.data(), 1, line.size(), df);
+      }
+      fclose(df);
+    }
+  }
+  fclose(cf);
+  if (rc) {
+    close_out();
+    return rc;
+  }
+  // mem_sampling_statistics (mem_sampling.c:357-361): a float percentage
+  float percent = 100.0 * (nb_samples_total - found_total) / nb_samples_total;
+  fprintf(out, "%" PRIu64 " samples (including %" PRIu64 " samples that do not match a known memory buffer / %f%%)\n",
+          nb_samples_total, nb_samples_total - found_total, percent);
+  close_out();
+  return NMG_OK;
+}
+
+}  // namespace nmg
+
+extern "C" int nmg_report_host(const nmg_host_results* res, const nmg_object_meta* meta,
+                               const nmg_report_options* opts, const char* stdout_path) {
+  if (!res || (res->nb_entries && (!meta || !res->first_ordinal || !res->count_weight || !res->buffer_size)) ||
+      (res->nb_buffers && (!res->buf_samples || !res->buf_found || !res->buf_bytes)) ||
+      (res->nb_cells && !res->cells) || res->nb_threads > NMG_MAX_THREADS)
+    return NMG_ERR_INVALID;
+  for (int64_t i = 0; i < res->nb_cells; i++)
+    if (res->cells[4 * i] >= res->nb_entries || (i && res->cells[4 * i] < res->cells[4 * i - 4]))
+      return NMG_ERR_INVALID;
+  std::string err;
+  int rc = nmg::write_report(res, meta, opts, stdout_path, err);
+  if (rc && !err.empty()) fprintf(stderr, "nmg_report: %s\n", err.c_str());
+  return rc;
+}

@@ -1,0 +1,145 @@
+"""Multi-GPU analysis: one process per GPU, buffers sharded, counters merged
+with RCCL (torch.distributed "nccl") over xGMI.
+
+The reference analyses the `samples` list on one thread
+(src/mem_sampling.c:324-342); each buffer is independent given the read-only
+object table (__analyze_buffer only reads samples->thread_rank/access_type and
+the table), so the analysis-ordered buffer list is split into contiguous,
+byte-balanced ranges, one per rank.  Every rank carries its range's global
+analysis index (seq_base) so first-match ordinals stay globally comparable.
+The only exchange step is the merge of the counters:
+
+* u64 sums (global counts/weights, per-object counts/weights/levels)  -> SUM
+* u64 mins (global bucket min_weight, first-match ordinals, error word) -> MIN
+* u64 maxes (global bucket max_weight)                                 -> MAX
+* u32 page histogram                                                   -> SUM
+* sparse page cells, per-buffer counts: variable length -> gathered to the root
+
+RCCL reduces int64, not uint64: sums are bit-identical under two's
+complement; MIN/MAX use the order-preserving map x ^ 2^63.
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+
+INT64_MIN = -(1 << 63)
+
+
+def shard_ranges(lengths: Sequence[int], world: int) -> List[Tuple[int, int]]:
+    """Contiguous [lo, hi) buffer ranges with balanced byte counts."""
+    lengths = np.asarray(lengths, dtype=np.int64)
+    n = lengths.shape[0]
+    if world <= 1 or n == 0:
+        return [(0, n)] + [(n, n)] * max(0, world - 1)
+    csum = np.concatenate([[0], np.cumsum(lengths)])
+    total = csum[-1]
+    cuts = [0]
+    for r in range(1, world):
+        target = total * r / world
+        c = int(np.searchsorted(csum, target, side="left"))
+        cuts.append(min(max(c, cuts[-1]), n))
+    cuts.append(n)
+    return [(cuts[r], cuts[r + 1]) for r in range(world)]
+
+
+def reduce_u64(t, op: str, dst: Optional[int] = 0, group=None):
+    """Reduce a tensor of u64 bit patterns stored as int64.  dst=None -> all-reduce."""
+    import torch
+    import torch.distributed as dist
+
+    assert t.dtype == torch.int64
+    flip = op in ("min", "max")
+    if flip:
+        t.bitwise_xor_(INT64_MIN)
+    rop = {"sum": dist.ReduceOp.SUM, "min": dist.ReduceOp.MIN, "max": dist.ReduceOp.MAX}[op]
+    if dst is None:
+        dist.all_reduce(t, op=rop, group=group)
+    else:
+        dist.reduce(t, dst=dst, op=rop, group=group)
+    if flip:
+        t.bitwise_xor_(INT64_MIN)
+    return t
+
+
+def reduce_u32_sum(t, dst: Optional[int] = 0, group=None):
+    import torch
+    import torch.distributed as dist
+
+    assert t.dtype == torch.int32
+    if dst is None:
+        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+    else:
+        dist.reduce(t, dst=dst, op=dist.ReduceOp.SUM, group=group)
+    return t
+
+
+def gather_arrays(a: np.ndarray, dst: int = 0, group=None):
+    """Variable-length gather of a numpy array; returns the list on dst."""
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group)
+    out = [None] * world if dist.get_rank(group) == dst else None
+    dist.gather_object(a, out, dst=dst, group=group)
+    return out
+
+
+def merge_sparse(parts) -> Tuple[np.ndarray, np.ndarray]:
+    keys = np.concatenate([p[0] for p in parts]) if parts else np.zeros(0, np.uint64)
+    vals = np.concatenate([p[1] for p in parts]) if parts else np.zeros(0, np.uint32)
+    if keys.shape[0] == 0:
+        return keys.astype(np.uint64), vals.astype(np.uint32)
+    u, inv = np.unique(keys, return_inverse=True)
+    s = np.zeros(u.shape[0], dtype=np.uint64)
+    np.add.at(s, inv, vals.astype(np.uint64))
+    return u, (s & 0xFFFFFFFF).astype(np.uint32)
+
+
+def merge_engine(eng, dst: int = 0, group=None, device=None) -> None:
+    """Merge every rank's partial counters into rank dst's engine (RCCL reduce
+    of the dense arrays over xGMI; gathers of the small variable-length ones)."""
+    import torch
+    import torch.distributed as dist
+
+    from . import _lib
+
+    rank = dist.get_rank(group)
+    dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
+    for which, op in ((_lib.NMG_ARR_SUM64, "sum"), (_lib.NMG_ARR_MIN64, "min"), (_lib.NMG_ARR_MAX64, "max")):
+        n = eng.array_size(which)
+        if n == 0:
+            continue
+        t = torch.empty(n, dtype=torch.int64, device=dev)
+        eng.export_array(which, t.data_ptr())
+        reduce_u64(t, op, dst=dst, group=group)
+        if rank == dst:
+            torch.cuda.synchronize(dev)
+            eng.import_array(which, t.data_ptr())
+    n = eng.array_size(_lib.NMG_ARR_HIST32)
+    if n:
+        t = torch.empty(n, dtype=torch.int32, device=dev)
+        eng.export_array(_lib.NMG_ARR_HIST32, t.data_ptr())
+        reduce_u32_sum(t, dst=dst, group=group)
+        if rank == dst:
+            torch.cuda.synchronize(dev)
+            eng.import_array(_lib.NMG_ARR_HIST32, t.data_ptr())
+    merge_host_side(eng, dst=dst, group=group)
+
+
+def merge_host_side(eng, dst: int = 0, group=None) -> None:
+    """Sparse page cells and per-buffer counts (variable length): gathered."""
+    import torch.distributed as dist
+
+    rank = dist.get_rank(group)
+    k, v = eng.sparse_export()
+    parts = gather_arrays(np.stack([k, v.astype(np.uint64)]) if k.shape[0] else np.zeros((2, 0), np.uint64),
+                          dst=dst, group=group)
+    s, f = eng.buffer_counts()
+    nbytes = np.asarray(eng.buffer_bytes, dtype=np.uint64)
+    counts = gather_arrays(np.stack([s.astype(np.uint64), f.astype(np.uint64), nbytes]), dst=dst, group=group)
+    if rank == dst:
+        keys, vals = merge_sparse([(p[0], p[1].astype(np.uint32)) for p in parts])
+        eng.sparse_import(keys, vals)
+        allc = np.concatenate(counts, axis=1)
+        eng.set_buffer_counts(allc[0].astype(np.uint32), allc[1].astype(np.uint32), allc[2])

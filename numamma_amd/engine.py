@@ -1,0 +1,217 @@
+"""Python handle on the MI355X engine (thin wrapper over the C-ABI).
+
+Mirrors the reference's analysis interface: ``set_objects`` takes the object
+table snapshot, ``submit_ring`` is ``__copy_buffer`` (src/mem_sampling.c:675),
+``analyze`` is the ``while(samples)`` loop of ``mem_sampling_finalize``
+(:311-346) and ``report`` is the report half of ``ma_finalize``
+(src/mem_analyzer.c:1802-1884).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Optional
+
+import numpy as np
+
+from . import _lib
+from ._lib import check, lib
+from .replay import ObjectTable, Replay
+
+
+def _ptr(a: np.ndarray, ctype):
+    return a.ctypes.data_as(C.POINTER(ctype))
+
+
+def counters_to_numpy(c: "_lib.nmg_mem_counters") -> np.ndarray:
+    """struct mem_counters -> u64[75] (total_count, total_weight, na, 18 x (count, min, max, sum))."""
+    return np.frombuffer(bytes(c), dtype="<u8").copy()
+
+
+class Engine:
+    def __init__(self, device: int = 0, flags: int = _lib.NMG_F_DEFAULT, nb_threads: int = 1,
+                 hist_budget_bytes: int = 0, sparse_capacity: int = 0):
+        opt = _lib.nmg_options(device, flags, nb_threads, 0, hist_budget_bytes, sparse_capacity)
+        h = _lib.H()
+        check(lib.nmg_create(C.byref(h), C.byref(opt)))
+        self.h = h
+        self.flags = flags
+        self.nb_threads = nb_threads
+        self._keep = []
+        self.table: Optional[ObjectTable] = None
+        self.buffer_bytes: list = []  # lengths of the analysed (non-empty) buffers
+
+    def close(self):
+        if self.h:
+            lib.nmg_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _c(self, rc):
+        return check(rc, self.h)
+
+    # ------------------------------------------------------------------
+    def set_objects(self, table: ObjectTable):
+        ent = table.entries
+        objs = np.zeros(table.nb_entries, dtype=[("a", "<u8"), ("s", "<u8"), ("al", "<u8"), ("fr", "<u8")])
+        objs["a"] = ent["buffer_addr"]
+        objs["s"] = ent["buffer_size"]
+        objs["al"] = ent["alloc_date"]
+        objs["fr"] = ent["free_date"]
+        keys = np.ascontiguousarray(table.keys, dtype=np.uint64)
+        off = np.ascontiguousarray(table.entry_off, dtype=np.uint32)
+        self._c(lib.nmg_set_objects(self.h, _ptr(keys, C.c_uint64), _ptr(off, C.c_uint32), keys.shape[0],
+                                    objs.ctypes.data_as(C.POINTER(_lib.nmg_object)), table.nb_entries))
+        self.table = table
+
+    def submit_ring(self, ring: np.ndarray, tail: int, head: int, thread_rank: int, access: int):
+        ring = np.ascontiguousarray(ring, dtype=np.uint8)
+        self._c(lib.nmg_submit_ring(self.h, ring.ctypes.data, ring.shape[0], tail, head, thread_rank, access))
+        n = (head - tail) if head >= tail else ring.shape[0] - tail + head
+        if n:
+            self.buffer_bytes.append(n)
+
+    def submit_buffer(self, data: np.ndarray, thread_rank: int, access: int):
+        data = np.ascontiguousarray(data, dtype=np.uint8)
+        self._c(lib.nmg_submit_buffer(self.h, data.ctypes.data, data.shape[0], thread_rank, access))
+        if data.shape[0]:
+            self.buffer_bytes.append(data.shape[0])
+
+    def submit_replay(self, replay: Replay):
+        for b in replay.buffers:
+            self.submit_ring(b.ring, b.data_tail, b.data_head, b.thread_rank, b.access_type)
+
+    def set_device_buffers(self, d_ptr: int, offsets, lengths, ranks, access, seq_base: int = 0):
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        lengths = np.ascontiguousarray(lengths, dtype=np.uint64)
+        ranks = np.ascontiguousarray(ranks, dtype=np.uint32)
+        access = np.ascontiguousarray(access, dtype=np.uint32)
+        self._keep = [offsets, lengths, ranks, access]
+        self._c(lib.nmg_set_device_buffers(self.h, C.c_void_p(d_ptr), _ptr(offsets, C.c_uint64),
+                                           _ptr(lengths, C.c_uint64), _ptr(ranks, C.c_uint32),
+                                           _ptr(access, C.c_uint32), offsets.shape[0], seq_base))
+        self.buffer_bytes = [int(x) for x in lengths if x]
+
+    def clear_buffers(self):
+        self._c(lib.nmg_clear_buffers(self.h))
+        self.buffer_bytes = []
+
+    def analyze(self):
+        self._c(lib.nmg_analyze(self.h))
+
+    def synchronize(self):
+        self._c(lib.nmg_synchronize(self.h))
+
+    def reset(self):
+        self._c(lib.nmg_reset_counters(self.h))
+
+    def last_analyze_ms(self) -> float:
+        ms = C.c_float()
+        self._c(lib.nmg_last_analyze_ms(self.h, C.byref(ms)))
+        return ms.value
+
+    # ------------------------------------------------------------------
+    def global_counters(self):
+        out = (_lib.nmg_mem_counters * 2)()
+        ns, nf = C.c_uint64(), C.c_uint64()
+        self._c(lib.nmg_get_global_counters(self.h, out, C.byref(ns), C.byref(nf)))
+        return np.stack([counters_to_numpy(out[0]), counters_to_numpy(out[1])]), ns.value, nf.value
+
+    def buffer_counts(self):
+        n = lib.nmg_get_nb_buffers(self.h)
+        s = np.zeros(n, dtype=np.uint32)
+        f = np.zeros(n, dtype=np.uint32)
+        self._c(lib.nmg_get_buffer_counts(self.h, _ptr(s, C.c_uint32), _ptr(f, C.c_uint32)))
+        return s, f
+
+    def object_counters(self):
+        E = self.table.nb_entries
+        first = np.zeros(E, dtype=np.uint64)
+        cw = np.zeros((E, 2, 2), dtype=np.uint64)
+        self._c(lib.nmg_get_object_counters(self.h, _ptr(first, C.c_uint64), _ptr(cw, C.c_uint64)))
+        return first, cw
+
+    def object_levels(self):
+        E = self.table.nb_entries
+        lv = np.zeros((E, 2, 37), dtype=np.uint64)
+        self._c(lib.nmg_get_object_levels(self.h, _ptr(lv, C.c_uint64)))
+        return lv
+
+    def page_cells(self) -> np.ndarray:
+        n = lib.nmg_count_page_cells(self.h)
+        self._c(n)
+        rows = np.zeros((n, 4), dtype=np.uint32)
+        self._c(lib.nmg_get_page_cells(self.h, _ptr(rows, C.c_uint32), n))
+        return rows
+
+    # ------------------------------------------------------------------
+    def report(self, output_dir: str, stdout_path: Optional[str] = None, dump_single_items: int = 1):
+        meta, keep = build_meta(self.table)
+        ro = _lib.nmg_report_options(output_dir.encode(), dump_single_items, 0)
+        self._c(lib.nmg_report(self.h, meta, C.byref(ro), stdout_path.encode() if stdout_path else None))
+        del keep
+
+    # ---- multi-GPU merge helpers
+    def array_size(self, which: int) -> int:
+        return int(lib.nmg_array_size(self.h, which))
+
+    def export_array(self, which: int, d_dst: int):
+        self._c(lib.nmg_export_array(self.h, which, C.c_void_p(d_dst)))
+
+    def import_array(self, which: int, d_src: int):
+        self._c(lib.nmg_import_array(self.h, which, C.c_void_p(d_src)))
+
+    def sparse_export(self):
+        n = lib.nmg_sparse_count(self.h)
+        self._c(n)
+        k = np.zeros(n, dtype=np.uint64)
+        v = np.zeros(n, dtype=np.uint32)
+        self._c(lib.nmg_sparse_export(self.h, _ptr(k, C.c_uint64), _ptr(v, C.c_uint32), n))
+        return k, v
+
+    def sparse_import(self, keys: np.ndarray, counts: np.ndarray):
+        keys = np.ascontiguousarray(keys, dtype=np.uint64)
+        counts = np.ascontiguousarray(counts, dtype=np.uint32)
+        self._c(lib.nmg_sparse_import(self.h, _ptr(keys, C.c_uint64), _ptr(counts, C.c_uint32), keys.shape[0]))
+
+    def set_buffer_counts(self, samples: np.ndarray, found: np.ndarray, nbytes: np.ndarray):
+        samples = np.ascontiguousarray(samples, dtype=np.uint32)
+        found = np.ascontiguousarray(found, dtype=np.uint32)
+        nbytes = np.ascontiguousarray(nbytes, dtype=np.uint64)
+        self._c(lib.nmg_set_buffer_counts(self.h, samples.shape[0], _ptr(samples, C.c_uint32),
+                                          _ptr(found, C.c_uint32), _ptr(nbytes, C.c_uint64)))
+
+
+def build_meta(table: ObjectTable):
+    """nmg_object_meta[] for the call-site registry (+ objects to keep alive)."""
+    E = table.nb_entries
+    meta = (_lib.nmg_object_meta * E)()
+    ent = table.entries
+    pool = np.ascontiguousarray(table.callstack_pool, dtype=np.uint64)
+    pool_ptr = pool.ctypes.data
+    strings = C.create_string_buffer(table.string_pool + b"\0", len(table.string_pool) + 1)
+    sbase = C.addressof(strings)
+    for e in range(E):
+        m = meta[e]
+        r = ent[e]
+        m.initial_buffer_size = int(r["initial_buffer_size"])
+        m.caller_rip = int(r["caller_rip"])
+        m.callstack_size = int(r["callstack_size"])
+        m.mem_type = int(r["mem_type"])
+        m.id = int(r["id"])
+        if r["has_callstack"]:
+            m.callstack = C.cast(C.c_void_p(pool_ptr + 8 * int(r["callstack_off"])), C.POINTER(C.c_uint64))
+        if int(r["caller_off"]) != 0xFFFFFFFF:
+            m.caller = C.cast(C.c_void_p(sbase + int(r["caller_off"])), C.c_char_p)
+    return meta, (pool, strings)
+
+
+def run_replay(path: str, output_dir: str, stdout_path: Optional[str] = None, raw_path: Optional[str] = None,
+               device: int = 0, flags: int = _lib.NMG_F_DEFAULT) -> None:
+    """The nmg_replay CLI in-process (C++ driver)."""
+    check(lib.nmg_run_replay(path.encode(), output_dir.encode(), stdout_path.encode() if stdout_path else None,
+                             raw_path.encode() if raw_path else None, device, flags))

@@ -1,0 +1,36 @@
+/*
+ * nmg_oracle.h -- TEST INFRASTRUCTURE ONLY (see nmg_oracle.c header).
+ * CPU restatement of NumaMMa's offline sample-analysis path.
+ */
+#ifndef NMG_ORACLE_H
+#define NMG_ORACLE_H
+#include <stdint.h>
+
+#define NMO_ERR_IO -1
+#define NMO_ERR_FORMAT -2
+#define NMO_ERR_ZERO_SIZE -3
+#define NMO_ERR_TRUNCATED -4
+
+struct nmo_settings {
+  int match_samples;     /* settings.match_samples (numamma.h.in:27) */
+  int dump_single_items; /* settings.dump_single_items (numamma.h.in:32) */
+};
+
+struct nmo_timing {
+  double analysis_s; /* mem_sampling_finalize() loop */
+  double total_s;    /* analysis + report */
+  uint64_t nb_samples;
+};
+
+/* Run the whole offline analysis of a replay file: writes the reference's
+ * stdout report to stdout_path (or stdout), call_sites.log and
+ * callsite_counters_<id>.dat into outdir, and (optionally) the canonical
+ * raw-results dump to raw_path.  Returns 0 or a NMO_ERR_* code. */
+int nmo_run(const char *replay_path, const char *outdir, const char *stdout_path,
+            const char *raw_path, const struct nmo_settings *settings,
+            struct nmo_timing *timing);
+const char *nmo_strerror(int rc);
+int64_t nmo_lookup(const uint64_t *keys, const uint32_t *entry_off, uint32_t nb_keys,
+                   const uint64_t *ent4, uint64_t addr, uint64_t ts);
+
+#endif

@@ -1,0 +1,93 @@
+"""TEST INFRASTRUCTURE ONLY -- ctypes access to the CPU oracle (liboracle.so)
+and to the reference's own AVL index (oracle/_ref/libref_hash.so).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may use
+this module, and only as the checker / CPU baseline.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ORACLE_SO = os.path.join(HERE, "liboracle.so")
+REF_SO = os.path.join(HERE, "_ref", "libref_hash.so")
+REF_HASH_TEST = os.path.join(HERE, "_ref", "hash_test")
+
+
+def build(quiet: bool = True) -> None:
+    """make -C oracle (the reference pieces only build where /root/reference exists)."""
+    subprocess.run(["make", "-C", HERE], check=True, stdout=subprocess.DEVNULL if quiet else None)
+
+
+class _Settings(C.Structure):
+    _fields_ = [("match_samples", C.c_int), ("dump_single_items", C.c_int)]
+
+
+class _Timing(C.Structure):
+    _fields_ = [("analysis_s", C.c_double), ("total_s", C.c_double), ("nb_samples", C.c_uint64)]
+
+
+_oracle = None
+
+
+def oracle():
+    global _oracle
+    if _oracle is None:
+        if not os.path.exists(ORACLE_SO):
+            build()
+        lib = C.CDLL(ORACLE_SO)
+        lib.nmo_run.restype = C.c_int
+        lib.nmo_run.argtypes = [C.c_char_p, C.c_char_p, C.c_char_p, C.c_char_p, C.POINTER(_Settings), C.POINTER(_Timing)]
+        lib.nmo_strerror.restype = C.c_char_p
+        lib.nmo_strerror.argtypes = [C.c_int]
+        lib.nmo_lookup.restype = C.c_int64
+        lib.nmo_lookup.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint64, C.c_uint64]
+        _oracle = lib
+    return _oracle
+
+
+def run(replay_path: str, outdir: str, stdout_path: str, raw_path: str | None = None,
+        match_samples: bool = True, dump_single_items: bool = True) -> dict:
+    lib = oracle()
+    s = _Settings(int(match_samples), int(dump_single_items))
+    t = _Timing()
+    rc = lib.nmo_run(replay_path.encode(), outdir.encode(), stdout_path.encode(),
+                     raw_path.encode() if raw_path else None, C.byref(s), C.byref(t))
+    if rc:
+        raise RuntimeError(f"oracle failed: {lib.nmo_strerror(rc).decode()} ({rc})")
+    return {"analysis_s": t.analysis_s, "total_s": t.total_s, "nb_samples": t.nb_samples}
+
+
+def lookup(keys, entry_off, ent4, addr: int, ts: int) -> int:
+    import numpy as np
+
+    keys = np.ascontiguousarray(keys, dtype=np.uint64)
+    entry_off = np.ascontiguousarray(entry_off, dtype=np.uint32)
+    ent4 = np.ascontiguousarray(ent4, dtype=np.uint64)
+    return oracle().nmo_lookup(keys.ctypes.data, entry_off.ctypes.data, keys.shape[0], ent4.ctypes.data, addr, ts)
+
+
+_ref = None
+
+
+def ref_available() -> bool:
+    return os.path.exists(REF_SO)
+
+
+def ref():
+    """The reference's tools/hash.c (unchanged) behind oracle/ref_hash_shim.c."""
+    global _ref
+    if _ref is None:
+        lib = C.CDLL(REF_SO)
+        lib.ref_reset.restype = None
+        lib.ref_insert.argtypes = [C.c_uint64, C.c_uint64]
+        lib.ref_insert.restype = None
+        lib.ref_lower_key.argtypes = [C.c_uint64, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.c_int]
+        lib.ref_lower_key.restype = C.c_int
+        lib.ref_foreach.argtypes = [C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.c_int64]
+        lib.ref_foreach.restype = C.c_int64
+        lib.ref_size.restype = C.c_int
+        _ref = lib
+    return _ref

@@ -1,0 +1,42 @@
+"""The C-ABI library loads, exports every symbol include/numamma_gpu.h
+declares, and fails loudly (no CPU fallback) when no GPU is present."""
+import ctypes as C
+
+import pytest
+import torch
+
+from numamma_amd import _lib
+
+
+def test_all_declared_symbols_exported():
+    declared = _lib.declared_symbols()
+    assert len(declared) >= 30
+    missing = [s for s in declared if not hasattr(_lib.lib, s)]
+    assert missing == []
+
+
+def test_strerror_names_every_code():
+    for code in range(-10, 1):
+        msg = _lib.lib.nmg_strerror(code).decode()
+        assert msg and msg != "unknown error"
+
+
+def test_struct_layouts_match_reference():
+    # struct mem_counters is 600 bytes in the reference (mem_analyzer.h:17-41)
+    assert C.sizeof(_lib.nmg_mem_counters) == 600
+    assert C.sizeof(_lib.nmg_count) == 32
+
+
+@pytest.mark.skipif(torch.cuda.device_count() > 0, reason="GPU present")
+def test_create_fails_loudly_without_gpu():
+    from numamma_amd.engine import Engine
+
+    with pytest.raises(_lib.NmgError) as ei:
+        Engine(device=0)
+    assert ei.value.code == -2  # NMG_ERR_HIP
+
+
+def test_null_arguments_rejected():
+    assert _lib.lib.nmg_create(None, None) == -1
+    assert _lib.lib.nmg_analyze(None) == -1
+    assert _lib.lib.nmg_report_host(None, None, None, None) == -1

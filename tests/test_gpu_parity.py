@@ -1,0 +1,255 @@
+"""Parity of the HIP engine (through the C-ABI) with the CPU oracle.
+
+Bit-exact: every counter of the canonical raw-results dump, the stdout
+report, call_sites.log and every callsite_counters_<id>.dat -- on seeded
+synthetic replays (edge cases included), on the README fixture, at the full
+configs[1] size (10M samples, 1k intervals), through the device-resident
+entry point, and through a sharded two-engine merge."""
+import os
+
+import numpy as np
+import pytest
+
+import pyoracle
+import readme_fixture
+from numamma_amd import _lib
+from numamma_amd.replay import RECORD_DTYPE, SynthConfig, generate
+from numamma_amd.results import RawResults, report_host
+
+pytestmark = pytest.mark.gpu
+
+
+def _oracle(rp, d):
+    path = os.path.join(d, "replay.bin")
+    rp.write(path)
+    odir = os.path.join(d, "oracle")
+    pyoracle.run(path, odir, os.path.join(d, "oracle_stdout.txt"), os.path.join(d, "oracle_raw.bin"))
+    return path, odir
+
+
+def _engine_replay(path, d, flags=_lib.NMG_F_DEFAULT):
+    from numamma_amd.engine import run_replay
+
+    edir = os.path.join(d, "engine")
+    run_replay(path, edir, os.path.join(d, "engine_stdout.txt"), os.path.join(d, "engine_raw.bin"), flags=flags)
+    return edir
+
+
+def _same_dirs(a, b):
+    fa, fb = sorted(os.listdir(a)), sorted(os.listdir(b))
+    assert fa == fb
+    for f in fa:
+        assert open(os.path.join(a, f), "rb").read() == open(os.path.join(b, f), "rb").read(), f
+
+
+def _assert_raw_equal(pa, pb):
+    a, b = RawResults.read(pa), RawResults.read(pb)
+    assert np.array_equal(a.global_counters, b.global_counters)
+    assert (a.nb_samples, a.nb_found) == (b.nb_samples, b.nb_found)
+    assert np.array_equal(a.buf_samples, b.buf_samples) and np.array_equal(a.buf_found, b.buf_found)
+    assert np.array_equal(a.entries, b.entries)
+    assert np.array_equal(a.cells, b.cells)
+    assert open(pa, "rb").read() == open(pb, "rb").read()
+
+
+CONFIGS = [
+    SynthConfig(nb_samples=200_000, nb_intervals=1_000, seed=1),
+    SynthConfig(nb_samples=100_000, nb_intervals=5_000, nb_threads=5, lost_frac=1e-3, wrap_one=True, seed=2),
+    SynthConfig(nb_samples=50_000, nb_intervals=20, nb_threads=64, site_ratio=1.0, seed=3),
+    SynthConfig(nb_samples=80_000, nb_intervals=3_000, reuse_frac=0.4, realloc_frac=0.2, frac_gap=0.3,
+                buffer_records=97, seed=4),
+    SynthConfig(nb_samples=30_000, nb_intervals=1, nb_globals=0, with_stack=False, buffer_records=10_000, seed=5),
+    SynthConfig(nb_samples=60_000, nb_intervals=200_000, size_min=8, size_max=512, seed=6),
+]
+
+
+@pytest.mark.parametrize("cfg", CONFIGS, ids=[f"cfg{i}" for i in range(len(CONFIGS))])
+def test_engine_bit_exact_vs_oracle(tmp_path, cfg):
+    d = str(tmp_path)
+    path, odir = _oracle(generate(cfg), d)
+    edir = _engine_replay(path, d)
+    _assert_raw_equal(os.path.join(d, "oracle_raw.bin"), os.path.join(d, "engine_raw.bin"))
+    assert open(os.path.join(d, "oracle_stdout.txt"), "rb").read() == open(os.path.join(d, "engine_stdout.txt"), "rb").read()
+    _same_dirs(odir, edir)
+
+
+def test_readme_block_on_gpu(tmp_path):
+    d = str(tmp_path)
+    path, odir = _oracle(readme_fixture.build(), d)
+    _engine_replay(path, d)
+    got = readme_fixture.normalize(open(os.path.join(d, "engine_stdout.txt"), newline="").read())
+    assert got == readme_fixture.expected_lines()
+    _assert_raw_equal(os.path.join(d, "oracle_raw.bin"), os.path.join(d, "engine_raw.bin"))
+
+
+def test_full_config2_bit_exact(tmp_path):
+    """BASELINE configs[1] at full size: 10M records, 1k intervals."""
+    d = str(tmp_path)
+    path, odir = _oracle(generate(SynthConfig(nb_samples=10_000_000, nb_intervals=1_000, seed=42)), d)
+    edir = _engine_replay(path, d)
+    _assert_raw_equal(os.path.join(d, "oracle_raw.bin"), os.path.join(d, "engine_raw.bin"))
+    _same_dirs(odir, edir)
+
+
+def test_no_match_mode(tmp_path):
+    d = str(tmp_path)
+    rp = generate(SynthConfig(nb_samples=40_000, nb_intervals=100, seed=8))
+    path = os.path.join(d, "replay.bin")
+    rp.write(path)
+    pyoracle.run(path, os.path.join(d, "oracle"), os.path.join(d, "o.txt"), os.path.join(d, "oracle_raw.bin"),
+                 match_samples=False)
+    _engine_replay(path, d, flags=_lib.NMG_F_PAGE_HIST)
+    assert open(os.path.join(d, "o.txt"), "rb").read() == open(os.path.join(d, "engine_stdout.txt"), "rb").read()
+
+
+def test_sparse_histogram_path(tmp_path):
+    """Every object's page histogram forced sparse (hashed cells)."""
+    from numamma_amd.engine import Engine
+
+    d = str(tmp_path)
+    rp = generate(SynthConfig(nb_samples=100_000, nb_intervals=400, seed=9))
+    path, odir = _oracle(rp, d)
+    eng = Engine(flags=_lib.NMG_F_DEFAULT, nb_threads=rp.nb_threads, hist_budget_bytes=4, sparse_capacity=1 << 16)
+    eng.set_objects(rp.table)
+    eng.submit_replay(rp)
+    eng.analyze()
+    eng.synchronize()
+    edir = os.path.join(d, "engine")
+    eng.report(edir, os.path.join(d, "e.txt"))
+    assert open(os.path.join(d, "oracle_stdout.txt"), "rb").read() == open(os.path.join(d, "e.txt"), "rb").read()
+    _same_dirs(odir, edir)
+    raw = RawResults.read(os.path.join(d, "oracle_raw.bin"))
+    assert np.array_equal(eng.page_cells(), raw.cells)
+
+
+def test_device_resident_buffers(tmp_path):
+    """nmg_set_device_buffers on a torch-allocated HBM arena == staged path."""
+    import torch
+    from numamma_amd.engine import Engine
+
+    d = str(tmp_path)
+    rp = generate(SynthConfig(nb_samples=150_000, nb_intervals=2_000, lost_frac=1e-3, seed=10))
+    path, odir = _oracle(rp, d)
+    arena, offs, lens, ranks, acc = rp.packed()
+    dev = torch.from_numpy(arena).cuda()
+    eng = Engine(nb_threads=rp.nb_threads)
+    eng.set_objects(rp.table)
+    eng.set_device_buffers(dev.data_ptr(), offs, lens, ranks, acc)
+    for _ in range(3):  # reset + analyse repeatedly: no state leaks between steps
+        eng.reset()
+        eng.analyze()
+    eng.synchronize()
+    edir = os.path.join(d, "engine")
+    eng.report(edir, os.path.join(d, "e.txt"))
+    assert open(os.path.join(d, "oracle_stdout.txt"), "rb").read() == open(os.path.join(d, "e.txt"), "rb").read()
+    _same_dirs(odir, edir)
+    raw = RawResults.read(os.path.join(d, "oracle_raw.bin"))
+    first, cw = eng.object_counters()
+    assert np.array_equal(first, raw.first_ordinal)
+    assert np.array_equal(cw, raw.count_weight)
+    g, ns, nf = eng.global_counters()
+    assert np.array_equal(g, raw.global_counters) and (ns, nf) == (raw.nb_samples, raw.nb_found)
+
+
+def test_two_shard_merge_matches_single(tmp_path):
+    """The multi-GPU scheme on one device: two engines, contiguous shards with
+    seq_base, merged (sum / min / max / gathers) -> identical report."""
+    import torch
+    from numamma_amd.distributed import merge_sparse, shard_ranges
+    from numamma_amd.engine import Engine
+
+    d = str(tmp_path)
+    rp = generate(SynthConfig(nb_samples=200_000, nb_intervals=3_000, seed=11))
+    path, odir = _oracle(rp, d)
+    arena, offs, lens, ranks, acc = rp.packed()
+    dev = torch.from_numpy(arena).cuda()
+    engines = []
+    for lo, hi in shard_ranges(lens, 2):
+        e = Engine(nb_threads=rp.nb_threads, hist_budget_bytes=4, sparse_capacity=1 << 18)
+        e.set_objects(rp.table)
+        e.set_device_buffers(dev.data_ptr(), offs[lo:hi], lens[lo:hi], ranks[lo:hi], acc[lo:hi], seq_base=lo)
+        e.analyze()
+        e.synchronize()
+        engines.append(e)
+    # merge into engine 0 exactly as merge_engine does over RCCL
+    for which, op in ((_lib.NMG_ARR_SUM64, "sum"), (_lib.NMG_ARR_MIN64, "min"), (_lib.NMG_ARR_MAX64, "max")):
+        n = engines[0].array_size(which)
+        ts = []
+        for e in engines:
+            t = torch.empty(n, dtype=torch.int64, device="cuda")
+            e.export_array(which, t.data_ptr())
+            ts.append(t)
+        if op == "sum":
+            m = ts[0] + ts[1]
+        else:
+            f = [t ^ torch.tensor(-(1 << 63), dtype=torch.int64, device="cuda") for t in ts]
+            m = (torch.minimum(*f) if op == "min" else torch.maximum(*f)) ^ torch.tensor(-(1 << 63), dtype=torch.int64, device="cuda")
+        torch.cuda.synchronize()
+        engines[0].import_array(which, m.data_ptr())
+    parts = [e.sparse_export() for e in engines]
+    engines[0].sparse_import(*merge_sparse(parts))
+    cs = [e.buffer_counts() for e in engines]
+    engines[0].set_buffer_counts(np.concatenate([c[0] for c in cs]), np.concatenate([c[1] for c in cs]),
+                                 np.concatenate([np.array(e.buffer_bytes, dtype=np.uint64) for e in engines]))
+    edir = os.path.join(d, "engine")
+    engines[0].report(edir, os.path.join(d, "e.txt"))
+    assert open(os.path.join(d, "oracle_stdout.txt"), "rb").read() == open(os.path.join(d, "e.txt"), "rb").read()
+    _same_dirs(odir, edir)
+
+
+def _one_buffer_replay(raw_bytes):
+    from numamma_amd.replay import Buffer, Replay
+
+    rp = generate(SynthConfig(nb_samples=100, nb_intervals=10, seed=1))
+    rp.buffers = [Buffer(0, 0, np.frombuffer(raw_bytes, dtype=np.uint8).copy(), 0, len(raw_bytes))]
+    return rp
+
+
+@pytest.mark.parametrize("case,code", [("zero_size", -4), ("truncated", -5), ("odd_size", -9)])
+def test_error_codes(tmp_path, case, code):
+    """Malformed records: the reference abort()s (size 0, mem_sampling.c:857)
+    or reads out of bounds (truncated SAMPLE, :865-879); the engine returns
+    the matching NMG_ERR_* code instead."""
+    from numamma_amd.engine import Engine
+
+    rec = np.zeros(20, dtype=RECORD_DTYPE)
+    rec["type"] = 9
+    rec["size"] = 40
+    raw = bytearray(rec.tobytes())
+    if case == "zero_size":
+        raw[40 * 7 + 6:40 * 7 + 8] = b"\0\0"
+    elif case == "truncated":
+        raw = raw[:-16]
+    else:
+        raw[40 * 3 + 6:40 * 3 + 8] = (44).to_bytes(2, "little")
+    rp = _one_buffer_replay(bytes(raw))
+    eng = Engine(nb_threads=rp.nb_threads)
+    eng.set_objects(rp.table)
+    eng.submit_replay(rp)
+    eng.analyze()
+    with pytest.raises(_lib.NmgError) as ei:
+        eng.synchronize()
+    assert ei.value.code == code
+
+
+def test_empty_inputs(tmp_path):
+    """No buffers at all, and an empty object table."""
+    from numamma_amd.engine import Engine
+    from numamma_amd.replay import ObjectTable
+
+    rp = generate(SynthConfig(nb_samples=1000, nb_intervals=10, seed=1))
+    eng = Engine(nb_threads=rp.nb_threads)
+    eng.set_objects(rp.table)
+    eng.analyze()
+    eng.synchronize()
+    g, ns, nf = eng.global_counters()
+    assert ns == 0 and nf == 0
+    empty = ObjectTable(np.zeros(0, np.uint64), np.zeros(1, np.uint32), rp.table.entries[:0],
+                        np.zeros(0, np.uint64), b"")
+    eng2 = Engine(nb_threads=rp.nb_threads)
+    eng2.set_objects(empty)
+    eng2.submit_replay(rp)
+    eng2.analyze()
+    eng2.synchronize()
+    g, ns, nf = eng2.global_counters()
+    assert ns == rp.nb_records() and nf == 0

@@ -1,0 +1,73 @@
+"""Replay format, ring linearisation (__copy_buffer) and the generator."""
+import numpy as np
+import pytest
+
+from numamma_amd.replay import (RECORD_BYTES, Buffer, Replay, SynthConfig, flatten_insertions,
+                                generate)
+
+
+def test_roundtrip(tmp_path):
+    rp = generate(SynthConfig(nb_samples=20_000, nb_intervals=300, lost_frac=1e-3, wrap_one=True, seed=3))
+    p = str(tmp_path / "r.bin")
+    rp.write(p)
+    back = Replay.read(p)
+    assert back.nb_threads == rp.nb_threads
+    assert np.array_equal(back.table.keys, rp.table.keys)
+    assert np.array_equal(back.table.entry_off, rp.table.entry_off)
+    assert back.table.entries.tobytes() == rp.table.entries.tobytes()
+    assert back.table.string_pool == rp.table.string_pool
+    assert len(back.buffers) == len(rp.buffers)
+    for a, b in zip(back.buffers, rp.buffers):
+        assert (a.thread_rank, a.access_type, a.data_tail, a.data_head) == (b.thread_rank, b.access_type, b.data_tail, b.data_head)
+        assert np.array_equal(a.ring, b.ring)
+
+
+def test_generator_is_deterministic():
+    a = generate(SynthConfig(nb_samples=5000, nb_intervals=100, seed=11))
+    b = generate(SynthConfig(nb_samples=5000, nb_intervals=100, seed=11))
+    assert a.table.entries.tobytes() == b.table.entries.tobytes()
+    assert all(np.array_equal(x.ring, y.ring) for x, y in zip(a.buffers, b.buffers))
+
+
+def test_copy_buffer_semantics():
+    """__copy_buffer (mem_sampling.c:675-738): [tail, head) with wrap; empty
+    segments are dropped."""
+    ring = np.arange(100, dtype=np.uint8)
+    assert np.array_equal(Buffer(0, 0, ring, 10, 30).linear(), ring[10:30])
+    wrapped = Buffer(0, 0, ring, 90, 8).linear()
+    assert np.array_equal(wrapped, np.concatenate([ring[90:], ring[:8]]))
+    assert Buffer(0, 0, ring, 42, 42).linear().shape[0] == 0
+
+
+def test_generator_shape():
+    cfg = SynthConfig(nb_samples=50_000, nb_intervals=500, seed=5)
+    rp = generate(cfg)
+    t = rp.table
+    t.validate()
+    assert rp.nb_records() == cfg.nb_samples
+    # every buffer fits a 128 KiB ring (mem_sampling.c:298)
+    assert max(b.ring.shape[0] for b in rp.buffers) <= 3276 * RECORD_BYTES
+    # address reuse -> keys with two entries; globals share one size and a NULL rip
+    assert np.any(np.diff(t.entry_off.astype(np.int64)) == 2)
+    glob = t.entries[t.entries["mem_type"] == 1]
+    assert glob.shape[0] == cfg.nb_globals and np.all(glob["caller_rip"] == 0)
+    assert t.entries[-1]["mem_type"] == 2  # [stack]
+    # analysis order is newest capture first (LIFO list)
+    first_ts = [int(np.frombuffer(b.ring[8:16].tobytes(), "<u8")[0]) for b in rp.buffers]
+    assert first_ts[0] >= first_ts[-1]
+
+
+def test_flatten_insertions_lifo():
+    keys, off, order = flatten_insertions([30, 10, 30, 20, 10, 30])
+    assert list(keys) == [10, 20, 30]
+    assert list(off) == [0, 2, 3, 6]
+    assert list(order) == [4, 1, 3, 5, 2, 0]
+
+
+def test_packed_alignment():
+    rp = generate(SynthConfig(nb_samples=9000, nb_intervals=50, lost_frac=5e-3, seed=2))
+    arena, offs, lens, ranks, acc = rp.packed()
+    assert np.all(offs % 16 == 0)
+    lin = rp.linear_buffers()
+    for (r, a, data), o, n in zip(lin, offs, lens):
+        assert np.array_equal(arena[int(o):int(o) + int(n)], data)
