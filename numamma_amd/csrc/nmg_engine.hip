@@ -34,13 +34,19 @@
 
 namespace nmg {
 
-constexpr int kWG = 256;
+constexpr int kWG = 512;
 constexpr int kSegBytes = 20480;               // 512 x 40 B records per LDS window
 constexpr int kLdsBytes = kSegBytes + 64;      // + overlap: a record starting in the window has its 40 B
 constexpr int kMaxFences = 1024;               // LDS fence table (8 KiB)
 constexpr int kMaxList = kSegBytes / 8;        // slow path: record offsets of one window
 constexpr uint32_t kSampleType = 9;            // PERF_RECORD_SAMPLE
 constexpr uint32_t kRecBytes = 40;             // perf_event_header (8) + struct mem_sample (32)
+// per-buffer LDS aggregation tables (flushed to global once per buffer)
+constexpr uint32_t kObjSlots = 1024;           // entry -> (count, weight, first offset)
+constexpr uint32_t kPageSlots = 2048;          // (entry, page) -> count
+constexpr uint32_t kProbes = 32;
+constexpr uint32_t kEmpty32 = 0xffffffffu;
+constexpr uint64_t kEmpty64 = ~0ull;
 
 // PERF_MEM_LVL_* (/usr/include/linux/perf_event.h:1250-1263)
 constexpr uint32_t LVL_NA = 0x01, LVL_HIT = 0x02, LVL_MISS = 0x04;
@@ -163,14 +169,14 @@ __device__ __forceinline__ int64_t find_entry(const Params& p, const uint64_t* s
   return -1;
 }
 
-__device__ __forceinline__ void sparse_add(Params& p, uint64_t key, uint64_t seq, uint32_t off) {
+__device__ __forceinline__ void sparse_add(Params& p, uint64_t key, uint64_t seq, uint32_t off, uint32_t cnt) {
   uint64_t h = (key * 0x9E3779B97F4A7C15ull) >> 20;
   uint32_t slot = uint32_t(h) & p.sparse_mask;
   for (uint32_t probe = 0; probe <= p.sparse_mask; probe++) {
     unsigned long long prev = atomicCAS(reinterpret_cast<unsigned long long*>(p.sparse_keys + slot),
                                         ~0ull, (unsigned long long)key);
     if (prev == ~0ull || prev == key) {
-      atomicAdd(p.sparse_vals + slot, 1u);
+      atomicAdd(p.sparse_vals + slot, cnt);
       return;
     }
     slot = (slot + 1) & p.sparse_mask;
@@ -184,7 +190,35 @@ struct WgCounters {
   unsigned long long mins[18];
   unsigned long long maxs[18];
   unsigned int nb_samples, nb_found;
+  // per-buffer aggregation of the per-object counters: one buffer is one
+  // thread and one access type, so (entry) and (entry, page) are the keys
+  unsigned int okey[kObjSlots];
+  unsigned int ocnt[kObjSlots];
+  unsigned int ooff[kObjSlots];          // smallest record offset (first match)
+  unsigned long long owt[kObjSlots];
+  unsigned long long pkey[kPageSlots];   // (entry << 32) | page
+  unsigned int pcnt[kPageSlots];
 };
+
+__device__ __forceinline__ int obj_slot(WgCounters& wc, uint32_t e) {
+  uint32_t s = (e * 2654435761u) >> (32 - 10);
+  for (uint32_t i = 0; i < kProbes; i++) {
+    unsigned prev = atomicCAS(&wc.okey[s], kEmpty32, e);
+    if (prev == kEmpty32 || prev == e) return (int)s;
+    s = (s + 1) & (kObjSlots - 1);
+  }
+  return -1;
+}
+
+__device__ __forceinline__ int page_slot(WgCounters& wc, uint64_t key) {
+  uint32_t s = uint32_t((key * 0x9E3779B97F4A7C15ull) >> (64 - 11));
+  for (uint32_t i = 0; i < kProbes; i++) {
+    unsigned long long prev = atomicCAS(&wc.pkey[s], (unsigned long long)kEmpty64, (unsigned long long)key);
+    if (prev == kEmpty64 || prev == key) return (int)s;
+    s = (s + 1) & (kPageSlots - 1);
+  }
+  return -1;
+}
 
 // Process one decoded record (`valid` = it is a SAMPLE).  Every lane of the
 // wave calls this together (wave-level reductions inside).
@@ -242,20 +276,30 @@ __device__ __forceinline__ void process_sample(Params& p, WgCounters& wc, const 
   uint64_t fmask = __ballot(e >= 0);
   if (lane == 0 && fmask) atomicAdd(&wc.nb_found, (unsigned)__popcll(fmask));
   if (e < 0) return;
-  unsigned long long* cw = reinterpret_cast<unsigned long long*>(p.sum64 + objcw_index(e, access, 0));
-  atomicAdd(cw, 1ull);
-  if (w) atomicAdd(cw + 1, (unsigned long long)w);
-  // first match in analysis order -> call-site id order (quirk Q7)
-  uint64_t ord = (seq << 32) | off;
-  unsigned long long* fp = reinterpret_cast<unsigned long long*>(p.min64 + 36 + e);
-  if (ord < *fp) atomicMin(fp, (unsigned long long)ord);
+  // per-object counters, aggregated for the whole buffer in LDS
+  int os = obj_slot(wc, (uint32_t)e);
+  if (os >= 0) {
+    atomicAdd(&wc.ocnt[os], 1u);
+    if (w) atomicAdd(&wc.owt[os], (unsigned long long)w);
+    if (off < wc.ooff[os]) atomicMin(&wc.ooff[os], off);
+  } else {  // table full: straight to global
+    unsigned long long* cw = reinterpret_cast<unsigned long long*>(p.sum64 + objcw_index(e, access, 0));
+    atomicAdd(cw, 1ull);
+    if (w) atomicAdd(cw + 1, (unsigned long long)w);
+    // first match in analysis order -> call-site id order (quirk Q7)
+    uint64_t ord = (seq << 32) | off;
+    unsigned long long* fp = reinterpret_cast<unsigned long long*>(p.min64 + 36 + e);
+    if (ord < *fp) atomicMin(fp, (unsigned long long)ord);
+  }
   if (p.flags & NMG_F_PAGE_HIST) {
     // ma_get_block: page_no = (int)((addr - buffer_addr) / 4096) (mem_analyzer.c:530-531)
     uint32_t page = uint32_t(int(uint64_t(addr - ent.addr) / kPageSize));
-    if (ent.hist != kHistSparse) {
-      atomicAdd(p.hist + ent.hist + uint64_t(page) * p.nb_threads + th, 1u);
-    } else if (ent.sidx != ~0u) {
-      sparse_add(p, sparse_key(ent.sidx, th, page), seq, off);
+    int ps = (ent.hist != kHistSparse || ent.sidx != ~0u) ? page_slot(wc, (uint64_t(e) << 32) | page) : -2;
+    if (ps >= 0) {
+      atomicAdd(&wc.pcnt[ps], 1u);
+    } else if (ps == -1) {
+      if (ent.hist != kHistSparse) atomicAdd(p.hist + ent.hist + uint64_t(page) * p.nb_threads + th, 1u);
+      else sparse_add(p, sparse_key(ent.sidx, th, page), seq, off, 1u);
     }
   }
   if (p.flags & NMG_F_OBJECT_LEVELS) {
@@ -290,6 +334,16 @@ __global__ __launch_bounds__(kWG) void attribute_kernel(Params p) {
     const uint8_t* base = p.data + d.offset;
     const uint32_t len = d.len;
     for (int i = tid; i < (int)kGlobalSums; i += kWG) wc.sums[i] = 0;
+    for (int i = tid; i < (int)kObjSlots; i += kWG) {
+      wc.okey[i] = kEmpty32;
+      wc.ocnt[i] = 0;
+      wc.ooff[i] = kEmpty32;
+      wc.owt[i] = 0;
+    }
+    for (int i = tid; i < (int)kPageSlots; i += kWG) {
+      wc.pkey[i] = kEmpty64;
+      wc.pcnt[i] = 0;
+    }
     if (tid < 18) {
       wc.mins[tid] = ~0ull;  // INIT_COUNTER: min = UINT64_MAX (mem_analyzer.c:415-420)
       wc.maxs[tid] = 0;
@@ -406,6 +460,27 @@ __global__ __launch_bounds__(kWG) void attribute_kernel(Params p) {
       atomicAdd(p.bufcnt + b, wc.nb_samples);
       atomicAdd(p.bufcnt + p.nb_bufs + b, wc.nb_found);
     }
+    // per-object counters of this buffer: one global update per distinct key
+    for (int i = tid; i < (int)kObjSlots; i += kWG) {
+      uint32_t e = wc.okey[i];
+      if (e == kEmpty32) continue;
+      unsigned long long* cw = reinterpret_cast<unsigned long long*>(p.sum64 + objcw_index(e, a, 0));
+      atomicAdd(cw, (unsigned long long)wc.ocnt[i]);
+      if (wc.owt[i]) atomicAdd(cw + 1, wc.owt[i]);
+      uint64_t ord = (d.seq << 32) | wc.ooff[i];
+      unsigned long long* fp = reinterpret_cast<unsigned long long*>(p.min64 + 36 + e);
+      if (ord < *fp) atomicMin(fp, (unsigned long long)ord);
+    }
+    for (int i = tid; i < (int)kPageSlots; i += kWG) {
+      uint64_t k = wc.pkey[i];
+      if (k == kEmpty64) continue;
+      uint32_t e = uint32_t(k >> 32), page = uint32_t(k);
+      const uint4* q = reinterpret_cast<const uint4*>(p.entries + e);
+      uint4 c = q[2];
+      uint64_t hist = (uint64_t(c.y) << 32) | c.x;
+      if (hist != kHistSparse) atomicAdd(p.hist + hist + uint64_t(page) * p.nb_threads + d.thread_rank, wc.pcnt[i]);
+      else sparse_add(p, sparse_key(c.z, d.thread_rank, page), d.seq, 0, wc.pcnt[i]);
+    }
     __syncthreads();
   }
 }
@@ -424,6 +499,7 @@ struct nmg_engine {
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   int num_cus = 256;
+  int blocks_per_cu = 0;
   bool launched = false;
 
   // object table
@@ -892,7 +968,13 @@ extern "C" int nmg_analyze(nmg_engine* h) {
   p.sparse_vals = h->d_sparse_vals;
   HIP_TRY(h, hipEventRecord(h->ev0, h->stream));
   if (nb) {
-    uint32_t grid = std::min<uint32_t>(nb, (uint32_t)h->num_cus * 4);
+    if (h->blocks_per_cu <= 0) {
+      int bpc = 0;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, attribute_kernel, kWG, 0) != hipSuccess || bpc <= 0) bpc = 1;
+      h->blocks_per_cu = bpc;
+    }
+    // persistent grid: every resident workgroup walks buffers round-robin
+    uint32_t grid = std::min<uint32_t>(nb, (uint32_t)(h->num_cus * h->blocks_per_cu));
     hipLaunchKernelGGL(attribute_kernel, dim3(grid), dim3(kWG), 0, h->stream, p);
     HIP_TRY(h, hipGetLastError());
   }

@@ -1,0 +1,54 @@
+#!/bin/bash
+# One GPU-box session: parity tests, bench, rocprofv3 kernel trace.
+# Every GPU step has its own time limit; the first failure ends the call.
+#   gpurun -- bash tools/gpu_round.sh [tag] [stages...]
+#   stages: test bench prof smoke (default: test bench prof)
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
+TAG=${1:-r1}
+shift || true
+STAGES=${*:-test bench prof}
+OUT=gpurun_out
+mkdir -p $OUT
+export TMPDIR=/tmp
+ROOT=$PWD
+
+for s in $STAGES; do
+  case $s in
+    smoke)
+      echo "== smoke"
+      timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke_$TAG.log 2>&1 \
+        || { echo "smoke failed"; tail -40 $OUT/smoke_$TAG.log; exit 1; }
+      tail -3 $OUT/smoke_$TAG.log ;;
+    test)
+      echo "== pytest -m gpu"
+      timeout -k 10 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider > $OUT/pytest_gpu_$TAG.log 2>&1 \
+        || { echo "pytest failed"; tail -60 $OUT/pytest_gpu_$TAG.log; exit 1; }
+      tail -5 $OUT/pytest_gpu_$TAG.log ;;
+    bench)
+      echo "== bench"
+      timeout -k 10 600 python bench.py --steps 20 --warmup 3 > $OUT/bench_$TAG.json 2> $OUT/bench_$TAG.err \
+        || { echo "bench failed"; tail -40 $OUT/bench_$TAG.err; exit 1; }
+      cat $OUT/bench_$TAG.json ;;
+    bench3)
+      echo "== bench c3"
+      timeout -k 10 900 python bench.py --workload c3 --steps 10 --warmup 2 --no-cpu-baseline > $OUT/bench_c3_$TAG.json 2> $OUT/bench_c3_$TAG.err \
+        || { echo "bench c3 failed"; tail -40 $OUT/bench_c3_$TAG.err; exit 1; }
+      cat $OUT/bench_c3_$TAG.json ;;
+    prof)
+      echo "== rocprofv3 kernel trace"
+      rm -rf $OUT/prof_$TAG
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $ROOT/$OUT/prof_$TAG -o run --output-format csv \
+        -- python3 $ROOT/bench.py --steps 10 --warmup 2 --no-cpu-baseline > $OUT/prof_$TAG.log 2>&1 \
+        || { echo "rocprof failed"; tail -40 $OUT/prof_$TAG.log; exit 1; }
+      find $OUT/prof_$TAG -name "*kernel_stats.csv" -exec cat {} \; | head -20 ;;
+    pmc)
+      echo "== rocprofv3 pmc FETCH_SIZE"
+      rm -rf $OUT/pmc_$TAG
+      timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $ROOT/$OUT/pmc_$TAG -o run --output-format csv \
+        -- python3 $ROOT/bench.py --steps 5 --warmup 1 --no-cpu-baseline > $OUT/pmc_$TAG.log 2>&1 \
+        || { echo "rocprof pmc failed"; tail -40 $OUT/pmc_$TAG.log; exit 1; }
+      find $OUT/pmc_$TAG -name "*counter_collection.csv" -exec head -5 {} \; ;;
+  esac
+done
+echo "== done"
