@@ -122,14 +122,12 @@ def main():
     for _ in range(args.warmup):
         step()
     barrier()
-    kernel_ms = []
     t_start = time.perf_counter()
     for _ in range(args.steps):
         step()
-        eng.synchronize()  # also raises on a kernel-reported error
-        kernel_ms.append(eng.last_analyze_ms())
-    barrier()
+    barrier()  # device sync; raises on a kernel-reported error
     elapsed = time.perf_counter() - t_start
+    kernel_ms = eng.launch_times(min(args.steps, 64))  # HIP events on the engine stream
     if distributed:
         tt = torch.tensor([elapsed], dtype=torch.float64, device=device)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)

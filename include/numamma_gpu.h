@@ -199,6 +199,8 @@ int nmg_set_buffer_counts(nmg_engine *h, uint32_t nb_buffers, const uint32_t *nb
 
 /* ---- device timing of the last nmg_analyze (HIP events on the engine stream) ---- */
 int nmg_last_analyze_ms(nmg_engine *h, float *ms);
+/* durations of up to n most recent launches (oldest first, max 64); returns the count */
+int nmg_get_launch_times(nmg_engine *h, float *ms, int n);
 
 /*
  * Report: the stdout text of mem_sampling_finalize + ma_finalize from

@@ -42,11 +42,16 @@ constexpr int kMaxList = kSegBytes / 8;        // slow path: record offsets of o
 constexpr uint32_t kSampleType = 9;            // PERF_RECORD_SAMPLE
 constexpr uint32_t kRecBytes = 40;             // perf_event_header (8) + struct mem_sample (32)
 // per-buffer LDS aggregation tables (flushed to global once per buffer)
-constexpr uint32_t kObjSlots = 1024;           // entry -> (count, weight, first offset)
-constexpr uint32_t kPageSlots = 2048;          // (entry, page) -> count
+constexpr uint32_t kObjSlots = 1024;           // entry -> (count, weight, first ordinal)
+constexpr uint32_t kPageSlots = 2048;          // dense page cell -> count
 constexpr uint32_t kProbes = 32;
 constexpr uint32_t kEmpty32 = 0xffffffffu;
 constexpr uint64_t kEmpty64 = ~0ull;
+// internal ablation switches (tools/ablate.py only; not part of the C-ABI)
+constexpr uint32_t kDbgLoadOnly = 0x100;   // stage + validate windows, decode nothing
+constexpr uint32_t kDbgNoGlobal = 0x200;   // skip the global mem_counters update
+constexpr uint32_t kDbgNoFlush = 0x400;    // LDS tables filled but never written to global
+constexpr uint32_t kDbgNoTables = 0x800;   // lookup only: no per-object / per-page accumulation
 
 // PERF_MEM_LVL_* (/usr/include/linux/perf_event.h:1250-1263)
 constexpr uint32_t LVL_NA = 0x01, LVL_HIT = 0x02, LVL_MISS = 0x04;
@@ -80,6 +85,8 @@ static_assert(sizeof(DevEntry) == 64, "DevEntry");
 struct Params {
   const uint8_t* data;
   const BufDesc* bufs;
+  const uint32_t* order;   // buffers sorted by stream (access, thread_rank)
+  const uint32_t* ranges;  // [gridDim.x + 1]: workgroup w takes order[ranges[w] .. ranges[w+1])
   uint32_t nb_bufs;
   uint32_t nb_keys;
   const uint64_t* keys;
@@ -92,6 +99,7 @@ struct Params {
   uint32_t flags;
   uint32_t nb_entries;
   uint32_t sparse_mask;  // capacity - 1 (power of two)
+  uint64_t hist_cells;   // dense cells per thread: histogram index = thread * hist_cells + cell
   uint64_t* sum64;
   uint64_t* min64;
   uint64_t* max64;
@@ -108,6 +116,42 @@ __device__ __forceinline__ uint64_t wave_sum(uint64_t v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
+}
+
+// Full-wave u32 sum with DPP (VALU only, no LDS traffic): Hillis-Steele
+// within each 16-lane row, then row_bcast:15 / row_bcast:31; lane 63 holds
+// the total.
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ uint32_t dpp0(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROW_MASK, 0xf, true);
+}
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
+  v += dpp0<0x111, 0xf>(v);  // row_shr:1
+  v += dpp0<0x112, 0xf>(v);  // row_shr:2
+  v += dpp0<0x114, 0xf>(v);  // row_shr:4
+  v += dpp0<0x118, 0xf>(v);  // row_shr:8
+  v += dpp0<0x142, 0xa>(v);  // row_bcast:15 into rows 1 and 3
+  v += dpp0<0x143, 0xc>(v);  // row_bcast:31 into rows 2 and 3
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+// Sum of per-lane weights; `big` (wave-uniform) = some weight >= 2^26, in
+// which case 64 lanes could overflow 32 bits and the u64 path is taken.
+__device__ __forceinline__ uint64_t wave_sum_w(uint64_t w, bool big) {
+  return big ? wave_sum(w) : (uint64_t)wave_sum_u32((uint32_t)w);
+}
+
+// update_counters' level classification (mem_sampling.c:521-591) as an
+// 18-bit mask: bit g (0..8) = hit bucket of level group g, bit 9+g = miss.
+// Groups: L1, L2, L3, LFB, local RAM, remote RAM 1|2, remote cache 1|2, IO,
+// uncached (the bucket order of struct mem_counters).  HIT beats MISS and
+// every group is independent (quirk Q12).
+__device__ __forceinline__ uint32_t bucket_mask(uint32_t lvl) {
+  uint32_t g = ((lvl >> 3) & 1) | (((lvl >> 5) & 1) << 1) | (((lvl >> 6) & 1) << 2) |
+               (((lvl >> 4) & 1) << 3) | (((lvl >> 7) & 1) << 4) | ((((lvl >> 8) | (lvl >> 9)) & 1) << 5) |
+               ((((lvl >> 10) | (lvl >> 11)) & 1) << 6) | (((lvl >> 12) & 1) << 7) | (((lvl >> 13) & 1) << 8);
+  if (lvl & LVL_HIT) return g;
+  if (lvl & LVL_MISS) return g << 9;
+  return 0;
 }
 
 // Records are 8-byte multiples (sizes that are not are rejected), so every
@@ -194,35 +238,111 @@ struct WgCounters {
   // thread and one access type, so (entry) and (entry, page) are the keys
   unsigned int okey[kObjSlots];
   unsigned int ocnt[kObjSlots];
-  unsigned int ooff[kObjSlots];          // smallest record offset (first match)
+  unsigned long long ofirst[kObjSlots];  // smallest (seq << 32 | offset): first match
   unsigned long long owt[kObjSlots];
-  unsigned long long pkey[kPageSlots];   // (entry << 32) | page
+  unsigned int pkey[kPageSlots];         // dense cell index (hist_base(entry) + page)
   unsigned int pcnt[kPageSlots];
+  unsigned int nobj, npage;              // occupied slots
 };
 
+// Direct-mapped slots with linear probing: slot order follows key order, so
+// the flush walks entries / cells in (mostly) ascending address order and its
+// global atomics coalesce into shared 64-byte lines.  A slot already holding
+// the key (hot objects) is found with a plain broadcast read, no CAS.
 __device__ __forceinline__ int obj_slot(WgCounters& wc, uint32_t e) {
-  uint32_t s = (e * 2654435761u) >> (32 - 10);
+  uint32_t s = e & (kObjSlots - 1);
   for (uint32_t i = 0; i < kProbes; i++) {
-    unsigned prev = atomicCAS(&wc.okey[s], kEmpty32, e);
-    if (prev == kEmpty32 || prev == e) return (int)s;
+    unsigned k = wc.okey[s];
+    if (k == e) return (int)s;
+    if (k == kEmpty32) {
+      unsigned prev = atomicCAS(&wc.okey[s], kEmpty32, e);
+      if (prev == kEmpty32) {
+        atomicAdd(&wc.nobj, 1u);
+        return (int)s;
+      }
+      if (prev == e) return (int)s;
+    }
     s = (s + 1) & (kObjSlots - 1);
   }
   return -1;
 }
 
-__device__ __forceinline__ int page_slot(WgCounters& wc, uint64_t key) {
-  uint32_t s = uint32_t((key * 0x9E3779B97F4A7C15ull) >> (64 - 11));
+__device__ __forceinline__ int page_slot(WgCounters& wc, uint32_t cell) {
+  uint32_t s = cell & (kPageSlots - 1);
   for (uint32_t i = 0; i < kProbes; i++) {
-    unsigned long long prev = atomicCAS(&wc.pkey[s], (unsigned long long)kEmpty64, (unsigned long long)key);
-    if (prev == kEmpty64 || prev == key) return (int)s;
+    unsigned k = wc.pkey[s];
+    if (k == cell) return (int)s;
+    if (k == kEmpty32) {
+      unsigned prev = atomicCAS(&wc.pkey[s], kEmpty32, cell);
+      if (prev == kEmpty32) {
+        atomicAdd(&wc.npage, 1u);
+        return (int)s;
+      }
+      if (prev == cell) return (int)s;
+    }
     s = (s + 1) & (kPageSlots - 1);
   }
   return -1;
 }
 
+// Per-lane privatised mem_counters of the current stream: packed u16 counts
+// and u32 weight sums per bucket, plus total count / weight / N/A.  Bounded:
+// drained at least every kDrainWindows windows and only weights < 2^23 take
+// this path, so nothing overflows (256 x 2^23 = 2^31).
+constexpr uint32_t kDrainWindows = 256;
+constexpr uint64_t kLaneMaxWeight = 1ull << 23;
+// Only the 9 hit buckets live in registers (the common case in PEBS data);
+// miss buckets are updated in LDS directly.
+struct LaneAcc {
+  uint32_t cnt2[5];  // counts of hit buckets 2k (low 16 bits) and 2k+1 (high 16 bits)
+  uint32_t sum[9];
+  uint32_t tc, tw, na;
+};
+
+__device__ __forceinline__ void lane_acc_clear(LaneAcc& a) {
+#pragma unroll
+  for (int k = 0; k < 5; k++) a.cnt2[k] = 0;
+#pragma unroll
+  for (int k = 0; k < 9; k++) a.sum[k] = 0;
+  a.tc = a.tw = a.na = 0;
+}
+
+// exact sum over the wave of a u32 per lane (as two 16-bit halves, DPP)
+__device__ __forceinline__ uint64_t wave_sum_u32x(uint32_t v) {
+  const uint32_t lo = wave_sum_u32(v & 0xffffu), hi = wave_sum_u32(v >> 16);
+  return (uint64_t)lo + ((uint64_t)hi << 16);
+}
+
+// lanes -> workgroup LDS counters (every lane of the wave calls this)
+__device__ __forceinline__ void lane_acc_drain(LaneAcc& a, WgCounters& wc, int lane) {
+  if (__ballot(a.tc != 0) == 0) return;
+  const uint64_t tc = wave_sum_u32x(a.tc), tw = wave_sum_u32x(a.tw), na = wave_sum_u32x(a.na);
+  if (lane == 0) {
+    atomicAdd(&wc.sums[0], (unsigned long long)tc);
+    if (tw) atomicAdd(&wc.sums[1], (unsigned long long)tw);
+    if (na) atomicAdd(&wc.sums[2], (unsigned long long)na);
+  }
+#pragma unroll
+  for (int k = 0; k < 5; k++) {
+    if (__ballot(a.cnt2[k] != 0) == 0) continue;
+    const uint32_t c0 = wave_sum_u32(a.cnt2[k] & 0xffffu), c1 = wave_sum_u32(a.cnt2[k] >> 16);
+    if (lane == 0) {
+      if (c0) atomicAdd(&wc.sums[3 + 2 * (2 * k)], (unsigned long long)c0);
+      if (c1 && 2 * k + 1 < 9) atomicAdd(&wc.sums[3 + 2 * (2 * k + 1)], (unsigned long long)c1);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 9; k++) {
+    if (__ballot(a.sum[k] != 0) == 0) continue;
+    const uint64_t sk = wave_sum_u32x(a.sum[k]);
+    if (lane == 0) atomicAdd(&wc.sums[4 + 2 * k], (unsigned long long)sk);
+  }
+  lane_acc_clear(a);
+}
+
 // Process one decoded record (`valid` = it is a SAMPLE).  Every lane of the
 // wave calls this together (wave-level reductions inside).
-__device__ __forceinline__ void process_sample(Params& p, WgCounters& wc, const uint64_t* s_fences,
+__device__ __forceinline__ void process_sample(Params& p, WgCounters& wc, LaneAcc& acc, const uint64_t* s_fences,
                                                bool valid, uint64_t ts, uint64_t addr,
                                                uint64_t w, uint64_t dsrc, uint32_t access,
                                                uint32_t th, uint64_t seq, uint32_t off) {
@@ -231,43 +351,41 @@ __device__ __forceinline__ void process_sample(Params& p, WgCounters& wc, const 
   // ---- global counters: update_counters(global_counters, ...) (mem_sampling.c:882)
   uint64_t vmask = __ballot(valid);
   if (vmask == 0) return;
-  uint64_t wsum = wave_sum(valid ? w : 0);
-  uint64_t namask = __ballot(valid && (lvl & LVL_NA));
-  if (lane == 0) {
-    atomicAdd(&wc.sums[0], (unsigned long long)__popcll(vmask));
-    if (wsum) atomicAdd(&wc.sums[1], (unsigned long long)wsum);
-    if (namask) atomicAdd(&wc.sums[2], (unsigned long long)__popcll(namask));
-    atomicAdd(&wc.nb_samples, (unsigned)__popcll(vmask));
-  }
+  if (lane == 0) atomicAdd(&wc.nb_samples, (unsigned)__popcll(vmask));
+  if (valid && !(p.flags & kDbgNoGlobal)) {
+    const uint32_t bm = bucket_mask(lvl);
+    if (w < kLaneMaxWeight) {  // register accumulation (no LDS traffic)
+      const uint32_t w32 = (uint32_t)w;
+      acc.tc += 1;
+      acc.tw += w32;
+      acc.na += lvl & LVL_NA;
 #pragma unroll
-  for (int g = 0; g < 9; g++) {
-    bool has = valid && (lvl & c_level_mask[g]);
-    // HIT beats MISS; each level group is independent (quirk Q12)
-    int bucket = (lvl & LVL_HIT) ? g : ((lvl & LVL_MISS) ? 9 + g : -1);
-    bool in = has && bucket >= 0;
-    uint64_t m = __ballot(in);
-    if (m == 0) continue;
-    // buckets taken within a group differ only by HIT vs MISS
-    uint64_t mhit = __ballot(in && bucket == g);
-    uint64_t mmiss = m & ~mhit;
-    uint64_t shit = mhit ? wave_sum((in && bucket == g) ? w : 0) : 0;
-    uint64_t smiss = mmiss ? wave_sum((in && bucket != g) ? w : 0) : 0;
-    if (lane == 0) {
-      if (mhit) {
-        atomicAdd(&wc.sums[3 + 2 * g], (unsigned long long)__popcll(mhit));
-        if (shit) atomicAdd(&wc.sums[4 + 2 * g], (unsigned long long)shit);
+      for (int k = 0; k < 5; k++) acc.cnt2[k] += ((bm >> (2 * k)) & 1) | ((k < 4 ? (bm >> (2 * k + 1)) & 1 : 0) << 16);
+#pragma unroll
+      for (int k = 0; k < 9; k++) acc.sum[k] += ((bm >> k) & 1) * w32;
+      for (uint32_t m = bm >> 9; m; m &= m - 1) {  // miss buckets
+        const uint32_t b = 9 + (uint32_t)__builtin_ctz(m);
+        atomicAdd(&wc.sums[3 + 2 * b], 1ull);
+        if (w) atomicAdd(&wc.sums[4 + 2 * b], (unsigned long long)w);
       }
-      if (mmiss) {
-        atomicAdd(&wc.sums[3 + 2 * (9 + g)], (unsigned long long)__popcll(mmiss));
-        if (smiss) atomicAdd(&wc.sums[4 + 2 * (9 + g)], (unsigned long long)smiss);
+    } else {  // weights >= 2^23 cycles: straight to the LDS counters
+      atomicAdd(&wc.sums[0], 1ull);
+      atomicAdd(&wc.sums[1], (unsigned long long)w);
+      if (lvl & LVL_NA) atomicAdd(&wc.sums[2], 1ull);
+      for (uint32_t m = bm; m; m &= m - 1) {
+        const uint32_t b = (uint32_t)__builtin_ctz(m);
+        atomicAdd(&wc.sums[3 + 2 * b], 1ull);
+        atomicAdd(&wc.sums[4 + 2 * b], (unsigned long long)w);
       }
     }
     // min / max only move monotonically: read first, atomic only on improvement
-    if (in) {
-      if (w < wc.mins[bucket]) atomicMin(&wc.mins[bucket], (unsigned long long)w);
-      if (w > wc.maxs[bucket]) atomicMax(&wc.maxs[bucket], (unsigned long long)w);
+    for (uint32_t m = bm; m; m &= m - 1) {
+      const uint32_t b = (uint32_t)__builtin_ctz(m);
+      if (w < wc.mins[b]) atomicMin(&wc.mins[b], (unsigned long long)w);
+      if (w > wc.maxs[b]) atomicMax(&wc.maxs[b], (unsigned long long)w);
     }
   }
+match:
   if (!(p.flags & NMG_F_MATCH_SAMPLES)) return;
 
   // ---- __match_sample (mem_sampling.c:594-673)
@@ -275,17 +393,19 @@ __device__ __forceinline__ void process_sample(Params& p, WgCounters& wc, const 
   int64_t e = valid ? find_entry(p, s_fences, addr, ts, &ent) : -1;
   uint64_t fmask = __ballot(e >= 0);
   if (lane == 0 && fmask) atomicAdd(&wc.nb_found, (unsigned)__popcll(fmask));
-  if (e < 0) return;
+  if (e < 0 || (p.flags & kDbgNoTables)) return;
   // per-object counters, aggregated for the whole buffer in LDS
   int os = obj_slot(wc, (uint32_t)e);
   if (os >= 0) {
     atomicAdd(&wc.ocnt[os], 1u);
     if (w) atomicAdd(&wc.owt[os], (unsigned long long)w);
-    if (off < wc.ooff[os]) atomicMin(&wc.ooff[os], off);
+    const unsigned long long ord = (seq << 32) | off;
+    if (ord < wc.ofirst[os]) atomicMin(&wc.ofirst[os], ord);
   } else {  // table full: straight to global
-    unsigned long long* cw = reinterpret_cast<unsigned long long*>(p.sum64 + objcw_index(e, access, 0));
-    atomicAdd(cw, 1ull);
-    if (w) atomicAdd(cw + 1, (unsigned long long)w);
+    atomicAdd(reinterpret_cast<unsigned long long*>(p.sum64 + objcw_index(e, access, 0, p.nb_entries)), 1ull);
+    if (w)
+      atomicAdd(reinterpret_cast<unsigned long long*>(p.sum64 + objcw_index(e, access, 1, p.nb_entries)),
+                (unsigned long long)w);
     // first match in analysis order -> call-site id order (quirk Q7)
     uint64_t ord = (seq << 32) | off;
     unsigned long long* fp = reinterpret_cast<unsigned long long*>(p.min64 + 36 + e);
@@ -294,12 +414,13 @@ __device__ __forceinline__ void process_sample(Params& p, WgCounters& wc, const 
   if (p.flags & NMG_F_PAGE_HIST) {
     // ma_get_block: page_no = (int)((addr - buffer_addr) / 4096) (mem_analyzer.c:530-531)
     uint32_t page = uint32_t(int(uint64_t(addr - ent.addr) / kPageSize));
-    int ps = (ent.hist != kHistSparse || ent.sidx != ~0u) ? page_slot(wc, (uint64_t(e) << 32) | page) : -2;
-    if (ps >= 0) {
-      atomicAdd(&wc.pcnt[ps], 1u);
-    } else if (ps == -1) {
-      if (ent.hist != kHistSparse) atomicAdd(p.hist + ent.hist + uint64_t(page) * p.nb_threads + th, 1u);
-      else sparse_add(p, sparse_key(ent.sidx, th, page), seq, off, 1u);
+    if (ent.hist != kHistSparse) {
+      const uint32_t cell = uint32_t(ent.hist + page);
+      int ps = page_slot(wc, cell);
+      if (ps >= 0) atomicAdd(&wc.pcnt[ps], 1u);
+      else atomicAdd(p.hist + uint64_t(th) * p.hist_cells + cell, 1u);
+    } else if (ent.sidx != ~0u) {  // huge objects ([stack]): hashed cells in global memory
+      sparse_add(p, sparse_key(ent.sidx, th, page), seq, off, 1u);
     }
   }
   if (p.flags & NMG_F_OBJECT_LEVELS) {
@@ -317,9 +438,62 @@ __device__ __forceinline__ void process_sample(Params& p, WgCounters& wc, const 
 }
 
 // ---------------------------------------------------------------------------
+// per-workgroup aggregation state: reset, and flush to global memory
+
+__device__ __forceinline__ void reset_state(WgCounters& wc, int tid) {
+  for (int i = tid; i < (int)kGlobalSums; i += kWG) wc.sums[i] = 0;
+  for (int i = tid; i < (int)kObjSlots; i += kWG) {
+    wc.okey[i] = kEmpty32;
+    wc.ocnt[i] = 0;
+    wc.ofirst[i] = kEmpty64;
+    wc.owt[i] = 0;
+  }
+  for (int i = tid; i < (int)kPageSlots; i += kWG) {
+    wc.pkey[i] = kEmpty32;
+    wc.pcnt[i] = 0;
+  }
+  if (tid < 18) {
+    wc.mins[tid] = ~0ull;  // INIT_COUNTER: min = UINT64_MAX (mem_analyzer.c:415-420)
+    wc.maxs[tid] = 0;
+  }
+  if (tid == 0) {
+    wc.nobj = 0;
+    wc.npage = 0;
+  }
+}
+
+// One stream (access type a, thread rank th): global mem_counters[a], then one
+// global update per distinct entry / (entry, page) accumulated since the last flush.
+__device__ __forceinline__ void flush_state(Params& p, WgCounters& wc, int tid, uint32_t a, uint32_t th) {
+  if (p.flags & kDbgNoFlush) return;
+  for (int i = tid; i < (int)kGlobalSums; i += kWG)
+    if (wc.sums[i]) atomicAdd(reinterpret_cast<unsigned long long*>(p.sum64 + gsum_index(a, i)), wc.sums[i]);
+  if (tid < 18 && wc.sums[3 + 2 * tid]) {
+    atomicMin(reinterpret_cast<unsigned long long*>(p.min64 + a * 18 + tid), wc.mins[tid]);
+    atomicMax(reinterpret_cast<unsigned long long*>(p.max64 + a * 18 + tid), wc.maxs[tid]);
+  }
+  for (int i = tid; i < (int)kObjSlots; i += kWG) {
+    uint32_t e = wc.okey[i];
+    if (e == kEmpty32) continue;
+    atomicAdd(reinterpret_cast<unsigned long long*>(p.sum64 + objcw_index(e, a, 0, p.nb_entries)),
+              (unsigned long long)wc.ocnt[i]);
+    if (wc.owt[i])
+      atomicAdd(reinterpret_cast<unsigned long long*>(p.sum64 + objcw_index(e, a, 1, p.nb_entries)), wc.owt[i]);
+    unsigned long long* fp = reinterpret_cast<unsigned long long*>(p.min64 + 36 + e);
+    if (wc.ofirst[i] < *fp) atomicMin(fp, wc.ofirst[i]);
+  }
+  unsigned int* hrow = p.hist + uint64_t(th) * p.hist_cells;
+  for (int i = tid; i < (int)kPageSlots; i += kWG) {
+    uint32_t cell = wc.pkey[i];
+    if (cell != kEmpty32) atomicAdd(hrow + cell, wc.pcnt[i]);
+  }
+}
+
+// ---------------------------------------------------------------------------
 // the attribution kernel
 
-__global__ __launch_bounds__(kWG) void attribute_kernel(Params p) {
+// 2 workgroups of 512 threads per CU = 4 waves per SIMD (<= 128 VGPRs)
+__global__ __launch_bounds__(kWG, 4) void attribute_kernel(Params p) {
   __shared__ __attribute__((aligned(16))) uint8_t s_data[kLdsBytes];
   __shared__ uint64_t s_fences[kMaxFences];
   __shared__ uint16_t s_list[kMaxList];
@@ -329,24 +503,37 @@ __global__ __launch_bounds__(kWG) void attribute_kernel(Params p) {
   const int tid = threadIdx.x;
   for (uint32_t i = tid; i < p.nb_fences; i += kWG) s_fences[i] = p.fences[i];
 
-  for (uint32_t b = blockIdx.x; b < p.nb_bufs; b += gridDim.x) {
+  // This workgroup's contiguous, byte-balanced share of the stream-sorted
+  // buffer list.  Consecutive buffers of one stream (thread, access) share
+  // the LDS tables, so global updates happen once per stream run, not once
+  // per buffer.
+  const uint32_t r0 = p.ranges[blockIdx.x], r1 = p.ranges[blockIdx.x + 1];
+  const int lane = tid & 63;
+  uint32_t cur_access = ~0u, cur_thread = ~0u;
+  LaneAcc acc;
+  lane_acc_clear(acc);
+  uint32_t acc_windows = 0;
+  reset_state(wc, tid);
+  __syncthreads();
+  for (uint32_t idx = r0; idx < r1; idx++) {
+    const uint32_t b = p.order[idx];
     const BufDesc d = p.bufs[b];
     const uint8_t* base = p.data + d.offset;
     const uint32_t len = d.len;
-    for (int i = tid; i < (int)kGlobalSums; i += kWG) wc.sums[i] = 0;
-    for (int i = tid; i < (int)kObjSlots; i += kWG) {
-      wc.okey[i] = kEmpty32;
-      wc.ocnt[i] = 0;
-      wc.ooff[i] = kEmpty32;
-      wc.owt[i] = 0;
-    }
-    for (int i = tid; i < (int)kPageSlots; i += kWG) {
-      wc.pkey[i] = kEmpty64;
-      wc.pcnt[i] = 0;
-    }
-    if (tid < 18) {
-      wc.mins[tid] = ~0ull;  // INIT_COUNTER: min = UINT64_MAX (mem_analyzer.c:415-420)
-      wc.maxs[tid] = 0;
+    // leave room for a whole buffer (~1k distinct cells) so probe chains stay short;
+    // the flush itself is cheap (its atomics coalesce)
+    const bool full = wc.nobj > kObjSlots * 5 / 8 || wc.npage > kPageSlots / 4;
+    if (d.access != cur_access || d.thread_rank != cur_thread || full) {
+      if (cur_access != ~0u) {
+        lane_acc_drain(acc, wc, lane);
+        acc_windows = 0;
+        __syncthreads();
+        flush_state(p, wc, tid, cur_access, cur_thread);
+        __syncthreads();
+        reset_state(wc, tid);
+      }
+      cur_access = d.access;
+      cur_thread = d.thread_rank;
     }
     if (tid == 0) {
       wc.nb_samples = 0;
@@ -356,14 +543,27 @@ __global__ __launch_bounds__(kWG) void attribute_kernel(Params p) {
     __syncthreads();
 
     uint32_t cur = 0;  // byte cursor, as `cur_cpt` in __analyze_buffer
+    // next window's 16 B chunks, loaded into registers while the current
+    // window is processed (software pipelining of the HBM stream)
+    static_assert((kLdsBytes / 16 + kWG - 1) / kWG == 3, "three prefetch registers per lane");
+    uint4 pf0 = {0, 0, 0, 0}, pf1 = {0, 0, 0, 0}, pf2 = {0, 0, 0, 0};
+    uint32_t pf_win = ~0u;
+    const uint32_t len16 = (len + 15u) & ~15u;
     while (cur < len) {
       const uint32_t win = cur & ~15u;
-      const uint32_t win_end = min(win + (uint32_t)kLdsBytes, (len + 15u) & ~15u);
+      const uint32_t win_end = min(win + (uint32_t)kLdsBytes, len16);
       // ---- stage the window into LDS: coalesced 16 B loads
       const uint4* src = reinterpret_cast<const uint4*>(base + win);
       uint4* dst = reinterpret_cast<uint4*>(s_data);
       const uint32_t nchunks = (win_end - win) >> 4;
-      for (uint32_t c = tid; c < nchunks; c += kWG) dst[c] = src[c];
+      if (pf_win == win) {
+        if ((uint32_t)tid < nchunks) dst[tid] = pf0;
+        if ((uint32_t)tid + kWG < nchunks) dst[tid + kWG] = pf1;
+        if ((uint32_t)tid + 2 * kWG < nchunks) dst[tid + 2 * kWG] = pf2;
+      } else {
+        for (uint32_t c = tid; c < nchunks; c += kWG) dst[c] = src[c];
+      }
+      pf_win = ~0u;
       if (tid == 0) s_flag = 0;
       __syncthreads();
 
@@ -379,8 +579,20 @@ __global__ __launch_bounds__(kWG) void attribute_kernel(Params p) {
       if (bad) s_flag = 1;
       __syncthreads();
 
-      if (s_flag == 0) {
+      if (p.flags & kDbgLoadOnly) {
+        cur += n_cand * kRecBytes;
+      } else if (s_flag == 0) {
         // ---- fast path: decode all n_cand records in parallel
+        const uint32_t next = cur + n_cand * kRecBytes;
+        if (next < len) {  // issue the next window's loads now, consume them next iteration
+          const uint32_t nwin = next & ~15u;
+          const uint32_t nchunks2 = (min(nwin + (uint32_t)kLdsBytes, len16) - nwin) >> 4;
+          const uint4* nsrc = reinterpret_cast<const uint4*>(base + nwin);
+          if ((uint32_t)tid < nchunks2) pf0 = nsrc[tid];
+          if ((uint32_t)tid + kWG < nchunks2) pf1 = nsrc[tid + kWG];
+          if ((uint32_t)tid + 2 * kWG < nchunks2) pf2 = nsrc[tid + 2 * kWG];
+          pf_win = nwin;
+        }
         for (uint32_t i0 = 0; i0 < n_cand; i0 += kWG) {
           uint32_t i = i0 + tid;
           bool valid = false;
@@ -395,7 +607,7 @@ __global__ __launch_bounds__(kWG) void attribute_kernel(Params p) {
             w = lds_u64(s_data, o + 24);
             dsrc = lds_u64(s_data, o + 32);
           }
-          process_sample(p, wc, s_fences, valid, ts, addr, w, dsrc, d.access, d.thread_rank, d.seq, pos);
+          process_sample(p, wc, acc, s_fences, valid, ts, addr, w, dsrc, d.access, d.thread_rank, d.seq, pos);
         }
         cur += n_cand * kRecBytes;
       } else {
@@ -438,51 +650,63 @@ __global__ __launch_bounds__(kWG) void attribute_kernel(Params p) {
             w = lds_u64(s_data, o + 24);
             dsrc = lds_u64(s_data, o + 32);
           }
-          process_sample(p, wc, s_fences, valid, ts, addr, w, dsrc, d.access, d.thread_rank, d.seq,
+          process_sample(p, wc, acc, s_fences, valid, ts, addr, w, dsrc, d.access, d.thread_rank, d.seq,
                          win + o);
         }
         cur = s_next;
         if (s_err) break;  // the reference aborts here; stop this buffer
       }
+      if (++acc_windows == kDrainWindows) {  // keep the per-lane u32 sums bounded
+        lane_acc_drain(acc, wc, lane);
+        acc_windows = 0;
+      }
       __syncthreads();  // LDS window is rewritten next iteration
     }
     __syncthreads();
 
-    // ---- flush the buffer's counters (one set per access type)
-    const uint32_t a = d.access;
-    for (int i = tid; i < (int)kGlobalSums; i += kWG)
-      if (wc.sums[i]) atomicAdd(reinterpret_cast<unsigned long long*>(p.sum64 + gsum_index(a, i)), wc.sums[i]);
-    if (tid < 18 && wc.sums[3 + 2 * tid]) {
-      atomicMin(reinterpret_cast<unsigned long long*>(p.min64 + a * 18 + tid), wc.mins[tid]);
-      atomicMax(reinterpret_cast<unsigned long long*>(p.max64 + a * 18 + tid), wc.maxs[tid]);
-    }
     if (tid == 0) {
       atomicAdd(p.bufcnt + b, wc.nb_samples);
       atomicAdd(p.bufcnt + p.nb_bufs + b, wc.nb_found);
     }
-    // per-object counters of this buffer: one global update per distinct key
-    for (int i = tid; i < (int)kObjSlots; i += kWG) {
-      uint32_t e = wc.okey[i];
-      if (e == kEmpty32) continue;
-      unsigned long long* cw = reinterpret_cast<unsigned long long*>(p.sum64 + objcw_index(e, a, 0));
-      atomicAdd(cw, (unsigned long long)wc.ocnt[i]);
-      if (wc.owt[i]) atomicAdd(cw + 1, wc.owt[i]);
-      uint64_t ord = (d.seq << 32) | wc.ooff[i];
-      unsigned long long* fp = reinterpret_cast<unsigned long long*>(p.min64 + 36 + e);
-      if (ord < *fp) atomicMin(fp, (unsigned long long)ord);
-    }
-    for (int i = tid; i < (int)kPageSlots; i += kWG) {
-      uint64_t k = wc.pkey[i];
-      if (k == kEmpty64) continue;
-      uint32_t e = uint32_t(k >> 32), page = uint32_t(k);
-      const uint4* q = reinterpret_cast<const uint4*>(p.entries + e);
-      uint4 c = q[2];
-      uint64_t hist = (uint64_t(c.y) << 32) | c.x;
-      if (hist != kHistSparse) atomicAdd(p.hist + hist + uint64_t(page) * p.nb_threads + d.thread_rank, wc.pcnt[i]);
-      else sparse_add(p, sparse_key(c.z, d.thread_rank, page), d.seq, 0, wc.pcnt[i]);
-    }
     __syncthreads();
   }
+  if (cur_access != ~0u) {
+    lane_acc_drain(acc, wc, lane);
+    __syncthreads();
+    flush_state(p, wc, tid, cur_access, cur_thread);
+  }
+}
+
+// One launch re-initialises every counter array (INIT_COUNTER semantics:
+// sums and maxes 0, mins and first-match ordinals UINT64_MAX; sparse keys empty).
+struct ResetParams {
+  uint64_t* sum64;
+  uint64_t n_sum64;
+  uint64_t* min64;
+  uint64_t n_min64;
+  uint64_t* max64;
+  uint64_t n_max64;
+  uint4* hist;  // zeroed in 16 B units
+  uint64_t n_hist16;
+  uint64_t* sparse_keys;
+  uint32_t* sparse_vals;
+  uint64_t sparse_cap;
+  uint32_t* bufcnt;
+  uint64_t n_bufcnt;
+};
+
+__global__ __launch_bounds__(256) void reset_kernel(ResetParams r) {
+  const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
+  const uint64_t i0 = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  for (uint64_t i = i0; i < r.n_hist16; i += stride) r.hist[i] = make_uint4(0, 0, 0, 0);
+  for (uint64_t i = i0; i < r.n_sum64; i += stride) r.sum64[i] = 0;
+  for (uint64_t i = i0; i < r.n_min64; i += stride) r.min64[i] = ~0ull;
+  for (uint64_t i = i0; i < r.n_max64; i += stride) r.max64[i] = 0;
+  for (uint64_t i = i0; i < r.sparse_cap; i += stride) {
+    r.sparse_keys[i] = ~0ull;
+    r.sparse_vals[i] = 0;
+  }
+  for (uint64_t i = i0; i < r.n_bufcnt; i += stride) r.bufcnt[i] = 0;
 }
 
 }  // namespace nmg
@@ -498,6 +722,9 @@ struct nmg_engine {
   uint32_t T = 1;
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  static constexpr int kRing = 64;  // per-launch timing events (nmg_get_launch_times)
+  hipEvent_t ring0[kRing] = {}, ring1[kRing] = {};
+  uint64_t nlaunch = 0;
   int num_cus = 256;
   int blocks_per_cu = 0;
   bool launched = false;
@@ -535,6 +762,9 @@ struct nmg_engine {
   bool staged_dirty = false;
   BufDesc* d_descs = nullptr;
   size_t descs_cap = 0;
+  uint32_t* d_order = nullptr;   // stream-sorted buffer order
+  uint32_t* d_ranges = nullptr;  // per-workgroup [begin, end) in d_order
+  uint32_t sched_grid = 0;       // grid the current schedule was built for
   bool descs_dirty = false;
   uint32_t* d_bufcnt = nullptr;
   size_t bufcnt_cap = 0;
@@ -664,9 +894,15 @@ extern "C" void nmg_destroy(nmg_engine* h) {
   (void)hipFree(h->d_arena);
   (void)hipFree(h->d_descs);
   (void)hipFree(h->d_bufcnt);
+  (void)hipFree(h->d_order);
+  (void)hipFree(h->d_ranges);
   if (h->h_stage) (void)hipHostFree(h->h_stage);
   if (h->ev0) (void)hipEventDestroy(h->ev0);
   if (h->ev1) (void)hipEventDestroy(h->ev1);
+  for (int i = 0; i < nmg_engine::kRing; i++) {
+    if (h->ring0[i]) (void)hipEventDestroy(h->ring0[i]);
+    if (h->ring1[i]) (void)hipEventDestroy(h->ring1[i]);
+  }
   if (h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
 }
@@ -675,17 +911,30 @@ extern "C" int nmg_reset_counters(nmg_engine* h) {
   if (!h) return NMG_ERR_INVALID;
   if (!h->have_table) return fail(h, NMG_ERR_STATE, "nmg_reset_counters before nmg_set_objects");
   HIP_TRY(h, hipSetDevice(h->device));
-  HIP_TRY(h, hipMemsetAsync(h->d_sum64, 0, h->n_sum64 * 8, h->stream));
-  HIP_TRY(h, hipMemsetAsync(h->d_min64, 0xff, h->n_min64 * 8, h->stream));
-  HIP_TRY(h, hipMemsetAsync(h->d_max64, 0, h->n_max64 * 8, h->stream));
-  if (h->hist_cells) HIP_TRY(h, hipMemsetAsync(h->d_hist, 0, h->hist_cells * 4, h->stream));
+  ResetParams r;
+  memset(&r, 0, sizeof(r));
+  r.sum64 = h->d_sum64;
+  r.n_sum64 = h->n_sum64;
+  r.min64 = h->d_min64;
+  r.n_min64 = h->n_min64;
+  r.max64 = h->d_max64;
+  r.n_max64 = h->n_max64;
+  const uint64_t hist_bytes = h->hist_cells * h->T * 4;
+  if (hist_bytes & 15) HIP_TRY(h, hipMemsetAsync(h->d_hist, 0, hist_bytes, h->stream));  // (16 B multiple always)
+  r.hist = reinterpret_cast<uint4*>(h->d_hist);
+  r.n_hist16 = hist_bytes / 16;
   if (h->d_sparse_keys) {
-    HIP_TRY(h, hipMemsetAsync(h->d_sparse_keys, 0xff, h->sparse_cap * 8, h->stream));
-    HIP_TRY(h, hipMemsetAsync(h->d_sparse_vals, 0, h->sparse_cap * 4, h->stream));
+    r.sparse_keys = h->d_sparse_keys;
+    r.sparse_vals = h->d_sparse_vals;
+    r.sparse_cap = h->sparse_cap;
   }
   // (a pending descriptor upload zeroes the per-buffer counts itself)
-  if (h->d_bufcnt && !h->descs_dirty && !h->descs.empty() && h->descs.size() <= h->descs_cap)
-    HIP_TRY(h, hipMemsetAsync(h->d_bufcnt, 0, h->descs.size() * 2 * 4, h->stream));
+  if (h->d_bufcnt && !h->descs_dirty && !h->descs.empty() && h->descs.size() <= h->descs_cap) {
+    r.bufcnt = h->d_bufcnt;
+    r.n_bufcnt = h->descs.size() * 2;
+  }
+  hipLaunchKernelGGL(reset_kernel, dim3(h->num_cus * 4), dim3(256), 0, h->stream, r);
+  HIP_TRY(h, hipGetLastError());
   return NMG_OK;
 }
 
@@ -733,11 +982,12 @@ extern "C" int nmg_set_objects(nmg_engine* h, const uint64_t* keys, const uint32
     d.hist = kHistSparse;
     d.sidx = ~0u;
     if (!want_hist) continue;
-    uint64_t cells = np * T;
-    if (cells <= max_cells_per_entry && h->hist_cells + cells <= budget_cells) {
+    // dense cells: histogram index = thread * hist_cells + hist_base(entry) + page
+    if (np * T <= max_cells_per_entry && (h->hist_cells + np) * T <= budget_cells &&
+        h->hist_cells + np < 0xffffffffull) {
       d.hist = h->hist_cells;
       h->hist_base[e] = h->hist_cells;
-      h->hist_cells += cells;
+      h->hist_cells += np;
     } else {
       if (h->sparse_entries.size() >= (1u << 22)) return fail(h, NMG_ERR_CAPACITY, "too many sparse entries");
       d.sidx = (uint32_t)h->sparse_entries.size();
@@ -771,7 +1021,9 @@ extern "C" int nmg_set_objects(nmg_engine* h, const uint64_t* keys, const uint32
   HIP_TRY(h, hipMalloc(&h->d_sum64, h->n_sum64 * 8));
   HIP_TRY(h, hipMalloc(&h->d_min64, h->n_min64 * 8));
   HIP_TRY(h, hipMalloc(&h->d_max64, h->n_max64 * 8));
-  if (h->hist_cells) HIP_TRY(h, hipMalloc(&h->d_hist, h->hist_cells * 4));
+  // pad the dense arena to a multiple of 4 cells per thread so it is zeroed in 16 B units
+  h->hist_cells = (h->hist_cells + 3) & ~uint64_t(3);
+  if (h->hist_cells) HIP_TRY(h, hipMalloc(&h->d_hist, h->hist_cells * h->T * 4));
   if (!h->sparse_entries.empty()) {
     HIP_TRY(h, hipMalloc(&h->d_sparse_keys, h->sparse_cap * 8));
     HIP_TRY(h, hipMalloc(&h->d_sparse_vals, h->sparse_cap * 4));
@@ -936,17 +1188,65 @@ static int upload_buffers(nmg_engine* h) {
   return NMG_OK;
 }
 
+// Work schedule: buffers sorted by stream (access type, thread rank) -- the
+// order in which they are analysed changes no result (all merges are sums,
+// mins and maxes; first-match ordinals carry the analysis position) -- and
+// cut into `grid` contiguous ranges of about equal bytes.
+static int build_schedule(nmg_engine* h, uint32_t grid) {
+  const uint32_t nb = (uint32_t)h->descs.size();
+  std::vector<uint32_t> order(nb);
+  for (uint32_t i = 0; i < nb; i++) order[i] = i;
+  std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) {
+    const BufDesc &x = h->descs[a], &y = h->descs[b];
+    if (x.access != y.access) return x.access < y.access;
+    return x.thread_rank < y.thread_rank;
+  });
+  std::vector<uint64_t> csum(nb + 1, 0);
+  for (uint32_t i = 0; i < nb; i++) csum[i + 1] = csum[i] + h->descs[order[i]].len + 64;
+  std::vector<uint32_t> ranges(grid + 1, 0);
+  for (uint32_t w = 1; w < grid; w++) {
+    const uint64_t target = csum[nb] * w / grid;
+    uint32_t c = (uint32_t)(std::lower_bound(csum.begin(), csum.end(), target) - csum.begin());
+    ranges[w] = std::max(ranges[w - 1], std::min(c, nb));
+  }
+  ranges[grid] = nb;
+  (void)hipFree(h->d_order);
+  (void)hipFree(h->d_ranges);
+  h->d_order = nullptr;
+  h->d_ranges = nullptr;
+  HIP_TRY(h, hipMalloc(&h->d_order, std::max<size_t>(nb, 1) * 4));
+  HIP_TRY(h, hipMalloc(&h->d_ranges, (grid + 1) * 4));
+  if (nb) HIP_TRY(h, hipMemcpy(h->d_order, order.data(), nb * 4, hipMemcpyHostToDevice));
+  HIP_TRY(h, hipMemcpy(h->d_ranges, ranges.data(), (grid + 1) * 4, hipMemcpyHostToDevice));
+  h->sched_grid = grid;
+  return NMG_OK;
+}
+
 extern "C" int nmg_analyze(nmg_engine* h) {
   if (!h) return NMG_ERR_INVALID;
   if (!h->have_table) return fail(h, NMG_ERR_STATE, "nmg_analyze before nmg_set_objects");
   HIP_TRY(h, hipSetDevice(h->device));
+  const bool resched = h->descs_dirty;
   int rc = upload_buffers(h);
   if (rc) return rc;
   const uint32_t nb = (uint32_t)h->descs.size();
+  if (h->blocks_per_cu <= 0) {
+    int bpc = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, attribute_kernel, kWG, 0) != hipSuccess || bpc <= 0) bpc = 1;
+    h->blocks_per_cu = bpc;
+  }
+  // persistent grid: one resident workgroup per slot, each with a byte-balanced range
+  const uint32_t grid = nb ? std::min<uint32_t>(nb, (uint32_t)(h->num_cus * h->blocks_per_cu)) : 0;
+  if (nb && (resched || grid != h->sched_grid)) {
+    rc = build_schedule(h, grid);
+    if (rc) return rc;
+  }
   Params p;
   memset(&p, 0, sizeof(p));
   p.data = h->d_data;
   p.bufs = h->d_descs;
+  p.order = h->d_order;
+  p.ranges = h->d_ranges;
   p.nb_bufs = nb;
   p.nb_keys = h->K;
   p.keys = h->d_keys;
@@ -959,6 +1259,7 @@ extern "C" int nmg_analyze(nmg_engine* h) {
   p.flags = h->flags;
   p.nb_entries = h->E;
   p.sparse_mask = (uint32_t)(h->sparse_cap - 1);
+  p.hist_cells = h->hist_cells;
   p.sum64 = h->d_sum64;
   p.min64 = h->d_min64;
   p.max64 = h->d_max64;
@@ -966,19 +1267,20 @@ extern "C" int nmg_analyze(nmg_engine* h) {
   p.bufcnt = h->d_bufcnt;
   p.sparse_keys = h->d_sparse_keys;
   p.sparse_vals = h->d_sparse_vals;
+  const int slot = (int)(h->nlaunch % nmg_engine::kRing);
+  if (!h->ring0[slot]) {
+    HIP_TRY(h, hipEventCreate(&h->ring0[slot]));
+    HIP_TRY(h, hipEventCreate(&h->ring1[slot]));
+  }
   HIP_TRY(h, hipEventRecord(h->ev0, h->stream));
+  HIP_TRY(h, hipEventRecord(h->ring0[slot], h->stream));
   if (nb) {
-    if (h->blocks_per_cu <= 0) {
-      int bpc = 0;
-      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, attribute_kernel, kWG, 0) != hipSuccess || bpc <= 0) bpc = 1;
-      h->blocks_per_cu = bpc;
-    }
-    // persistent grid: every resident workgroup walks buffers round-robin
-    uint32_t grid = std::min<uint32_t>(nb, (uint32_t)(h->num_cus * h->blocks_per_cu));
     hipLaunchKernelGGL(attribute_kernel, dim3(grid), dim3(kWG), 0, h->stream, p);
     HIP_TRY(h, hipGetLastError());
   }
+  HIP_TRY(h, hipEventRecord(h->ring1[slot], h->stream));
   HIP_TRY(h, hipEventRecord(h->ev1, h->stream));
+  h->nlaunch++;
   h->launched = true;
   return NMG_OK;
 }
@@ -1008,6 +1310,19 @@ extern "C" int nmg_synchronize(nmg_engine* h) {
   uint64_t w = ~0ull;
   HIP_TRY(h, hipMemcpy(&w, h->d_min64 + 36 + h->E, 8, hipMemcpyDeviceToHost));
   return decode_error_word(h, w);
+}
+
+extern "C" int nmg_get_launch_times(nmg_engine* h, float* ms, int n) {
+  if (!h || (n > 0 && !ms)) return NMG_ERR_INVALID;
+  HIP_TRY(h, hipSetDevice(h->device));
+  HIP_TRY(h, hipStreamSynchronize(h->stream));
+  const int avail = (int)std::min<uint64_t>(h->nlaunch, nmg_engine::kRing);
+  const int cnt = std::min(n, avail);
+  for (int i = 0; i < cnt; i++) {  // the cnt most recent launches, oldest first
+    const int slot = (int)((h->nlaunch - cnt + i) % nmg_engine::kRing);
+    HIP_TRY(h, hipEventElapsedTime(&ms[i], h->ring0[slot], h->ring1[slot]));
+  }
+  return cnt;
 }
 
 extern "C" int nmg_last_analyze_ms(nmg_engine* h, float* ms) {
@@ -1044,7 +1359,10 @@ int engine_download(nmg_engine* h, HostResults& r) {
   }
   const uint64_t E = h->E;
   r.first.assign(mn.begin() + 36, mn.begin() + 36 + E);
-  r.count_weight.assign(sum.begin() + 2 * kGlobalSums, sum.begin() + 2 * kGlobalSums + 4 * E);
+  r.count_weight.resize(4 * E);  // SoA [2][2][E] -> [E][2][2]
+  for (uint64_t e = 0; e < E; e++)
+    for (uint32_t a = 0; a < 2; a++)
+      for (uint32_t w = 0; w < 2; w++) r.count_weight[e * 4 + a * 2 + w] = sum[objcw_index(e, a, w, E)];
   if (h->flags & NMG_F_OBJECT_LEVELS)
     r.levels.assign(sum.begin() + 2 * kGlobalSums + 4 * E, sum.end());
   else
@@ -1074,8 +1392,8 @@ int engine_download(nmg_engine* h, HostResults& r) {
 int engine_download_hist(nmg_engine* h, std::vector<uint32_t>& cells) {
   int rc = nmg_synchronize(h);
   if (rc) return rc;
-  cells.resize(h->hist_cells);
-  if (h->hist_cells) HIP_TRY(h, hipMemcpy(cells.data(), h->d_hist, h->hist_cells * 4, hipMemcpyDeviceToHost));
+  cells.resize(h->hist_cells * h->T);
+  if (h->hist_cells) HIP_TRY(h, hipMemcpy(cells.data(), h->d_hist, cells.size() * 4, hipMemcpyDeviceToHost));
   return NMG_OK;
 }
 }  // namespace nmg
@@ -1112,8 +1430,14 @@ extern "C" int nmg_get_object_counters(nmg_engine* h, uint64_t* first_ordinal, u
   if (rc) return rc;
   if (first_ordinal && h->E)
     HIP_TRY(h, hipMemcpy(first_ordinal, h->d_min64 + 36, (size_t)h->E * 8, hipMemcpyDeviceToHost));
-  if (count_weight && h->E)
-    HIP_TRY(h, hipMemcpy(count_weight, h->d_sum64 + 2 * kGlobalSums, (size_t)h->E * 32, hipMemcpyDeviceToHost));
+  if (count_weight && h->E) {
+    std::vector<uint64_t> soa((size_t)h->E * 4);
+    HIP_TRY(h, hipMemcpy(soa.data(), h->d_sum64 + 2 * kGlobalSums, soa.size() * 8, hipMemcpyDeviceToHost));
+    for (uint64_t e = 0; e < h->E; e++)
+      for (uint32_t a = 0; a < 2; a++)
+        for (uint32_t w = 0; w < 2; w++)
+          count_weight[e * 4 + a * 2 + w] = soa[objcw_index(e, a, w, h->E) - 2 * kGlobalSums];
+  }
   return NMG_OK;
 }
 
@@ -1153,10 +1477,9 @@ static int collect_page_cells(nmg_engine* h, std::vector<uint32_t>* rows, int64_
   const uint64_t T = h->T;
   for (uint32_t e = 0; e < h->E; e++) {
     if (h->hist_base[e] != kHistSparse) {
-      const uint32_t* c = cells.data() + h->hist_base[e];
       for (uint32_t th = 0; th < T; th++)
         for (uint64_t pg = 0; pg < h->npages[e]; pg++) {
-          uint32_t v = c[pg * T + th];
+          uint32_t v = cells[th * h->hist_cells + h->hist_base[e] + pg];
           if (!v) continue;
           if (rows) {
             rows->push_back(e);
@@ -1208,7 +1531,7 @@ extern "C" uint64_t nmg_array_size(nmg_engine* h, int which) {
     case NMG_ARR_SUM64: return h->n_sum64;
     case NMG_ARR_MIN64: return h->n_min64;
     case NMG_ARR_MAX64: return h->n_max64;
-    case NMG_ARR_HIST32: return h->hist_cells;
+    case NMG_ARR_HIST32: return h->hist_cells * h->T;
     default: return 0;
   }
 }
@@ -1218,7 +1541,7 @@ static void* array_ptr(nmg_engine* h, int which, size_t* bytes) {
     case NMG_ARR_SUM64: *bytes = h->n_sum64 * 8; return h->d_sum64;
     case NMG_ARR_MIN64: *bytes = h->n_min64 * 8; return h->d_min64;
     case NMG_ARR_MAX64: *bytes = h->n_max64 * 8; return h->d_max64;
-    case NMG_ARR_HIST32: *bytes = h->hist_cells * 4; return h->d_hist;
+    case NMG_ARR_HIST32: *bytes = h->hist_cells * h->T * 4; return h->d_hist;
     default: *bytes = 0; return nullptr;
   }
 }

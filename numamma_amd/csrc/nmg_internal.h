@@ -12,7 +12,8 @@ namespace nmg {
 // Layout of the flat merge arrays (see nmg_export_array):
 //   sum64: [2 access][39] global sums   (total_count, total_weight, na_miss_count,
 //                                         18 x (count, sum_weight))
-//          [E][2 access][2]              per-entry (count, weight)
+//          [2 access][2][E]              per-entry count, weight (SoA: a flush in
+//                                         entry order coalesces its atomics)
 //          [E][2 access][37]             per-entry levels (na, 18 x (count, sum)), optional
 //   min64: [2][18] global bucket min_weight, [E] first-match ordinal, [1] error word
 //   max64: [2][18] global bucket max_weight
@@ -22,8 +23,8 @@ constexpr uint64_t kHistSparse = ~0ull;
 constexpr uint32_t kPageSize = 4096;  // src/mem_analyzer.c:471
 
 constexpr uint64_t gsum_index(uint32_t access, uint32_t i) { return access * kGlobalSums + i; }
-constexpr uint64_t objcw_index(uint64_t e, uint32_t access, uint32_t w) {
-  return 2 * kGlobalSums + e * 4 + access * 2 + w;
+constexpr uint64_t objcw_index(uint64_t e, uint32_t access, uint32_t w, uint64_t nb_entries) {
+  return 2 * kGlobalSums + (uint64_t(access) * 2 + w) * nb_entries + e;
 }
 
 // Error word: min over ((seq << 40) | (byte offset << 8) | code) so the first

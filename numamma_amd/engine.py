@@ -109,6 +109,11 @@ class Engine:
     def reset(self):
         self._c(lib.nmg_reset_counters(self.h))
 
+    def launch_times(self, n: int = 64):
+        buf = (C.c_float * n)()
+        cnt = self._c(lib.nmg_get_launch_times(self.h, buf, n))
+        return [buf[i] for i in range(cnt)]
+
     def last_analyze_ms(self) -> float:
         ms = C.c_float()
         self._c(lib.nmg_last_analyze_ms(self.h, C.byref(ms)))

@@ -1,0 +1,74 @@
+#!/usr/bin/env python3
+"""Kernel ablation on the GPU: time nmg::attribute_kernel with parts of its
+work switched off, interleaved in one process (cdna_hip_programming.md
+§5.4 rule 24).  Prints one JSON line per (workload, variant)."""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+VARIANTS = {
+    "load_only": 0x100,
+    "decode_global": 0x0,               # decode + global mem_counters, no matching
+    "lookup_only": 0x1 | 0x200 | 0x800,  # decode + lookup, nothing accumulated
+    "match_no_global": 0x1 | 0x200,     # lookup + object counters only
+    "match": 0x1,                       # + object counters
+    "full_noflush": 0x3 | 0x400,        # LDS tables filled, never flushed to global
+    "full": 0x3,                        # + page histogram (default product path)
+}
+
+WORKLOADS = {
+    "c2": dict(nb_samples=10_000_000, nb_intervals=1_000),
+    "k100k": dict(nb_samples=10_000_000, nb_intervals=100_000),
+    "k1m": dict(nb_samples=10_000_000, nb_intervals=1_000_000, size_max=64 * 1024),
+}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--workloads", default="c2,k100k,k1m")
+    ap.add_argument("--reps", type=int, default=10)
+    args = ap.parse_args()
+    import torch
+
+    from numamma_amd.engine import Engine
+    from numamma_amd.replay import SynthConfig, generate
+
+    for wname in args.workloads.split(","):
+        t0 = time.time()
+        rp = generate(SynthConfig(seed=1, **WORKLOADS[wname]))
+        arena, offs, lens, ranks, acc = rp.packed()
+        d = torch.from_numpy(arena).cuda()
+        nbytes = int(lens.sum())
+        engines = {}
+        for v, f in VARIANTS.items():
+            e = Engine(flags=f, nb_threads=rp.nb_threads)
+            e.set_objects(rp.table)
+            e.set_device_buffers(d.data_ptr(), offs, lens, ranks, acc)
+            engines[v] = e
+        print(f"# {wname}: generated in {time.time() - t0:.1f}s", file=sys.stderr, flush=True)
+        times = {v: [] for v in VARIANTS}
+        for r in range(args.reps + 2):
+            for v, e in engines.items():
+                e.reset()
+                e.analyze()
+                e.synchronize()
+                if r >= 2:
+                    times[v].append(e.last_analyze_ms())
+        for v, ts in times.items():
+            med = float(np.median(ts))
+            print(json.dumps({"workload": wname, "variant": v, "median_ms": med, "min_ms": float(np.min(ts)),
+                              "GBps": nbytes / med / 1e6, "Gsamples_s": nbytes / 40 / med / 1e6}), flush=True)
+        for e in engines.values():
+            e.close()
+        del d
+
+
+if __name__ == "__main__":
+    main()

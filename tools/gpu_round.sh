@@ -42,6 +42,25 @@ for s in $STAGES; do
         -- python3 $ROOT/bench.py --steps 10 --warmup 2 --no-cpu-baseline > $OUT/prof_$TAG.log 2>&1 \
         || { echo "rocprof failed"; tail -40 $OUT/prof_$TAG.log; exit 1; }
       find $OUT/prof_$TAG -name "*kernel_stats.csv" -exec cat {} \; | head -20 ;;
+    ablate)
+      echo "== ablation"
+      timeout -k 10 900 python tools/ablate.py > $OUT/ablate_$TAG.json 2> $OUT/ablate_$TAG.err \
+        || { echo "ablate failed"; tail -40 $OUT/ablate_$TAG.err; exit 1; }
+      cat $OUT/ablate_$TAG.json ;;
+    pmcsq)
+      echo "== rocprofv3 -L + SQ counter passes"
+      timeout -k 10 120 rocprofv3 -L > $OUT/counters_list.txt 2>&1 || true
+      i=0
+      for set in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT" \
+                 "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VALU SQ_INSTS_SMEM SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE" \
+                 "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum TCC_EA0_ATOMIC_sum"; do
+        i=$((i+1))
+        rm -rf $OUT/pmc_${TAG}_$i
+        timeout -k 10 400 rocprofv3 --pmc $set --kernel-trace -d $ROOT/$OUT/pmc_${TAG}_$i -o run --output-format csv \
+          -- python3 $ROOT/bench.py --steps 3 --warmup 1 --no-cpu-baseline > $OUT/pmc_${TAG}_$i.log 2>&1 \
+          || { echo "pmc pass $i failed"; tail -20 $OUT/pmc_${TAG}_$i.log; exit 1; }
+      done
+      echo "pmc passes done" ;;
     pmc)
       echo "== rocprofv3 pmc FETCH_SIZE"
       rm -rf $OUT/pmc_$TAG
