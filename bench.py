@@ -60,13 +60,21 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # test hooks for the multi-rank path on a one-GPU box (never used by the driver):
+    # NMG_BENCH_BACKEND=gloo, NMG_BENCH_SAME_GPU=1 (every rank on GPU 0)
+    backend = os.environ.get("NMG_BENCH_BACKEND", "nccl")
+    if os.environ.get("NMG_BENCH_SAME_GPU") == "1":
+        local = 0
     if world != args.gpus:
         log(f"warning: WORLD_SIZE={world} but --gpus={args.gpus}; using WORLD_SIZE")
     distributed = world > 1
     if distributed:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     device = torch.device("cuda", local)
 
     from numamma_amd import _lib

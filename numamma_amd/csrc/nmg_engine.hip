@@ -70,6 +70,9 @@ struct BufDesc {
 };
 static_assert(sizeof(BufDesc) == 32, "BufDesc");
 
+// One table entry (64 B).  The node array holds, for node k, a copy of its
+// newest entry with `first` = its entry id and `count` = the node's number of
+// entries, so the common one-entry node costs a single dependent load.
 struct DevEntry {
   uint64_t addr;   // buffer_addr
   uint64_t end;    // buffer_addr + buffer_size (mod 2^64, as the reference's void* sum)
@@ -77,8 +80,10 @@ struct DevEntry {
   uint64_t free;   // free_date
   uint64_t hist;   // dense histogram base cell, or kHistSparse
   uint32_t sidx;   // sparse index (valid when hist == kHistSparse && sidx != ~0u)
+  uint32_t first;  // (node records) entry id of the node's newest entry
+  uint32_t count;  // (node records) entries of the node
   uint32_t pad0;
-  uint64_t pad1[2];
+  uint64_t pad1;
 };
 static_assert(sizeof(DevEntry) == 64, "DevEntry");
 
@@ -89,12 +94,13 @@ struct Params {
   const uint32_t* ranges;  // [gridDim.x + 1]: workgroup w takes order[ranges[w] .. ranges[w+1])
   uint32_t nb_bufs;
   uint32_t nb_keys;
-  const uint64_t* keys;
-  const uint32_t* entry_off;
+  const uint64_t* keys;      // padded with ~0 to nb_fences * fence_step
+  const DevEntry* nodes;     // [nb_keys] node records
   const DevEntry* entries;
-  const uint64_t* fences;
+  const uint64_t* fences;    // padded with ~0 to fence_p2
   uint32_t nb_fences;
-  uint32_t fence_step;
+  uint32_t fence_p2;         // power of two >= nb_fences
+  uint32_t fence_step;       // power of two
   uint32_t nb_threads;
   uint32_t flags;
   uint32_t nb_entries;
@@ -168,45 +174,47 @@ __device__ __forceinline__ void set_error(Params& p, uint64_t seq, uint32_t off,
 
 // Largest key <= addr (ht_lower_key, tools/hash.c:63-77): fence table in LDS,
 // then binary search of the fence's key bucket in global memory.
-__device__ __forceinline__ int64_t lower_key(const Params& p, const uint64_t* s_fences,
-                                             uint64_t addr) {
-  if (p.nb_fences == 0 || addr < s_fences[0]) return -1;
-  uint32_t lo = 0, hi = p.nb_fences - 1;
-  while (lo < hi) {
-    uint32_t mid = (lo + hi + 1) >> 1;
-    if (s_fences[mid] <= addr) lo = mid;
-    else hi = mid - 1;
-  }
-  if (p.fence_step == 1) return lo;
-  uint32_t klo = lo * p.fence_step;
-  uint32_t khi = min(klo + p.fence_step, p.nb_keys) - 1;
-  while (klo < khi) {
-    uint32_t mid = (klo + khi + 1) >> 1;
-    if (p.keys[mid] <= addr) klo = mid;
-    else khi = mid - 1;
-  }
-  return klo;
+// Largest key <= addr (ht_lower_key, tools/hash.c:63-77).  Both levels are
+// branch-free, fixed-trip-count binary searches (every lane runs the same
+// steps, no divergence): the LDS fence table, then the fence's key bucket in
+// global memory (L2/MALL resident).  Returns nb_keys when no key <= addr.
+__device__ __forceinline__ uint32_t lower_key(const Params& p, const uint64_t* s_fences, uint64_t addr) {
+  uint32_t idx = 0;
+  for (uint32_t st = p.fence_p2 >> 1; st; st >>= 1) idx = (s_fences[idx + st] <= addr) ? idx + st : idx;
+  idx = min(idx, p.nb_fences - 1);  // ~0 padding: addr == UINT64_MAX
+  uint32_t k = idx * p.fence_step;
+  for (uint32_t st = p.fence_step >> 1; st; st >>= 1) k = (p.keys[k + st] <= addr) ? k + st : k;
+  k = min(k, p.nb_keys - 1);
+  return (p.nb_keys == 0 || addr < s_fences[0]) ? p.nb_keys : k;
 }
 
 // __ma_find_mem_info_from_sample_generic (mem_analyzer.c:249-286) with
 // is_sample_in_buffer (:141-155): only the lower-bound node, newest entry first.
+__device__ __forceinline__ bool entry_match(uint4 a, uint4 b, uint64_t addr, uint64_t ts) {
+  const uint64_t baddr = (uint64_t(a.y) << 32) | a.x, bend = (uint64_t(a.w) << 32) | a.z;
+  const uint64_t alloc = (uint64_t(b.y) << 32) | b.x, fr = (uint64_t(b.w) << 32) | b.z;
+  return baddr <= addr && addr < bend && alloc <= ts && ts <= fr;
+}
+
 __device__ __forceinline__ int64_t find_entry(const Params& p, const uint64_t* s_fences,
                                               uint64_t addr, uint64_t ts, DevEntry* out) {
-  int64_t k = lower_key(p, s_fences, addr);
-  if (k < 0) return -1;
-  uint32_t e0 = p.entry_off[k], e1 = p.entry_off[k + 1];
-  for (uint32_t e = e0; e < e1; e++) {
-    const uint4* q = reinterpret_cast<const uint4*>(p.entries + e);
-    uint4 a = q[0], b = q[1];
-    uint64_t baddr = (uint64_t(a.y) << 32) | a.x;
-    uint64_t bend = (uint64_t(a.w) << 32) | a.z;
-    uint64_t alloc = (uint64_t(b.y) << 32) | b.x;
-    uint64_t fr = (uint64_t(b.w) << 32) | b.z;
-    if (baddr <= addr && addr < bend && alloc <= ts && ts <= fr) {
-      uint4 c = q[2];
-      out->addr = baddr;
-      out->hist = (uint64_t(c.y) << 32) | c.x;
-      out->sidx = c.z;
+  const uint32_t k = lower_key(p, s_fences, addr);
+  if (k >= p.nb_keys) return -1;
+  const uint4* q = reinterpret_cast<const uint4*>(p.nodes + k);
+  const uint4 a = q[0], b = q[1], c = q[2];
+  out->addr = (uint64_t(a.y) << 32) | a.x;
+  out->hist = (uint64_t(c.y) << 32) | c.x;
+  out->sidx = c.z;
+  if (entry_match(a, b, addr, ts)) return c.w;
+  const uint4 d = q[3];
+  for (uint32_t e = c.w + 1; e < c.w + d.x; e++) {  // older entries of a reused address
+    const uint4* r = reinterpret_cast<const uint4*>(p.entries + e);
+    const uint4 ra = r[0], rb = r[1];
+    if (entry_match(ra, rb, addr, ts)) {
+      const uint4 rc = r[2];
+      out->addr = (uint64_t(ra.y) << 32) | ra.x;
+      out->hist = (uint64_t(rc.y) << 32) | rc.x;
+      out->sidx = rc.z;
       return e;
     }
   }
@@ -249,7 +257,9 @@ struct WgCounters {
 // the flush walks entries / cells in (mostly) ascending address order and its
 // global atomics coalesce into shared 64-byte lines.  A slot already holding
 // the key (hot objects) is found with a plain broadcast read, no CAS.
-__device__ __forceinline__ int obj_slot(WgCounters& wc, uint32_t e) {
+// Probe chains (first-touch insertion / collisions); the common case -- the
+// key already sits in its home slot -- is handled inline by the callers.
+__device__ __forceinline__ int obj_slot_probe(WgCounters& wc, uint32_t e) {
   uint32_t s = e & (kObjSlots - 1);
   for (uint32_t i = 0; i < kProbes; i++) {
     unsigned k = wc.okey[s];
@@ -267,7 +277,7 @@ __device__ __forceinline__ int obj_slot(WgCounters& wc, uint32_t e) {
   return -1;
 }
 
-__device__ __forceinline__ int page_slot(WgCounters& wc, uint32_t cell) {
+__device__ __forceinline__ int page_slot_probe(WgCounters& wc, uint32_t cell) {
   uint32_t s = cell & (kPageSlots - 1);
   for (uint32_t i = 0; i < kProbes; i++) {
     unsigned k = wc.pkey[s];
@@ -283,6 +293,16 @@ __device__ __forceinline__ int page_slot(WgCounters& wc, uint32_t cell) {
     s = (s + 1) & (kPageSlots - 1);
   }
   return -1;
+}
+
+__device__ __forceinline__ int obj_slot(WgCounters& wc, uint32_t e) {
+  const uint32_t s = e & (kObjSlots - 1);
+  return wc.okey[s] == e ? (int)s : obj_slot_probe(wc, e);
+}
+
+__device__ __forceinline__ int page_slot(WgCounters& wc, uint32_t cell) {
+  const uint32_t s = cell & (kPageSlots - 1);
+  return wc.pkey[s] == cell ? (int)s : page_slot_probe(wc, cell);
 }
 
 // Per-lane privatised mem_counters of the current stream: packed u16 counts
@@ -379,10 +399,15 @@ __device__ __forceinline__ void process_sample(Params& p, WgCounters& wc, LaneAc
       }
     }
     // min / max only move monotonically: read first, atomic only on improvement
-    for (uint32_t m = bm; m; m &= m - 1) {
-      const uint32_t b = (uint32_t)__builtin_ctz(m);
+    if (bm) {
+      const uint32_t b = (uint32_t)__builtin_ctz(bm);
       if (w < wc.mins[b]) atomicMin(&wc.mins[b], (unsigned long long)w);
       if (w > wc.maxs[b]) atomicMax(&wc.maxs[b], (unsigned long long)w);
+      for (uint32_t m = bm & (bm - 1); m; m &= m - 1) {  // several level groups (rare)
+        const uint32_t b2 = (uint32_t)__builtin_ctz(m);
+        if (w < wc.mins[b2]) atomicMin(&wc.mins[b2], (unsigned long long)w);
+        if (w > wc.maxs[b2]) atomicMax(&wc.maxs[b2], (unsigned long long)w);
+      }
     }
   }
 match:
@@ -501,7 +526,7 @@ __global__ __launch_bounds__(kWG, 4) void attribute_kernel(Params p) {
   __shared__ uint32_t s_flag, s_nlist, s_next, s_err;
 
   const int tid = threadIdx.x;
-  for (uint32_t i = tid; i < p.nb_fences; i += kWG) s_fences[i] = p.fences[i];
+  for (uint32_t i = tid; i < p.fence_p2; i += kWG) s_fences[i] = p.fences[i];
 
   // This workgroup's contiguous, byte-balanced share of the stream-sorted
   // buffer list.  Consecutive buffers of one stream (thread, access) share
@@ -733,10 +758,10 @@ struct nmg_engine {
   bool have_table = false;
   uint32_t K = 0, E = 0;
   uint64_t* d_keys = nullptr;
-  uint32_t* d_entry_off = nullptr;
+  DevEntry* d_nodes = nullptr;
   DevEntry* d_entries = nullptr;
   uint64_t* d_fences = nullptr;
-  uint32_t nb_fences = 0, fence_step = 1;
+  uint32_t nb_fences = 0, fence_step = 1, fence_p2 = 1;
   std::vector<uint64_t> hist_base, npages, buffer_size;
   std::vector<uint32_t> sparse_entries;
   uint64_t hist_cells = 0;
@@ -840,11 +865,11 @@ static void free_counters(nmg_engine* h) {
 
 static void free_table(nmg_engine* h) {
   (void)hipFree(h->d_keys);
-  (void)hipFree(h->d_entry_off);
+  (void)hipFree(h->d_nodes);
   (void)hipFree(h->d_entries);
   (void)hipFree(h->d_fences);
   h->d_keys = nullptr;
-  h->d_entry_off = nullptr;
+  h->d_nodes = nullptr;
   h->d_entries = nullptr;
   h->d_fences = nullptr;
 }
@@ -994,12 +1019,24 @@ extern "C" int nmg_set_objects(nmg_engine* h, const uint64_t* keys, const uint32
       h->sparse_entries.push_back(e);
     }
   }
-  // LDS fence table: every fence_step-th key
+  // LDS fence table: every fence_step-th key (fence_step a power of two), padded
+  // with ~0 to a power of two; the key array is padded to nb_fences * fence_step
   h->fence_step = 1;
-  while ((uint64_t)nb_keys > (uint64_t)h->fence_step * kMaxFences) h->fence_step++;
-  h->nb_fences = nb_keys ? (nb_keys + h->fence_step - 1) / h->fence_step : 0;
-  std::vector<uint64_t> fences(h->nb_fences);
-  for (uint32_t f = 0; f < h->nb_fences; f++) fences[f] = keys[(uint64_t)f * h->fence_step];
+  while ((uint64_t)nb_keys > (uint64_t)h->fence_step * kMaxFences) h->fence_step <<= 1;
+  h->nb_fences = nb_keys ? (nb_keys + h->fence_step - 1) / h->fence_step : 1;
+  h->fence_p2 = 1;
+  while (h->fence_p2 < h->nb_fences) h->fence_p2 <<= 1;
+  std::vector<uint64_t> fences(h->fence_p2, ~0ull);
+  for (uint32_t f = 0; f < h->nb_fences && (uint64_t)f * h->fence_step < nb_keys; f++)
+    fences[f] = keys[(uint64_t)f * h->fence_step];
+  std::vector<uint64_t> padded_keys((uint64_t)h->nb_fences * h->fence_step, ~0ull);
+  if (nb_keys) memcpy(padded_keys.data(), keys, (size_t)nb_keys * 8);
+  std::vector<DevEntry> nodes(nb_keys);
+  for (uint32_t k = 0; k < nb_keys; k++) {
+    nodes[k] = dev[entry_off[k]];
+    nodes[k].first = entry_off[k];
+    nodes[k].count = entry_off[k + 1] - entry_off[k];
+  }
 
   auto alloc_copy = [&](void** dptr, const void* src, size_t bytes) -> hipError_t {
     hipError_t e = hipMalloc(dptr, bytes ? bytes : 16);
@@ -1007,10 +1044,8 @@ extern "C" int nmg_set_objects(nmg_engine* h, const uint64_t* keys, const uint32
     if (bytes) return hipMemcpyAsync(*dptr, src, bytes, hipMemcpyHostToDevice, h->stream);
     return hipSuccess;
   };
-  HIP_TRY(h, alloc_copy((void**)&h->d_keys, keys, (size_t)nb_keys * 8));
-  std::vector<uint32_t> off0;
-  if (!entry_off) off0.assign(1, 0);
-  HIP_TRY(h, alloc_copy((void**)&h->d_entry_off, entry_off ? entry_off : off0.data(), ((size_t)nb_keys + 1) * 4));
+  HIP_TRY(h, alloc_copy((void**)&h->d_keys, padded_keys.data(), padded_keys.size() * 8));
+  HIP_TRY(h, alloc_copy((void**)&h->d_nodes, nodes.data(), (size_t)nb_keys * sizeof(DevEntry)));
   HIP_TRY(h, alloc_copy((void**)&h->d_entries, dev.data(), (size_t)nb_entries * sizeof(DevEntry)));
   HIP_TRY(h, alloc_copy((void**)&h->d_fences, fences.data(), fences.size() * 8));
 
@@ -1250,10 +1285,11 @@ extern "C" int nmg_analyze(nmg_engine* h) {
   p.nb_bufs = nb;
   p.nb_keys = h->K;
   p.keys = h->d_keys;
-  p.entry_off = h->d_entry_off;
+  p.nodes = h->d_nodes;
   p.entries = h->d_entries;
   p.fences = h->d_fences;
   p.nb_fences = h->nb_fences;
+  p.fence_p2 = h->fence_p2;
   p.fence_step = h->fence_step;
   p.nb_threads = h->T;
   p.flags = h->flags;

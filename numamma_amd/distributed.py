@@ -44,6 +44,22 @@ def shard_ranges(lengths: Sequence[int], world: int) -> List[Tuple[int, int]]:
     return [(cuts[r], cuts[r + 1]) for r in range(world)]
 
 
+def _collective(t, rop, dst, group):
+    """reduce / all_reduce; a device tensor goes through host memory when the
+    backend is not RCCL (gloo test runs)."""
+    import torch.distributed as dist
+
+    staged = t.is_cuda and dist.get_backend(group) != "nccl"
+    x = t.cpu() if staged else t
+    if dst is None:
+        dist.all_reduce(x, op=rop, group=group)
+    else:
+        dist.reduce(x, dst=dst, op=rop, group=group)
+    if staged:
+        t.copy_(x)
+    return t
+
+
 def reduce_u64(t, op: str, dst: Optional[int] = 0, group=None):
     """Reduce a tensor of u64 bit patterns stored as int64.  dst=None -> all-reduce."""
     import torch
@@ -54,10 +70,7 @@ def reduce_u64(t, op: str, dst: Optional[int] = 0, group=None):
     if flip:
         t.bitwise_xor_(INT64_MIN)
     rop = {"sum": dist.ReduceOp.SUM, "min": dist.ReduceOp.MIN, "max": dist.ReduceOp.MAX}[op]
-    if dst is None:
-        dist.all_reduce(t, op=rop, group=group)
-    else:
-        dist.reduce(t, dst=dst, op=rop, group=group)
+    _collective(t, rop, dst, group)
     if flip:
         t.bitwise_xor_(INT64_MIN)
     return t
@@ -68,11 +81,7 @@ def reduce_u32_sum(t, dst: Optional[int] = 0, group=None):
     import torch.distributed as dist
 
     assert t.dtype == torch.int32
-    if dst is None:
-        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
-    else:
-        dist.reduce(t, dst=dst, op=dist.ReduceOp.SUM, group=group)
-    return t
+    return _collective(t, dist.ReduceOp.SUM, dst, group)
 
 
 def gather_arrays(a: np.ndarray, dst: int = 0, group=None):

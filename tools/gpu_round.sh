@@ -47,6 +47,17 @@ for s in $STAGES; do
       timeout -k 10 900 python tools/ablate.py > $OUT/ablate_$TAG.json 2> $OUT/ablate_$TAG.err \
         || { echo "ablate failed"; tail -40 $OUT/ablate_$TAG.err; exit 1; }
       cat $OUT/ablate_$TAG.json ;;
+    e2e)
+      echo "== end-to-end (host buffers, PCIe)"
+      timeout -k 10 600 python tools/e2e.py c2 > $OUT/e2e_$TAG.json 2> $OUT/e2e_$TAG.err \
+        || { echo "e2e failed"; tail -30 $OUT/e2e_$TAG.err; exit 1; }
+      cat $OUT/e2e_$TAG.json ;;
+    bench2g)
+      echo "== bench, 2 ranks sharing GPU 0 over gloo (multi-rank code path)"
+      timeout -k 10 600 env NMG_BENCH_BACKEND=gloo NMG_BENCH_SAME_GPU=1 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+        --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 5 --warmup 1 > $OUT/bench2g_$TAG.json 2> $OUT/bench2g_$TAG.err \
+        || { echo "bench2g failed"; tail -40 $OUT/bench2g_$TAG.err; exit 1; }
+      cat $OUT/bench2g_$TAG.json ;;
     pmcsq)
       echo "== rocprofv3 -L + SQ counter passes"
       timeout -k 10 120 rocprofv3 -L > $OUT/counters_list.txt 2>&1 || true
