@@ -6,21 +6,23 @@
 // ma_get_block :494-534).
 //
 // Kernel shape (DESIGN.md "Kernels"):
-//   * one workgroup owns one captured buffer at a time (persistent grid,
-//     round-robin over buffers) and walks it in 20 KiB LDS windows, so the
-//     record chain is followed exactly as the reference's byte cursor does
-//     (variable-size non-SAMPLE records, size==0 abort, truncation), while
-//     every HBM byte is read once with coalesced 16 B loads;
-//   * fast path: when every 40 B stride slot of a window is a 40 B record the
-//     whole window is decoded in parallel; otherwise lane 0 walks the headers
-//     in LDS and the window's SAMPLE offsets are processed in parallel;
-//   * global counters (mem_counters[2]) are privatised in LDS per buffer
-//     (wave-reduced sums, monotone min/max) and flushed once per buffer;
-//   * object lookup = LDS fence table -> binary search of the sorted key
-//     array in global (L2/MALL resident) -> LIFO entry scan with the
-//     inclusive timestamp window (quirks Q1-Q4);
-//   * per-object / per-page counters are u64/u32 atomics: integer adds,
-//     mins and maxes are order independent, so results are bit-exact.
+//   * persistent grid, one 1024-thread workgroup per CU, each owning a
+//     byte-balanced range of the buffer list sorted by stream (access type,
+//     thread rank); a buffer is walked in windows of 1024 stride slots of
+//     40 B, one per lane, loaded straight into registers, the next window
+//     issued before the current one is processed;
+//   * fast path when every slot of a window holds a whole 40 B record (the
+//     record chain is then known without reading it sequentially); otherwise
+//     wave 0 follows the header chain exactly as the reference's byte cursor
+//     does (variable-size non-SAMPLE records, size==0 abort, truncation);
+//   * global counters (mem_counters[2]) in per-lane registers / LDS, flushed
+//     once per stream run;
+//   * object lookup = branch-free search of the LDS fence table -> node record
+//     (in LDS for <= 1024 keys, else global after a key-bucket search) ->
+//     older entries of the node (quirks Q1-Q4);
+//   * per-object and per-page counters aggregated in direct-mapped LDS tables,
+//     flushed with coalesced global atomics; integer adds, mins and maxes are
+//     order independent, so results are bit-exact.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -34,16 +36,20 @@
 
 namespace nmg {
 
-constexpr int kWG = 512;
-constexpr int kSegBytes = 20480;               // 512 x 40 B records per LDS window
-constexpr int kLdsBytes = kSegBytes + 64;      // + overlap: a record starting in the window has its 40 B
-constexpr int kMaxFences = 1024;               // LDS fence table (8 KiB)
-constexpr int kMaxList = kSegBytes / 8;        // slow path: record offsets of one window
+constexpr int kWG = 1024;                      // one workgroup per CU
 constexpr uint32_t kSampleType = 9;            // PERF_RECORD_SAMPLE
 constexpr uint32_t kRecBytes = 40;             // perf_event_header (8) + struct mem_sample (32)
-// per-buffer LDS aggregation tables (flushed to global once per buffer)
-constexpr uint32_t kObjSlots = 1024;           // entry -> (count, weight, first ordinal)
-constexpr uint32_t kPageSlots = 2048;          // dense page cell -> count
+constexpr uint32_t kWinBytes = kWG * kRecBytes;  // one 40 B stride slot per lane per window
+constexpr int kMaxFences = 1024;               // LDS fence table (8 KiB)
+constexpr uint32_t kLdsNodes = 1024;           // node records held in LDS when nb_keys <= this
+constexpr uint32_t kMaxList = kWG;             // slow path: SAMPLE offsets listed per step
+// per-stream LDS aggregation tables (flushed to global on a stream change or
+// when half full)
+constexpr uint32_t kObjSlots = 2048;           // entry -> (count, weight, first ordinal)
+constexpr uint32_t kPageBuckets = 896;         // dense page cell -> count: 8-slot buckets
+constexpr uint32_t kPageSlots = kPageBuckets * 8;  // 7168 cells (56 KiB)
+constexpr uint32_t kObjHigh = kObjSlots / 2;   // at most kWG new keys per window on top
+constexpr uint32_t kPageHigh = kPageSlots / 2;
 constexpr uint32_t kProbes = 32;
 constexpr uint32_t kEmpty32 = 0xffffffffu;
 constexpr uint64_t kEmpty64 = ~0ull;
@@ -104,6 +110,7 @@ struct Params {
   uint32_t nb_threads;
   uint32_t flags;
   uint32_t nb_entries;
+  uint32_t lds_nodes;    // node records fit in LDS (nb_keys <= kLdsNodes)
   uint32_t sparse_mask;  // capacity - 1 (power of two)
   uint64_t hist_cells;   // dense cells per thread: histogram index = thread * hist_cells + cell
   uint64_t* sum64;
@@ -160,12 +167,6 @@ __device__ __forceinline__ uint32_t bucket_mask(uint32_t lvl) {
   return 0;
 }
 
-// Records are 8-byte multiples (sizes that are not are rejected), so every
-// record offset is 8-byte aligned in the 16-byte aligned LDS window.
-__device__ __forceinline__ uint64_t lds_u64(const uint8_t* s, uint32_t off) {
-  return *reinterpret_cast<const uint64_t*>(s + off);
-}
-
 __device__ __forceinline__ void set_error(Params& p, uint64_t seq, uint32_t off, uint32_t code) {
   uint64_t w = (seq << 40) | (uint64_t(off) << 8) | code;
   atomicMin(reinterpret_cast<unsigned long long*>(p.min64 + 36 + p.nb_entries),
@@ -196,31 +197,6 @@ __device__ __forceinline__ bool entry_match(uint4 a, uint4 b, uint64_t addr, uin
   return baddr <= addr && addr < bend && alloc <= ts && ts <= fr;
 }
 
-__device__ __forceinline__ int64_t find_entry(const Params& p, const uint64_t* s_fences,
-                                              uint64_t addr, uint64_t ts, DevEntry* out) {
-  const uint32_t k = lower_key(p, s_fences, addr);
-  if (k >= p.nb_keys) return -1;
-  const uint4* q = reinterpret_cast<const uint4*>(p.nodes + k);
-  const uint4 a = q[0], b = q[1], c = q[2];
-  out->addr = (uint64_t(a.y) << 32) | a.x;
-  out->hist = (uint64_t(c.y) << 32) | c.x;
-  out->sidx = c.z;
-  if (entry_match(a, b, addr, ts)) return c.w;
-  const uint4 d = q[3];
-  for (uint32_t e = c.w + 1; e < c.w + d.x; e++) {  // older entries of a reused address
-    const uint4* r = reinterpret_cast<const uint4*>(p.entries + e);
-    const uint4 ra = r[0], rb = r[1];
-    if (entry_match(ra, rb, addr, ts)) {
-      const uint4 rc = r[2];
-      out->addr = (uint64_t(ra.y) << 32) | ra.x;
-      out->hist = (uint64_t(rc.y) << 32) | rc.x;
-      out->sidx = rc.z;
-      return e;
-    }
-  }
-  return -1;
-}
-
 __device__ __forceinline__ void sparse_add(Params& p, uint64_t key, uint64_t seq, uint32_t off, uint32_t cnt) {
   uint64_t h = (key * 0x9E3779B97F4A7C15ull) >> 20;
   uint32_t slot = uint32_t(h) & p.sparse_mask;
@@ -236,29 +212,27 @@ __device__ __forceinline__ void sparse_add(Params& p, uint64_t key, uint64_t seq
   set_error(p, seq, off, kErrCapacity);
 }
 
-// Per-workgroup privatised counters for the buffer being analysed.
+// Per-workgroup privatised counters of the stream (access type, thread rank)
+// being analysed.  One stream at a time per workgroup, so (entry) and
+// (entry, page) are the keys of the aggregation tables.
 struct WgCounters {
   unsigned long long sums[kGlobalSums];  // total_count, total_weight, na, 18 x (count, sum)
   unsigned long long mins[18];
   unsigned long long maxs[18];
-  unsigned int nb_samples, nb_found;
-  // per-buffer aggregation of the per-object counters: one buffer is one
-  // thread and one access type, so (entry) and (entry, page) are the keys
   unsigned int okey[kObjSlots];
   unsigned int ocnt[kObjSlots];
   unsigned long long ofirst[kObjSlots];  // smallest (seq << 32 | offset): first match
   unsigned long long owt[kObjSlots];
-  unsigned int pkey[kPageSlots];         // dense cell index (hist_base(entry) + page)
+  uint4 pkey4[kPageSlots / 4];           // dense cell index (hist_base(entry) + page), 8 per bucket
   unsigned int pcnt[kPageSlots];
   unsigned int nobj, npage;              // occupied slots
 };
 
 // Direct-mapped slots with linear probing: slot order follows key order, so
-// the flush walks entries / cells in (mostly) ascending address order and its
+// a flush walks entries / cells in (mostly) ascending address order and its
 // global atomics coalesce into shared 64-byte lines.  A slot already holding
-// the key (hot objects) is found with a plain broadcast read, no CAS.
-// Probe chains (first-touch insertion / collisions); the common case -- the
-// key already sits in its home slot -- is handled inline by the callers.
+// the key (hot objects) is found with a plain broadcast read, no CAS; the
+// probe chain (first touch, collisions) is the out-of-line case.
 __device__ __forceinline__ int obj_slot_probe(WgCounters& wc, uint32_t e) {
   uint32_t s = e & (kObjSlots - 1);
   for (uint32_t i = 0; i < kProbes; i++) {
@@ -277,38 +251,51 @@ __device__ __forceinline__ int obj_slot_probe(WgCounters& wc, uint32_t e) {
   return -1;
 }
 
-__device__ __forceinline__ int page_slot_probe(WgCounters& wc, uint32_t cell) {
-  uint32_t s = cell & (kPageSlots - 1);
-  for (uint32_t i = 0; i < kProbes; i++) {
-    unsigned k = wc.pkey[s];
-    if (k == cell) return (int)s;
-    if (k == kEmpty32) {
-      unsigned prev = atomicCAS(&wc.pkey[s], kEmpty32, cell);
-      if (prev == kEmpty32) {
-        atomicAdd(&wc.npage, 1u);
-        return (int)s;
-      }
-      if (prev == cell) return (int)s;
-    }
-    s = (s + 1) & (kPageSlots - 1);
-  }
-  return -1;
-}
-
 __device__ __forceinline__ int obj_slot(WgCounters& wc, uint32_t e) {
   const uint32_t s = e & (kObjSlots - 1);
   return wc.okey[s] == e ? (int)s : obj_slot_probe(wc, e);
 }
 
+// Page cells: a Fibonacci hash picks one 8-slot bucket (two 16 B LDS reads,
+// no probe chain).  A missing cell takes the first empty slot by CAS; every
+// inserter scans the bucket in the same order and a slot leaves "empty" only
+// once, so a cell never lands in two slots.  A full bucket returns -1 (the
+// caller then updates global memory directly).
+__device__ __forceinline__ uint32_t page_bucket(uint32_t cell) {
+  return (uint32_t)(((uint64_t)(cell * 0x9E3779B1u) * kPageBuckets) >> 32);
+}
+
 __device__ __forceinline__ int page_slot(WgCounters& wc, uint32_t cell) {
-  const uint32_t s = cell & (kPageSlots - 1);
-  return wc.pkey[s] == cell ? (int)s : page_slot_probe(wc, cell);
+  const uint32_t hb = page_bucket(cell);
+  const uint4 k0 = wc.pkey4[2 * hb], k1 = wc.pkey4[2 * hb + 1];
+  uint32_t key[8] = {k0.x, k0.y, k0.z, k0.w, k1.x, k1.y, k1.z, k1.w};
+  int j = -1;
+#pragma unroll
+  for (int i = 7; i >= 0; i--) j = key[i] == cell ? i : j;
+  if (j >= 0) return (int)(hb * 8 + j);
+  unsigned int* slots = reinterpret_cast<unsigned int*>(&wc.pkey4[2 * hb]);
+  for (int attempt = 0; attempt < 8; attempt++) {
+    int f = -1;
+#pragma unroll
+    for (int i = 7; i >= 0; i--) f = key[i] == kEmpty32 ? i : f;
+    if (f < 0) return -1;
+    const unsigned prev = atomicCAS(&slots[f], kEmpty32, cell);
+    if (prev == kEmpty32) {
+      atomicAdd(&wc.npage, 1u);
+      return (int)(hb * 8 + f);
+    }
+    if (prev == cell) return (int)(hb * 8 + f);
+#pragma unroll
+    for (int i = 0; i < 8; i++) key[i] = i == f ? prev : key[i];
+  }
+  return -1;
 }
 
 // Per-lane privatised mem_counters of the current stream: packed u16 counts
 // and u32 weight sums per bucket, plus total count / weight / N/A.  Bounded:
-// drained at least every kDrainWindows windows and only weights < 2^23 take
-// this path, so nothing overflows (256 x 2^23 = 2^31).
+// drained at least every kDrainWindows windows (one record per lane per
+// window) and only weights < 2^23 take this path, so nothing overflows
+// (256 x 2^23 = 2^31).
 constexpr uint32_t kDrainWindows = 256;
 constexpr uint64_t kLaneMaxWeight = 1ull << 23;
 // Only the 9 hit buckets live in registers (the common case in PEBS data);
@@ -360,18 +347,88 @@ __device__ __forceinline__ void lane_acc_drain(LaneAcc& a, WgCounters& wc, int l
   lane_acc_clear(a);
 }
 
+// The object table as the kernel sees it: node records in LDS (small tables)
+// or in global memory (L2/MALL resident) behind the LDS fence table.
+struct Lookup {
+  const uint64_t* fences;  // LDS
+  const uint4* nodes;      // LDS: 2 x uint4 per node: (addr, end), (alloc, free)
+  const uint2* ninfo;      // LDS: (dense histogram base or ~0, entry id | older-entries << 31)
+};
+
+struct Match {
+  int64_t e;       // entry id, -1 = no match
+  uint64_t baddr;  // the entry's buffer_addr
+  uint64_t hist;   // dense histogram base cell, or kHistSparse
+};
+
+__device__ __forceinline__ void match_older(const Params& p, uint32_t first, uint32_t count, uint64_t addr,
+                                            uint64_t ts, Match& m) {
+  for (uint32_t e = first + 1; e < first + count; e++) {  // older entries of a reused address
+    const uint4* r = reinterpret_cast<const uint4*>(p.entries + e);
+    const uint4 ra = r[0], rb = r[1];
+    if (entry_match(ra, rb, addr, ts)) {
+      const uint4 rc = r[2];
+      m.e = e;
+      m.baddr = (uint64_t(ra.y) << 32) | ra.x;
+      m.hist = (uint64_t(rc.y) << 32) | rc.x;
+      return;
+    }
+  }
+}
+
+// __ma_find_mem_info_from_sample_generic (mem_analyzer.c:249-286): the
+// lower-bound node only (ht_lower_key, tools/hash.c:63-77), newest entry
+// first, inclusive timestamp window (is_sample_in_buffer, :141-155).
+__device__ __forceinline__ Match find_entry(const Params& p, const Lookup& L, uint64_t addr, uint64_t ts) {
+  Match m;
+  m.e = -1;
+  m.baddr = 0;
+  m.hist = kHistSparse;
+  if (p.lds_nodes) {
+    // nb_keys <= kLdsNodes: the fence table is the key array itself
+    uint32_t idx = 0;
+    for (uint32_t st = p.fence_p2 >> 1; st; st >>= 1) idx = (L.fences[idx + st] <= addr) ? idx + st : idx;
+    idx = min(idx, p.nb_keys - 1);  // ~0 padding: addr == UINT64_MAX
+    if (p.nb_keys == 0 || addr < L.fences[0]) return m;
+    const uint4 a = L.nodes[2 * idx], b = L.nodes[2 * idx + 1];
+    const uint2 inf = L.ninfo[idx];
+    if (entry_match(a, b, addr, ts)) {
+      m.e = inf.y & 0x7fffffffu;
+      m.baddr = (uint64_t(a.y) << 32) | a.x;
+      m.hist = inf.x == kEmpty32 ? kHistSparse : (uint64_t)inf.x;
+    } else if (inf.y >> 31) {
+      match_older(p, inf.y & 0x7fffffffu, p.nodes[idx].count, addr, ts, m);
+    }
+    return m;
+  }
+  const uint32_t k = lower_key(p, L.fences, addr);
+  if (k >= p.nb_keys) return m;
+  const uint4* q = reinterpret_cast<const uint4*>(p.nodes + k);
+  const uint4 a = q[0], b = q[1], c = q[2];
+  if (entry_match(a, b, addr, ts)) {
+    m.e = c.w;
+    m.baddr = (uint64_t(a.y) << 32) | a.x;
+    m.hist = (uint64_t(c.y) << 32) | c.x;
+    return m;
+  }
+  const uint4 d = q[3];
+  if (d.x > 1) match_older(p, c.w, d.x, addr, ts, m);
+  return m;
+}
+
 // Process one decoded record (`valid` = it is a SAMPLE).  Every lane of the
-// wave calls this together (wave-level reductions inside).
-__device__ __forceinline__ void process_sample(Params& p, WgCounters& wc, LaneAcc& acc, const uint64_t* s_fences,
+// wave calls this together (wave-level reductions inside); nsamp / nfound are
+// wave-uniform per-buffer tallies.
+__device__ __forceinline__ void process_sample(Params& p, WgCounters& wc, LaneAcc& acc, const Lookup& L,
                                                bool valid, uint64_t ts, uint64_t addr,
                                                uint64_t w, uint64_t dsrc, uint32_t access,
-                                               uint32_t th, uint64_t seq, uint32_t off) {
-  const int lane = threadIdx.x & 63;
+                                               uint32_t th, uint64_t seq, uint32_t off,
+                                               uint32_t& nsamp, uint32_t& nfound) {
   const uint32_t lvl = uint32_t(dsrc >> 5) & 0x3fff;  // data_src.mem_lvl
   // ---- global counters: update_counters(global_counters, ...) (mem_sampling.c:882)
-  uint64_t vmask = __ballot(valid);
+  const uint64_t vmask = __ballot(valid);
   if (vmask == 0) return;
-  if (lane == 0) atomicAdd(&wc.nb_samples, (unsigned)__popcll(vmask));
+  nsamp += (uint32_t)__popcll(vmask);
   if (valid && !(p.flags & kDbgNoGlobal)) {
     const uint32_t bm = bucket_mask(lvl);
     if (w < kLaneMaxWeight) {  // register accumulation (no LDS traffic)
@@ -410,42 +467,42 @@ __device__ __forceinline__ void process_sample(Params& p, WgCounters& wc, LaneAc
       }
     }
   }
-match:
   if (!(p.flags & NMG_F_MATCH_SAMPLES)) return;
 
   // ---- __match_sample (mem_sampling.c:594-673)
-  DevEntry ent;
-  int64_t e = valid ? find_entry(p, s_fences, addr, ts, &ent) : -1;
-  uint64_t fmask = __ballot(e >= 0);
-  if (lane == 0 && fmask) atomicAdd(&wc.nb_found, (unsigned)__popcll(fmask));
+  Match m;
+  m.e = -1;
+  if (valid) m = find_entry(p, L, addr, ts);
+  const int64_t e = m.e;
+  nfound += (uint32_t)__popcll(__ballot(e >= 0));
   if (e < 0 || (p.flags & kDbgNoTables)) return;
-  // per-object counters, aggregated for the whole buffer in LDS
-  int os = obj_slot(wc, (uint32_t)e);
+  // per-object counters, aggregated per stream in LDS
+  const int os = obj_slot(wc, (uint32_t)e);
+  const unsigned long long ord = (seq << 32) | off;  // first match in analysis order (quirk Q7)
   if (os >= 0) {
     atomicAdd(&wc.ocnt[os], 1u);
     if (w) atomicAdd(&wc.owt[os], (unsigned long long)w);
-    const unsigned long long ord = (seq << 32) | off;
     if (ord < wc.ofirst[os]) atomicMin(&wc.ofirst[os], ord);
   } else {  // table full: straight to global
     atomicAdd(reinterpret_cast<unsigned long long*>(p.sum64 + objcw_index(e, access, 0, p.nb_entries)), 1ull);
     if (w)
       atomicAdd(reinterpret_cast<unsigned long long*>(p.sum64 + objcw_index(e, access, 1, p.nb_entries)),
                 (unsigned long long)w);
-    // first match in analysis order -> call-site id order (quirk Q7)
-    uint64_t ord = (seq << 32) | off;
     unsigned long long* fp = reinterpret_cast<unsigned long long*>(p.min64 + 36 + e);
-    if (ord < *fp) atomicMin(fp, (unsigned long long)ord);
+    if (ord < *fp) atomicMin(fp, ord);
   }
   if (p.flags & NMG_F_PAGE_HIST) {
     // ma_get_block: page_no = (int)((addr - buffer_addr) / 4096) (mem_analyzer.c:530-531)
-    uint32_t page = uint32_t(int(uint64_t(addr - ent.addr) / kPageSize));
-    if (ent.hist != kHistSparse) {
-      const uint32_t cell = uint32_t(ent.hist + page);
-      int ps = page_slot(wc, cell);
+    const uint32_t page = uint32_t(int(uint64_t(addr - m.baddr) / kPageSize));
+    if (m.hist != kHistSparse) {
+      const uint32_t cell = uint32_t(m.hist + page);
+      const int ps = page_slot(wc, cell);
       if (ps >= 0) atomicAdd(&wc.pcnt[ps], 1u);
       else atomicAdd(p.hist + uint64_t(th) * p.hist_cells + cell, 1u);
-    } else if (ent.sidx != ~0u) {  // huge objects ([stack]): hashed cells in global memory
-      sparse_add(p, sparse_key(ent.sidx, th, page), seq, off, 1u);
+    } else {
+      const uint32_t sidx = p.entries[e].sidx;
+      if (sidx != ~0u)  // huge objects ([stack]): hashed cells in global memory
+        sparse_add(p, sparse_key(sidx, th, page), seq, off, 1u);
     }
   }
   if (p.flags & NMG_F_OBJECT_LEVELS) {
@@ -463,10 +520,70 @@ match:
 }
 
 // ---------------------------------------------------------------------------
-// per-workgroup aggregation state: reset, and flush to global memory
+// per-workgroup aggregation state: flush to global memory and clear, slot by
+// slot (each thread owns the slots it flushes; callers fence with barriers)
 
-__device__ __forceinline__ void reset_state(WgCounters& wc, int tid) {
-  for (int i = tid; i < (int)kGlobalSums; i += kWG) wc.sums[i] = 0;
+__device__ __forceinline__ void flush_objects(Params& p, WgCounters& wc, int tid, uint32_t a) {
+  const bool write = !(p.flags & kDbgNoFlush);
+  for (int i = tid; i < (int)kObjSlots; i += kWG) {
+    const uint32_t e = wc.okey[i];
+    if (e == kEmpty32) continue;
+    if (write) {
+      atomicAdd(reinterpret_cast<unsigned long long*>(p.sum64 + objcw_index(e, a, 0, p.nb_entries)),
+                (unsigned long long)wc.ocnt[i]);
+      if (wc.owt[i])
+        atomicAdd(reinterpret_cast<unsigned long long*>(p.sum64 + objcw_index(e, a, 1, p.nb_entries)), wc.owt[i]);
+      unsigned long long* fp = reinterpret_cast<unsigned long long*>(p.min64 + 36 + e);
+      if (wc.ofirst[i] < *fp) atomicMin(fp, wc.ofirst[i]);
+    }
+    wc.okey[i] = kEmpty32;
+    wc.ocnt[i] = 0;
+    wc.ofirst[i] = kEmpty64;
+    wc.owt[i] = 0;
+  }
+  if (tid == 0) wc.nobj = 0;
+}
+
+__device__ __forceinline__ void flush_pages(Params& p, WgCounters& wc, int tid, uint32_t th) {
+  const bool write = !(p.flags & kDbgNoFlush);
+  unsigned int* hrow = p.hist + uint64_t(th) * p.hist_cells;
+  unsigned int* pkey = reinterpret_cast<unsigned int*>(wc.pkey4);
+  for (int i = tid; i < (int)kPageSlots; i += kWG) {
+    const uint32_t cell = pkey[i];
+    if (cell == kEmpty32) continue;
+    if (write) atomicAdd(hrow + cell, wc.pcnt[i]);
+    pkey[i] = kEmpty32;
+    wc.pcnt[i] = 0;
+  }
+  if (tid == 0) wc.npage = 0;
+}
+
+// global mem_counters[a] of the stream (after the lanes were drained)
+__device__ __forceinline__ void flush_sums(Params& p, WgCounters& wc, int tid, uint32_t a) {
+  const bool write = !(p.flags & kDbgNoFlush);
+  if (tid < (int)kGlobalSums) {
+    if (write && wc.sums[tid])
+      atomicAdd(reinterpret_cast<unsigned long long*>(p.sum64 + gsum_index(a, tid)), wc.sums[tid]);
+  }
+  if (tid < 18) {
+    if (write && wc.sums[3 + 2 * tid]) {
+      atomicMin(reinterpret_cast<unsigned long long*>(p.min64 + a * 18 + tid), wc.mins[tid]);
+      atomicMax(reinterpret_cast<unsigned long long*>(p.max64 + a * 18 + tid), wc.maxs[tid]);
+    }
+  }
+  // (cleared after a barrier: sums[3 + 2 * tid] is read by other threads above)
+}
+
+__device__ __forceinline__ void clear_sums(WgCounters& wc, int tid) {
+  if (tid < (int)kGlobalSums) wc.sums[tid] = 0;
+  if (tid < 18) {
+    wc.mins[tid] = ~0ull;  // INIT_COUNTER: min = UINT64_MAX (mem_analyzer.c:415-420)
+    wc.maxs[tid] = 0;
+  }
+}
+
+__device__ __forceinline__ void clear_state(WgCounters& wc, int tid) {
+  clear_sums(wc, tid);
   for (int i = tid; i < (int)kObjSlots; i += kWG) {
     wc.okey[i] = kEmpty32;
     wc.ocnt[i] = 0;
@@ -474,12 +591,8 @@ __device__ __forceinline__ void reset_state(WgCounters& wc, int tid) {
     wc.owt[i] = 0;
   }
   for (int i = tid; i < (int)kPageSlots; i += kWG) {
-    wc.pkey[i] = kEmpty32;
+    reinterpret_cast<unsigned int*>(wc.pkey4)[i] = kEmpty32;
     wc.pcnt[i] = 0;
-  }
-  if (tid < 18) {
-    wc.mins[tid] = ~0ull;  // INIT_COUNTER: min = UINT64_MAX (mem_analyzer.c:415-420)
-    wc.maxs[tid] = 0;
   }
   if (tid == 0) {
     wc.nobj = 0;
@@ -487,219 +600,235 @@ __device__ __forceinline__ void reset_state(WgCounters& wc, int tid) {
   }
 }
 
-// One stream (access type a, thread rank th): global mem_counters[a], then one
-// global update per distinct entry / (entry, page) accumulated since the last flush.
-__device__ __forceinline__ void flush_state(Params& p, WgCounters& wc, int tid, uint32_t a, uint32_t th) {
-  if (p.flags & kDbgNoFlush) return;
-  for (int i = tid; i < (int)kGlobalSums; i += kWG)
-    if (wc.sums[i]) atomicAdd(reinterpret_cast<unsigned long long*>(p.sum64 + gsum_index(a, i)), wc.sums[i]);
-  if (tid < 18 && wc.sums[3 + 2 * tid]) {
-    atomicMin(reinterpret_cast<unsigned long long*>(p.min64 + a * 18 + tid), wc.mins[tid]);
-    atomicMax(reinterpret_cast<unsigned long long*>(p.max64 + a * 18 + tid), wc.maxs[tid]);
+// ---------------------------------------------------------------------------
+// record loads straight into registers
+
+// One 40 B stride slot: 16 B + 16 B + 8 B loads whose offsets depend on the
+// slot's 16 B parity (records are 8-aligned in a 16-aligned buffer), so every
+// lane issues the same three instructions.  Decoded only when consumed, so a
+// prefetched window stays in flight while the current one is processed.
+struct RawRec {
+  uint4 x, y;
+  uint2 z;
+};
+
+__device__ __forceinline__ void load_rec(const uint8_t* base, uint64_t pos, uint64_t len, RawRec& r) {
+  if (pos + kRecBytes <= len) {
+    const uint32_t odd = uint32_t(pos >> 3) & 1;
+    const uint8_t* q = base + pos;
+    r.x = *reinterpret_cast<const uint4*>(q + (odd ? 8 : 0));
+    r.y = *reinterpret_cast<const uint4*>(q + (odd ? 24 : 16));
+    r.z = *reinterpret_cast<const uint2*>(q + (odd ? 0 : 32));
+  } else {
+    r.x = make_uint4(0, 0, 0, 0);
+    r.y = make_uint4(0, 0, 0, 0);
+    r.z = make_uint2(0, 0);
   }
-  for (int i = tid; i < (int)kObjSlots; i += kWG) {
-    uint32_t e = wc.okey[i];
-    if (e == kEmpty32) continue;
-    atomicAdd(reinterpret_cast<unsigned long long*>(p.sum64 + objcw_index(e, a, 0, p.nb_entries)),
-              (unsigned long long)wc.ocnt[i]);
-    if (wc.owt[i])
-      atomicAdd(reinterpret_cast<unsigned long long*>(p.sum64 + objcw_index(e, a, 1, p.nb_entries)), wc.owt[i]);
-    unsigned long long* fp = reinterpret_cast<unsigned long long*>(p.min64 + 36 + e);
-    if (wc.ofirst[i] < *fp) atomicMin(fp, wc.ofirst[i]);
+}
+
+struct Rec {
+  uint64_t hdr, ts, addr, w, dsrc;
+};
+
+__device__ __forceinline__ uint64_t u64of(uint32_t lo, uint32_t hi) { return (uint64_t(hi) << 32) | lo; }
+
+__device__ __forceinline__ Rec decode_rec(const RawRec& r, uint64_t pos) {
+  Rec d;
+  if ((pos >> 3) & 1) {  // hdr | ts addr | w dsrc
+    d.hdr = u64of(r.z.x, r.z.y);
+    d.ts = u64of(r.x.x, r.x.y);
+    d.addr = u64of(r.x.z, r.x.w);
+    d.w = u64of(r.y.x, r.y.y);
+    d.dsrc = u64of(r.y.z, r.y.w);
+  } else {  // hdr ts | addr w | dsrc
+    d.hdr = u64of(r.x.x, r.x.y);
+    d.ts = u64of(r.x.z, r.x.w);
+    d.addr = u64of(r.y.x, r.y.y);
+    d.w = u64of(r.y.z, r.y.w);
+    d.dsrc = u64of(r.z.x, r.z.y);
   }
-  unsigned int* hrow = p.hist + uint64_t(th) * p.hist_cells;
-  for (int i = tid; i < (int)kPageSlots; i += kWG) {
-    uint32_t cell = wc.pkey[i];
-    if (cell != kEmpty32) atomicAdd(hrow + cell, wc.pcnt[i]);
-  }
+  return d;
 }
 
 // ---------------------------------------------------------------------------
 // the attribution kernel
-
-// 2 workgroups of 512 threads per CU = 4 waves per SIMD (<= 128 VGPRs)
-__global__ __launch_bounds__(kWG, 4) void attribute_kernel(Params p) {
-  __shared__ __attribute__((aligned(16))) uint8_t s_data[kLdsBytes];
+//
+// One 1024-thread workgroup per CU (LDS: fences 8 KiB, node records 40 KiB,
+// object table 48 KiB, page table 56 KiB, slow-path list 4 KiB), persistent
+// over a byte-balanced range of the stream-sorted buffer list.  A window is
+// 1024 stride slots of 40 B, one per lane, loaded straight into registers;
+// the next window (of this buffer or the next one) is issued before the
+// current one is processed.  One barrier per window: it publishes the window's
+// "irregular" bit and the tables' fill level through rotating flag words.
+__global__ __launch_bounds__(kWG, 1) void attribute_kernel(Params p) {
   __shared__ uint64_t s_fences[kMaxFences];
-  __shared__ uint16_t s_list[kMaxList];
+  __shared__ uint4 s_nodes[2 * kLdsNodes];
+  __shared__ uint2 s_ninfo[kLdsNodes];
+  __shared__ uint32_t s_list[kMaxList];
   __shared__ WgCounters wc;
-  __shared__ uint32_t s_flag, s_nlist, s_next, s_err;
+  __shared__ uint32_t s_flags[3], s_nlist, s_next, s_err;
 
   const int tid = threadIdx.x;
-  for (uint32_t i = tid; i < p.fence_p2; i += kWG) s_fences[i] = p.fences[i];
-
-  // This workgroup's contiguous, byte-balanced share of the stream-sorted
-  // buffer list.  Consecutive buffers of one stream (thread, access) share
-  // the LDS tables, so global updates happen once per stream run, not once
-  // per buffer.
-  const uint32_t r0 = p.ranges[blockIdx.x], r1 = p.ranges[blockIdx.x + 1];
   const int lane = tid & 63;
-  uint32_t cur_access = ~0u, cur_thread = ~0u;
+  for (uint32_t i = tid; i < p.fence_p2; i += kWG) s_fences[i] = p.fences[i];
+  if (p.lds_nodes) {
+    for (uint32_t i = tid; i < p.nb_keys; i += kWG) {
+      const uint4* q = reinterpret_cast<const uint4*>(p.nodes + i);
+      const uint4 a = q[0], b = q[1], c = q[2], d = q[3];
+      s_nodes[2 * i] = a;
+      s_nodes[2 * i + 1] = b;
+      s_ninfo[i] = make_uint2(c.y == 0 ? c.x : kEmpty32, c.w | (d.x > 1 ? 0x80000000u : 0u));
+    }
+  }
+  clear_state(wc, tid);
+  if (tid < 3) s_flags[tid] = 0;
+  __syncthreads();
+  const Lookup L{s_fences, s_nodes, s_ninfo};
+
+  const uint32_t r0 = p.ranges[blockIdx.x], r1 = p.ranges[blockIdx.x + 1];
+  if (r0 >= r1) return;
+  uint32_t idx = r0;
+  uint32_t b = p.order[idx];
+  BufDesc d = p.bufs[b];
+  uint32_t cur = 0;  // byte cursor, as `cur_cpt` in __analyze_buffer (mem_sampling.c:836)
+  uint32_t cur_access = d.access, cur_thread = d.thread_rank;
+  RawRec nx;
+  load_rec(p.data + d.offset, uint64_t(tid) * kRecBytes, d.len, nx);
   LaneAcc acc;
   lane_acc_clear(acc);
-  uint32_t acc_windows = 0;
-  reset_state(wc, tid);
-  __syncthreads();
-  for (uint32_t idx = r0; idx < r1; idx++) {
-    const uint32_t b = p.order[idx];
-    const BufDesc d = p.bufs[b];
+  uint32_t win = 0, acc_windows = 0, nsamp = 0, nfound = 0;
+
+  while (true) {
     const uint8_t* base = p.data + d.offset;
-    const uint32_t len = d.len;
-    // leave room for a whole buffer (~1k distinct cells) so probe chains stay short;
-    // the flush itself is cheap (its atomics coalesce)
-    const bool full = wc.nobj > kObjSlots * 5 / 8 || wc.npage > kPageSlots / 4;
-    if (d.access != cur_access || d.thread_rank != cur_thread || full) {
-      if (cur_access != ~0u) {
-        lane_acc_drain(acc, wc, lane);
-        acc_windows = 0;
-        __syncthreads();
-        flush_state(p, wc, tid, cur_access, cur_thread);
-        __syncthreads();
-        reset_state(wc, tid);
-      }
-      cur_access = d.access;
-      cur_thread = d.thread_rank;
-    }
-    if (tid == 0) {
-      wc.nb_samples = 0;
-      wc.nb_found = 0;
-      s_err = 0;
-    }
+    const uint64_t len = d.len;
+    const uint64_t pos = uint64_t(cur) + uint64_t(tid) * kRecBytes;
+    const uint32_t n_cand = uint32_t((min(len - cur, (uint64_t)kWinBytes) + kRecBytes - 1) / kRecBytes);
+    const Rec r = decode_rec(nx, pos);
+    // ---- fast-path check: every 40 B stride slot holds a whole 40 B record
+    const bool bad = (cur & 7) != 0 || ((uint32_t)tid < n_cand && (pos + kRecBytes > len || (r.hdr >> 48) != kRecBytes));
+    if (__ballot(bad) && lane == 0) atomicOr(&s_flags[win % 3], 1u);
+    if (tid == 0 && (wc.nobj > kObjHigh || wc.npage > kPageHigh)) atomicOr(&s_flags[win % 3], 2u);
     __syncthreads();
-
-    uint32_t cur = 0;  // byte cursor, as `cur_cpt` in __analyze_buffer
-    // next window's 16 B chunks, loaded into registers while the current
-    // window is processed (software pipelining of the HBM stream)
-    static_assert((kLdsBytes / 16 + kWG - 1) / kWG == 3, "three prefetch registers per lane");
-    uint4 pf0 = {0, 0, 0, 0}, pf1 = {0, 0, 0, 0}, pf2 = {0, 0, 0, 0};
-    uint32_t pf_win = ~0u;
-    const uint32_t len16 = (len + 15u) & ~15u;
-    while (cur < len) {
-      const uint32_t win = cur & ~15u;
-      const uint32_t win_end = min(win + (uint32_t)kLdsBytes, len16);
-      // ---- stage the window into LDS: coalesced 16 B loads
-      const uint4* src = reinterpret_cast<const uint4*>(base + win);
-      uint4* dst = reinterpret_cast<uint4*>(s_data);
-      const uint32_t nchunks = (win_end - win) >> 4;
-      if (pf_win == win) {
-        if ((uint32_t)tid < nchunks) dst[tid] = pf0;
-        if ((uint32_t)tid + kWG < nchunks) dst[tid + kWG] = pf1;
-        if ((uint32_t)tid + 2 * kWG < nchunks) dst[tid + 2 * kWG] = pf2;
-      } else {
-        for (uint32_t c = tid; c < nchunks; c += kWG) dst[c] = src[c];
-      }
-      pf_win = ~0u;
-      if (tid == 0) s_flag = 0;
+    const uint32_t f = s_flags[win % 3];
+    if (tid == 0) s_flags[(win + 2) % 3] = 0;  // last read before the previous barrier
+    win++;
+    if (f & 2) {  // tables filling up: flush them mid-stream (every insert happened before the barrier)
+      flush_objects(p, wc, tid, cur_access);
+      flush_pages(p, wc, tid, cur_thread);
       __syncthreads();
+    }
 
-      const uint32_t seg_end = min(win + (uint32_t)kSegBytes, len);
-      const uint32_t n_cand = (seg_end - cur + kRecBytes - 1) / kRecBytes;
-      // ---- fast-path check: every 40 B stride slot holds a 40 B record
-      bool bad = (cur & 7) != 0;
-      for (uint32_t i = tid; i < n_cand && !bad; i += kWG) {
-        uint32_t pos = cur + i * kRecBytes;
-        uint64_t hdr = lds_u64(s_data, pos - win);
-        if ((hdr >> 48) != kRecBytes || pos + kRecBytes > len) bad = true;
-      }
-      if (bad) s_flag = 1;
-      __syncthreads();
-
-      if (p.flags & kDbgLoadOnly) {
-        cur += n_cand * kRecBytes;
-      } else if (s_flag == 0) {
-        // ---- fast path: decode all n_cand records in parallel
-        const uint32_t next = cur + n_cand * kRecBytes;
-        if (next < len) {  // issue the next window's loads now, consume them next iteration
-          const uint32_t nwin = next & ~15u;
-          const uint32_t nchunks2 = (min(nwin + (uint32_t)kLdsBytes, len16) - nwin) >> 4;
-          const uint4* nsrc = reinterpret_cast<const uint4*>(base + nwin);
-          if ((uint32_t)tid < nchunks2) pf0 = nsrc[tid];
-          if ((uint32_t)tid + kWG < nchunks2) pf1 = nsrc[tid + kWG];
-          if ((uint32_t)tid + 2 * kWG < nchunks2) pf2 = nsrc[tid + 2 * kWG];
-          pf_win = nwin;
+    uint64_t ncur;
+    if (!(f & 1)) {
+      // ---- fast path: one record per lane
+      ncur = cur + uint64_t(n_cand) * kRecBytes;
+    } else {
+      // ---- slow path: wave 0 follows the header chain from global memory,
+      // 64 stride slots per step (a run of regular 40 B records is taken in
+      // one step, an irregular record is handled alone), listing SAMPLE offsets
+      if (tid < 64) {
+        uint64_t q0 = cur;
+        uint32_t n = 0, err = 0;
+        const uint64_t lim = min(uint64_t(cur) + kWinBytes, len);
+        while (q0 < lim && n + 65 <= kMaxList) {
+          const uint64_t q = q0 + uint64_t(lane) * kRecBytes;
+          const uint64_t hdr = (q + 8 <= len) ? *reinterpret_cast<const uint64_t*>(base + q) : 0;
+          const bool reg = q < lim && q + kRecBytes <= len && (hdr >> 48) == kRecBytes;
+          const uint64_t rm = __ballot(reg);
+          const uint32_t run = ~rm ? (uint32_t)__builtin_ctzll(~rm) : 64u;
+          const bool smp = (uint32_t)lane < run && uint32_t(hdr) == kSampleType;
+          const uint64_t sm = __ballot(smp);
+          if (smp) s_list[n + (uint32_t)__popcll(sm & ((1ull << lane) - 1))] = (uint32_t)q;
+          n += (uint32_t)__popcll(sm);
+          q0 += uint64_t(run) * kRecBytes;
+          if (run == 64 || q0 >= lim) continue;
+          // record at q0 (lane `run`'s slot) is not a whole 40 B record
+          if (q0 + 8 > len) { err = kErrTruncated; break; }
+          const uint64_t h = (uint64_t)__shfl(hdr, (int)run, 64);
+          const uint32_t size = uint32_t(h >> 48);
+          if (size == 0) { err = kErrZeroSize; break; }  // mem_sampling.c:857-860
+          if (size & 7) { err = kErrUnaligned; break; }  // perf records are 8-byte multiples
+          if (uint32_t(h) == kSampleType) {
+            if (q0 + kRecBytes > len || q0 + size > len) { err = kErrTruncated; break; }
+            if (lane == 0) s_list[n] = (uint32_t)q0;
+            n++;
+          }
+          q0 += size;  // non-SAMPLE records are skipped by their size (:918)
         }
-        for (uint32_t i0 = 0; i0 < n_cand; i0 += kWG) {
-          uint32_t i = i0 + tid;
-          bool valid = false;
-          uint64_t ts = 0, addr = 0, w = 0, dsrc = 0;
-          uint32_t pos = cur + i * kRecBytes;
-          if (i < n_cand) {
-            uint32_t o = pos - win;
-            uint64_t hdr = lds_u64(s_data, o);
-            valid = uint32_t(hdr) == kSampleType;
-            ts = lds_u64(s_data, o + 8);
-            addr = lds_u64(s_data, o + 16);
-            w = lds_u64(s_data, o + 24);
-            dsrc = lds_u64(s_data, o + 32);
-          }
-          process_sample(p, wc, acc, s_fences, valid, ts, addr, w, dsrc, d.access, d.thread_rank, d.seq, pos);
-        }
-        cur += n_cand * kRecBytes;
-      } else {
-        // ---- slow path: follow the header chain in LDS (lane 0), then
-        // process the window's SAMPLE records in parallel
-        if (tid == 0) {
-          uint32_t pos = cur, n = 0, err = 0;
-          while (pos < seg_end) {
-            if (uint64_t(pos) + 8 > len) { err = kErrTruncated; break; }
-            uint64_t hdr = lds_u64(s_data, pos - win);
-            uint32_t size = uint32_t(hdr >> 48);
-            if (size == 0) { err = kErrZeroSize; break; }  // mem_sampling.c:857-860
-            if (size & 7) { err = kErrUnaligned; break; }  // perf records are 8-byte multiples
-            if (uint32_t(hdr) == kSampleType) {
-              if (uint64_t(pos) + kRecBytes > len || uint64_t(pos) + size > len) {
-                err = kErrTruncated;
-                break;
-              }
-              s_list[n++] = uint16_t(pos - win);
-            }
-            pos += size;  // non-SAMPLE records are skipped by their size (:918)
-          }
-          if (err) {
-            set_error(p, d.seq, pos, err);
-            s_err = 1;
-          }
+        if (lane == 0) {
+          if (err) set_error(p, d.seq, (uint32_t)q0, err);
+          s_err = err;
           s_nlist = n;
-          s_next = pos;
+          s_next = (uint32_t)min(q0, len);
         }
-        __syncthreads();
-        const uint32_t n = s_nlist;
-        for (uint32_t i0 = 0; i0 < n; i0 += kWG) {
-          uint32_t i = i0 + tid;
-          bool valid = i < n;
-          uint64_t ts = 0, addr = 0, w = 0, dsrc = 0;
-          uint32_t o = valid ? s_list[i] : 0;
-          if (valid) {
-            ts = lds_u64(s_data, o + 8);
-            addr = lds_u64(s_data, o + 16);
-            w = lds_u64(s_data, o + 24);
-            dsrc = lds_u64(s_data, o + 32);
-          }
-          process_sample(p, wc, acc, s_fences, valid, ts, addr, w, dsrc, d.access, d.thread_rank, d.seq,
-                         win + o);
-        }
-        cur = s_next;
-        if (s_err) break;  // the reference aborts here; stop this buffer
       }
-      if (++acc_windows == kDrainWindows) {  // keep the per-lane u32 sums bounded
+      __syncthreads();
+      const uint32_t n = s_nlist;
+      ncur = s_err ? len : s_next;  // the reference aborts on an error: stop this buffer
+      const bool valid = (uint32_t)tid < n;
+      const uint32_t off = valid ? s_list[tid] : 0;
+      RawRec rr;
+      load_rec(base, off, valid ? len : 0, rr);
+      if (!(p.flags & kDbgLoadOnly)) {
+        const Rec sr = decode_rec(rr, off);
+        process_sample(p, wc, acc, L, valid, sr.ts, sr.addr, sr.w, sr.dsrc, d.access, d.thread_rank, d.seq, off,
+                       nsamp, nfound);
+      }
+    }
+
+    // ---- issue the next window: this buffer, or the first of the next one
+    uint32_t nidx = idx;
+    BufDesc nd = d;
+    if (ncur >= len) {
+      nidx = idx + 1;
+      ncur = 0;
+      if (nidx < r1) nd = p.bufs[p.order[nidx]];
+    }
+    if (nidx < r1) load_rec(p.data + nd.offset, ncur + uint64_t(tid) * kRecBytes, nd.len, nx);
+
+    if (!(f & 1) && !(p.flags & kDbgLoadOnly)) {
+      const bool valid = (uint32_t)tid < n_cand && uint32_t(r.hdr) == kSampleType;
+      process_sample(p, wc, acc, L, valid, r.ts, r.addr, r.w, r.dsrc, d.access, d.thread_rank, d.seq,
+                     (uint32_t)pos, nsamp, nfound);
+    }
+    if (++acc_windows == kDrainWindows) {  // keep the per-lane u32 sums bounded
+      lane_acc_drain(acc, wc, lane);
+      acc_windows = 0;
+    }
+
+    if (nidx != idx) {
+      // buffer b done: its sample / match tallies (mem_sampling.c:921-926)
+      if (lane == 0) {
+        if (nsamp) atomicAdd(p.bufcnt + b, nsamp);
+        if (nfound) atomicAdd(p.bufcnt + p.nb_bufs + b, nfound);
+      }
+      nsamp = nfound = 0;
+      if (nidx >= r1) break;
+      idx = nidx;
+      b = p.order[idx];
+      d = nd;
+      if (d.access != cur_access || d.thread_rank != cur_thread) {
+        // next stream: publish this one's counters
         lane_acc_drain(acc, wc, lane);
         acc_windows = 0;
+        __syncthreads();
+        flush_sums(p, wc, tid, cur_access);
+        flush_objects(p, wc, tid, cur_access);
+        flush_pages(p, wc, tid, cur_thread);
+        __syncthreads();
+        clear_sums(wc, tid);
+        __syncthreads();
+        cur_access = d.access;
+        cur_thread = d.thread_rank;
       }
-      __syncthreads();  // LDS window is rewritten next iteration
     }
-    __syncthreads();
-
-    if (tid == 0) {
-      atomicAdd(p.bufcnt + b, wc.nb_samples);
-      atomicAdd(p.bufcnt + p.nb_bufs + b, wc.nb_found);
-    }
-    __syncthreads();
+    cur = (uint32_t)ncur;
   }
-  if (cur_access != ~0u) {
-    lane_acc_drain(acc, wc, lane);
-    __syncthreads();
-    flush_state(p, wc, tid, cur_access, cur_thread);
-  }
+  lane_acc_drain(acc, wc, lane);
+  __syncthreads();
+  flush_sums(p, wc, tid, cur_access);
+  flush_objects(p, wc, tid, cur_access);
+  flush_pages(p, wc, tid, cur_thread);
 }
 
 // One launch re-initialises every counter array (INIT_COUNTER semantics:
@@ -1294,6 +1423,7 @@ extern "C" int nmg_analyze(nmg_engine* h) {
   p.nb_threads = h->T;
   p.flags = h->flags;
   p.nb_entries = h->E;
+  p.lds_nodes = h->K <= kLdsNodes;
   p.sparse_mask = (uint32_t)(h->sparse_cap - 1);
   p.hist_cells = h->hist_cells;
   p.sum64 = h->d_sum64;
