@@ -41,7 +41,8 @@ constexpr uint32_t kSampleType = 9;            // PERF_RECORD_SAMPLE
 constexpr uint32_t kRecBytes = 40;             // perf_event_header (8) + struct mem_sample (32)
 constexpr uint32_t kWinBytes = kWG * kRecBytes;  // one 40 B stride slot per lane per window
 constexpr int kMaxFences = 1024;               // LDS fence table (8 KiB)
-constexpr uint32_t kLdsNodes = 1024;           // node records held in LDS when nb_keys <= this
+constexpr uint32_t kLdsNodes = 1023;           // keys held in LDS (Eytzinger tree of <= 10 levels)
+static_assert(kLdsNodes + 1 <= (uint32_t)kMaxFences, "s_fences holds the Eytzinger keys");
 constexpr uint32_t kMaxList = kWG;             // slow path: SAMPLE offsets listed per step
 // per-stream LDS aggregation tables (flushed to global on a stream change or
 // when half full)
@@ -110,7 +111,11 @@ struct Params {
   uint32_t nb_threads;
   uint32_t flags;
   uint32_t nb_entries;
-  uint32_t lds_nodes;    // node records fit in LDS (nb_keys <= kLdsNodes)
+  uint32_t lds_nodes;    // nb_keys <= kLdsNodes: keys + node records in LDS, Eytzinger order
+                         // (arrays of kLdsNodes + 1 = 2^10 slots, index 0 unused)
+  uint32_t elevels;      // levels of the Eytzinger tree (2^elevels - 1 >= nb_keys)
+  const uint64_t* efences;   // [2^elevels] keys in Eytzinger (BFS) order, [0] unused, ~0 padding
+  const DevEntry* enodes;    // [2^elevels] node records in the same order
   uint32_t sparse_mask;  // capacity - 1 (power of two)
   uint64_t hist_cells;   // dense cells per thread: histogram index = thread * hist_cells + cell
   uint64_t* sum64;
@@ -385,11 +390,14 @@ __device__ __forceinline__ Match find_entry(const Params& p, const Lookup& L, ui
   m.baddr = 0;
   m.hist = kHistSparse;
   if (p.lds_nodes) {
-    // nb_keys <= kLdsNodes: the fence table is the key array itself
-    uint32_t idx = 0;
-    for (uint32_t st = p.fence_p2 >> 1; st; st >>= 1) idx = (L.fences[idx + st] <= addr) ? idx + st : idx;
-    idx = min(idx, p.nb_keys - 1);  // ~0 padding: addr == UINT64_MAX
-    if (p.nb_keys == 0 || addr < L.fences[0]) return m;
+    // Eytzinger tree: node i has children 2i, 2i+1; a fixed number of levels,
+    // one LDS read each, branch-free.  The levels above the 7th fit in one
+    // 256 B bank row, so the search is conflict-free where every lane reads.
+    uint32_t i = 1;
+    for (uint32_t l = 0; l < p.elevels; l++) i = 2 * i + (L.fences[i] <= addr ? 1u : 0u);
+    // largest key <= addr = the node of the last right turn (0: none)
+    const uint32_t idx = i >> (__builtin_ctz(i) + 1);
+    if (idx == 0) return m;
     const uint4 a = L.nodes[2 * idx], b = L.nodes[2 * idx + 1];
     const uint2 inf = L.ninfo[idx];
     if (entry_match(a, b, addr, ts)) {
@@ -397,7 +405,7 @@ __device__ __forceinline__ Match find_entry(const Params& p, const Lookup& L, ui
       m.baddr = (uint64_t(a.y) << 32) | a.x;
       m.hist = inf.x == kEmpty32 ? kHistSparse : (uint64_t)inf.x;
     } else if (inf.y >> 31) {
-      match_older(p, inf.y & 0x7fffffffu, p.nodes[idx].count, addr, ts, m);
+      match_older(p, inf.y & 0x7fffffffu, p.enodes[idx].count, addr, ts, m);
     }
     return m;
   }
@@ -662,23 +670,26 @@ __device__ __forceinline__ Rec decode_rec(const RawRec& r, uint64_t pos) {
 // "irregular" bit and the tables' fill level through rotating flag words.
 __global__ __launch_bounds__(kWG, 1) void attribute_kernel(Params p) {
   __shared__ uint64_t s_fences[kMaxFences];
-  __shared__ uint4 s_nodes[2 * kLdsNodes];
-  __shared__ uint2 s_ninfo[kLdsNodes];
+  __shared__ uint4 s_nodes[2 * (kLdsNodes + 1)];  // Eytzinger index 1..kLdsNodes
+  __shared__ uint2 s_ninfo[kLdsNodes + 1];
   __shared__ uint32_t s_list[kMaxList];
   __shared__ WgCounters wc;
   __shared__ uint32_t s_flags[3], s_nlist, s_next, s_err;
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
-  for (uint32_t i = tid; i < p.fence_p2; i += kWG) s_fences[i] = p.fences[i];
   if (p.lds_nodes) {
-    for (uint32_t i = tid; i < p.nb_keys; i += kWG) {
-      const uint4* q = reinterpret_cast<const uint4*>(p.nodes + i);
+    const uint32_t n = 1u << p.elevels;
+    for (uint32_t i = tid; i < n; i += kWG) s_fences[i] = p.efences[i];
+    for (uint32_t i = 1 + tid; i < n; i += kWG) {
+      const uint4* q = reinterpret_cast<const uint4*>(p.enodes + i);
       const uint4 a = q[0], b = q[1], c = q[2], d = q[3];
       s_nodes[2 * i] = a;
       s_nodes[2 * i + 1] = b;
       s_ninfo[i] = make_uint2(c.y == 0 ? c.x : kEmpty32, c.w | (d.x > 1 ? 0x80000000u : 0u));
     }
+  } else {
+    for (uint32_t i = tid; i < p.fence_p2; i += kWG) s_fences[i] = p.fences[i];
   }
   clear_state(wc, tid);
   if (tid < 3) s_flags[tid] = 0;
@@ -888,6 +899,9 @@ struct nmg_engine {
   uint32_t K = 0, E = 0;
   uint64_t* d_keys = nullptr;
   DevEntry* d_nodes = nullptr;
+  uint64_t* d_efences = nullptr;  // small tables: Eytzinger-ordered keys / node records
+  DevEntry* d_enodes = nullptr;
+  uint32_t elevels = 0;
   DevEntry* d_entries = nullptr;
   uint64_t* d_fences = nullptr;
   uint32_t nb_fences = 0, fence_step = 1, fence_p2 = 1;
@@ -995,6 +1009,10 @@ static void free_counters(nmg_engine* h) {
 static void free_table(nmg_engine* h) {
   (void)hipFree(h->d_keys);
   (void)hipFree(h->d_nodes);
+  (void)hipFree(h->d_efences);
+  (void)hipFree(h->d_enodes);
+  h->d_efences = nullptr;
+  h->d_enodes = nullptr;
   (void)hipFree(h->d_entries);
   (void)hipFree(h->d_fences);
   h->d_keys = nullptr;
@@ -1175,6 +1193,39 @@ extern "C" int nmg_set_objects(nmg_engine* h, const uint64_t* keys, const uint32
   };
   HIP_TRY(h, alloc_copy((void**)&h->d_keys, padded_keys.data(), padded_keys.size() * 8));
   HIP_TRY(h, alloc_copy((void**)&h->d_nodes, nodes.data(), (size_t)nb_keys * sizeof(DevEntry)));
+  if (nb_keys <= kLdsNodes) {
+    // Eytzinger (BFS) order for the LDS search: an in-order walk of the
+    // complete tree of 2^L - 1 nodes hands out the keys in sorted order; the
+    // slots after the last key are ~0 keys carrying a copy of the last node
+    // (reached only for addr == UINT64_MAX, where the last key is the answer)
+    h->elevels = 0;
+    while (((1u << h->elevels) - 1) < nb_keys) h->elevels++;
+    const uint32_t n = 1u << h->elevels;
+    std::vector<uint64_t> ef(n, ~0ull);
+    std::vector<DevEntry> en(n);
+    memset(en.data(), 0, n * sizeof(DevEntry));
+    uint32_t r = 0;
+    std::vector<uint32_t> stack;
+    uint32_t i = 1;
+    while (i < n || !stack.empty()) {  // iterative in-order walk
+      while (i < n) {
+        stack.push_back(i);
+        i = 2 * i;
+      }
+      i = stack.back();
+      stack.pop_back();
+      if (r < nb_keys) {
+        ef[i] = keys[r];
+        en[i] = nodes[r];
+      } else if (nb_keys) {
+        en[i] = nodes[nb_keys - 1];
+      }
+      r++;
+      i = 2 * i + 1;
+    }
+    HIP_TRY(h, alloc_copy((void**)&h->d_efences, ef.data(), n * 8));
+    HIP_TRY(h, alloc_copy((void**)&h->d_enodes, en.data(), n * sizeof(DevEntry)));
+  }
   HIP_TRY(h, alloc_copy((void**)&h->d_entries, dev.data(), (size_t)nb_entries * sizeof(DevEntry)));
   HIP_TRY(h, alloc_copy((void**)&h->d_fences, fences.data(), fences.size() * 8));
 
@@ -1424,6 +1475,9 @@ extern "C" int nmg_analyze(nmg_engine* h) {
   p.flags = h->flags;
   p.nb_entries = h->E;
   p.lds_nodes = h->K <= kLdsNodes;
+  p.elevels = h->elevels;
+  p.efences = h->d_efences;
+  p.enodes = h->d_enodes;
   p.sparse_mask = (uint32_t)(h->sparse_cap - 1);
   p.hist_cells = h->hist_cells;
   p.sum64 = h->d_sum64;

@@ -253,3 +253,61 @@ def test_empty_inputs(tmp_path):
     eng2.synchronize()
     g, ns, nf = eng2.global_counters()
     assert ns == rp.nb_records() and nf == 0
+
+
+def _edge_replay(nkeys, seed):
+    """A table of exactly `nkeys` keys (a generated table cut down) and samples
+    at every lookup boundary: each key, key - 1, end - 1, end, the
+    alloc / free dates themselves and one tick outside, address 0 and the
+    top of the address space."""
+    from numamma_amd.replay import Buffer, ObjectTable, Replay
+
+    rp = generate(SynthConfig(nb_samples=1000, nb_intervals=nkeys + 50, reuse_frac=0.2, seed=seed))
+    t = rp.table
+    assert t.nb_keys >= nkeys
+    ne = int(t.entry_off[nkeys])
+    tab = ObjectTable(t.keys[:nkeys].copy(), t.entry_off[:nkeys + 1].copy(), t.entries[:ne].copy(),
+                      t.callstack_pool, t.string_pool)
+    rng = np.random.default_rng(seed)
+    e = tab.entries
+    first = tab.entry_off[:-1]
+    addrs, tss = [], []
+    for k in range(nkeys):
+        x = e[first[k]]
+        a, end = int(x["buffer_addr"]), int(x["buffer_addr"]) + int(x["buffer_size"])
+        al, fr = int(x["alloc_date"]), int(x["free_date"])
+        for ad in (int(tab.keys[k]), int(tab.keys[k]) - 1, a, end - 1, end):
+            for ts in (al, fr, max(al - 1, 0), min(fr + 1, 2**64 - 1), (al + fr) // 2):
+                addrs.append(ad % 2**64)
+                tss.append(ts)
+    for ad in (0, 1, 2**64 - 1, 2**64 - 2, 2**63):
+        for ts in (0, 2**64 - 1, int(e["alloc_date"][0])):
+            addrs.append(ad)
+            tss.append(ts)
+    n = len(addrs)
+    rec = np.zeros(n, dtype=RECORD_DTYPE)
+    rec["type"] = 9
+    rec["size"] = 40
+    rec["timestamp"] = np.array(tss, dtype=np.uint64)
+    rec["addr"] = np.array(addrs, dtype=np.uint64)
+    rec["weight"] = rng.integers(0, 2000, n)
+    rec["data_src"] = (np.uint64(0x42) << np.uint64(5))  # L1 hit
+    perm = rng.permutation(n)
+    rec = rec[perm]
+    bufs = []
+    for s in range(0, n, 1500):
+        raw = np.frombuffer(rec[s:s + 1500].tobytes(), dtype=np.uint8).copy()
+        bufs.append(Buffer(int(rng.integers(0, rp.nb_threads)), int(rng.integers(0, 2)), raw, 0, raw.shape[0]))
+    return Replay(rp.nb_threads, tab, bufs)
+
+
+@pytest.mark.parametrize("nkeys", [1, 2, 1022, 1023, 1024, 1025])
+def test_lookup_boundaries_bit_exact(tmp_path, nkeys):
+    """Both lookup layouts: <= 1023 keys use the LDS Eytzinger tree, larger
+    tables the LDS fences + global key buckets; the crossover is covered on
+    both sides."""
+    d = str(tmp_path)
+    path, odir = _oracle(_edge_replay(nkeys, 100 + nkeys), d)
+    edir = _engine_replay(path, d)
+    _assert_raw_equal(os.path.join(d, "oracle_raw.bin"), os.path.join(d, "engine_raw.bin"))
+    _same_dirs(odir, edir)
