@@ -49,7 +49,9 @@ constexpr uint32_t kMaxList = kWG;             // slow path: SAMPLE offsets list
 constexpr uint32_t kObjSlots = 2048;           // entry -> (count, weight, first ordinal)
 constexpr uint32_t kPageBuckets = 896;         // dense page cell -> count: 8-slot buckets
 constexpr uint32_t kPageSlots = kPageBuckets * 8;  // 7168 cells (56 KiB)
-constexpr uint32_t kObjHigh = kObjSlots / 2;   // at most kWG new keys per window on top
+// fill levels that trigger a flush; it runs after the window that saw them, so
+// up to two windows of new keys (2 x kWG) come on top
+constexpr uint32_t kObjHigh = kObjSlots / 2;
 constexpr uint32_t kPageHigh = kPageSlots / 2;
 constexpr uint32_t kProbes = 32;
 constexpr uint32_t kEmpty32 = 0xffffffffu;
@@ -59,6 +61,9 @@ constexpr uint32_t kDbgLoadOnly = 0x100;   // stage + validate windows, decode n
 constexpr uint32_t kDbgNoGlobal = 0x200;   // skip the global mem_counters update
 constexpr uint32_t kDbgNoFlush = 0x400;    // LDS tables filled but never written to global
 constexpr uint32_t kDbgNoTables = 0x800;   // lookup only: no per-object / per-page accumulation
+constexpr uint32_t kDbgTiming = 0x1000;    // per-wave phase cycle counts (tools/phase_timing.py)
+constexpr int kTimingWords = 24;           // per wave: load+check, barrier, process, rest, total, windows, -, -,
+                                           // then (wave 0) 8 x 2 words of window trace
 
 // PERF_MEM_LVL_* (/usr/include/linux/perf_event.h:1250-1263)
 constexpr uint32_t LVL_NA = 0x01, LVL_HIT = 0x02, LVL_MISS = 0x04;
@@ -72,7 +77,7 @@ struct BufDesc {
   uint32_t len;     // linearised length (< 4 GiB, mem_sampling.c:831-834)
   uint32_t thread_rank;
   uint32_t access;
-  uint32_t pad;
+  uint32_t pad;  // (schedule copy) index of the buffer in submission order
   uint64_t seq;  // analysis-order index (global across shards)
 };
 static_assert(sizeof(BufDesc) == 32, "BufDesc");
@@ -96,9 +101,8 @@ static_assert(sizeof(DevEntry) == 64, "DevEntry");
 
 struct Params {
   const uint8_t* data;
-  const BufDesc* bufs;
-  const uint32_t* order;   // buffers sorted by stream (access, thread_rank)
-  const uint32_t* ranges;  // [gridDim.x + 1]: workgroup w takes order[ranges[w] .. ranges[w+1])
+  const BufDesc* sbufs;    // descriptors in schedule order (sorted by stream; .pad = buffer index)
+  const uint32_t* ranges;  // [gridDim.x + 1]: workgroup w takes sbufs[ranges[w] .. ranges[w+1])
   uint32_t nb_bufs;
   uint32_t nb_keys;
   const uint64_t* keys;      // padded with ~0 to nb_fences * fence_step
@@ -125,6 +129,7 @@ struct Params {
   uint32_t* bufcnt;  // [2][nb_bufs]: samples, found
   uint64_t* sparse_keys;
   uint32_t* sparse_vals;
+  unsigned long long* dbg;  // kDbgTiming: [grid][waves][kTimingWords]
 };
 
 // ---------------------------------------------------------------------------
@@ -425,18 +430,18 @@ __device__ __forceinline__ Match find_entry(const Params& p, const Lookup& L, ui
 }
 
 // Process one decoded record (`valid` = it is a SAMPLE).  Every lane of the
-// wave calls this together (wave-level reductions inside); nsamp / nfound are
-// wave-uniform per-buffer tallies.
+// wave calls this together (wave-level reductions inside); vmask / fmask are
+// the wave's SAMPLE and matched lanes.
 __device__ __forceinline__ void process_sample(Params& p, WgCounters& wc, LaneAcc& acc, const Lookup& L,
                                                bool valid, uint64_t ts, uint64_t addr,
                                                uint64_t w, uint64_t dsrc, uint32_t access,
                                                uint32_t th, uint64_t seq, uint32_t off,
-                                               uint32_t& nsamp, uint32_t& nfound) {
+                                               uint64_t& vmask, uint64_t& fmask) {
   const uint32_t lvl = uint32_t(dsrc >> 5) & 0x3fff;  // data_src.mem_lvl
   // ---- global counters: update_counters(global_counters, ...) (mem_sampling.c:882)
-  const uint64_t vmask = __ballot(valid);
+  vmask = __ballot(valid);
+  fmask = 0;
   if (vmask == 0) return;
-  nsamp += (uint32_t)__popcll(vmask);
   if (valid && !(p.flags & kDbgNoGlobal)) {
     const uint32_t bm = bucket_mask(lvl);
     if (w < kLaneMaxWeight) {  // register accumulation (no LDS traffic)
@@ -482,7 +487,7 @@ __device__ __forceinline__ void process_sample(Params& p, WgCounters& wc, LaneAc
   m.e = -1;
   if (valid) m = find_entry(p, L, addr, ts);
   const int64_t e = m.e;
-  nfound += (uint32_t)__popcll(__ballot(e >= 0));
+  fmask = __ballot(e >= 0);
   if (e < 0 || (p.flags & kDbgNoTables)) return;
   // per-object counters, aggregated per stream in LDS
   const int os = obj_slot(wc, (uint32_t)e);
@@ -668,6 +673,44 @@ __device__ __forceinline__ Rec decode_rec(const RawRec& r, uint64_t pos) {
 // the next window (of this buffer or the next one) is issued before the
 // current one is processed.  One barrier per window: it publishes the window's
 // "irregular" bit and the tables' fill level through rotating flag words.
+// One lane's stride slot in window (cur of d0) [+ head of d1 when d1 is the
+// next buffer of the same stream].
+struct WinLane {
+  uint32_t pos;     // slot offset within its buffer (buffers are < 4 GiB)
+  uint32_t n0, n1;  // slots in d0 / in d1 (uniform)
+  bool in1;         // the slot is in d1
+  bool cand;        // this lane has a slot
+};
+
+__device__ __forceinline__ WinLane win_lane(int tid, uint32_t cur, const BufDesc& d0, const BufDesc& d1, bool has1) {
+  WinLane w;
+  const uint32_t left = d0.len - cur;
+  w.n0 = min(left / kRecBytes + (left % kRecBytes != 0), (uint32_t)kWG);
+  w.n1 = 0;
+  if (has1 && w.n0 < (uint32_t)kWG && d1.access == d0.access && d1.thread_rank == d0.thread_rank)
+    w.n1 = min(d1.len / kRecBytes + (d1.len % kRecBytes != 0), (uint32_t)kWG - w.n0);
+  w.in1 = (uint32_t)tid >= w.n0;
+  w.cand = (uint32_t)tid < w.n0 + w.n1;
+  w.pos = w.in1 ? (uint32_t(tid) - w.n0) * kRecBytes : cur + uint32_t(tid) * kRecBytes;
+  return w;
+}
+
+__device__ __forceinline__ void load_slot(const Params& p, const WinLane& w, const BufDesc& d0, const BufDesc& d1,
+                                          RawRec& r) {
+  const uint64_t off = w.in1 ? d1.offset : d0.offset;
+  const uint32_t len = w.cand ? (w.in1 ? d1.len : d0.len) : 0;
+  load_rec(p.data + off, w.pos, len, r);
+}
+
+// shader-clock stamp that the scheduler does not move work across
+__device__ __forceinline__ uint64_t stamp() {
+  __builtin_amdgcn_sched_barrier(0);
+  const uint64_t t = __builtin_amdgcn_s_memtime();
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+
+template <bool TIMING>
 __global__ __launch_bounds__(kWG, 1) void attribute_kernel(Params p) {
   __shared__ uint64_t s_fences[kMaxFences];
   __shared__ uint4 s_nodes[2 * (kLdsNodes + 1)];  // Eytzinger index 1..kLdsNodes
@@ -696,47 +739,88 @@ __global__ __launch_bounds__(kWG, 1) void attribute_kernel(Params p) {
   __syncthreads();
   const Lookup L{s_fences, s_nodes, s_ninfo};
 
+  // A window is (idx, cur): up to kWG stride slots from byte `cur` of buffer
+  // idx; when that buffer ends inside the window and the next buffer belongs
+  // to the same stream, the remaining lanes take the head of the next buffer
+  // (no partly idle window at every buffer end).
   const uint32_t r0 = p.ranges[blockIdx.x], r1 = p.ranges[blockIdx.x + 1];
   if (r0 >= r1) return;
   uint32_t idx = r0;
-  uint32_t b = p.order[idx];
-  BufDesc d = p.bufs[b];
   uint32_t cur = 0;  // byte cursor, as `cur_cpt` in __analyze_buffer (mem_sampling.c:836)
-  uint32_t cur_access = d.access, cur_thread = d.thread_rank;
+  BufDesc d0 = p.sbufs[idx];
+  BufDesc d1 = idx + 1 < r1 ? p.sbufs[idx + 1] : d0;
+  bool has1 = idx + 1 < r1;
+  uint32_t cur_access = d0.access, cur_thread = d0.thread_rank;
   RawRec nx;
-  load_rec(p.data + d.offset, uint64_t(tid) * kRecBytes, d.len, nx);
+  {
+    const WinLane wl = win_lane(tid, 0, d0, d1, has1);
+    load_slot(p, wl, d0, d1, nx);
+  }
   LaneAcc acc;
   lane_acc_clear(acc);
-  uint32_t win = 0, acc_windows = 0, nsamp = 0, nfound = 0;
+  uint32_t win = 0, acc_windows = 0;
+  uint32_t ns0 = 0, nf0 = 0, ns1 = 0, nf1 = 0;  // per-buffer tallies: buffer idx, idx + 1
+  uint64_t tacc[4] = {0, 0, 0, 0}, t_start = 0, t0 = 0, t1 = 0;
+  if (TIMING) t_start = t0 = stamp();
 
   while (true) {
-    const uint8_t* base = p.data + d.offset;
-    const uint64_t len = d.len;
-    const uint64_t pos = uint64_t(cur) + uint64_t(tid) * kRecBytes;
-    const uint32_t n_cand = uint32_t((min(len - cur, (uint64_t)kWinBytes) + kRecBytes - 1) / kRecBytes);
-    const Rec r = decode_rec(nx, pos);
+    const WinLane wl = win_lane(tid, cur, d0, d1, has1);
+    const Rec r = decode_rec(nx, wl.pos);
     // ---- fast-path check: every 40 B stride slot holds a whole 40 B record
-    const bool bad = (cur & 7) != 0 || ((uint32_t)tid < n_cand && (pos + kRecBytes > len || (r.hdr >> 48) != kRecBytes));
-    if (__ballot(bad) && lane == 0) atomicOr(&s_flags[win % 3], 1u);
+    const uint32_t wlen = wl.in1 ? d1.len : d0.len;
+    const bool bad = (cur & 7) != 0 || (wl.cand && (uint64_t(wl.pos) + kRecBytes > wlen || (r.hdr >> 48) != kRecBytes));
+    const uint64_t badm = __ballot(bad);
+    if (TIMING) {
+      t1 = stamp();
+      tacc[0] += t1 - t0;
+      t0 = t1;
+    }
+    if (badm && lane == 0) atomicOr(&s_flags[win % 3], 1u);
     if (tid == 0 && (wc.nobj > kObjHigh || wc.npage > kPageHigh)) atomicOr(&s_flags[win % 3], 2u);
     __syncthreads();
-    const uint32_t f = s_flags[win % 3];
+    // (LDS broadcasts are made wave-uniform explicitly: the branches below
+    // hold barriers and steer the scalar loop state)
+    const uint32_t f = __builtin_amdgcn_readfirstlane(s_flags[win % 3]);
     if (tid == 0) s_flags[(win + 2) % 3] = 0;  // last read before the previous barrier
     win++;
-    if (f & 2) {  // tables filling up: flush them mid-stream (every insert happened before the barrier)
-      flush_objects(p, wc, tid, cur_access);
-      flush_pages(p, wc, tid, cur_thread);
-      __syncthreads();
+    if (TIMING) {
+      t1 = stamp();
+      tacc[1] += t1 - t0;
+      t0 = t1;
     }
-
+    uint32_t nidx = idx;
     uint64_t ncur;
+    // the record this lane processes in this window
+    Rec rec = r;
+    bool valid;
+    uint64_t rseq;
+    uint32_t roff;
     if (!(f & 1)) {
+      valid = wl.cand && uint32_t(r.hdr) == kSampleType;
+      rseq = wl.in1 ? d1.seq : d0.seq;
+      roff = wl.pos;
       // ---- fast path: one record per lane
-      ncur = cur + uint64_t(n_cand) * kRecBytes;
+      if (wl.n1) {
+        nidx = idx + 1;
+        ncur = uint64_t(wl.n1) * kRecBytes;
+        if (ncur >= d1.len) {
+          nidx = idx + 2;
+          ncur = 0;
+        }
+      } else {
+        ncur = cur + uint64_t(wl.n0) * kRecBytes;
+        if (ncur >= d0.len) {
+          nidx = idx + 1;
+          ncur = 0;
+        }
+      }
     } else {
-      // ---- slow path: wave 0 follows the header chain from global memory,
-      // 64 stride slots per step (a run of regular 40 B records is taken in
-      // one step, an irregular record is handled alone), listing SAMPLE offsets
+      // ---- slow path (buffer idx only): wave 0 follows the header chain from
+      // global memory, 64 stride slots per step (a run of regular 40 B records
+      // is taken in one step, an irregular record is handled alone), listing
+      // SAMPLE offsets; then every lane processes one listed record
+      const uint8_t* base = p.data + d0.offset;
+      const uint64_t len = d0.len;
       if (tid < 64) {
         uint64_t q0 = cur;
         uint32_t n = 0, err = 0;
@@ -767,79 +851,125 @@ __global__ __launch_bounds__(kWG, 1) void attribute_kernel(Params p) {
           q0 += size;  // non-SAMPLE records are skipped by their size (:918)
         }
         if (lane == 0) {
-          if (err) set_error(p, d.seq, (uint32_t)q0, err);
+          if (err) set_error(p, d0.seq, (uint32_t)q0, err);
           s_err = err;
           s_nlist = n;
           s_next = (uint32_t)min(q0, len);
         }
       }
       __syncthreads();
-      const uint32_t n = s_nlist;
-      ncur = s_err ? len : s_next;  // the reference aborts on an error: stop this buffer
-      const bool valid = (uint32_t)tid < n;
-      const uint32_t off = valid ? s_list[tid] : 0;
-      RawRec rr;
-      load_rec(base, off, valid ? len : 0, rr);
-      if (!(p.flags & kDbgLoadOnly)) {
-        const Rec sr = decode_rec(rr, off);
-        process_sample(p, wc, acc, L, valid, sr.ts, sr.addr, sr.w, sr.dsrc, d.access, d.thread_rank, d.seq, off,
-                       nsamp, nfound);
+      const uint32_t n = __builtin_amdgcn_readfirstlane(s_nlist);
+      const uint32_t serr = __builtin_amdgcn_readfirstlane(s_err);
+      ncur = serr ? len : __builtin_amdgcn_readfirstlane(s_next);  // the reference aborts on an error: stop this buffer
+      if (ncur >= len) {
+        nidx = idx + 1;
+        ncur = 0;
       }
+      valid = (uint32_t)tid < n;
+      roff = valid ? s_list[tid] : 0;
+      rseq = d0.seq;
+      RawRec rr;
+      load_rec(base, roff, valid ? len : 0, rr);
+      rec = decode_rec(rr, roff);
     }
 
-    // ---- issue the next window: this buffer, or the first of the next one
-    uint32_t nidx = idx;
-    BufDesc nd = d;
-    if (ncur >= len) {
-      nidx = idx + 1;
-      ncur = 0;
-      if (nidx < r1) nd = p.bufs[p.order[nidx]];
+    // ---- descriptors of the next window, and its loads (issued before this
+    // window's records are processed)
+    BufDesc nd0 = d0, nd1 = d1;
+    if (nidx == idx + 1) {
+      nd0 = d1;
+      if (nidx + 1 < r1) nd1 = p.sbufs[nidx + 1];
+    } else if (nidx == idx + 2) {
+      if (nidx < r1) nd0 = p.sbufs[nidx];
+      if (nidx + 1 < r1) nd1 = p.sbufs[nidx + 1];
     }
-    if (nidx < r1) load_rec(p.data + nd.offset, ncur + uint64_t(tid) * kRecBytes, nd.len, nx);
+    const bool nhas1 = nidx + 1 < r1;
+    if (nidx < r1) {
+      const WinLane nl = win_lane(tid, (uint32_t)ncur, nd0, nd1, nhas1);
+      load_slot(p, nl, nd0, nd1, nx);
+    }
 
-    if (!(f & 1) && !(p.flags & kDbgLoadOnly)) {
-      const bool valid = (uint32_t)tid < n_cand && uint32_t(r.hdr) == kSampleType;
-      process_sample(p, wc, acc, L, valid, r.ts, r.addr, r.w, r.dsrc, d.access, d.thread_rank, d.seq,
-                     (uint32_t)pos, nsamp, nfound);
+    if (TIMING && tid == 0 && win <= 8) {
+      unsigned long long* o = p.dbg + uint64_t(blockIdx.x) * (kWG / 64) * kTimingWords + 8 + 2 * (win - 1);
+      o[0] = (uint64_t(idx) << 40) | cur;
+      o[1] = uint64_t(wl.n0) | (uint64_t(wl.n1) << 11) | (uint64_t(f) << 22) | (uint64_t(nidx) << 24) |
+             (uint64_t((uint32_t)ncur) << 32);
     }
-    if (++acc_windows == kDrainWindows) {  // keep the per-lane u32 sums bounded
+    uint64_t vm = 0, fm = 0;
+    if (!(p.flags & kDbgLoadOnly))
+      process_sample(p, wc, acc, L, valid, rec.ts, rec.addr, rec.w, rec.dsrc, d0.access, d0.thread_rank, rseq, roff,
+                     vm, fm);
+    {
+      // lanes of this wave in buffer idx + 1 (tid >= n0)
+      const uint32_t w0 = uint32_t(tid) & ~63u;
+      const uint64_t m1 = ((f & 1) || wl.n0 >= w0 + 64) ? 0ull : (wl.n0 <= w0 ? ~0ull : (~0ull << (wl.n0 - w0)));
+      ns0 += (uint32_t)__popcll(vm & ~m1);
+      nf0 += (uint32_t)__popcll(fm & ~m1);
+      ns1 += (uint32_t)__popcll(vm & m1);
+      nf1 += (uint32_t)__popcll(fm & m1);
+    }
+    if (TIMING) {
+      t1 = stamp();
+      tacc[2] += t1 - t0;
+      t0 = t1;
+    }
+    // end of the stream run (or of this workgroup's range): publish the
+    // stream's counters; tables over their fill threshold (as of this
+    // window's barrier) are flushed here too -- the single flush site
+    const bool stream_end = nidx != idx && (nidx >= r1 || nd0.access != cur_access || nd0.thread_rank != cur_thread);
+    if (++acc_windows == kDrainWindows || stream_end) {  // keep the per-lane u32 sums bounded
       lane_acc_drain(acc, wc, lane);
       acc_windows = 0;
     }
-
     if (nidx != idx) {
-      // buffer b done: its sample / match tallies (mem_sampling.c:921-926)
+      // buffer idx (and idx + 1 when skipped over) done: sample / match
+      // tallies (mem_sampling.c:921-926)
       if (lane == 0) {
-        if (nsamp) atomicAdd(p.bufcnt + b, nsamp);
-        if (nfound) atomicAdd(p.bufcnt + p.nb_bufs + b, nfound);
+        if (ns0) atomicAdd(p.bufcnt + d0.pad, ns0);
+        if (nf0) atomicAdd(p.bufcnt + p.nb_bufs + d0.pad, nf0);
+        if (nidx == idx + 2) {
+          if (ns1) atomicAdd(p.bufcnt + d1.pad, ns1);
+          if (nf1) atomicAdd(p.bufcnt + p.nb_bufs + d1.pad, nf1);
+        }
       }
-      nsamp = nfound = 0;
-      if (nidx >= r1) break;
-      idx = nidx;
-      b = p.order[idx];
-      d = nd;
-      if (d.access != cur_access || d.thread_rank != cur_thread) {
-        // next stream: publish this one's counters
-        lane_acc_drain(acc, wc, lane);
-        acc_windows = 0;
-        __syncthreads();
-        flush_sums(p, wc, tid, cur_access);
-        flush_objects(p, wc, tid, cur_access);
-        flush_pages(p, wc, tid, cur_thread);
-        __syncthreads();
-        clear_sums(wc, tid);
-        __syncthreads();
-        cur_access = d.access;
-        cur_thread = d.thread_rank;
+      if (nidx == idx + 1) {
+        ns0 = ns1;
+        nf0 = nf1;
+      } else {
+        ns0 = nf0 = 0;
+      }
+      ns1 = nf1 = 0;
+    }
+    if (stream_end || (f & 2)) {
+      __syncthreads();  // every insert and drain of this window is done
+      if (stream_end) flush_sums(p, wc, tid, cur_access);
+      flush_objects(p, wc, tid, cur_access);
+      flush_pages(p, wc, tid, cur_thread);
+      __syncthreads();
+      if (stream_end) {
+        clear_sums(wc, tid);  // (sums are next written after the next window's barrier)
+        cur_access = nd0.access;
+        cur_thread = nd0.thread_rank;
       }
     }
+    idx = nidx;
     cur = (uint32_t)ncur;
+    d0 = nd0;
+    d1 = nd1;
+    has1 = nhas1;
+    if (TIMING) {
+      t1 = stamp();
+      tacc[3] += t1 - t0;
+      t0 = t1;
+    }
+    if (idx >= r1) break;  // the loop's only exit, after the state update
   }
-  lane_acc_drain(acc, wc, lane);
-  __syncthreads();
-  flush_sums(p, wc, tid, cur_access);
-  flush_objects(p, wc, tid, cur_access);
-  flush_pages(p, wc, tid, cur_thread);
+  if (TIMING && lane == 0) {
+    unsigned long long* o = p.dbg + (uint64_t(blockIdx.x) * (kWG / 64) + tid / 64) * kTimingWords;
+    for (int k = 0; k < 4; k++) o[k] = tacc[k];
+    o[4] = stamp() - t_start;
+    o[5] = win;
+  }
 }
 
 // One launch re-initialises every counter array (INIT_COUNTER semantics:
@@ -930,7 +1060,7 @@ struct nmg_engine {
   bool staged_dirty = false;
   BufDesc* d_descs = nullptr;
   size_t descs_cap = 0;
-  uint32_t* d_order = nullptr;   // stream-sorted buffer order
+  BufDesc* d_sdescs = nullptr;   // descriptors in stream-sorted schedule order
   uint32_t* d_ranges = nullptr;  // per-workgroup [begin, end) in d_order
   uint32_t sched_grid = 0;       // grid the current schedule was built for
   bool descs_dirty = false;
@@ -944,6 +1074,10 @@ struct nmg_engine {
 
   std::string last_error;
   float last_ms = 0.f;
+
+  // kDbgTiming (internal): per-wave phase cycles of the last launch
+  uint64_t* d_dbg = nullptr;
+  size_t dbg_cap = 0, dbg_len = 0;
 };
 
 #define HIP_TRY(h, expr)                                                        \
@@ -1066,8 +1200,9 @@ extern "C" void nmg_destroy(nmg_engine* h) {
   (void)hipFree(h->d_arena);
   (void)hipFree(h->d_descs);
   (void)hipFree(h->d_bufcnt);
-  (void)hipFree(h->d_order);
+  (void)hipFree(h->d_sdescs);
   (void)hipFree(h->d_ranges);
+  (void)hipFree(h->d_dbg);
   if (h->h_stage) (void)hipHostFree(h->h_stage);
   if (h->ev0) (void)hipEventDestroy(h->ev0);
   if (h->ev1) (void)hipEventDestroy(h->ev1);
@@ -1425,13 +1560,18 @@ static int build_schedule(nmg_engine* h, uint32_t grid) {
     ranges[w] = std::max(ranges[w - 1], std::min(c, nb));
   }
   ranges[grid] = nb;
-  (void)hipFree(h->d_order);
+  std::vector<BufDesc> sorted(nb);
+  for (uint32_t i = 0; i < nb; i++) {
+    sorted[i] = h->descs[order[i]];
+    sorted[i].pad = order[i];
+  }
+  (void)hipFree(h->d_sdescs);
   (void)hipFree(h->d_ranges);
-  h->d_order = nullptr;
+  h->d_sdescs = nullptr;
   h->d_ranges = nullptr;
-  HIP_TRY(h, hipMalloc(&h->d_order, std::max<size_t>(nb, 1) * 4));
+  HIP_TRY(h, hipMalloc(&h->d_sdescs, std::max<size_t>(nb, 1) * sizeof(BufDesc)));
   HIP_TRY(h, hipMalloc(&h->d_ranges, (grid + 1) * 4));
-  if (nb) HIP_TRY(h, hipMemcpy(h->d_order, order.data(), nb * 4, hipMemcpyHostToDevice));
+  if (nb) HIP_TRY(h, hipMemcpy(h->d_sdescs, sorted.data(), nb * sizeof(BufDesc), hipMemcpyHostToDevice));
   HIP_TRY(h, hipMemcpy(h->d_ranges, ranges.data(), (grid + 1) * 4, hipMemcpyHostToDevice));
   h->sched_grid = grid;
   return NMG_OK;
@@ -1447,7 +1587,7 @@ extern "C" int nmg_analyze(nmg_engine* h) {
   const uint32_t nb = (uint32_t)h->descs.size();
   if (h->blocks_per_cu <= 0) {
     int bpc = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, attribute_kernel, kWG, 0) != hipSuccess || bpc <= 0) bpc = 1;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, attribute_kernel<false>, kWG, 0) != hipSuccess || bpc <= 0) bpc = 1;
     h->blocks_per_cu = bpc;
   }
   // persistent grid: one resident workgroup per slot, each with a byte-balanced range
@@ -1459,8 +1599,7 @@ extern "C" int nmg_analyze(nmg_engine* h) {
   Params p;
   memset(&p, 0, sizeof(p));
   p.data = h->d_data;
-  p.bufs = h->d_descs;
-  p.order = h->d_order;
+  p.sbufs = h->d_sdescs;
   p.ranges = h->d_ranges;
   p.nb_bufs = nb;
   p.nb_keys = h->K;
@@ -1495,7 +1634,21 @@ extern "C" int nmg_analyze(nmg_engine* h) {
   HIP_TRY(h, hipEventRecord(h->ev0, h->stream));
   HIP_TRY(h, hipEventRecord(h->ring0[slot], h->stream));
   if (nb) {
-    hipLaunchKernelGGL(attribute_kernel, dim3(grid), dim3(kWG), 0, h->stream, p);
+    if (h->flags & kDbgTiming) {
+      const size_t n = (size_t)grid * (kWG / 64) * kTimingWords;
+      if (n > h->dbg_cap) {
+        (void)hipFree(h->d_dbg);
+        h->d_dbg = nullptr;
+        HIP_TRY(h, hipMalloc(&h->d_dbg, n * 8));
+        h->dbg_cap = n;
+      }
+      HIP_TRY(h, hipMemsetAsync(h->d_dbg, 0, n * 8, h->stream));
+      h->dbg_len = n;
+      p.dbg = reinterpret_cast<unsigned long long*>(h->d_dbg);
+      hipLaunchKernelGGL(attribute_kernel<true>, dim3(grid), dim3(kWG), 0, h->stream, p);
+    } else {
+      hipLaunchKernelGGL(attribute_kernel<false>, dim3(grid), dim3(kWG), 0, h->stream, p);
+    }
     HIP_TRY(h, hipGetLastError());
   }
   HIP_TRY(h, hipEventRecord(h->ring1[slot], h->stream));
@@ -1895,4 +2048,17 @@ extern "C" int nmg_report(nmg_engine* h, const nmg_object_meta* meta, const nmg_
   rc = write_report(&res, meta, opts, stdout_path, err);
   if (rc && !err.empty()) h->last_error = err;
   return rc;
+}
+
+// Internal (not in include/numamma_gpu.h): per-wave phase cycle counts of the
+// last launch made with flag 0x1000, [grid][16 waves][8] u64:
+// load+check, barrier, process, rest, total, windows.  tools/phase_timing.py.
+extern "C" int nmg_debug_timing(nmg_engine* h, uint64_t* out, size_t n, size_t* len) {
+  if (!h || !len) return NMG_ERR_INVALID;
+  *len = h->dbg_len;
+  if (!out || !h->dbg_len) return NMG_OK;
+  HIP_TRY(h, hipSetDevice(h->device));
+  HIP_TRY(h, hipStreamSynchronize(h->stream));
+  HIP_TRY(h, hipMemcpy(out, h->d_dbg, std::min(n, h->dbg_len) * 8, hipMemcpyDeviceToHost));
+  return NMG_OK;
 }

@@ -44,7 +44,7 @@ for s in $STAGES; do
       find $OUT/prof_$TAG -name "*kernel_stats.csv" -exec cat {} \; | head -20 ;;
     ablate)
       echo "== ablation"
-      timeout -k 10 900 python tools/ablate.py > $OUT/ablate_$TAG.json 2> $OUT/ablate_$TAG.err \
+      timeout -k 10 900 python tools/ablate.py --workloads ${ABLATE_WL:-c2,k100k,k1m} > $OUT/ablate_$TAG.json 2> $OUT/ablate_$TAG.err \
         || { echo "ablate failed"; tail -40 $OUT/ablate_$TAG.err; exit 1; }
       cat $OUT/ablate_$TAG.json ;;
     e2e)
@@ -52,6 +52,11 @@ for s in $STAGES; do
       timeout -k 10 600 python tools/e2e.py c2 > $OUT/e2e_$TAG.json 2> $OUT/e2e_$TAG.err \
         || { echo "e2e failed"; tail -30 $OUT/e2e_$TAG.err; exit 1; }
       cat $OUT/e2e_$TAG.json ;;
+    phases)
+      echo "== phase timing"
+      timeout -k 10 600 python tools/phase_timing.py --workloads ${PHASE_WL:-c2,k100k} > $OUT/phases_$TAG.json 2> $OUT/phases_$TAG.err \
+        || { echo "phase timing failed"; tail -30 $OUT/phases_$TAG.err; exit 1; }
+      cat $OUT/phases_$TAG.json ;;
     bench2g)
       echo "== bench, 2 ranks sharing GPU 0 over gloo (multi-rank code path)"
       timeout -k 10 600 env NMG_BENCH_BACKEND=gloo NMG_BENCH_SAME_GPU=1 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
