@@ -502,7 +502,7 @@ __device__ __forceinline__ void process_sample(Params& p, WgCounters& wc, LaneAc
       atomicAdd(reinterpret_cast<unsigned long long*>(p.sum64 + objcw_index(e, access, 1, p.nb_entries)),
                 (unsigned long long)w);
     unsigned long long* fp = reinterpret_cast<unsigned long long*>(p.min64 + 36 + e);
-    if (ord < *fp) atomicMin(fp, ord);
+    atomicMin(fp, ord);
   }
   if (p.flags & NMG_F_PAGE_HIST) {
     // ma_get_block: page_no = (int)((addr - buffer_addr) / 4096) (mem_analyzer.c:530-531)
@@ -547,7 +547,7 @@ __device__ __forceinline__ void flush_objects(Params& p, WgCounters& wc, int tid
       if (wc.owt[i])
         atomicAdd(reinterpret_cast<unsigned long long*>(p.sum64 + objcw_index(e, a, 1, p.nb_entries)), wc.owt[i]);
       unsigned long long* fp = reinterpret_cast<unsigned long long*>(p.min64 + 36 + e);
-      if (wc.ofirst[i] < *fp) atomicMin(fp, wc.ofirst[i]);
+      atomicMin(fp, wc.ofirst[i]);  // no read first: a returning load would stall the flush
     }
     wc.okey[i] = kEmpty32;
     wc.ocnt[i] = 0;
