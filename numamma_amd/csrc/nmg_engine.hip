@@ -40,9 +40,18 @@ constexpr int kWG = 1024;                      // one workgroup per CU
 constexpr uint32_t kSampleType = 9;            // PERF_RECORD_SAMPLE
 constexpr uint32_t kRecBytes = 40;             // perf_event_header (8) + struct mem_sample (32)
 constexpr uint32_t kWinBytes = kWG * kRecBytes;  // one 40 B stride slot per lane per window
-constexpr int kMaxFences = 1024;               // LDS fence table (8 KiB)
-constexpr uint32_t kLdsNodes = 1023;           // keys held in LDS (Eytzinger tree of <= 10 levels)
-static_assert(kLdsNodes + 1 <= (uint32_t)kMaxFences, "s_fences holds the Eytzinger keys");
+constexpr uint32_t kLdsNodes = 1023;           // keys held in LDS with their node records (<= 10 levels)
+// Larger tables: up to 4095 fences (every S-th key) in a 12-level Eytzinger
+// tree in LDS, then one load from a per-fence-bucket directory in global memory
+constexpr uint32_t kFenceLevels = 12;
+constexpr uint32_t kMaxFences = (1u << kFenceLevels) - 1;
+constexpr uint32_t kShiftSearch = 0xff;        // bucket without a directory: binary search of its keys
+// One LDS region holds the lookup structure of either mode:
+//   <= kLdsNodes keys: Eytzinger keys (8 KiB) | node records (32 KiB) | node info (8 KiB)
+//   larger tables:     Eytzinger fences (32 KiB) | per-bucket directory shift (4 KiB)
+constexpr uint32_t kTabBytes = 48 * 1024;
+static_assert((kLdsNodes + 1) * (8 + 32 + 8) <= kTabBytes, "small-table LDS layout");
+static_assert((kMaxFences + 1) * (8 + 1) <= kTabBytes, "fence LDS layout");
 constexpr uint32_t kMaxList = kWG;             // slow path: SAMPLE offsets listed per step
 // per-stream LDS aggregation tables (flushed to global on a stream change or
 // when half full)
@@ -105,13 +114,16 @@ struct Params {
   const uint32_t* ranges;  // [gridDim.x + 1]: workgroup w takes sbufs[ranges[w] .. ranges[w+1])
   uint32_t nb_bufs;
   uint32_t nb_keys;
-  const uint64_t* keys;      // padded with ~0 to nb_fences * fence_step
+  const uint64_t* keys;      // [nb_keys] sorted unique keys
   const DevEntry* nodes;     // [nb_keys] node records
   const DevEntry* entries;
-  const uint64_t* fences;    // padded with ~0 to fence_p2
+  // large tables (nb_keys > kLdsNodes): fence b = keys[b * fence_step]
+  const uint64_t* ffences;   // [2^kFenceLevels] fences in Eytzinger order, [0] unused, ~0 padding
+  const uint8_t* fshift;     // [nb_fences] slot width log2 of bucket b's directory, or kShiftSearch
+  const uint2* dir;          // [nb_fences << dir_log2] {lo | cnt << 16, offset of the slot's first key}
   uint32_t nb_fences;
-  uint32_t fence_p2;         // power of two >= nb_fences
-  uint32_t fence_step;       // power of two
+  uint32_t fence_log2;       // fence_step = 2^fence_log2 keys per bucket
+  uint32_t dir_log2;         // directory slots per bucket = 2^dir_log2 (0: fence_step == 1, no directory)
   uint32_t nb_threads;
   uint32_t flags;
   uint32_t nb_entries;
@@ -183,20 +195,56 @@ __device__ __forceinline__ void set_error(Params& p, uint64_t seq, uint32_t off,
             (unsigned long long)w);
 }
 
-// Largest key <= addr (ht_lower_key, tools/hash.c:63-77): fence table in LDS,
-// then binary search of the fence's key bucket in global memory.
-// Largest key <= addr (ht_lower_key, tools/hash.c:63-77).  Both levels are
-// branch-free, fixed-trip-count binary searches (every lane runs the same
-// steps, no divergence): the LDS fence table, then the fence's key bucket in
-// global memory (L2/MALL resident).  Returns nb_keys when no key <= addr.
-__device__ __forceinline__ uint32_t lower_key(const Params& p, const uint64_t* s_fences, uint64_t addr) {
-  uint32_t idx = 0;
-  for (uint32_t st = p.fence_p2 >> 1; st; st >>= 1) idx = (s_fences[idx + st] <= addr) ? idx + st : idx;
-  idx = min(idx, p.nb_fences - 1);  // ~0 padding: addr == UINT64_MAX
-  uint32_t k = idx * p.fence_step;
-  for (uint32_t st = p.fence_step >> 1; st; st >>= 1) k = (p.keys[k + st] <= addr) ? k + st : k;
-  k = min(k, p.nb_keys - 1);
-  return (p.nb_keys == 0 || addr < s_fences[0]) ? p.nb_keys : k;
+// Largest key <= addr (ht_lower_key, tools/hash.c:63-77) for tables larger
+// than kLdsNodes.  Returns nb_keys when no key <= addr.
+//  1. LDS: branch-free search of the 12-level Eytzinger fence tree -> bucket b
+//     (keys [b*S, (b+1)*S), S = fence_step);
+//  2. global: one 8 B directory slot of bucket b.  The bucket's key span is
+//     cut into 2^dir_log2 equal slots of 2^shift bytes; a slot holds the
+//     bucket-relative index of the largest key <= the slot start, the number
+//     of keys strictly inside the slot and the offset of the first of them.
+//     Zero or one key inside the slot is resolved by that one load;
+//  3. more keys inside the slot (or a bucket too wide for a directory): a
+//     binary search of those keys in global memory (L2 / MALL resident).
+__device__ __forceinline__ uint32_t lower_key(const Params& p, const uint64_t* s_fences, const uint8_t* s_shift,
+                                              uint64_t addr) {
+  uint32_t i = 1;
+#pragma unroll
+  for (uint32_t l = 0; l < kFenceLevels; l++) i = 2 * i + (s_fences[i] <= addr ? 1u : 0u);
+  const uint32_t idx = i >> (__builtin_ctz(i) + 1);  // node of the last right turn
+  if (idx == 0) return p.nb_keys;                    // addr < first key
+  // in-order rank of Eytzinger node idx at depth d of a complete tree
+  const uint32_t d = 31 - __builtin_clz(idx);
+  const uint32_t b = (((idx - (1u << d)) * 2 + 1) << (kFenceLevels - 1 - d)) - 1;
+  if (b >= p.nb_fences) return p.nb_keys - 1;  // ~0 padding: addr == UINT64_MAX
+  const uint32_t k0 = b << p.fence_log2;
+  if (p.dir_log2 == 0) return k0;  // one key per fence
+  const uint32_t kend = min(k0 + (1u << p.fence_log2), p.nb_keys);
+  const uint32_t sh = s_shift[b];
+  uint32_t lo, n;  // answer in [lo, lo + n): keys[lo] <= addr known
+  if (sh != kShiftSearch) {
+    const uint64_t f = s_fences[idx];
+    const uint32_t slots = 1u << p.dir_log2;
+    const uint64_t rel = addr - f;
+    const uint32_t j = (uint32_t)min(rel >> sh, (uint64_t)(slots - 1));
+    const uint2 de = p.dir[(uint64_t(b) << p.dir_log2) + j];
+    lo = k0 + (de.x & 0xffffu);
+    const uint32_t cnt = de.x >> 16;
+    // first key inside the slot is <= addr: the answer is among the cnt keys
+    if (cnt == 0 || rel - (uint64_t(j) << sh) < de.y) return lo;
+    lo += 1;
+    n = cnt;
+  } else {
+    lo = k0;
+    n = kend - k0;
+  }
+  while (n > 1) {  // keys[lo] <= addr < keys[lo + n] (or lo + n == bucket end)
+    const uint32_t half = n >> 1;
+    const bool le = p.keys[lo + half] <= addr;
+    lo = le ? lo + half : lo;
+    n = le ? n - half : half;
+  }
+  return lo;
 }
 
 // __ma_find_mem_info_from_sample_generic (mem_analyzer.c:249-286) with
@@ -360,9 +408,10 @@ __device__ __forceinline__ void lane_acc_drain(LaneAcc& a, WgCounters& wc, int l
 // The object table as the kernel sees it: node records in LDS (small tables)
 // or in global memory (L2/MALL resident) behind the LDS fence table.
 struct Lookup {
-  const uint64_t* fences;  // LDS
-  const uint4* nodes;      // LDS: 2 x uint4 per node: (addr, end), (alloc, free)
-  const uint2* ninfo;      // LDS: (dense histogram base or ~0, entry id | older-entries << 31)
+  const uint64_t* fences;  // LDS: Eytzinger keys (small tables) or fences (large tables)
+  const uint4* nodes;      // LDS (small tables): 2 x uint4 per node: (addr, end), (alloc, free)
+  const uint2* ninfo;      // LDS (small tables): (dense histogram base or ~0, entry id | older-entries << 31)
+  const uint8_t* shift;    // LDS (large tables): per-bucket directory shift
 };
 
 struct Match {
@@ -414,7 +463,7 @@ __device__ __forceinline__ Match find_entry(const Params& p, const Lookup& L, ui
     }
     return m;
   }
-  const uint32_t k = lower_key(p, L.fences, addr);
+  const uint32_t k = lower_key(p, L.fences, L.shift, addr);
   if (k >= p.nb_keys) return m;
   const uint4* q = reinterpret_cast<const uint4*>(p.nodes + k);
   const uint4 a = q[0], b = q[1], c = q[2];
@@ -712,15 +761,17 @@ __device__ __forceinline__ uint64_t stamp() {
 
 template <bool TIMING>
 __global__ __launch_bounds__(kWG, 1) void attribute_kernel(Params p) {
-  __shared__ uint64_t s_fences[kMaxFences];
-  __shared__ uint4 s_nodes[2 * (kLdsNodes + 1)];  // Eytzinger index 1..kLdsNodes
-  __shared__ uint2 s_ninfo[kLdsNodes + 1];
+  __shared__ uint4 s_tab[kTabBytes / 16];  // lookup structure (layouts at kTabBytes)
   __shared__ uint32_t s_list[kMaxList];
   __shared__ WgCounters wc;
   __shared__ uint32_t s_flags[3], s_nlist, s_next, s_err;
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
+  uint64_t* const s_fences = reinterpret_cast<uint64_t*>(s_tab);
+  uint4* const s_nodes = s_tab + (kLdsNodes + 1) / 2;                    // after 8 KiB of keys
+  uint2* const s_ninfo = reinterpret_cast<uint2*>(s_tab + (kLdsNodes + 1) * 5 / 2);  // after 40 KiB
+  uint8_t* const s_shift = reinterpret_cast<uint8_t*>(s_tab + (kMaxFences + 1) / 2);  // after 32 KiB
   if (p.lds_nodes) {
     const uint32_t n = 1u << p.elevels;
     for (uint32_t i = tid; i < n; i += kWG) s_fences[i] = p.efences[i];
@@ -731,13 +782,14 @@ __global__ __launch_bounds__(kWG, 1) void attribute_kernel(Params p) {
       s_nodes[2 * i + 1] = b;
       s_ninfo[i] = make_uint2(c.y == 0 ? c.x : kEmpty32, c.w | (d.x > 1 ? 0x80000000u : 0u));
     }
-  } else {
-    for (uint32_t i = tid; i < p.fence_p2; i += kWG) s_fences[i] = p.fences[i];
+  } else if (p.nb_keys) {
+    for (uint32_t i = tid; i <= kMaxFences; i += kWG) s_fences[i] = p.ffences[i];
+    for (uint32_t i = tid; i < p.nb_fences; i += kWG) s_shift[i] = p.fshift[i];
   }
   clear_state(wc, tid);
   if (tid < 3) s_flags[tid] = 0;
   __syncthreads();
-  const Lookup L{s_fences, s_nodes, s_ninfo};
+  const Lookup L{s_fences, s_nodes, s_ninfo, s_shift};
 
   // A window is (idx, cur): up to kWG stride slots from byte `cur` of buffer
   // idx; when that buffer ends inside the window and the next buffer belongs
@@ -1033,8 +1085,10 @@ struct nmg_engine {
   DevEntry* d_enodes = nullptr;
   uint32_t elevels = 0;
   DevEntry* d_entries = nullptr;
-  uint64_t* d_fences = nullptr;
-  uint32_t nb_fences = 0, fence_step = 1, fence_p2 = 1;
+  uint64_t* d_ffences = nullptr;  // large tables: Eytzinger fences, directory shifts, directory
+  uint8_t* d_fshift = nullptr;
+  uint2* d_dir = nullptr;
+  uint32_t nb_fences = 0, fence_log2 = 0, dir_log2 = 0;
   std::vector<uint64_t> hist_base, npages, buffer_size;
   std::vector<uint32_t> sparse_entries;
   uint64_t hist_cells = 0;
@@ -1148,11 +1202,15 @@ static void free_table(nmg_engine* h) {
   h->d_efences = nullptr;
   h->d_enodes = nullptr;
   (void)hipFree(h->d_entries);
-  (void)hipFree(h->d_fences);
+  (void)hipFree(h->d_ffences);
+  (void)hipFree(h->d_fshift);
+  (void)hipFree(h->d_dir);
   h->d_keys = nullptr;
   h->d_nodes = nullptr;
   h->d_entries = nullptr;
-  h->d_fences = nullptr;
+  h->d_ffences = nullptr;
+  h->d_fshift = nullptr;
+  h->d_dir = nullptr;
 }
 
 extern "C" int nmg_create(nmg_engine** out, const nmg_options* opt) {
@@ -1245,6 +1303,65 @@ extern "C" int nmg_reset_counters(nmg_engine* h) {
   return NMG_OK;
 }
 
+// Lookup structure of a table larger than kLdsNodes keys (see lower_key):
+// fence b = keys[b << fence_log2] (<= kMaxFences fences, Eytzinger order),
+// and per bucket a directory of 2^dir_log2 equal-width slots over the bucket's
+// key span [first key, last key].
+struct BigLookup {
+  uint32_t nb_fences = 0, fence_log2 = 0, dir_log2 = 0;
+  std::vector<uint64_t> efences;  // [kMaxFences + 1]
+  std::vector<uint8_t> shift;     // [nb_fences]
+  std::vector<uint2> dir;         // [nb_fences << dir_log2]
+};
+
+static void build_big_lookup(const uint64_t* keys, uint32_t K, BigLookup& bl) {
+  while (((uint64_t)K + (1u << bl.fence_log2) - 1) >> bl.fence_log2 > kMaxFences) bl.fence_log2++;
+  const uint32_t S = 1u << bl.fence_log2;
+  bl.nb_fences = (uint32_t)(((uint64_t)K + S - 1) >> bl.fence_log2);
+  // Eytzinger order: an in-order walk of the complete 12-level tree hands out
+  // the fences in sorted order; the slots after the last fence hold ~0
+  bl.efences.assign(kMaxFences + 1, ~0ull);
+  {
+    uint32_t r = 0, i = 1;
+    std::vector<uint32_t> stack;
+    while (i <= kMaxFences || !stack.empty()) {
+      while (i <= kMaxFences) {
+        stack.push_back(i);
+        i = 2 * i;
+      }
+      i = stack.back();
+      stack.pop_back();
+      if (r < bl.nb_fences) bl.efences[i] = keys[(uint64_t)r << bl.fence_log2];
+      r++;
+      i = 2 * i + 1;
+    }
+  }
+  bl.shift.assign(bl.nb_fences, kShiftSearch);
+  // bucket-relative indices and counts are 16-bit: S <= 2^16
+  if (S == 1 || S > (1u << 16)) return;
+  bl.dir_log2 = bl.fence_log2 + 1;  // two slots per key
+  const uint32_t D = 1u << bl.dir_log2;
+  bl.dir.assign((size_t)bl.nb_fences << bl.dir_log2, make_uint2(0, 0));
+  for (uint32_t b = 0; b < bl.nb_fences; b++) {
+    const uint32_t k0 = b * S, k1 = std::min<uint64_t>((uint64_t)k0 + S, K);
+    const uint64_t f = keys[k0], span = keys[k1 - 1] - f;
+    uint32_t sh = 0;
+    while (sh < 64 && (span >> sh) >= D) sh++;
+    if (sh > 32) continue;  // slot offsets must fit 32 bits: binary search instead
+    bl.shift[b] = (uint8_t)sh;
+    uint2* dd = &bl.dir[(size_t)b << bl.dir_log2];
+    uint32_t k = k0;  // largest key <= slot start
+    for (uint32_t j = 0; j < D; j++) {
+      const uint64_t s0 = (uint64_t)j << sh;  // slot [s0, s0 + 2^sh) relative to f; the last slot is open
+      while (k + 1 < k1 && keys[k + 1] - f <= s0) k++;
+      uint32_t c = 0;
+      while (k + 1 + c < k1 && (j == D - 1 || keys[k + 1 + c] - f < s0 + (1ull << sh))) c++;
+      dd[j].x = (k - k0) | (std::min<uint32_t>(c, 0xffffu) << 16);
+      dd[j].y = c ? (uint32_t)(keys[k + 1] - f - s0) : 0u;
+    }
+  }
+}
+
 extern "C" int nmg_set_objects(nmg_engine* h, const uint64_t* keys, const uint32_t* entry_off,
                                uint32_t nb_keys, const nmg_object* entries, uint32_t nb_entries) {
   if (!h || (nb_keys && (!keys || !entry_off)) || (nb_entries && !entries))
@@ -1301,18 +1418,6 @@ extern "C" int nmg_set_objects(nmg_engine* h, const uint64_t* keys, const uint32
       h->sparse_entries.push_back(e);
     }
   }
-  // LDS fence table: every fence_step-th key (fence_step a power of two), padded
-  // with ~0 to a power of two; the key array is padded to nb_fences * fence_step
-  h->fence_step = 1;
-  while ((uint64_t)nb_keys > (uint64_t)h->fence_step * kMaxFences) h->fence_step <<= 1;
-  h->nb_fences = nb_keys ? (nb_keys + h->fence_step - 1) / h->fence_step : 1;
-  h->fence_p2 = 1;
-  while (h->fence_p2 < h->nb_fences) h->fence_p2 <<= 1;
-  std::vector<uint64_t> fences(h->fence_p2, ~0ull);
-  for (uint32_t f = 0; f < h->nb_fences && (uint64_t)f * h->fence_step < nb_keys; f++)
-    fences[f] = keys[(uint64_t)f * h->fence_step];
-  std::vector<uint64_t> padded_keys((uint64_t)h->nb_fences * h->fence_step, ~0ull);
-  if (nb_keys) memcpy(padded_keys.data(), keys, (size_t)nb_keys * 8);
   std::vector<DevEntry> nodes(nb_keys);
   for (uint32_t k = 0; k < nb_keys; k++) {
     nodes[k] = dev[entry_off[k]];
@@ -1326,7 +1431,7 @@ extern "C" int nmg_set_objects(nmg_engine* h, const uint64_t* keys, const uint32
     if (bytes) return hipMemcpyAsync(*dptr, src, bytes, hipMemcpyHostToDevice, h->stream);
     return hipSuccess;
   };
-  HIP_TRY(h, alloc_copy((void**)&h->d_keys, padded_keys.data(), padded_keys.size() * 8));
+  HIP_TRY(h, alloc_copy((void**)&h->d_keys, keys, (size_t)nb_keys * 8));
   HIP_TRY(h, alloc_copy((void**)&h->d_nodes, nodes.data(), (size_t)nb_keys * sizeof(DevEntry)));
   if (nb_keys <= kLdsNodes) {
     // Eytzinger (BFS) order for the LDS search: an in-order walk of the
@@ -1361,8 +1466,18 @@ extern "C" int nmg_set_objects(nmg_engine* h, const uint64_t* keys, const uint32
     HIP_TRY(h, alloc_copy((void**)&h->d_efences, ef.data(), n * 8));
     HIP_TRY(h, alloc_copy((void**)&h->d_enodes, en.data(), n * sizeof(DevEntry)));
   }
+  h->nb_fences = h->fence_log2 = h->dir_log2 = 0;
+  if (nb_keys > kLdsNodes) {
+    BigLookup bl;
+    build_big_lookup(keys, nb_keys, bl);
+    h->nb_fences = bl.nb_fences;
+    h->fence_log2 = bl.fence_log2;
+    h->dir_log2 = bl.dir_log2;
+    HIP_TRY(h, alloc_copy((void**)&h->d_ffences, bl.efences.data(), bl.efences.size() * 8));
+    HIP_TRY(h, alloc_copy((void**)&h->d_fshift, bl.shift.data(), bl.shift.size()));
+    HIP_TRY(h, alloc_copy((void**)&h->d_dir, bl.dir.data(), bl.dir.size() * sizeof(uint2)));
+  }
   HIP_TRY(h, alloc_copy((void**)&h->d_entries, dev.data(), (size_t)nb_entries * sizeof(DevEntry)));
-  HIP_TRY(h, alloc_copy((void**)&h->d_fences, fences.data(), fences.size() * 8));
 
   h->n_sum64 = 2 * kGlobalSums + (uint64_t)nb_entries * 4;
   if (h->flags & NMG_F_OBJECT_LEVELS) h->n_sum64 += (uint64_t)nb_entries * 2 * kLevelWords;
@@ -1606,10 +1721,12 @@ extern "C" int nmg_analyze(nmg_engine* h) {
   p.keys = h->d_keys;
   p.nodes = h->d_nodes;
   p.entries = h->d_entries;
-  p.fences = h->d_fences;
+  p.ffences = h->d_ffences;
+  p.fshift = h->d_fshift;
+  p.dir = h->d_dir;
   p.nb_fences = h->nb_fences;
-  p.fence_p2 = h->fence_p2;
-  p.fence_step = h->fence_step;
+  p.fence_log2 = h->fence_log2;
+  p.dir_log2 = h->dir_log2;
   p.nb_threads = h->T;
   p.flags = h->flags;
   p.nb_entries = h->E;

@@ -60,6 +60,9 @@ CONFIGS = [
                 buffer_records=97, seed=4),
     SynthConfig(nb_samples=30_000, nb_intervals=1, nb_globals=0, with_stack=False, buffer_records=10_000, seed=5),
     SynthConfig(nb_samples=60_000, nb_intervals=200_000, size_min=8, size_max=512, seed=6),
+    # 1M intervals (configs[3]'s table): fences + per-bucket directory lookup.
+    # Few call sites: the reference's site list and sort are quadratic (the oracle keeps that cost)
+    SynthConfig(nb_samples=300_000, nb_intervals=1_000_000, size_max=64 * 1024, site_ratio=0.002, seed=12),
 ]
 
 
@@ -255,11 +258,13 @@ def test_empty_inputs(tmp_path):
     assert ns == rp.nb_records() and nf == 0
 
 
-def _edge_replay(nkeys, seed):
+def _edge_replay(nkeys, seed, cluster=0):
     """A table of exactly `nkeys` keys (a generated table cut down) and samples
     at every lookup boundary: each key, key - 1, end - 1, end, the
     alloc / free dates themselves and one tick outside, address 0 and the
-    top of the address space."""
+    top of the address space.  `cluster` > 0 moves every run of `cluster`
+    consecutive keys (with their objects) 2^40 bytes further up than the
+    previous run: buckets spanning a huge gap, many keys per directory slot."""
     from numamma_amd.replay import Buffer, ObjectTable, Replay
 
     rp = generate(SynthConfig(nb_samples=1000, nb_intervals=nkeys + 50, reuse_frac=0.2, seed=seed))
@@ -268,6 +273,11 @@ def _edge_replay(nkeys, seed):
     ne = int(t.entry_off[nkeys])
     tab = ObjectTable(t.keys[:nkeys].copy(), t.entry_off[:nkeys + 1].copy(), t.entries[:ne].copy(),
                       t.callstack_pool, t.string_pool)
+    if cluster:
+        shift = (np.arange(nkeys, dtype=np.uint64) // np.uint64(cluster)) << np.uint64(40)
+        tab.keys += shift
+        per_entry = np.repeat(shift, np.diff(tab.entry_off).astype(np.int64))
+        tab.entries["buffer_addr"] += per_entry
     rng = np.random.default_rng(seed)
     e = tab.entries
     first = tab.entry_off[:-1]
@@ -301,13 +311,17 @@ def _edge_replay(nkeys, seed):
     return Replay(rp.nb_threads, tab, bufs)
 
 
-@pytest.mark.parametrize("nkeys", [1, 2, 1022, 1023, 1024, 1025])
-def test_lookup_boundaries_bit_exact(tmp_path, nkeys):
-    """Both lookup layouts: <= 1023 keys use the LDS Eytzinger tree, larger
-    tables the LDS fences + global key buckets; the crossover is covered on
-    both sides."""
+@pytest.mark.parametrize("nkeys,cluster", [(1, 0), (2, 0), (1022, 0), (1023, 0), (1024, 0), (1025, 0),
+                                          (4095, 0), (4096, 0), (8191, 0), (40_000, 0),
+                                          (20_000, 300), (20_000, 7)])
+def test_lookup_boundaries_bit_exact(tmp_path, nkeys, cluster):
+    """Every lookup layout: <= 1023 keys use the LDS Eytzinger tree with node
+    records; up to 4095 keys are all fences; larger tables add the per-bucket
+    directory (1 to 2^16 keys per bucket), whose slots can hold many keys or
+    be skipped for a binary search when a bucket spans a huge gap (`cluster`).
+    Each crossover is covered on both sides."""
     d = str(tmp_path)
-    path, odir = _oracle(_edge_replay(nkeys, 100 + nkeys), d)
+    path, odir = _oracle(_edge_replay(nkeys, 100 + nkeys, cluster), d)
     edir = _engine_replay(path, d)
     _assert_raw_equal(os.path.join(d, "oracle_raw.bin"), os.path.join(d, "engine_raw.bin"))
     _same_dirs(odir, edir)
