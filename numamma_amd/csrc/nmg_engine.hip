@@ -63,6 +63,16 @@ constexpr uint32_t kPageSlots = kPageBuckets * 8;  // 7168 cells (56 KiB)
 constexpr uint32_t kObjHigh = kObjSlots / 2;
 constexpr uint32_t kPageHigh = kPageSlots / 2;
 constexpr uint32_t kProbes = 32;
+// Dense modes (template flags of attribute_kernel):
+//   kModeDenseObj:  nb_entries <= kObjSlots: slot = entry id, no key check;
+//   kModeDensePage: dense histogram cells per thread <= kDensePageCells: u16
+//                   counts, two per LDS word, flushed at least every
+//                   kDensePageWindows windows (<= 1024 samples per cell each,
+//                   so a u16 cannot overflow into its neighbour)
+constexpr int kModeDenseObj = 1, kModeDensePage = 2;
+constexpr uint32_t kDensePageCells = kPageSlots * 4;  // the page table's 56 KiB as u16 cells
+constexpr uint32_t kDensePageWindows = 62;
+static_assert(kDensePageWindows * kWG < 65536u, "u16 page counts");
 constexpr uint32_t kEmpty32 = 0xffffffffu;
 constexpr uint64_t kEmpty64 = ~0ull;
 // internal ablation switches (tools/ablate.py only; not part of the C-ABI)
@@ -281,8 +291,13 @@ struct WgCounters {
   unsigned int ocnt[kObjSlots];
   unsigned long long ofirst[kObjSlots];  // smallest (seq << 32 | offset): first match
   unsigned long long owt[kObjSlots];
-  uint4 pkey4[kPageSlots / 4];           // dense cell index (hist_base(entry) + page), 8 per bucket
-  unsigned int pcnt[kPageSlots];
+  union {
+    struct {
+      uint4 pkey4[kPageSlots / 4];  // dense cell index (hist_base(entry) + page), 8 per bucket
+      unsigned int pcnt[kPageSlots];
+    };
+    unsigned int pdense[kDensePageCells / 2];  // kModeDensePage: u16 count per cell, two per word
+  };
   unsigned int nobj, npage;              // occupied slots
 };
 
@@ -481,6 +496,7 @@ __device__ __forceinline__ Match find_entry(const Params& p, const Lookup& L, ui
 // Process one decoded record (`valid` = it is a SAMPLE).  Every lane of the
 // wave calls this together (wave-level reductions inside); vmask / fmask are
 // the wave's SAMPLE and matched lanes.
+template <int MODE>
 __device__ __forceinline__ void process_sample(Params& p, WgCounters& wc, LaneAcc& acc, const Lookup& L,
                                                bool valid, uint64_t ts, uint64_t addr,
                                                uint64_t w, uint64_t dsrc, uint32_t access,
@@ -539,7 +555,7 @@ __device__ __forceinline__ void process_sample(Params& p, WgCounters& wc, LaneAc
   fmask = __ballot(e >= 0);
   if (e < 0 || (p.flags & kDbgNoTables)) return;
   // per-object counters, aggregated per stream in LDS
-  const int os = obj_slot(wc, (uint32_t)e);
+  const int os = (MODE & kModeDenseObj) ? (int)e : obj_slot(wc, (uint32_t)e);
   const unsigned long long ord = (seq << 32) | off;  // first match in analysis order (quirk Q7)
   if (os >= 0) {
     atomicAdd(&wc.ocnt[os], 1u);
@@ -558,9 +574,13 @@ __device__ __forceinline__ void process_sample(Params& p, WgCounters& wc, LaneAc
     const uint32_t page = uint32_t(int(uint64_t(addr - m.baddr) / kPageSize));
     if (m.hist != kHistSparse) {
       const uint32_t cell = uint32_t(m.hist + page);
-      const int ps = page_slot(wc, cell);
-      if (ps >= 0) atomicAdd(&wc.pcnt[ps], 1u);
-      else atomicAdd(p.hist + uint64_t(th) * p.hist_cells + cell, 1u);
+      if (MODE & kModeDensePage) {
+        atomicAdd(&wc.pdense[cell >> 1], 1u << (16 * (cell & 1)));
+      } else {
+        const int ps = page_slot(wc, cell);
+        if (ps >= 0) atomicAdd(&wc.pcnt[ps], 1u);
+        else atomicAdd(p.hist + uint64_t(th) * p.hist_cells + cell, 1u);
+      }
     } else {
       const uint32_t sidx = p.entries[e].sidx;
       if (sidx != ~0u)  // huge objects ([stack]): hashed cells in global memory
@@ -585,11 +605,13 @@ __device__ __forceinline__ void process_sample(Params& p, WgCounters& wc, LaneAc
 // per-workgroup aggregation state: flush to global memory and clear, slot by
 // slot (each thread owns the slots it flushes; callers fence with barriers)
 
+template <int MODE>
 __device__ __forceinline__ void flush_objects(Params& p, WgCounters& wc, int tid, uint32_t a) {
   const bool write = !(p.flags & kDbgNoFlush);
-  for (int i = tid; i < (int)kObjSlots; i += kWG) {
-    const uint32_t e = wc.okey[i];
-    if (e == kEmpty32) continue;
+  const int n = (MODE & kModeDenseObj) ? (int)p.nb_entries : (int)kObjSlots;
+  for (int i = tid; i < n; i += kWG) {
+    const uint32_t e = (MODE & kModeDenseObj) ? (uint32_t)i : wc.okey[i];
+    if ((MODE & kModeDenseObj) ? wc.ocnt[i] == 0 : e == kEmpty32) continue;
     if (write) {
       atomicAdd(reinterpret_cast<unsigned long long*>(p.sum64 + objcw_index(e, a, 0, p.nb_entries)),
                 (unsigned long long)wc.ocnt[i]);
@@ -606,9 +628,23 @@ __device__ __forceinline__ void flush_objects(Params& p, WgCounters& wc, int tid
   if (tid == 0) wc.nobj = 0;
 }
 
+template <int MODE>
 __device__ __forceinline__ void flush_pages(Params& p, WgCounters& wc, int tid, uint32_t th) {
   const bool write = !(p.flags & kDbgNoFlush);
   unsigned int* hrow = p.hist + uint64_t(th) * p.hist_cells;
+  if (MODE & kModeDensePage) {  // cells in order: consecutive lanes add to consecutive words
+    const uint32_t nw = (uint32_t)(p.hist_cells + 1) / 2;
+    for (uint32_t i = tid; i < nw; i += kWG) {
+      const uint32_t v = wc.pdense[i];
+      if (!v) continue;
+      if (write) {
+        if (v & 0xffffu) atomicAdd(hrow + 2 * i, v & 0xffffu);
+        if (v >> 16) atomicAdd(hrow + 2 * i + 1, v >> 16);
+      }
+      wc.pdense[i] = 0;
+    }
+    return;
+  }
   unsigned int* pkey = reinterpret_cast<unsigned int*>(wc.pkey4);
   for (int i = tid; i < (int)kPageSlots; i += kWG) {
     const uint32_t cell = pkey[i];
@@ -644,6 +680,7 @@ __device__ __forceinline__ void clear_sums(WgCounters& wc, int tid) {
   }
 }
 
+template <int MODE>
 __device__ __forceinline__ void clear_state(WgCounters& wc, int tid) {
   clear_sums(wc, tid);
   for (int i = tid; i < (int)kObjSlots; i += kWG) {
@@ -652,9 +689,13 @@ __device__ __forceinline__ void clear_state(WgCounters& wc, int tid) {
     wc.ofirst[i] = kEmpty64;
     wc.owt[i] = 0;
   }
-  for (int i = tid; i < (int)kPageSlots; i += kWG) {
-    reinterpret_cast<unsigned int*>(wc.pkey4)[i] = kEmpty32;
-    wc.pcnt[i] = 0;
+  if (MODE & kModeDensePage) {
+    for (int i = tid; i < (int)(kDensePageCells / 2); i += kWG) wc.pdense[i] = 0;
+  } else {
+    for (int i = tid; i < (int)kPageSlots; i += kWG) {
+      reinterpret_cast<unsigned int*>(wc.pkey4)[i] = kEmpty32;
+      wc.pcnt[i] = 0;
+    }
   }
   if (tid == 0) {
     wc.nobj = 0;
@@ -759,7 +800,7 @@ __device__ __forceinline__ uint64_t stamp() {
   return t;
 }
 
-template <bool TIMING>
+template <bool TIMING, int MODE>
 __global__ __launch_bounds__(kWG, 1) void attribute_kernel(Params p) {
   __shared__ uint4 s_tab[kTabBytes / 16];  // lookup structure (layouts at kTabBytes)
   __shared__ uint32_t s_list[kMaxList];
@@ -786,7 +827,7 @@ __global__ __launch_bounds__(kWG, 1) void attribute_kernel(Params p) {
     for (uint32_t i = tid; i <= kMaxFences; i += kWG) s_fences[i] = p.ffences[i];
     for (uint32_t i = tid; i < p.nb_fences; i += kWG) s_shift[i] = p.fshift[i];
   }
-  clear_state(wc, tid);
+  clear_state<MODE>(wc, tid);
   if (tid < 3) s_flags[tid] = 0;
   __syncthreads();
   const Lookup L{s_fences, s_nodes, s_ninfo, s_shift};
@@ -810,7 +851,7 @@ __global__ __launch_bounds__(kWG, 1) void attribute_kernel(Params p) {
   }
   LaneAcc acc;
   lane_acc_clear(acc);
-  uint32_t win = 0, acc_windows = 0;
+  uint32_t win = 0, acc_windows = 0, last_flush = 0;
   uint32_t ns0 = 0, nf0 = 0, ns1 = 0, nf1 = 0;  // per-buffer tallies: buffer idx, idx + 1
   uint64_t tacc[4] = {0, 0, 0, 0}, t_start = 0, t0 = 0, t1 = 0;
   if (TIMING) t_start = t0 = stamp();
@@ -949,7 +990,7 @@ __global__ __launch_bounds__(kWG, 1) void attribute_kernel(Params p) {
     }
     uint64_t vm = 0, fm = 0;
     if (!(p.flags & kDbgLoadOnly))
-      process_sample(p, wc, acc, L, valid, rec.ts, rec.addr, rec.w, rec.dsrc, d0.access, d0.thread_rank, rseq, roff,
+      process_sample<MODE>(p, wc, acc, L, valid, rec.ts, rec.addr, rec.w, rec.dsrc, d0.access, d0.thread_rank, rseq, roff,
                      vm, fm);
     {
       // lanes of this wave in buffer idx + 1 (tid >= n0)
@@ -992,11 +1033,12 @@ __global__ __launch_bounds__(kWG, 1) void attribute_kernel(Params p) {
       }
       ns1 = nf1 = 0;
     }
-    if (stream_end || (f & 2)) {
+    if (stream_end || (f & 2) || ((MODE & kModeDensePage) && win - last_flush >= kDensePageWindows)) {
       __syncthreads();  // every insert and drain of this window is done
       if (stream_end) flush_sums(p, wc, tid, cur_access);
-      flush_objects(p, wc, tid, cur_access);
-      flush_pages(p, wc, tid, cur_thread);
+      flush_objects<MODE>(p, wc, tid, cur_access);
+      flush_pages<MODE>(p, wc, tid, cur_thread);
+      last_flush = win;
       __syncthreads();
       if (stream_end) {
         clear_sums(wc, tid);  // (sums are next written after the next window's barrier)
@@ -1692,6 +1734,14 @@ static int build_schedule(nmg_engine* h, uint32_t grid) {
   return NMG_OK;
 }
 
+typedef void (*AttributeKernel)(Params);
+static AttributeKernel kernel_for(bool timing, int mode) {
+  static const AttributeKernel k[2][4] = {
+      {attribute_kernel<false, 0>, attribute_kernel<false, 1>, attribute_kernel<false, 2>, attribute_kernel<false, 3>},
+      {attribute_kernel<true, 0>, attribute_kernel<true, 1>, attribute_kernel<true, 2>, attribute_kernel<true, 3>}};
+  return k[timing ? 1 : 0][mode & 3];
+}
+
 extern "C" int nmg_analyze(nmg_engine* h) {
   if (!h) return NMG_ERR_INVALID;
   if (!h->have_table) return fail(h, NMG_ERR_STATE, "nmg_analyze before nmg_set_objects");
@@ -1702,7 +1752,7 @@ extern "C" int nmg_analyze(nmg_engine* h) {
   const uint32_t nb = (uint32_t)h->descs.size();
   if (h->blocks_per_cu <= 0) {
     int bpc = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, attribute_kernel<false>, kWG, 0) != hipSuccess || bpc <= 0) bpc = 1;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, attribute_kernel<false, 0>, kWG, 0) != hipSuccess || bpc <= 0) bpc = 1;
     h->blocks_per_cu = bpc;
   }
   // persistent grid: one resident workgroup per slot, each with a byte-balanced range
@@ -1743,6 +1793,9 @@ extern "C" int nmg_analyze(nmg_engine* h) {
   p.bufcnt = h->d_bufcnt;
   p.sparse_keys = h->d_sparse_keys;
   p.sparse_vals = h->d_sparse_vals;
+  // dense LDS tables when the table is small enough (DESIGN.md "Kernels")
+  const int mode = (h->E <= kObjSlots ? kModeDenseObj : 0) |
+                   (h->hist_cells <= kDensePageCells ? kModeDensePage : 0);
   const int slot = (int)(h->nlaunch % nmg_engine::kRing);
   if (!h->ring0[slot]) {
     HIP_TRY(h, hipEventCreate(&h->ring0[slot]));
@@ -1762,9 +1815,9 @@ extern "C" int nmg_analyze(nmg_engine* h) {
       HIP_TRY(h, hipMemsetAsync(h->d_dbg, 0, n * 8, h->stream));
       h->dbg_len = n;
       p.dbg = reinterpret_cast<unsigned long long*>(h->d_dbg);
-      hipLaunchKernelGGL(attribute_kernel<true>, dim3(grid), dim3(kWG), 0, h->stream, p);
+      hipLaunchKernelGGL(kernel_for(true, mode), dim3(grid), dim3(kWG), 0, h->stream, p);
     } else {
-      hipLaunchKernelGGL(attribute_kernel<false>, dim3(grid), dim3(kWG), 0, h->stream, p);
+      hipLaunchKernelGGL(kernel_for(false, mode), dim3(grid), dim3(kWG), 0, h->stream, p);
     }
     HIP_TRY(h, hipGetLastError());
   }

@@ -63,6 +63,13 @@ CONFIGS = [
     # 1M intervals (configs[3]'s table): fences + per-bucket directory lookup.
     # Few call sites: the reference's site list and sort are quadratic (the oracle keeps that cost)
     SynthConfig(nb_samples=300_000, nb_intervals=1_000_000, size_max=64 * 1024, site_ratio=0.002, seed=12),
+    # kernel table modes: dense objects + hashed page cells (large objects) ...
+    SynthConfig(nb_samples=150_000, nb_intervals=1_500, size_min=64 * 1024, size_max=1024 * 1024, seed=13),
+    # ... hashed objects + dense u16 page cells (many small objects) ...
+    SynthConfig(nb_samples=100_000, nb_intervals=5_000, size_max=4096, seed=14),
+    # ... and 4 MiB buffers: > 62 windows per workgroup, so the dense page
+    # counts are flushed on their cadence, not only at stream ends
+    SynthConfig(nb_samples=3_000_000, nb_intervals=800, buffer_records=100_000, seed=15),
 ]
 
 
