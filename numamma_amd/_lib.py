@@ -11,6 +11,9 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libnumamma_gpu.so")
+# tools/ab.py only: time an alternative in-tree build of the same C-ABI
+if os.environ.get("NMG_LIB_VARIANT"):
+    LIB_PATH = os.path.join(_HERE, "build", "variants", "libnumamma_gpu_%s.so" % os.environ["NMG_LIB_VARIANT"])
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "numamma_gpu.h")
 
 if not os.path.exists(LIB_PATH):

@@ -72,6 +72,13 @@ constexpr uint32_t kProbes = 32;
 constexpr int kModeDenseObj = 1, kModeDensePage = 2;
 constexpr uint32_t kDensePageCells = kPageSlots * 4;  // the page table's 56 KiB as u16 cells
 constexpr uint32_t kDensePageWindows = 62;
+#ifdef NMG_NO_PACK_OBJ
+constexpr bool kPackObj = false;
+#else
+constexpr bool kPackObj = true;
+#endif
+constexpr uint32_t kPackShift = 44;  // kModeDenseObj: per-entry count << 44 | weight sum
+static_assert((uint64_t)kDensePageWindows * kWG < (1ull << (64 - kPackShift)), "packed count");
 static_assert(kDensePageWindows * kWG < 65536u, "u16 page counts");
 constexpr uint32_t kEmpty32 = 0xffffffffu;
 constexpr uint64_t kEmpty64 = ~0ull;
@@ -205,6 +212,31 @@ __device__ __forceinline__ void set_error(Params& p, uint64_t seq, uint32_t off,
             (unsigned long long)w);
 }
 
+// Descend `levels` levels of an Eytzinger tree (node i has children 2i, 2i+1)
+// from the root and return the index below the last level: one 8 B LDS read
+// per level.  (NMG_EYTZ_GROUPED reads node i, its children and grandchildren
+// together -- one round trip per three levels -- but the extra LDS bytes and
+// bank conflicts cost more than the shorter chain saves.)  Reads stay below
+// 2^levels.
+__device__ __forceinline__ uint32_t eytz_descend(const uint64_t* F, uint32_t levels, uint64_t addr) {
+  uint32_t i = 1;
+#ifdef NMG_EYTZ_GROUPED  // measured slower on c2 (0.196 vs 0.182 ms): more LDS bytes and conflicts
+  for (; levels >= 3; levels -= 3) {
+    const uint64_t k0 = F[i];
+    const ulonglong2 k1 = *reinterpret_cast<const ulonglong2*>(F + 2 * i);
+    const ulonglong2 k2a = *reinterpret_cast<const ulonglong2*>(F + 4 * i);
+    const ulonglong2 k2b = *reinterpret_cast<const ulonglong2*>(F + 4 * i + 2);
+    const bool b0 = k0 <= addr;
+    const bool b1 = (b0 ? k1.y : k1.x) <= addr;
+    const uint64_t kg = b0 ? (b1 ? k2b.y : k2b.x) : (b1 ? k2a.y : k2a.x);
+    const bool b2 = kg <= addr;
+    i = 8 * i + 4 * (uint32_t)b0 + 2 * (uint32_t)b1 + (uint32_t)b2;
+  }
+#endif
+  for (; levels > 0; levels--) i = 2 * i + (F[i] <= addr ? 1u : 0u);
+  return i;
+}
+
 // Largest key <= addr (ht_lower_key, tools/hash.c:63-77) for tables larger
 // than kLdsNodes.  Returns nb_keys when no key <= addr.
 //  1. LDS: branch-free search of the 12-level Eytzinger fence tree -> bucket b
@@ -218,9 +250,7 @@ __device__ __forceinline__ void set_error(Params& p, uint64_t seq, uint32_t off,
 //     binary search of those keys in global memory (L2 / MALL resident).
 __device__ __forceinline__ uint32_t lower_key(const Params& p, const uint64_t* s_fences, const uint8_t* s_shift,
                                               uint64_t addr) {
-  uint32_t i = 1;
-#pragma unroll
-  for (uint32_t l = 0; l < kFenceLevels; l++) i = 2 * i + (s_fences[i] <= addr ? 1u : 0u);
+  const uint32_t i = eytz_descend(s_fences, kFenceLevels, addr);
   const uint32_t idx = i >> (__builtin_ctz(i) + 1);  // node of the last right turn
   if (idx == 0) return p.nb_keys;                    // addr < first key
   // in-order rank of Eytzinger node idx at depth d of a complete tree
@@ -371,6 +401,7 @@ __device__ __forceinline__ int page_slot(WgCounters& wc, uint32_t cell) {
 // (256 x 2^23 = 2^31).
 constexpr uint32_t kDrainWindows = 256;
 constexpr uint64_t kLaneMaxWeight = 1ull << 23;
+static_assert((uint64_t)kDensePageWindows * kWG * kLaneMaxWeight < (1ull << kPackShift), "packed weight");
 // Only the 9 hit buckets live in registers (the common case in PEBS data);
 // miss buckets are updated in LDS directly.
 struct LaneAcc {
@@ -462,8 +493,7 @@ __device__ __forceinline__ Match find_entry(const Params& p, const Lookup& L, ui
     // Eytzinger tree: node i has children 2i, 2i+1; a fixed number of levels,
     // one LDS read each, branch-free.  The levels above the 7th fit in one
     // 256 B bank row, so the search is conflict-free where every lane reads.
-    uint32_t i = 1;
-    for (uint32_t l = 0; l < p.elevels; l++) i = 2 * i + (L.fences[i] <= addr ? 1u : 0u);
+    const uint32_t i = eytz_descend(L.fences, p.elevels, addr);
     // largest key <= addr = the node of the last right turn (0: none)
     const uint32_t idx = i >> (__builtin_ctz(i) + 1);
     if (idx == 0) return m;
@@ -557,11 +587,16 @@ __device__ __forceinline__ void process_sample(Params& p, WgCounters& wc, LaneAc
   // per-object counters, aggregated per stream in LDS
   const int os = (MODE & kModeDenseObj) ? (int)e : obj_slot(wc, (uint32_t)e);
   const unsigned long long ord = (seq << 32) | off;  // first match in analysis order (quirk Q7)
-  if (os >= 0) {
+  if ((MODE & kModeDenseObj) && w < kLaneMaxWeight && kPackObj) {
+    // one packed add: count in bits 44..63, weight below (bounded by the
+    // kDensePageWindows flush cadence: < 2^16 samples of < 2^23 each)
+    atomicAdd(&wc.owt[os], (1ull << kPackShift) | w);
+    if (ord < wc.ofirst[os]) atomicMin(&wc.ofirst[os], ord);
+  } else if (os >= 0 && !((MODE & kModeDenseObj) && kPackObj)) {
     atomicAdd(&wc.ocnt[os], 1u);
     if (w) atomicAdd(&wc.owt[os], (unsigned long long)w);
     if (ord < wc.ofirst[os]) atomicMin(&wc.ofirst[os], ord);
-  } else {  // table full: straight to global
+  } else {  // table full (or a weight >= 2^23 in dense mode): straight to global
     atomicAdd(reinterpret_cast<unsigned long long*>(p.sum64 + objcw_index(e, access, 0, p.nb_entries)), 1ull);
     if (w)
       atomicAdd(reinterpret_cast<unsigned long long*>(p.sum64 + objcw_index(e, access, 1, p.nb_entries)),
@@ -611,12 +646,16 @@ __device__ __forceinline__ void flush_objects(Params& p, WgCounters& wc, int tid
   const int n = (MODE & kModeDenseObj) ? (int)p.nb_entries : (int)kObjSlots;
   for (int i = tid; i < n; i += kWG) {
     const uint32_t e = (MODE & kModeDenseObj) ? (uint32_t)i : wc.okey[i];
-    if ((MODE & kModeDenseObj) ? wc.ocnt[i] == 0 : e == kEmpty32) continue;
+    constexpr bool packed = (MODE & kModeDenseObj) && kPackObj;
+    if ((MODE & kModeDenseObj) ? (packed ? wc.owt[i] == 0 : wc.ocnt[i] == 0) : e == kEmpty32) continue;
+    const uint64_t cnt = packed ? wc.owt[i] >> kPackShift : wc.ocnt[i];
+    const uint64_t wt = packed ? wc.owt[i] & ((1ull << kPackShift) - 1) : wc.owt[i];
     if (write) {
       atomicAdd(reinterpret_cast<unsigned long long*>(p.sum64 + objcw_index(e, a, 0, p.nb_entries)),
-                (unsigned long long)wc.ocnt[i]);
-      if (wc.owt[i])
-        atomicAdd(reinterpret_cast<unsigned long long*>(p.sum64 + objcw_index(e, a, 1, p.nb_entries)), wc.owt[i]);
+                (unsigned long long)cnt);
+      if (wt)
+        atomicAdd(reinterpret_cast<unsigned long long*>(p.sum64 + objcw_index(e, a, 1, p.nb_entries)),
+                  (unsigned long long)wt);
       unsigned long long* fp = reinterpret_cast<unsigned long long*>(p.min64 + 36 + e);
       atomicMin(fp, wc.ofirst[i]);  // no read first: a returning load would stall the flush
     }
@@ -719,9 +758,20 @@ __device__ __forceinline__ void load_rec(const uint8_t* base, uint64_t pos, uint
   if (pos + kRecBytes <= len) {
     const uint32_t odd = uint32_t(pos >> 3) & 1;
     const uint8_t* q = base + pos;
+#ifdef NMG_NT_LOADS
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+    const u32x4 a = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(q + (odd ? 8 : 0)));
+    const u32x4 b = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(q + (odd ? 24 : 16)));
+    const u32x2 c = __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(q + (odd ? 0 : 32)));
+    r.x = make_uint4(a.x, a.y, a.z, a.w);
+    r.y = make_uint4(b.x, b.y, b.z, b.w);
+    r.z = make_uint2(c.x, c.y);
+#else
     r.x = *reinterpret_cast<const uint4*>(q + (odd ? 8 : 0));
     r.y = *reinterpret_cast<const uint4*>(q + (odd ? 24 : 16));
     r.z = *reinterpret_cast<const uint2*>(q + (odd ? 0 : 32));
+#endif
   } else {
     r.x = make_uint4(0, 0, 0, 0);
     r.y = make_uint4(0, 0, 0, 0);
@@ -1033,7 +1083,7 @@ __global__ __launch_bounds__(kWG, 1) void attribute_kernel(Params p) {
       }
       ns1 = nf1 = 0;
     }
-    if (stream_end || (f & 2) || ((MODE & kModeDensePage) && win - last_flush >= kDensePageWindows)) {
+    if (stream_end || (f & 2) || ((MODE & (kModeDensePage | kModeDenseObj)) && win - last_flush >= kDensePageWindows)) {
       __syncthreads();  // every insert and drain of this window is done
       if (stream_end) flush_sums(p, wc, tid, cur_access);
       flush_objects<MODE>(p, wc, tid, cur_access);
@@ -1801,7 +1851,6 @@ extern "C" int nmg_analyze(nmg_engine* h) {
     HIP_TRY(h, hipEventCreate(&h->ring0[slot]));
     HIP_TRY(h, hipEventCreate(&h->ring1[slot]));
   }
-  HIP_TRY(h, hipEventRecord(h->ev0, h->stream));
   HIP_TRY(h, hipEventRecord(h->ring0[slot], h->stream));
   if (nb) {
     if (h->flags & kDbgTiming) {
@@ -1822,7 +1871,6 @@ extern "C" int nmg_analyze(nmg_engine* h) {
     HIP_TRY(h, hipGetLastError());
   }
   HIP_TRY(h, hipEventRecord(h->ring1[slot], h->stream));
-  HIP_TRY(h, hipEventRecord(h->ev1, h->stream));
   h->nlaunch++;
   h->launched = true;
   return NMG_OK;
@@ -1848,7 +1896,10 @@ extern "C" int nmg_synchronize(nmg_engine* h) {
   if (!h) return NMG_ERR_INVALID;
   HIP_TRY(h, hipSetDevice(h->device));
   HIP_TRY(h, hipStreamSynchronize(h->stream));
-  if (h->launched) HIP_TRY(h, hipEventElapsedTime(&h->last_ms, h->ev0, h->ev1));
+  if (h->launched) {  // the most recent launch's start / end events
+    const int slot = (int)((h->nlaunch - 1) % nmg_engine::kRing);
+    HIP_TRY(h, hipEventElapsedTime(&h->last_ms, h->ring0[slot], h->ring1[slot]));
+  }
   if (!h->have_table) return NMG_OK;
   uint64_t w = ~0ull;
   HIP_TRY(h, hipMemcpy(&w, h->d_min64 + 36 + h->E, 8, hipMemcpyDeviceToHost));

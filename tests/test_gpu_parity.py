@@ -101,6 +101,28 @@ def test_full_config2_bit_exact(tmp_path):
     _same_dirs(odir, edir)
 
 
+@pytest.mark.parametrize("nb_intervals", [300, 6_000])
+def test_large_weights_bit_exact(tmp_path, nb_intervals):
+    """Weights at and above the kernel's packing limits (2^23 per lane, 2^26
+    per wave sum, 2^32, up to 2^63): the unpacked LDS / global paths of the
+    dense (<= 2048 entries) and hashed table modes must agree with the oracle,
+    including u64 wrap-around of the weight sums (mem_sampling.c:531)."""
+    d = str(tmp_path)
+    rp = generate(SynthConfig(nb_samples=200_000, nb_intervals=nb_intervals, seed=16))
+    rng = np.random.default_rng(16)
+    big = np.array([(1 << 23) - 1, 1 << 23, (1 << 26) + 5, (1 << 32) - 1, 1 << 32, (1 << 40) + 7,
+                    (1 << 63) + 3, (1 << 64) - 1], dtype=np.uint64)
+    for b in rp.buffers:
+        rec = b.ring.view(RECORD_DTYPE)  # pure 40 B SAMPLE streams (lost_frac = 0, no wrap)
+        pick = rng.random(rec.shape[0]) < 0.05
+        rec["weight"][pick] = big[rng.integers(0, big.shape[0], int(pick.sum()))]
+    path, odir = _oracle(rp, d)
+    edir = _engine_replay(path, d)
+    _assert_raw_equal(os.path.join(d, "oracle_raw.bin"), os.path.join(d, "engine_raw.bin"))
+    assert open(os.path.join(d, "oracle_stdout.txt"), "rb").read() == open(os.path.join(d, "engine_stdout.txt"), "rb").read()
+    _same_dirs(odir, edir)
+
+
 def test_no_match_mode(tmp_path):
     d = str(tmp_path)
     rp = generate(SynthConfig(nb_samples=40_000, nb_intervals=100, seed=8))
