@@ -95,7 +95,7 @@ struct nmg_options {
   int32_t device;            /* HIP device ordinal */
   uint32_t flags;            /* NMG_F_* */
   uint32_t nb_threads;       /* next_thread_rank: page-histogram columns (<= 1024) */
-  uint32_t reserved;
+  uint32_t copy_threads;     /* host threads for nmg_submit_buffers copies (0 = 1) */
   uint64_t hist_budget_bytes; /* dense page-histogram arena cap (0 = default 4 GiB) */
   uint64_t sparse_capacity;   /* sparse (object, page, thread) slots (0 = default 1<<22) */
 };
@@ -137,6 +137,34 @@ int nmg_submit_ring(nmg_engine *h, const void *ring, uint64_t ring_size, uint64_
                     uint64_t data_head, uint32_t thread_rank, uint32_t access_type);
 int nmg_submit_buffer(nmg_engine *h, const void *bytes, uint64_t len, uint32_t thread_rank,
                       uint32_t access_type);
+
+/*
+ * Batch form of nmg_submit_buffer: n linearised buffers (host pointers, e.g.
+ * the malloc'd __copy_buffer copies of the `samples` list, mem_sampling.c:696),
+ * in analysis order.  The copies into pinned staging are split over the
+ * engine's copy threads (nmg_options.copy_threads / nmg_stream_begin).  Empty buffers are
+ * dropped like in nmg_submit_buffer.
+ */
+int nmg_submit_buffers(nmg_engine *h, uint32_t n, const void *const *bytes, const uint64_t *lens,
+                       const uint32_t *thread_ranks, const uint32_t *access_types);
+
+/*
+ * Streaming (BASELINE configs[4]; the online branch of __process_samples,
+ * mem_sampling.c:953-957, fed at each alarm, :130-177): buffers submitted
+ * after nmg_stream_begin are uploaded and analysed in chunks of about
+ * chunk_bytes while the caller keeps submitting -- double-buffered pinned
+ * staging, hipMemcpyAsync on a copy stream, the attribution kernel on the
+ * engine stream as soon as its chunk has landed.  A submit blocks only when
+ * both staging halves are still in flight.  nmg_analyze() flushes the last
+ * partial chunk; results accumulate exactly as for one nmg_analyze over all
+ * buffers (analysis order = submission order across chunks).  copy_threads
+ * (>= 1) host threads copy each nmg_submit_buffers batch.  Attribution uses
+ * the table of the last nmg_set_objects (online semantics).
+ * Not combinable with nmg_set_device_buffers.
+ */
+int nmg_stream_begin(nmg_engine *h, uint64_t chunk_bytes, uint32_t copy_threads);
+/* Flush the open chunk and leave streaming mode (buffers stay counted). */
+int nmg_stream_end(nmg_engine *h);
 
 /*
  * Device-resident variant: linearised buffers already in HBM (caller-owned).

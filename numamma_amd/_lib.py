@@ -78,7 +78,7 @@ class nmg_options(C.Structure):
         ("device", C.c_int32),
         ("flags", C.c_uint32),
         ("nb_threads", C.c_uint32),
-        ("reserved", C.c_uint32),
+        ("copy_threads", C.c_uint32),
         ("hist_budget_bytes", C.c_uint64),
         ("sparse_capacity", C.c_uint64),
     ]
@@ -123,6 +123,9 @@ _SIGS = {
     "nmg_set_objects": (C.c_int, [H, u64p, u32p, C.c_uint32, C.POINTER(nmg_object), C.c_uint32]),
     "nmg_submit_ring": (C.c_int, [H, P, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32]),
     "nmg_submit_buffer": (C.c_int, [H, P, C.c_uint64, C.c_uint32, C.c_uint32]),
+    "nmg_submit_buffers": (C.c_int, [H, C.c_uint32, C.POINTER(C.c_void_p), u64p, u32p, u32p]),
+    "nmg_stream_begin": (C.c_int, [H, C.c_uint64, C.c_uint32]),
+    "nmg_stream_end": (C.c_int, [H]),
     "nmg_set_device_buffers": (C.c_int, [H, P, u64p, u64p, u32p, u32p, C.c_uint32, C.c_uint64]),
     "nmg_analyze": (C.c_int, [H]),
     "nmg_synchronize": (C.c_int, [H]),

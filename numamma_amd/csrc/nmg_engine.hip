@@ -30,6 +30,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "nmg_internal.h"
@@ -53,16 +54,15 @@ constexpr uint32_t kTabBytes = 48 * 1024;
 static_assert((kLdsNodes + 1) * (8 + 32 + 8) <= kTabBytes, "small-table LDS layout");
 static_assert((kMaxFences + 1) * (8 + 1) <= kTabBytes, "fence LDS layout");
 constexpr uint32_t kMaxList = kWG;             // slow path: SAMPLE offsets listed per step
-// per-stream LDS aggregation tables (flushed to global on a stream change or
-// when half full)
+// per-stream LDS aggregation tables (flushed to global at a stream change and
+// on a window cadence)
 constexpr uint32_t kObjSlots = 2048;           // entry -> (count, weight, first ordinal)
 constexpr uint32_t kPageBuckets = 896;         // dense page cell -> count: 8-slot buckets
 constexpr uint32_t kPageSlots = kPageBuckets * 8;  // 7168 cells (56 KiB)
-// fill levels that trigger a flush; it runs after the window that saw them, so
-// up to two windows of new keys (2 x kWG) come on top
-constexpr uint32_t kObjHigh = kObjSlots / 2;
-constexpr uint32_t kPageHigh = kPageSlots / 2;
-constexpr uint32_t kProbes = 32;
+constexpr uint32_t kObjBuckets = kObjSlots / 8;
+// hashed (non-dense) tables are flushed at least every kTableWindows windows:
+// u32 counts stay far from overflow and the first-come slots are re-learnt
+constexpr uint32_t kTableWindows = 256;
 // Dense modes (template flags of attribute_kernel):
 //   kModeDenseObj:  nb_entries <= kObjSlots: slot = entry id, no key check;
 //   kModeDensePage: dense histogram cells per thread <= kDensePageCells: u16
@@ -317,7 +317,7 @@ struct WgCounters {
   unsigned long long sums[kGlobalSums];  // total_count, total_weight, na, 18 x (count, sum)
   unsigned long long mins[18];
   unsigned long long maxs[18];
-  unsigned int okey[kObjSlots];
+  alignas(16) unsigned int okey[kObjSlots];  // entry id, 8 per bucket (hashed modes)
   unsigned int ocnt[kObjSlots];
   unsigned long long ofirst[kObjSlots];  // smallest (seq << 32 | offset): first match
   unsigned long long owt[kObjSlots];
@@ -328,35 +328,43 @@ struct WgCounters {
     };
     unsigned int pdense[kDensePageCells / 2];  // kModeDensePage: u16 count per cell, two per word
   };
-  unsigned int nobj, npage;              // occupied slots
 };
 
-// Direct-mapped slots with linear probing: slot order follows key order, so
-// a flush walks entries / cells in (mostly) ascending address order and its
-// global atomics coalesce into shared 64-byte lines.  A slot already holding
-// the key (hot objects) is found with a plain broadcast read, no CAS; the
-// probe chain (first touch, collisions) is the out-of-line case.
-__device__ __forceinline__ int obj_slot_probe(WgCounters& wc, uint32_t e) {
-  uint32_t s = e & (kObjSlots - 1);
-  for (uint32_t i = 0; i < kProbes; i++) {
-    unsigned k = wc.okey[s];
-    if (k == e) return (int)s;
-    if (k == kEmpty32) {
-      unsigned prev = atomicCAS(&wc.okey[s], kEmpty32, e);
-      if (prev == kEmpty32) {
-        atomicAdd(&wc.nobj, 1u);
-        return (int)s;
-      }
-      if (prev == e) return (int)s;
-    }
-    s = (s + 1) & (kObjSlots - 1);
+// Entries (tables with more than kObjSlots entries): a Fibonacci hash picks
+// one 8-slot bucket, found with two 16 B LDS reads; a missing entry takes the
+// first empty slot by CAS (same protocol as page_slot below).  Slots are
+// first come, first served until the next flush (stream end or the
+// kTableWindows cadence): the hot entries of a Zipf-like stream claim them
+// in its first windows, and a full bucket sends the sample straight to the
+// global counters -- no probe chains and no fill-level flushes.
+__device__ __forceinline__ uint32_t obj_bucket(uint32_t e) {
+  return (uint32_t)(((uint64_t)(e * 0x9E3779B1u) * kObjBuckets) >> 32);
+}
+
+__device__ __forceinline__ int bucket_slot(unsigned int* slots8, uint32_t key) {
+  const uint4 k0 = reinterpret_cast<const uint4*>(slots8)[0], k1 = reinterpret_cast<const uint4*>(slots8)[1];
+  uint32_t k[8] = {k0.x, k0.y, k0.z, k0.w, k1.x, k1.y, k1.z, k1.w};
+  int j = -1;
+#pragma unroll
+  for (int i = 7; i >= 0; i--) j = k[i] == key ? i : j;
+  if (j >= 0) return j;
+  for (int attempt = 0; attempt < 8; attempt++) {
+    int f = -1;
+#pragma unroll
+    for (int i = 7; i >= 0; i--) f = k[i] == kEmpty32 ? i : f;
+    if (f < 0) return -1;
+    const unsigned prev = atomicCAS(&slots8[f], kEmpty32, key);
+    if (prev == kEmpty32 || prev == key) return f;
+#pragma unroll
+    for (int i = 0; i < 8; i++) k[i] = i == f ? prev : k[i];
   }
   return -1;
 }
 
 __device__ __forceinline__ int obj_slot(WgCounters& wc, uint32_t e) {
-  const uint32_t s = e & (kObjSlots - 1);
-  return wc.okey[s] == e ? (int)s : obj_slot_probe(wc, e);
+  const uint32_t hb = obj_bucket(e);
+  const int j = bucket_slot(&wc.okey[hb * 8], e);
+  return j < 0 ? -1 : (int)(hb * 8 + (uint32_t)j);
 }
 
 // Page cells: a Fibonacci hash picks one 8-slot bucket (two 16 B LDS reads,
@@ -370,28 +378,8 @@ __device__ __forceinline__ uint32_t page_bucket(uint32_t cell) {
 
 __device__ __forceinline__ int page_slot(WgCounters& wc, uint32_t cell) {
   const uint32_t hb = page_bucket(cell);
-  const uint4 k0 = wc.pkey4[2 * hb], k1 = wc.pkey4[2 * hb + 1];
-  uint32_t key[8] = {k0.x, k0.y, k0.z, k0.w, k1.x, k1.y, k1.z, k1.w};
-  int j = -1;
-#pragma unroll
-  for (int i = 7; i >= 0; i--) j = key[i] == cell ? i : j;
-  if (j >= 0) return (int)(hb * 8 + j);
-  unsigned int* slots = reinterpret_cast<unsigned int*>(&wc.pkey4[2 * hb]);
-  for (int attempt = 0; attempt < 8; attempt++) {
-    int f = -1;
-#pragma unroll
-    for (int i = 7; i >= 0; i--) f = key[i] == kEmpty32 ? i : f;
-    if (f < 0) return -1;
-    const unsigned prev = atomicCAS(&slots[f], kEmpty32, cell);
-    if (prev == kEmpty32) {
-      atomicAdd(&wc.npage, 1u);
-      return (int)(hb * 8 + f);
-    }
-    if (prev == cell) return (int)(hb * 8 + f);
-#pragma unroll
-    for (int i = 0; i < 8; i++) key[i] = i == f ? prev : key[i];
-  }
-  return -1;
+  const int j = bucket_slot(reinterpret_cast<unsigned int*>(&wc.pkey4[2 * hb]), cell);
+  return j < 0 ? -1 : (int)(hb * 8 + (uint32_t)j);
 }
 
 // Per-lane privatised mem_counters of the current stream: packed u16 counts
@@ -664,7 +652,6 @@ __device__ __forceinline__ void flush_objects(Params& p, WgCounters& wc, int tid
     wc.ofirst[i] = kEmpty64;
     wc.owt[i] = 0;
   }
-  if (tid == 0) wc.nobj = 0;
 }
 
 template <int MODE>
@@ -692,7 +679,6 @@ __device__ __forceinline__ void flush_pages(Params& p, WgCounters& wc, int tid, 
     pkey[i] = kEmpty32;
     wc.pcnt[i] = 0;
   }
-  if (tid == 0) wc.npage = 0;
 }
 
 // global mem_counters[a] of the stream (after the lanes were drained)
@@ -735,10 +721,6 @@ __device__ __forceinline__ void clear_state(WgCounters& wc, int tid) {
       reinterpret_cast<unsigned int*>(wc.pkey4)[i] = kEmpty32;
       wc.pcnt[i] = 0;
     }
-  }
-  if (tid == 0) {
-    wc.nobj = 0;
-    wc.npage = 0;
   }
 }
 
@@ -919,7 +901,6 @@ __global__ __launch_bounds__(kWG, 1) void attribute_kernel(Params p) {
       t0 = t1;
     }
     if (badm && lane == 0) atomicOr(&s_flags[win % 3], 1u);
-    if (tid == 0 && (wc.nobj > kObjHigh || wc.npage > kPageHigh)) atomicOr(&s_flags[win % 3], 2u);
     __syncthreads();
     // (LDS broadcasts are made wave-uniform explicitly: the branches below
     // hold barriers and steer the scalar loop state)
@@ -1083,7 +1064,8 @@ __global__ __launch_bounds__(kWG, 1) void attribute_kernel(Params p) {
       }
       ns1 = nf1 = 0;
     }
-    if (stream_end || (f & 2) || ((MODE & (kModeDensePage | kModeDenseObj)) && win - last_flush >= kDensePageWindows)) {
+    const uint32_t cadence = (MODE & (kModeDensePage | kModeDenseObj)) ? kDensePageWindows : kTableWindows;
+    if (stream_end || win - last_flush >= cadence) {
       __syncthreads();  // every insert and drain of this window is done
       if (stream_end) flush_sums(p, wc, tid, cur_access);
       flush_objects<MODE>(p, wc, tid, cur_access);
@@ -1211,7 +1193,30 @@ struct nmg_engine {
   uint32_t sched_grid = 0;       // grid the current schedule was built for
   bool descs_dirty = false;
   uint32_t* d_bufcnt = nullptr;
-  size_t bufcnt_cap = 0;
+  size_t bufcnt_cap = 0;     // buffers the per-buffer count array holds ([2][bufcnt_stride] u32)
+  size_t bufcnt_stride = 0;
+
+  // streaming (nmg_stream_begin): two staging halves, each a chunk in flight
+  struct StreamSlot {
+    uint8_t* h_stage = nullptr;  // pinned
+    size_t cap = 0, len = 0;
+    uint8_t* d_arena = nullptr;
+    size_t dcap = 0;
+    BufDesc* h_sdescs = nullptr;  // pinned schedule (sorted descriptors, then ranges)
+    size_t hs_cap = 0;            // bytes
+    BufDesc* d_sdescs = nullptr;
+    size_t ds_cap = 0;            // bytes
+    std::vector<BufDesc> descs;   // this chunk: offset in the slot, global seq, .pad = global index
+    hipEvent_t copied = nullptr;  // H2D of the chunk done: the host may refill h_stage
+    hipEvent_t done = nullptr;    // kernel of the chunk done: the device may refill d_arena
+    bool used = false;
+  };
+  bool streaming = false, streamed = false;
+  uint64_t chunk_cap = 0;
+  uint32_t copy_threads = 1;
+  StreamSlot slots[2];
+  int cur_slot = 0;
+  hipStream_t copy_stream = nullptr;
 
   // multi-GPU override of per-buffer counts (rank 0 reporting)
   bool counts_override = false;
@@ -1314,6 +1319,7 @@ extern "C" int nmg_create(nmg_engine** out, const nmg_options* opt) {
     h->device = opt->device;
     h->flags = opt->flags;
     h->T = opt->nb_threads ? opt->nb_threads : 1;
+    h->copy_threads = opt->copy_threads ? opt->copy_threads : 1;
     if (opt->hist_budget_bytes) h->hist_budget = opt->hist_budget_bytes;
     if (opt->sparse_capacity) {
       uint64_t c = 1;
@@ -1354,6 +1360,16 @@ extern "C" void nmg_destroy(nmg_engine* h) {
   (void)hipFree(h->d_ranges);
   (void)hipFree(h->d_dbg);
   if (h->h_stage) (void)hipHostFree(h->h_stage);
+  if (h->copy_stream) (void)hipStreamSynchronize(h->copy_stream);
+  for (auto& sl : h->slots) {
+    if (sl.h_stage) (void)hipHostFree(sl.h_stage);
+    if (sl.h_sdescs) (void)hipHostFree(sl.h_sdescs);
+    (void)hipFree(sl.d_arena);
+    (void)hipFree(sl.d_sdescs);
+    if (sl.copied) (void)hipEventDestroy(sl.copied);
+    if (sl.done) (void)hipEventDestroy(sl.done);
+  }
+  if (h->copy_stream) (void)hipStreamDestroy(h->copy_stream);
   if (h->ev0) (void)hipEventDestroy(h->ev0);
   if (h->ev1) (void)hipEventDestroy(h->ev1);
   for (int i = 0; i < nmg_engine::kRing; i++) {
@@ -1386,9 +1402,9 @@ extern "C" int nmg_reset_counters(nmg_engine* h) {
     r.sparse_cap = h->sparse_cap;
   }
   // (a pending descriptor upload zeroes the per-buffer counts itself)
-  if (h->d_bufcnt && !h->descs_dirty && !h->descs.empty() && h->descs.size() <= h->descs_cap) {
+  if (h->d_bufcnt && (h->streaming || h->streamed || (!h->descs_dirty && !h->descs.empty()))) {
     r.bufcnt = h->d_bufcnt;
-    r.n_bufcnt = h->descs.size() * 2;
+    r.n_bufcnt = h->bufcnt_stride * 2;
   }
   hipLaunchKernelGGL(reset_kernel, dim3(h->num_cus * 4), dim3(256), 0, h->stream, r);
   HIP_TRY(h, hipGetLastError());
@@ -1627,8 +1643,23 @@ static int check_buffer_args(nmg_engine* h, uint64_t len, uint32_t thread_rank, 
     return fail(h, NMG_ERR_RANGE, "thread_rank >= nb_threads (set nmg_options.nb_threads)");
   if (len >= (1ull << 32)) return fail(h, NMG_ERR_RANGE, "buffer >= 4 GiB (unsigned cursors, mem_sampling.c:831-834)");
   if (h->external) return fail(h, NMG_ERR_STATE, "device buffers are set; call nmg_clear_buffers first");
+  if (h->streamed && !h->streaming) return fail(h, NMG_ERR_STATE, "stream ended; call nmg_clear_buffers first");
   return NMG_OK;
 }
+
+// a host copy into pinned staging, run by one of the copy threads
+struct CopyTask {
+  uint8_t* dst;
+  const uint8_t* src;
+  uint64_t len;
+};
+static int stream_dst(nmg_engine* h, uint64_t len, uint8_t** dst, std::vector<CopyTask>* pending);
+static void ensure_occupancy(nmg_engine* h);
+static void make_schedule(const std::vector<BufDesc>& descs, uint32_t grid, uint32_t index_base, BufDesc* sorted,
+                          uint32_t* ranges);
+static int launch_attribution(nmg_engine* h, const uint8_t* data, const BufDesc* sdescs, const uint32_t* ranges,
+                              uint32_t nb, uint32_t grid);
+static int stream_append(nmg_engine* h, uint64_t len, uint32_t thread_rank, uint32_t access);
 
 extern "C" int nmg_submit_buffer(nmg_engine* h, const void* bytes, uint64_t len, uint32_t thread_rank,
                                  uint32_t access_type) {
@@ -1636,6 +1667,13 @@ extern "C" int nmg_submit_buffer(nmg_engine* h, const void* bytes, uint64_t len,
   int rc = check_buffer_args(h, len, thread_rank, access_type);
   if (rc) return rc;
   if (len == 0) return NMG_OK;  // __copy_buffer drops empty segments (mem_sampling.c:680-682)
+  if (h->streaming) {
+    uint8_t* dst = nullptr;
+    rc = stream_dst(h, len, &dst, nullptr);
+    if (rc) return rc;
+    memcpy(dst, bytes, len);
+    return stream_append(h, len, thread_rank, access_type);
+  }
   rc = stage_reserve(h, h->stage_len + len + 16);
   if (rc) return rc;
   memcpy(h->h_stage + h->stage_len, bytes, len);
@@ -1650,10 +1688,15 @@ extern "C" int nmg_submit_ring(nmg_engine* h, const void* ring, uint64_t ring_si
   if (data_head < data_tail) len = ring_size - data_tail + data_head;  // :687-694
   int rc = check_buffer_args(h, len, thread_rank, access_type);
   if (rc) return rc;
-  rc = stage_reserve(h, h->stage_len + len + 16);
+  uint8_t* dst = nullptr;
+  if (h->streaming) {
+    rc = stream_dst(h, len, &dst, nullptr);
+  } else {
+    rc = stage_reserve(h, h->stage_len + len + 16);
+    dst = h->h_stage + h->stage_len;
+  }
   if (rc) return rc;
   const uint8_t* r = (const uint8_t*)ring;
-  uint8_t* dst = h->h_stage + h->stage_len;
   if (data_head < data_tail) {  // :704-713: two segments
     uint64_t first = ring_size - data_tail;
     memcpy(dst, r + data_tail, first);
@@ -1661,7 +1704,239 @@ extern "C" int nmg_submit_ring(nmg_engine* h, const void* ring, uint64_t ring_si
   } else {
     memcpy(dst, r + data_tail, len);
   }
-  return append_desc(h, len, thread_rank, access_type);
+  return h->streaming ? stream_append(h, len, thread_rank, access_type) : append_desc(h, len, thread_rank, access_type);
+}
+
+// ---------------------------------------------------------------------------
+// host copies split over threads (nmg_submit_buffers)
+
+static void run_copies(const std::vector<CopyTask>& tasks, uint32_t nthreads) {
+  if (tasks.empty()) return;
+  uint64_t total = 0;
+  for (const auto& t : tasks) total += t.len;
+  const uint32_t T = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(nthreads, total >> 20));  // >= 1 MiB each
+  if (T <= 1) {
+    for (const auto& t : tasks) memcpy(t.dst, t.src, t.len);
+    return;
+  }
+  // contiguous task ranges of about equal bytes
+  std::vector<size_t> cut(T + 1, tasks.size());
+  cut[0] = 0;
+  uint64_t acc = 0;
+  uint32_t k = 1;
+  for (size_t i = 0; i < tasks.size() && k < T; i++) {
+    acc += tasks[i].len;
+    if (acc * T >= total * k) cut[k++] = i + 1;
+  }
+  auto work = [&](uint32_t w) {
+    for (size_t i = cut[w]; i < cut[w + 1]; i++) memcpy(tasks[i].dst, tasks[i].src, tasks[i].len);
+  };
+  std::vector<std::thread> pool;
+  for (uint32_t w = 1; w < T; w++) pool.emplace_back(work, w);
+  work(0);
+  for (auto& t : pool) t.join();
+}
+
+// ---------------------------------------------------------------------------
+// streaming: chunks of submitted buffers staged in one of two pinned halves,
+// uploaded on the copy stream and analysed on the engine stream
+
+// wait until the host may refill slot s (its previous chunk's H2D is done)
+static int slot_acquire(nmg_engine* h, int s) {
+  auto& sl = h->slots[s];
+  if (sl.used) HIP_TRY(h, hipEventSynchronize(sl.copied));
+  sl.len = 0;
+  sl.descs.clear();
+  return NMG_OK;
+}
+
+// per-buffer count array for `need` buffers; its stride stays fixed while
+// chunks are in flight (grown by doubling after draining the engine stream)
+static int ensure_bufcnt(nmg_engine* h, size_t need) {
+  if (need <= h->bufcnt_stride) return NMG_OK;
+  if (h->bufcnt_stride == 0 && need <= h->bufcnt_cap) {  // a kept array, first chunk
+    h->bufcnt_stride = h->bufcnt_cap;
+    HIP_TRY(h, hipMemsetAsync(h->d_bufcnt, 0, h->bufcnt_cap * 2 * 4, h->stream));
+    return NMG_OK;
+  }
+  const size_t cap = std::max<size_t>({need, h->bufcnt_cap * 2, (size_t)4096});
+  uint32_t* nb = nullptr;
+  HIP_TRY(h, hipStreamSynchronize(h->stream));
+  HIP_TRY(h, hipMalloc(&nb, cap * 2 * 4));
+  HIP_TRY(h, hipMemsetAsync(nb, 0, cap * 2 * 4, h->stream));
+  if (h->d_bufcnt && h->bufcnt_stride) {
+    HIP_TRY(h, hipMemcpyAsync(nb, h->d_bufcnt, h->bufcnt_stride * 4, hipMemcpyDeviceToDevice, h->stream));
+    HIP_TRY(h, hipMemcpyAsync(nb + cap, h->d_bufcnt + h->bufcnt_stride, h->bufcnt_stride * 4,
+                              hipMemcpyDeviceToDevice, h->stream));
+  }
+  HIP_TRY(h, hipStreamSynchronize(h->stream));
+  (void)hipFree(h->d_bufcnt);
+  h->d_bufcnt = nb;
+  h->bufcnt_cap = cap;
+  h->bufcnt_stride = cap;
+  return NMG_OK;
+}
+
+// Enqueue the open chunk: schedule on the host, H2D on the copy stream (after
+// the slot's previous kernel released its device arena), then the kernel on
+// the engine stream once the copy has landed.
+static int stream_flush(nmg_engine* h) {
+  auto& sl = h->slots[h->cur_slot];
+  if (sl.descs.empty()) return NMG_OK;
+  const uint32_t nb = (uint32_t)sl.descs.size();
+  ensure_occupancy(h);
+  const uint32_t grid = std::min<uint32_t>(nb, (uint32_t)(h->num_cus * h->blocks_per_cu));
+  int rc = ensure_bufcnt(h, h->descs.size());
+  if (rc) return rc;
+  const size_t sched_bytes = nb * sizeof(BufDesc) + (grid + 1) * 4;
+  if (sched_bytes > sl.hs_cap) {  // (slot acquired: its previous H2D is done)
+    if (sl.h_sdescs) (void)hipHostFree(sl.h_sdescs);
+    sl.h_sdescs = nullptr;
+    sl.hs_cap = std::max<size_t>(sched_bytes * 2, 64 << 10);
+    HIP_TRY(h, hipHostMalloc((void**)&sl.h_sdescs, sl.hs_cap, hipHostMallocDefault));
+  }
+  const uint32_t index_base = (uint32_t)(h->descs.size() - nb);
+  uint32_t* h_ranges = reinterpret_cast<uint32_t*>(sl.h_sdescs + nb);
+  make_schedule(sl.descs, grid, index_base, sl.h_sdescs, h_ranges);
+  if (sl.len + 64 > sl.dcap || sched_bytes > sl.ds_cap) {  // grow the device side: wait for its last kernel
+    if (sl.used) HIP_TRY(h, hipEventSynchronize(sl.done));
+    if (sl.len + 64 > sl.dcap) {
+      (void)hipFree(sl.d_arena);
+      sl.d_arena = nullptr;
+      sl.dcap = std::max<size_t>(sl.len + 64, sl.cap + 64);
+      HIP_TRY(h, hipMalloc(&sl.d_arena, sl.dcap));
+    }
+    if (sched_bytes > sl.ds_cap) {
+      (void)hipFree(sl.d_sdescs);
+      sl.d_sdescs = nullptr;
+      sl.ds_cap = sl.hs_cap;
+      HIP_TRY(h, hipMalloc(&sl.d_sdescs, sl.ds_cap));
+    }
+  }
+  if (sl.used) HIP_TRY(h, hipStreamWaitEvent(h->copy_stream, sl.done, 0));
+  HIP_TRY(h, hipMemcpyAsync(sl.d_arena, sl.h_stage, sl.len, hipMemcpyHostToDevice, h->copy_stream));
+  HIP_TRY(h, hipMemcpyAsync(sl.d_sdescs, sl.h_sdescs, sched_bytes, hipMemcpyHostToDevice, h->copy_stream));
+  HIP_TRY(h, hipEventRecord(sl.copied, h->copy_stream));
+  HIP_TRY(h, hipStreamWaitEvent(h->stream, sl.copied, 0));
+  rc = launch_attribution(h, sl.d_arena, sl.d_sdescs, reinterpret_cast<const uint32_t*>(sl.d_sdescs + nb), nb, grid);
+  if (rc) return rc;
+  HIP_TRY(h, hipEventRecord(sl.done, h->stream));
+  sl.used = true;
+  // switch halves; the next submit refills the other one once its H2D is done
+  h->cur_slot ^= 1;
+  return slot_acquire(h, h->cur_slot);
+}
+
+// Destination in the open chunk for `len` bytes; flushes the chunk first when
+// it is full (running the batch's pending copies into it before the upload).
+static int stream_dst(nmg_engine* h, uint64_t len, uint8_t** dst, std::vector<CopyTask>* pending) {
+  auto* sl = &h->slots[h->cur_slot];
+  if (!sl->descs.empty() && sl->len + len + 16 > h->chunk_cap) {
+    if (pending) {
+      run_copies(*pending, h->copy_threads);
+      pending->clear();
+    }
+    int rc = stream_flush(h);
+    if (rc) return rc;
+    sl = &h->slots[h->cur_slot];
+  }
+  if (sl->len + len + 16 > sl->cap) {  // first use, or one buffer larger than a chunk
+    const size_t cap = std::max<size_t>(h->chunk_cap, sl->len + len + 16);
+    uint8_t* p = nullptr;
+    HIP_TRY(h, hipHostMalloc((void**)&p, cap, hipHostMallocDefault));
+    if (sl->len) {
+      if (pending) {  // pending copies target the old block
+        run_copies(*pending, h->copy_threads);
+        pending->clear();
+      }
+      memcpy(p, sl->h_stage, sl->len);
+    }
+    if (sl->h_stage) (void)hipHostFree(sl->h_stage);
+    sl->h_stage = p;
+    sl->cap = cap;
+  }
+  *dst = sl->h_stage + sl->len;
+  return NMG_OK;
+}
+
+static int stream_append(nmg_engine* h, uint64_t len, uint32_t thread_rank, uint32_t access) {
+  auto& sl = h->slots[h->cur_slot];
+  BufDesc d;
+  d.offset = sl.len;
+  d.len = (uint32_t)len;
+  d.thread_rank = thread_rank;
+  d.access = access;
+  d.pad = 0;
+  d.seq = h->descs.size();  // analysis order across chunks
+  sl.descs.push_back(d);
+  h->descs.push_back(d);
+  h->buf_bytes.push_back(len);
+  sl.len = (sl.len + len + 15) & ~size_t(15);
+  return NMG_OK;
+}
+
+extern "C" int nmg_stream_begin(nmg_engine* h, uint64_t chunk_bytes, uint32_t copy_threads) {
+  if (!h || copy_threads == 0) return NMG_ERR_INVALID;
+  if (h->external) return fail(h, NMG_ERR_STATE, "device buffers are set; call nmg_clear_buffers first");
+  if (h->staged_dirty || (!h->streaming && !h->streamed && !h->descs.empty()))
+    return fail(h, NMG_ERR_STATE, "buffers already submitted; call nmg_clear_buffers first");
+  HIP_TRY(h, hipSetDevice(h->device));
+  if (!h->copy_stream) {
+    HIP_TRY(h, hipStreamCreateWithFlags(&h->copy_stream, hipStreamNonBlocking));
+    for (auto& sl : h->slots) {
+      HIP_TRY(h, hipEventCreateWithFlags(&sl.copied, hipEventDisableTiming));
+      HIP_TRY(h, hipEventCreateWithFlags(&sl.done, hipEventDisableTiming));
+    }
+  }
+  h->chunk_cap = std::max<uint64_t>(chunk_bytes, 64 << 10);
+  h->copy_threads = copy_threads;
+  h->streaming = true;
+  h->streamed = true;
+  return NMG_OK;
+}
+
+extern "C" int nmg_stream_end(nmg_engine* h) {
+  if (!h) return NMG_ERR_INVALID;
+  if (!h->streaming) return NMG_OK;
+  HIP_TRY(h, hipSetDevice(h->device));
+  int rc = h->have_table ? stream_flush(h) : NMG_OK;
+  h->streaming = false;
+  return rc;
+}
+
+extern "C" int nmg_submit_buffers(nmg_engine* h, uint32_t n, const void* const* bytes, const uint64_t* lens,
+                                  const uint32_t* thread_ranks, const uint32_t* access_types) {
+  if (!h || (n && (!bytes || !lens || !thread_ranks || !access_types))) return NMG_ERR_INVALID;
+  for (uint32_t i = 0; i < n; i++) {
+    if (lens[i] && !bytes[i]) return NMG_ERR_INVALID;
+    int rc = check_buffer_args(h, lens[i], thread_ranks[i], access_types[i]);
+    if (rc) return rc;
+  }
+  std::vector<CopyTask> tasks;
+  tasks.reserve(n);
+  if (!h->streaming) {
+    uint64_t total = 0;
+    for (uint32_t i = 0; i < n; i++) total += (lens[i] + 15) & ~uint64_t(15);
+    int rc = stage_reserve(h, h->stage_len + total + 16);
+    if (rc) return rc;
+    for (uint32_t i = 0; i < n; i++) {
+      if (!lens[i]) continue;
+      tasks.push_back({h->h_stage + h->stage_len, (const uint8_t*)bytes[i], lens[i]});
+      append_desc(h, lens[i], thread_ranks[i], access_types[i]);
+    }
+    run_copies(tasks, h->copy_threads);
+    return NMG_OK;
+  }
+  for (uint32_t i = 0; i < n; i++) {
+    if (!lens[i]) continue;
+    uint8_t* dst = nullptr;
+    int rc = stream_dst(h, lens[i], &dst, &tasks);
+    if (rc) return rc;
+    tasks.push_back({dst, (const uint8_t*)bytes[i], lens[i]});
+    stream_append(h, lens[i], thread_ranks[i], access_types[i]);
+  }
+  run_copies(tasks, h->copy_threads);
+  return NMG_OK;
 }
 
 extern "C" int nmg_set_device_buffers(nmg_engine* h, const void* d_data, const uint64_t* offsets,
@@ -1669,6 +1944,7 @@ extern "C" int nmg_set_device_buffers(nmg_engine* h, const void* d_data, const u
                                       const uint32_t* access_types, uint32_t nb_buffers, uint64_t seq_base) {
   if (!h || (nb_buffers && (!d_data || !offsets || !lengths || !thread_ranks || !access_types)))
     return NMG_ERR_INVALID;
+  if (h->streaming || h->streamed) return fail(h, NMG_ERR_STATE, "streaming buffers are set; call nmg_clear_buffers first");
   std::vector<BufDesc> descs;
   std::vector<uint64_t> bytes;
   descs.reserve(nb_buffers);
@@ -1700,6 +1976,18 @@ extern "C" int nmg_set_device_buffers(nmg_engine* h, const void* d_data, const u
 
 extern "C" int nmg_clear_buffers(nmg_engine* h) {
   if (!h) return NMG_ERR_INVALID;
+  if (h->streaming || h->streamed) {
+    HIP_TRY(h, hipSetDevice(h->device));
+    HIP_TRY(h, hipStreamSynchronize(h->stream));
+    HIP_TRY(h, hipStreamSynchronize(h->copy_stream));
+    for (auto& sl : h->slots) {
+      sl.descs.clear();
+      sl.len = 0;
+      sl.used = false;
+    }
+    h->streamed = false;
+    h->bufcnt_stride = 0;  // per-buffer counts restart (the array is kept)
+  }
   h->descs.clear();
   h->buf_bytes.clear();
   h->stage_len = 0;
@@ -1732,9 +2020,11 @@ static int upload_buffers(nmg_engine* h) {
       h->d_descs = nullptr;
       h->d_bufcnt = nullptr;
       h->descs_cap = n;
+      h->bufcnt_cap = n;
       HIP_TRY(h, hipMalloc(&h->d_descs, n * sizeof(BufDesc)));
       HIP_TRY(h, hipMalloc(&h->d_bufcnt, n * 2 * 4));
     }
+    h->bufcnt_stride = n;
     if (n) {
       HIP_TRY(h, hipMemcpyAsync(h->d_descs, h->descs.data(), n * sizeof(BufDesc), hipMemcpyHostToDevice, h->stream));
       HIP_TRY(h, hipMemsetAsync(h->d_bufcnt, 0, n * 2 * 4, h->stream));
@@ -1749,29 +2039,39 @@ static int upload_buffers(nmg_engine* h) {
 // order in which they are analysed changes no result (all merges are sums,
 // mins and maxes; first-match ordinals carry the analysis position) -- and
 // cut into `grid` contiguous ranges of about equal bytes.
-static int build_schedule(nmg_engine* h, uint32_t grid) {
-  const uint32_t nb = (uint32_t)h->descs.size();
+// Host half: `sorted` = descs in schedule order with .pad = index_base + the
+// buffer's position in `descs` (its per-buffer count slot), `ranges` = grid + 1
+// cut points of about equal bytes.
+static void make_schedule(const std::vector<BufDesc>& descs, uint32_t grid, uint32_t index_base, BufDesc* sorted,
+                          uint32_t* ranges) {
+  const uint32_t nb = (uint32_t)descs.size();
   std::vector<uint32_t> order(nb);
   for (uint32_t i = 0; i < nb; i++) order[i] = i;
   std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) {
-    const BufDesc &x = h->descs[a], &y = h->descs[b];
+    const BufDesc &x = descs[a], &y = descs[b];
     if (x.access != y.access) return x.access < y.access;
     return x.thread_rank < y.thread_rank;
   });
   std::vector<uint64_t> csum(nb + 1, 0);
-  for (uint32_t i = 0; i < nb; i++) csum[i + 1] = csum[i] + h->descs[order[i]].len + 64;
-  std::vector<uint32_t> ranges(grid + 1, 0);
+  for (uint32_t i = 0; i < nb; i++) csum[i + 1] = csum[i] + descs[order[i]].len + 64;
+  ranges[0] = 0;
   for (uint32_t w = 1; w < grid; w++) {
     const uint64_t target = csum[nb] * w / grid;
     uint32_t c = (uint32_t)(std::lower_bound(csum.begin(), csum.end(), target) - csum.begin());
     ranges[w] = std::max(ranges[w - 1], std::min(c, nb));
   }
   ranges[grid] = nb;
-  std::vector<BufDesc> sorted(nb);
   for (uint32_t i = 0; i < nb; i++) {
-    sorted[i] = h->descs[order[i]];
-    sorted[i].pad = order[i];
+    sorted[i] = descs[order[i]];
+    sorted[i].pad = index_base + order[i];
   }
+}
+
+static int build_schedule(nmg_engine* h, uint32_t grid) {
+  const uint32_t nb = (uint32_t)h->descs.size();
+  std::vector<uint32_t> ranges(grid + 1, 0);
+  std::vector<BufDesc> sorted(nb);
+  make_schedule(h->descs, grid, 0, sorted.data(), ranges.data());
   (void)hipFree(h->d_sdescs);
   (void)hipFree(h->d_ranges);
   h->d_sdescs = nullptr;
@@ -1792,31 +2092,25 @@ static AttributeKernel kernel_for(bool timing, int mode) {
   return k[timing ? 1 : 0][mode & 3];
 }
 
-extern "C" int nmg_analyze(nmg_engine* h) {
-  if (!h) return NMG_ERR_INVALID;
-  if (!h->have_table) return fail(h, NMG_ERR_STATE, "nmg_analyze before nmg_set_objects");
-  HIP_TRY(h, hipSetDevice(h->device));
-  const bool resched = h->descs_dirty;
-  int rc = upload_buffers(h);
-  if (rc) return rc;
-  const uint32_t nb = (uint32_t)h->descs.size();
+static void ensure_occupancy(nmg_engine* h) {
   if (h->blocks_per_cu <= 0) {
     int bpc = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, attribute_kernel<false, 0>, kWG, 0) != hipSuccess || bpc <= 0) bpc = 1;
     h->blocks_per_cu = bpc;
   }
-  // persistent grid: one resident workgroup per slot, each with a byte-balanced range
-  const uint32_t grid = nb ? std::min<uint32_t>(nb, (uint32_t)(h->num_cus * h->blocks_per_cu)) : 0;
-  if (nb && (resched || grid != h->sched_grid)) {
-    rc = build_schedule(h, grid);
-    if (rc) return rc;
-  }
+}
+
+// One attribution launch over `nb` buffers whose stream-sorted descriptors and
+// per-workgroup ranges are already on the device, on the engine stream,
+// bracketed by the launch-timing events.
+static int launch_attribution(nmg_engine* h, const uint8_t* data, const BufDesc* sdescs, const uint32_t* ranges,
+                              uint32_t nb, uint32_t grid) {
   Params p;
   memset(&p, 0, sizeof(p));
-  p.data = h->d_data;
-  p.sbufs = h->d_sdescs;
-  p.ranges = h->d_ranges;
-  p.nb_bufs = nb;
+  p.data = data;
+  p.sbufs = sdescs;
+  p.ranges = ranges;
+  p.nb_bufs = (uint32_t)h->bufcnt_stride;
   p.nb_keys = h->K;
   p.keys = h->d_keys;
   p.nodes = h->d_nodes;
@@ -1874,6 +2168,28 @@ extern "C" int nmg_analyze(nmg_engine* h) {
   h->nlaunch++;
   h->launched = true;
   return NMG_OK;
+}
+
+static int stream_flush(nmg_engine* h);
+
+extern "C" int nmg_analyze(nmg_engine* h) {
+  if (!h) return NMG_ERR_INVALID;
+  if (!h->have_table) return fail(h, NMG_ERR_STATE, "nmg_analyze before nmg_set_objects");
+  HIP_TRY(h, hipSetDevice(h->device));
+  if (h->streaming) return stream_flush(h);  // earlier chunks are already enqueued
+  if (h->streamed) return NMG_OK;             // nmg_stream_end flushed everything
+  const bool resched = h->descs_dirty;
+  int rc = upload_buffers(h);
+  if (rc) return rc;
+  const uint32_t nb = (uint32_t)h->descs.size();
+  ensure_occupancy(h);
+  // persistent grid: one resident workgroup per slot, each with a byte-balanced range
+  const uint32_t grid = nb ? std::min<uint32_t>(nb, (uint32_t)(h->num_cus * h->blocks_per_cu)) : 0;
+  if (nb && (resched || grid != h->sched_grid)) {
+    rc = build_schedule(h, grid);
+    if (rc) return rc;
+  }
+  return launch_attribution(h, h->d_data, h->d_sdescs, h->d_ranges, nb, grid);
 }
 
 static int decode_error_word(nmg_engine* h, uint64_t w) {
@@ -1966,11 +2282,13 @@ int engine_download(nmg_engine* h, HostResults& r) {
     r.buf_found = h->ov_found;
     r.buf_bytes = h->ov_bytes;
   } else {
-    size_t n = h->descs.size();
-    std::vector<uint32_t> cnt(2 * n);
-    if (n) HIP_TRY(h, hipMemcpy(cnt.data(), h->d_bufcnt, 2 * n * 4, hipMemcpyDeviceToHost));
-    r.buf_samples.assign(cnt.begin(), cnt.begin() + n);
-    r.buf_found.assign(cnt.begin() + n, cnt.end());
+    const size_t n = h->descs.size();
+    r.buf_samples.assign(n, 0);
+    r.buf_found.assign(n, 0);
+    if (n) {
+      HIP_TRY(h, hipMemcpy(r.buf_samples.data(), h->d_bufcnt, n * 4, hipMemcpyDeviceToHost));
+      HIP_TRY(h, hipMemcpy(r.buf_found.data(), h->d_bufcnt + h->bufcnt_stride, n * 4, hipMemcpyDeviceToHost));
+    }
     r.buf_bytes = h->buf_bytes;
   }
   // mem_sampling_finalize accumulates the per-buffer int counters (:334-335)

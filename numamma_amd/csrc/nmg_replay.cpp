@@ -210,6 +210,14 @@ extern "C" int nmg_run_replay(const char* replay_path, const char* output_dir, c
   opt.device = device;
   opt.flags = flags | (raw_path ? NMG_F_OBJECT_LEVELS : 0);
   opt.nb_threads = r.nb_threads ? r.nb_threads : 1;
+  // NMG_REPLAY_STREAM="chunk_bytes[:copy_threads[:batch]]": feed the buffers
+  // in nmg_submit_buffers batches (unwrapped ring segments; wrapped ones through
+  // nmg_submit_ring), through the streaming path when chunk_bytes > 0
+  const char* stream = getenv("NMG_REPLAY_STREAM");
+  unsigned long long chunk = 0;
+  unsigned threads = 1, batch = 64;
+  if (stream && *stream) sscanf(stream, "%llu:%u:%u", &chunk, &threads, &batch);
+  opt.copy_threads = threads ? threads : 1;
   nmg_engine* h = nullptr;
   rc = nmg_create(&h, &opt);
   if (rc) {
@@ -225,9 +233,44 @@ extern "C" int nmg_run_replay(const char* replay_path, const char* output_dir, c
   };
   rc = nmg_set_objects(h, r.keys, r.entry_off, r.nb_keys, r.objects.data(), r.nb_entries);
   if (rc) return bail(rc);
-  for (const auto& b : r.bufs) {
-    rc = nmg_submit_ring(h, b.bytes, b.ring, b.tail, b.head, b.rank, b.access);
+  if (stream && *stream) {
+    if (chunk) {
+      rc = nmg_stream_begin(h, chunk, threads ? threads : 1);
+      if (rc) return bail(rc);
+    }
+    std::vector<const void*> ptrs;
+    std::vector<uint64_t> lens;
+    std::vector<uint32_t> ranks, accs;
+    auto drain = [&]() {
+      int e = ptrs.empty() ? NMG_OK
+                           : nmg_submit_buffers(h, (uint32_t)ptrs.size(), ptrs.data(), lens.data(), ranks.data(),
+                                                accs.data());
+      ptrs.clear();
+      lens.clear();
+      ranks.clear();
+      accs.clear();
+      return e;
+    };
+    for (const auto& b : r.bufs) {
+      if (b.head < b.tail) {  // wrapped: linearised by the engine (__copy_buffer)
+        rc = drain();
+        if (!rc) rc = nmg_submit_ring(h, b.bytes, b.ring, b.tail, b.head, b.rank, b.access);
+      } else {
+        ptrs.push_back(b.bytes + b.tail);
+        lens.push_back(b.head - b.tail);
+        ranks.push_back(b.rank);
+        accs.push_back(b.access);
+        rc = ptrs.size() >= (batch ? batch : 1) ? drain() : NMG_OK;
+      }
+      if (rc) return bail(rc);
+    }
+    rc = drain();
     if (rc) return bail(rc);
+  } else {
+    for (const auto& b : r.bufs) {
+      rc = nmg_submit_ring(h, b.bytes, b.ring, b.tail, b.head, b.rank, b.access);
+      if (rc) return bail(rc);
+    }
   }
   rc = nmg_analyze(h);
   if (rc) return bail(rc);

@@ -29,8 +29,8 @@ def counters_to_numpy(c: "_lib.nmg_mem_counters") -> np.ndarray:
 
 class Engine:
     def __init__(self, device: int = 0, flags: int = _lib.NMG_F_DEFAULT, nb_threads: int = 1,
-                 hist_budget_bytes: int = 0, sparse_capacity: int = 0):
-        opt = _lib.nmg_options(device, flags, nb_threads, 0, hist_budget_bytes, sparse_capacity)
+                 hist_budget_bytes: int = 0, sparse_capacity: int = 0, copy_threads: int = 1):
+        opt = _lib.nmg_options(device, flags, nb_threads, copy_threads, hist_budget_bytes, sparse_capacity)
         h = _lib.H()
         check(lib.nmg_create(C.byref(h), C.byref(opt)))
         self.h = h
@@ -80,6 +80,27 @@ class Engine:
         self._c(lib.nmg_submit_buffer(self.h, data.ctypes.data, data.shape[0], thread_rank, access))
         if data.shape[0]:
             self.buffer_bytes.append(data.shape[0])
+
+    def submit_buffers(self, bufs):
+        """nmg_submit_buffers: [(thread_rank, access, u8 array), ...] in analysis
+        order, copied into pinned staging by the engine's copy threads."""
+        n = len(bufs)
+        arrs = [np.ascontiguousarray(b[2], dtype=np.uint8) for b in bufs]
+        ptrs = (C.c_void_p * max(n, 1))(*[a.ctypes.data for a in arrs])
+        lens = np.array([a.shape[0] for a in arrs], dtype=np.uint64)
+        ranks = np.array([b[0] for b in bufs], dtype=np.uint32)
+        acc = np.array([b[1] for b in bufs], dtype=np.uint32)
+        self._c(lib.nmg_submit_buffers(self.h, n, ptrs, _ptr(lens, C.c_uint64), _ptr(ranks, C.c_uint32),
+                                       _ptr(acc, C.c_uint32)))
+        self.buffer_bytes.extend(int(x) for x in lens if x)
+
+    def stream_begin(self, chunk_bytes: int = 64 << 20, copy_threads: int = 1):
+        """Streaming mode (configs[4]): chunks are uploaded and analysed while
+        buffers keep arriving; analyze() flushes the last one."""
+        self._c(lib.nmg_stream_begin(self.h, chunk_bytes, copy_threads))
+
+    def stream_end(self):
+        self._c(lib.nmg_stream_end(self.h))
 
     def submit_replay(self, replay: Replay):
         for b in replay.buffers:

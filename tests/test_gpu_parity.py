@@ -354,3 +354,65 @@ def test_lookup_boundaries_bit_exact(tmp_path, nkeys, cluster):
     edir = _engine_replay(path, d)
     _assert_raw_equal(os.path.join(d, "oracle_raw.bin"), os.path.join(d, "engine_raw.bin"))
     _same_dirs(odir, edir)
+
+
+# ---- batch submit and streaming (configs[4]): same results as one nmg_analyze
+STREAM_CASES = [
+    # (replay config, NMG_REPLAY_STREAM = chunk_bytes:copy_threads:batch)
+    (SynthConfig(nb_samples=120_000, nb_intervals=2_000, lost_frac=1e-3, wrap_one=True, seed=31), "0:4:16"),
+    (SynthConfig(nb_samples=120_000, nb_intervals=2_000, lost_frac=1e-3, wrap_one=True, seed=32), "262144:1:7"),
+    (SynthConfig(nb_samples=400_000, nb_intervals=5_000, seed=33), "1048576:4:64"),
+    (SynthConfig(nb_samples=50_000, nb_intervals=300, seed=34), "65536:2:1"),  # ~one buffer per chunk
+    # buffers larger than a chunk, > 62 windows per workgroup in a chunk
+    (SynthConfig(nb_samples=2_000_000, nb_intervals=900, buffer_records=100_000, seed=35), "1048576:3:4"),
+    # large table in a stream
+    (SynthConfig(nb_samples=200_000, nb_intervals=60_000, seed=36), "2097152:8:32"),
+]
+
+
+@pytest.mark.parametrize("cfg,mode", STREAM_CASES, ids=[f"stream{i}" for i in range(len(STREAM_CASES))])
+def test_streaming_bit_exact_vs_oracle(tmp_path, monkeypatch, cfg, mode):
+    """nmg_submit_buffers (copy threads) and nmg_stream_begin chunks (uploaded
+    and analysed while submission continues) give byte-identical reports and raw
+    results: analysis order, per-buffer counts and first-match ordinals span
+    the chunks (mem_sampling.c:953-957 online branch fed per alarm)."""
+    d = str(tmp_path)
+    path, odir = _oracle(generate(cfg), d)
+    monkeypatch.setenv("NMG_REPLAY_STREAM", mode)
+    edir = _engine_replay(path, d)
+    _assert_raw_equal(os.path.join(d, "oracle_raw.bin"), os.path.join(d, "engine_raw.bin"))
+    assert open(os.path.join(d, "oracle_stdout.txt"), "rb").read() == open(os.path.join(d, "engine_stdout.txt"), "rb").read()
+    _same_dirs(odir, edir)
+
+
+def test_streaming_python_api_repeat(tmp_path):
+    """Engine.stream_begin + submit_buffers in alarm-sized batches, analysed,
+    then cleared and streamed again on the same engine (state reuse), equal to
+    a single device-resident analysis of the same buffers."""
+    from numamma_amd.engine import Engine
+
+    rp = generate(SynthConfig(nb_samples=300_000, nb_intervals=1_500, seed=37))
+    lins = rp.linear_buffers()
+    ref = Engine(nb_threads=rp.nb_threads)
+    ref.set_objects(rp.table)
+    for r, a, data in lins:
+        ref.submit_buffer(data, r, a)
+    ref.analyze()
+    ref.synchronize()
+    want = (ref.global_counters(), ref.buffer_counts(), ref.object_counters(), ref.page_cells())
+    ref.close()
+    eng = Engine(nb_threads=rp.nb_threads)
+    eng.set_objects(rp.table)
+    for rnd in range(2):
+        eng.clear_buffers()
+        eng.reset()
+        eng.stream_begin(chunk_bytes=512 << 10, copy_threads=3)
+        for i in range(0, len(lins), 23):
+            eng.submit_buffers(lins[i:i + 23])
+        eng.analyze()
+        eng.synchronize()
+        got = (eng.global_counters(), eng.buffer_counts(), eng.object_counters(), eng.page_cells())
+        for a, b in zip(want, got):
+            for x, y in zip(a if isinstance(a, tuple) else (a,), b if isinstance(b, tuple) else (b,)):
+                assert np.array_equal(np.asarray(x), np.asarray(y)), rnd
+    eng.close()

@@ -1,11 +1,22 @@
 #!/usr/bin/env python3
 """End-to-end rate of the drop-in path with host-resident buffers, as the
-reference's C host would drive it: buffers start in pageable
-host memory (the malloc'd __copy_buffer copies, mem_sampling.c:696),
-nmg_submit_buffer stages them into pinned memory, nmg_analyze uploads with
-hipMemcpyAsync and runs the kernel, and the results come back D2H
-(nmg_get_global_counters + object counters + page cells).  Prints one JSON
-line per phase split, next to the device-resident kernel time."""
+reference's C host would drive it, next to the device-resident
+kernel time.  Buffers start in pageable host memory (the malloc'd
+__copy_buffer copies of the `samples` list, mem_sampling.c:696); the results
+come back D2H (global counters, per-buffer counts, object counters, page cells:
+everything nmg_report reads).  Modes (one JSON line each):
+
+  per_buffer  nmg_submit_buffer per buffer (a ctypes call each), then
+              nmg_analyze: pinned staging copy, H2D, kernel, serialised
+  batch       one nmg_submit_buffers call, copies split over T host threads,
+              then nmg_analyze (H2D + kernel)
+  stream      nmg_stream_begin(chunk, T) and nmg_submit_buffers in alarm-sized
+              batches: each chunk's H2D (copy stream) and kernel (engine
+              stream) overlap the copies of the next chunk (configs[4])
+
+    python tools/e2e.py [c2] [--threads 16] [--chunk-mb 64] [--batch 256]
+"""
+import argparse
 import json
 import os
 import sys
@@ -18,43 +29,67 @@ sys.path.insert(0, ROOT)
 
 
 def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("workload", nargs="?", default="c2")
+    ap.add_argument("--threads", type=int, default=16)
+    ap.add_argument("--chunk-mb", type=int, default=64)
+    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--reps", type=int, default=4)
+    ap.add_argument("--modes", default="per_buffer,batch,stream")
+    a = ap.parse_args()
+
     from numamma_amd.engine import Engine
     from numamma_amd.replay import CONFIGS, generate
 
-    wl = sys.argv[1] if len(sys.argv) > 1 else "c2"
-    rp = generate(CONFIGS[wl])
+    rp = generate(CONFIGS[a.workload])
     lins = rp.linear_buffers()
     nbytes = sum(x[2].shape[0] for x in lins)
     nsamples = nbytes // 40
-    eng = Engine(nb_threads=rp.nb_threads)
+    eng = Engine(nb_threads=rp.nb_threads, copy_threads=a.threads)
     eng.set_objects(rp.table)
-    reps = []
-    for r in range(4):
-        eng.clear_buffers()
-        eng.reset()
-        eng.synchronize()
-        t0 = time.perf_counter()
-        for rank, acc, data in lins:  # host copy into pinned staging
-            eng.submit_buffer(data, rank, acc)
-        t1 = time.perf_counter()
-        eng.analyze()  # H2D + kernel
-        eng.synchronize()
-        t2 = time.perf_counter()
+
+    def results():  # D2H of everything the report reads
         eng.global_counters()
+        eng.buffer_counts()
         eng.object_counters()
-        eng.page_cells()  # D2H of everything the report reads
-        t3 = time.perf_counter()
-        reps.append((t1 - t0, t2 - t1, t3 - t2, eng.last_analyze_ms() / 1e3))
-    st, up, dn, kern = np.median(np.array(reps[1:]), axis=0)
-    total = st + up + dn
-    print(json.dumps({
-        "workload": wl, "records": int(nsamples), "bytes": int(nbytes),
-        "stage_host_s": st, "h2d_plus_kernel_s": up, "d2h_results_s": dn, "kernel_s": kern,
-        "e2e_samples_per_s": nsamples / total,
-        "e2e_excl_staging_samples_per_s": nsamples / (up + dn),
-        "h2d_GBps_est": nbytes / max(up - kern, 1e-9) / 1e9,
-        "device_resident_samples_per_s": nsamples / kern,
-    }), flush=True)
+        eng.page_cells()
+
+    for mode in a.modes.split(","):
+        reps = []
+        for r in range(a.reps + 1):
+            eng.clear_buffers()
+            eng.reset()
+            eng.synchronize()
+            t0 = time.perf_counter()
+            if mode == "per_buffer":
+                for rank, acc, data in lins:
+                    eng.submit_buffer(data, rank, acc)
+            elif mode == "batch":
+                eng.submit_buffers(lins)
+            else:
+                eng.stream_begin(chunk_bytes=a.chunk_mb << 20, copy_threads=a.threads)
+                for i in range(0, len(lins), a.batch):
+                    eng.submit_buffers(lins[i:i + a.batch])
+            t1 = time.perf_counter()
+            eng.analyze()
+            eng.synchronize()
+            t2 = time.perf_counter()
+            results()
+            t3 = time.perf_counter()
+            kern = float(np.sum(eng.launch_times(64 if mode == "stream" else 1))) / 1e3
+            if r:
+                reps.append((t1 - t0, t2 - t1, t3 - t2, kern))
+        submit, tail, d2h, kern = np.median(np.array(reps), axis=0)
+        total = submit + tail + d2h
+        print(json.dumps({
+            "workload": a.workload, "mode": mode, "records": int(nsamples), "bytes": int(nbytes),
+            "copy_threads": a.threads if mode != "per_buffer" else 1,
+            "chunk_bytes": (a.chunk_mb << 20) if mode == "stream" else None,
+            "submit_s": submit, "analyze_to_sync_s": tail, "d2h_results_s": d2h, "kernel_s": kern,
+            "e2e_s": total, "e2e_samples_per_s": nsamples / total,
+            "device_resident_samples_per_s": nsamples / kern if kern else None,
+        }), flush=True)
+    eng.close()
 
 
 if __name__ == "__main__":

@@ -27,6 +27,7 @@ VARIANTS = {"load_only": 0x100, "lookup_only": 0x1 | 0x200 | 0x800, "match": 0x1
 WORKLOADS = {
     "c2": dict(nb_samples=10_000_000, nb_intervals=1_000),
     "k100k": dict(nb_samples=10_000_000, nb_intervals=100_000),
+    "k1m": dict(nb_samples=10_000_000, nb_intervals=1_000_000, size_max=64 * 1024),
 }
 
 

@@ -39,6 +39,8 @@ def main():
         out["hbm_read_bytes"] = out["FETCH_SIZE"] * 1024 * 2
     if "WRITE_SIZE" in out:
         out["hbm_write_bytes"] = out["WRITE_SIZE"] * 1024
+    if "hbm_read_bytes" in out and "hbm_write_bytes" in out:  # bench.py roofline.traffic
+        out["hbm_bytes_per_launch"] = out["hbm_read_bytes"] + out["hbm_write_bytes"]
     if "SQ_WAVES" in out and "SQ_INSTS_VALU" in out:
         out["valu_per_wave"] = out["SQ_INSTS_VALU"] / out["SQ_WAVES"]
         out["salu_per_wave"] = out["SQ_INSTS_SALU"] / out["SQ_WAVES"]
