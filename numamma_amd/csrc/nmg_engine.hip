@@ -26,9 +26,13 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <functional>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <condition_variable>
+#include <memory>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -572,7 +576,9 @@ __device__ __forceinline__ void process_sample(Params& p, WgCounters& wc, LaneAc
   const int64_t e = m.e;
   fmask = __ballot(e >= 0);
   if (e < 0 || (p.flags & kDbgNoTables)) return;
-  // per-object counters, aggregated per stream in LDS
+  // per-object counters, aggregated per stream in LDS.  (Admitting an entry
+  // only on its second sample -- a doorkeeper bitset -- was measured slower at
+  // 1M intervals: the per-sample bit test costs more than the flushes it saves.)
   const int os = (MODE & kModeDenseObj) ? (int)e : obj_slot(wc, (uint32_t)e);
   const unsigned long long ord = (seq << 32) | off;  // first match in analysis order (quirk Q7)
   if ((MODE & kModeDenseObj) && w < kLaneMaxWeight && kPackObj) {
@@ -1137,6 +1143,60 @@ __global__ __launch_bounds__(256) void reset_kernel(ResetParams r) {
 
 using namespace nmg;
 
+// Persistent host threads for the staging copies of nmg_submit_buffers (a
+// batch per alarm in streaming mode would otherwise pay a thread start per
+// copy thread per batch).
+struct CopyPool {
+  std::vector<std::thread> workers;
+  std::mutex m;
+  std::condition_variable wake, idle;
+  std::function<void(uint32_t)> job;
+  uint64_t gen = 0;
+  uint32_t pending = 0;
+  bool stop = false;
+
+  explicit CopyPool(uint32_t n) {
+    for (uint32_t w = 1; w < n; w++)
+      workers.emplace_back([this, w] {
+        uint64_t seen = 0;
+        for (;;) {
+          std::function<void(uint32_t)> f;
+          {
+            std::unique_lock<std::mutex> lk(m);
+            wake.wait(lk, [&] { return stop || gen != seen; });
+            if (stop) return;
+            seen = gen;
+            f = job;
+          }
+          f(w);
+          std::lock_guard<std::mutex> lk(m);
+          if (--pending == 0) idle.notify_one();
+        }
+      });
+  }
+  // run f(0..n-1) with worker w taking part w (the caller runs part 0)
+  void run(const std::function<void(uint32_t)>& f) {
+    {
+      std::lock_guard<std::mutex> lk(m);
+      job = f;
+      pending = (uint32_t)workers.size();
+      gen++;
+    }
+    wake.notify_all();
+    f(0);
+    std::unique_lock<std::mutex> lk(m);
+    idle.wait(lk, [&] { return pending == 0; });
+  }
+  ~CopyPool() {
+    {
+      std::lock_guard<std::mutex> lk(m);
+      stop = true;
+    }
+    wake.notify_all();
+    for (auto& t : workers) t.join();
+  }
+};
+
 struct nmg_engine {
   int device = 0;
   uint32_t flags = NMG_F_DEFAULT;
@@ -1214,6 +1274,7 @@ struct nmg_engine {
   bool streaming = false, streamed = false;
   uint64_t chunk_cap = 0;
   uint32_t copy_threads = 1;
+  std::unique_ptr<CopyPool> pool;  // copy_threads - 1 workers, started on first use
   StreamSlot slots[2];
   int cur_slot = 0;
   hipStream_t copy_stream = nullptr;
@@ -1710,15 +1771,17 @@ extern "C" int nmg_submit_ring(nmg_engine* h, const void* ring, uint64_t ring_si
 // ---------------------------------------------------------------------------
 // host copies split over threads (nmg_submit_buffers)
 
-static void run_copies(const std::vector<CopyTask>& tasks, uint32_t nthreads) {
+static void run_copies(nmg_engine* h, const std::vector<CopyTask>& tasks) {
   if (tasks.empty()) return;
   uint64_t total = 0;
   for (const auto& t : tasks) total += t.len;
-  const uint32_t T = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(nthreads, total >> 20));  // >= 1 MiB each
-  if (T <= 1) {
+  const uint32_t nthreads = h->copy_threads;
+  if (nthreads <= 1 || total < (2u << 20)) {
     for (const auto& t : tasks) memcpy(t.dst, t.src, t.len);
     return;
   }
+  if (!h->pool) h->pool.reset(new CopyPool(nthreads));
+  const uint32_t T = nthreads;
   // contiguous task ranges of about equal bytes
   std::vector<size_t> cut(T + 1, tasks.size());
   cut[0] = 0;
@@ -1728,13 +1791,9 @@ static void run_copies(const std::vector<CopyTask>& tasks, uint32_t nthreads) {
     acc += tasks[i].len;
     if (acc * T >= total * k) cut[k++] = i + 1;
   }
-  auto work = [&](uint32_t w) {
+  h->pool->run([&](uint32_t w) {
     for (size_t i = cut[w]; i < cut[w + 1]; i++) memcpy(tasks[i].dst, tasks[i].src, tasks[i].len);
-  };
-  std::vector<std::thread> pool;
-  for (uint32_t w = 1; w < T; w++) pool.emplace_back(work, w);
-  work(0);
-  for (auto& t : pool) t.join();
+  });
 }
 
 // ---------------------------------------------------------------------------
@@ -1833,7 +1892,7 @@ static int stream_dst(nmg_engine* h, uint64_t len, uint8_t** dst, std::vector<Co
   auto* sl = &h->slots[h->cur_slot];
   if (!sl->descs.empty() && sl->len + len + 16 > h->chunk_cap) {
     if (pending) {
-      run_copies(*pending, h->copy_threads);
+      run_copies(h, *pending);
       pending->clear();
     }
     int rc = stream_flush(h);
@@ -1846,7 +1905,7 @@ static int stream_dst(nmg_engine* h, uint64_t len, uint8_t** dst, std::vector<Co
     HIP_TRY(h, hipHostMalloc((void**)&p, cap, hipHostMallocDefault));
     if (sl->len) {
       if (pending) {  // pending copies target the old block
-        run_copies(*pending, h->copy_threads);
+        run_copies(h, *pending);
         pending->clear();
       }
       memcpy(p, sl->h_stage, sl->len);
@@ -1889,6 +1948,7 @@ extern "C" int nmg_stream_begin(nmg_engine* h, uint64_t chunk_bytes, uint32_t co
     }
   }
   h->chunk_cap = std::max<uint64_t>(chunk_bytes, 64 << 10);
+  if (copy_threads != h->copy_threads) h->pool.reset();
   h->copy_threads = copy_threads;
   h->streaming = true;
   h->streamed = true;
@@ -1924,7 +1984,7 @@ extern "C" int nmg_submit_buffers(nmg_engine* h, uint32_t n, const void* const* 
       tasks.push_back({h->h_stage + h->stage_len, (const uint8_t*)bytes[i], lens[i]});
       append_desc(h, lens[i], thread_ranks[i], access_types[i]);
     }
-    run_copies(tasks, h->copy_threads);
+    run_copies(h, tasks);
     return NMG_OK;
   }
   for (uint32_t i = 0; i < n; i++) {
@@ -1935,7 +1995,7 @@ extern "C" int nmg_submit_buffers(nmg_engine* h, uint32_t n, const void* const* 
     tasks.push_back({dst, (const uint8_t*)bytes[i], lens[i]});
     stream_append(h, lens[i], thread_ranks[i], access_types[i]);
   }
-  run_copies(tasks, h->copy_threads);
+  run_copies(h, tasks);
   return NMG_OK;
 }
 
