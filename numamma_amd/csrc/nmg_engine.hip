@@ -162,6 +162,7 @@ struct Params {
   uint32_t* bufcnt;  // [2][nb_bufs]: samples, found
   uint64_t* sparse_keys;
   uint32_t* sparse_vals;
+  uint32_t* sparse_dirty;  // set on any sparse insert: the next reset must clear the table
   unsigned long long* dbg;  // kDbgTiming: [grid][waves][kTimingWords]
 };
 
@@ -300,6 +301,7 @@ __device__ __forceinline__ bool entry_match(uint4 a, uint4 b, uint64_t addr, uin
 }
 
 __device__ __forceinline__ void sparse_add(Params& p, uint64_t key, uint64_t seq, uint32_t off, uint32_t cnt) {
+  *p.sparse_dirty = 1u;
   uint64_t h = (key * 0x9E3779B97F4A7C15ull) >> 20;
   uint32_t slot = uint32_t(h) & p.sparse_mask;
   for (uint32_t probe = 0; probe <= p.sparse_mask; probe++) {
@@ -1121,6 +1123,8 @@ struct ResetParams {
   uint64_t* sparse_keys;
   uint32_t* sparse_vals;
   uint64_t sparse_cap;
+  const uint32_t* sparse_read;  // dirty flag of the analyses since the previous reset
+  uint32_t* sparse_clear;       // the flag the analyses after this reset will set
   uint32_t* bufcnt;
   uint64_t n_bufcnt;
 };
@@ -1132,7 +1136,11 @@ __global__ __launch_bounds__(256) void reset_kernel(ResetParams r) {
   for (uint64_t i = i0; i < r.n_sum64; i += stride) r.sum64[i] = 0;
   for (uint64_t i = i0; i < r.n_min64; i += stride) r.min64[i] = ~0ull;
   for (uint64_t i = i0; i < r.n_max64; i += stride) r.max64[i] = 0;
-  for (uint64_t i = i0; i < r.sparse_cap; i += stride) {
+  // the sparse table is cleared only when something was inserted since the
+  // last reset (it is large, and the [stack] range it serves never matches, Q4)
+  if (i0 == 0 && r.sparse_clear) *r.sparse_clear = 0u;
+  const uint64_t scap = (r.sparse_read && *r.sparse_read) ? r.sparse_cap : 0;
+  for (uint64_t i = i0; i < scap; i += stride) {
     r.sparse_keys[i] = ~0ull;
     r.sparse_vals[i] = 0;
   }
@@ -1238,6 +1246,8 @@ struct nmg_engine {
   uint32_t* d_hist = nullptr;
   uint64_t* d_sparse_keys = nullptr;
   uint32_t* d_sparse_vals = nullptr;
+  uint32_t* d_sparse_dirty = nullptr;  // [2] parity flags (see reset_kernel)
+  uint64_t nreset = 0;
 
   // buffers
   std::vector<BufDesc> descs;
@@ -1353,6 +1363,8 @@ static void free_counters(nmg_engine* h) {
   h->d_hist = nullptr;
   h->d_sparse_keys = nullptr;
   h->d_sparse_vals = nullptr;
+  (void)hipFree(h->d_sparse_dirty);
+  h->d_sparse_dirty = nullptr;
 }
 
 static void free_table(nmg_engine* h) {
@@ -1464,13 +1476,22 @@ extern "C" int nmg_reset_counters(nmg_engine* h) {
     r.sparse_keys = h->d_sparse_keys;
     r.sparse_vals = h->d_sparse_vals;
     r.sparse_cap = h->sparse_cap;
+    // reset #n reads the flag the analyses since reset #n-1 set, and clears
+    // the one the analyses after it will set
+    r.sparse_read = h->d_sparse_dirty + (h->nreset & 1);
+    r.sparse_clear = h->d_sparse_dirty + ((h->nreset + 1) & 1);
   }
   // (a pending descriptor upload zeroes the per-buffer counts itself)
   if (h->d_bufcnt && (h->streaming || h->streamed || (!h->descs_dirty && !h->descs.empty()))) {
     r.bufcnt = h->d_bufcnt;
     r.n_bufcnt = h->bufcnt_stride * 2;
   }
-  hipLaunchKernelGGL(reset_kernel, dim3(h->num_cus * 4), dim3(256), 0, h->stream, r);
+  // grid sized to the work (~16 stores per thread of the longest array), at
+  // most 4 workgroups per CU: small tables reset in one short launch
+  const uint64_t longest = std::max<uint64_t>({r.n_hist16, r.n_sum64, r.n_min64, r.sparse_cap, r.n_bufcnt, 1});
+  const uint32_t rgrid = (uint32_t)std::min<uint64_t>((longest + 256 * 16 - 1) / (256 * 16), (uint64_t)h->num_cus * 4);
+  hipLaunchKernelGGL(reset_kernel, dim3(rgrid), dim3(256), 0, h->stream, r);
+  h->nreset++;
   HIP_TRY(h, hipGetLastError());
   return NMG_OK;
 }
@@ -1664,6 +1685,9 @@ extern "C" int nmg_set_objects(nmg_engine* h, const uint64_t* keys, const uint32
   if (!h->sparse_entries.empty()) {
     HIP_TRY(h, hipMalloc(&h->d_sparse_keys, h->sparse_cap * 8));
     HIP_TRY(h, hipMalloc(&h->d_sparse_vals, h->sparse_cap * 4));
+    HIP_TRY(h, hipMalloc(&h->d_sparse_dirty, 2 * 4));
+    const uint32_t ones[2] = {1u, 1u};  // the first reset clears the fresh table
+    HIP_TRY(h, hipMemcpy(h->d_sparse_dirty, ones, 8, hipMemcpyHostToDevice));
   }
   h->have_table = true;
   HIP_TRY(h, hipStreamSynchronize(h->stream));
@@ -2200,6 +2224,7 @@ static int launch_attribution(nmg_engine* h, const uint8_t* data, const BufDesc*
   p.bufcnt = h->d_bufcnt;
   p.sparse_keys = h->d_sparse_keys;
   p.sparse_vals = h->d_sparse_vals;
+  p.sparse_dirty = h->d_sparse_dirty ? h->d_sparse_dirty + (h->nreset & 1) : nullptr;
   // dense LDS tables when the table is small enough (DESIGN.md "Kernels")
   const int mode = (h->E <= kObjSlots ? kModeDenseObj : 0) |
                    (h->hist_cells <= kDensePageCells ? kModeDensePage : 0);
@@ -2604,6 +2629,8 @@ extern "C" int nmg_sparse_import(nmg_engine* h, const uint64_t* keys, const uint
   HIP_TRY(h, hipSetDevice(h->device));
   HIP_TRY(h, hipMemcpy(h->d_sparse_keys, k.data(), h->sparse_cap * 8, hipMemcpyHostToDevice));
   HIP_TRY(h, hipMemcpy(h->d_sparse_vals, v.data(), h->sparse_cap * 4, hipMemcpyHostToDevice));
+  const uint32_t one = 1;  // imported cells: the next reset must clear the table
+  HIP_TRY(h, hipMemcpy(h->d_sparse_dirty + (h->nreset & 1), &one, 4, hipMemcpyHostToDevice));
   return NMG_OK;
 }
 

@@ -416,3 +416,32 @@ def test_streaming_python_api_repeat(tmp_path):
             for x, y in zip(a if isinstance(a, tuple) else (a,), b if isinstance(b, tuple) else (b,)):
                 assert np.array_equal(np.asarray(x), np.asarray(y)), rnd
     eng.close()
+
+
+def test_sparse_table_reset_cycles():
+    """The sparse (object, thread, page) table is cleared by a reset only when
+    an analysis inserted into it since the previous reset (two parity flags):
+    accumulate without reset, reset, reset twice in a row, re-analyse."""
+    from numamma_amd.engine import Engine
+
+    rp = generate(SynthConfig(nb_samples=60_000, nb_intervals=300, seed=38))
+    eng = Engine(flags=_lib.NMG_F_DEFAULT, nb_threads=rp.nb_threads, hist_budget_bytes=4, sparse_capacity=1 << 16)
+    eng.set_objects(rp.table)
+    eng.submit_replay(rp)
+    eng.analyze()
+    eng.synchronize()
+    once = eng.page_cells()
+    assert once.shape[0] > 0
+    eng.analyze()  # counters accumulate
+    eng.synchronize()
+    twice = eng.page_cells()
+    assert np.array_equal(twice[:, :3], once[:, :3]) and np.array_equal(twice[:, 3], 2 * once[:, 3])
+    for resets in (1, 2, 1):
+        for _ in range(resets):
+            eng.reset()
+        eng.synchronize()
+        assert eng.page_cells().shape[0] == 0
+        eng.analyze()
+        eng.synchronize()
+        assert np.array_equal(eng.page_cells(), once)
+    eng.close()

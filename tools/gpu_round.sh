@@ -77,6 +77,18 @@ for s in $STAGES; do
           || { echo "pmc pass $i failed"; tail -20 $OUT/pmc_${TAG}_$i.log; exit 1; }
       done
       echo "pmc passes done" ;;
+    traffic)
+      # HBM bytes per launch for bench.py's roofline.traffic: FETCH_SIZE and
+      # WRITE_SIZE in passes of their own (MI355X_MICROARCH.md, HBM/rocprofv3)
+      echo "== rocprofv3 traffic passes (${TRAFFIC_WL:-c2})"
+      for c in FETCH_SIZE WRITE_SIZE; do
+        rm -rf $OUT/traffic_${TAG}_$c
+        timeout -k 10 300 rocprofv3 --pmc $c --kernel-trace -d $ROOT/$OUT/traffic_${TAG}_$c -o run --output-format csv \
+          -- python3 $ROOT/bench.py --workload ${TRAFFIC_WL:-c2} --steps 3 --warmup 1 --no-cpu-baseline \
+          > $OUT/traffic_${TAG}_$c.log 2>&1 || { echo "traffic pass $c failed"; tail -20 $OUT/traffic_${TAG}_$c.log; exit 1; }
+      done
+      python3 tools/pmc_summary.py $OUT/traffic_${TAG}_FETCH_SIZE $OUT/traffic_${TAG}_WRITE_SIZE \
+        > $OUT/pmc_${TRAFFIC_WL:-c2}_$TAG.json && cat $OUT/pmc_${TRAFFIC_WL:-c2}_$TAG.json ;;
     pmc)
       echo "== rocprofv3 pmc FETCH_SIZE"
       rm -rf $OUT/pmc_$TAG
