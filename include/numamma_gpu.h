@@ -269,6 +269,28 @@ int nmg_report_host(const struct nmg_host_results *res, const struct nmg_object_
 int nmg_run_replay(const char *replay_path, const char *output_dir, const char *stdout_path,
                    const char *raw_path, int device, uint32_t flags);
 
+/*
+ * Capture/replay bridge: record a live run's analysis input
+ * in the replay format, host-only (no GPU), so that it can be analysed later,
+ * elsewhere, or by an out-of-process helper (`nmg_replay` CLI) when HIP must
+ * not run inside the LD_PRELOAD'ed process.
+ *   nmg_replay_open: the object-table snapshot, with the same arrays as
+ *     nmg_set_objects plus the call-site metadata (taken where ma_finalize
+ *     walks mem_list, src/mem_analyzer.c:1813); callstacks and caller strings
+ *     are copied into the file's pools;
+ *   nmg_replay_add_ring: one `samples` list element in analysis order
+ *     (mem_sampling.c:324), stored as given (the ring segment [data_tail,
+ *     data_head) is linearised at analysis time, like nmg_submit_ring);
+ *   nmg_replay_close: patches the buffer count and closes the file.
+ */
+typedef struct nmg_replay_writer nmg_replay_writer;
+int nmg_replay_open(nmg_replay_writer **out, const char *path, uint32_t nb_threads, const uint64_t *keys,
+                    const uint32_t *entry_off, uint32_t nb_keys, const struct nmg_object *entries,
+                    const struct nmg_object_meta *meta, uint32_t nb_entries);
+int nmg_replay_add_ring(nmg_replay_writer *w, const void *ring, uint64_t ring_size, uint64_t data_tail,
+                        uint64_t data_head, uint32_t thread_rank, uint32_t access_type);
+int nmg_replay_close(nmg_replay_writer *w);
+
 #ifdef __cplusplus
 }
 #endif

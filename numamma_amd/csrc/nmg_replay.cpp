@@ -9,6 +9,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <new>
 #include <string>
 #include <vector>
 
@@ -288,4 +289,137 @@ extern "C" int nmg_run_replay(const char* replay_path, const char* output_dir, c
   }
   nmg_destroy(h);
   return NMG_OK;
+}
+
+// ---------------------------------------------------------------------------
+// capture side of the bridge: the replay writer (format: DESIGN.md §4,
+// numamma_amd/replay.py).  Host-only; every write is checked.
+
+struct nmg_replay_writer {
+  FILE* f = nullptr;
+  uint32_t nb_buffers = 0;
+  uint32_t nb_threads = 0;
+  bool ok = true;
+};
+
+namespace {
+
+template <class T>
+void put(std::vector<uint8_t>& out, T v) {
+  const size_t n = out.size();
+  out.resize(n + sizeof(T));
+  memcpy(out.data() + n, &v, sizeof(T));
+}
+void pad_to8(std::vector<uint8_t>& out) { out.resize(pad8(out.size()), 0); }
+
+}  // namespace
+
+extern "C" int nmg_replay_open(nmg_replay_writer** out, const char* path, uint32_t nb_threads, const uint64_t* keys,
+                               const uint32_t* entry_off, uint32_t nb_keys, const nmg_object* entries,
+                               const nmg_object_meta* meta, uint32_t nb_entries) {
+  if (!out || !path || (nb_keys && (!keys || !entry_off)) || (nb_entries && (!entries || !meta)))
+    return NMG_ERR_INVALID;
+  *out = nullptr;
+  if (nb_threads > NMG_MAX_THREADS) return NMG_ERR_RANGE;
+  if (entry_off && (entry_off[0] != 0 || entry_off[nb_keys] != nb_entries)) return NMG_ERR_INVALID;
+  // pools: callstacks (u64) and caller strings (NUL-terminated), in entry order
+  std::vector<uint64_t> cs_pool;
+  std::string str_pool;
+  std::vector<uint8_t> ent;
+  ent.reserve((size_t)nb_entries * kEntryBytes);
+  for (uint32_t e = 0; e < nb_entries; e++) {
+    const nmg_object& o = entries[e];
+    const nmg_object_meta& m = meta[e];
+    uint32_t cs_off = 0, has_cs = 0, caller_off = 0xFFFFFFFFu;
+    if (m.callstack) {
+      if (m.callstack_size < 0) return NMG_ERR_INVALID;
+      cs_off = (uint32_t)cs_pool.size();
+      cs_pool.insert(cs_pool.end(), m.callstack, m.callstack + m.callstack_size);
+      has_cs = 1;
+    }
+    if (m.caller) {
+      caller_off = (uint32_t)str_pool.size();
+      str_pool.append(m.caller);
+      str_pool.push_back('\0');
+    }
+    put<uint64_t>(ent, o.buffer_addr);
+    put<uint64_t>(ent, o.buffer_size);
+    put<uint64_t>(ent, m.initial_buffer_size);
+    put<uint64_t>(ent, o.alloc_date);
+    put<uint64_t>(ent, o.free_date);
+    put<uint64_t>(ent, m.caller_rip);
+    put<uint32_t>(ent, m.mem_type);
+    put<uint32_t>(ent, m.id);
+    put<uint32_t>(ent, cs_off);
+    put<int32_t>(ent, m.callstack_size);
+    put<uint32_t>(ent, caller_off);
+    put<uint32_t>(ent, has_cs);
+  }
+  std::vector<uint8_t> hdr;
+  hdr.insert(hdr.end(), {'N', 'M', 'G', 'R', 'P', 'L', 'Y', '1'});
+  put<uint32_t>(hdr, 1);
+  put<uint32_t>(hdr, nb_threads);
+  put<uint32_t>(hdr, nb_keys);
+  put<uint32_t>(hdr, nb_entries);
+  put<uint32_t>(hdr, 0);  // nb_buffers, patched by nmg_replay_close
+  put<uint32_t>(hdr, 0);
+  put<uint64_t>(hdr, cs_pool.size());
+  put<uint64_t>(hdr, str_pool.size());
+  put<uint64_t>(hdr, 0);
+  put<uint64_t>(hdr, 0);
+  for (uint32_t k = 0; k < nb_keys; k++) put<uint64_t>(hdr, keys[k]);
+  for (uint32_t k = 0; k <= nb_keys; k++) put<uint32_t>(hdr, entry_off ? entry_off[k] : 0);
+  pad_to8(hdr);
+  hdr.insert(hdr.end(), ent.begin(), ent.end());
+  for (uint64_t v : cs_pool) put<uint64_t>(hdr, v);
+  hdr.insert(hdr.end(), str_pool.begin(), str_pool.end());
+  pad_to8(hdr);
+  nmg_replay_writer* w = new (std::nothrow) nmg_replay_writer();
+  if (!w) return NMG_ERR_NOMEM;
+  w->f = fopen(path, "wb");
+  if (!w->f) {
+    delete w;
+    return NMG_ERR_IO;
+  }
+  w->nb_threads = nb_threads;
+  if (fwrite(hdr.data(), 1, hdr.size(), w->f) != hdr.size()) {
+    fclose(w->f);
+    delete w;
+    return NMG_ERR_IO;
+  }
+  *out = w;
+  return NMG_OK;
+}
+
+extern "C" int nmg_replay_add_ring(nmg_replay_writer* w, const void* ring, uint64_t ring_size, uint64_t data_tail,
+                                   uint64_t data_head, uint32_t thread_rank, uint32_t access_type) {
+  if (!w || !w->f || (ring_size && !ring) || data_tail > ring_size || data_head > ring_size || access_type > 1)
+    return NMG_ERR_INVALID;
+  if (thread_rank >= NMG_MAX_THREADS || (w->nb_threads && thread_rank >= w->nb_threads)) return NMG_ERR_RANGE;
+  std::vector<uint8_t> h;
+  put<uint32_t>(h, thread_rank);
+  put<uint32_t>(h, access_type);
+  put<uint64_t>(h, data_tail);
+  put<uint64_t>(h, data_head);
+  put<uint64_t>(h, ring_size);
+  static const uint8_t zeros[8] = {0};
+  const size_t padn = pad8(ring_size) - ring_size;
+  if (fwrite(h.data(), 1, h.size(), w->f) != h.size() || fwrite(ring, 1, ring_size, w->f) != ring_size ||
+      fwrite(zeros, 1, padn, w->f) != padn) {
+    w->ok = false;
+    return NMG_ERR_IO;
+  }
+  w->nb_buffers++;
+  return NMG_OK;
+}
+
+extern "C" int nmg_replay_close(nmg_replay_writer* w) {
+  if (!w) return NMG_ERR_INVALID;
+  bool ok = w->ok && w->f;
+  if (w->f) {
+    ok = ok && fseek(w->f, 24, SEEK_SET) == 0 && fwrite(&w->nb_buffers, 4, 1, w->f) == 1;
+    ok = (fclose(w->f) == 0) && ok;
+  }
+  delete w;
+  return ok ? NMG_OK : NMG_ERR_IO;
 }

@@ -56,12 +56,7 @@ class Engine:
 
     # ------------------------------------------------------------------
     def set_objects(self, table: ObjectTable):
-        ent = table.entries
-        objs = np.zeros(table.nb_entries, dtype=[("a", "<u8"), ("s", "<u8"), ("al", "<u8"), ("fr", "<u8")])
-        objs["a"] = ent["buffer_addr"]
-        objs["s"] = ent["buffer_size"]
-        objs["al"] = ent["alloc_date"]
-        objs["fr"] = ent["free_date"]
+        objs = table_objects(table)
         keys = np.ascontiguousarray(table.keys, dtype=np.uint64)
         off = np.ascontiguousarray(table.entry_off, dtype=np.uint32)
         self._c(lib.nmg_set_objects(self.h, _ptr(keys, C.c_uint64), _ptr(off, C.c_uint32), keys.shape[0],
@@ -210,6 +205,38 @@ class Engine:
         nbytes = np.ascontiguousarray(nbytes, dtype=np.uint64)
         self._c(lib.nmg_set_buffer_counts(self.h, samples.shape[0], _ptr(samples, C.c_uint32),
                                           _ptr(found, C.c_uint32), _ptr(nbytes, C.c_uint64)))
+
+
+def table_objects(table: ObjectTable) -> np.ndarray:
+    """struct nmg_object[] (buffer_addr, buffer_size, alloc_date, free_date) of a table."""
+    ent = table.entries
+    objs = np.zeros(table.nb_entries, dtype=[("a", "<u8"), ("s", "<u8"), ("al", "<u8"), ("fr", "<u8")])
+    objs["a"] = ent["buffer_addr"]
+    objs["s"] = ent["buffer_size"]
+    objs["al"] = ent["alloc_date"]
+    objs["fr"] = ent["free_date"]
+    return objs
+
+
+def write_replay_c(path: str, replay: Replay) -> None:
+    """Record a replay through the C-ABI capture bridge (nmg_replay_open /
+    add_ring / close): what the LD_PRELOAD host calls at finalize."""
+    t = replay.table
+    objs = table_objects(t)
+    meta, keep = build_meta(t)
+    keys = np.ascontiguousarray(t.keys, dtype=np.uint64)
+    off = np.ascontiguousarray(t.entry_off, dtype=np.uint32)
+    w = C.c_void_p()
+    check(lib.nmg_replay_open(C.byref(w), path.encode(), replay.nb_threads, _ptr(keys, C.c_uint64),
+                              _ptr(off, C.c_uint32), keys.shape[0], objs.ctypes.data_as(C.POINTER(_lib.nmg_object)),
+                              meta, t.nb_entries))
+    try:
+        for b in replay.buffers:
+            ring = np.ascontiguousarray(b.ring, dtype=np.uint8)
+            check(lib.nmg_replay_add_ring(w, ring.ctypes.data, ring.shape[0], b.data_tail, b.data_head,
+                                          b.thread_rank, b.access_type))
+    finally:
+        check(lib.nmg_replay_close(w))
 
 
 def build_meta(table: ObjectTable):

@@ -1,4 +1,6 @@
 """Replay format, ring linearisation (__copy_buffer) and the generator."""
+import os
+
 import numpy as np
 import pytest
 
@@ -71,3 +73,45 @@ def test_packed_alignment():
     lin = rp.linear_buffers()
     for (r, a, data), o, n in zip(lin, offs, lens):
         assert np.array_equal(arena[int(o):int(o) + int(n)], data)
+
+
+def test_c_replay_writer_matches_python(tmp_path):
+    """Capture bridge: a replay recorded through the C-ABI
+    writer holds the same table, pools and buffers as the Python writer's, and
+    the oracle's report on it is byte-identical."""
+    import pyoracle
+    from numamma_amd.engine import write_replay_c
+    from numamma_amd.replay import Replay, SynthConfig, generate
+
+    rp = generate(SynthConfig(nb_samples=30_000, nb_intervals=400, lost_frac=1e-3, wrap_one=True, seed=41))
+    pa, pb = str(tmp_path / "py.bin"), str(tmp_path / "c.bin")
+    rp.write(pa)
+    write_replay_c(pb, rp)
+    a, b = Replay.read(pa), Replay.read(pb)
+    assert a.nb_threads == b.nb_threads
+    assert np.array_equal(a.table.keys, b.table.keys) and np.array_equal(a.table.entry_off, b.table.entry_off)
+    plain = [f for f in a.table.entries.dtype.names if f not in ("callstack_off", "caller_off")]
+    for f in plain:
+        assert np.array_equal(a.table.entries[f], b.table.entries[f]), f
+    for ea, eb in zip(a.table.entries, b.table.entries):  # pools compared by content
+        n = int(ea["callstack_size"])
+        if ea["has_callstack"]:
+            assert np.array_equal(a.table.callstack_pool[ea["callstack_off"]:ea["callstack_off"] + n],
+                                  b.table.callstack_pool[eb["callstack_off"]:eb["callstack_off"] + n])
+        for t, e in ((a.table, ea), (b.table, eb)):
+            assert (int(e["caller_off"]) == 0xFFFFFFFF) == (int(ea["caller_off"]) == 0xFFFFFFFF)
+        if int(ea["caller_off"]) != 0xFFFFFFFF:
+            sa = a.table.string_pool[int(ea["caller_off"]):].split(b"\0")[0]
+            sb = b.table.string_pool[int(eb["caller_off"]):].split(b"\0")[0]
+            assert sa == sb
+    assert len(a.buffers) == len(b.buffers)
+    for x, y in zip(a.buffers, b.buffers):
+        assert (x.thread_rank, x.access_type, x.data_tail, x.data_head) == (y.thread_rank, y.access_type,
+                                                                           y.data_tail, y.data_head)
+        assert np.array_equal(x.ring, y.ring)
+    outs = []
+    for p in (pa, pb):
+        d = str(tmp_path / ("o_" + os.path.basename(p)))
+        pyoracle.run(p, d, d + ".txt", d + "_raw.bin")
+        outs.append((open(d + ".txt", "rb").read(), open(d + "_raw.bin", "rb").read(), open(d + "/call_sites.log", "rb").read()))
+    assert outs[0] == outs[1]
