@@ -54,6 +54,7 @@ extern "C" {
 #define NMG_F_MATCH_SAMPLES 0x1  /* settings.match_samples (numamma.h.in:27) */
 #define NMG_F_PAGE_HIST 0x2      /* per-(object, page, thread) counts for callsite_counters_<id>.dat */
 #define NMG_F_OBJECT_LEVELS 0x4  /* per-object level buckets (count, sum) for callsite_summary_<id>.dat */
+#define NMG_F_SAMPLE_MATCHES 0x8 /* keep every SAMPLE record's match (object or none) for the dump modes */
 #define NMG_F_DEFAULT (NMG_F_MATCH_SAMPLES | NMG_F_PAGE_HIST)
 
 /* struct count, src/mem_analyzer.h:10-15 */
@@ -103,8 +104,19 @@ struct nmg_options {
 struct nmg_report_options {
   const char *output_dir;  /* settings.output_dir; call_sites.log etc. land here */
   int32_t dump_single_items; /* write callsite_counters_<id>.dat (default 1) */
-  int32_t reserved;
+  int32_t dump_flags;        /* NMG_DUMP_*: the dump modes (engine created with
+                                NMG_F_SAMPLE_MATCHES | NMG_F_OBJECT_LEVELS) */
+  const char *maps_path;     /* NMG_DUMP_UNMATCHED header: the traced process's "/proc/<pid>/maps" */
+  const char *maps_text;     /* ... and that file's content, captured with the run (NULL: none) */
 };
+/* dump modes (settings.dump / dump_all / dump_unmatched, numamma.h.in:28-31;
+ * mem_sampling.c:599-650, 740-808, 895-914; mem_analyzer.c:1489-1528):
+ * callsite_dump_<id>.dat and callsite_summary_<id>.dat, all_memory_accesses.dat,
+ * unmatched_samples.log.  get_data_src_level() strings are numap's (unpinned
+ * beyond "L1_Hit", "L2_Hit", "L3_Hit", README.md:142-147). */
+#define NMG_DUMP_CALLSITES 0x1 /* -d */
+#define NMG_DUMP_ALL 0x2       /* -D */
+#define NMG_DUMP_UNMATCHED 0x4 /* -u */
 
 struct nmg_engine;
 typedef struct nmg_engine nmg_engine;

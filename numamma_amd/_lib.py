@@ -27,7 +27,9 @@ NMG_OK = 0
 NMG_F_MATCH_SAMPLES = 0x1
 NMG_F_PAGE_HIST = 0x2
 NMG_F_OBJECT_LEVELS = 0x4
+NMG_F_SAMPLE_MATCHES = 0x8
 NMG_F_DEFAULT = NMG_F_MATCH_SAMPLES | NMG_F_PAGE_HIST
+NMG_DUMP_CALLSITES, NMG_DUMP_ALL, NMG_DUMP_UNMATCHED = 0x1, 0x2, 0x4
 NMG_ARR_SUM64, NMG_ARR_MIN64, NMG_ARR_MAX64, NMG_ARR_HIST32 = range(4)
 ERRORS = {
     -1: "NMG_ERR_INVALID",
@@ -85,7 +87,8 @@ class nmg_options(C.Structure):
 
 
 class nmg_report_options(C.Structure):
-    _fields_ = [("output_dir", C.c_char_p), ("dump_single_items", C.c_int32), ("reserved", C.c_int32)]
+    _fields_ = [("output_dir", C.c_char_p), ("dump_single_items", C.c_int32), ("dump_flags", C.c_int32),
+                ("maps_path", C.c_char_p), ("maps_text", C.c_char_p)]
 
 
 class nmg_host_results(C.Structure):

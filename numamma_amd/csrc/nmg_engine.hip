@@ -163,6 +163,7 @@ struct Params {
   uint64_t* sparse_keys;
   uint32_t* sparse_vals;
   uint32_t* sparse_dirty;  // set on any sparse insert: the next reset must clear the table
+  uint32_t* smatch;        // NMG_F_SAMPLE_MATCHES: [(buffer offset + record offset) / 8] = entry + 1, 0 = none
   unsigned long long* dbg;  // kDbgTiming: [grid][waves][kTimingWords]
 };
 
@@ -524,7 +525,7 @@ template <int MODE>
 __device__ __forceinline__ void process_sample(Params& p, WgCounters& wc, LaneAcc& acc, const Lookup& L,
                                                bool valid, uint64_t ts, uint64_t addr,
                                                uint64_t w, uint64_t dsrc, uint32_t access,
-                                               uint32_t th, uint64_t seq, uint32_t off,
+                                               uint32_t th, uint64_t seq, uint32_t off, uint64_t rbase,
                                                uint64_t& vmask, uint64_t& fmask) {
   const uint32_t lvl = uint32_t(dsrc >> 5) & 0x3fff;  // data_src.mem_lvl
   // ---- global counters: update_counters(global_counters, ...) (mem_sampling.c:882)
@@ -577,6 +578,9 @@ __device__ __forceinline__ void process_sample(Params& p, WgCounters& wc, LaneAc
   if (valid) m = find_entry(p, L, addr, ts);
   const int64_t e = m.e;
   fmask = __ballot(e >= 0);
+  // dump modes: every SAMPLE record's match at its arena position (host
+  // formats the per-sample lines in analysis order)
+  if (p.smatch && valid) p.smatch[(rbase + off) >> 3] = e >= 0 ? (uint32_t)e + 1u : 0u;
   if (e < 0 || (p.flags & kDbgNoTables)) return;
   // per-object counters, aggregated per stream in LDS.  (Admitting an entry
   // only on its second sample -- a doorkeeper bitset -- was measured slower at
@@ -928,11 +932,12 @@ __global__ __launch_bounds__(kWG, 1) void attribute_kernel(Params p) {
     // the record this lane processes in this window
     Rec rec = r;
     bool valid;
-    uint64_t rseq;
+    uint64_t rseq, rbase;
     uint32_t roff;
     if (!(f & 1)) {
       valid = wl.cand && uint32_t(r.hdr) == kSampleType;
       rseq = wl.in1 ? d1.seq : d0.seq;
+      rbase = wl.in1 ? d1.offset : d0.offset;
       roff = wl.pos;
       // ---- fast path: one record per lane
       if (wl.n1) {
@@ -1003,6 +1008,7 @@ __global__ __launch_bounds__(kWG, 1) void attribute_kernel(Params p) {
       valid = (uint32_t)tid < n;
       roff = valid ? s_list[tid] : 0;
       rseq = d0.seq;
+      rbase = d0.offset;
       RawRec rr;
       load_rec(base, roff, valid ? len : 0, rr);
       rec = decode_rec(rr, roff);
@@ -1033,7 +1039,7 @@ __global__ __launch_bounds__(kWG, 1) void attribute_kernel(Params p) {
     uint64_t vm = 0, fm = 0;
     if (!(p.flags & kDbgLoadOnly))
       process_sample<MODE>(p, wc, acc, L, valid, rec.ts, rec.addr, rec.w, rec.dsrc, d0.access, d0.thread_rank, rseq, roff,
-                     vm, fm);
+                           rbase, vm, fm);
     {
       // lanes of this wave in buffer idx + 1 (tid >= n0)
       const uint32_t w0 = uint32_t(tid) & ~63u;
@@ -1234,7 +1240,7 @@ struct nmg_engine {
   uint8_t* d_fshift = nullptr;
   uint2* d_dir = nullptr;
   uint32_t nb_fences = 0, fence_log2 = 0, dir_log2 = 0;
-  std::vector<uint64_t> hist_base, npages, buffer_size;
+  std::vector<uint64_t> hist_base, npages, buffer_size, entry_addr;
   std::vector<uint32_t> sparse_entries;
   uint64_t hist_cells = 0;
   uint64_t hist_budget = 4ull << 30;
@@ -1247,6 +1253,8 @@ struct nmg_engine {
   uint64_t* d_sparse_keys = nullptr;
   uint32_t* d_sparse_vals = nullptr;
   uint32_t* d_sparse_dirty = nullptr;  // [2] parity flags (see reset_kernel)
+  uint32_t* d_smatch = nullptr;        // NMG_F_SAMPLE_MATCHES: per 8 B of the arena span
+  size_t smatch_cap = 0;
   uint64_t nreset = 0;
 
   // buffers
@@ -1435,6 +1443,7 @@ extern "C" void nmg_destroy(nmg_engine* h) {
   (void)hipFree(h->d_sdescs);
   (void)hipFree(h->d_ranges);
   (void)hipFree(h->d_dbg);
+  (void)hipFree(h->d_smatch);
   if (h->h_stage) (void)hipHostFree(h->h_stage);
   if (h->copy_stream) (void)hipStreamSynchronize(h->copy_stream);
   for (auto& sl : h->slots) {
@@ -1580,6 +1589,7 @@ extern "C" int nmg_set_objects(nmg_engine* h, const uint64_t* keys, const uint32
   h->hist_base.assign(nb_entries, kHistSparse);
   h->npages.resize(nb_entries);
   h->buffer_size.resize(nb_entries);
+  h->entry_addr.resize(nb_entries);
   h->sparse_entries.clear();
   h->hist_cells = 0;
   std::vector<DevEntry> dev(nb_entries);
@@ -1596,6 +1606,7 @@ extern "C" int nmg_set_objects(nmg_engine* h, const uint64_t* keys, const uint32
     uint64_t np = o.buffer_size / kPageSize + 1;
     h->npages[e] = np;
     h->buffer_size[e] = o.buffer_size;
+    h->entry_addr[e] = o.buffer_addr;
     d.hist = kHistSparse;
     d.sidx = ~0u;
     if (!want_hist) continue;
@@ -1964,6 +1975,8 @@ static int stream_append(nmg_engine* h, uint64_t len, uint32_t thread_rank, uint
 extern "C" int nmg_stream_begin(nmg_engine* h, uint64_t chunk_bytes, uint32_t copy_threads) {
   if (!h || copy_threads == 0) return NMG_ERR_INVALID;
   if (h->external) return fail(h, NMG_ERR_STATE, "device buffers are set; call nmg_clear_buffers first");
+  if (h->flags & NMG_F_SAMPLE_MATCHES)
+    return fail(h, NMG_ERR_STATE, "dump modes (NMG_F_SAMPLE_MATCHES) need nmg_analyze over submitted buffers");
   if (h->staged_dirty || (!h->streaming && !h->streamed && !h->descs.empty()))
     return fail(h, NMG_ERR_STATE, "buffers already submitted; call nmg_clear_buffers first");
   HIP_TRY(h, hipSetDevice(h->device));
@@ -2225,6 +2238,7 @@ static int launch_attribution(nmg_engine* h, const uint8_t* data, const BufDesc*
   p.sparse_keys = h->d_sparse_keys;
   p.sparse_vals = h->d_sparse_vals;
   p.sparse_dirty = h->d_sparse_dirty ? h->d_sparse_dirty + (h->nreset & 1) : nullptr;
+  p.smatch = (h->flags & NMG_F_SAMPLE_MATCHES) ? h->d_smatch : nullptr;
   // dense LDS tables when the table is small enough (DESIGN.md "Kernels")
   const int mode = (h->E <= kObjSlots ? kModeDenseObj : 0) |
                    (h->hist_cells <= kDensePageCells ? kModeDensePage : 0);
@@ -2270,6 +2284,18 @@ extern "C" int nmg_analyze(nmg_engine* h) {
   int rc = upload_buffers(h);
   if (rc) return rc;
   const uint32_t nb = (uint32_t)h->descs.size();
+  if (h->flags & NMG_F_SAMPLE_MATCHES) {  // one u32 per 8 B of the buffers' arena span
+    uint64_t span = 0;
+    for (const BufDesc& d : h->descs) span = std::max<uint64_t>(span, d.offset + d.len);
+    const size_t need = (size_t)(span / 8 + 1);
+    if (need > h->smatch_cap) {
+      HIP_TRY(h, hipStreamSynchronize(h->stream));
+      (void)hipFree(h->d_smatch);
+      h->d_smatch = nullptr;
+      HIP_TRY(h, hipMalloc(&h->d_smatch, need * 4));
+      h->smatch_cap = need;
+    }
+  }
   ensure_occupancy(h);
   // persistent grid: one resident workgroup per slot, each with a byte-balanced range
   const uint32_t grid = nb ? std::min<uint32_t>(nb, (uint32_t)(h->num_cus * h->blocks_per_cu)) : 0;
@@ -2673,8 +2699,36 @@ extern "C" int nmg_report(nmg_engine* h, const nmg_object_meta* meta, const nmg_
   res.nb_cells = ncells;
   res.nb_threads = h->T;
   res.match_samples = (h->flags & NMG_F_MATCH_SAMPLES) ? 1 : 0;
+  // dump modes: the buffers' bytes (staging, or D2H of device-resident ones)
+  // and every SAMPLE record's match
+  DumpInput dump;
+  std::vector<uint8_t> dev_bytes;
+  std::vector<uint32_t> smatch;
+  const bool dumps = opts && opts->dump_flags && (h->flags & NMG_F_MATCH_SAMPLES);
+  if (dumps) {
+    if (!(h->flags & NMG_F_SAMPLE_MATCHES) || !(h->flags & NMG_F_OBJECT_LEVELS))
+      return fail(h, NMG_ERR_STATE, "dump modes need an engine created with NMG_F_SAMPLE_MATCHES | NMG_F_OBJECT_LEVELS");
+    if (h->streamed || h->counts_override)
+      return fail(h, NMG_ERR_STATE, "dump modes need the buffers of one nmg_analyze on this engine");
+    uint64_t span = 0;
+    for (const BufDesc& d : h->descs) span = std::max<uint64_t>(span, d.offset + d.len);
+    smatch.resize(span / 8 + 1);
+    if (!h->descs.empty()) {
+      HIP_TRY(h, hipMemcpy(smatch.data(), h->d_smatch, smatch.size() * 4, hipMemcpyDeviceToHost));
+    }
+    const uint8_t* base = h->h_stage;
+    if (h->external) {
+      dev_bytes.resize(span);
+      if (span) HIP_TRY(h, hipMemcpy(dev_bytes.data(), h->d_data, span, hipMemcpyDeviceToHost));
+      base = dev_bytes.data();
+    }
+    for (const BufDesc& d : h->descs)
+      dump.buffers.push_back({base + d.offset, d.len, d.thread_rank, d.access, smatch.data() + d.offset / 8});
+    dump.entry_addr = h->entry_addr.data();
+    dump.levels = r.levels.data();
+  }
   std::string err;
-  rc = write_report(&res, meta, opts, stdout_path, err);
+  rc = write_report(&res, meta, opts, stdout_path, err, dumps ? &dump : nullptr);
   if (rc && !err.empty()) h->last_error = err;
   return rc;
 }

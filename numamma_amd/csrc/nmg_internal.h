@@ -74,8 +74,21 @@ constexpr uint32_t sparse_key_idx(uint64_t k) { return uint32_t(k >> 42); }
 constexpr uint32_t sparse_key_thread(uint64_t k) { return uint32_t((k >> 32) & 0x3ff); }
 constexpr uint32_t sparse_key_page(uint64_t k) { return uint32_t(k); }
 
+// ---- dump modes: what the report writer needs besides the counters
+struct DumpBuffer {
+  const uint8_t* data;    // the linearised buffer
+  uint64_t len;
+  uint32_t thread_rank, access;
+  const uint32_t* match;  // [byte offset / 8] = entry + 1 for SAMPLE records, 0 = unmatched
+};
+struct DumpInput {
+  std::vector<DumpBuffer> buffers;  // analysis order
+  const uint64_t* entry_addr;       // [E] buffer_addr (sample offsets)
+  const uint64_t* levels;           // [E][2][kLevelWords] (callsite_summary_<id>.dat)
+};
+
 // ---- report writer (nmg_report.cpp)
 int write_report(const nmg_host_results* r, const nmg_object_meta* meta, const nmg_report_options* opts,
-                 const char* stdout_path, std::string& err);
+                 const char* stdout_path, std::string& err, const DumpInput* dump = nullptr);
 
 }  // namespace nmg

@@ -22,6 +22,7 @@
 #include <cstdio>
 #include <cstring>
 #include <functional>
+#include <set>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -264,10 +265,76 @@ struct SiteHist {
   }
 };
 
+// get_data_src_level() belongs to numap (unpinned HEAD, absent here): only
+// "L1_Hit", "L2_Hit" and "L3_Hit" are pinned, by README.md:142-147.  The same
+// restatement as the oracle's o_data_src_level: the first level bit present
+// names the level, then "_Hit" / "_Miss".
+std::string data_src_level(uint64_t data_src) {
+  const uint32_t lvl = (uint32_t)(data_src >> 5) & 0x3fff;  // union perf_mem_data_src.mem_lvl
+  static const struct {
+    uint32_t bit;
+    const char* name;
+  } names[] = {{0x01, "NA"},
+               {0x08, "L1"},
+               {0x10, "LFB"},
+               {0x20, "L2"},
+               {0x40, "L3"},
+               {0x80, "Local_RAM"},
+               {0x100, "Remote_RAM_1_hop"},
+               {0x200, "Remote_RAM_2_hops"},
+               {0x400, "Remote_Cache_1_hop"},
+               {0x800, "Remote_Cache_2_hops"},
+               {0x1000, "IO_Memory"},
+               {0x2000, "Uncached_Memory"}};
+  const char* n = "Unknown";
+  for (const auto& x : names)
+    if (lvl & x.bit) {
+      n = x.name;
+      break;
+    }
+  return std::string(n) + ((lvl & 0x02) ? "_Hit" : ((lvl & 0x04) ? "_Miss" : ""));
+}
+
+template <class T>
+T load(const uint8_t* p) {
+  T v;
+  memcpy(&v, p, sizeof(T));
+  return v;
+}
+
+// The unmatched-sample log header (mem_sampling.c:608-638): the traced
+// process's maps file copied by `while (!feof) { fgets(line, 1024); fprintf }`,
+// which repeats the last line when the file ends with a newline.
+void write_maps_header(FILE* f, const nmg_report_options* opts) {
+  fprintf(f, "# %s content:\n", opts->maps_path ? opts->maps_path : "/proc/self/maps");
+  const char* t = opts->maps_text ? opts->maps_text : "";
+  const size_t len = strlen(t);
+  char line[1024];
+  line[0] = 0;
+  size_t pos = 0;
+  bool eof = len == 0;
+  while (!eof) {
+    if (pos >= len) {
+      eof = true;  // fgets returns NULL; line keeps the last line
+    } else {
+      size_t n = 0;
+      while (pos < len && n < sizeof(line) - 1) {
+        line[n++] = t[pos++];
+        if (line[n - 1] == '\n') break;
+      }
+      line[n] = 0;
+      if (pos >= len && line[n - 1] != '\n') eof = true;  // EOF met inside the last line
+    }
+    fprintf(f, "# %s", line);
+  }
+  fprintf(f, "#\n#\n#\n");
+  fprintf(f, "#thread_rank timestamp address mem_level access_weight access_type\n");
+}
+
 }  // namespace
 
 int write_report(const nmg_host_results* r, const nmg_object_meta* meta, const nmg_report_options* opts,
-                 const char* stdout_path, std::string& err) {
+                 const char* stdout_path, std::string& err, const DumpInput* dump) {
   const uint32_t E = r->nb_entries;
   const uint32_t T = r->nb_threads;
   FILE* out = stdout;
@@ -334,16 +401,141 @@ int write_report(const nmg_host_results* r, const nmg_object_meta* meta, const n
   }
   std::vector<Site>& sites = reg.sites;
 
+  // ---- dump modes (mem_sampling.c:895-914): per SAMPLE record in analysis order
+  const char* dir = opts && opts->output_dir ? opts->output_dir : ".";
+  const int dflags = opts ? opts->dump_flags : 0;
+  const bool dump_single = opts ? opts->dump_single_items != 0 : true;
+  mkdir(dir, S_IRWXU);  // get_log_dir (mem_intercept.c:402-409)
+  std::vector<FILE*> site_file(sites.size(), nullptr);
+  FILE* all_file = nullptr;
+  FILE* unmatched_file = nullptr;
+  auto open_out = [&](const std::string& base) -> FILE* {
+    FILE* f = fopen((std::string(dir) + "/" + base).c_str(), "w");
+    if (!f) err = "cannot open " + std::string(dir) + "/" + base;
+    return f;
+  };
+  auto close_dumps = [&]() {
+    for (FILE*& f : site_file)
+      if (f) fclose(f), f = nullptr;
+    if (all_file) fclose(all_file), all_file = nullptr;
+    if (unmatched_file) fclose(unmatched_file), unmatched_file = nullptr;
+  };
+  if (dflags & NMG_DUMP_UNMATCHED) {  // opened at init (mem_intercept.c:528-535)
+    unmatched_file = open_out("unmatched_samples.log");
+    if (!unmatched_file) {
+      close_out();
+      return NMG_ERR_IO;
+    }
+  }
+  if (dump && r->match_samples) {
+    bool maps_read = false;
+    const bool dump_matched = dflags & (NMG_DUMP_CALLSITES | NMG_DUMP_ALL);
+    for (const DumpBuffer& b : dump->buffers) {
+      const char acc = b.access == NMG_ACCESS_READ ? 'r' : 'w';
+      for (uint64_t cur = 0; cur + 8 <= b.len;) {
+        const uint32_t type = load<uint32_t>(b.data + cur);
+        const uint16_t size = load<uint16_t>(b.data + cur + 6);
+        if (size == 0) break;  // (the analysis already reported it)
+        if (type == 9 && cur + 40 <= b.len) {
+          const uint64_t ts = load<uint64_t>(b.data + cur + 8), addr = load<uint64_t>(b.data + cur + 16);
+          const uint64_t w = load<uint64_t>(b.data + cur + 24), dsrc = load<uint64_t>(b.data + cur + 32);
+          const uint32_t m = b.match[cur / 8];
+          if (!m) {
+            if (unmatched_file) {
+              if (!maps_read) {
+                write_maps_header(unmatched_file, opts);
+                maps_read = true;
+              }
+              fprintf(unmatched_file, "%u %" PRIu64 " 0x%" PRIxPTR " %s %" PRIu64 " %c\n", b.thread_rank, ts,
+                      (uintptr_t)addr, data_src_level(dsrc).c_str(), w, acc);
+            }
+          } else if (dump_matched) {
+            const uint32_t e = m - 1;
+            const uint64_t offset = addr - dump->entry_addr[e];
+            if ((dflags & NMG_DUMP_ALL) && meta[e].mem_type != kMemTypeStack) {  // _dump_mem_info (:740-773)
+              if (!all_file) {
+                if (!(all_file = open_out("all_memory_accesses.dat"))) break;
+                fprintf(all_file, "#thread_rank timestamp object_id offset mem_level access_weight access_type\n");
+              }
+              fprintf(all_file, "%u %" PRIu64 " %u %" PRIu64 " %s %" PRIu64 " %c\n", b.thread_rank, ts, meta[e].id,
+                      offset, data_src_level(dsrc).c_str(), w, acc);
+            }
+            if (dump_single && meta[e].mem_type != kMemTypeStack) {  // _dump_call_site (:775-808)
+              const int64_t si = reg.find(e);
+              if (si >= 0) {
+                if (!site_file[si]) {
+                  char fn[64];
+                  snprintf(fn, sizeof(fn), "callsite_dump_%d.dat", (int)sites[si].id);
+                  if (!(site_file[si] = open_out(fn))) break;
+                  fprintf(site_file[si], "#thread_rank timestamp offset mem_level access_weight access_type\n");
+                }
+                fprintf(site_file[si], "%u %" PRIu64 " %" PRIuPTR " %s %" PRIu64 " %c\n", b.thread_rank, ts,
+                        (uintptr_t)offset, data_src_level(dsrc).c_str(), w, acc);
+              }
+            }
+          }
+        }
+        cur += size;
+      }
+      if (!err.empty()) {
+        close_dumps();
+        close_out();
+        return NMG_ERR_IO;
+      }
+    }
+  }
+
   // ---- ma_finalize prints (mem_analyzer.c:1877-1881)
   print_counters(out, r->global);
   fprintf(out, "Summary of the call sites:\n");
   fprintf(out, "--------------------------\n");
   fprintf(out, "Sorting call sites\n");
   std::vector<int64_t> order = sort_sites(sites);
-
-  const char* dir = opts && opts->output_dir ? opts->output_dir : ".";
-  const bool dump_single = opts ? opts->dump_single_items != 0 : true;
-  mkdir(dir, S_IRWXU);  // get_log_dir (mem_intercept.c:402-409)
+  // __remove_site during the sort (mem_analyzer.c:1506-1528): the site the
+  // walk stops at -- the removed one when it heads the list, else its
+  // predecessor (quirk Q10) -- gets callsite_summary_<id>.dat and its dump
+  // file closed, if it has one.  The list is id-descending; removals run in
+  // the reverse of the final order.
+  if (dump) {
+    std::set<int64_t> remaining;
+    for (int64_t i = 0; i < (int64_t)sites.size(); i++) remaining.insert(i);
+    for (auto it = order.rbegin(); it != order.rend(); ++it) {
+      auto pos = remaining.find(*it);
+      auto nxt = std::next(pos);
+      const int64_t cur = nxt == remaining.end() ? *it : *nxt;
+      remaining.erase(pos);
+      if (!site_file[cur]) continue;
+      // __print_call_site_stats (:1489-1503): the cumulated counters, whose
+      // min / max stay 0 (memset, and ACC_COUNTER's inverted tests: Q8)
+      nmg_mem_counters cc[2];
+      memset(cc, 0, sizeof(cc));
+      for (uint32_t e : sites[cur].objects)
+        for (uint32_t a = 0; a < 2; a++) {
+          const uint64_t* cw = r->count_weight + (uint64_t)e * 4 + a * 2;
+          const uint64_t* lv = dump->levels + ((uint64_t)e * 2 + a) * kLevelWords;
+          cc[a].total_count += cw[0];
+          cc[a].total_weight += cw[1];
+          cc[a].na_miss_count += lv[0];
+          for (int k = 0; k < 18; k++) {
+            cc[a].b[k].count += lv[1 + 2 * k];
+            cc[a].b[k].sum_weight += lv[2 + 2 * k];
+          }
+        }
+      char fn[64];
+      snprintf(fn, sizeof(fn), "callsite_summary_%d.dat", (int)sites[cur].id);
+      FILE* sf = open_out(fn);
+      if (!sf) {
+        close_dumps();
+        close_out();
+        return NMG_ERR_IO;
+      }
+      print_counters(sf, cc);
+      fclose(sf);
+      fclose(site_file[cur]);
+      site_file[cur] = nullptr;
+    }
+  }
+  close_dumps();  // the rest stay open until exit in the reference
   std::string cs_path = std::string(dir) + "/call_sites.log";
   FILE* cf = fopen(cs_path.c_str(), "w");
   if (!cf) {

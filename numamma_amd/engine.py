@@ -170,9 +170,14 @@ class Engine:
         return rows
 
     # ------------------------------------------------------------------
-    def report(self, output_dir: str, stdout_path: Optional[str] = None, dump_single_items: int = 1):
+    def report(self, output_dir: str, stdout_path: Optional[str] = None, dump_single_items: int = 1,
+               dump_flags: int = 0, maps_path: Optional[str] = None, maps_text: Optional[str] = None):
+        """nmg_report; dump_flags = NMG_DUMP_* (engine created with
+        NMG_F_SAMPLE_MATCHES | NMG_F_OBJECT_LEVELS)."""
         meta, keep = build_meta(self.table)
-        ro = _lib.nmg_report_options(output_dir.encode(), dump_single_items, 0)
+        ro = _lib.nmg_report_options(output_dir.encode(), dump_single_items, dump_flags,
+                                     maps_path.encode() if maps_path else None,
+                                     maps_text.encode() if maps_text else None)
         self._c(lib.nmg_report(self.h, meta, C.byref(ro), stdout_path.encode() if stdout_path else None))
         del keep
 

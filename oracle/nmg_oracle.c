@@ -108,6 +108,7 @@ struct o_site {
   uint64_t mem_info_buffer_size; /* site->mem_info.buffer_size (:1363) */
   struct o_block **blocks;       /* site->mem_info.blocks */
   struct o_block cumulated;      /* site->cumulated_counters */
+  FILE *dump_file;               /* site->dump_file: callsite_dump_<id>.dat (dump modes) */
   struct o_site *next;
 };
 
@@ -132,6 +133,13 @@ struct o_state {
   uint32_t *buf_samples, *buf_found;
   struct o_site *call_sites; /* mem_analyzer.c:1300 */
   uint32_t next_call_site_id;
+  /* dump modes (settings.dump / dump_all / dump_unmatched) */
+  const struct nmo_settings *set;
+  const char *outdir;
+  FILE *dump_all_file;       /* mem_sampling.c:24 */
+  FILE *dump_unmatched_file; /* mem_intercept.c:26, opened at init (:528-535) */
+  int maps_read;             /* mem_sampling.c:608 */
+  int dump_err;
   /* raw file bytes */
   uint8_t *file;
   size_t file_size;
@@ -525,11 +533,11 @@ static void o_update_call_sites(struct o_state *st, struct o_mem *m) {
 /* analysis                                                            */
 
 /* __match_sample -- src/mem_sampling.c:594-673 */
-static int o_match_sample(struct o_state *st, uint64_t addr, uint64_t ts,
-                          uint64_t weight, uint64_t data_src, int access,
-                          unsigned th, uint64_t ordinal) {
+static int64_t o_match_sample(struct o_state *st, uint64_t addr, uint64_t ts,
+                              uint64_t weight, uint64_t data_src, int access,
+                              unsigned th, uint64_t ordinal) {
   int64_t e = o_find(st, addr, ts);
-  if (e < 0) return 0;
+  if (e < 0) return -1;
   struct o_mem *m = &st->mems[e];
   if (!m->blocks) m->blocks = o_allocate_counters();
   if (ordinal < m->first_ordinal) m->first_ordinal = ordinal;
@@ -539,7 +547,106 @@ static int o_match_sample(struct o_state *st, uint64_t addr, uint64_t ts,
     m->call_site = o_find_call_site(st, m);
     if (!m->call_site) m->call_site = o_new_call_site(st, m);
   }
-  return 1;
+  return e;
+}
+
+/* ------------------------------------------------------------------ */
+/* dump modes -- src/mem_sampling.c:599-650, 740-808, 895-914          */
+
+/* get_data_src_level() belongs to numap (unpinned HEAD, absent here): only
+ * "L1_Hit", "L2_Hit" and "L3_Hit" are pinned, by the reference's README
+ * (README.md:142-147).  Restated: the first level bit present names the
+ * level, then "_Hit" / "_Miss"; the engine's report writer uses the same
+ * restatement (parity unpinned beyond those three strings). */
+static void o_data_src_level(uint64_t data_src, char *out) {
+  const uint32_t lvl = (uint32_t)(data_src >> 5) & 0x3fff; /* union perf_mem_data_src.mem_lvl */
+  static const struct { uint32_t bit; const char *name; } names[] = {
+      {LVL_NA, "NA"}, {LVL_L1, "L1"}, {LVL_LFB, "LFB"}, {LVL_L2, "L2"}, {LVL_L3, "L3"},
+      {LVL_LOC_RAM, "Local_RAM"}, {LVL_REM_RAM1, "Remote_RAM_1_hop"}, {LVL_REM_RAM2, "Remote_RAM_2_hops"},
+      {LVL_REM_CCE1, "Remote_Cache_1_hop"}, {LVL_REM_CCE2, "Remote_Cache_2_hops"}, {LVL_IO, "IO_Memory"},
+      {LVL_UNC, "Uncached_Memory"}};
+  const char *n = "Unknown";
+  for (unsigned i = 0; i < sizeof(names) / sizeof(names[0]); i++)
+    if (lvl & names[i].bit) {
+      n = names[i].name;
+      break;
+    }
+  sprintf(out, "%s%s", n, (lvl & LVL_HIT) ? "_Hit" : ((lvl & LVL_MISS) ? "_Miss" : ""));
+}
+
+static FILE *o_open_out(struct o_state *st, const char *base) {
+  char fn[4096];
+  snprintf(fn, sizeof(fn), "%s/%s", st->outdir ? st->outdir : ".", base);
+  FILE *f = fopen(fn, "w");
+  if (!f) st->dump_err = NMO_ERR_IO;
+  return f;
+}
+
+/* the unmatched branch of __match_sample (:602-650).  The header copies the
+ * traced process's /proc/<pid>/maps with `while(!feof) { fgets; fprintf }`,
+ * which prints the last line twice when the file ends with a newline. */
+static void o_dump_unmatched(struct o_state *st, const struct o_buffer *buf, uint64_t ts, uint64_t addr,
+                             uint64_t weight, uint64_t dsrc) {
+  FILE *f = st->dump_unmatched_file;
+  if (!f) return;
+  if (!st->maps_read) {
+    fprintf(f, "# %s content:\n", st->set->maps_path ? st->set->maps_path : "/proc/self/maps");
+    const char *t = st->set->maps_text ? st->set->maps_text : "";
+    char line[1024];
+    line[0] = 0;
+    size_t pos = 0, len = strlen(t);
+    int eof = len == 0;
+    while (!eof) { /* fgets(line, 1024, maps) over the captured text */
+      if (pos >= len) {
+        eof = 1; /* fgets returns NULL, line unchanged */
+      } else {
+        size_t n = 0;
+        while (pos < len && n < sizeof(line) - 1) {
+          line[n++] = t[pos++];
+          if (line[n - 1] == '\n') break;
+        }
+        line[n] = 0;
+        if (pos >= len && line[n - 1] != '\n') eof = 1; /* EOF hit while reading */
+      }
+      fprintf(f, "# %s", line);
+    }
+    fprintf(f, "#\n#\n#\n");
+    st->maps_read = 1;
+    fprintf(f, "#thread_rank timestamp address mem_level access_weight access_type\n");
+  }
+  char lvl[64];
+  o_data_src_level(dsrc, lvl);
+  fprintf(f, "%u %" PRIu64 " 0x%" PRIxPTR " %s %" PRIu64 " %c\n", buf->thread_rank, ts, (uintptr_t)addr, lvl,
+          weight, buf->access_type == ACCESS_READ ? 'r' : 'w');
+}
+
+/* _dump_mem_info (:740-773) and _dump_call_site (:775-808) */
+static void o_dump_matched(struct o_state *st, const struct o_buffer *buf, struct o_mem *m, uint64_t ts,
+                           uint64_t offset, uint64_t weight, uint64_t dsrc) {
+  char lvl[64];
+  o_data_src_level(dsrc, lvl);
+  const char acc = buf->access_type == ACCESS_READ ? 'r' : 'w';
+  if (st->set->dump_all && m->mem_type != MEM_TYPE_STACK) {
+    if (!st->dump_all_file) {
+      st->dump_all_file = o_open_out(st, "all_memory_accesses.dat");
+      if (!st->dump_all_file) return;
+      fprintf(st->dump_all_file, "#thread_rank timestamp object_id offset mem_level access_weight access_type\n");
+    }
+    fprintf(st->dump_all_file, "%u %" PRIu64 " %u %" PRIu64 " %s %" PRIu64 " %c\n", buf->thread_rank, ts, m->id,
+            offset, lvl, weight, acc);
+  }
+  if (st->set->dump_single_items && m->call_site && m->mem_type != MEM_TYPE_STACK) {
+    struct o_site *site = m->call_site;
+    if (!site->dump_file) {
+      char base[64];
+      snprintf(base, sizeof(base), "callsite_dump_%d.dat", (int)site->id);
+      site->dump_file = o_open_out(st, base);
+      if (!site->dump_file) return;
+      fprintf(site->dump_file, "#thread_rank timestamp offset mem_level access_weight access_type\n");
+    }
+    fprintf(site->dump_file, "%u %" PRIu64 " %" PRIuPTR " %s %" PRIu64 " %c\n", buf->thread_rank, ts,
+            (uintptr_t)offset, lvl, weight, acc);
+  }
 }
 
 /* __analyze_buffer -- src/mem_sampling.c:815-927 on a linearised copy
@@ -565,11 +672,18 @@ static int o_analyze_buffer(struct o_state *st, uint32_t bidx, int match_samples
       uint64_t weight = rd_u64(ev + 24), dsrc = rd_u64(ev + 32);
       (*nb_samples)++;
       o_update_counters(st->global_counters, weight, dsrc, (int)buf->access_type);
+      int64_t e = -1;
       if (match_samples) {
         uint64_t ordinal = ((uint64_t)bidx << 32) | cur;
-        if (o_match_sample(st, addr, ts, weight, dsrc, (int)buf->access_type,
-                           buf->thread_rank, ordinal))
+        e = o_match_sample(st, addr, ts, weight, dsrc, (int)buf->access_type, buf->thread_rank, ordinal);
+        if (e >= 0)
           (*found)++;
+        else if (st->set && st->set->dump_unmatched)
+          o_dump_unmatched(st, buf, ts, addr, weight, dsrc);
+      }
+      if (st->set && (st->set->dump || st->set->dump_all) && e >= 0) {
+        struct o_mem *m = &st->mems[e];
+        o_dump_matched(st, buf, m, ts, addr - m->buffer_addr, weight, dsrc);
       }
     }
     cur += size; /* :918 */
@@ -621,19 +735,38 @@ static void o_print_counters(FILE *f, const struct o_counters *counters) {
   }
 }
 
-/* __remove_site -- src/mem_analyzer.c:1506-1528 (dump_file always NULL here) */
+/* __print_call_site_stats -- src/mem_analyzer.c:1489-1503 */
+static void o_print_call_site_stats(struct o_state *st, struct o_site *site) {
+  char base[64];
+  snprintf(base, sizeof(base), "callsite_summary_%d.dat", (int)site->id);
+  FILE *f = o_open_out(st, base);
+  if (!f) return;
+  o_print_counters(f, site->cumulated.counters);
+  fclose(f);
+}
+
+/* __remove_site -- src/mem_analyzer.c:1506-1528.  On leaving, the site the
+ * walk stopped at -- the removed site itself when it was the head, else its
+ * predecessor (quirk Q10) -- has its summary written and its dump file closed
+ * when it has one (dump modes). */
 static void o_remove_site(struct o_state *st, struct o_site *site) {
   struct o_site *cur = st->call_sites;
   if (cur == site) {
     st->call_sites = cur->next;
-    return;
+    goto out;
   }
   while (cur->next) {
     if (cur->next == site) {
       cur->next = site->next;
-      return;
+      goto out;
     }
     cur = cur->next;
+  }
+out:
+  if (cur && cur->dump_file) {
+    o_print_call_site_stats(st, cur);
+    fclose(cur->dump_file);
+    cur->dump_file = NULL;
   }
 }
 
@@ -864,6 +997,17 @@ int nmo_run(const char *replay_path, const char *outdir, const char *stdout_path
     }
   }
   if (outdir) mkdir(outdir, 0700);
+  struct nmo_settings defaults = {1, 1, 0, 0, 0, 0, NULL, NULL};
+  st.set = settings ? settings : &defaults;
+  st.outdir = outdir;
+  if (st.set->dump_unmatched) { /* opened at init, mem_intercept.c:528-535 */
+    st.dump_unmatched_file = o_open_out(&st, "unmatched_samples.log");
+    if (!st.dump_unmatched_file) {
+      if (out != stdout) fclose(out);
+      o_free(&st);
+      return NMO_ERR_IO;
+    }
+  }
   o_init_counters(&st.global_counters[0]); /* mem_sampling.c:212-213 */
   o_init_counters(&st.global_counters[1]);
   st.buf_samples = calloc(st.nb_buffers ? st.nb_buffers : 1, 4);
@@ -914,6 +1058,12 @@ int nmo_run(const char *replay_path, const char *outdir, const char *stdout_path
           st.nb_samples_total, st.nb_samples_total - st.nb_found_samples_total, percent);
   double t2 = o_now();
   if (out != stdout) fclose(out);
+  /* files still open at exit are flushed by the C runtime in the reference */
+  for (struct o_site *s = st.call_sites; s; s = s->next)
+    if (s->dump_file) fclose(s->dump_file), s->dump_file = NULL;
+  if (st.dump_all_file) fclose(st.dump_all_file);
+  if (st.dump_unmatched_file) fclose(st.dump_unmatched_file); /* mem_intercept.c:582-584 */
+  if (!rc && st.dump_err) rc = st.dump_err;
   if (!rc && raw_path) rc = o_write_raw(&st, raw_path);
   if (timing) {
     timing->analysis_s = t1 - t0;
@@ -965,7 +1115,7 @@ int main(int argc, char **argv) {
     fprintf(stderr, "usage: %s replay.bin outdir [raw.bin] [--no-match]\n", argv[0]);
     return 2;
   }
-  struct nmo_settings s = {1, 1};
+  struct nmo_settings s = {1, 1, 0, 0, 0, 0, NULL, NULL};
   const char *raw = NULL;
   for (int i = 3; i < argc; i++) {
     if (!strcmp(argv[i], "--no-match")) s.match_samples = 0;

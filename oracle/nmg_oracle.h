@@ -14,6 +14,12 @@
 struct nmo_settings {
   int match_samples;     /* settings.match_samples (numamma.h.in:27) */
   int dump_single_items; /* settings.dump_single_items (numamma.h.in:32) */
+  int dump;              /* settings.dump, -d (numamma.h.in:28) */
+  int dump_all;          /* settings.dump_all, -D (numamma.h.in:29) */
+  int dump_unmatched;    /* settings.dump_unmatched, -u (numamma.h.in:31) */
+  int reserved;
+  const char *maps_path; /* "/proc/<pid>/maps" of the traced process (unmatched_samples.log header) */
+  const char *maps_text; /* that file's content, captured with the run (NULL: empty) */
 };
 
 struct nmo_timing {

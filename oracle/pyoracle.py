@@ -22,7 +22,9 @@ def build(quiet: bool = True) -> None:
 
 
 class _Settings(C.Structure):
-    _fields_ = [("match_samples", C.c_int), ("dump_single_items", C.c_int)]
+    _fields_ = [("match_samples", C.c_int), ("dump_single_items", C.c_int), ("dump", C.c_int),
+                ("dump_all", C.c_int), ("dump_unmatched", C.c_int), ("reserved", C.c_int),
+                ("maps_path", C.c_char_p), ("maps_text", C.c_char_p)]
 
 
 class _Timing(C.Structure):
@@ -49,9 +51,14 @@ def oracle():
 
 
 def run(replay_path: str, outdir: str, stdout_path: str, raw_path: str | None = None,
-        match_samples: bool = True, dump_single_items: bool = True) -> dict:
+        match_samples: bool = True, dump_single_items: bool = True, dump: bool = False,
+        dump_all: bool = False, dump_unmatched: bool = False, maps_path: str | None = None,
+        maps_text: str | None = None) -> dict:
+    """Dump modes (-d / -D / -u) write callsite_dump_<id>.dat, callsite_summary_<id>.dat,
+    all_memory_accesses.dat and unmatched_samples.log into outdir like the reference."""
     lib = oracle()
-    s = _Settings(int(match_samples), int(dump_single_items))
+    s = _Settings(int(match_samples), int(dump_single_items), int(dump), int(dump_all), int(dump_unmatched), 0,
+                  maps_path.encode() if maps_path else None, maps_text.encode() if maps_text else None)
     t = _Timing()
     rc = lib.nmo_run(replay_path.encode(), outdir.encode(), stdout_path.encode(),
                      raw_path.encode() if raw_path else None, C.byref(s), C.byref(t))

@@ -445,3 +445,52 @@ def test_sparse_table_reset_cycles():
         eng.synchronize()
         assert np.array_equal(eng.page_cells(), once)
     eng.close()
+
+
+# ---- dump modes: -d / -D / -u and callsite_summary_<id>.dat
+MAPS = ("00400000-00452000 r-xp 00000000 08:02 173521 /usr/bin/app\n"
+        "555500000000-555600000000 rw-p 00000000 00:00 0 [heap]\n"
+        "7ffd0000-7ffd1000 rw-p 00000000 00:00 0 [stack]\n")
+
+
+@pytest.mark.parametrize("dump,dump_all,unmatched,single,resident", [
+    (1, 0, 0, 1, False), (0, 1, 0, 1, False), (1, 1, 1, 1, False), (0, 0, 1, 1, True),
+    (1, 1, 1, 0, True), (1, 1, 1, 1, True)])
+def test_dump_modes_bit_exact(tmp_path, dump, dump_all, unmatched, single, resident):
+    """Every dump file byte-identical to the oracle's: callsite_dump_<id>.dat,
+    callsite_summary_<id>.dat for the sort's predecessor sites (Q10),
+    all_memory_accesses.dat, unmatched_samples.log with the maps header
+    (last line repeated by the reference's feof loop); staged and
+    device-resident buffers."""
+    import torch
+    from numamma_amd.engine import Engine
+
+    d = str(tmp_path)
+    rp = generate(SynthConfig(nb_samples=40_000, nb_intervals=300, lost_frac=2e-3, wrap_one=True, seed=51))
+    path = os.path.join(d, "replay.bin")
+    rp.write(path)
+    odir = os.path.join(d, "oracle")
+    pyoracle.run(path, odir, os.path.join(d, "o.txt"), dump_single_items=bool(single), dump=bool(dump),
+                 dump_all=bool(dump_all), dump_unmatched=bool(unmatched), maps_path="/proc/4242/maps", maps_text=MAPS)
+    flags = _lib.NMG_F_DEFAULT | _lib.NMG_F_SAMPLE_MATCHES | _lib.NMG_F_OBJECT_LEVELS
+    eng = Engine(flags=flags, nb_threads=rp.nb_threads)
+    eng.set_objects(rp.table)
+    keep = None
+    if resident:
+        arena, offs, lens, ranks, acc = rp.packed()
+        keep = torch.from_numpy(arena).cuda()
+        eng.set_device_buffers(keep.data_ptr(), offs, lens, ranks, acc)
+    else:
+        eng.submit_replay(rp)
+    eng.analyze()
+    eng.synchronize()
+    edir = os.path.join(d, "engine")
+    dflags = ((_lib.NMG_DUMP_CALLSITES if dump else 0) | (_lib.NMG_DUMP_ALL if dump_all else 0)
+              | (_lib.NMG_DUMP_UNMATCHED if unmatched else 0))
+    eng.report(edir, os.path.join(d, "e.txt"), dump_single_items=single, dump_flags=dflags,
+               maps_path="/proc/4242/maps", maps_text=MAPS)
+    eng.close()
+    assert open(os.path.join(d, "o.txt"), "rb").read() == open(os.path.join(d, "e.txt"), "rb").read()
+    names = sorted(os.listdir(odir))
+    assert any(n.startswith("callsite_summary_") for n in names) == bool((dump or dump_all) and single)
+    _same_dirs(odir, edir)
