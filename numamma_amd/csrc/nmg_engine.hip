@@ -17,12 +17,18 @@
 //     does (variable-size non-SAMPLE records, size==0 abort, truncation);
 //   * global counters (mem_counters[2]) in per-lane registers / LDS, flushed
 //     once per stream run;
-//   * object lookup = branch-free search of the LDS fence table -> node record
-//     (in LDS for <= 1024 keys, else global after a key-bucket search) ->
-//     older entries of the node (quirks Q1-Q4);
-//   * per-object and per-page counters aggregated in direct-mapped LDS tables,
-//     flushed with coalesced global atomics; integer adds, mins and maxes are
-//     order independent, so results are bit-exact.
+//   * object lookup: <= 1023 keys, an Eytzinger search of keys + node records
+//     held in LDS; larger tables, an Eytzinger search of up to 4095 LDS fences,
+//     one 8 B load of the fence bucket's directory slot, then the node record
+//     (L2 / MALL) -> older entries of the node (quirks Q1-Q4);
+//   * per-object and per-page counters aggregated in LDS tables (dense by
+//     entry id / cell for small tables, first-come 8-way buckets otherwise),
+//     flushed with global atomics at stream ends and on a window cadence;
+//     integer adds, mins and maxes are order independent, so results are
+//     bit-exact;
+//   * host side: the C-ABI, the stream-sorted schedule, the streaming pipeline
+//     (copy stream + double-buffered pinned staging), the reset kernel and the
+//     result downloads.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -806,7 +812,7 @@ __device__ __forceinline__ Rec decode_rec(const RawRec& r, uint64_t pos) {
 // 1024 stride slots of 40 B, one per lane, loaded straight into registers;
 // the next window (of this buffer or the next one) is issued before the
 // current one is processed.  One barrier per window: it publishes the window's
-// "irregular" bit and the tables' fill level through rotating flag words.
+// "irregular" bit through rotating flag words.
 // One lane's stride slot in window (cur of d0) [+ head of d1 when d1 is the
 // next buffer of the same stream].
 struct WinLane {
