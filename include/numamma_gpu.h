@@ -108,6 +108,21 @@ struct nmg_report_options {
                                 NMG_F_SAMPLE_MATCHES | NMG_F_OBJECT_LEVELS) */
   const char *maps_path;     /* NMG_DUMP_UNMATCHED header: the traced process's "/proc/<pid>/maps" */
   const char *maps_text;     /* ... and that file's content, captured with the run (NULL: none) */
+  /* NMG_DUMP_ALL: all_memory_objects.dat's callstack_offsets column resolves
+   * each frame as dladdr() did in the traced process (_print_object_summary,
+   * mem_analyzer.c:1660-1690): the module whose [lo, hi) holds the rip gives
+   * dli_fname and dli_fbase.  A frame outside every module prints
+   * "(null):<rip>" (dladdr failed; the reference reads an uninitialised
+   * Dl_info there -- unpinned). */
+  const struct nmg_module *modules;
+  uint32_t nb_modules;
+  uint32_t reserved;
+};
+
+struct nmg_module {
+  uint64_t lo, hi;   /* text range of the loaded object */
+  uint64_t fbase;    /* Dl_info.dli_fbase */
+  const char *fname; /* Dl_info.dli_fname */
 };
 /* dump modes (settings.dump / dump_all / dump_unmatched, numamma.h.in:28-31;
  * mem_sampling.c:599-650, 740-808, 895-914; mem_analyzer.c:1489-1528):
@@ -115,7 +130,7 @@ struct nmg_report_options {
  * unmatched_samples.log.  get_data_src_level() strings are numap's (unpinned
  * beyond "L1_Hit", "L2_Hit", "L3_Hit", README.md:142-147). */
 #define NMG_DUMP_CALLSITES 0x1 /* -d */
-#define NMG_DUMP_ALL 0x2       /* -D */
+#define NMG_DUMP_ALL 0x2       /* -D; also all_memory_objects.dat (mem_analyzer.c:1728-1748) */
 #define NMG_DUMP_UNMATCHED 0x4 /* -u */
 
 struct nmg_engine;
@@ -272,6 +287,9 @@ struct nmg_host_results {
   int64_t nb_cells;
   uint32_t nb_threads;    /* next_thread_rank */
   uint32_t match_samples; /* settings.match_samples */
+  /* per entry (the nmg_set_objects table): all_memory_objects.dat rows
+   * (NMG_DUMP_ALL); may be NULL otherwise */
+  const struct nmg_object *objects;
 };
 int nmg_report_host(const struct nmg_host_results *res, const struct nmg_object_meta *meta,
                     const struct nmg_report_options *opts, const char *stdout_path);

@@ -86,9 +86,21 @@ class nmg_options(C.Structure):
     ]
 
 
+class nmg_module(C.Structure):
+    _fields_ = [("lo", C.c_uint64), ("hi", C.c_uint64), ("fbase", C.c_uint64), ("fname", C.c_char_p)]
+
+
 class nmg_report_options(C.Structure):
     _fields_ = [("output_dir", C.c_char_p), ("dump_single_items", C.c_int32), ("dump_flags", C.c_int32),
-                ("maps_path", C.c_char_p), ("maps_text", C.c_char_p)]
+                ("maps_path", C.c_char_p), ("maps_text", C.c_char_p),
+                ("modules", C.POINTER(nmg_module)), ("nb_modules", C.c_uint32), ("reserved", C.c_uint32)]
+
+
+def module_array(modules):
+    """[(lo, hi, fbase, fname)] -> (nmg_module array, count) for nmg_report_options."""
+    mods = list(modules or [])
+    arr = (nmg_module * max(1, len(mods)))(*[nmg_module(lo, hi, fb, fn.encode()) for lo, hi, fb, fn in mods])
+    return arr, len(mods)
 
 
 class nmg_host_results(C.Structure):
@@ -106,6 +118,7 @@ class nmg_host_results(C.Structure):
         ("nb_cells", C.c_int64),
         ("nb_threads", C.c_uint32),
         ("match_samples", C.c_uint32),
+        ("objects", C.POINTER(nmg_object)),
     ]
 
 

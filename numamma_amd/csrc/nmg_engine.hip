@@ -1247,6 +1247,7 @@ struct nmg_engine {
   uint2* d_dir = nullptr;
   uint32_t nb_fences = 0, fence_log2 = 0, dir_log2 = 0;
   std::vector<uint64_t> hist_base, npages, buffer_size, entry_addr;
+  std::vector<nmg_object> objects;  // the table as given (all_memory_objects.dat)
   std::vector<uint32_t> sparse_entries;
   uint64_t hist_cells = 0;
   uint64_t hist_budget = 4ull << 30;
@@ -1596,6 +1597,7 @@ extern "C" int nmg_set_objects(nmg_engine* h, const uint64_t* keys, const uint32
   h->npages.resize(nb_entries);
   h->buffer_size.resize(nb_entries);
   h->entry_addr.resize(nb_entries);
+  h->objects.assign(entries, entries + nb_entries);
   h->sparse_entries.clear();
   h->hist_cells = 0;
   std::vector<DevEntry> dev(nb_entries);
@@ -2705,6 +2707,7 @@ extern "C" int nmg_report(nmg_engine* h, const nmg_object_meta* meta, const nmg_
   res.nb_cells = ncells;
   res.nb_threads = h->T;
   res.match_samples = (h->flags & NMG_F_MATCH_SAMPLES) ? 1 : 0;
+  res.objects = h->objects.data();
   // dump modes: the buffers' bytes (staging, or D2H of device-resident ones)
   // and every SAMPLE record's match
   DumpInput dump;

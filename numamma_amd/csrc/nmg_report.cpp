@@ -115,6 +115,7 @@ class Registry {
     if (cs && cs_size > 3) k.tail.assign(cs + 3, cs + cs_size);
     return k;
   }
+ public:
   // get_caller_function_from_rip (src/mem_tools.c:91-131): "???" for a NULL
   // rip; replays carry the symbolised string; strings live in 1024-byte slots.
   static std::string caller_string(const nmg_object_meta& m) {
@@ -127,6 +128,8 @@ class Registry {
       snprintf(buf, sizeof(buf), "[0x%" PRIx64 "]", m.caller_rip);
     return buf;
   }
+
+ private:
   const nmg_object_meta* meta_;
   std::unordered_map<CsKey, int64_t, CsKeyHash> by_cs_;
   std::unordered_map<RipKey, int64_t, RipKeyHash> by_rip_;
@@ -329,6 +332,77 @@ void write_maps_header(FILE* f, const nmg_report_options* opts) {
   }
   fprintf(f, "#\n#\n#\n");
   fprintf(f, "#thread_rank timestamp address mem_level access_weight access_type\n");
+}
+
+// dladdr() of a callstack frame, from the traced process's module table
+const nmg_module* find_module(const std::vector<const nmg_module*>& mods, uint64_t rip) {
+  auto it = std::upper_bound(mods.begin(), mods.end(), rip,
+                             [](uint64_t x, const nmg_module* m) { return x < m->lo; });
+  if (it == mods.begin()) return nullptr;
+  const nmg_module* m = *(it - 1);
+  return rip < m->hi ? m : nullptr;
+}
+
+// print_object_summary (mem_analyzer.c:1728-1748): one row per object of
+// mem_list in FOREACH_HASH order (= the table's entry order).  Under
+// USE_HASHTABLE (:23) print_object_summary_from_list ignores its list
+// argument, so the second call, meant for past_mem_list, prints mem_list
+// again (quirk Q20: every row twice).
+int write_object_summary(const std::string& path, const nmg_host_results* r, const nmg_object_meta* meta,
+                         const nmg_report_options* opts, std::string& err) {
+  FILE* f = fopen(path.c_str(), "w");
+  if (!f) {
+    err = "cannot open " + path;
+    return NMG_ERR_IO;
+  }
+  std::vector<const nmg_module*> mods;
+  for (uint32_t i = 0; opts->modules && i < opts->nb_modules; i++) mods.push_back(&opts->modules[i]);
+  std::sort(mods.begin(), mods.end(), [](const nmg_module* a, const nmg_module* b) { return a->lo < b->lo; });
+  fprintf(f, "#object_id\taddress\tsize\tallocation_date\tdeallocation_date\tcallstack_rip\tcallstack_offsets"
+             "\tcallsite_rip\tcallsite\n");
+  // _print_object_summary (:1642-1704)
+  std::vector<std::string> rows(r->nb_entries);
+  std::string rips, offs;
+  char buf[64];
+  for (uint32_t e = 0; e < r->nb_entries; e++) {
+    const nmg_object& o = r->objects[e];
+    const nmg_object_meta& m = meta[e];
+    rips.clear();
+    offs.clear();
+    if (m.callstack) {
+      for (int32_t i = 3; i < m.callstack_size; i++) {
+        const uint64_t rip = m.callstack[i];
+        const char* prefix = i == 3 ? "" : ",";
+        const nmg_module* mod = find_module(mods, rip);
+        const uint64_t fbase = mod ? mod->fbase : 0;
+        snprintf(buf, sizeof(buf), "%s0x%" PRIx64, prefix, rip);
+        rips += buf;
+        offs += prefix;
+        offs += mod && mod->fname ? mod->fname : "(null)";
+        snprintf(buf, sizeof(buf), ":%td", (ptrdiff_t)(rip - fbase));
+        offs += buf;
+      }
+    } else {
+      rips = "NULL";
+      offs = "NULL";
+    }
+    std::string& row = rows[e];
+    snprintf(buf, sizeof(buf), "%d\t0x%" PRIx64 "\t%ld\t", (int)m.id, o.buffer_addr, (long)o.buffer_size);
+    row = buf;
+    snprintf(buf, sizeof(buf), "%" PRIu64 "\t%" PRIu64 "\t", o.alloc_date, o.free_date);
+    row += buf;
+    row += rips;
+    row += '\t';
+    row += offs;
+    snprintf(buf, sizeof(buf), "\t0x%" PRIx64 "\t", m.caller_rip);
+    row += buf;
+    row += Registry::caller_string(m);
+    row += '\n';
+  }
+  for (int pass = 0; pass < 2; pass++)
+    for (const std::string& row : rows) fwrite(row.data(), 1, row.size(), f);
+  fclose(f);
+  return NMG_OK;
 }
 
 }  // namespace
@@ -598,6 +672,14 @@ int write_report(const nmg_host_results* r, const nmg_object_meta* meta, const n
     }
   }
   fclose(cf);
+  if (!rc && (dflags & NMG_DUMP_ALL)) {
+    if (r->objects)
+      rc = write_object_summary(std::string(dir) + "/all_memory_objects.dat", r, meta, opts, err);
+    else {
+      rc = NMG_ERR_INVALID;
+      err = "NMG_DUMP_ALL needs nmg_host_results.objects (all_memory_objects.dat)";
+    }
+  }
   if (rc) {
     close_out();
     return rc;

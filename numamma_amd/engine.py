@@ -171,13 +171,16 @@ class Engine:
 
     # ------------------------------------------------------------------
     def report(self, output_dir: str, stdout_path: Optional[str] = None, dump_single_items: int = 1,
-               dump_flags: int = 0, maps_path: Optional[str] = None, maps_text: Optional[str] = None):
+               dump_flags: int = 0, maps_path: Optional[str] = None, maps_text: Optional[str] = None,
+               modules=None):
         """nmg_report; dump_flags = NMG_DUMP_* (engine created with
-        NMG_F_SAMPLE_MATCHES | NMG_F_OBJECT_LEVELS)."""
+        NMG_F_SAMPLE_MATCHES | NMG_F_OBJECT_LEVELS); modules = [(lo, hi, fbase,
+        fname)], dladdr()'s view of the traced process (all_memory_objects.dat)."""
         meta, keep = build_meta(self.table)
+        marr, nmods = _lib.module_array(modules)
         ro = _lib.nmg_report_options(output_dir.encode(), dump_single_items, dump_flags,
                                      maps_path.encode() if maps_path else None,
-                                     maps_text.encode() if maps_text else None)
+                                     maps_text.encode() if maps_text else None, marr, nmods)
         self._c(lib.nmg_report(self.h, meta, C.byref(ro), stdout_path.encode() if stdout_path else None))
         del keep
 

@@ -71,10 +71,13 @@ class RawResults:
 
 
 def report_host(res: RawResults, table, buf_bytes: np.ndarray, output_dir: str,
-                stdout_path: Optional[str], match_samples: bool = True, dump_single_items: int = 1) -> None:
-    """nmg_report_host(): the report from host arrays (no GPU involved)."""
+                stdout_path: Optional[str], match_samples: bool = True, dump_single_items: int = 1,
+                dump_flags: int = 0, modules=None) -> None:
+    """nmg_report_host(): the report from host arrays (no GPU involved).
+    dump_flags: NMG_DUMP_ALL writes all_memory_objects.dat (the sample dumps
+    need the engine's per-sample matches: nmg_report)."""
     from . import _lib
-    from .engine import build_meta
+    from .engine import build_meta, table_objects
 
     hr = _lib.nmg_host_results()
     gbytes = np.ascontiguousarray(res.global_counters, dtype="<u8").tobytes()
@@ -98,8 +101,12 @@ def report_host(res: RawResults, table, buf_bytes: np.ndarray, output_dir: str,
     hr.nb_cells = res.cells.shape[0]
     hr.nb_threads = res.nb_threads
     hr.match_samples = int(match_samples)
+    objs = table_objects(table)
+    keep.append(objs)
+    hr.objects = objs.ctypes.data_as(C.POINTER(_lib.nmg_object))
     meta, kmeta = build_meta(table)
-    ro = _lib.nmg_report_options(output_dir.encode(), dump_single_items, 0)
+    marr, nmods = _lib.module_array(modules)
+    ro = _lib.nmg_report_options(output_dir.encode(), dump_single_items, dump_flags, None, None, marr, nmods)
     _lib.check(_lib.lib.nmg_report_host(C.byref(hr), meta, C.byref(ro),
                                         stdout_path.encode() if stdout_path else None))
     del keep, kmeta

@@ -28,6 +28,7 @@
 #define _GNU_SOURCE
 #include <errno.h>
 #include <inttypes.h>
+#include <stddef.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -855,6 +856,64 @@ static int o_print_call_site_summary(struct o_state *st, FILE *out, const char *
 }
 
 /* ------------------------------------------------------------------ */
+/* all_memory_objects.dat -- src/mem_analyzer.c:1642-1748             */
+
+/* dladdr(): the module holding rip (linear scan: test sizes) */
+static const struct nmo_module *o_dladdr(const struct nmo_settings *set, uint64_t rip) {
+  for (uint32_t i = 0; set->modules && i < set->nb_modules; i++)
+    if (set->modules[i].lo <= rip && rip < set->modules[i].hi) return &set->modules[i];
+  return NULL;
+}
+
+/* _print_object_summary -- mem_analyzer.c:1642-1704 */
+static void o_print_object_row(struct o_state *st, FILE *f, const struct o_mem *m) {
+  char caller[1024];
+  o_caller_string(m, caller);
+  size_t cap = 64 + (m->callstack_size > 0 ? (size_t)m->callstack_size : 0) * 32;
+  char *rips = malloc(cap), *offs;
+  size_t ocap = 64;
+  for (int i = 3; m->callstack && i < m->callstack_size; i++) {
+    const struct nmo_module *mod = o_dladdr(st->set, m->callstack[i]);
+    ocap += 32 + (mod && mod->fname ? strlen(mod->fname) : 8);
+  }
+  offs = malloc(ocap);
+  rips[0] = offs[0] = '\0';
+  if (m->callstack) {
+    size_t rl = 0, ol = 0;
+    for (int i = 3; i < m->callstack_size; i++) {
+      uint64_t rip = m->callstack[i];
+      const struct nmo_module *mod = o_dladdr(st->set, rip);
+      uint64_t fbase = mod ? mod->fbase : 0;
+      const char *prefix = i == 3 ? "" : ",";
+      rl += (size_t)sprintf(rips + rl, "%s0x%" PRIx64, prefix, rip);
+      ol += (size_t)sprintf(offs + ol, "%s%s:%td", prefix, mod && mod->fname ? mod->fname : "(null)",
+                            (ptrdiff_t)(rip - fbase));
+    }
+  } else {
+    strcpy(rips, "NULL");
+    strcpy(offs, "NULL");
+  }
+  fprintf(f, "%d\t0x%" PRIx64 "\t%ld\t%" PRIu64 "\t%" PRIu64 "\t%s\t%s\t0x%" PRIx64 "\t%s\n", (int)m->id,
+          m->buffer_addr, (long)m->buffer_size, m->alloc_date, m->free_date, rips, offs, m->caller_rip, caller);
+  free(rips);
+  free(offs);
+}
+
+/* print_object_summary -- mem_analyzer.c:1728-1748.  With USE_HASHTABLE
+ * (:23) print_object_summary_from_list walks mem_list whatever list it is
+ * given (:1706-1716), so the past_mem_list call prints mem_list again (Q20). */
+static int o_print_object_summary(struct o_state *st) {
+  FILE *f = o_open_out(st, "all_memory_objects.dat");
+  if (!f) return NMO_ERR_IO;
+  fprintf(f, "#object_id\taddress\tsize\tallocation_date\tdeallocation_date\tcallstack_rip\tcallstack_offsets"
+             "\tcallsite_rip\tcallsite\n");
+  for (int pass = 0; pass < 2; pass++)
+    for (uint32_t e = 0; e < st->nb_entries; e++) o_print_object_row(st, f, &st->mems[e]);
+  fclose(f);
+  return 0;
+}
+
+/* ------------------------------------------------------------------ */
 /* raw-results dump (canonical format shared with the engine tests)    */
 
 static int o_write_raw(struct o_state *st, const char *path) {
@@ -997,7 +1056,7 @@ int nmo_run(const char *replay_path, const char *outdir, const char *stdout_path
     }
   }
   if (outdir) mkdir(outdir, 0700);
-  struct nmo_settings defaults = {1, 1, 0, 0, 0, 0, NULL, NULL};
+  struct nmo_settings defaults = {1, 1, 0, 0, 0, 0, NULL, NULL, NULL, 0, 0};
   st.set = settings ? settings : &defaults;
   st.outdir = outdir;
   if (st.set->dump_unmatched) { /* opened at init, mem_intercept.c:528-535 */
@@ -1050,6 +1109,7 @@ int nmo_run(const char *replay_path, const char *outdir, const char *stdout_path
     if (st.mems[e].blocks) o_update_call_sites(&st, &st.mems[e]);
   o_print_counters(out, st.global_counters);
   if (outdir) rc = o_print_call_site_summary(&st, out, outdir, dump_single);
+  if (!rc && outdir && st.set->dump_all) rc = o_print_object_summary(&st);
   /* mem_sampling_statistics -- src/mem_sampling.c:357-361 */
   float percent = 100.0 * (st.nb_samples_total - st.nb_found_samples_total) / st.nb_samples_total;
   fprintf(out,

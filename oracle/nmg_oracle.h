@@ -20,6 +20,15 @@ struct nmo_settings {
   int reserved;
   const char *maps_path; /* "/proc/<pid>/maps" of the traced process (unmatched_samples.log header) */
   const char *maps_text; /* that file's content, captured with the run (NULL: empty) */
+  const struct nmo_module *modules; /* dladdr() of the traced process (all_memory_objects.dat) */
+  uint32_t nb_modules;
+  uint32_t reserved2;
+};
+
+/* Dl_info of the frames in [lo, hi): dli_fbase, dli_fname */
+struct nmo_module {
+  uint64_t lo, hi, fbase;
+  const char *fname;
 };
 
 struct nmo_timing {

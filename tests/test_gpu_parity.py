@@ -451,6 +451,8 @@ def test_sparse_table_reset_cycles():
 MAPS = ("00400000-00452000 r-xp 00000000 08:02 173521 /usr/bin/app\n"
         "555500000000-555600000000 rw-p 00000000 00:00 0 [heap]\n"
         "7ffd0000-7ffd1000 rw-p 00000000 00:00 0 [stack]\n")
+# dladdr() view for all_memory_objects.dat (frames past 0x4f0000: no module)
+DUMP_MODULES = [(0x400000, 0x480000, 0x400000, "/usr/bin/app"), (0x480000, 0x4F0000, 0x470000, "/usr/lib/libfoo.so.1")]
 
 
 @pytest.mark.parametrize("dump,dump_all,unmatched,single,resident", [
@@ -459,7 +461,7 @@ MAPS = ("00400000-00452000 r-xp 00000000 08:02 173521 /usr/bin/app\n"
 def test_dump_modes_bit_exact(tmp_path, dump, dump_all, unmatched, single, resident):
     """Every dump file byte-identical to the oracle's: callsite_dump_<id>.dat,
     callsite_summary_<id>.dat for the sort's predecessor sites (Q10),
-    all_memory_accesses.dat, unmatched_samples.log with the maps header
+    all_memory_accesses.dat, all_memory_objects.dat, unmatched_samples.log with the maps header
     (last line repeated by the reference's feof loop); staged and
     device-resident buffers."""
     import torch
@@ -471,7 +473,8 @@ def test_dump_modes_bit_exact(tmp_path, dump, dump_all, unmatched, single, resid
     rp.write(path)
     odir = os.path.join(d, "oracle")
     pyoracle.run(path, odir, os.path.join(d, "o.txt"), dump_single_items=bool(single), dump=bool(dump),
-                 dump_all=bool(dump_all), dump_unmatched=bool(unmatched), maps_path="/proc/4242/maps", maps_text=MAPS)
+                 dump_all=bool(dump_all), dump_unmatched=bool(unmatched), maps_path="/proc/4242/maps", maps_text=MAPS,
+                 modules=DUMP_MODULES)
     flags = _lib.NMG_F_DEFAULT | _lib.NMG_F_SAMPLE_MATCHES | _lib.NMG_F_OBJECT_LEVELS
     eng = Engine(flags=flags, nb_threads=rp.nb_threads)
     eng.set_objects(rp.table)
@@ -488,9 +491,10 @@ def test_dump_modes_bit_exact(tmp_path, dump, dump_all, unmatched, single, resid
     dflags = ((_lib.NMG_DUMP_CALLSITES if dump else 0) | (_lib.NMG_DUMP_ALL if dump_all else 0)
               | (_lib.NMG_DUMP_UNMATCHED if unmatched else 0))
     eng.report(edir, os.path.join(d, "e.txt"), dump_single_items=single, dump_flags=dflags,
-               maps_path="/proc/4242/maps", maps_text=MAPS)
+               maps_path="/proc/4242/maps", maps_text=MAPS, modules=DUMP_MODULES)
     eng.close()
     assert open(os.path.join(d, "o.txt"), "rb").read() == open(os.path.join(d, "e.txt"), "rb").read()
     names = sorted(os.listdir(odir))
     assert any(n.startswith("callsite_summary_") for n in names) == bool((dump or dump_all) and single)
+    assert ("all_memory_objects.dat" in names) == bool(dump_all)
     _same_dirs(odir, edir)

@@ -112,3 +112,68 @@ def test_sort_with_int_truncated_weights(tmp_path):
         lst.remove(pick)
         head.insert(0, pick)
     assert ids == head
+
+
+# ---- all_memory_objects.dat (-D): print_object_summary, mem_analyzer.c:1642-1748
+# dladdr()'s view of the traced process: the synthetic callstack tails live in
+# [0x400000, 0x500000); frames in [0x4f0000, 0x500000) belong to no module.
+MODULES = [(0x400000, 0x480000, 0x400000, "/usr/bin/app"), (0x480000, 0x4F0000, 0x470000, "/usr/lib/libfoo.so.1")]
+
+
+def _expected_object_rows(table):
+    """The row format restated a third time, from _print_object_summary's
+    fprintf (:1699-1703) and its dladdr loop (:1660-1690)."""
+    ent, pool, strings = table.entries, table.callstack_pool, table.string_pool
+    rows = []
+    for r in ent:
+        if r["has_callstack"]:
+            cs = [int(x) for x in pool[int(r["callstack_off"]):int(r["callstack_off"]) + int(r["callstack_size"])]]
+            rips, offs = [], []
+            for rip in cs[3:]:
+                mod = next((m for m in MODULES if m[0] <= rip < m[1]), None)
+                rips.append(f"0x{rip:x}")
+                offs.append(f"{mod[3]}:{rip - mod[2]}" if mod else f"(null):{rip}")
+            rips, offs = ",".join(rips), ",".join(offs)
+        else:
+            rips = offs = "NULL"
+        if int(r["caller_off"]) != 0xFFFFFFFF:
+            o = int(r["caller_off"])
+            caller = strings[o:strings.index(b"\0", o)].decode()
+        else:
+            caller = "???" if int(r["caller_rip"]) == 0 else f"[0x{int(r['caller_rip']):x}]"
+        rows.append(f"{int(r['id'])}\t0x{int(r['buffer_addr']):x}\t{int(r['buffer_size'])}\t{int(r['alloc_date'])}\t"
+                    f"{int(r['free_date'])}\t{rips}\t{offs}\t0x{int(r['caller_rip']):x}\t{caller}\n")
+    head = ("#object_id\taddress\tsize\tallocation_date\tdeallocation_date\tcallstack_rip\tcallstack_offsets"
+            "\tcallsite_rip\tcallsite\n")
+    return head + "".join(rows) * 2  # USE_HASHTABLE: mem_list printed twice (Q20)
+
+
+@pytest.mark.parametrize("cfg", [
+    SynthConfig(nb_samples=20_000, nb_intervals=300, lost_frac=2e-3, seed=21),
+    SynthConfig(nb_samples=10_000, nb_intervals=120, null_callstack_frac=0.5, reuse_frac=0.3, realloc_frac=0.2,
+                site_ratio=0.5, seed=22),
+])
+def test_all_memory_objects(tmp_path, cfg):
+    """all_memory_objects.dat from the product's host report writer, the
+    oracle, and the test's own restatement: byte-identical."""
+    from numamma_amd import _lib
+
+    d = str(tmp_path)
+    rp = generate(cfg)
+    path = os.path.join(d, "replay.bin")
+    rp.write(path)
+    odir = os.path.join(d, "oracle")
+    pyoracle.run(path, odir, os.path.join(d, "o.txt"), os.path.join(d, "raw.bin"), dump_all=True, modules=MODULES)
+    raw = RawResults.read(os.path.join(d, "raw.bin"))
+    pdir = os.path.join(d, "product")
+    report_host(raw, rp.table, _buf_bytes(rp), pdir, os.path.join(d, "p.txt"), dump_flags=_lib.NMG_DUMP_ALL,
+                modules=MODULES)
+    want = _expected_object_rows(rp.table)
+    got_o = open(os.path.join(odir, "all_memory_objects.dat"), newline="").read()
+    got_p = open(os.path.join(pdir, "all_memory_objects.dat"), newline="").read()
+    assert got_o == want
+    assert got_p == want
+    assert "(null):" in want and "/usr/lib/libfoo.so.1:" in want and "\tNULL\tNULL\t" in want
+    assert open(os.path.join(d, "o.txt"), "rb").read() == open(os.path.join(d, "p.txt"), "rb").read()
+    for f in ("call_sites.log",):
+        assert open(os.path.join(odir, f), "rb").read() == open(os.path.join(pdir, f), "rb").read()
