@@ -12,7 +12,7 @@ records per GPU in 128 KiB per-thread buffers, 1k object intervals (+ 8
 globals + [stack]), 8 threads.  Weak scaling: every rank analyses its own
 10M-record shard against the same object table.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2|c3|c4]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2|c3|c4|k1m]
     torchrun --nproc-per-node N bench.py --gpus N ...
 """
 from __future__ import annotations
@@ -36,6 +36,8 @@ WORKLOADS = {
     "c3": dict(nb_samples=100_000_000, nb_intervals=100_000, desc="configs[2]: 100M PEBS records/GPU, 100k intervals, per-page on"),
     "c4": dict(nb_samples=125_000_000, nb_intervals=1_000_000, size_max=64 * 1024,
                desc="configs[3] per-GPU shard: 1B records / 8 GPUs, 1M intervals"),
+    "k1m": dict(nb_samples=10_000_000, nb_intervals=1_000_000, size_max=64 * 1024,
+                desc="north-star table size: 10M PEBS records/GPU, 1M object intervals"),
 }
 
 

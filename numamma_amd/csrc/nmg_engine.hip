@@ -171,6 +171,13 @@ struct Params {
   uint32_t* sparse_dirty;  // set on any sparse insert: the next reset must clear the table
   uint32_t* smatch;        // NMG_F_SAMPLE_MATCHES: [(buffer offset + record offset) / 8] = entry + 1, 0 = none
   unsigned long long* dbg;  // kDbgTiming: [grid][waves][kTimingWords]
+  // hashed object mode: per-launch packed [2 access][E] (count << pk_shift |
+  // weight) for the global path, one atomic instead of two; exact because
+  // samples per launch < 2^(64 - pk_shift) and only weights < pk_wlim are
+  // packed (their sum < 2^pk_shift); unpack_kernel adds it into sum64
+  unsigned long long* pk64;  // null: packing off
+  uint32_t pk_shift;
+  uint64_t pk_wlim;
 };
 
 // ---------------------------------------------------------------------------
@@ -591,7 +598,9 @@ __device__ __forceinline__ void process_sample(Params& p, WgCounters& wc, LaneAc
   // per-object counters, aggregated per stream in LDS.  (Admitting an entry
   // only on its second sample -- a doorkeeper bitset -- was measured slower at
   // 1M intervals: the per-sample bit test costs more than the flushes it saves.)
-  const int os = (MODE & kModeDenseObj) ? (int)e : obj_slot(wc, (uint32_t)e);
+  // (with packing, a slot only sums packable weights: its flush is packed too)
+  const bool pk = !(MODE & kModeDenseObj) && p.pk64 && w < p.pk_wlim;
+  const int os = (MODE & kModeDenseObj) ? (int)e : ((p.pk64 && !pk) ? -1 : obj_slot(wc, (uint32_t)e));
   const unsigned long long ord = (seq << 32) | off;  // first match in analysis order (quirk Q7)
   if ((MODE & kModeDenseObj) && w < kLaneMaxWeight && kPackObj) {
     // one packed add: count in bits 44..63, weight below (bounded by the
@@ -602,6 +611,10 @@ __device__ __forceinline__ void process_sample(Params& p, WgCounters& wc, LaneAc
     atomicAdd(&wc.ocnt[os], 1u);
     if (w) atomicAdd(&wc.owt[os], (unsigned long long)w);
     if (ord < wc.ofirst[os]) atomicMin(&wc.ofirst[os], ord);
+  } else if (pk) {  // table full: one packed global add
+    atomicAdd(p.pk64 + uint64_t(access) * p.nb_entries + e, (1ull << p.pk_shift) | w);
+    unsigned long long* fp = reinterpret_cast<unsigned long long*>(p.min64 + 36 + e);
+    atomicMin(fp, ord);
   } else {  // table full (or a weight >= 2^23 in dense mode): straight to global
     atomicAdd(reinterpret_cast<unsigned long long*>(p.sum64 + objcw_index(e, access, 0, p.nb_entries)), 1ull);
     if (w)
@@ -656,7 +669,10 @@ __device__ __forceinline__ void flush_objects(Params& p, WgCounters& wc, int tid
     if ((MODE & kModeDenseObj) ? (packed ? wc.owt[i] == 0 : wc.ocnt[i] == 0) : e == kEmpty32) continue;
     const uint64_t cnt = packed ? wc.owt[i] >> kPackShift : wc.ocnt[i];
     const uint64_t wt = packed ? wc.owt[i] & ((1ull << kPackShift) - 1) : wc.owt[i];
-    if (write) {
+    if (write && !(MODE & kModeDenseObj) && p.pk64) {
+      atomicAdd(p.pk64 + uint64_t(a) * p.nb_entries + e, (cnt << p.pk_shift) | wt);
+      atomicMin(reinterpret_cast<unsigned long long*>(p.min64 + 36 + e), wc.ofirst[i]);
+    } else if (write) {
       atomicAdd(reinterpret_cast<unsigned long long*>(p.sum64 + objcw_index(e, a, 0, p.nb_entries)),
                 (unsigned long long)cnt);
       if (wt)
@@ -1121,6 +1137,22 @@ __global__ __launch_bounds__(kWG, 1) void attribute_kernel(Params p) {
   }
 }
 
+// Adds the launch's packed long-tail object counters into sum64 and clears
+// them (same stream, after attribute_kernel).
+__global__ __launch_bounds__(256) void unpack_kernel(uint64_t* sum64, unsigned long long* pk64, uint32_t nb_entries,
+                                                     uint32_t shift) {
+  const uint64_t n = 2ull * nb_entries;
+  for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += gridDim.x * 256ull) {
+    const uint64_t v = pk64[i];
+    if (!v) continue;
+    const uint32_t a = i >= nb_entries;
+    const uint64_t e = i - uint64_t(a) * nb_entries;
+    sum64[objcw_index(e, a, 0, nb_entries)] += v >> shift;
+    sum64[objcw_index(e, a, 1, nb_entries)] += v & ((1ull << shift) - 1);
+    pk64[i] = 0;
+  }
+}
+
 // One launch re-initialises every counter array (INIT_COUNTER semantics:
 // sums and maxes 0, mins and first-match ordinals UINT64_MAX; sparse keys empty).
 struct ResetParams {
@@ -1261,6 +1293,7 @@ struct nmg_engine {
   uint32_t* d_sparse_vals = nullptr;
   uint32_t* d_sparse_dirty = nullptr;  // [2] parity flags (see reset_kernel)
   uint32_t* d_smatch = nullptr;        // NMG_F_SAMPLE_MATCHES: per 8 B of the arena span
+  unsigned long long* d_pk64 = nullptr;  // hashed object mode: packed long-tail counters (0 between launches)
   size_t smatch_cap = 0;
   uint64_t nreset = 0;
 
@@ -1380,6 +1413,8 @@ static void free_counters(nmg_engine* h) {
   h->d_sparse_vals = nullptr;
   (void)hipFree(h->d_sparse_dirty);
   h->d_sparse_dirty = nullptr;
+  (void)hipFree(h->d_pk64);
+  h->d_pk64 = nullptr;
 }
 
 static void free_table(nmg_engine* h) {
@@ -1698,6 +1733,10 @@ extern "C" int nmg_set_objects(nmg_engine* h, const uint64_t* keys, const uint32
   HIP_TRY(h, hipMalloc(&h->d_sum64, h->n_sum64 * 8));
   HIP_TRY(h, hipMalloc(&h->d_min64, h->n_min64 * 8));
   HIP_TRY(h, hipMalloc(&h->d_max64, h->n_max64 * 8));
+  if (nb_entries > kObjSlots) {  // hashed object mode (see launch_attribution)
+    HIP_TRY(h, hipMalloc(&h->d_pk64, (size_t)nb_entries * 2 * 8));
+    HIP_TRY(h, hipMemset(h->d_pk64, 0, (size_t)nb_entries * 2 * 8));
+  }
   // pad the dense arena to a multiple of 4 cells per thread so it is zeroed in 16 B units
   h->hist_cells = (h->hist_cells + 3) & ~uint64_t(3);
   if (h->hist_cells) HIP_TRY(h, hipMalloc(&h->d_hist, h->hist_cells * h->T * 4));
@@ -1765,7 +1804,7 @@ static void ensure_occupancy(nmg_engine* h);
 static void make_schedule(const std::vector<BufDesc>& descs, uint32_t grid, uint32_t index_base, BufDesc* sorted,
                           uint32_t* ranges);
 static int launch_attribution(nmg_engine* h, const uint8_t* data, const BufDesc* sdescs, const uint32_t* ranges,
-                              uint32_t nb, uint32_t grid);
+                              uint32_t nb, uint32_t grid, uint64_t nbytes);
 static int stream_append(nmg_engine* h, uint64_t len, uint32_t thread_rank, uint32_t access);
 
 extern "C" int nmg_submit_buffer(nmg_engine* h, const void* bytes, uint64_t len, uint32_t thread_rank,
@@ -1923,7 +1962,8 @@ static int stream_flush(nmg_engine* h) {
   HIP_TRY(h, hipMemcpyAsync(sl.d_sdescs, sl.h_sdescs, sched_bytes, hipMemcpyHostToDevice, h->copy_stream));
   HIP_TRY(h, hipEventRecord(sl.copied, h->copy_stream));
   HIP_TRY(h, hipStreamWaitEvent(h->stream, sl.copied, 0));
-  rc = launch_attribution(h, sl.d_arena, sl.d_sdescs, reinterpret_cast<const uint32_t*>(sl.d_sdescs + nb), nb, grid);
+  rc = launch_attribution(h, sl.d_arena, sl.d_sdescs, reinterpret_cast<const uint32_t*>(sl.d_sdescs + nb), nb, grid,
+                          sl.len);
   if (rc) return rc;
   HIP_TRY(h, hipEventRecord(sl.done, h->stream));
   sl.used = true;
@@ -2212,7 +2252,7 @@ static void ensure_occupancy(nmg_engine* h) {
 // per-workgroup ranges are already on the device, on the engine stream,
 // bracketed by the launch-timing events.
 static int launch_attribution(nmg_engine* h, const uint8_t* data, const BufDesc* sdescs, const uint32_t* ranges,
-                              uint32_t nb, uint32_t grid) {
+                              uint32_t nb, uint32_t grid, uint64_t nbytes) {
   Params p;
   memset(&p, 0, sizeof(p));
   p.data = data;
@@ -2250,6 +2290,18 @@ static int launch_attribution(nmg_engine* h, const uint8_t* data, const BufDesc*
   // dense LDS tables when the table is small enough (DESIGN.md "Kernels")
   const int mode = (h->E <= kObjSlots ? kModeDenseObj : 0) |
                    (h->hist_cells <= kDensePageCells ? kModeDensePage : 0);
+#ifndef NMG_NO_PACK_TAIL
+  if (!(mode & kModeDenseObj) && h->d_pk64) {
+    // < 2^cbits samples in this launch (a SAMPLE record is 40 B); packed
+    // weights < 2^(64 - 2 cbits), so any entry's packed sum < 2^(64 - cbits)
+    const uint32_t cbits = 64 - (uint32_t)__builtin_clzll(nbytes / kRecBytes + 1);
+    if (2 * cbits < 64) {
+      p.pk64 = h->d_pk64;
+      p.pk_shift = 64 - cbits;
+      p.pk_wlim = 1ull << (64 - 2 * cbits);
+    }
+  }
+#endif
   const int slot = (int)(h->nlaunch % nmg_engine::kRing);
   if (!h->ring0[slot]) {
     HIP_TRY(h, hipEventCreate(&h->ring0[slot]));
@@ -2273,6 +2325,12 @@ static int launch_attribution(nmg_engine* h, const uint8_t* data, const BufDesc*
       hipLaunchKernelGGL(kernel_for(false, mode), dim3(grid), dim3(kWG), 0, h->stream, p);
     }
     HIP_TRY(h, hipGetLastError());
+    if (p.pk64) {
+      const uint32_t blocks = (uint32_t)std::min<uint64_t>(2048, (2ull * h->E + 255) / 256);
+      hipLaunchKernelGGL(unpack_kernel, dim3(blocks), dim3(256), 0, h->stream, h->d_sum64, p.pk64, h->E,
+                         p.pk_shift);
+      HIP_TRY(h, hipGetLastError());
+    }
   }
   HIP_TRY(h, hipEventRecord(h->ring1[slot], h->stream));
   h->nlaunch++;
@@ -2311,7 +2369,9 @@ extern "C" int nmg_analyze(nmg_engine* h) {
     rc = build_schedule(h, grid);
     if (rc) return rc;
   }
-  return launch_attribution(h, h->d_data, h->d_sdescs, h->d_ranges, nb, grid);
+  uint64_t nbytes = 0;
+  for (const BufDesc& d : h->descs) nbytes += d.len;
+  return launch_attribution(h, h->d_data, h->d_sdescs, h->d_ranges, nb, grid, nbytes);
 }
 
 static int decode_error_word(nmg_engine* h, uint64_t w) {

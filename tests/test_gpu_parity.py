@@ -110,8 +110,9 @@ def test_large_weights_bit_exact(tmp_path, nb_intervals):
     d = str(tmp_path)
     rp = generate(SynthConfig(nb_samples=200_000, nb_intervals=nb_intervals, seed=16))
     rng = np.random.default_rng(16)
-    big = np.array([(1 << 23) - 1, 1 << 23, (1 << 26) + 5, (1 << 32) - 1, 1 << 32, (1 << 40) + 7,
-                    (1 << 63) + 3, (1 << 64) - 1], dtype=np.uint64)
+    # (2^28: the hashed mode's packed long-tail limit at 200k records, 2^(64 - 2 * 18))
+    big = np.array([(1 << 23) - 1, 1 << 23, (1 << 26) + 5, (1 << 28) - 1, 1 << 28, (1 << 32) - 1, 1 << 32,
+                    (1 << 40) + 7, (1 << 63) + 3, (1 << 64) - 1], dtype=np.uint64)
     for b in rp.buffers:
         rec = b.ring.view(RECORD_DTYPE)  # pure 40 B SAMPLE streams (lost_frac = 0, no wrap)
         pick = rng.random(rec.shape[0]) < 0.05

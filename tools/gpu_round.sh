@@ -49,7 +49,7 @@ for s in $STAGES; do
       cat $OUT/ablate_$TAG.json ;;
     e2e)
       echo "== end-to-end (host buffers, PCIe)"
-      timeout -k 10 600 python tools/e2e.py c2 --threads 16 > $OUT/e2e_$TAG.json 2> $OUT/e2e_$TAG.err \
+      timeout -k 10 600 python tools/e2e.py c2 --threads ${E2E_THREADS:-16} --chunk-mb ${E2E_CHUNK:-64} > $OUT/e2e_$TAG.json 2> $OUT/e2e_$TAG.err \
         || { echo "e2e failed"; tail -30 $OUT/e2e_$TAG.err; exit 1; }
       cat $OUT/e2e_$TAG.json ;;
     phases)
@@ -89,6 +89,23 @@ for s in $STAGES; do
       done
       python3 tools/pmc_summary.py $OUT/traffic_${TAG}_FETCH_SIZE $OUT/traffic_${TAG}_WRITE_SIZE \
         > $OUT/pmc_${TRAFFIC_WL:-c2}_$TAG.json && cat $OUT/pmc_${TRAFFIC_WL:-c2}_$TAG.json ;;
+    l2)
+      # L2 hit rate and memory-side atomics of the attribution kernel
+      echo "== rocprofv3 L2 passes (${L2_WL:-k1m})"
+      i=0
+      for set in "TCC_HIT_sum TCC_MISS_sum TCC_EA0_ATOMIC_sum TCC_EA0_RDREQ_sum" "TCC_EA0_WRREQ_sum TCC_EA0_RDREQ_32B_sum"; do
+        i=$((i+1))
+        rm -rf $OUT/l2_${TAG}_$i
+        timeout -k 10 400 rocprofv3 --pmc $set --kernel-trace -d $ROOT/$OUT/l2_${TAG}_$i -o run --output-format csv \
+          -- python3 $ROOT/bench.py --workload ${L2_WL:-k1m} --steps 3 --warmup 1 --no-cpu-baseline > $OUT/l2_${TAG}_$i.log 2>&1 \
+          || { echo "l2 pass $i failed"; tail -20 $OUT/l2_${TAG}_$i.log; exit 1; }
+      done
+      echo "l2 passes done" ;;
+    ab)
+      echo "== A/B variants (${AB_VARIANTS:-base})"
+      timeout -k 10 900 python tools/ab.py --variants ${AB_VARIANTS:-base} --workloads ${AB_WL:-c2,k1m} --rounds 2 \
+        > $OUT/ab_$TAG.json 2> $OUT/ab_$TAG.err || { echo "ab failed"; tail -30 $OUT/ab_$TAG.err; exit 1; }
+      cat $OUT/ab_$TAG.json ;;
     pmc)
       echo "== rocprofv3 pmc FETCH_SIZE"
       rm -rf $OUT/pmc_$TAG
