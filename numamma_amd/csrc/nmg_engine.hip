@@ -67,6 +67,11 @@ constexpr uint32_t kMaxList = kWG;             // slow path: SAMPLE offsets list
 // per-stream LDS aggregation tables (flushed to global at a stream change and
 // on a window cadence)
 constexpr uint32_t kObjSlots = 2048;           // entry -> (count, weight, first ordinal)
+// long-tail log (hashed object mode): per workgroup, kLogParts sub-logs by
+// entry range of 24 B records {entry | access << 31, count, weight, ordinal}
+constexpr uint32_t kLogParts = 256;
+constexpr uint32_t kLogChunk = 4096;   // entries per LDS pass of tlog_reduce_kernel
+constexpr uint32_t kLogMaxGrid = 1024;  // attribution workgroups a log can serve
 constexpr uint32_t kPageBuckets = 896;         // dense page cell -> count: 8-slot buckets
 constexpr uint32_t kPageSlots = kPageBuckets * 8;  // 7168 cells (56 KiB)
 constexpr uint32_t kObjBuckets = kObjSlots / 8;
@@ -178,6 +183,13 @@ struct Params {
   unsigned long long* pk64;  // null: packing off
   uint32_t pk_shift;
   uint64_t pk_wlim;
+  // long-tail log: instead of scattered global atomics, table-full samples
+  // and flushed slots append to sub-log (workgroup, entry >> tlog_rshift);
+  // tlog_reduce_kernel sums each entry range from LDS.  A full sub-log falls
+  // back to the atomics.
+  unsigned long long* tlog;  // [grid][tlog_parts][tlog_cap][3] u64; null: off
+  uint32_t* tlog_cnt;        // [grid][tlog_parts] records written
+  uint32_t tlog_cap, tlog_rshift, tlog_parts;
 };
 
 // ---------------------------------------------------------------------------
@@ -348,6 +360,7 @@ struct WgCounters {
     };
     unsigned int pdense[kDensePageCells / 2];  // kModeDensePage: u16 count per cell, two per word
   };
+  unsigned int tcur[kLogParts];  // long-tail sub-log cursors
 };
 
 // Entries (tables with more than kObjSlots entries): a Fibonacci hash picks
@@ -531,6 +544,20 @@ __device__ __forceinline__ Match find_entry(const Params& p, const Lookup& L, ui
   return m;
 }
 
+// One long-tail contribution to this workgroup's sub-log of entry e; false
+// when the sub-log is full (the caller then issues the global atomics).
+__device__ __forceinline__ bool tlog_append(const Params& p, WgCounters& wc, uint32_t e, uint32_t a, uint32_t cnt,
+                                            uint64_t wt, uint64_t ord) {
+  const uint32_t part = e >> p.tlog_rshift;
+  const uint32_t k = atomicAdd(&wc.tcur[part], 1u);
+  if (k >= p.tlog_cap) return false;
+  unsigned long long* r = p.tlog + ((uint64_t(blockIdx.x) * p.tlog_parts + part) * p.tlog_cap + k) * 3;
+  r[0] = (unsigned long long)(e | (a << 31)) | ((unsigned long long)cnt << 32);
+  r[1] = wt;
+  r[2] = ord;
+  return true;
+}
+
 // Process one decoded record (`valid` = it is a SAMPLE).  Every lane of the
 // wave calls this together (wave-level reductions inside); vmask / fmask are
 // the wave's SAMPLE and matched lanes.
@@ -611,6 +638,8 @@ __device__ __forceinline__ void process_sample(Params& p, WgCounters& wc, LaneAc
     atomicAdd(&wc.ocnt[os], 1u);
     if (w) atomicAdd(&wc.owt[os], (unsigned long long)w);
     if (ord < wc.ofirst[os]) atomicMin(&wc.ofirst[os], ord);
+  } else if (!(MODE & kModeDenseObj) && p.tlog && tlog_append(p, wc, (uint32_t)e, access, 1u, w, ord)) {
+    // table full: logged for tlog_reduce_kernel
   } else if (pk) {  // table full: one packed global add
     atomicAdd(p.pk64 + uint64_t(access) * p.nb_entries + e, (1ull << p.pk_shift) | w);
     unsigned long long* fp = reinterpret_cast<unsigned long long*>(p.min64 + 36 + e);
@@ -669,7 +698,9 @@ __device__ __forceinline__ void flush_objects(Params& p, WgCounters& wc, int tid
     if ((MODE & kModeDenseObj) ? (packed ? wc.owt[i] == 0 : wc.ocnt[i] == 0) : e == kEmpty32) continue;
     const uint64_t cnt = packed ? wc.owt[i] >> kPackShift : wc.ocnt[i];
     const uint64_t wt = packed ? wc.owt[i] & ((1ull << kPackShift) - 1) : wc.owt[i];
-    if (write && !(MODE & kModeDenseObj) && p.pk64) {
+    if (write && !(MODE & kModeDenseObj) && p.tlog && tlog_append(p, wc, e, a, (uint32_t)cnt, wt, wc.ofirst[i])) {
+      // logged
+    } else if (write && !(MODE & kModeDenseObj) && p.pk64) {
       atomicAdd(p.pk64 + uint64_t(a) * p.nb_entries + e, (cnt << p.pk_shift) | wt);
       atomicMin(reinterpret_cast<unsigned long long*>(p.min64 + 36 + e), wc.ofirst[i]);
     } else if (write) {
@@ -894,6 +925,9 @@ __global__ __launch_bounds__(kWG, 1) void attribute_kernel(Params p) {
     for (uint32_t i = tid; i < p.nb_fences; i += kWG) s_shift[i] = p.fshift[i];
   }
   clear_state<MODE>(wc, tid);
+  constexpr bool kLog = !(MODE & kModeDenseObj);  // the long-tail log serves the hashed object mode
+  if (kLog && p.tlog)
+    for (uint32_t i = tid; i < kLogParts; i += kWG) wc.tcur[i] = 0;
   if (tid < 3) s_flags[tid] = 0;
   __syncthreads();
   const Lookup L{s_fences, s_nodes, s_ninfo, s_shift};
@@ -903,7 +937,11 @@ __global__ __launch_bounds__(kWG, 1) void attribute_kernel(Params p) {
   // to the same stream, the remaining lanes take the head of the next buffer
   // (no partly idle window at every buffer end).
   const uint32_t r0 = p.ranges[blockIdx.x], r1 = p.ranges[blockIdx.x + 1];
-  if (r0 >= r1) return;
+  if (r0 >= r1) {
+    if (kLog && p.tlog)
+      for (uint32_t i = tid; i < p.tlog_parts; i += kWG) p.tlog_cnt[uint64_t(blockIdx.x) * p.tlog_parts + i] = 0;
+    return;
+  }
   uint32_t idx = r0;
   uint32_t cur = 0;  // byte cursor, as `cur_cpt` in __analyze_buffer (mem_sampling.c:836)
   BufDesc d0 = p.sbufs[idx];
@@ -1129,11 +1167,95 @@ __global__ __launch_bounds__(kWG, 1) void attribute_kernel(Params p) {
     }
     if (idx >= r1) break;  // the loop's only exit, after the state update
   }
+  if (kLog && p.tlog) {  // the sub-logs' fill (every append of this workgroup is done)
+    __syncthreads();
+    for (uint32_t i = tid; i < p.tlog_parts; i += kWG)
+      p.tlog_cnt[uint64_t(blockIdx.x) * p.tlog_parts + i] = min(wc.tcur[i], p.tlog_cap);
+  }
   if (TIMING && lane == 0) {
     unsigned long long* o = p.dbg + (uint64_t(blockIdx.x) * (kWG / 64) + tid / 64) * kTimingWords;
     for (int k = 0; k < 4; k++) o[k] = tacc[k];
     o[4] = stamp() - t_start;
     o[5] = win;
+  }
+}
+
+// Sums the long-tail log of one attribution launch: workgroup `part` owns the
+// entries [part << rshift, (part + 1) << rshift), reads that range's sub-log
+// of every attribution workgroup, adds counts / weights and takes the first
+// ordinal in LDS, then updates sum64 / min64 with plain read-modify-writes
+// (no other writer of those words is running).  Folds the packed counters of
+// the range too.
+struct TlogParams {
+  const unsigned long long* tlog;
+  const uint32_t* tlog_cnt;
+  uint64_t* sum64;
+  uint64_t* min64;
+  unsigned long long* pk64;  // may be null
+  uint32_t grid, parts, cap, rshift, nb_entries, pk_shift;
+};
+
+__global__ __launch_bounds__(1024, 1) void tlog_reduce_kernel(TlogParams r) {
+  __shared__ uint32_t s_cnt[2][kLogChunk];
+  __shared__ unsigned long long s_wt[2][kLogChunk];
+  __shared__ unsigned long long s_ord[kLogChunk];
+  __shared__ uint32_t s_pre[kLogMaxGrid + 1];
+  const uint32_t part = blockIdx.x, tid = threadIdx.x;
+  for (uint32_t w = tid; w < r.grid; w += 1024) s_pre[w + 1] = r.tlog_cnt[uint64_t(w) * r.parts + part];
+  __syncthreads();
+  if (tid == 0) {  // exclusive prefix over the source workgroups
+    s_pre[0] = 0;
+    for (uint32_t w = 1; w <= r.grid; w++) s_pre[w] += s_pre[w - 1];
+  }
+  __syncthreads();
+  const uint32_t total = s_pre[r.grid];
+  const uint64_t e0 = uint64_t(part) << r.rshift;
+  const uint64_t e1 = min(e0 + (1ull << r.rshift), (uint64_t)r.nb_entries);
+  for (uint64_t base = e0; base < e1; base += kLogChunk) {
+    const uint32_t n = (uint32_t)min((uint64_t)kLogChunk, e1 - base);
+    for (uint32_t j = tid; j < n; j += 1024) {
+      s_cnt[0][j] = s_cnt[1][j] = 0;
+      s_wt[0][j] = s_wt[1][j] = 0;
+      s_ord[j] = ~0ull;
+    }
+    __syncthreads();
+    for (uint32_t i = tid; i < total; i += 1024) {
+      uint32_t lo = 0, hi = r.grid;  // source workgroup: s_pre[lo] <= i < s_pre[lo + 1]
+      while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (s_pre[mid] <= i) lo = mid;
+        else hi = mid;
+      }
+      const unsigned long long* q = r.tlog + ((uint64_t(lo) * r.parts + part) * r.cap + (i - s_pre[lo])) * 3;
+      const unsigned long long k = q[0];
+      const uint32_t e = uint32_t(k) & 0x7fffffffu, a = uint32_t(k) >> 31;
+      const uint64_t j = e - base;
+      if (e < base || j >= n) continue;
+      atomicAdd(&s_cnt[a][j], uint32_t(k >> 32));
+      const unsigned long long wt = q[1];
+      if (wt) atomicAdd(&s_wt[a][j], wt);
+      atomicMin(&s_ord[j], q[2]);
+    }
+    __syncthreads();
+    for (uint32_t j = tid; j < n; j += 1024) {
+      const uint64_t e = base + j;
+      for (uint32_t a = 0; a < 2; a++) {
+        uint64_t c = s_cnt[a][j], w = s_wt[a][j];
+        if (r.pk64) {
+          const uint64_t v = r.pk64[uint64_t(a) * r.nb_entries + e];
+          if (v) {
+            c += v >> r.pk_shift;
+            w += v & ((1ull << r.pk_shift) - 1);
+            r.pk64[uint64_t(a) * r.nb_entries + e] = 0;
+          }
+        }
+        if (c) r.sum64[objcw_index(e, a, 0, r.nb_entries)] += c;
+        if (w) r.sum64[objcw_index(e, a, 1, r.nb_entries)] += w;
+      }
+      const uint64_t o = s_ord[j];
+      if (o < r.min64[36 + e]) r.min64[36 + e] = o;
+    }
+    __syncthreads();
   }
 }
 
@@ -1294,6 +1416,10 @@ struct nmg_engine {
   uint32_t* d_sparse_dirty = nullptr;  // [2] parity flags (see reset_kernel)
   uint32_t* d_smatch = nullptr;        // NMG_F_SAMPLE_MATCHES: per 8 B of the arena span
   unsigned long long* d_pk64 = nullptr;  // hashed object mode: packed long-tail counters (0 between launches)
+  unsigned long long* d_tlog = nullptr;  // hashed object mode: long-tail log (see Params::tlog)
+  size_t tlog_bytes = 0;
+  uint32_t* d_tlog_cnt = nullptr;
+  size_t tlog_cnt_cap = 0;
   size_t smatch_cap = 0;
   uint64_t nreset = 0;
 
@@ -1415,6 +1541,12 @@ static void free_counters(nmg_engine* h) {
   h->d_sparse_dirty = nullptr;
   (void)hipFree(h->d_pk64);
   h->d_pk64 = nullptr;
+  (void)hipFree(h->d_tlog);
+  h->d_tlog = nullptr;
+  h->tlog_bytes = 0;
+  (void)hipFree(h->d_tlog_cnt);
+  h->d_tlog_cnt = nullptr;
+  h->tlog_cnt_cap = 0;
 }
 
 static void free_table(nmg_engine* h) {
@@ -2302,6 +2434,40 @@ static int launch_attribution(nmg_engine* h, const uint8_t* data, const BufDesc*
     }
   }
 #endif
+#ifndef NMG_NO_TAIL_LOG
+  if (!(mode & kModeDenseObj) && nb && grid <= kLogMaxGrid && (h->flags & NMG_F_MATCH_SAMPLES) &&
+      nbytes / kRecBytes < (1ull << 31)) {
+    uint32_t rshift = 0;
+    while ((((uint64_t)h->E + (1ull << rshift) - 1) >> rshift) > kLogParts) rshift++;
+    const uint32_t parts = (uint32_t)(((uint64_t)h->E + (1ull << rshift) - 1) >> rshift);
+    // sized for about every sample of the launch spread evenly; a full
+    // sub-log only sends its overflow to the atomics
+    const uint64_t cap = std::min<uint64_t>(1u << 20, (nbytes / kRecBytes) / ((uint64_t)grid * parts) + 32);
+    const size_t need = (size_t)grid * parts * cap * 24;
+    if (need > h->tlog_bytes || (size_t)grid * parts > h->tlog_cnt_cap) {
+      HIP_TRY(h, hipStreamSynchronize(h->stream));  // an earlier launch may still read the old log
+      if (need > h->tlog_bytes) {
+        (void)hipFree(h->d_tlog);
+        h->d_tlog = nullptr;
+        h->tlog_bytes = 0;
+        HIP_TRY(h, hipMalloc(&h->d_tlog, need));
+        h->tlog_bytes = need;
+      }
+      if ((size_t)grid * parts > h->tlog_cnt_cap) {
+        (void)hipFree(h->d_tlog_cnt);
+        h->d_tlog_cnt = nullptr;
+        h->tlog_cnt_cap = 0;
+        HIP_TRY(h, hipMalloc(&h->d_tlog_cnt, (size_t)grid * parts * 4));
+        h->tlog_cnt_cap = (size_t)grid * parts;
+      }
+    }
+    p.tlog = h->d_tlog;
+    p.tlog_cnt = h->d_tlog_cnt;
+    p.tlog_cap = (uint32_t)cap;
+    p.tlog_rshift = rshift;
+    p.tlog_parts = parts;
+  }
+#endif
   const int slot = (int)(h->nlaunch % nmg_engine::kRing);
   if (!h->ring0[slot]) {
     HIP_TRY(h, hipEventCreate(&h->ring0[slot]));
@@ -2325,7 +2491,22 @@ static int launch_attribution(nmg_engine* h, const uint8_t* data, const BufDesc*
       hipLaunchKernelGGL(kernel_for(false, mode), dim3(grid), dim3(kWG), 0, h->stream, p);
     }
     HIP_TRY(h, hipGetLastError());
-    if (p.pk64) {
+    if (p.tlog) {  // sums the log per entry range, folds the packed counters
+      TlogParams r;
+      r.tlog = p.tlog;
+      r.tlog_cnt = p.tlog_cnt;
+      r.sum64 = h->d_sum64;
+      r.min64 = h->d_min64;
+      r.pk64 = p.pk64;
+      r.grid = grid;
+      r.parts = p.tlog_parts;
+      r.cap = p.tlog_cap;
+      r.rshift = p.tlog_rshift;
+      r.nb_entries = h->E;
+      r.pk_shift = p.pk_shift;
+      hipLaunchKernelGGL(tlog_reduce_kernel, dim3(p.tlog_parts), dim3(1024), 0, h->stream, r);
+      HIP_TRY(h, hipGetLastError());
+    } else if (p.pk64) {
       const uint32_t blocks = (uint32_t)std::min<uint64_t>(2048, (2ull * h->E + 255) / 256);
       hipLaunchKernelGGL(unpack_kernel, dim3(blocks), dim3(256), 0, h->stream, h->d_sum64, p.pk64, h->E,
                          p.pk_shift);
