@@ -279,10 +279,40 @@ __device__ __forceinline__ uint32_t eytz_descend(const uint64_t* F, uint32_t lev
 //     Zero or one key inside the slot is resolved by that one load;
 //  3. more keys inside the slot (or a bucket too wide for a directory): a
 //     binary search of those keys in global memory (L2 / MALL resident).
-__device__ __forceinline__ uint32_t lower_key(const Params& p, const uint64_t* s_fences, const uint8_t* s_shift,
-                                              uint64_t addr) {
+// A lane's lookup of the next window started early (large tables): the fence
+// node of `addr` and, when the lookup needs it, its directory slot, loaded
+// while the current window is processed.  Valid for a record whose address
+// equals `addr` (idx 0: none).
+struct SpecDir {
+  uint64_t addr;
+  uint32_t idx;
+  uint2 de;
+};
+
+__device__ __forceinline__ uint32_t fence_node(const uint64_t* s_fences, uint64_t addr) {
   const uint32_t i = eytz_descend(s_fences, kFenceLevels, addr);
-  const uint32_t idx = i >> (__builtin_ctz(i) + 1);  // node of the last right turn
+  return i >> (__builtin_ctz(i) + 1);  // node of the last right turn (0: addr < every fence)
+}
+
+// The directory slot that lower_key reads for (addr, fence node idx), or
+// null when it reads none.
+__device__ __forceinline__ const uint2* dir_slot(const Params& p, const uint64_t* s_fences, const uint8_t* s_shift,
+                                                 uint64_t addr, uint32_t idx) {
+  if (idx == 0 || p.dir_log2 == 0) return nullptr;
+  const uint32_t d = 31 - __builtin_clz(idx);
+  const uint32_t b = (((idx - (1u << d)) * 2 + 1) << (kFenceLevels - 1 - d)) - 1;
+  if (b >= p.nb_fences) return nullptr;
+  const uint32_t sh = s_shift[b];
+  if (sh == kShiftSearch) return nullptr;
+  const uint64_t rel = addr - s_fences[idx];
+  const uint32_t j = (uint32_t)min(rel >> sh, (uint64_t)((1u << p.dir_log2) - 1));
+  return p.dir + ((uint64_t(b) << p.dir_log2) + j);
+}
+
+__device__ __forceinline__ uint32_t lower_key(const Params& p, const uint64_t* s_fences, const uint8_t* s_shift,
+                                              uint64_t addr, const SpecDir& sp) {
+  const bool spec = sp.idx != 0 && sp.addr == addr;
+  const uint32_t idx = spec ? sp.idx : fence_node(s_fences, addr);
   if (idx == 0) return p.nb_keys;                    // addr < first key
   // in-order rank of Eytzinger node idx at depth d of a complete tree
   const uint32_t d = 31 - __builtin_clz(idx);
@@ -298,7 +328,7 @@ __device__ __forceinline__ uint32_t lower_key(const Params& p, const uint64_t* s
     const uint32_t slots = 1u << p.dir_log2;
     const uint64_t rel = addr - f;
     const uint32_t j = (uint32_t)min(rel >> sh, (uint64_t)(slots - 1));
-    const uint2 de = p.dir[(uint64_t(b) << p.dir_log2) + j];
+    const uint2 de = spec ? sp.de : p.dir[(uint64_t(b) << p.dir_log2) + j];
     lo = k0 + (de.x & 0xffffu);
     const uint32_t cnt = de.x >> 16;
     // first key inside the slot is <= addr: the answer is among the cnt keys
@@ -505,7 +535,8 @@ __device__ __forceinline__ void match_older(const Params& p, uint32_t first, uin
 // __ma_find_mem_info_from_sample_generic (mem_analyzer.c:249-286): the
 // lower-bound node only (ht_lower_key, tools/hash.c:63-77), newest entry
 // first, inclusive timestamp window (is_sample_in_buffer, :141-155).
-__device__ __forceinline__ Match find_entry(const Params& p, const Lookup& L, uint64_t addr, uint64_t ts) {
+__device__ __forceinline__ Match find_entry(const Params& p, const Lookup& L, uint64_t addr, uint64_t ts,
+                                            const SpecDir& sp) {
   Match m;
   m.e = -1;
   m.baddr = 0;
@@ -529,7 +560,7 @@ __device__ __forceinline__ Match find_entry(const Params& p, const Lookup& L, ui
     }
     return m;
   }
-  const uint32_t k = lower_key(p, L.fences, L.shift, addr);
+  const uint32_t k = lower_key(p, L.fences, L.shift, addr, sp);
   if (k >= p.nb_keys) return m;
   const uint4* q = reinterpret_cast<const uint4*>(p.nodes + k);
   const uint4 a = q[0], b = q[1], c = q[2];
@@ -566,7 +597,7 @@ __device__ __forceinline__ void process_sample(Params& p, WgCounters& wc, LaneAc
                                                bool valid, uint64_t ts, uint64_t addr,
                                                uint64_t w, uint64_t dsrc, uint32_t access,
                                                uint32_t th, uint64_t seq, uint32_t off, uint64_t rbase,
-                                               uint64_t& vmask, uint64_t& fmask) {
+                                               uint64_t& vmask, uint64_t& fmask, const SpecDir& sp) {
   const uint32_t lvl = uint32_t(dsrc >> 5) & 0x3fff;  // data_src.mem_lvl
   // ---- global counters: update_counters(global_counters, ...) (mem_sampling.c:882)
   vmask = __ballot(valid);
@@ -615,7 +646,7 @@ __device__ __forceinline__ void process_sample(Params& p, WgCounters& wc, LaneAc
   // ---- __match_sample (mem_sampling.c:594-673)
   Match m;
   m.e = -1;
-  if (valid) m = find_entry(p, L, addr, ts);
+  if (valid) m = find_entry(p, L, addr, ts, sp);
   const int64_t e = m.e;
   fmask = __ballot(e >= 0);
   // dump modes: every SAMPLE record's match at its arena position (host
@@ -959,6 +990,15 @@ __global__ __launch_bounds__(kWG, 1) void attribute_kernel(Params p) {
   uint32_t ns0 = 0, nf0 = 0, ns1 = 0, nf1 = 0;  // per-buffer tallies: buffer idx, idx + 1
   uint64_t tacc[4] = {0, 0, 0, 0}, t_start = 0, t0 = 0, t1 = 0;
   if (TIMING) t_start = t0 = stamp();
+#ifndef NMG_NO_SPEC_DIR
+  constexpr bool kSpec = !(MODE & kModeDenseObj);  // large tables come with the hashed object mode
+#else
+  constexpr bool kSpec = false;
+#endif
+  SpecDir sp;
+  sp.addr = 0;
+  sp.idx = 0;
+  sp.de = make_uint2(0, 0);
 
   while (true) {
     const WinLane wl = win_lane(tid, cur, d0, d1, has1);
@@ -1085,9 +1125,13 @@ __global__ __launch_bounds__(kWG, 1) void attribute_kernel(Params p) {
       if (nidx + 1 < r1) nd1 = p.sbufs[nidx + 1];
     }
     const bool nhas1 = nidx + 1 < r1;
+    uint32_t npos = 0;
+    bool ncand = false;
     if (nidx < r1) {
       const WinLane nl = win_lane(tid, (uint32_t)ncur, nd0, nd1, nhas1);
       load_slot(p, nl, nd0, nd1, nx);
+      npos = nl.pos;
+      ncand = nl.cand;
     }
 
     if (TIMING && tid == 0 && win <= 8) {
@@ -1099,7 +1143,20 @@ __global__ __launch_bounds__(kWG, 1) void attribute_kernel(Params p) {
     uint64_t vm = 0, fm = 0;
     if (!(p.flags & kDbgLoadOnly))
       process_sample<MODE>(p, wc, acc, L, valid, rec.ts, rec.addr, rec.w, rec.dsrc, d0.access, d0.thread_rank, rseq, roff,
-                           rbase, vm, fm);
+                           rbase, vm, fm, sp);
+    if (kSpec && !p.lds_nodes && (p.flags & NMG_F_MATCH_SAMPLES)) {
+      // start the next window's lookup: its record (loaded above, arrived
+      // during this window's lookups) -> fence node -> directory slot load,
+      // in flight across the flush and the barrier.  Used when the record
+      // this lane processes next has the same address (fast-path windows).
+      sp.idx = 0;
+      if (nidx < r1 && ncand) {
+        sp.addr = decode_rec(nx, npos).addr;
+        sp.idx = fence_node(L.fences, sp.addr);
+        const uint2* ds = dir_slot(p, L.fences, L.shift, sp.addr, sp.idx);
+        if (ds) sp.de = *ds;
+      }
+    }
     {
       // lanes of this wave in buffer idx + 1 (tid >= n0)
       const uint32_t w0 = uint32_t(tid) & ~63u;
@@ -1203,9 +1260,21 @@ __global__ __launch_bounds__(1024, 1) void tlog_reduce_kernel(TlogParams r) {
   const uint32_t part = blockIdx.x, tid = threadIdx.x;
   for (uint32_t w = tid; w < r.grid; w += 1024) s_pre[w + 1] = r.tlog_cnt[uint64_t(w) * r.parts + part];
   __syncthreads();
-  if (tid == 0) {  // exclusive prefix over the source workgroups
-    s_pre[0] = 0;
-    for (uint32_t w = 1; w <= r.grid; w++) s_pre[w] += s_pre[w - 1];
+  if (tid < 64) {  // prefix over the source workgroups: a chunk per lane, then a wave scan
+    const uint32_t per = (r.grid + 63) / 64, b = min(tid * per, r.grid), e = min(b + per, r.grid);
+    uint32_t sum = 0;
+    for (uint32_t w = b; w < e; w++) sum += s_pre[w + 1];
+    uint32_t incl = sum;
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t t = __shfl_up(incl, o, 64);
+      if ((int)tid >= o) incl += t;
+    }
+    uint32_t run = incl - sum;
+    for (uint32_t w = b; w < e; w++) {
+      run += s_pre[w + 1];
+      s_pre[w + 1] = run;
+    }
+    if (tid == 0) s_pre[0] = 0;
   }
   __syncthreads();
   const uint32_t total = s_pre[r.grid];
@@ -1219,41 +1288,73 @@ __global__ __launch_bounds__(1024, 1) void tlog_reduce_kernel(TlogParams r) {
       s_ord[j] = ~0ull;
     }
     __syncthreads();
-    for (uint32_t i = tid; i < total; i += 1024) {
-      uint32_t lo = 0, hi = r.grid;  // source workgroup: s_pre[lo] <= i < s_pre[lo + 1]
-      while (hi - lo > 1) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (s_pre[mid] <= i) lo = mid;
-        else hi = mid;
+    constexpr int kU = 4;  // records per thread in flight
+    for (uint32_t i0 = tid; i0 < total; i0 += kU * 1024) {
+      unsigned long long kv[kU], wv[kU], ov[kU];
+#pragma unroll
+      for (int u = 0; u < kU; u++) {
+        const uint32_t i = i0 + u * 1024;
+        kv[u] = ~0ull;  // (no record: entry ids are < 2^31)
+        if (i >= total) continue;
+        uint32_t lo = 0, hi = r.grid;  // source workgroup: s_pre[lo] <= i < s_pre[lo + 1]
+        while (hi - lo > 1) {
+          const uint32_t mid = (lo + hi) >> 1;
+          if (s_pre[mid] <= i) lo = mid;
+          else hi = mid;
+        }
+        const unsigned long long* q = r.tlog + ((uint64_t(lo) * r.parts + part) * r.cap + (i - s_pre[lo])) * 3;
+        kv[u] = q[0];
+        wv[u] = q[1];
+        ov[u] = q[2];
       }
-      const unsigned long long* q = r.tlog + ((uint64_t(lo) * r.parts + part) * r.cap + (i - s_pre[lo])) * 3;
-      const unsigned long long k = q[0];
-      const uint32_t e = uint32_t(k) & 0x7fffffffu, a = uint32_t(k) >> 31;
-      const uint64_t j = e - base;
-      if (e < base || j >= n) continue;
-      atomicAdd(&s_cnt[a][j], uint32_t(k >> 32));
-      const unsigned long long wt = q[1];
-      if (wt) atomicAdd(&s_wt[a][j], wt);
-      atomicMin(&s_ord[j], q[2]);
+#pragma unroll
+      for (int u = 0; u < kU; u++) {
+        if (kv[u] == ~0ull) continue;
+        const uint32_t e = uint32_t(kv[u]) & 0x7fffffffu, a = uint32_t(kv[u]) >> 31;
+        const uint64_t j = e - base;
+        if (e < base || j >= n) continue;
+        atomicAdd(&s_cnt[a][j], uint32_t(kv[u] >> 32));
+        if (wv[u]) atomicAdd(&s_wt[a][j], wv[u]);
+        atomicMin(&s_ord[j], ov[u]);
+      }
     }
     __syncthreads();
-    for (uint32_t j = tid; j < n; j += 1024) {
-      const uint64_t e = base + j;
-      for (uint32_t a = 0; a < 2; a++) {
-        uint64_t c = s_cnt[a][j], w = s_wt[a][j];
-        if (r.pk64) {
-          const uint64_t v = r.pk64[uint64_t(a) * r.nb_entries + e];
+    // every global word of kU entries loaded before any is updated (the
+    // read-modify-writes would otherwise wait on one load at a time)
+    for (uint32_t j0 = tid; j0 < n; j0 += kU * 1024) {
+      uint64_t gc[kU][2], gw[kU][2], pv[kU][2], gm[kU];
+#pragma unroll
+      for (int u = 0; u < kU; u++) {
+        const uint32_t j = j0 + u * 1024;
+        if (j >= n) continue;
+        const uint64_t e = base + j;
+#pragma unroll
+        for (uint32_t a = 0; a < 2; a++) {
+          gc[u][a] = r.sum64[objcw_index(e, a, 0, r.nb_entries)];
+          gw[u][a] = r.sum64[objcw_index(e, a, 1, r.nb_entries)];
+          pv[u][a] = r.pk64 ? r.pk64[uint64_t(a) * r.nb_entries + e] : 0;
+        }
+        gm[u] = r.min64[36 + e];
+      }
+#pragma unroll
+      for (int u = 0; u < kU; u++) {
+        const uint32_t j = j0 + u * 1024;
+        if (j >= n) continue;
+        const uint64_t e = base + j;
+#pragma unroll
+        for (uint32_t a = 0; a < 2; a++) {
+          uint64_t c = s_cnt[a][j], w = s_wt[a][j];
+          const uint64_t v = pv[u][a];
           if (v) {
             c += v >> r.pk_shift;
             w += v & ((1ull << r.pk_shift) - 1);
             r.pk64[uint64_t(a) * r.nb_entries + e] = 0;
           }
+          if (c) r.sum64[objcw_index(e, a, 0, r.nb_entries)] = gc[u][a] + c;
+          if (w) r.sum64[objcw_index(e, a, 1, r.nb_entries)] = gw[u][a] + w;
         }
-        if (c) r.sum64[objcw_index(e, a, 0, r.nb_entries)] += c;
-        if (w) r.sum64[objcw_index(e, a, 1, r.nb_entries)] += w;
+        if (s_ord[j] < gm[u]) r.min64[36 + e] = s_ord[j];
       }
-      const uint64_t o = s_ord[j];
-      if (o < r.min64[36 + e]) r.min64[36 + e] = o;
     }
     __syncthreads();
   }
