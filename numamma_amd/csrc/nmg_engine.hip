@@ -1,34 +1,8 @@
-// nmg_engine.hip -- MI355X (gfx950) sample-attribution engine + C-ABI.
-//
-// Replaces NumaMMa's offline analysis loop (src/mem_sampling.c:311-346 ->
-// __analyze_buffer :815-927 -> update_counters :517-592 / __match_sample
-// :594-673 -> ma_find_mem_info_from_sample src/mem_analyzer.c:249-306 ->
-// ma_get_block :494-534).
-//
-// Kernel shape (DESIGN.md "Kernels"):
-//   * persistent grid, one 1024-thread workgroup per CU, each owning a
-//     byte-balanced range of the buffer list sorted by stream (access type,
-//     thread rank); a buffer is walked in windows of 1024 stride slots of
-//     40 B, one per lane, loaded straight into registers, the next window
-//     issued before the current one is processed;
-//   * fast path when every slot of a window holds a whole 40 B record (the
-//     record chain is then known without reading it sequentially); otherwise
-//     wave 0 follows the header chain exactly as the reference's byte cursor
-//     does (variable-size non-SAMPLE records, size==0 abort, truncation);
-//   * global counters (mem_counters[2]) in per-lane registers / LDS, flushed
-//     once per stream run;
-//   * object lookup: <= 1023 keys, an Eytzinger search of keys + node records
-//     held in LDS; larger tables, an Eytzinger search of up to 4095 LDS fences,
-//     one 8 B load of the fence bucket's directory slot, then the node record
-//     (L2 / MALL) -> older entries of the node (quirks Q1-Q4);
-//   * per-object and per-page counters aggregated in LDS tables (dense by
-//     entry id / cell for small tables, first-come 8-way buckets otherwise),
-//     flushed with global atomics at stream ends and on a window cadence;
-//     integer adds, mins and maxes are order independent, so results are
-//     bit-exact;
-//   * host side: the C-ABI, the stream-sorted schedule, the streaming pipeline
-//     (copy stream + double-buffered pinned staging), the reset kernel and the
-//     result downloads.
+// nmg_engine.hip -- host side of the MI355X sample-attribution engine: the
+// C-ABI (include/numamma_gpu.h), table upload and lookup-structure build, the
+// stream-sorted schedule, the streaming pipeline (copy stream + double-buffered
+// pinned staging), launches and result downloads.  The kernels are in
+// nmg_kernels.hip (DESIGN.md "Kernels").
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -43,1378 +17,7 @@
 #include <thread>
 #include <vector>
 
-#include "nmg_internal.h"
-
-namespace nmg {
-
-constexpr int kWG = 1024;                      // one workgroup per CU
-constexpr uint32_t kSampleType = 9;            // PERF_RECORD_SAMPLE
-constexpr uint32_t kRecBytes = 40;             // perf_event_header (8) + struct mem_sample (32)
-constexpr uint32_t kWinBytes = kWG * kRecBytes;  // one 40 B stride slot per lane per window
-constexpr uint32_t kLdsNodes = 1023;           // keys held in LDS with their node records (<= 10 levels)
-// Larger tables: up to 4095 fences (every S-th key) in a 12-level Eytzinger
-// tree in LDS, then one load from a per-fence-bucket directory in global memory
-constexpr uint32_t kFenceLevels = 12;
-constexpr uint32_t kMaxFences = (1u << kFenceLevels) - 1;
-constexpr uint32_t kShiftSearch = 0xff;        // bucket without a directory: binary search of its keys
-// One LDS region holds the lookup structure of either mode:
-//   <= kLdsNodes keys: Eytzinger keys (8 KiB) | node records (32 KiB) | node info (8 KiB)
-//   larger tables:     Eytzinger fences (32 KiB) | per-bucket directory shift (4 KiB)
-constexpr uint32_t kTabBytes = 48 * 1024;
-static_assert((kLdsNodes + 1) * (8 + 32 + 8) <= kTabBytes, "small-table LDS layout");
-static_assert((kMaxFences + 1) * (8 + 1) <= kTabBytes, "fence LDS layout");
-constexpr uint32_t kMaxList = kWG;             // slow path: SAMPLE offsets listed per step
-// per-stream LDS aggregation tables (flushed to global at a stream change and
-// on a window cadence)
-constexpr uint32_t kObjSlots = 2048;           // entry -> (count, weight, first ordinal)
-// long-tail log (hashed object mode): per workgroup, kLogParts sub-logs by
-// entry range of 24 B records {entry | access << 31, count, weight, ordinal}
-constexpr uint32_t kLogParts = 256;
-constexpr uint32_t kLogChunk = 4096;   // entries per LDS pass of tlog_reduce_kernel
-constexpr uint32_t kLogMaxGrid = 1024;  // attribution workgroups a log can serve
-constexpr uint32_t kPageBuckets = 896;         // dense page cell -> count: 8-slot buckets
-constexpr uint32_t kPageSlots = kPageBuckets * 8;  // 7168 cells (56 KiB)
-constexpr uint32_t kObjBuckets = kObjSlots / 8;
-// hashed (non-dense) tables are flushed at least every kTableWindows windows:
-// u32 counts stay far from overflow and the first-come slots are re-learnt
-constexpr uint32_t kTableWindows = 256;
-// Dense modes (template flags of attribute_kernel):
-//   kModeDenseObj:  nb_entries <= kObjSlots: slot = entry id, no key check;
-//   kModeDensePage: dense histogram cells per thread <= kDensePageCells: u16
-//                   counts, two per LDS word, flushed at least every
-//                   kDensePageWindows windows (<= 1024 samples per cell each,
-//                   so a u16 cannot overflow into its neighbour)
-constexpr int kModeDenseObj = 1, kModeDensePage = 2;
-constexpr uint32_t kDensePageCells = kPageSlots * 4;  // the page table's 56 KiB as u16 cells
-constexpr uint32_t kDensePageWindows = 62;
-#ifdef NMG_NO_PACK_OBJ
-constexpr bool kPackObj = false;
-#else
-constexpr bool kPackObj = true;
-#endif
-constexpr uint32_t kPackShift = 44;  // kModeDenseObj: per-entry count << 44 | weight sum
-static_assert((uint64_t)kDensePageWindows * kWG < (1ull << (64 - kPackShift)), "packed count");
-static_assert(kDensePageWindows * kWG < 65536u, "u16 page counts");
-constexpr uint32_t kEmpty32 = 0xffffffffu;
-constexpr uint64_t kEmpty64 = ~0ull;
-// internal ablation switches (tools/ablate.py only; not part of the C-ABI)
-constexpr uint32_t kDbgLoadOnly = 0x100;   // stage + validate windows, decode nothing
-constexpr uint32_t kDbgNoGlobal = 0x200;   // skip the global mem_counters update
-constexpr uint32_t kDbgNoFlush = 0x400;    // LDS tables filled but never written to global
-constexpr uint32_t kDbgNoTables = 0x800;   // lookup only: no per-object / per-page accumulation
-constexpr uint32_t kDbgTiming = 0x1000;    // per-wave phase cycle counts (tools/phase_timing.py)
-constexpr int kTimingWords = 24;           // per wave: load+check, barrier, process, rest, total, windows, -, -,
-                                           // then (wave 0) 8 x 2 words of window trace
-
-// PERF_MEM_LVL_* (/usr/include/linux/perf_event.h:1250-1263)
-constexpr uint32_t LVL_NA = 0x01, LVL_HIT = 0x02, LVL_MISS = 0x04;
-__constant__ uint32_t c_level_mask[9] = {0x08,  0x20,  0x40,  0x10,  0x80,
-                                         0x300, 0xC00, 0x1000, 0x2000};
-// order: L1, L2, L3, LFB, LOC_RAM, REM_RAM1|2, REM_CCE1|2, IO, UNC
-// (the bucket order of struct mem_counters, mem_analyzer.h:23-40)
-
-struct BufDesc {
-  uint64_t offset;  // byte offset in the data arena (16-aligned)
-  uint32_t len;     // linearised length (< 4 GiB, mem_sampling.c:831-834)
-  uint32_t thread_rank;
-  uint32_t access;
-  uint32_t pad;  // (schedule copy) index of the buffer in submission order
-  uint64_t seq;  // analysis-order index (global across shards)
-};
-static_assert(sizeof(BufDesc) == 32, "BufDesc");
-
-// One table entry (64 B).  The node array holds, for node k, a copy of its
-// newest entry with `first` = its entry id and `count` = the node's number of
-// entries, so the common one-entry node costs a single dependent load.
-struct DevEntry {
-  uint64_t addr;   // buffer_addr
-  uint64_t end;    // buffer_addr + buffer_size (mod 2^64, as the reference's void* sum)
-  uint64_t alloc;  // alloc_date
-  uint64_t free;   // free_date
-  uint64_t hist;   // dense histogram base cell, or kHistSparse
-  uint32_t sidx;   // sparse index (valid when hist == kHistSparse && sidx != ~0u)
-  uint32_t first;  // (node records) entry id of the node's newest entry
-  uint32_t count;  // (node records) entries of the node
-  uint32_t pad0;
-  uint64_t pad1;
-};
-static_assert(sizeof(DevEntry) == 64, "DevEntry");
-
-struct Params {
-  const uint8_t* data;
-  const BufDesc* sbufs;    // descriptors in schedule order (sorted by stream; .pad = buffer index)
-  const uint32_t* ranges;  // [gridDim.x + 1]: workgroup w takes sbufs[ranges[w] .. ranges[w+1])
-  uint32_t nb_bufs;
-  uint32_t nb_keys;
-  const uint64_t* keys;      // [nb_keys] sorted unique keys
-  const DevEntry* nodes;     // [nb_keys] node records
-  const DevEntry* entries;
-  // large tables (nb_keys > kLdsNodes): fence b = keys[b * fence_step]
-  const uint64_t* ffences;   // [2^kFenceLevels] fences in Eytzinger order, [0] unused, ~0 padding
-  const uint8_t* fshift;     // [nb_fences] slot width log2 of bucket b's directory, or kShiftSearch
-  const uint2* dir;          // [nb_fences << dir_log2] {lo | cnt << 16, offset of the slot's first key}
-  uint32_t nb_fences;
-  uint32_t fence_log2;       // fence_step = 2^fence_log2 keys per bucket
-  uint32_t dir_log2;         // directory slots per bucket = 2^dir_log2 (0: fence_step == 1, no directory)
-  uint32_t nb_threads;
-  uint32_t flags;
-  uint32_t nb_entries;
-  uint32_t lds_nodes;    // nb_keys <= kLdsNodes: keys + node records in LDS, Eytzinger order
-                         // (arrays of kLdsNodes + 1 = 2^10 slots, index 0 unused)
-  uint32_t elevels;      // levels of the Eytzinger tree (2^elevels - 1 >= nb_keys)
-  const uint64_t* efences;   // [2^elevels] keys in Eytzinger (BFS) order, [0] unused, ~0 padding
-  const DevEntry* enodes;    // [2^elevels] node records in the same order
-  uint32_t sparse_mask;  // capacity - 1 (power of two)
-  uint64_t hist_cells;   // dense cells per thread: histogram index = thread * hist_cells + cell
-  uint64_t* sum64;
-  uint64_t* min64;
-  uint64_t* max64;
-  uint32_t* hist;
-  uint32_t* bufcnt;  // [2][nb_bufs]: samples, found
-  uint64_t* sparse_keys;
-  uint32_t* sparse_vals;
-  uint32_t* sparse_dirty;  // set on any sparse insert: the next reset must clear the table
-  uint32_t* smatch;        // NMG_F_SAMPLE_MATCHES: [(buffer offset + record offset) / 8] = entry + 1, 0 = none
-  unsigned long long* dbg;  // kDbgTiming: [grid][waves][kTimingWords]
-  // hashed object mode: per-launch packed [2 access][E] (count << pk_shift |
-  // weight) for the global path, one atomic instead of two; exact because
-  // samples per launch < 2^(64 - pk_shift) and only weights < pk_wlim are
-  // packed (their sum < 2^pk_shift); unpack_kernel adds it into sum64
-  unsigned long long* pk64;  // null: packing off
-  uint32_t pk_shift;
-  uint64_t pk_wlim;
-  // long-tail log: instead of scattered global atomics, table-full samples
-  // and flushed slots append to sub-log (workgroup, entry >> tlog_rshift);
-  // tlog_reduce_kernel sums each entry range from LDS.  A full sub-log falls
-  // back to the atomics.
-  unsigned long long* tlog;  // [grid][tlog_parts][tlog_cap][3] u64; null: off
-  uint32_t* tlog_cnt;        // [grid][tlog_parts] records written
-  uint32_t tlog_cap, tlog_rshift, tlog_parts;
-};
-
-// ---------------------------------------------------------------------------
-// device helpers
-
-__device__ __forceinline__ uint64_t wave_sum(uint64_t v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
-}
-
-// Full-wave u32 sum with DPP (VALU only, no LDS traffic): Hillis-Steele
-// within each 16-lane row, then row_bcast:15 / row_bcast:31; lane 63 holds
-// the total.
-template <int CTRL, int ROW_MASK>
-__device__ __forceinline__ uint32_t dpp0(uint32_t v) {
-  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROW_MASK, 0xf, true);
-}
-__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
-  v += dpp0<0x111, 0xf>(v);  // row_shr:1
-  v += dpp0<0x112, 0xf>(v);  // row_shr:2
-  v += dpp0<0x114, 0xf>(v);  // row_shr:4
-  v += dpp0<0x118, 0xf>(v);  // row_shr:8
-  v += dpp0<0x142, 0xa>(v);  // row_bcast:15 into rows 1 and 3
-  v += dpp0<0x143, 0xc>(v);  // row_bcast:31 into rows 2 and 3
-  return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
-}
-// Sum of per-lane weights; `big` (wave-uniform) = some weight >= 2^26, in
-// which case 64 lanes could overflow 32 bits and the u64 path is taken.
-__device__ __forceinline__ uint64_t wave_sum_w(uint64_t w, bool big) {
-  return big ? wave_sum(w) : (uint64_t)wave_sum_u32((uint32_t)w);
-}
-
-// update_counters' level classification (mem_sampling.c:521-591) as an
-// 18-bit mask: bit g (0..8) = hit bucket of level group g, bit 9+g = miss.
-// Groups: L1, L2, L3, LFB, local RAM, remote RAM 1|2, remote cache 1|2, IO,
-// uncached (the bucket order of struct mem_counters).  HIT beats MISS and
-// every group is independent (quirk Q12).
-__device__ __forceinline__ uint32_t bucket_mask(uint32_t lvl) {
-  uint32_t g = ((lvl >> 3) & 1) | (((lvl >> 5) & 1) << 1) | (((lvl >> 6) & 1) << 2) |
-               (((lvl >> 4) & 1) << 3) | (((lvl >> 7) & 1) << 4) | ((((lvl >> 8) | (lvl >> 9)) & 1) << 5) |
-               ((((lvl >> 10) | (lvl >> 11)) & 1) << 6) | (((lvl >> 12) & 1) << 7) | (((lvl >> 13) & 1) << 8);
-  if (lvl & LVL_HIT) return g;
-  if (lvl & LVL_MISS) return g << 9;
-  return 0;
-}
-
-__device__ __forceinline__ void set_error(Params& p, uint64_t seq, uint32_t off, uint32_t code) {
-  uint64_t w = (seq << 40) | (uint64_t(off) << 8) | code;
-  atomicMin(reinterpret_cast<unsigned long long*>(p.min64 + 36 + p.nb_entries),
-            (unsigned long long)w);
-}
-
-// Descend `levels` levels of an Eytzinger tree (node i has children 2i, 2i+1)
-// from the root and return the index below the last level: one 8 B LDS read
-// per level.  (NMG_EYTZ_GROUPED reads node i, its children and grandchildren
-// together -- one round trip per three levels -- but the extra LDS bytes and
-// bank conflicts cost more than the shorter chain saves.)  Reads stay below
-// 2^levels.
-__device__ __forceinline__ uint32_t eytz_descend(const uint64_t* F, uint32_t levels, uint64_t addr) {
-  uint32_t i = 1;
-#ifdef NMG_EYTZ_GROUPED  // measured slower on c2 (0.196 vs 0.182 ms): more LDS bytes and conflicts
-  for (; levels >= 3; levels -= 3) {
-    const uint64_t k0 = F[i];
-    const ulonglong2 k1 = *reinterpret_cast<const ulonglong2*>(F + 2 * i);
-    const ulonglong2 k2a = *reinterpret_cast<const ulonglong2*>(F + 4 * i);
-    const ulonglong2 k2b = *reinterpret_cast<const ulonglong2*>(F + 4 * i + 2);
-    const bool b0 = k0 <= addr;
-    const bool b1 = (b0 ? k1.y : k1.x) <= addr;
-    const uint64_t kg = b0 ? (b1 ? k2b.y : k2b.x) : (b1 ? k2a.y : k2a.x);
-    const bool b2 = kg <= addr;
-    i = 8 * i + 4 * (uint32_t)b0 + 2 * (uint32_t)b1 + (uint32_t)b2;
-  }
-#endif
-  for (; levels > 0; levels--) i = 2 * i + (F[i] <= addr ? 1u : 0u);
-  return i;
-}
-
-// Largest key <= addr (ht_lower_key, tools/hash.c:63-77) for tables larger
-// than kLdsNodes.  Returns nb_keys when no key <= addr.
-//  1. LDS: branch-free search of the 12-level Eytzinger fence tree -> bucket b
-//     (keys [b*S, (b+1)*S), S = fence_step);
-//  2. global: one 8 B directory slot of bucket b.  The bucket's key span is
-//     cut into 2^dir_log2 equal slots of 2^shift bytes; a slot holds the
-//     bucket-relative index of the largest key <= the slot start, the number
-//     of keys strictly inside the slot and the offset of the first of them.
-//     Zero or one key inside the slot is resolved by that one load;
-//  3. more keys inside the slot (or a bucket too wide for a directory): a
-//     binary search of those keys in global memory (L2 / MALL resident).
-// A lane's lookup of the next window started early (large tables): the fence
-// node of `addr` and, when the lookup needs it, its directory slot, loaded
-// while the current window is processed.  Valid for a record whose address
-// equals `addr` (idx 0: none).
-struct SpecDir {
-  uint64_t addr;
-  uint32_t idx;
-  uint2 de;
-};
-
-__device__ __forceinline__ uint32_t fence_node(const uint64_t* s_fences, uint64_t addr) {
-  const uint32_t i = eytz_descend(s_fences, kFenceLevels, addr);
-  return i >> (__builtin_ctz(i) + 1);  // node of the last right turn (0: addr < every fence)
-}
-
-// The directory slot that lower_key reads for (addr, fence node idx), or
-// null when it reads none.
-__device__ __forceinline__ const uint2* dir_slot(const Params& p, const uint64_t* s_fences, const uint8_t* s_shift,
-                                                 uint64_t addr, uint32_t idx) {
-  if (idx == 0 || p.dir_log2 == 0) return nullptr;
-  const uint32_t d = 31 - __builtin_clz(idx);
-  const uint32_t b = (((idx - (1u << d)) * 2 + 1) << (kFenceLevels - 1 - d)) - 1;
-  if (b >= p.nb_fences) return nullptr;
-  const uint32_t sh = s_shift[b];
-  if (sh == kShiftSearch) return nullptr;
-  const uint64_t rel = addr - s_fences[idx];
-  const uint32_t j = (uint32_t)min(rel >> sh, (uint64_t)((1u << p.dir_log2) - 1));
-  return p.dir + ((uint64_t(b) << p.dir_log2) + j);
-}
-
-__device__ __forceinline__ uint32_t lower_key(const Params& p, const uint64_t* s_fences, const uint8_t* s_shift,
-                                              uint64_t addr, const SpecDir& sp) {
-  const bool spec = sp.idx != 0 && sp.addr == addr;
-  const uint32_t idx = spec ? sp.idx : fence_node(s_fences, addr);
-  if (idx == 0) return p.nb_keys;                    // addr < first key
-  // in-order rank of Eytzinger node idx at depth d of a complete tree
-  const uint32_t d = 31 - __builtin_clz(idx);
-  const uint32_t b = (((idx - (1u << d)) * 2 + 1) << (kFenceLevels - 1 - d)) - 1;
-  if (b >= p.nb_fences) return p.nb_keys - 1;  // ~0 padding: addr == UINT64_MAX
-  const uint32_t k0 = b << p.fence_log2;
-  if (p.dir_log2 == 0) return k0;  // one key per fence
-  const uint32_t kend = min(k0 + (1u << p.fence_log2), p.nb_keys);
-  const uint32_t sh = s_shift[b];
-  uint32_t lo, n;  // answer in [lo, lo + n): keys[lo] <= addr known
-  if (sh != kShiftSearch) {
-    const uint64_t f = s_fences[idx];
-    const uint32_t slots = 1u << p.dir_log2;
-    const uint64_t rel = addr - f;
-    const uint32_t j = (uint32_t)min(rel >> sh, (uint64_t)(slots - 1));
-    const uint2 de = spec ? sp.de : p.dir[(uint64_t(b) << p.dir_log2) + j];
-    lo = k0 + (de.x & 0xffffu);
-    const uint32_t cnt = de.x >> 16;
-    // first key inside the slot is <= addr: the answer is among the cnt keys
-    if (cnt == 0 || rel - (uint64_t(j) << sh) < de.y) return lo;
-    lo += 1;
-    n = cnt;
-  } else {
-    lo = k0;
-    n = kend - k0;
-  }
-  while (n > 1) {  // keys[lo] <= addr < keys[lo + n] (or lo + n == bucket end)
-    const uint32_t half = n >> 1;
-    const bool le = p.keys[lo + half] <= addr;
-    lo = le ? lo + half : lo;
-    n = le ? n - half : half;
-  }
-  return lo;
-}
-
-// __ma_find_mem_info_from_sample_generic (mem_analyzer.c:249-286) with
-// is_sample_in_buffer (:141-155): only the lower-bound node, newest entry first.
-__device__ __forceinline__ bool entry_match(uint4 a, uint4 b, uint64_t addr, uint64_t ts) {
-  const uint64_t baddr = (uint64_t(a.y) << 32) | a.x, bend = (uint64_t(a.w) << 32) | a.z;
-  const uint64_t alloc = (uint64_t(b.y) << 32) | b.x, fr = (uint64_t(b.w) << 32) | b.z;
-  return baddr <= addr && addr < bend && alloc <= ts && ts <= fr;
-}
-
-__device__ __forceinline__ void sparse_add(Params& p, uint64_t key, uint64_t seq, uint32_t off, uint32_t cnt) {
-  *p.sparse_dirty = 1u;
-  uint64_t h = (key * 0x9E3779B97F4A7C15ull) >> 20;
-  uint32_t slot = uint32_t(h) & p.sparse_mask;
-  for (uint32_t probe = 0; probe <= p.sparse_mask; probe++) {
-    unsigned long long prev = atomicCAS(reinterpret_cast<unsigned long long*>(p.sparse_keys + slot),
-                                        ~0ull, (unsigned long long)key);
-    if (prev == ~0ull || prev == key) {
-      atomicAdd(p.sparse_vals + slot, cnt);
-      return;
-    }
-    slot = (slot + 1) & p.sparse_mask;
-  }
-  set_error(p, seq, off, kErrCapacity);
-}
-
-// Per-workgroup privatised counters of the stream (access type, thread rank)
-// being analysed.  One stream at a time per workgroup, so (entry) and
-// (entry, page) are the keys of the aggregation tables.
-struct WgCounters {
-  unsigned long long sums[kGlobalSums];  // total_count, total_weight, na, 18 x (count, sum)
-  unsigned long long mins[18];
-  unsigned long long maxs[18];
-  alignas(16) unsigned int okey[kObjSlots];  // entry id, 8 per bucket (hashed modes)
-  unsigned int ocnt[kObjSlots];
-  unsigned long long ofirst[kObjSlots];  // smallest (seq << 32 | offset): first match
-  unsigned long long owt[kObjSlots];
-  union {
-    struct {
-      uint4 pkey4[kPageSlots / 4];  // dense cell index (hist_base(entry) + page), 8 per bucket
-      unsigned int pcnt[kPageSlots];
-    };
-    unsigned int pdense[kDensePageCells / 2];  // kModeDensePage: u16 count per cell, two per word
-  };
-  unsigned int tcur[kLogParts];  // long-tail sub-log cursors
-};
-
-// Entries (tables with more than kObjSlots entries): a Fibonacci hash picks
-// one 8-slot bucket, found with two 16 B LDS reads; a missing entry takes the
-// first empty slot by CAS (same protocol as page_slot below).  Slots are
-// first come, first served until the next flush (stream end or the
-// kTableWindows cadence): the hot entries of a Zipf-like stream claim them
-// in its first windows, and a full bucket sends the sample straight to the
-// global counters -- no probe chains and no fill-level flushes.
-__device__ __forceinline__ uint32_t obj_bucket(uint32_t e) {
-  return (uint32_t)(((uint64_t)(e * 0x9E3779B1u) * kObjBuckets) >> 32);
-}
-
-__device__ __forceinline__ int bucket_slot(unsigned int* slots8, uint32_t key) {
-  const uint4 k0 = reinterpret_cast<const uint4*>(slots8)[0], k1 = reinterpret_cast<const uint4*>(slots8)[1];
-  uint32_t k[8] = {k0.x, k0.y, k0.z, k0.w, k1.x, k1.y, k1.z, k1.w};
-  int j = -1;
-#pragma unroll
-  for (int i = 7; i >= 0; i--) j = k[i] == key ? i : j;
-  if (j >= 0) return j;
-  for (int attempt = 0; attempt < 8; attempt++) {
-    int f = -1;
-#pragma unroll
-    for (int i = 7; i >= 0; i--) f = k[i] == kEmpty32 ? i : f;
-    if (f < 0) return -1;
-    const unsigned prev = atomicCAS(&slots8[f], kEmpty32, key);
-    if (prev == kEmpty32 || prev == key) return f;
-#pragma unroll
-    for (int i = 0; i < 8; i++) k[i] = i == f ? prev : k[i];
-  }
-  return -1;
-}
-
-__device__ __forceinline__ int obj_slot(WgCounters& wc, uint32_t e) {
-  const uint32_t hb = obj_bucket(e);
-  const int j = bucket_slot(&wc.okey[hb * 8], e);
-  return j < 0 ? -1 : (int)(hb * 8 + (uint32_t)j);
-}
-
-// Page cells: a Fibonacci hash picks one 8-slot bucket (two 16 B LDS reads,
-// no probe chain).  A missing cell takes the first empty slot by CAS; every
-// inserter scans the bucket in the same order and a slot leaves "empty" only
-// once, so a cell never lands in two slots.  A full bucket returns -1 (the
-// caller then updates global memory directly).
-__device__ __forceinline__ uint32_t page_bucket(uint32_t cell) {
-  return (uint32_t)(((uint64_t)(cell * 0x9E3779B1u) * kPageBuckets) >> 32);
-}
-
-__device__ __forceinline__ int page_slot(WgCounters& wc, uint32_t cell) {
-  const uint32_t hb = page_bucket(cell);
-  const int j = bucket_slot(reinterpret_cast<unsigned int*>(&wc.pkey4[2 * hb]), cell);
-  return j < 0 ? -1 : (int)(hb * 8 + (uint32_t)j);
-}
-
-// Per-lane privatised mem_counters of the current stream: packed u16 counts
-// and u32 weight sums per bucket, plus total count / weight / N/A.  Bounded:
-// drained at least every kDrainWindows windows (one record per lane per
-// window) and only weights < 2^23 take this path, so nothing overflows
-// (256 x 2^23 = 2^31).
-constexpr uint32_t kDrainWindows = 256;
-constexpr uint64_t kLaneMaxWeight = 1ull << 23;
-static_assert((uint64_t)kDensePageWindows * kWG * kLaneMaxWeight < (1ull << kPackShift), "packed weight");
-// Only the 9 hit buckets live in registers (the common case in PEBS data);
-// miss buckets are updated in LDS directly.
-struct LaneAcc {
-  uint32_t cnt2[5];  // counts of hit buckets 2k (low 16 bits) and 2k+1 (high 16 bits)
-  uint32_t sum[9];
-  uint32_t tc, tw, na;
-};
-
-__device__ __forceinline__ void lane_acc_clear(LaneAcc& a) {
-#pragma unroll
-  for (int k = 0; k < 5; k++) a.cnt2[k] = 0;
-#pragma unroll
-  for (int k = 0; k < 9; k++) a.sum[k] = 0;
-  a.tc = a.tw = a.na = 0;
-}
-
-// exact sum over the wave of a u32 per lane (as two 16-bit halves, DPP)
-__device__ __forceinline__ uint64_t wave_sum_u32x(uint32_t v) {
-  const uint32_t lo = wave_sum_u32(v & 0xffffu), hi = wave_sum_u32(v >> 16);
-  return (uint64_t)lo + ((uint64_t)hi << 16);
-}
-
-// lanes -> workgroup LDS counters (every lane of the wave calls this)
-__device__ __forceinline__ void lane_acc_drain(LaneAcc& a, WgCounters& wc, int lane) {
-  if (__ballot(a.tc != 0) == 0) return;
-  const uint64_t tc = wave_sum_u32x(a.tc), tw = wave_sum_u32x(a.tw), na = wave_sum_u32x(a.na);
-  if (lane == 0) {
-    atomicAdd(&wc.sums[0], (unsigned long long)tc);
-    if (tw) atomicAdd(&wc.sums[1], (unsigned long long)tw);
-    if (na) atomicAdd(&wc.sums[2], (unsigned long long)na);
-  }
-#pragma unroll
-  for (int k = 0; k < 5; k++) {
-    if (__ballot(a.cnt2[k] != 0) == 0) continue;
-    const uint32_t c0 = wave_sum_u32(a.cnt2[k] & 0xffffu), c1 = wave_sum_u32(a.cnt2[k] >> 16);
-    if (lane == 0) {
-      if (c0) atomicAdd(&wc.sums[3 + 2 * (2 * k)], (unsigned long long)c0);
-      if (c1 && 2 * k + 1 < 9) atomicAdd(&wc.sums[3 + 2 * (2 * k + 1)], (unsigned long long)c1);
-    }
-  }
-#pragma unroll
-  for (int k = 0; k < 9; k++) {
-    if (__ballot(a.sum[k] != 0) == 0) continue;
-    const uint64_t sk = wave_sum_u32x(a.sum[k]);
-    if (lane == 0) atomicAdd(&wc.sums[4 + 2 * k], (unsigned long long)sk);
-  }
-  lane_acc_clear(a);
-}
-
-// The object table as the kernel sees it: node records in LDS (small tables)
-// or in global memory (L2/MALL resident) behind the LDS fence table.
-struct Lookup {
-  const uint64_t* fences;  // LDS: Eytzinger keys (small tables) or fences (large tables)
-  const uint4* nodes;      // LDS (small tables): 2 x uint4 per node: (addr, end), (alloc, free)
-  const uint2* ninfo;      // LDS (small tables): (dense histogram base or ~0, entry id | older-entries << 31)
-  const uint8_t* shift;    // LDS (large tables): per-bucket directory shift
-};
-
-struct Match {
-  int64_t e;       // entry id, -1 = no match
-  uint64_t baddr;  // the entry's buffer_addr
-  uint64_t hist;   // dense histogram base cell, or kHistSparse
-};
-
-__device__ __forceinline__ void match_older(const Params& p, uint32_t first, uint32_t count, uint64_t addr,
-                                            uint64_t ts, Match& m) {
-  for (uint32_t e = first + 1; e < first + count; e++) {  // older entries of a reused address
-    const uint4* r = reinterpret_cast<const uint4*>(p.entries + e);
-    const uint4 ra = r[0], rb = r[1];
-    if (entry_match(ra, rb, addr, ts)) {
-      const uint4 rc = r[2];
-      m.e = e;
-      m.baddr = (uint64_t(ra.y) << 32) | ra.x;
-      m.hist = (uint64_t(rc.y) << 32) | rc.x;
-      return;
-    }
-  }
-}
-
-// __ma_find_mem_info_from_sample_generic (mem_analyzer.c:249-286): the
-// lower-bound node only (ht_lower_key, tools/hash.c:63-77), newest entry
-// first, inclusive timestamp window (is_sample_in_buffer, :141-155).
-__device__ __forceinline__ Match find_entry(const Params& p, const Lookup& L, uint64_t addr, uint64_t ts,
-                                            const SpecDir& sp) {
-  Match m;
-  m.e = -1;
-  m.baddr = 0;
-  m.hist = kHistSparse;
-  if (p.lds_nodes) {
-    // Eytzinger tree: node i has children 2i, 2i+1; a fixed number of levels,
-    // one LDS read each, branch-free.  The levels above the 7th fit in one
-    // 256 B bank row, so the search is conflict-free where every lane reads.
-    const uint32_t i = eytz_descend(L.fences, p.elevels, addr);
-    // largest key <= addr = the node of the last right turn (0: none)
-    const uint32_t idx = i >> (__builtin_ctz(i) + 1);
-    if (idx == 0) return m;
-    const uint4 a = L.nodes[2 * idx], b = L.nodes[2 * idx + 1];
-    const uint2 inf = L.ninfo[idx];
-    if (entry_match(a, b, addr, ts)) {
-      m.e = inf.y & 0x7fffffffu;
-      m.baddr = (uint64_t(a.y) << 32) | a.x;
-      m.hist = inf.x == kEmpty32 ? kHistSparse : (uint64_t)inf.x;
-    } else if (inf.y >> 31) {
-      match_older(p, inf.y & 0x7fffffffu, p.enodes[idx].count, addr, ts, m);
-    }
-    return m;
-  }
-  const uint32_t k = lower_key(p, L.fences, L.shift, addr, sp);
-  if (k >= p.nb_keys) return m;
-  const uint4* q = reinterpret_cast<const uint4*>(p.nodes + k);
-  const uint4 a = q[0], b = q[1], c = q[2];
-  if (entry_match(a, b, addr, ts)) {
-    m.e = c.w;
-    m.baddr = (uint64_t(a.y) << 32) | a.x;
-    m.hist = (uint64_t(c.y) << 32) | c.x;
-    return m;
-  }
-  const uint4 d = q[3];
-  if (d.x > 1) match_older(p, c.w, d.x, addr, ts, m);
-  return m;
-}
-
-// One long-tail contribution to this workgroup's sub-log of entry e; false
-// when the sub-log is full (the caller then issues the global atomics).
-__device__ __forceinline__ bool tlog_append(const Params& p, WgCounters& wc, uint32_t e, uint32_t a, uint32_t cnt,
-                                            uint64_t wt, uint64_t ord) {
-  const uint32_t part = e >> p.tlog_rshift;
-  const uint32_t k = atomicAdd(&wc.tcur[part], 1u);
-  if (k >= p.tlog_cap) return false;
-  unsigned long long* r = p.tlog + ((uint64_t(blockIdx.x) * p.tlog_parts + part) * p.tlog_cap + k) * 3;
-  r[0] = (unsigned long long)(e | (a << 31)) | ((unsigned long long)cnt << 32);
-  r[1] = wt;
-  r[2] = ord;
-  return true;
-}
-
-// Process one decoded record (`valid` = it is a SAMPLE).  Every lane of the
-// wave calls this together (wave-level reductions inside); vmask / fmask are
-// the wave's SAMPLE and matched lanes.
-template <int MODE>
-__device__ __forceinline__ void process_sample(Params& p, WgCounters& wc, LaneAcc& acc, const Lookup& L,
-                                               bool valid, uint64_t ts, uint64_t addr,
-                                               uint64_t w, uint64_t dsrc, uint32_t access,
-                                               uint32_t th, uint64_t seq, uint32_t off, uint64_t rbase,
-                                               uint64_t& vmask, uint64_t& fmask, const SpecDir& sp) {
-  const uint32_t lvl = uint32_t(dsrc >> 5) & 0x3fff;  // data_src.mem_lvl
-  // ---- global counters: update_counters(global_counters, ...) (mem_sampling.c:882)
-  vmask = __ballot(valid);
-  fmask = 0;
-  if (vmask == 0) return;
-  if (valid && !(p.flags & kDbgNoGlobal)) {
-    const uint32_t bm = bucket_mask(lvl);
-    if (w < kLaneMaxWeight) {  // register accumulation (no LDS traffic)
-      const uint32_t w32 = (uint32_t)w;
-      acc.tc += 1;
-      acc.tw += w32;
-      acc.na += lvl & LVL_NA;
-#pragma unroll
-      for (int k = 0; k < 5; k++) acc.cnt2[k] += ((bm >> (2 * k)) & 1) | ((k < 4 ? (bm >> (2 * k + 1)) & 1 : 0) << 16);
-#pragma unroll
-      for (int k = 0; k < 9; k++) acc.sum[k] += ((bm >> k) & 1) * w32;
-      for (uint32_t m = bm >> 9; m; m &= m - 1) {  // miss buckets
-        const uint32_t b = 9 + (uint32_t)__builtin_ctz(m);
-        atomicAdd(&wc.sums[3 + 2 * b], 1ull);
-        if (w) atomicAdd(&wc.sums[4 + 2 * b], (unsigned long long)w);
-      }
-    } else {  // weights >= 2^23 cycles: straight to the LDS counters
-      atomicAdd(&wc.sums[0], 1ull);
-      atomicAdd(&wc.sums[1], (unsigned long long)w);
-      if (lvl & LVL_NA) atomicAdd(&wc.sums[2], 1ull);
-      for (uint32_t m = bm; m; m &= m - 1) {
-        const uint32_t b = (uint32_t)__builtin_ctz(m);
-        atomicAdd(&wc.sums[3 + 2 * b], 1ull);
-        atomicAdd(&wc.sums[4 + 2 * b], (unsigned long long)w);
-      }
-    }
-    // min / max only move monotonically: read first, atomic only on improvement
-    if (bm) {
-      const uint32_t b = (uint32_t)__builtin_ctz(bm);
-      if (w < wc.mins[b]) atomicMin(&wc.mins[b], (unsigned long long)w);
-      if (w > wc.maxs[b]) atomicMax(&wc.maxs[b], (unsigned long long)w);
-      for (uint32_t m = bm & (bm - 1); m; m &= m - 1) {  // several level groups (rare)
-        const uint32_t b2 = (uint32_t)__builtin_ctz(m);
-        if (w < wc.mins[b2]) atomicMin(&wc.mins[b2], (unsigned long long)w);
-        if (w > wc.maxs[b2]) atomicMax(&wc.maxs[b2], (unsigned long long)w);
-      }
-    }
-  }
-  if (!(p.flags & NMG_F_MATCH_SAMPLES)) return;
-
-  // ---- __match_sample (mem_sampling.c:594-673)
-  Match m;
-  m.e = -1;
-  if (valid) m = find_entry(p, L, addr, ts, sp);
-  const int64_t e = m.e;
-  fmask = __ballot(e >= 0);
-  // dump modes: every SAMPLE record's match at its arena position (host
-  // formats the per-sample lines in analysis order)
-  if (p.smatch && valid) p.smatch[(rbase + off) >> 3] = e >= 0 ? (uint32_t)e + 1u : 0u;
-  if (e < 0 || (p.flags & kDbgNoTables)) return;
-  // per-object counters, aggregated per stream in LDS.  (Admitting an entry
-  // only on its second sample -- a doorkeeper bitset -- was measured slower at
-  // 1M intervals: the per-sample bit test costs more than the flushes it saves.)
-  // (with packing, a slot only sums packable weights: its flush is packed too)
-  const bool pk = !(MODE & kModeDenseObj) && p.pk64 && w < p.pk_wlim;
-  const int os = (MODE & kModeDenseObj) ? (int)e : ((p.pk64 && !pk) ? -1 : obj_slot(wc, (uint32_t)e));
-  const unsigned long long ord = (seq << 32) | off;  // first match in analysis order (quirk Q7)
-  if ((MODE & kModeDenseObj) && w < kLaneMaxWeight && kPackObj) {
-    // one packed add: count in bits 44..63, weight below (bounded by the
-    // kDensePageWindows flush cadence: < 2^16 samples of < 2^23 each)
-    atomicAdd(&wc.owt[os], (1ull << kPackShift) | w);
-    if (ord < wc.ofirst[os]) atomicMin(&wc.ofirst[os], ord);
-  } else if (os >= 0 && !((MODE & kModeDenseObj) && kPackObj)) {
-    atomicAdd(&wc.ocnt[os], 1u);
-    if (w) atomicAdd(&wc.owt[os], (unsigned long long)w);
-    if (ord < wc.ofirst[os]) atomicMin(&wc.ofirst[os], ord);
-  } else if (!(MODE & kModeDenseObj) && p.tlog && tlog_append(p, wc, (uint32_t)e, access, 1u, w, ord)) {
-    // table full: logged for tlog_reduce_kernel
-  } else if (pk) {  // table full: one packed global add
-    atomicAdd(p.pk64 + uint64_t(access) * p.nb_entries + e, (1ull << p.pk_shift) | w);
-    unsigned long long* fp = reinterpret_cast<unsigned long long*>(p.min64 + 36 + e);
-    atomicMin(fp, ord);
-  } else {  // table full (or a weight >= 2^23 in dense mode): straight to global
-    atomicAdd(reinterpret_cast<unsigned long long*>(p.sum64 + objcw_index(e, access, 0, p.nb_entries)), 1ull);
-    if (w)
-      atomicAdd(reinterpret_cast<unsigned long long*>(p.sum64 + objcw_index(e, access, 1, p.nb_entries)),
-                (unsigned long long)w);
-    unsigned long long* fp = reinterpret_cast<unsigned long long*>(p.min64 + 36 + e);
-    atomicMin(fp, ord);
-  }
-  if (p.flags & NMG_F_PAGE_HIST) {
-    // ma_get_block: page_no = (int)((addr - buffer_addr) / 4096) (mem_analyzer.c:530-531)
-    const uint32_t page = uint32_t(int(uint64_t(addr - m.baddr) / kPageSize));
-    if (m.hist != kHistSparse) {
-      const uint32_t cell = uint32_t(m.hist + page);
-      if (MODE & kModeDensePage) {
-        atomicAdd(&wc.pdense[cell >> 1], 1u << (16 * (cell & 1)));
-      } else {
-        const int ps = page_slot(wc, cell);
-        if (ps >= 0) atomicAdd(&wc.pcnt[ps], 1u);
-        else atomicAdd(p.hist + uint64_t(th) * p.hist_cells + cell, 1u);
-      }
-    } else {
-      const uint32_t sidx = p.entries[e].sidx;
-      if (sidx != ~0u)  // huge objects ([stack]): hashed cells in global memory
-        sparse_add(p, sparse_key(sidx, th, page), seq, off, 1u);
-    }
-  }
-  if (p.flags & NMG_F_OBJECT_LEVELS) {
-    unsigned long long* lv = reinterpret_cast<unsigned long long*>(
-        p.sum64 + 2 * kGlobalSums + uint64_t(p.nb_entries) * 4 + (uint64_t(e) * 2 + access) * kLevelWords);
-    if (lvl & LVL_NA) atomicAdd(lv, 1ull);
-    for (int g = 0; g < 9; g++) {
-      if (!(lvl & c_level_mask[g])) continue;
-      int bucket = (lvl & LVL_HIT) ? g : ((lvl & LVL_MISS) ? 9 + g : -1);
-      if (bucket < 0) continue;
-      atomicAdd(lv + 1 + 2 * bucket, 1ull);
-      if (w) atomicAdd(lv + 2 + 2 * bucket, (unsigned long long)w);
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------
-// per-workgroup aggregation state: flush to global memory and clear, slot by
-// slot (each thread owns the slots it flushes; callers fence with barriers)
-
-template <int MODE>
-__device__ __forceinline__ void flush_objects(Params& p, WgCounters& wc, int tid, uint32_t a) {
-  const bool write = !(p.flags & kDbgNoFlush);
-  const int n = (MODE & kModeDenseObj) ? (int)p.nb_entries : (int)kObjSlots;
-  for (int i = tid; i < n; i += kWG) {
-    const uint32_t e = (MODE & kModeDenseObj) ? (uint32_t)i : wc.okey[i];
-    constexpr bool packed = (MODE & kModeDenseObj) && kPackObj;
-    if ((MODE & kModeDenseObj) ? (packed ? wc.owt[i] == 0 : wc.ocnt[i] == 0) : e == kEmpty32) continue;
-    const uint64_t cnt = packed ? wc.owt[i] >> kPackShift : wc.ocnt[i];
-    const uint64_t wt = packed ? wc.owt[i] & ((1ull << kPackShift) - 1) : wc.owt[i];
-    if (write && !(MODE & kModeDenseObj) && p.tlog && tlog_append(p, wc, e, a, (uint32_t)cnt, wt, wc.ofirst[i])) {
-      // logged
-    } else if (write && !(MODE & kModeDenseObj) && p.pk64) {
-      atomicAdd(p.pk64 + uint64_t(a) * p.nb_entries + e, (cnt << p.pk_shift) | wt);
-      atomicMin(reinterpret_cast<unsigned long long*>(p.min64 + 36 + e), wc.ofirst[i]);
-    } else if (write) {
-      atomicAdd(reinterpret_cast<unsigned long long*>(p.sum64 + objcw_index(e, a, 0, p.nb_entries)),
-                (unsigned long long)cnt);
-      if (wt)
-        atomicAdd(reinterpret_cast<unsigned long long*>(p.sum64 + objcw_index(e, a, 1, p.nb_entries)),
-                  (unsigned long long)wt);
-      unsigned long long* fp = reinterpret_cast<unsigned long long*>(p.min64 + 36 + e);
-      atomicMin(fp, wc.ofirst[i]);  // no read first: a returning load would stall the flush
-    }
-    wc.okey[i] = kEmpty32;
-    wc.ocnt[i] = 0;
-    wc.ofirst[i] = kEmpty64;
-    wc.owt[i] = 0;
-  }
-}
-
-template <int MODE>
-__device__ __forceinline__ void flush_pages(Params& p, WgCounters& wc, int tid, uint32_t th) {
-  const bool write = !(p.flags & kDbgNoFlush);
-  unsigned int* hrow = p.hist + uint64_t(th) * p.hist_cells;
-  if (MODE & kModeDensePage) {  // cells in order: consecutive lanes add to consecutive words
-    const uint32_t nw = (uint32_t)(p.hist_cells + 1) / 2;
-    for (uint32_t i = tid; i < nw; i += kWG) {
-      const uint32_t v = wc.pdense[i];
-      if (!v) continue;
-      if (write) {
-        if (v & 0xffffu) atomicAdd(hrow + 2 * i, v & 0xffffu);
-        if (v >> 16) atomicAdd(hrow + 2 * i + 1, v >> 16);
-      }
-      wc.pdense[i] = 0;
-    }
-    return;
-  }
-  unsigned int* pkey = reinterpret_cast<unsigned int*>(wc.pkey4);
-  for (int i = tid; i < (int)kPageSlots; i += kWG) {
-    const uint32_t cell = pkey[i];
-    if (cell == kEmpty32) continue;
-    if (write) atomicAdd(hrow + cell, wc.pcnt[i]);
-    pkey[i] = kEmpty32;
-    wc.pcnt[i] = 0;
-  }
-}
-
-// global mem_counters[a] of the stream (after the lanes were drained)
-__device__ __forceinline__ void flush_sums(Params& p, WgCounters& wc, int tid, uint32_t a) {
-  const bool write = !(p.flags & kDbgNoFlush);
-  if (tid < (int)kGlobalSums) {
-    if (write && wc.sums[tid])
-      atomicAdd(reinterpret_cast<unsigned long long*>(p.sum64 + gsum_index(a, tid)), wc.sums[tid]);
-  }
-  if (tid < 18) {
-    if (write && wc.sums[3 + 2 * tid]) {
-      atomicMin(reinterpret_cast<unsigned long long*>(p.min64 + a * 18 + tid), wc.mins[tid]);
-      atomicMax(reinterpret_cast<unsigned long long*>(p.max64 + a * 18 + tid), wc.maxs[tid]);
-    }
-  }
-  // (cleared after a barrier: sums[3 + 2 * tid] is read by other threads above)
-}
-
-__device__ __forceinline__ void clear_sums(WgCounters& wc, int tid) {
-  if (tid < (int)kGlobalSums) wc.sums[tid] = 0;
-  if (tid < 18) {
-    wc.mins[tid] = ~0ull;  // INIT_COUNTER: min = UINT64_MAX (mem_analyzer.c:415-420)
-    wc.maxs[tid] = 0;
-  }
-}
-
-template <int MODE>
-__device__ __forceinline__ void clear_state(WgCounters& wc, int tid) {
-  clear_sums(wc, tid);
-  for (int i = tid; i < (int)kObjSlots; i += kWG) {
-    wc.okey[i] = kEmpty32;
-    wc.ocnt[i] = 0;
-    wc.ofirst[i] = kEmpty64;
-    wc.owt[i] = 0;
-  }
-  if (MODE & kModeDensePage) {
-    for (int i = tid; i < (int)(kDensePageCells / 2); i += kWG) wc.pdense[i] = 0;
-  } else {
-    for (int i = tid; i < (int)kPageSlots; i += kWG) {
-      reinterpret_cast<unsigned int*>(wc.pkey4)[i] = kEmpty32;
-      wc.pcnt[i] = 0;
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------
-// record loads straight into registers
-
-// One 40 B stride slot: 16 B + 16 B + 8 B loads whose offsets depend on the
-// slot's 16 B parity (records are 8-aligned in a 16-aligned buffer), so every
-// lane issues the same three instructions.  Decoded only when consumed, so a
-// prefetched window stays in flight while the current one is processed.
-struct RawRec {
-  uint4 x, y;
-  uint2 z;
-};
-
-__device__ __forceinline__ void load_rec(const uint8_t* base, uint64_t pos, uint64_t len, RawRec& r) {
-  if (pos + kRecBytes <= len) {
-    const uint32_t odd = uint32_t(pos >> 3) & 1;
-    const uint8_t* q = base + pos;
-#ifdef NMG_NT_LOADS
-    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-    typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-    const u32x4 a = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(q + (odd ? 8 : 0)));
-    const u32x4 b = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(q + (odd ? 24 : 16)));
-    const u32x2 c = __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(q + (odd ? 0 : 32)));
-    r.x = make_uint4(a.x, a.y, a.z, a.w);
-    r.y = make_uint4(b.x, b.y, b.z, b.w);
-    r.z = make_uint2(c.x, c.y);
-#else
-    r.x = *reinterpret_cast<const uint4*>(q + (odd ? 8 : 0));
-    r.y = *reinterpret_cast<const uint4*>(q + (odd ? 24 : 16));
-    r.z = *reinterpret_cast<const uint2*>(q + (odd ? 0 : 32));
-#endif
-  } else {
-    r.x = make_uint4(0, 0, 0, 0);
-    r.y = make_uint4(0, 0, 0, 0);
-    r.z = make_uint2(0, 0);
-  }
-}
-
-struct Rec {
-  uint64_t hdr, ts, addr, w, dsrc;
-};
-
-__device__ __forceinline__ uint64_t u64of(uint32_t lo, uint32_t hi) { return (uint64_t(hi) << 32) | lo; }
-
-__device__ __forceinline__ Rec decode_rec(const RawRec& r, uint64_t pos) {
-  Rec d;
-  if ((pos >> 3) & 1) {  // hdr | ts addr | w dsrc
-    d.hdr = u64of(r.z.x, r.z.y);
-    d.ts = u64of(r.x.x, r.x.y);
-    d.addr = u64of(r.x.z, r.x.w);
-    d.w = u64of(r.y.x, r.y.y);
-    d.dsrc = u64of(r.y.z, r.y.w);
-  } else {  // hdr ts | addr w | dsrc
-    d.hdr = u64of(r.x.x, r.x.y);
-    d.ts = u64of(r.x.z, r.x.w);
-    d.addr = u64of(r.y.x, r.y.y);
-    d.w = u64of(r.y.z, r.y.w);
-    d.dsrc = u64of(r.z.x, r.z.y);
-  }
-  return d;
-}
-
-// ---------------------------------------------------------------------------
-// the attribution kernel
-//
-// One 1024-thread workgroup per CU (LDS: fences 8 KiB, node records 40 KiB,
-// object table 48 KiB, page table 56 KiB, slow-path list 4 KiB), persistent
-// over a byte-balanced range of the stream-sorted buffer list.  A window is
-// 1024 stride slots of 40 B, one per lane, loaded straight into registers;
-// the next window (of this buffer or the next one) is issued before the
-// current one is processed.  One barrier per window: it publishes the window's
-// "irregular" bit through rotating flag words.
-// One lane's stride slot in window (cur of d0) [+ head of d1 when d1 is the
-// next buffer of the same stream].
-struct WinLane {
-  uint32_t pos;     // slot offset within its buffer (buffers are < 4 GiB)
-  uint32_t n0, n1;  // slots in d0 / in d1 (uniform)
-  bool in1;         // the slot is in d1
-  bool cand;        // this lane has a slot
-};
-
-__device__ __forceinline__ WinLane win_lane(int tid, uint32_t cur, const BufDesc& d0, const BufDesc& d1, bool has1) {
-  WinLane w;
-  const uint32_t left = d0.len - cur;
-  w.n0 = min(left / kRecBytes + (left % kRecBytes != 0), (uint32_t)kWG);
-  w.n1 = 0;
-  if (has1 && w.n0 < (uint32_t)kWG && d1.access == d0.access && d1.thread_rank == d0.thread_rank)
-    w.n1 = min(d1.len / kRecBytes + (d1.len % kRecBytes != 0), (uint32_t)kWG - w.n0);
-  w.in1 = (uint32_t)tid >= w.n0;
-  w.cand = (uint32_t)tid < w.n0 + w.n1;
-  w.pos = w.in1 ? (uint32_t(tid) - w.n0) * kRecBytes : cur + uint32_t(tid) * kRecBytes;
-  return w;
-}
-
-__device__ __forceinline__ void load_slot(const Params& p, const WinLane& w, const BufDesc& d0, const BufDesc& d1,
-                                          RawRec& r) {
-  const uint64_t off = w.in1 ? d1.offset : d0.offset;
-  const uint32_t len = w.cand ? (w.in1 ? d1.len : d0.len) : 0;
-  load_rec(p.data + off, w.pos, len, r);
-}
-
-// shader-clock stamp that the scheduler does not move work across
-__device__ __forceinline__ uint64_t stamp() {
-  __builtin_amdgcn_sched_barrier(0);
-  const uint64_t t = __builtin_amdgcn_s_memtime();
-  __builtin_amdgcn_sched_barrier(0);
-  return t;
-}
-
-template <bool TIMING, int MODE>
-__global__ __launch_bounds__(kWG, 1) void attribute_kernel(Params p) {
-  __shared__ uint4 s_tab[kTabBytes / 16];  // lookup structure (layouts at kTabBytes)
-  __shared__ uint32_t s_list[kMaxList];
-  __shared__ WgCounters wc;
-  __shared__ uint32_t s_flags[3], s_nlist, s_next, s_err;
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  uint64_t* const s_fences = reinterpret_cast<uint64_t*>(s_tab);
-  uint4* const s_nodes = s_tab + (kLdsNodes + 1) / 2;                    // after 8 KiB of keys
-  uint2* const s_ninfo = reinterpret_cast<uint2*>(s_tab + (kLdsNodes + 1) * 5 / 2);  // after 40 KiB
-  uint8_t* const s_shift = reinterpret_cast<uint8_t*>(s_tab + (kMaxFences + 1) / 2);  // after 32 KiB
-  if (p.lds_nodes) {
-    const uint32_t n = 1u << p.elevels;
-    for (uint32_t i = tid; i < n; i += kWG) s_fences[i] = p.efences[i];
-    for (uint32_t i = 1 + tid; i < n; i += kWG) {
-      const uint4* q = reinterpret_cast<const uint4*>(p.enodes + i);
-      const uint4 a = q[0], b = q[1], c = q[2], d = q[3];
-      s_nodes[2 * i] = a;
-      s_nodes[2 * i + 1] = b;
-      s_ninfo[i] = make_uint2(c.y == 0 ? c.x : kEmpty32, c.w | (d.x > 1 ? 0x80000000u : 0u));
-    }
-  } else if (p.nb_keys) {
-    for (uint32_t i = tid; i <= kMaxFences; i += kWG) s_fences[i] = p.ffences[i];
-    for (uint32_t i = tid; i < p.nb_fences; i += kWG) s_shift[i] = p.fshift[i];
-  }
-  clear_state<MODE>(wc, tid);
-  constexpr bool kLog = !(MODE & kModeDenseObj);  // the long-tail log serves the hashed object mode
-  if (kLog && p.tlog)
-    for (uint32_t i = tid; i < kLogParts; i += kWG) wc.tcur[i] = 0;
-  if (tid < 3) s_flags[tid] = 0;
-  __syncthreads();
-  const Lookup L{s_fences, s_nodes, s_ninfo, s_shift};
-
-  // A window is (idx, cur): up to kWG stride slots from byte `cur` of buffer
-  // idx; when that buffer ends inside the window and the next buffer belongs
-  // to the same stream, the remaining lanes take the head of the next buffer
-  // (no partly idle window at every buffer end).
-  const uint32_t r0 = p.ranges[blockIdx.x], r1 = p.ranges[blockIdx.x + 1];
-  if (r0 >= r1) {
-    if (kLog && p.tlog)
-      for (uint32_t i = tid; i < p.tlog_parts; i += kWG) p.tlog_cnt[uint64_t(blockIdx.x) * p.tlog_parts + i] = 0;
-    return;
-  }
-  uint32_t idx = r0;
-  uint32_t cur = 0;  // byte cursor, as `cur_cpt` in __analyze_buffer (mem_sampling.c:836)
-  BufDesc d0 = p.sbufs[idx];
-  BufDesc d1 = idx + 1 < r1 ? p.sbufs[idx + 1] : d0;
-  bool has1 = idx + 1 < r1;
-  uint32_t cur_access = d0.access, cur_thread = d0.thread_rank;
-  RawRec nx;
-  {
-    const WinLane wl = win_lane(tid, 0, d0, d1, has1);
-    load_slot(p, wl, d0, d1, nx);
-  }
-  LaneAcc acc;
-  lane_acc_clear(acc);
-  uint32_t win = 0, acc_windows = 0, last_flush = 0;
-  uint32_t ns0 = 0, nf0 = 0, ns1 = 0, nf1 = 0;  // per-buffer tallies: buffer idx, idx + 1
-  uint64_t tacc[4] = {0, 0, 0, 0}, t_start = 0, t0 = 0, t1 = 0;
-  if (TIMING) t_start = t0 = stamp();
-#ifndef NMG_NO_SPEC_DIR
-  constexpr bool kSpec = !(MODE & kModeDenseObj);  // large tables come with the hashed object mode
-#else
-  constexpr bool kSpec = false;
-#endif
-  SpecDir sp;
-  sp.addr = 0;
-  sp.idx = 0;
-  sp.de = make_uint2(0, 0);
-
-  while (true) {
-    const WinLane wl = win_lane(tid, cur, d0, d1, has1);
-    const Rec r = decode_rec(nx, wl.pos);
-    // ---- fast-path check: every 40 B stride slot holds a whole 40 B record
-    const uint32_t wlen = wl.in1 ? d1.len : d0.len;
-    const bool bad = (cur & 7) != 0 || (wl.cand && (uint64_t(wl.pos) + kRecBytes > wlen || (r.hdr >> 48) != kRecBytes));
-    const uint64_t badm = __ballot(bad);
-    if (TIMING) {
-      t1 = stamp();
-      tacc[0] += t1 - t0;
-      t0 = t1;
-    }
-    // (Dropping this barrier -- each wave deciding from its own slots, exact
-    // only on pure 40 B SAMPLE streams -- was timed as an upper bound for a
-    // barrier-free protocol: c2 -7.6 %, 1M intervals +6 %: not worth one.)
-    if (badm && lane == 0) atomicOr(&s_flags[win % 3], 1u);
-    __syncthreads();
-    // (LDS broadcasts are made wave-uniform explicitly: the branches below
-    // hold barriers and steer the scalar loop state)
-    const uint32_t f = __builtin_amdgcn_readfirstlane(s_flags[win % 3]);
-    if (tid == 0) s_flags[(win + 2) % 3] = 0;  // last read before the previous barrier
-    win++;
-    if (TIMING) {
-      t1 = stamp();
-      tacc[1] += t1 - t0;
-      t0 = t1;
-    }
-    uint32_t nidx = idx;
-    uint64_t ncur;
-    // the record this lane processes in this window
-    Rec rec = r;
-    bool valid;
-    uint64_t rseq, rbase;
-    uint32_t roff;
-    if (!(f & 1)) {
-      valid = wl.cand && uint32_t(r.hdr) == kSampleType;
-      rseq = wl.in1 ? d1.seq : d0.seq;
-      rbase = wl.in1 ? d1.offset : d0.offset;
-      roff = wl.pos;
-      // ---- fast path: one record per lane
-      if (wl.n1) {
-        nidx = idx + 1;
-        ncur = uint64_t(wl.n1) * kRecBytes;
-        if (ncur >= d1.len) {
-          nidx = idx + 2;
-          ncur = 0;
-        }
-      } else {
-        ncur = cur + uint64_t(wl.n0) * kRecBytes;
-        if (ncur >= d0.len) {
-          nidx = idx + 1;
-          ncur = 0;
-        }
-      }
-    } else {
-      // ---- slow path (buffer idx only): wave 0 follows the header chain from
-      // global memory, 64 stride slots per step (a run of regular 40 B records
-      // is taken in one step, an irregular record is handled alone), listing
-      // SAMPLE offsets; then every lane processes one listed record
-      const uint8_t* base = p.data + d0.offset;
-      const uint64_t len = d0.len;
-      if (tid < 64) {
-        uint64_t q0 = cur;
-        uint32_t n = 0, err = 0;
-        const uint64_t lim = min(uint64_t(cur) + kWinBytes, len);
-        while (q0 < lim && n + 65 <= kMaxList) {
-          const uint64_t q = q0 + uint64_t(lane) * kRecBytes;
-          const uint64_t hdr = (q + 8 <= len) ? *reinterpret_cast<const uint64_t*>(base + q) : 0;
-          const bool reg = q < lim && q + kRecBytes <= len && (hdr >> 48) == kRecBytes;
-          const uint64_t rm = __ballot(reg);
-          const uint32_t run = ~rm ? (uint32_t)__builtin_ctzll(~rm) : 64u;
-          const bool smp = (uint32_t)lane < run && uint32_t(hdr) == kSampleType;
-          const uint64_t sm = __ballot(smp);
-          if (smp) s_list[n + (uint32_t)__popcll(sm & ((1ull << lane) - 1))] = (uint32_t)q;
-          n += (uint32_t)__popcll(sm);
-          q0 += uint64_t(run) * kRecBytes;
-          if (run == 64 || q0 >= lim) continue;
-          // record at q0 (lane `run`'s slot) is not a whole 40 B record
-          if (q0 + 8 > len) { err = kErrTruncated; break; }
-          const uint64_t h = (uint64_t)__shfl(hdr, (int)run, 64);
-          const uint32_t size = uint32_t(h >> 48);
-          if (size == 0) { err = kErrZeroSize; break; }  // mem_sampling.c:857-860
-          if (size & 7) { err = kErrUnaligned; break; }  // perf records are 8-byte multiples
-          if (uint32_t(h) == kSampleType) {
-            if (q0 + kRecBytes > len || q0 + size > len) { err = kErrTruncated; break; }
-            if (lane == 0) s_list[n] = (uint32_t)q0;
-            n++;
-          }
-          q0 += size;  // non-SAMPLE records are skipped by their size (:918)
-        }
-        if (lane == 0) {
-          if (err) set_error(p, d0.seq, (uint32_t)q0, err);
-          s_err = err;
-          s_nlist = n;
-          s_next = (uint32_t)min(q0, len);
-        }
-      }
-      __syncthreads();
-      const uint32_t n = __builtin_amdgcn_readfirstlane(s_nlist);
-      const uint32_t serr = __builtin_amdgcn_readfirstlane(s_err);
-      ncur = serr ? len : __builtin_amdgcn_readfirstlane(s_next);  // the reference aborts on an error: stop this buffer
-      if (ncur >= len) {
-        nidx = idx + 1;
-        ncur = 0;
-      }
-      valid = (uint32_t)tid < n;
-      roff = valid ? s_list[tid] : 0;
-      rseq = d0.seq;
-      rbase = d0.offset;
-      RawRec rr;
-      load_rec(base, roff, valid ? len : 0, rr);
-      rec = decode_rec(rr, roff);
-    }
-
-    // ---- descriptors of the next window, and its loads (issued before this
-    // window's records are processed)
-    BufDesc nd0 = d0, nd1 = d1;
-    if (nidx == idx + 1) {
-      nd0 = d1;
-      if (nidx + 1 < r1) nd1 = p.sbufs[nidx + 1];
-    } else if (nidx == idx + 2) {
-      if (nidx < r1) nd0 = p.sbufs[nidx];
-      if (nidx + 1 < r1) nd1 = p.sbufs[nidx + 1];
-    }
-    const bool nhas1 = nidx + 1 < r1;
-    uint32_t npos = 0;
-    bool ncand = false;
-    if (nidx < r1) {
-      const WinLane nl = win_lane(tid, (uint32_t)ncur, nd0, nd1, nhas1);
-      load_slot(p, nl, nd0, nd1, nx);
-      npos = nl.pos;
-      ncand = nl.cand;
-    }
-
-    if (TIMING && tid == 0 && win <= 8) {
-      unsigned long long* o = p.dbg + uint64_t(blockIdx.x) * (kWG / 64) * kTimingWords + 8 + 2 * (win - 1);
-      o[0] = (uint64_t(idx) << 40) | cur;
-      o[1] = uint64_t(wl.n0) | (uint64_t(wl.n1) << 11) | (uint64_t(f) << 22) | (uint64_t(nidx) << 24) |
-             (uint64_t((uint32_t)ncur) << 32);
-    }
-    uint64_t vm = 0, fm = 0;
-    if (!(p.flags & kDbgLoadOnly))
-      process_sample<MODE>(p, wc, acc, L, valid, rec.ts, rec.addr, rec.w, rec.dsrc, d0.access, d0.thread_rank, rseq, roff,
-                           rbase, vm, fm, sp);
-    if (kSpec && !p.lds_nodes && (p.flags & NMG_F_MATCH_SAMPLES)) {
-      // start the next window's lookup: its record (loaded above, arrived
-      // during this window's lookups) -> fence node -> directory slot load,
-      // in flight across the flush and the barrier.  Used when the record
-      // this lane processes next has the same address (fast-path windows).
-      sp.idx = 0;
-      if (nidx < r1 && ncand) {
-        sp.addr = decode_rec(nx, npos).addr;
-        sp.idx = fence_node(L.fences, sp.addr);
-        const uint2* ds = dir_slot(p, L.fences, L.shift, sp.addr, sp.idx);
-        if (ds) sp.de = *ds;
-      }
-    }
-    {
-      // lanes of this wave in buffer idx + 1 (tid >= n0)
-      const uint32_t w0 = uint32_t(tid) & ~63u;
-      const uint64_t m1 = ((f & 1) || wl.n0 >= w0 + 64) ? 0ull : (wl.n0 <= w0 ? ~0ull : (~0ull << (wl.n0 - w0)));
-      ns0 += (uint32_t)__popcll(vm & ~m1);
-      nf0 += (uint32_t)__popcll(fm & ~m1);
-      ns1 += (uint32_t)__popcll(vm & m1);
-      nf1 += (uint32_t)__popcll(fm & m1);
-    }
-    if (TIMING) {
-      t1 = stamp();
-      tacc[2] += t1 - t0;
-      t0 = t1;
-    }
-    // end of the stream run (or of this workgroup's range): publish the
-    // stream's counters; tables over their fill threshold (as of this
-    // window's barrier) are flushed here too -- the single flush site
-    const bool stream_end = nidx != idx && (nidx >= r1 || nd0.access != cur_access || nd0.thread_rank != cur_thread);
-    if (++acc_windows == kDrainWindows || stream_end) {  // keep the per-lane u32 sums bounded
-      lane_acc_drain(acc, wc, lane);
-      acc_windows = 0;
-    }
-    if (nidx != idx) {
-      // buffer idx (and idx + 1 when skipped over) done: sample / match
-      // tallies (mem_sampling.c:921-926)
-      if (lane == 0) {
-        if (ns0) atomicAdd(p.bufcnt + d0.pad, ns0);
-        if (nf0) atomicAdd(p.bufcnt + p.nb_bufs + d0.pad, nf0);
-        if (nidx == idx + 2) {
-          if (ns1) atomicAdd(p.bufcnt + d1.pad, ns1);
-          if (nf1) atomicAdd(p.bufcnt + p.nb_bufs + d1.pad, nf1);
-        }
-      }
-      if (nidx == idx + 1) {
-        ns0 = ns1;
-        nf0 = nf1;
-      } else {
-        ns0 = nf0 = 0;
-      }
-      ns1 = nf1 = 0;
-    }
-    const uint32_t cadence = (MODE & (kModeDensePage | kModeDenseObj)) ? kDensePageWindows : kTableWindows;
-    if (stream_end || win - last_flush >= cadence) {
-      __syncthreads();  // every insert and drain of this window is done
-      if (stream_end) flush_sums(p, wc, tid, cur_access);
-      flush_objects<MODE>(p, wc, tid, cur_access);
-      flush_pages<MODE>(p, wc, tid, cur_thread);
-      last_flush = win;
-      __syncthreads();
-      if (stream_end) {
-        clear_sums(wc, tid);  // (sums are next written after the next window's barrier)
-        cur_access = nd0.access;
-        cur_thread = nd0.thread_rank;
-      }
-    }
-    idx = nidx;
-    cur = (uint32_t)ncur;
-    d0 = nd0;
-    d1 = nd1;
-    has1 = nhas1;
-    if (TIMING) {
-      t1 = stamp();
-      tacc[3] += t1 - t0;
-      t0 = t1;
-    }
-    if (idx >= r1) break;  // the loop's only exit, after the state update
-  }
-  if (kLog && p.tlog) {  // the sub-logs' fill (every append of this workgroup is done)
-    __syncthreads();
-    for (uint32_t i = tid; i < p.tlog_parts; i += kWG)
-      p.tlog_cnt[uint64_t(blockIdx.x) * p.tlog_parts + i] = min(wc.tcur[i], p.tlog_cap);
-  }
-  if (TIMING && lane == 0) {
-    unsigned long long* o = p.dbg + (uint64_t(blockIdx.x) * (kWG / 64) + tid / 64) * kTimingWords;
-    for (int k = 0; k < 4; k++) o[k] = tacc[k];
-    o[4] = stamp() - t_start;
-    o[5] = win;
-  }
-}
-
-// Sums the long-tail log of one attribution launch: workgroup `part` owns the
-// entries [part << rshift, (part + 1) << rshift), reads that range's sub-log
-// of every attribution workgroup, adds counts / weights and takes the first
-// ordinal in LDS, then updates sum64 / min64 with plain read-modify-writes
-// (no other writer of those words is running).  Folds the packed counters of
-// the range too.
-struct TlogParams {
-  const unsigned long long* tlog;
-  const uint32_t* tlog_cnt;
-  uint64_t* sum64;
-  uint64_t* min64;
-  unsigned long long* pk64;  // may be null
-  uint32_t grid, parts, cap, rshift, nb_entries, pk_shift;
-};
-
-__global__ __launch_bounds__(1024, 1) void tlog_reduce_kernel(TlogParams r) {
-  __shared__ uint32_t s_cnt[2][kLogChunk];
-  __shared__ unsigned long long s_wt[2][kLogChunk];
-  __shared__ unsigned long long s_ord[kLogChunk];
-  __shared__ uint32_t s_pre[kLogMaxGrid + 1];
-  const uint32_t part = blockIdx.x, tid = threadIdx.x;
-  for (uint32_t w = tid; w < r.grid; w += 1024) s_pre[w + 1] = r.tlog_cnt[uint64_t(w) * r.parts + part];
-  __syncthreads();
-  if (tid < 64) {  // prefix over the source workgroups: a chunk per lane, then a wave scan
-    const uint32_t per = (r.grid + 63) / 64, b = min(tid * per, r.grid), e = min(b + per, r.grid);
-    uint32_t sum = 0;
-    for (uint32_t w = b; w < e; w++) sum += s_pre[w + 1];
-    uint32_t incl = sum;
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t t = __shfl_up(incl, o, 64);
-      if ((int)tid >= o) incl += t;
-    }
-    uint32_t run = incl - sum;
-    for (uint32_t w = b; w < e; w++) {
-      run += s_pre[w + 1];
-      s_pre[w + 1] = run;
-    }
-    if (tid == 0) s_pre[0] = 0;
-  }
-  __syncthreads();
-  const uint32_t total = s_pre[r.grid];
-  const uint64_t e0 = uint64_t(part) << r.rshift;
-  const uint64_t e1 = min(e0 + (1ull << r.rshift), (uint64_t)r.nb_entries);
-  for (uint64_t base = e0; base < e1; base += kLogChunk) {
-    const uint32_t n = (uint32_t)min((uint64_t)kLogChunk, e1 - base);
-    for (uint32_t j = tid; j < n; j += 1024) {
-      s_cnt[0][j] = s_cnt[1][j] = 0;
-      s_wt[0][j] = s_wt[1][j] = 0;
-      s_ord[j] = ~0ull;
-    }
-    __syncthreads();
-    constexpr int kU = 4;  // records per thread in flight
-    for (uint32_t i0 = tid; i0 < total; i0 += kU * 1024) {
-      unsigned long long kv[kU], wv[kU], ov[kU];
-#pragma unroll
-      for (int u = 0; u < kU; u++) {
-        const uint32_t i = i0 + u * 1024;
-        kv[u] = ~0ull;  // (no record: entry ids are < 2^31)
-        if (i >= total) continue;
-        uint32_t lo = 0, hi = r.grid;  // source workgroup: s_pre[lo] <= i < s_pre[lo + 1]
-        while (hi - lo > 1) {
-          const uint32_t mid = (lo + hi) >> 1;
-          if (s_pre[mid] <= i) lo = mid;
-          else hi = mid;
-        }
-        const unsigned long long* q = r.tlog + ((uint64_t(lo) * r.parts + part) * r.cap + (i - s_pre[lo])) * 3;
-        kv[u] = q[0];
-        wv[u] = q[1];
-        ov[u] = q[2];
-      }
-#pragma unroll
-      for (int u = 0; u < kU; u++) {
-        if (kv[u] == ~0ull) continue;
-        const uint32_t e = uint32_t(kv[u]) & 0x7fffffffu, a = uint32_t(kv[u]) >> 31;
-        const uint64_t j = e - base;
-        if (e < base || j >= n) continue;
-        atomicAdd(&s_cnt[a][j], uint32_t(kv[u] >> 32));
-        if (wv[u]) atomicAdd(&s_wt[a][j], wv[u]);
-        atomicMin(&s_ord[j], ov[u]);
-      }
-    }
-    __syncthreads();
-    // every global word of kU entries loaded before any is updated (the
-    // read-modify-writes would otherwise wait on one load at a time)
-    for (uint32_t j0 = tid; j0 < n; j0 += kU * 1024) {
-      uint64_t gc[kU][2], gw[kU][2], pv[kU][2], gm[kU];
-#pragma unroll
-      for (int u = 0; u < kU; u++) {
-        const uint32_t j = j0 + u * 1024;
-        if (j >= n) continue;
-        const uint64_t e = base + j;
-#pragma unroll
-        for (uint32_t a = 0; a < 2; a++) {
-          gc[u][a] = r.sum64[objcw_index(e, a, 0, r.nb_entries)];
-          gw[u][a] = r.sum64[objcw_index(e, a, 1, r.nb_entries)];
-          pv[u][a] = r.pk64 ? r.pk64[uint64_t(a) * r.nb_entries + e] : 0;
-        }
-        gm[u] = r.min64[36 + e];
-      }
-#pragma unroll
-      for (int u = 0; u < kU; u++) {
-        const uint32_t j = j0 + u * 1024;
-        if (j >= n) continue;
-        const uint64_t e = base + j;
-#pragma unroll
-        for (uint32_t a = 0; a < 2; a++) {
-          uint64_t c = s_cnt[a][j], w = s_wt[a][j];
-          const uint64_t v = pv[u][a];
-          if (v) {
-            c += v >> r.pk_shift;
-            w += v & ((1ull << r.pk_shift) - 1);
-            r.pk64[uint64_t(a) * r.nb_entries + e] = 0;
-          }
-          if (c) r.sum64[objcw_index(e, a, 0, r.nb_entries)] = gc[u][a] + c;
-          if (w) r.sum64[objcw_index(e, a, 1, r.nb_entries)] = gw[u][a] + w;
-        }
-        if (s_ord[j] < gm[u]) r.min64[36 + e] = s_ord[j];
-      }
-    }
-    __syncthreads();
-  }
-}
-
-// Adds the launch's packed long-tail object counters into sum64 and clears
-// them (same stream, after attribute_kernel).
-__global__ __launch_bounds__(256) void unpack_kernel(uint64_t* sum64, unsigned long long* pk64, uint32_t nb_entries,
-                                                     uint32_t shift) {
-  const uint64_t n = 2ull * nb_entries;
-  for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += gridDim.x * 256ull) {
-    const uint64_t v = pk64[i];
-    if (!v) continue;
-    const uint32_t a = i >= nb_entries;
-    const uint64_t e = i - uint64_t(a) * nb_entries;
-    sum64[objcw_index(e, a, 0, nb_entries)] += v >> shift;
-    sum64[objcw_index(e, a, 1, nb_entries)] += v & ((1ull << shift) - 1);
-    pk64[i] = 0;
-  }
-}
-
-// One launch re-initialises every counter array (INIT_COUNTER semantics:
-// sums and maxes 0, mins and first-match ordinals UINT64_MAX; sparse keys empty).
-struct ResetParams {
-  uint64_t* sum64;
-  uint64_t n_sum64;
-  uint64_t* min64;
-  uint64_t n_min64;
-  uint64_t* max64;
-  uint64_t n_max64;
-  uint4* hist;  // zeroed in 16 B units
-  uint64_t n_hist16;
-  uint64_t* sparse_keys;
-  uint32_t* sparse_vals;
-  uint64_t sparse_cap;
-  const uint32_t* sparse_read;  // dirty flag of the analyses since the previous reset
-  uint32_t* sparse_clear;       // the flag the analyses after this reset will set
-  uint32_t* bufcnt;
-  uint64_t n_bufcnt;
-};
-
-__global__ __launch_bounds__(256) void reset_kernel(ResetParams r) {
-  const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
-  const uint64_t i0 = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-  for (uint64_t i = i0; i < r.n_hist16; i += stride) r.hist[i] = make_uint4(0, 0, 0, 0);
-  for (uint64_t i = i0; i < r.n_sum64; i += stride) r.sum64[i] = 0;
-  for (uint64_t i = i0; i < r.n_min64; i += stride) r.min64[i] = ~0ull;
-  for (uint64_t i = i0; i < r.n_max64; i += stride) r.max64[i] = 0;
-  // the sparse table is cleared only when something was inserted since the
-  // last reset (it is large, and the [stack] range it serves never matches, Q4)
-  if (i0 == 0 && r.sparse_clear) *r.sparse_clear = 0u;
-  const uint64_t scap = (r.sparse_read && *r.sparse_read) ? r.sparse_cap : 0;
-  for (uint64_t i = i0; i < scap; i += stride) {
-    r.sparse_keys[i] = ~0ull;
-    r.sparse_vals[i] = 0;
-  }
-  for (uint64_t i = i0; i < r.n_bufcnt; i += stride) r.bufcnt[i] = 0;
-}
-
-}  // namespace nmg
+#include "nmg_kernels.h"
 
 // ===========================================================================
 // host side
@@ -1774,9 +377,8 @@ extern "C" int nmg_reset_counters(nmg_engine* h) {
   // most 4 workgroups per CU: small tables reset in one short launch
   const uint64_t longest = std::max<uint64_t>({r.n_hist16, r.n_sum64, r.n_min64, r.sparse_cap, r.n_bufcnt, 1});
   const uint32_t rgrid = (uint32_t)std::min<uint64_t>((longest + 256 * 16 - 1) / (256 * 16), (uint64_t)h->num_cus * 4);
-  hipLaunchKernelGGL(reset_kernel, dim3(rgrid), dim3(256), 0, h->stream, r);
+  HIP_TRY(h, launch_reset(rgrid, h->stream, r));
   h->nreset++;
-  HIP_TRY(h, hipGetLastError());
   return NMG_OK;
 }
 
@@ -2465,19 +1067,9 @@ static int build_schedule(nmg_engine* h, uint32_t grid) {
   return NMG_OK;
 }
 
-typedef void (*AttributeKernel)(Params);
-static AttributeKernel kernel_for(bool timing, int mode) {
-  static const AttributeKernel k[2][4] = {
-      {attribute_kernel<false, 0>, attribute_kernel<false, 1>, attribute_kernel<false, 2>, attribute_kernel<false, 3>},
-      {attribute_kernel<true, 0>, attribute_kernel<true, 1>, attribute_kernel<true, 2>, attribute_kernel<true, 3>}};
-  return k[timing ? 1 : 0][mode & 3];
-}
-
 static void ensure_occupancy(nmg_engine* h) {
   if (h->blocks_per_cu <= 0) {
-    int bpc = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, attribute_kernel<false, 0>, kWG, 0) != hipSuccess || bpc <= 0) bpc = 1;
-    h->blocks_per_cu = bpc;
+    h->blocks_per_cu = attribute_blocks_per_cu();
   }
 }
 
@@ -2587,11 +1179,10 @@ static int launch_attribution(nmg_engine* h, const uint8_t* data, const BufDesc*
       HIP_TRY(h, hipMemsetAsync(h->d_dbg, 0, n * 8, h->stream));
       h->dbg_len = n;
       p.dbg = reinterpret_cast<unsigned long long*>(h->d_dbg);
-      hipLaunchKernelGGL(kernel_for(true, mode), dim3(grid), dim3(kWG), 0, h->stream, p);
+      HIP_TRY(h, launch_attribute(true, mode, grid, h->stream, p));
     } else {
-      hipLaunchKernelGGL(kernel_for(false, mode), dim3(grid), dim3(kWG), 0, h->stream, p);
+      HIP_TRY(h, launch_attribute(false, mode, grid, h->stream, p));
     }
-    HIP_TRY(h, hipGetLastError());
     if (p.tlog) {  // sums the log per entry range, folds the packed counters
       TlogParams r;
       r.tlog = p.tlog;
@@ -2605,13 +1196,10 @@ static int launch_attribution(nmg_engine* h, const uint8_t* data, const BufDesc*
       r.rshift = p.tlog_rshift;
       r.nb_entries = h->E;
       r.pk_shift = p.pk_shift;
-      hipLaunchKernelGGL(tlog_reduce_kernel, dim3(p.tlog_parts), dim3(1024), 0, h->stream, r);
-      HIP_TRY(h, hipGetLastError());
+      HIP_TRY(h, launch_tlog_reduce(p.tlog_parts, h->stream, r));
     } else if (p.pk64) {
       const uint32_t blocks = (uint32_t)std::min<uint64_t>(2048, (2ull * h->E + 255) / 256);
-      hipLaunchKernelGGL(unpack_kernel, dim3(blocks), dim3(256), 0, h->stream, h->d_sum64, p.pk64, h->E,
-                         p.pk_shift);
-      HIP_TRY(h, hipGetLastError());
+      HIP_TRY(h, launch_unpack(blocks, h->stream, h->d_sum64, p.pk64, h->E, p.pk_shift));
     }
   }
   HIP_TRY(h, hipEventRecord(h->ring1[slot], h->stream));
