@@ -1116,7 +1116,7 @@ static int launch_attribution(nmg_engine* h, const uint8_t* data, const BufDesc*
   const int mode = (h->E <= kObjSlots ? kModeDenseObj : 0) |
                    (h->hist_cells <= kDensePageCells ? kModeDensePage : 0);
 #ifndef NMG_NO_PACK_TAIL
-  if (!(mode & kModeDenseObj) && h->d_pk64) {
+  if (!(mode & kModeDenseObj) && h->d_pk64 && !(h->flags & kDbgNoPack)) {
     // < 2^cbits samples in this launch (a SAMPLE record is 40 B); packed
     // weights < 2^(64 - 2 cbits), so any entry's packed sum < 2^(64 - cbits)
     const uint32_t cbits = 64 - (uint32_t)__builtin_clzll(nbytes / kRecBytes + 1);
@@ -1135,7 +1135,9 @@ static int launch_attribution(nmg_engine* h, const uint8_t* data, const BufDesc*
     const uint32_t parts = (uint32_t)(((uint64_t)h->E + (1ull << rshift) - 1) >> rshift);
     // sized for about every sample of the launch spread evenly; a full
     // sub-log only sends its overflow to the atomics
-    const uint64_t cap = std::min<uint64_t>(1u << 20, (nbytes / kRecBytes) / ((uint64_t)grid * parts) + 32);
+    const uint64_t cap = (h->flags & kDbgTinyLog)
+                             ? 2
+                             : std::min<uint64_t>(1u << 20, (nbytes / kRecBytes) / ((uint64_t)grid * parts) + 32);
     const size_t need = (size_t)grid * parts * cap * 24;
     if (need > h->tlog_bytes || (size_t)grid * parts > h->tlog_cnt_cap) {
       HIP_TRY(h, hipStreamSynchronize(h->stream));  // an earlier launch may still read the old log

@@ -67,6 +67,8 @@ constexpr uint32_t kDbgNoGlobal = 0x200;   // skip the global mem_counters updat
 constexpr uint32_t kDbgNoFlush = 0x400;    // LDS tables filled but never written to global
 constexpr uint32_t kDbgNoTables = 0x800;   // lookup only: no per-object / per-page accumulation
 constexpr uint32_t kDbgTiming = 0x1000;    // per-wave phase cycle counts (tools/phase_timing.py)
+constexpr uint32_t kDbgTinyLog = 0x2000;   // long-tail sub-logs of 2 records: exercises the overflow path (tests)
+constexpr uint32_t kDbgNoPack = 0x4000;    // overflow through plain atomics, not packed ones (tests)
 constexpr int kTimingWords = 24;           // per wave: load+check, barrier, process, rest, total, windows, -, -,
                                            // then (wave 0) 8 x 2 words of window trace
 

@@ -104,7 +104,7 @@ def test_full_config2_bit_exact(tmp_path):
 @pytest.mark.parametrize("nb_intervals", [300, 6_000])
 def test_large_weights_bit_exact(tmp_path, nb_intervals):
     """Weights at and above the kernel's packing limits (2^23 per lane, 2^26
-    per wave sum, 2^32, up to 2^63): the unpacked LDS / global paths of the
+    per wave sum, the packed long-tail limit 2^28, 2^32, up to 2^63): the unpacked LDS / global paths of the
     dense (<= 2048 entries) and hashed table modes must agree with the oracle,
     including u64 wrap-around of the weight sums (mem_sampling.c:531)."""
     d = str(tmp_path)
@@ -119,6 +119,28 @@ def test_large_weights_bit_exact(tmp_path, nb_intervals):
         rec["weight"][pick] = big[rng.integers(0, big.shape[0], int(pick.sum()))]
     path, odir = _oracle(rp, d)
     edir = _engine_replay(path, d)
+    _assert_raw_equal(os.path.join(d, "oracle_raw.bin"), os.path.join(d, "engine_raw.bin"))
+    assert open(os.path.join(d, "oracle_stdout.txt"), "rb").read() == open(os.path.join(d, "engine_stdout.txt"), "rb").read()
+    _same_dirs(odir, edir)
+
+
+@pytest.mark.parametrize("dbg", [0, 0x2000, 0x2000 | 0x4000])
+def test_long_tail_paths_bit_exact(tmp_path, dbg):
+    """Hashed object mode's three long-tail paths: the per-range log summed by
+    tlog_reduce_kernel, its overflow through packed atomics (internal switch
+    0x2000: sub-logs of 2 records) and through plain atomics (0x4000: no
+    packing); weights on both sides of the packing limit (2^(64 - 2 * 18) =
+    2^28 at 200k records) and past 2^32."""
+    d = str(tmp_path)
+    rp = generate(SynthConfig(nb_samples=200_000, nb_intervals=20_000, seed=17))
+    rng = np.random.default_rng(17)
+    big = np.array([(1 << 28) - 1, 1 << 28, (1 << 32) + 3, (1 << 63) + 1], dtype=np.uint64)
+    for b in rp.buffers:
+        rec = b.ring.view(RECORD_DTYPE)
+        pick = rng.random(rec.shape[0]) < 0.02
+        rec["weight"][pick] = big[rng.integers(0, big.shape[0], int(pick.sum()))]
+    path, odir = _oracle(rp, d)
+    edir = _engine_replay(path, d, flags=_lib.NMG_F_DEFAULT | dbg)
     _assert_raw_equal(os.path.join(d, "oracle_raw.bin"), os.path.join(d, "engine_raw.bin"))
     assert open(os.path.join(d, "oracle_stdout.txt"), "rb").read() == open(os.path.join(d, "engine_stdout.txt"), "rb").read()
     _same_dirs(odir, edir)
