@@ -319,6 +319,12 @@ int nmg_replay_open(nmg_replay_writer **out, const char *path, uint32_t nb_threa
                     const struct nmg_object_meta *meta, uint32_t nb_entries);
 int nmg_replay_add_ring(nmg_replay_writer *w, const void *ring, uint64_t ring_size, uint64_t data_tail,
                         uint64_t data_head, uint32_t thread_rank, uint32_t access_type);
+/* The dump modes' context of the traced process, stored in the replay's
+ * optional trailing section and used by nmg_run_replay when NMG_REPLAY_DUMP
+ * is set: the module table (dladdr, all_memory_objects.dat) and
+ * /proc/<pid>/maps (unmatched_samples.log header).  Call before close. */
+int nmg_replay_set_context(nmg_replay_writer *w, const struct nmg_module *modules, uint32_t nb_modules,
+                           const char *maps_path, const char *maps_text);
 int nmg_replay_close(nmg_replay_writer *w);
 
 #ifdef __cplusplus

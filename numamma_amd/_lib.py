@@ -146,6 +146,7 @@ _SIGS = {
                                   C.POINTER(nmg_object), C.POINTER(nmg_object_meta), C.c_uint32]),
     "nmg_replay_add_ring": (C.c_int, [C.c_void_p, P, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32]),
     "nmg_replay_close": (C.c_int, [C.c_void_p]),
+    "nmg_replay_set_context": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_char_p, C.c_char_p]),
     "nmg_set_device_buffers": (C.c_int, [H, P, u64p, u64p, u32p, u32p, C.c_uint32, C.c_uint64]),
     "nmg_analyze": (C.c_int, [H]),
     "nmg_synchronize": (C.c_int, [H]),

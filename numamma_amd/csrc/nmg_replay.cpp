@@ -32,7 +32,13 @@ struct Replay {
     const uint8_t* bytes;
   };
   std::vector<Buf> bufs;
+  // optional trailing context section (dump modes of the traced process)
+  std::vector<nmg_module> modules;  // fname points into `file`
+  std::string maps_path, maps_text;
+  bool has_maps_path = false;
 };
+
+constexpr char kCtxMagic[8] = {'N', 'M', 'G', 'M', 'O', 'D', 'S', '1'};
 
 template <class T>
 T get(const uint8_t* p) {
@@ -143,6 +149,33 @@ int load_replay(const char* path, Replay& r, std::string& err) {
     off += pad8(B.ring);
     r.bufs.push_back(B);
   }
+  // context section: "NMGMODS1", u32 nb_modules, u32 names_bytes, u32
+  // maps_path_bytes, u32 maps_text_bytes, u64 0; modules {u64 lo, hi, fbase,
+  // u32 name_off, u32 0}; names pool; maps path; maps text (each padded to 8)
+  if (off + 32 <= r.file.size() && memcmp(p + off, kCtxMagic, 8) == 0) {
+    const uint32_t nm = get<uint32_t>(p + off + 8), nb_names = get<uint32_t>(p + off + 12);
+    const uint32_t nb_path = get<uint32_t>(p + off + 16), nb_text = get<uint32_t>(p + off + 20);
+    off += 32;
+    const size_t mods_off = off, names_off = mods_off + 32ull * nm, path_off = names_off + pad8(nb_names),
+                 text_off = path_off + pad8(nb_path);
+    if (text_off + pad8(nb_text) > r.file.size() || (nb_names && p[names_off + nb_names - 1] != 0)) {
+      err = "truncated context section";
+      return NMG_ERR_INVALID;
+    }
+    for (uint32_t i = 0; i < nm; i++) {
+      const uint8_t* q = p + mods_off + 32ull * i;
+      const uint32_t name_off = get<uint32_t>(q + 24);
+      if (name_off >= nb_names) {
+        err = "module name out of range";
+        return NMG_ERR_INVALID;
+      }
+      r.modules.push_back({get<uint64_t>(q), get<uint64_t>(q + 8), get<uint64_t>(q + 16),
+                           reinterpret_cast<const char*>(p + names_off + name_off)});
+    }
+    r.has_maps_path = nb_path != 0;
+    r.maps_path.assign(reinterpret_cast<const char*>(p + path_off), nb_path);
+    r.maps_text.assign(reinterpret_cast<const char*>(p + text_off), nb_text);
+  }
   return NMG_OK;
 }
 
@@ -210,6 +243,11 @@ extern "C" int nmg_run_replay(const char* replay_path, const char* output_dir, c
   memset(&opt, 0, sizeof(opt));
   opt.device = device;
   opt.flags = flags | (raw_path ? NMG_F_OBJECT_LEVELS : 0);
+  // NMG_REPLAY_DUMP=<NMG_DUMP_* flags>: the dump modes, with the context
+  // section's module table and maps file (the -d / -D / -u outputs)
+  const char* dump_env = getenv("NMG_REPLAY_DUMP");
+  const int dump_flags = dump_env ? atoi(dump_env) : 0;
+  if (dump_flags) opt.flags |= NMG_F_SAMPLE_MATCHES | NMG_F_OBJECT_LEVELS;
   opt.nb_threads = r.nb_threads ? r.nb_threads : 1;
   // NMG_REPLAY_STREAM="chunk_bytes[:copy_threads[:batch]]": feed the buffers
   // in nmg_submit_buffers batches (unwrapped ring segments; wrapped ones through
@@ -281,6 +319,11 @@ extern "C" int nmg_run_replay(const char* replay_path, const char* output_dir, c
   memset(&ro, 0, sizeof(ro));
   ro.output_dir = output_dir;
   ro.dump_single_items = 1;
+  ro.dump_flags = dump_flags;
+  ro.maps_path = r.has_maps_path ? r.maps_path.c_str() : nullptr;
+  ro.maps_text = r.maps_text.empty() ? nullptr : r.maps_text.c_str();
+  ro.modules = r.modules.data();
+  ro.nb_modules = (uint32_t)r.modules.size();
   rc = nmg_report(h, r.meta.data(), &ro, stdout_path);
   if (rc) return bail(rc);
   if (raw_path) {
@@ -300,6 +343,7 @@ struct nmg_replay_writer {
   uint32_t nb_buffers = 0;
   uint32_t nb_threads = 0;
   bool ok = true;
+  std::vector<uint8_t> ctx;  // context section, written by nmg_replay_close
 };
 
 namespace {
@@ -413,9 +457,45 @@ extern "C" int nmg_replay_add_ring(nmg_replay_writer* w, const void* ring, uint6
   return NMG_OK;
 }
 
+extern "C" int nmg_replay_set_context(nmg_replay_writer* w, const nmg_module* modules, uint32_t nb_modules,
+                                      const char* maps_path, const char* maps_text) {
+  if (!w || !w->f || (nb_modules && !modules)) return NMG_ERR_INVALID;
+  std::string names;
+  std::vector<uint8_t> mods;
+  for (uint32_t i = 0; i < nb_modules; i++) {
+    const nmg_module& m = modules[i];
+    if (m.hi < m.lo) return NMG_ERR_INVALID;
+    put<uint64_t>(mods, m.lo);
+    put<uint64_t>(mods, m.hi);
+    put<uint64_t>(mods, m.fbase);
+    put<uint32_t>(mods, (uint32_t)names.size());
+    put<uint32_t>(mods, 0);
+    names.append(m.fname ? m.fname : "(null)");
+    names.push_back('\0');
+  }
+  const std::string path = maps_path ? maps_path : "", text = maps_text ? maps_text : "";
+  std::vector<uint8_t>& c = w->ctx;
+  c.clear();
+  c.insert(c.end(), kCtxMagic, kCtxMagic + 8);
+  put<uint32_t>(c, nb_modules);
+  put<uint32_t>(c, (uint32_t)names.size());
+  put<uint32_t>(c, (uint32_t)path.size());
+  put<uint32_t>(c, (uint32_t)text.size());
+  put<uint64_t>(c, 0);
+  c.insert(c.end(), mods.begin(), mods.end());
+  c.insert(c.end(), names.begin(), names.end());
+  pad_to8(c);
+  c.insert(c.end(), path.begin(), path.end());
+  pad_to8(c);
+  c.insert(c.end(), text.begin(), text.end());
+  pad_to8(c);
+  return NMG_OK;
+}
+
 extern "C" int nmg_replay_close(nmg_replay_writer* w) {
   if (!w) return NMG_ERR_INVALID;
   bool ok = w->ok && w->f;
+  if (ok && !w->ctx.empty()) ok = fwrite(w->ctx.data(), 1, w->ctx.size(), w->f) == w->ctx.size();
   if (w->f) {
     ok = ok && fseek(w->f, 24, SEEK_SET) == 0 && fwrite(&w->nb_buffers, 4, 1, w->f) == 1;
     ok = (fclose(w->f) == 0) && ok;

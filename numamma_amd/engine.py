@@ -243,6 +243,11 @@ def write_replay_c(path: str, replay: Replay) -> None:
             ring = np.ascontiguousarray(b.ring, dtype=np.uint8)
             check(lib.nmg_replay_add_ring(w, ring.ctypes.data, ring.shape[0], b.data_tail, b.data_head,
                                           b.thread_rank, b.access_type))
+        if replay.modules or replay.maps_path or replay.maps_text:
+            marr, nmods = _lib.module_array(replay.modules)
+            check(lib.nmg_replay_set_context(w, C.cast(marr, C.c_void_p), nmods,
+                                             replay.maps_path.encode() if replay.maps_path else None,
+                                             replay.maps_text.encode() if replay.maps_text else None))
     finally:
         check(lib.nmg_replay_close(w))
 

@@ -24,6 +24,10 @@ File layout (little endian, DESIGN.md "Replay format")::
     char string_pool[]                             (padded to 8)
     per buffer: u32 thread_rank, u32 access_type, u64 data_tail,
                 u64 data_head, u64 ring_size, ring bytes (padded to 8)
+    optional context (dump modes): "NMGMODS1", u32 nb_modules, u32 names_bytes,
+                u32 maps_path_bytes, u32 maps_text_bytes, u64 0; per module
+                u64 lo, u64 hi, u64 fbase, u32 name_off, u32 0; names pool,
+                maps path, maps text (each padded to 8)
 
 The generator follows SURVEY.md section 8(d): log-uniform object sizes with
 gaps, ~3 % address reuse (same key, disjoint lifetimes), ~0.5 % realloc'd
@@ -165,12 +169,35 @@ class Buffer:
         return r[t:h]
 
 
+CONTEXT_MAGIC = b"NMGMODS1"
+
+
+def _context_section(modules, maps_path, maps_text) -> bytes:
+    names = bytearray()
+    mods = bytearray()
+    for lo, hi, fb, fn in modules:
+        mods += struct.pack("<QQQII", lo, hi, fb, len(names), 0)
+        names += fn.encode() + b"\0"
+    path = (maps_path or "").encode()
+    text = (maps_text or "").encode()
+    out = bytearray(CONTEXT_MAGIC + struct.pack("<IIIIQ", len(modules), len(names), len(path), len(text), 0))
+    out += mods
+    for part in (bytes(names), path, text):
+        out += part + b"\0" * (_pad8(len(part)) - len(part))
+    return bytes(out)
+
+
 @dataclass
 class Replay:
     nb_threads: int
     table: ObjectTable
     buffers: List[Buffer]
     meta: dict = field(default_factory=dict)
+    # dump-mode context of the traced process: dladdr() module table
+    # [(lo, hi, fbase, fname)] and /proc/<pid>/maps (path, text)
+    modules: list = field(default_factory=list)
+    maps_path: Optional[str] = None
+    maps_text: Optional[str] = None
 
     # ------------------------------------------------------------------
     def write(self, path: str) -> None:
@@ -204,6 +231,8 @@ class Replay:
                 f.write(struct.pack("<IIQQQ", b.thread_rank, b.access_type, b.data_tail, b.data_head, ring.shape[0]))
                 f.write(ring.tobytes())
                 f.write(b"\0" * (_pad8(ring.shape[0]) - ring.shape[0]))
+            if self.modules or self.maps_path or self.maps_text:
+                f.write(_context_section(self.modules, self.maps_path, self.maps_text))
 
     @staticmethod
     def read(path: str) -> "Replay":
@@ -229,7 +258,19 @@ class Replay:
             off += 32
             bufs.append(Buffer(rank, acc, data[off : off + ring].copy(), tail, head))
             off += _pad8(ring)
-        return Replay(nthr, ObjectTable(keys, entry_off, entries, pool, strings), bufs)
+        rp = Replay(nthr, ObjectTable(keys, entry_off, entries, pool, strings), bufs)
+        if off + 32 <= len(raw) and raw[off : off + 8] == CONTEXT_MAGIC:
+            nm, nn, npath, ntext = struct.unpack_from("<IIII", raw, off + 8)
+            off += 32
+            mods = [struct.unpack_from("<QQQI", raw, off + 32 * i) for i in range(nm)]
+            off += 32 * nm
+            names = raw[off : off + nn]
+            off += _pad8(nn)
+            rp.maps_path = raw[off : off + npath].decode() if npath else None
+            off += _pad8(npath)
+            rp.maps_text = raw[off : off + ntext].decode() if ntext else None
+            rp.modules = [(lo, hi, fb, names[no : names.index(b"\0", no)].decode()) for lo, hi, fb, no in mods]
+        return rp
 
     # ------------------------------------------------------------------
     def linear_buffers(self):

@@ -521,3 +521,25 @@ def test_dump_modes_bit_exact(tmp_path, dump, dump_all, unmatched, single, resid
     assert any(n.startswith("callsite_summary_") for n in names) == bool((dump or dump_all) and single)
     assert ("all_memory_objects.dat" in names) == bool(dump_all)
     _same_dirs(odir, edir)
+
+
+def test_replay_helper_dump_modes(tmp_path, monkeypatch):
+    """The out-of-process helper path (nmg_run_replay, NMG_REPLAY_DUMP=7) with
+    the replay's context section (module table, maps file): every dump file,
+    all_memory_objects.dat included, byte-identical to the oracle's."""
+    d = str(tmp_path)
+    rp = generate(SynthConfig(nb_samples=40_000, nb_intervals=300, lost_frac=2e-3, wrap_one=True, seed=52))
+    rp.modules, rp.maps_path, rp.maps_text = DUMP_MODULES, "/proc/4242/maps", MAPS
+    path = os.path.join(d, "replay.bin")
+    rp.write(path)
+    odir = os.path.join(d, "oracle")
+    pyoracle.run(path, odir, os.path.join(d, "o.txt"), dump=True, dump_all=True, dump_unmatched=True,
+                 maps_path=rp.maps_path, maps_text=MAPS, modules=DUMP_MODULES)
+    monkeypatch.setenv("NMG_REPLAY_DUMP", str(_lib.NMG_DUMP_CALLSITES | _lib.NMG_DUMP_ALL | _lib.NMG_DUMP_UNMATCHED))
+    from numamma_amd.engine import run_replay
+
+    edir = os.path.join(d, "engine")
+    run_replay(path, edir, os.path.join(d, "e.txt"))
+    assert open(os.path.join(d, "o.txt"), "rb").read() == open(os.path.join(d, "e.txt"), "rb").read()
+    assert "all_memory_objects.dat" in os.listdir(edir)
+    _same_dirs(odir, edir)

@@ -115,3 +115,36 @@ def test_c_replay_writer_matches_python(tmp_path):
         pyoracle.run(p, d, d + ".txt", d + "_raw.bin")
         outs.append((open(d + ".txt", "rb").read(), open(d + "_raw.bin", "rb").read(), open(d + "/call_sites.log", "rb").read()))
     assert outs[0] == outs[1]
+
+
+def test_replay_context_section(tmp_path):
+    """The dump-mode context (dladdr module table, /proc/<pid>/maps) travels in
+    the replay's optional trailing section, written identically by the Python
+    writer and the C-ABI writer (nmg_replay_set_context); readers that do not
+    use it (the oracle) are unaffected."""
+    import pyoracle
+    from numamma_amd.engine import write_replay_c
+    from numamma_amd.replay import Replay, SynthConfig, generate
+
+    rp = generate(SynthConfig(nb_samples=5_000, nb_intervals=50, seed=43))
+    rp.modules = [(0x400000, 0x480000, 0x400000, "/usr/bin/app"), (0x480000, 0x4F0000, 0x470000, "/lib/libx.so.1")]
+    rp.maps_path = "/proc/4242/maps"
+    rp.maps_text = "00400000-00452000 r-xp 00000000 08:02 173521 /usr/bin/app\n"
+    pa, pb = str(tmp_path / "py.bin"), str(tmp_path / "c.bin")
+    rp.write(pa)
+    write_replay_c(pb, rp)
+    ta, tb = open(pa, "rb").read(), open(pb, "rb").read()
+    assert ta[ta.index(b"NMGMODS1"):] == tb[tb.index(b"NMGMODS1"):]  # (the pools may be laid out differently)
+    for p in (pa, pb):
+        back = Replay.read(p)
+        assert back.modules == rp.modules and back.maps_path == rp.maps_path and back.maps_text == rp.maps_text
+    plain = Replay.read(pa)
+    plain.modules, plain.maps_path, plain.maps_text = [], None, None
+    pc = str(tmp_path / "plain.bin")
+    plain.write(pc)
+    outs = []
+    for p in (pa, pc):
+        d = str(tmp_path / ("o_" + os.path.basename(p)))
+        pyoracle.run(p, d, d + ".txt", d + "_raw.bin")
+        outs.append((open(d + ".txt", "rb").read(), open(d + "_raw.bin", "rb").read()))
+    assert outs[0] == outs[1]
