@@ -1,5 +1,7 @@
 // nmg_replay CLI: analyse a replay file on the GPU and write NumaMMa's report.
 //   nmg_replay replay.bin outdir [--raw raw.bin] [--device N] [--no-match]
+// Environment: NMG_REPLAY_DUMP=<NMG_DUMP_* flags> (the -d / -D / -u outputs,
+// with the replay's context section), NMG_REPLAY_STREAM=chunk[:threads[:batch]].
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -8,7 +10,10 @@
 
 int main(int argc, char** argv) {
   if (argc < 3) {
-    fprintf(stderr, "usage: %s replay.bin outdir [--raw raw.bin] [--device N] [--no-match]\n", argv[0]);
+    fprintf(stderr,
+            "usage: %s replay.bin outdir [--raw raw.bin] [--device N] [--no-match]\n"
+            "  env NMG_REPLAY_DUMP=<1 -d | 2 -D | 4 -u>, NMG_REPLAY_STREAM=chunk[:threads[:batch]]\n",
+            argv[0]);
     return 2;
   }
   const char* raw = nullptr;
