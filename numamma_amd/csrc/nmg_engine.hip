@@ -124,6 +124,10 @@ struct nmg_engine {
   size_t tlog_bytes = 0;
   uint32_t* d_tlog_cnt = nullptr;
   size_t tlog_cnt_cap = 0;
+  unsigned long long* d_rlog = nullptr;  // partition-first lookup: routed samples (see Params::rlog)
+  size_t rlog_bytes = 0;
+  uint32_t* d_rcnt = nullptr;
+  size_t rcnt_cap = 0;
   size_t smatch_cap = 0;
   uint64_t nreset = 0;
 
@@ -251,6 +255,12 @@ static void free_counters(nmg_engine* h) {
   (void)hipFree(h->d_tlog_cnt);
   h->d_tlog_cnt = nullptr;
   h->tlog_cnt_cap = 0;
+  (void)hipFree(h->d_rlog);
+  h->d_rlog = nullptr;
+  h->rlog_bytes = 0;
+  (void)hipFree(h->d_rcnt);
+  h->d_rcnt = nullptr;
+  h->rcnt_cap = 0;
 }
 
 static void free_table(nmg_engine* h) {
@@ -1163,6 +1173,47 @@ static int launch_attribution(nmg_engine* h, const uint8_t* data, const BufDesc*
     p.tlog_parts = parts;
   }
 #endif
+  // partition-first lookup (large tables): ranges of 2^kRouteKeysLog2 keys
+  uint32_t route_kshift = 0;
+#ifdef NMG_ROUTE_DEFAULT
+  const bool route_req = true;
+#else
+  const bool route_req = (h->flags & kDbgRoute) != 0;
+#endif
+  if (!(mode & kModeDenseObj) && nb && !p.lds_nodes && route_req && (h->flags & NMG_F_MATCH_SAMPLES) &&
+      !(h->flags & (NMG_F_SAMPLE_MATCHES | NMG_F_OBJECT_LEVELS)) && grid <= kLogMaxGrid &&
+      h->fence_log2 < kRouteKeysLog2 && nbytes / kRecBytes < (1ull << 31)) {
+    const uint32_t rq = kRouteKeysLog2 - h->fence_log2;
+    const uint32_t parts = (h->nb_fences + (1u << rq) - 1) >> rq;
+    uint64_t cap = std::min<uint64_t>(1u << 16, 2 * (nbytes / kRecBytes) / ((uint64_t)grid * parts) + 16);
+    cap = std::min<uint64_t>(cap, (2ull << 30) / ((uint64_t)grid * parts * 32));
+    if (parts <= kRouteMaxParts && cap >= 4) {
+      const size_t need = (size_t)grid * parts * cap * 32;
+      if (need > h->rlog_bytes || (size_t)grid * parts > h->rcnt_cap) {
+        HIP_TRY(h, hipStreamSynchronize(h->stream));
+        if (need > h->rlog_bytes) {
+          (void)hipFree(h->d_rlog);
+          h->d_rlog = nullptr;
+          h->rlog_bytes = 0;
+          HIP_TRY(h, hipMalloc(&h->d_rlog, need));
+          h->rlog_bytes = need;
+        }
+        if ((size_t)grid * parts > h->rcnt_cap) {
+          (void)hipFree(h->d_rcnt);
+          h->d_rcnt = nullptr;
+          h->rcnt_cap = 0;
+          HIP_TRY(h, hipMalloc(&h->d_rcnt, (size_t)grid * parts * 4));
+          h->rcnt_cap = (size_t)grid * parts;
+        }
+      }
+      p.rlog = h->d_rlog;
+      p.rcnt = h->d_rcnt;
+      p.rcap = (uint32_t)cap;
+      p.rparts = parts;
+      p.rq_shift = rq;
+      route_kshift = h->fence_log2 + rq;
+    }
+  }
   const int slot = (int)(h->nlaunch % nmg_engine::kRing);
   if (!h->ring0[slot]) {
     HIP_TRY(h, hipEventCreate(&h->ring0[slot]));
@@ -1202,6 +1253,13 @@ static int launch_attribution(nmg_engine* h, const uint8_t* data, const BufDesc*
     } else if (p.pk64) {
       const uint32_t blocks = (uint32_t)std::min<uint64_t>(2048, (2ull * h->E + 255) / 256);
       HIP_TRY(h, launch_unpack(blocks, h->stream, h->d_sum64, p.pk64, h->E, p.pk_shift));
+    }
+    if (p.rlog) {  // routed samples: resolved per key range, then tallied per buffer
+      RouteParams rp;
+      rp.p = p;
+      rp.grid = grid;
+      rp.kshift = route_kshift;
+      HIP_TRY(h, launch_route(p.rparts, grid, h->stream, rp));
     }
   }
   HIP_TRY(h, hipEventRecord(h->ring1[slot], h->stream));
