@@ -1123,8 +1123,7 @@ static int launch_attribution(nmg_engine* h, const uint8_t* data, const BufDesc*
   p.sparse_dirty = h->d_sparse_dirty ? h->d_sparse_dirty + (h->nreset & 1) : nullptr;
   p.smatch = (h->flags & NMG_F_SAMPLE_MATCHES) ? h->d_smatch : nullptr;
   // dense LDS tables when the table is small enough (DESIGN.md "Kernels")
-  const int mode = (h->E <= kObjSlots ? kModeDenseObj : 0) |
-                   (h->hist_cells <= kDensePageCells ? kModeDensePage : 0);
+  int mode = (h->E <= kObjSlots ? kModeDenseObj : 0) | (h->hist_cells <= kDensePageCells ? kModeDensePage : 0);
 #ifndef NMG_NO_PACK_TAIL
   if (!(mode & kModeDenseObj) && h->d_pk64 && !(h->flags & kDbgNoPack)) {
     // < 2^cbits samples in this launch (a SAMPLE record is 40 B); packed
@@ -1212,6 +1211,7 @@ static int launch_attribution(nmg_engine* h, const uint8_t* data, const BufDesc*
       p.rparts = parts;
       p.rq_shift = rq;
       route_kshift = h->fence_log2 + rq;
+      mode |= kModeRoute;
     }
   }
   const int slot = (int)(h->nlaunch % nmg_engine::kRing);

@@ -54,6 +54,7 @@ constexpr uint32_t kTableWindows = 256;
 //                   kDensePageWindows windows (<= 1024 samples per cell each,
 //                   so a u16 cannot overflow into its neighbour)
 constexpr int kModeDenseObj = 1, kModeDensePage = 2;
+constexpr int kModeRoute = 4;  // partition-first lookup (hashed object mode only): Params::rlog is set
 constexpr uint32_t kDensePageCells = kPageSlots * 4;  // the page table's 56 KiB as u16 cells
 constexpr uint32_t kDensePageWindows = 62;
 #ifdef NMG_NO_PACK_OBJ

@@ -517,7 +517,7 @@ __device__ __forceinline__ void process_sample(Params& p, WgCounters& wc, LaneAc
   Match m;
   m.e = -1;
   // (routed samples are matched by route_resolve_kernel and tallied by route_tally_kernel)
-  const bool routed = !(MODE & kModeDenseObj) && p.rlog && valid && route_sample(p, L, s_rcur, rdesc, off, ts, addr, w);
+  const bool routed = (MODE & kModeRoute) && valid && route_sample(p, L, s_rcur, rdesc, off, ts, addr, w);
   if (valid && !routed) m = find_entry(p, L, addr, ts, sp);
   const int64_t e = m.e;
   fmask = __ballot(e >= 0);
@@ -834,7 +834,8 @@ __global__ __launch_bounds__(kWG, 1) void attribute_kernel(Params p) {
   constexpr bool kLog = !(MODE & kModeDenseObj);  // the long-tail log serves the hashed object mode
   if (kLog && p.tlog)
     for (uint32_t i = tid; i < kLogParts; i += kWG) wc.tcur[i] = 0;
-  if (kLog && p.rlog)
+  constexpr bool kRoute = (MODE & kModeRoute) != 0;
+  if (kRoute)
     for (uint32_t i = tid; i < p.rparts; i += kWG) s_rcur[i] = 0;
   if (tid < 3) s_flags[tid] = 0;
   __syncthreads();
@@ -848,7 +849,7 @@ __global__ __launch_bounds__(kWG, 1) void attribute_kernel(Params p) {
   if (r0 >= r1) {
     if (kLog && p.tlog)
       for (uint32_t i = tid; i < p.tlog_parts; i += kWG) p.tlog_cnt[uint64_t(blockIdx.x) * p.tlog_parts + i] = 0;
-    if (kLog && p.rlog)
+    if (kRoute)
       for (uint32_t i = tid; i < p.rparts; i += kWG) p.rcnt[uint64_t(blockIdx.x) * p.rparts + i] = 0;
     return;
   }
@@ -1025,7 +1026,7 @@ __global__ __launch_bounds__(kWG, 1) void attribute_kernel(Params p) {
     if (!(p.flags & kDbgLoadOnly))
       process_sample<MODE>(p, wc, acc, L, valid, rec.ts, rec.addr, rec.w, rec.dsrc, d0.access, d0.thread_rank, rseq, roff,
                            rbase, vm, fm, sp, s_rcur, rdesc);
-    if (kSpec && !p.lds_nodes && !p.rlog && (p.flags & NMG_F_MATCH_SAMPLES)) {
+    if (kSpec && !kRoute && !p.lds_nodes && (p.flags & NMG_F_MATCH_SAMPLES)) {
       // start the next window's lookup: its record (loaded above, arrived
       // during this window's lookups) -> fence node -> directory slot load,
       // in flight across the flush and the barrier.  Used when the record
@@ -1105,12 +1106,12 @@ __global__ __launch_bounds__(kWG, 1) void attribute_kernel(Params p) {
     }
     if (idx >= r1) break;  // the loop's only exit, after the state update
   }
-  if (kLog && (p.tlog || p.rlog)) {  // the sub-logs' fill (every append of this workgroup is done)
+  if (kLog && (p.tlog || kRoute)) {  // the sub-logs' fill (every append of this workgroup is done)
     __syncthreads();
     if (p.tlog)
       for (uint32_t i = tid; i < p.tlog_parts; i += kWG)
         p.tlog_cnt[uint64_t(blockIdx.x) * p.tlog_parts + i] = min(wc.tcur[i], p.tlog_cap);
-    if (p.rlog)
+    if (kRoute)
       for (uint32_t i = tid; i < p.rparts; i += kWG) p.rcnt[uint64_t(blockIdx.x) * p.rparts + i] = min(s_rcur[i], p.rcap);
   }
   if (TIMING && lane == 0) {
@@ -1490,10 +1491,14 @@ __global__ __launch_bounds__(256) void reset_kernel(ResetParams r) {
 typedef void (*AttributeKernel)(Params);
 
 hipError_t launch_attribute(bool timing, int mode, uint32_t grid, hipStream_t s, const Params& p) {
-  static const AttributeKernel k[2][4] = {
-      {attribute_kernel<false, 0>, attribute_kernel<false, 1>, attribute_kernel<false, 2>, attribute_kernel<false, 3>},
-      {attribute_kernel<true, 0>, attribute_kernel<true, 1>, attribute_kernel<true, 2>, attribute_kernel<true, 3>}};
-  hipLaunchKernelGGL(k[timing ? 1 : 0][mode & 3], dim3(grid), dim3(kWG), 0, s, p);
+  // (routing is built only into the hashed object modes: 5 and 7 never run)
+  static const AttributeKernel k[2][8] = {
+      {attribute_kernel<false, 0>, attribute_kernel<false, 1>, attribute_kernel<false, 2>, attribute_kernel<false, 3>,
+       attribute_kernel<false, 4>, attribute_kernel<false, 1>, attribute_kernel<false, 6>, attribute_kernel<false, 3>},
+      {attribute_kernel<true, 0>, attribute_kernel<true, 1>, attribute_kernel<true, 2>, attribute_kernel<true, 3>,
+       attribute_kernel<true, 4>, attribute_kernel<true, 1>, attribute_kernel<true, 6>, attribute_kernel<true, 3>}};
+  if ((mode & kModeRoute) && (mode & kModeDenseObj)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k[timing ? 1 : 0][mode & 7], dim3(grid), dim3(kWG), 0, s, p);
   return hipGetLastError();
 }
 
