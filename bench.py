@@ -4,21 +4,26 @@
 One step = one full analysis pass over one batch of synthetic PEBS buffers
 already resident in HBM: reset the counters, run the attribution kernel over
 every buffer (the body of mem_sampling_finalize's loop, src/mem_sampling.c:
-324-342) and, for N > 1, merge the per-rank counters into rank 0 with RCCL
-reduces over xGMI.  Report printing is outside the timed region.
+324-342) and its long-tail reduce, and, for N > 1, merge the per-rank
+counters into rank 0 with RCCL reduces over xGMI.  Report printing is outside
+the timed region.
 
-Workload (BASELINE.json configs[1], "c2"): 10M 40-byte PERF_RECORD_SAMPLE
-records per GPU in 128 KiB per-thread buffers, 1k object intervals (+ 8
-globals + [stack]), 8 threads.  Weak scaling: every rank analyses its own
-10M-record shard against the same object table.
+Default workload (the north-star configuration, BASELINE.json configs[3]'s
+per-GPU shard): 125M 40-byte PERF_RECORD_SAMPLE records per GPU in 128 KiB
+per-thread buffers, 1M object intervals (+ 8 globals + [stack]), 8 threads.
+Weak scaling: every rank analyses its own 125M-record shard against the same
+table, so --gpus 8 is configs[3] (1B records).  configs[1] (10M records, 1k
+intervals) is measured after it and reported in the same JSON line under
+"secondary".
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2|c3|c4|k1m]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c4|c2|c3|k1m]
     torchrun --nproc-per-node N bench.py --gpus N ...
 """
 from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -30,14 +35,15 @@ sys.path.insert(0, ROOT)
 
 RECORD_BYTES = 40
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+MIN_TIMED_S = 1.0      # default --steps: enough steps for at least this much timed work
 
 WORKLOADS = {
     "c2": dict(nb_samples=10_000_000, nb_intervals=1_000, desc="configs[1]: 10M PEBS records/GPU, 1k object intervals"),
     "c3": dict(nb_samples=100_000_000, nb_intervals=100_000, desc="configs[2]: 100M PEBS records/GPU, 100k intervals, per-page on"),
     "c4": dict(nb_samples=125_000_000, nb_intervals=1_000_000, size_max=64 * 1024,
-               desc="configs[3] per-GPU shard: 1B records / 8 GPUs, 1M intervals"),
+               desc="configs[3] per-GPU shard: 1B records / 8 GPUs, 1M intervals, per-page on"),
     "k1m": dict(nb_samples=10_000_000, nb_intervals=1_000_000, size_max=64 * 1024,
-                desc="north-star table size: 10M PEBS records/GPU, 1M object intervals"),
+                desc="north-star table size, small batch: 10M PEBS records/GPU, 1M object intervals"),
 }
 
 
@@ -45,15 +51,83 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+class Workload:
+    """One synthetic batch resident in HBM and an engine over it."""
+
+    def __init__(self, name, rank, device, distributed):
+        import torch
+
+        from numamma_amd import _lib
+        from numamma_amd.engine import Engine
+        from numamma_amd.replay import SynthConfig, generate
+
+        self.name = name
+        wl = WORKLOADS[name]
+        cfg_kw = {k: v for k, v in wl.items() if k != "desc"}
+        self.cfg = SynthConfig(seed=1, sample_seed=1000 + rank, **cfg_kw)
+        t0 = time.time()
+        self.rp = generate(self.cfg)
+        arena, offs, lens, ranks, acc = self.rp.packed()
+        log(f"[rank {rank}] {name}: {self.rp.nb_records()} records in {len(lens)} buffers, "
+            f"{arena.nbytes / 1e6:.0f} MB, generated in {time.time() - t0:.1f}s")
+        self.d_arena = torch.from_numpy(arena).to(device)
+        del arena
+        self.nb_buf = len(lens)
+        self.samples = int(lens.sum()) // RECORD_BYTES
+        self.eng = Engine(device=device.index, flags=_lib.NMG_F_DEFAULT, nb_threads=self.rp.nb_threads)
+        self.eng.set_objects(self.rp.table)
+        # global analysis order: rank-major (seq_base)
+        self.eng.set_device_buffers(self.d_arena.data_ptr(), offs, lens, ranks, acc, seq_base=rank * self.nb_buf)
+        self.merge_bufs = []
+        if distributed:  # merge buffers for the timed RCCL reduces (dense arrays)
+            for which, dt in ((_lib.NMG_ARR_SUM64, torch.int64), (_lib.NMG_ARR_MIN64, torch.int64),
+                              (_lib.NMG_ARR_MAX64, torch.int64), (_lib.NMG_ARR_HIST32, torch.int32)):
+                n = self.eng.array_size(which)
+                if n:
+                    self.merge_bufs.append((which, torch.empty(n, dtype=dt, device=device)))
+
+    def step(self):
+        from numamma_amd import _lib
+        from numamma_amd.distributed import reduce_u32_sum, reduce_u64
+
+        self.eng.reset()
+        self.eng.analyze()
+        if self.merge_bufs:
+            self.eng.synchronize()
+            for which, t in self.merge_bufs:
+                self.eng.export_array(which, t.data_ptr())
+                if which == _lib.NMG_ARR_HIST32:
+                    reduce_u32_sum(t, dst=0)
+                else:
+                    reduce_u64(t, {0: "sum", 1: "min", 2: "max"}[which], dst=0)
+
+
+def timed_run(w, steps, warmup, barrier):
+    for _ in range(warmup):
+        w.step()
+    barrier()
+    if steps <= 0:  # auto: one more step to size the timed region
+        t = time.perf_counter()
+        w.step()
+        barrier()
+        one = time.perf_counter() - t
+        steps = int(min(2000, max(20, math.ceil(MIN_TIMED_S / max(one, 1e-6)))))
+    t_start = time.perf_counter()
+    for _ in range(steps):
+        w.step()
+    barrier()  # device sync; raises on a kernel-reported error
+    return time.perf_counter() - t_start, steps
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=0, help="timed steps (0: enough for >= 1 s)")
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
+    ap.add_argument("--workload", default="c4", choices=sorted(WORKLOADS))
+    ap.add_argument("--secondary", default="c2", help="workload measured after the main one (N=1; '' = none)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample-frac", type=float, default=1.0)
-    ap.add_argument("--verify", action="store_true", help="check the merged counters against the oracle")
+    ap.add_argument("--cpu-records", type=int, default=10_000_000, help="records in the CPU baseline's sample")
     args = ap.parse_args()
 
     import torch
@@ -79,139 +153,118 @@ def main():
             dist.init_process_group(backend)
     device = torch.device("cuda", local)
 
-    from numamma_amd import _lib
-    from numamma_amd.distributed import merge_engine, reduce_u32_sum, reduce_u64
-    from numamma_amd.engine import Engine
-    from numamma_amd.replay import SynthConfig, generate
+    from numamma_amd.distributed import merge_engine
 
-    wl = WORKLOADS[args.workload]
-    cfg_kw = {k: v for k, v in wl.items() if k != "desc"}
-    cfg = SynthConfig(seed=1, sample_seed=1000 + rank, **cfg_kw)
-    t0 = time.time()
-    rp = generate(cfg)
-    arena, offs, lens, ranks, acc = rp.packed()
-    log(f"[rank {rank}] generated {rp.nb_records()} records in {len(lens)} buffers, "
-        f"{arena.nbytes / 1e6:.0f} MB, {time.time() - t0:.1f}s")
-    d_arena = torch.from_numpy(arena).to(device)
-    nb_buf = len(lens)
-    seq_base = rank * nb_buf  # global analysis order: rank-major
-
-    eng = Engine(device=local, flags=_lib.NMG_F_DEFAULT, nb_threads=rp.nb_threads)
-    eng.set_objects(rp.table)
-    eng.set_device_buffers(d_arena.data_ptr(), offs, lens, ranks, acc, seq_base=seq_base)
-    samples_per_rank = int(lens.sum()) // RECORD_BYTES
-
-    # merge buffers for the timed RCCL reduces (dense arrays only; the tiny
-    # variable-length gathers run once after timing)
-    merge_bufs = []
-    if distributed:
-        for which, dt in ((_lib.NMG_ARR_SUM64, torch.int64), (_lib.NMG_ARR_MIN64, torch.int64),
-                          (_lib.NMG_ARR_MAX64, torch.int64), (_lib.NMG_ARR_HIST32, torch.int32)):
-            n = eng.array_size(which)
-            if n:
-                merge_bufs.append((which, torch.empty(n, dtype=dt, device=device)))
-
-    def step():
-        eng.reset()
-        eng.analyze()
-        if distributed:
-            eng.synchronize()
-            for which, t in merge_bufs:
-                eng.export_array(which, t.data_ptr())
-                if which == _lib.NMG_ARR_HIST32:
-                    reduce_u32_sum(t, dst=0)
-                else:
-                    reduce_u64(t, {0: "sum", 1: "min", 2: "max"}[which], dst=0)
+    w = Workload(args.workload, rank, device, distributed)
 
     def barrier():
         if distributed:
             dist.barrier()
         torch.cuda.synchronize(device)
-        eng.synchronize()
+        w.eng.synchronize()
 
-    for _ in range(args.warmup):
-        step()
-    barrier()
-    t_start = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    barrier()  # device sync; raises on a kernel-reported error
-    elapsed = time.perf_counter() - t_start
-    kernel_ms = eng.launch_times(min(args.steps, 64))  # HIP events on the engine stream
+    elapsed, steps = timed_run(w, args.steps, args.warmup, barrier)
+    attr_ms, total_ms = w.eng.kernel_times(min(steps, 64))  # HIP events on the engine stream
     if distributed:
         tt = torch.tensor([elapsed], dtype=torch.float64, device=device)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
-    ms_per_step = elapsed * 1e3 / args.steps
-    total_samples = samples_per_rank * world
-    value = total_samples / (elapsed / args.steps)
+    ms_per_step = elapsed * 1e3 / steps
+    value = w.samples * world / (elapsed / steps)
 
     # sanity: every record of the batch was decoded exactly once per step
-    g, ns, nf = eng.global_counters()
-    assert ns == samples_per_rank, (ns, samples_per_rank)
+    g, ns, nf = w.eng.global_counters()
+    assert ns == w.samples, (ns, w.samples)
 
     if distributed:
-        merge_engine(eng, dst=0)  # full merge once (dense + gathers) for the report
+        merge_engine(w.eng, dst=0)  # full merge once (dense + gathers) for the report
 
     if rank == 0:
-        avg_kernel_ms = float(np.mean(kernel_ms))
-        achieved = samples_per_rank * RECORD_BYTES / (avg_kernel_ms * 1e-3) / 1e9
-        traffic = None
-        pmc_path = os.path.join(ROOT, "profiles", f"pmc_{args.workload}.json")
-        if os.path.exists(pmc_path):
-            try:
-                traffic = json.load(open(pmc_path)).get("hbm_bytes_per_launch")
-            except Exception:
-                traffic = None
-        out = {
-            "metric": "PEBS samples/s analysed (device-resident)",
-            "value": value,
-            "unit": "samples/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": ms_per_step,
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "u64",
-            "data": "synthetic (seeded SURVEY 8(d) generator: Zipf objects, mem_lvl mix, 128 KiB buffers)",
-            "config": {
-                "workload": f"{args.workload}: {wl['desc']}",
-                "records_per_gpu": samples_per_rank,
-                "buffers_per_gpu": nb_buf,
-                "object_intervals": int(cfg.nb_intervals),
-                "table_entries": rp.table.nb_entries,
-                "threads": rp.nb_threads,
-                "parallelism": f"buffers sharded over {world} GPU(s), RCCL reduce of counters" if world > 1 else "1 GPU",
-            },
-            "roofline": {
-                "bound": "hbm",
-                "kernel": "nmg::attribute_kernel",
-                "achieved": achieved,
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBS,
-                "traffic": traffic,
-                "avg_kernel_ms": avg_kernel_ms,
-                "algorithmic_bytes_per_launch": samples_per_rank * RECORD_BYTES,
-            },
-        }
+        out = result_line(args, w, world, steps, ms_per_step, value, attr_ms, total_ms)
+        if world == 1 and args.secondary:
+            s = Workload(args.secondary, rank, device, False)
+
+            def sbar():
+                torch.cuda.synchronize(device)
+                s.eng.synchronize()
+
+            se, sn = timed_run(s, 0, 3, sbar)
+            sa, st = s.eng.kernel_times(min(sn, 64))
+            out["secondary"] = {
+                s.name: {"workload": WORKLOADS[s.name]["desc"], "value": s.samples / (se / sn), "unit": "samples/s",
+                         "ms_per_step": se * 1e3 / sn, "steps": sn,
+                         "attribute_kernel_ms": float(np.mean(sa)), "launch_ms": float(np.mean(st)),
+                         "roofline_frac": s.samples * RECORD_BYTES / (float(np.mean(sa)) * 1e-3) / 1e9 / HBM_PEAK_GBS}}
+            s.eng.close()
         if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(rp, args.cpu_sample_frac)
+            out["cpu_baseline"] = cpu_baseline(w.rp, args.cpu_records)
         print(json.dumps(out), flush=True)
     if distributed:
         dist.barrier()
         dist.destroy_process_group()
-    eng.close()
+    w.eng.close()
 
 
-def cpu_baseline(rp, frac, target_s=10.0, max_runs=40):
+def result_line(args, w, world, steps, ms_per_step, value, attr_ms, total_ms):
+    wl = WORKLOADS[w.name]
+    avg_attr = float(np.mean(attr_ms))
+    avg_total = float(np.mean(total_ms))
+    algo = w.samples * RECORD_BYTES
+    achieved = algo / (avg_attr * 1e-3) / 1e9
+    traffic = None
+    pmc_path = os.path.join(ROOT, "profiles", f"pmc_{w.name}.json")
+    if os.path.exists(pmc_path):
+        try:
+            traffic = json.load(open(pmc_path)).get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+    return {
+        "metric": "PEBS samples/s analysed (device-resident)",
+        "value": value,
+        "unit": "samples/s",
+        "n_gpus": world,
+        "steps": steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u64",
+        "data": "synthetic (seeded SURVEY 8(d) generator: Zipf objects, mem_lvl mix, 128 KiB buffers)",
+        "config": {
+            "workload": f"{w.name}: {wl['desc']}",
+            "records_per_gpu": w.samples,
+            "buffers_per_gpu": w.nb_buf,
+            "object_intervals": int(w.cfg.nb_intervals),
+            "table_entries": w.rp.table.nb_entries,
+            "threads": w.rp.nb_threads,
+            "parallelism": f"buffers sharded over {world} GPU(s), RCCL reduce of counters" if world > 1 else "1 GPU",
+        },
+        "roofline": {
+            "bound": "hbm",
+            "kernel": "nmg::attribute_kernel",
+            "achieved": achieved,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS,
+            "traffic": traffic,
+            "algorithmic_bytes_per_launch": algo,
+            "avg_kernel_ms": avg_attr,
+            "avg_launch_ms": avg_total,
+            "note": "achieved = 40 B per record / attribution-kernel time (HIP events); the launch adds the "
+                    "long-tail reduce kernel; traffic = PMC FETCH_SIZE + WRITE_SIZE per launch "
+                    f"(profiles/pmc_{w.name}.json, record stream corrected x2)",
+        },
+    }
+
+
+def cpu_baseline(rp, max_records, target_s=10.0, max_runs=40):
     """The CPU oracle (a single-threaded C restatement of the reference's
-    offline analysis loop, oracle/nmg_oracle.c) timed on this host on the
-    same workload: the first `frac` of the buffers, analysed repeatedly until
-    about `target_s` seconds of analysis time have accumulated (the whole c2
-    batch takes well under a second), rate = records / analysis seconds."""
+    offline analysis loop, oracle/nmg_oracle.c) timed on this host on a
+    bounded sample of the same workload: the first buffers (up to
+    `max_records` records) against the full object table, analysed
+    repeatedly until about `target_s` seconds of analysis time have
+    accumulated; rate = records / analysis seconds."""
     import tempfile
 
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -219,7 +272,13 @@ def cpu_baseline(rp, frac, target_s=10.0, max_runs=40):
 
     from numamma_amd.replay import Replay
 
-    n = max(1, int(len(rp.buffers) * frac))
+    n, recs = 0, 0
+    for b in rp.buffers:
+        if recs >= max_records:
+            break
+        recs += b.linear().shape[0] // RECORD_BYTES
+        n += 1
+    n = max(1, n)
     sub = Replay(rp.nb_threads, rp.table, rp.buffers[:n])
     runs, samples, secs = 0, 0, 0.0
     with tempfile.TemporaryDirectory() as d:
@@ -235,8 +294,8 @@ def cpu_baseline(rp, frac, target_s=10.0, max_runs=40):
         "unit": "samples/s",
         "cores": 1,
         "kind": "port",
-        "sample": f"{n} of {len(rp.buffers)} buffers ({samples // runs} records) analysed {runs}x, "
-                  f"{secs:.1f}s of analysis loop; single-threaded like the reference "
+        "sample": f"first {n} of {len(rp.buffers)} buffers ({samples // runs} records, full object table) analysed "
+                  f"{runs}x, {secs:.1f}s of analysis loop; single-threaded like the reference "
                   f"(global mutex, mem_analyzer.c:254); host has {os.cpu_count()} CPUs",
     }
 

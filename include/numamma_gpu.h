@@ -256,6 +256,9 @@ int nmg_set_buffer_counts(nmg_engine *h, uint32_t nb_buffers, const uint32_t *nb
 int nmg_last_analyze_ms(nmg_engine *h, float *ms);
 /* durations of up to n most recent launches (oldest first, max 64); returns the count */
 int nmg_get_launch_times(nmg_engine *h, float *ms, int n);
+/* the same launches split: the attribution kernel alone (attribute_ms) and the
+ * whole launch including the long-tail reduce (total_ms); returns the count */
+int nmg_get_kernel_times(nmg_engine *h, float *attribute_ms, float *total_ms, int n);
 
 /*
  * Report: the stdout text of mem_sampling_finalize + ma_finalize from

@@ -168,6 +168,7 @@ _SIGS = {
     "nmg_set_buffer_counts": (C.c_int, [H, C.c_uint32, u32p, u32p, u64p]),
     "nmg_last_analyze_ms": (C.c_int, [H, C.POINTER(C.c_float)]),
     "nmg_get_launch_times": (C.c_int, [H, C.POINTER(C.c_float), C.c_int]),
+    "nmg_get_kernel_times": (C.c_int, [H, C.POINTER(C.c_float), C.POINTER(C.c_float), C.c_int]),
     "nmg_report": (C.c_int, [H, C.POINTER(nmg_object_meta), C.POINTER(nmg_report_options), C.c_char_p]),
     "nmg_report_host": (C.c_int, [C.POINTER(nmg_host_results), C.POINTER(nmg_object_meta), C.POINTER(nmg_report_options), C.c_char_p]),
     "nmg_run_replay": (C.c_int, [C.c_char_p, C.c_char_p, C.c_char_p, C.c_char_p, C.c_int, C.c_uint32]),

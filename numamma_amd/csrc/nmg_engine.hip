@@ -86,6 +86,7 @@ struct nmg_engine {
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   static constexpr int kRing = 64;  // per-launch timing events (nmg_get_launch_times)
   hipEvent_t ring0[kRing] = {}, ring1[kRing] = {};
+  hipEvent_t ringm[kRing] = {};  // after the attribution kernel (before the log reduce)
   uint64_t nlaunch = 0;
   int num_cus = 256;
   int blocks_per_cu = 0;
@@ -124,10 +125,6 @@ struct nmg_engine {
   size_t tlog_bytes = 0;
   uint32_t* d_tlog_cnt = nullptr;
   size_t tlog_cnt_cap = 0;
-  unsigned long long* d_rlog = nullptr;  // partition-first lookup: routed samples (see Params::rlog)
-  size_t rlog_bytes = 0;
-  uint32_t* d_rcnt = nullptr;
-  size_t rcnt_cap = 0;
   size_t smatch_cap = 0;
   uint64_t nreset = 0;
 
@@ -255,12 +252,6 @@ static void free_counters(nmg_engine* h) {
   (void)hipFree(h->d_tlog_cnt);
   h->d_tlog_cnt = nullptr;
   h->tlog_cnt_cap = 0;
-  (void)hipFree(h->d_rlog);
-  h->d_rlog = nullptr;
-  h->rlog_bytes = 0;
-  (void)hipFree(h->d_rcnt);
-  h->d_rcnt = nullptr;
-  h->rcnt_cap = 0;
 }
 
 static void free_table(nmg_engine* h) {
@@ -348,6 +339,7 @@ extern "C" void nmg_destroy(nmg_engine* h) {
   for (int i = 0; i < nmg_engine::kRing; i++) {
     if (h->ring0[i]) (void)hipEventDestroy(h->ring0[i]);
     if (h->ring1[i]) (void)hipEventDestroy(h->ring1[i]);
+    if (h->ringm[i]) (void)hipEventDestroy(h->ringm[i]);
   }
   if (h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
@@ -403,7 +395,7 @@ struct BigLookup {
   std::vector<uint2> dir;         // [nb_fences << dir_log2]
 };
 
-static void build_big_lookup(const uint64_t* keys, uint32_t K, BigLookup& bl) {
+static void build_big_lookup(const uint64_t* keys, uint32_t K, bool no_dir, BigLookup& bl) {
   while (((uint64_t)K + (1u << bl.fence_log2) - 1) >> bl.fence_log2 > kMaxFences) bl.fence_log2++;
   const uint32_t S = 1u << bl.fence_log2;
   bl.nb_fences = (uint32_t)(((uint64_t)K + S - 1) >> bl.fence_log2);
@@ -426,8 +418,9 @@ static void build_big_lookup(const uint64_t* keys, uint32_t K, BigLookup& bl) {
     }
   }
   bl.shift.assign(bl.nb_fences, kShiftSearch);
-  // bucket-relative indices and counts are 16-bit: S <= 2^16
-  if (S == 1 || S > (1u << 16)) return;
+  // bucket-relative indices and counts are 16-bit: S <= 2^16 (larger
+  // buckets -- more than 4095 << 16 keys -- are binary-searched)
+  if (S == 1 || S > (1u << 16) || no_dir) return;
   bl.dir_log2 = bl.fence_log2 + 1;  // two slots per key
   const uint32_t D = 1u << bl.dir_log2;
   bl.dir.assign((size_t)bl.nb_fences << bl.dir_log2, make_uint2(0, 0));
@@ -561,7 +554,7 @@ extern "C" int nmg_set_objects(nmg_engine* h, const uint64_t* keys, const uint32
   h->nb_fences = h->fence_log2 = h->dir_log2 = 0;
   if (nb_keys > kLdsNodes) {
     BigLookup bl;
-    build_big_lookup(keys, nb_keys, bl);
+    build_big_lookup(keys, nb_keys, (h->flags & kDbgNoDir) != 0, bl);
     h->nb_fences = bl.nb_fences;
     h->fence_log2 = bl.fence_log2;
     h->dir_log2 = bl.dir_log2;
@@ -1124,10 +1117,11 @@ static int launch_attribution(nmg_engine* h, const uint8_t* data, const BufDesc*
   p.smatch = (h->flags & NMG_F_SAMPLE_MATCHES) ? h->d_smatch : nullptr;
   // dense LDS tables when the table is small enough (DESIGN.md "Kernels")
   int mode = (h->E <= kObjSlots ? kModeDenseObj : 0) | (h->hist_cells <= kDensePageCells ? kModeDensePage : 0);
-#ifndef NMG_NO_PACK_TAIL
   if (!(mode & kModeDenseObj) && h->d_pk64 && !(h->flags & kDbgNoPack)) {
-    // < 2^cbits samples in this launch (a SAMPLE record is 40 B); packed
-    // weights < 2^(64 - 2 cbits), so any entry's packed sum < 2^(64 - cbits)
+    // < 2^cbits packed samples in this launch (only SAMPLE records of at
+    // least 40 B are packed: the kernel keeps shorter ones, which the
+    // reference's byte cursor accepts, on the plain path); packed weights
+    // < 2^(64 - 2 cbits), so any entry's packed sum < 2^(64 - cbits)
     const uint32_t cbits = 64 - (uint32_t)__builtin_clzll(nbytes / kRecBytes + 1);
     if (2 * cbits < 64) {
       p.pk64 = h->d_pk64;
@@ -1135,10 +1129,8 @@ static int launch_attribution(nmg_engine* h, const uint8_t* data, const BufDesc*
       p.pk_wlim = 1ull << (64 - 2 * cbits);
     }
   }
-#endif
-#ifndef NMG_NO_TAIL_LOG
   if (!(mode & kModeDenseObj) && nb && grid <= kLogMaxGrid && (h->flags & NMG_F_MATCH_SAMPLES) &&
-      nbytes / kRecBytes < (1ull << 31)) {
+      nbytes / 8 < (1ull << 32)) {  // (u32 per-entry sums in tlog_reduce; records are >= 8 B)
     uint32_t rshift = 0;
     while ((((uint64_t)h->E + (1ull << rshift) - 1) >> rshift) > kLogParts) rshift++;
     const uint32_t parts = (uint32_t)(((uint64_t)h->E + (1ull << rshift) - 1) >> rshift);
@@ -1171,52 +1163,10 @@ static int launch_attribution(nmg_engine* h, const uint8_t* data, const BufDesc*
     p.tlog_rshift = rshift;
     p.tlog_parts = parts;
   }
-#endif
-  // partition-first lookup (large tables): ranges of 2^kRouteKeysLog2 keys
-  uint32_t route_kshift = 0;
-#ifdef NMG_ROUTE_DEFAULT
-  const bool route_req = true;
-#else
-  const bool route_req = (h->flags & kDbgRoute) != 0;
-#endif
-  if (!(mode & kModeDenseObj) && nb && !p.lds_nodes && route_req && (h->flags & NMG_F_MATCH_SAMPLES) &&
-      !(h->flags & (NMG_F_SAMPLE_MATCHES | NMG_F_OBJECT_LEVELS)) && grid <= kLogMaxGrid &&
-      h->fence_log2 < kRouteKeysLog2 && nbytes / kRecBytes < (1ull << 31)) {
-    const uint32_t rq = kRouteKeysLog2 - h->fence_log2;
-    const uint32_t parts = (h->nb_fences + (1u << rq) - 1) >> rq;
-    uint64_t cap = std::min<uint64_t>(1u << 16, 2 * (nbytes / kRecBytes) / ((uint64_t)grid * parts) + 16);
-    cap = std::min<uint64_t>(cap, (2ull << 30) / ((uint64_t)grid * parts * 32));
-    if (parts <= kRouteMaxParts && cap >= 4) {
-      const size_t need = (size_t)grid * parts * cap * 32;
-      if (need > h->rlog_bytes || (size_t)grid * parts > h->rcnt_cap) {
-        HIP_TRY(h, hipStreamSynchronize(h->stream));
-        if (need > h->rlog_bytes) {
-          (void)hipFree(h->d_rlog);
-          h->d_rlog = nullptr;
-          h->rlog_bytes = 0;
-          HIP_TRY(h, hipMalloc(&h->d_rlog, need));
-          h->rlog_bytes = need;
-        }
-        if ((size_t)grid * parts > h->rcnt_cap) {
-          (void)hipFree(h->d_rcnt);
-          h->d_rcnt = nullptr;
-          h->rcnt_cap = 0;
-          HIP_TRY(h, hipMalloc(&h->d_rcnt, (size_t)grid * parts * 4));
-          h->rcnt_cap = (size_t)grid * parts;
-        }
-      }
-      p.rlog = h->d_rlog;
-      p.rcnt = h->d_rcnt;
-      p.rcap = (uint32_t)cap;
-      p.rparts = parts;
-      p.rq_shift = rq;
-      route_kshift = h->fence_log2 + rq;
-      mode |= kModeRoute;
-    }
-  }
   const int slot = (int)(h->nlaunch % nmg_engine::kRing);
   if (!h->ring0[slot]) {
     HIP_TRY(h, hipEventCreate(&h->ring0[slot]));
+    HIP_TRY(h, hipEventCreate(&h->ringm[slot]));
     HIP_TRY(h, hipEventCreate(&h->ring1[slot]));
   }
   HIP_TRY(h, hipEventRecord(h->ring0[slot], h->stream));
@@ -1236,6 +1186,7 @@ static int launch_attribution(nmg_engine* h, const uint8_t* data, const BufDesc*
     } else {
       HIP_TRY(h, launch_attribute(false, mode, grid, h->stream, p));
     }
+    HIP_TRY(h, hipEventRecord(h->ringm[slot], h->stream));
     if (p.tlog) {  // sums the log per entry range, folds the packed counters
       TlogParams r;
       r.tlog = p.tlog;
@@ -1254,14 +1205,8 @@ static int launch_attribution(nmg_engine* h, const uint8_t* data, const BufDesc*
       const uint32_t blocks = (uint32_t)std::min<uint64_t>(2048, (2ull * h->E + 255) / 256);
       HIP_TRY(h, launch_unpack(blocks, h->stream, h->d_sum64, p.pk64, h->E, p.pk_shift));
     }
-    if (p.rlog) {  // routed samples: resolved per key range, then tallied per buffer
-      RouteParams rp;
-      rp.p = p;
-      rp.grid = grid;
-      rp.kshift = route_kshift;
-      HIP_TRY(h, launch_route(p.rparts, grid, h->stream, rp));
-    }
   }
+  if (!nb) HIP_TRY(h, hipEventRecord(h->ringm[slot], h->stream));
   HIP_TRY(h, hipEventRecord(h->ring1[slot], h->stream));
   h->nlaunch++;
   h->launched = true;
@@ -1343,6 +1288,20 @@ extern "C" int nmg_get_launch_times(nmg_engine* h, float* ms, int n) {
   for (int i = 0; i < cnt; i++) {  // the cnt most recent launches, oldest first
     const int slot = (int)((h->nlaunch - cnt + i) % nmg_engine::kRing);
     HIP_TRY(h, hipEventElapsedTime(&ms[i], h->ring0[slot], h->ring1[slot]));
+  }
+  return cnt;
+}
+
+extern "C" int nmg_get_kernel_times(nmg_engine* h, float* attribute_ms, float* total_ms, int n) {
+  if (!h || (n > 0 && (!attribute_ms || !total_ms))) return NMG_ERR_INVALID;
+  HIP_TRY(h, hipSetDevice(h->device));
+  HIP_TRY(h, hipStreamSynchronize(h->stream));
+  const int avail = (int)std::min<uint64_t>(h->nlaunch, nmg_engine::kRing);
+  const int cnt = std::min(n, avail);
+  for (int i = 0; i < cnt; i++) {
+    const int slot = (int)((h->nlaunch - cnt + i) % nmg_engine::kRing);
+    HIP_TRY(h, hipEventElapsedTime(&attribute_ms[i], h->ring0[slot], h->ringm[slot]));
+    HIP_TRY(h, hipEventElapsedTime(&total_ms[i], h->ring0[slot], h->ring1[slot]));
   }
   return cnt;
 }

@@ -23,16 +23,9 @@ constexpr uint64_t kHistSparse = ~0ull;
 constexpr uint32_t kPageSize = 4096;  // src/mem_analyzer.c:471
 
 constexpr uint64_t gsum_index(uint32_t access, uint32_t i) { return access * kGlobalSums + i; }
-#ifdef NMG_AOS_COUNTS
-// [E][2 access][count, weight]: a sample's two counters share one 32 B block
-constexpr uint64_t objcw_index(uint64_t e, uint32_t access, uint32_t w, uint64_t /*nb_entries*/) {
-  return 2 * kGlobalSums + e * 4 + uint64_t(access) * 2 + w;
-}
-#else
 constexpr uint64_t objcw_index(uint64_t e, uint32_t access, uint32_t w, uint64_t nb_entries) {
   return 2 * kGlobalSums + (uint64_t(access) * 2 + w) * nb_entries + e;
 }
-#endif
 
 // Error word: min over ((seq << 40) | (byte offset << 8) | code) so the first
 // failing record in analysis order wins, as the reference's abort() would.

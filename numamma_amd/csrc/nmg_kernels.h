@@ -36,11 +36,6 @@ constexpr uint32_t kObjSlots = 2048;           // entry -> (count, weight, first
 constexpr uint32_t kLogParts = 256;
 constexpr uint32_t kLogChunk = 4096;   // entries per LDS pass of tlog_reduce_kernel
 constexpr uint32_t kLogMaxGrid = 1024;  // attribution workgroups a log can serve
-// partition-first lookup (large tables): samples routed by fence range to
-// per-workgroup sub-logs, resolved per range from LDS by route_resolve_kernel
-constexpr uint32_t kRouteKeysLog2 = 9;   // keys per range: 512 (staged in LDS)
-constexpr uint32_t kRouteMaxParts = 2048;
-constexpr uint32_t kRouteEnt = 1536;     // entries of a range counted in LDS (the rest: global atomics)
 constexpr uint32_t kPageBuckets = 896;         // dense page cell -> count: 8-slot buckets
 constexpr uint32_t kPageSlots = kPageBuckets * 8;  // 7168 cells (56 KiB)
 constexpr uint32_t kObjBuckets = kObjSlots / 8;
@@ -54,14 +49,9 @@ constexpr uint32_t kTableWindows = 256;
 //                   kDensePageWindows windows (<= 1024 samples per cell each,
 //                   so a u16 cannot overflow into its neighbour)
 constexpr int kModeDenseObj = 1, kModeDensePage = 2;
-constexpr int kModeRoute = 4;  // partition-first lookup (hashed object mode only): Params::rlog is set
 constexpr uint32_t kDensePageCells = kPageSlots * 4;  // the page table's 56 KiB as u16 cells
 constexpr uint32_t kDensePageWindows = 62;
-#ifdef NMG_NO_PACK_OBJ
-constexpr bool kPackObj = false;
-#else
 constexpr bool kPackObj = true;
-#endif
 constexpr uint32_t kPackShift = 44;  // kModeDenseObj: per-entry count << 44 | weight sum
 static_assert((uint64_t)kDensePageWindows * kWG < (1ull << (64 - kPackShift)), "packed count");
 static_assert(kDensePageWindows * kWG < 65536u, "u16 page counts");
@@ -75,7 +65,7 @@ constexpr uint32_t kDbgNoTables = 0x800;   // lookup only: no per-object / per-p
 constexpr uint32_t kDbgTiming = 0x1000;    // per-wave phase cycle counts (tools/phase_timing.py)
 constexpr uint32_t kDbgTinyLog = 0x2000;   // long-tail sub-logs of 2 records: exercises the overflow path (tests)
 constexpr uint32_t kDbgNoPack = 0x4000;    // overflow through plain atomics, not packed ones (tests)
-constexpr uint32_t kDbgRoute = 0x8000;     // partition-first lookup for large tables (opt-in while measured)
+constexpr uint32_t kDbgNoDir = 0x8000;     // large tables: no fence-bucket directory, binary search only (tests)
 constexpr int kTimingWords = 24;           // per wave: load+check, barrier, process, rest, total, windows, -, -,
                                            // then (wave 0) 8 x 2 words of window trace
 
@@ -160,18 +150,6 @@ struct Params {
   unsigned long long* tlog;  // [grid][tlog_parts][tlog_cap][3] u64; null: off
   uint32_t* tlog_cnt;        // [grid][tlog_parts] records written
   uint32_t tlog_cap, tlog_rshift, tlog_parts;
-  // partition-first lookup: routed samples {schedule index | matched << 31,
-  // offset, ts, addr, weight} (32 B) in sub-log (workgroup, fence >> rq_shift)
-  unsigned long long* rlog;  // [grid][rparts][rcap][4] u64; null: off
-  uint32_t* rcnt;            // [grid][rparts] records written
-  uint32_t rcap, rparts, rq_shift;
-};
-
-// route_resolve_kernel / route_tally_kernel
-struct RouteParams {
-  Params p;
-  uint32_t grid;    // attribution workgroups (sources of the sub-logs)
-  uint32_t kshift;  // keys per range = 2^kshift (fence_log2 + rq_shift)
 };
 
 // tlog_reduce_kernel (long-tail log, see Params::tlog)
@@ -210,6 +188,5 @@ hipError_t launch_tlog_reduce(uint32_t grid, hipStream_t s, const TlogParams& r)
 hipError_t launch_unpack(uint32_t grid, hipStream_t s, uint64_t* sum64, unsigned long long* pk64,
                          uint32_t nb_entries, uint32_t shift);
 hipError_t launch_reset(uint32_t grid, hipStream_t s, const ResetParams& r);
-hipError_t launch_route(uint32_t parts, uint32_t grid, hipStream_t s, const RouteParams& r);
 
 }  // namespace nmg

@@ -90,25 +90,10 @@ __device__ __forceinline__ void set_error(Params& p, uint64_t seq, uint32_t off,
 
 // Descend `levels` levels of an Eytzinger tree (node i has children 2i, 2i+1)
 // from the root and return the index below the last level: one 8 B LDS read
-// per level.  (NMG_EYTZ_GROUPED reads node i, its children and grandchildren
-// together -- one round trip per three levels -- but the extra LDS bytes and
-// bank conflicts cost more than the shorter chain saves.)  Reads stay below
-// 2^levels.
+// per level (reading three levels per round trip was measured slower: more
+// LDS bytes and bank conflicts).  Reads stay below 2^levels.
 __device__ __forceinline__ uint32_t eytz_descend(const uint64_t* F, uint32_t levels, uint64_t addr) {
   uint32_t i = 1;
-#ifdef NMG_EYTZ_GROUPED  // measured slower on c2 (0.196 vs 0.182 ms): more LDS bytes and conflicts
-  for (; levels >= 3; levels -= 3) {
-    const uint64_t k0 = F[i];
-    const ulonglong2 k1 = *reinterpret_cast<const ulonglong2*>(F + 2 * i);
-    const ulonglong2 k2a = *reinterpret_cast<const ulonglong2*>(F + 4 * i);
-    const ulonglong2 k2b = *reinterpret_cast<const ulonglong2*>(F + 4 * i + 2);
-    const bool b0 = k0 <= addr;
-    const bool b1 = (b0 ? k1.y : k1.x) <= addr;
-    const uint64_t kg = b0 ? (b1 ? k2b.y : k2b.x) : (b1 ? k2a.y : k2a.x);
-    const bool b2 = kg <= addr;
-    i = 8 * i + 4 * (uint32_t)b0 + 2 * (uint32_t)b1 + (uint32_t)b2;
-  }
-#endif
   for (; levels > 0; levels--) i = 2 * i + (F[i] <= addr ? 1u : 0u);
   return i;
 }
@@ -164,7 +149,9 @@ __device__ __forceinline__ uint32_t lower_key(const Params& p, const uint64_t* s
   const uint32_t b = (((idx - (1u << d)) * 2 + 1) << (kFenceLevels - 1 - d)) - 1;
   if (b >= p.nb_fences) return p.nb_keys - 1;  // ~0 padding: addr == UINT64_MAX
   const uint32_t k0 = b << p.fence_log2;
-  if (p.dir_log2 == 0) return k0;  // one key per fence
+  if (p.fence_log2 == 0) return k0;  // one key per fence
+  // (buckets without a directory -- more than 2^16 keys per bucket, or the
+  // kDbgNoDir switch -- have shift kShiftSearch: binary search below)
   const uint32_t kend = min(k0 + (1u << p.fence_log2), p.nb_keys);
   const uint32_t sh = s_shift[b];
   uint32_t lo, n;  // answer in [lo, lo + n): keys[lo] <= addr known
@@ -438,36 +425,15 @@ __device__ __forceinline__ bool tlog_append(const Params& p, WgCounters& wc, uin
   return true;
 }
 
-// Partition-first lookup (large tables): the sample goes to this workgroup's
-// sub-log of its fence range instead of being looked up here (only the LDS
-// fence tree is walked).  False when it cannot be routed -- below the first
-// key, or the sub-log is full -- and is then looked up directly.
-__device__ __forceinline__ bool route_sample(const Params& p, const Lookup& L, uint32_t* s_rcur, uint32_t desc,
-                                             uint32_t off, uint64_t ts, uint64_t addr, uint64_t w) {
-  const uint32_t idx = fence_node(L.fences, addr);
-  if (idx == 0) return false;
-  const uint32_t d = 31 - __builtin_clz(idx);
-  const uint32_t b = (((idx - (1u << d)) * 2 + 1) << (kFenceLevels - 1 - d)) - 1;
-  if (b >= p.nb_fences) return false;
-  const uint32_t q = b >> p.rq_shift;
-  const uint32_t k = atomicAdd(&s_rcur[q], 1u);
-  if (k >= p.rcap) return false;
-  uint4* r = reinterpret_cast<uint4*>(p.rlog + ((uint64_t(blockIdx.x) * p.rparts + q) * p.rcap + k) * 4);
-  r[0] = make_uint4(desc, off, uint32_t(ts), uint32_t(ts >> 32));
-  r[1] = make_uint4(uint32_t(addr), uint32_t(addr >> 32), uint32_t(w), uint32_t(w >> 32));
-  return true;
-}
-
 // Process one decoded record (`valid` = it is a SAMPLE).  Every lane of the
 // wave calls this together (wave-level reductions inside); vmask / fmask are
 // the wave's SAMPLE and matched lanes.
 template <int MODE>
 __device__ __forceinline__ void process_sample(Params& p, WgCounters& wc, LaneAcc& acc, const Lookup& L,
-                                               bool valid, uint64_t ts, uint64_t addr,
+                                               bool valid, bool shortrec, uint64_t ts, uint64_t addr,
                                                uint64_t w, uint64_t dsrc, uint32_t access,
                                                uint32_t th, uint64_t seq, uint32_t off, uint64_t rbase,
-                                               uint64_t& vmask, uint64_t& fmask, const SpecDir& sp,
-                                               uint32_t* s_rcur, uint32_t rdesc) {
+                                               uint64_t& vmask, uint64_t& fmask, const SpecDir& sp) {
   const uint32_t lvl = uint32_t(dsrc >> 5) & 0x3fff;  // data_src.mem_lvl
   // ---- global counters: update_counters(global_counters, ...) (mem_sampling.c:882)
   vmask = __ballot(valid);
@@ -516,9 +482,7 @@ __device__ __forceinline__ void process_sample(Params& p, WgCounters& wc, LaneAc
   // ---- __match_sample (mem_sampling.c:594-673)
   Match m;
   m.e = -1;
-  // (routed samples are matched by route_resolve_kernel and tallied by route_tally_kernel)
-  const bool routed = (MODE & kModeRoute) && valid && route_sample(p, L, s_rcur, rdesc, off, ts, addr, w);
-  if (valid && !routed) m = find_entry(p, L, addr, ts, sp);
+  if (valid) m = find_entry(p, L, addr, ts, sp);
   const int64_t e = m.e;
   fmask = __ballot(e >= 0);
   // dump modes: every SAMPLE record's match at its arena position (host
@@ -529,7 +493,7 @@ __device__ __forceinline__ void process_sample(Params& p, WgCounters& wc, LaneAc
   // only on its second sample -- a doorkeeper bitset -- was measured slower at
   // 1M intervals: the per-sample bit test costs more than the flushes it saves.)
   // (with packing, a slot only sums packable weights: its flush is packed too)
-  const bool pk = !(MODE & kModeDenseObj) && p.pk64 && w < p.pk_wlim;
+  const bool pk = !(MODE & kModeDenseObj) && p.pk64 && w < p.pk_wlim && !shortrec;
   const int os = (MODE & kModeDenseObj) ? (int)e : ((p.pk64 && !pk) ? -1 : obj_slot(wc, (uint32_t)e));
   const unsigned long long ord = (seq << 32) | off;  // first match in analysis order (quirk Q7)
   if ((MODE & kModeDenseObj) && w < kLaneMaxWeight && kPackObj) {
@@ -708,20 +672,9 @@ __device__ __forceinline__ void load_rec(const uint8_t* base, uint64_t pos, uint
   if (pos + kRecBytes <= len) {
     const uint32_t odd = uint32_t(pos >> 3) & 1;
     const uint8_t* q = base + pos;
-#ifdef NMG_NT_LOADS
-    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-    typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-    const u32x4 a = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(q + (odd ? 8 : 0)));
-    const u32x4 b = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(q + (odd ? 24 : 16)));
-    const u32x2 c = __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(q + (odd ? 0 : 32)));
-    r.x = make_uint4(a.x, a.y, a.z, a.w);
-    r.y = make_uint4(b.x, b.y, b.z, b.w);
-    r.z = make_uint2(c.x, c.y);
-#else
     r.x = *reinterpret_cast<const uint4*>(q + (odd ? 8 : 0));
     r.y = *reinterpret_cast<const uint4*>(q + (odd ? 24 : 16));
     r.z = *reinterpret_cast<const uint2*>(q + (odd ? 0 : 32));
-#endif
   } else {
     r.x = make_uint4(0, 0, 0, 0);
     r.y = make_uint4(0, 0, 0, 0);
@@ -813,9 +766,6 @@ __global__ __launch_bounds__(kWG, 1) void attribute_kernel(Params p) {
   uint4* const s_nodes = s_tab + (kLdsNodes + 1) / 2;                    // after 8 KiB of keys
   uint2* const s_ninfo = reinterpret_cast<uint2*>(s_tab + (kLdsNodes + 1) * 5 / 2);  // after 40 KiB
   uint8_t* const s_shift = reinterpret_cast<uint8_t*>(s_tab + (kMaxFences + 1) / 2);  // after 32 KiB
-  // route sub-log cursors, after the fences and shifts (large tables only)
-  uint32_t* const s_rcur = reinterpret_cast<uint32_t*>(s_tab + (kMaxFences + 1) / 2 + (kMaxFences + 1) / 16);
-  static_assert(((kMaxFences + 1) / 2 + (kMaxFences + 1) / 16) * 16 + kRouteMaxParts * 4 <= kTabBytes, "route cursors");
   if (p.lds_nodes) {
     const uint32_t n = 1u << p.elevels;
     for (uint32_t i = tid; i < n; i += kWG) s_fences[i] = p.efences[i];
@@ -834,9 +784,6 @@ __global__ __launch_bounds__(kWG, 1) void attribute_kernel(Params p) {
   constexpr bool kLog = !(MODE & kModeDenseObj);  // the long-tail log serves the hashed object mode
   if (kLog && p.tlog)
     for (uint32_t i = tid; i < kLogParts; i += kWG) wc.tcur[i] = 0;
-  constexpr bool kRoute = (MODE & kModeRoute) != 0;
-  if (kRoute)
-    for (uint32_t i = tid; i < p.rparts; i += kWG) s_rcur[i] = 0;
   if (tid < 3) s_flags[tid] = 0;
   __syncthreads();
   const Lookup L{s_fences, s_nodes, s_ninfo, s_shift};
@@ -849,8 +796,6 @@ __global__ __launch_bounds__(kWG, 1) void attribute_kernel(Params p) {
   if (r0 >= r1) {
     if (kLog && p.tlog)
       for (uint32_t i = tid; i < p.tlog_parts; i += kWG) p.tlog_cnt[uint64_t(blockIdx.x) * p.tlog_parts + i] = 0;
-    if (kRoute)
-      for (uint32_t i = tid; i < p.rparts; i += kWG) p.rcnt[uint64_t(blockIdx.x) * p.rparts + i] = 0;
     return;
   }
   uint32_t idx = r0;
@@ -870,11 +815,7 @@ __global__ __launch_bounds__(kWG, 1) void attribute_kernel(Params p) {
   uint32_t ns0 = 0, nf0 = 0, ns1 = 0, nf1 = 0;  // per-buffer tallies: buffer idx, idx + 1
   uint64_t tacc[4] = {0, 0, 0, 0}, t_start = 0, t0 = 0, t1 = 0;
   if (TIMING) t_start = t0 = stamp();
-#ifndef NMG_NO_SPEC_DIR
   constexpr bool kSpec = !(MODE & kModeDenseObj);  // large tables come with the hashed object mode
-#else
-  constexpr bool kSpec = false;
-#endif
   SpecDir sp;
   sp.addr = 0;
   sp.idx = 0;
@@ -913,13 +854,13 @@ __global__ __launch_bounds__(kWG, 1) void attribute_kernel(Params p) {
     Rec rec = r;
     bool valid;
     uint64_t rseq, rbase;
-    uint32_t roff, rdesc;
+    uint32_t roff;
+    bool shortrec = false;  // a SAMPLE record shorter than 40 B (slow path only)
     if (!(f & 1)) {
       valid = wl.cand && uint32_t(r.hdr) == kSampleType;
       rseq = wl.in1 ? d1.seq : d0.seq;
       rbase = wl.in1 ? d1.offset : d0.offset;
       roff = wl.pos;
-      rdesc = wl.in1 ? idx + 1 : idx;
       // ---- fast path: one record per lane
       if (wl.n1) {
         nidx = idx + 1;
@@ -966,7 +907,10 @@ __global__ __launch_bounds__(kWG, 1) void attribute_kernel(Params p) {
           if (size & 7) { err = kErrUnaligned; break; }  // perf records are 8-byte multiples
           if (uint32_t(h) == kSampleType) {
             if (q0 + kRecBytes > len || q0 + size > len) { err = kErrTruncated; break; }
-            if (lane == 0) s_list[n] = (uint32_t)q0;
+            // (offsets are 8-aligned: bit 0 marks a SAMPLE shorter than 40 B,
+            // which the reference's byte cursor accepts; it stays out of the
+            // packed long-tail counters, whose bound counts 40 B records)
+            if (lane == 0) s_list[n] = (uint32_t)q0 | (size < kRecBytes ? 1u : 0u);
             n++;
           }
           q0 += size;  // non-SAMPLE records are skipped by their size (:918)
@@ -988,9 +932,10 @@ __global__ __launch_bounds__(kWG, 1) void attribute_kernel(Params p) {
       }
       valid = (uint32_t)tid < n;
       roff = valid ? s_list[tid] : 0;
+      shortrec = (roff & 1u) != 0;
+      roff &= ~1u;
       rseq = d0.seq;
       rbase = d0.offset;
-      rdesc = idx;
       RawRec rr;
       load_rec(base, roff, valid ? len : 0, rr);
       rec = decode_rec(rr, roff);
@@ -1024,9 +969,9 @@ __global__ __launch_bounds__(kWG, 1) void attribute_kernel(Params p) {
     }
     uint64_t vm = 0, fm = 0;
     if (!(p.flags & kDbgLoadOnly))
-      process_sample<MODE>(p, wc, acc, L, valid, rec.ts, rec.addr, rec.w, rec.dsrc, d0.access, d0.thread_rank, rseq, roff,
-                           rbase, vm, fm, sp, s_rcur, rdesc);
-    if (kSpec && !kRoute && !p.lds_nodes && (p.flags & NMG_F_MATCH_SAMPLES)) {
+      process_sample<MODE>(p, wc, acc, L, valid, shortrec, rec.ts, rec.addr, rec.w, rec.dsrc, d0.access, d0.thread_rank, rseq, roff,
+                           rbase, vm, fm, sp);
+    if (kSpec && !p.lds_nodes && (p.flags & NMG_F_MATCH_SAMPLES)) {
       // start the next window's lookup: its record (loaded above, arrived
       // during this window's lookups) -> fence node -> directory slot load,
       // in flight across the flush and the barrier.  Used when the record
@@ -1106,13 +1051,10 @@ __global__ __launch_bounds__(kWG, 1) void attribute_kernel(Params p) {
     }
     if (idx >= r1) break;  // the loop's only exit, after the state update
   }
-  if (kLog && (p.tlog || kRoute)) {  // the sub-logs' fill (every append of this workgroup is done)
+  if (kLog && p.tlog) {  // the sub-logs' fill (every append of this workgroup is done)
     __syncthreads();
-    if (p.tlog)
-      for (uint32_t i = tid; i < p.tlog_parts; i += kWG)
-        p.tlog_cnt[uint64_t(blockIdx.x) * p.tlog_parts + i] = min(wc.tcur[i], p.tlog_cap);
-    if (kRoute)
-      for (uint32_t i = tid; i < p.rparts; i += kWG) p.rcnt[uint64_t(blockIdx.x) * p.rparts + i] = min(s_rcur[i], p.rcap);
+    for (uint32_t i = tid; i < p.tlog_parts; i += kWG)
+      p.tlog_cnt[uint64_t(blockIdx.x) * p.tlog_parts + i] = min(wc.tcur[i], p.tlog_cap);
   }
   if (TIMING && lane == 0) {
     unsigned long long* o = p.dbg + (uint64_t(blockIdx.x) * (kWG / 64) + tid / 64) * kTimingWords;
@@ -1236,219 +1178,6 @@ __global__ __launch_bounds__(1024, 1) void tlog_reduce_kernel(TlogParams r) {
   }
 }
 
-// Partition-first lookup, pass B: workgroup q owns key range q (2^kshift keys:
-// those of 2^rq_shift fence buckets, so every routed sample's lower-bound key
-// is inside it) and that range's entries.  It stages the keys and node
-// records in LDS, reads the range's sub-log of every attribution workgroup,
-// and matches each sample from LDS (older entries of reused addresses from
-// global memory); object counters and page cells are summed in LDS and
-// published once, first ordinals too.  A matched record gets bit 31 of its
-// schedule index set, for route_tally_kernel.
-__global__ __launch_bounds__(1024, 1) void route_resolve_kernel(RouteParams rp) {
-  __shared__ uint64_t s_keys[1u << kRouteKeysLog2];
-  __shared__ uint4 s_node[(1u << kRouteKeysLog2) * 4];
-  __shared__ uint32_t s_cnt[2][kRouteEnt];
-  __shared__ unsigned long long s_wt[2][kRouteEnt];
-  __shared__ unsigned long long s_ord[kRouteEnt];
-  __shared__ uint4 s_pkey4[kPageSlots / 4];
-  __shared__ unsigned int s_pcnt[kPageSlots];
-  __shared__ uint32_t s_pre[kLogMaxGrid + 1];
-  Params p = rp.p;
-  const uint32_t q = blockIdx.x, tid = threadIdx.x;
-  const uint32_t k0 = q << rp.kshift, k1 = min(k0 + (1u << rp.kshift), p.nb_keys);
-  const uint32_t nk = k1 - k0;
-  for (uint32_t i = tid; i < nk; i += 1024) {
-    s_keys[i] = p.keys[k0 + i];
-    const uint4* r = reinterpret_cast<const uint4*>(p.nodes + k0 + i);
-    s_node[4 * i] = r[0];
-    s_node[4 * i + 1] = r[1];
-    s_node[4 * i + 2] = r[2];
-    s_node[4 * i + 3] = r[3];
-  }
-  for (uint32_t j = tid; j < kRouteEnt; j += 1024) {
-    s_cnt[0][j] = s_cnt[1][j] = 0;
-    s_wt[0][j] = s_wt[1][j] = 0;
-    s_ord[j] = ~0ull;
-  }
-  for (uint32_t i = tid; i < kPageSlots / 4; i += 1024) s_pkey4[i] = make_uint4(kEmpty32, kEmpty32, kEmpty32, kEmpty32);
-  for (uint32_t i = tid; i < kPageSlots; i += 1024) s_pcnt[i] = 0;
-  for (uint32_t w = tid; w < rp.grid; w += 1024) s_pre[w + 1] = p.rcnt[uint64_t(w) * p.rparts + q];
-  __syncthreads();
-  if (tid < 64) {  // prefix over the source workgroups (as in tlog_reduce_kernel)
-    const uint32_t per = (rp.grid + 63) / 64, b = min(tid * per, rp.grid), e = min(b + per, rp.grid);
-    uint32_t sum = 0;
-    for (uint32_t w = b; w < e; w++) sum += s_pre[w + 1];
-    uint32_t incl = sum;
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t t = __shfl_up(incl, o, 64);
-      if ((int)tid >= o) incl += t;
-    }
-    uint32_t run = incl - sum;
-    for (uint32_t w = b; w < e; w++) {
-      run += s_pre[w + 1];
-      s_pre[w + 1] = run;
-    }
-    if (tid == 0) s_pre[0] = 0;
-  }
-  __syncthreads();
-  // entries of the range: contiguous, node by node (newest first)
-  const uint32_t e0 = s_node[2].w, e1 = s_node[4 * (nk - 1) + 2].w + s_node[4 * (nk - 1) + 3].x;
-  const uint32_t ne = min(e1 - e0, kRouteEnt);
-  const uint32_t total = s_pre[rp.grid];
-  constexpr int kU = 4;  // records per thread in flight
-  for (uint32_t i0 = tid; i0 < total; i0 += kU * 1024) {
-  uint4* recs[kU];
-  uint4 xs[kU], ys[kU];
-  BufDesc dscs[kU];
-#pragma unroll
-  for (int u = 0; u < kU; u++) {
-    const uint32_t i = i0 + u * 1024;
-    recs[u] = nullptr;
-    if (i >= total) continue;
-    uint32_t lo = 0, hi = rp.grid;
-    while (hi - lo > 1) {
-      const uint32_t mid = (lo + hi) >> 1;
-      if (s_pre[mid] <= i) lo = mid;
-      else hi = mid;
-    }
-    recs[u] = reinterpret_cast<uint4*>(p.rlog + ((uint64_t(lo) * p.rparts + q) * p.rcap + (i - s_pre[lo])) * 4);
-    xs[u] = recs[u][0];
-    ys[u] = recs[u][1];
-  }
-#pragma unroll
-  for (int u = 0; u < kU; u++)
-    if (recs[u]) dscs[u] = p.sbufs[xs[u].x];
-#pragma unroll
-  for (int u = 0; u < kU; u++) {
-    if (!recs[u]) continue;
-    uint4* rec = recs[u];
-    const uint4 x = xs[u], y = ys[u];
-    const uint32_t desc = x.x, off = x.y;
-    const uint64_t ts = u64of(x.z, x.w), addr = u64of(y.x, y.y), w = u64of(y.z, y.w);
-    uint32_t k = 0, n = nk;  // largest key <= addr (keys[k0] <= addr: the fence of its bucket)
-    while (n > 1) {
-      const uint32_t half = n >> 1;
-      const bool le = s_keys[k + half] <= addr;
-      k = le ? k + half : k;
-      n = le ? n - half : half;
-    }
-    const uint4 a = s_node[4 * k], b = s_node[4 * k + 1], c = s_node[4 * k + 2], d = s_node[4 * k + 3];
-    Match m;
-    m.e = -1;
-    if (entry_match(a, b, addr, ts)) {
-      m.e = c.w;
-      m.baddr = u64of(a.x, a.y);
-      m.hist = u64of(c.x, c.y);
-    } else if (d.x > 1) {
-      match_older(p, c.w, d.x, addr, ts, m);
-    }
-    if (m.e < 0) continue;
-    reinterpret_cast<uint32_t*>(rec)[0] = desc | 0x80000000u;
-    const BufDesc& dsc = dscs[u];
-    const uint32_t acc = dsc.access, th = dsc.thread_rank;
-    const unsigned long long ord = (dsc.seq << 32) | off;
-    const uint32_t e = (uint32_t)m.e, j = e - e0;
-    if (e >= e0 && j < ne) {
-      atomicAdd(&s_cnt[acc][j], 1u);
-      if (w) atomicAdd(&s_wt[acc][j], (unsigned long long)w);
-      if (ord < s_ord[j]) atomicMin(&s_ord[j], ord);
-    } else {
-      atomicAdd(reinterpret_cast<unsigned long long*>(p.sum64 + objcw_index(e, acc, 0, p.nb_entries)), 1ull);
-      if (w)
-        atomicAdd(reinterpret_cast<unsigned long long*>(p.sum64 + objcw_index(e, acc, 1, p.nb_entries)),
-                  (unsigned long long)w);
-      atomicMin(reinterpret_cast<unsigned long long*>(p.min64 + 36 + e), ord);
-    }
-    if (p.flags & NMG_F_PAGE_HIST) {
-      const uint32_t page = uint32_t(int(uint64_t(addr - m.baddr) / kPageSize));
-      if (m.hist != kHistSparse) {
-        const uint64_t cell = uint64_t(th) * p.hist_cells + m.hist + page;
-        const int ps = page_slot_at(s_pkey4, (uint32_t)cell);
-        if (ps >= 0) atomicAdd(&s_pcnt[ps], 1u);
-        else atomicAdd(p.hist + cell, 1u);
-      } else {
-        const uint32_t sidx = p.entries[e].sidx;
-        if (sidx != ~0u) sparse_add(p, sparse_key(sidx, th, page), dsc.seq, off, 1u);
-      }
-    }
-  }
-  }
-  __syncthreads();
-  // publish: this workgroup is the only writer of its entries' words now
-  for (uint32_t j = tid; j < ne; j += 1024) {
-    const uint64_t e = e0 + j;
-    for (uint32_t a = 0; a < 2; a++) {
-      if (s_cnt[a][j]) p.sum64[objcw_index(e, a, 0, p.nb_entries)] += s_cnt[a][j];
-      if (s_wt[a][j]) p.sum64[objcw_index(e, a, 1, p.nb_entries)] += s_wt[a][j];
-    }
-    if (s_ord[j] < p.min64[36 + e]) p.min64[36 + e] = s_ord[j];
-  }
-  const unsigned int* pkey = reinterpret_cast<const unsigned int*>(s_pkey4);
-  for (uint32_t i = tid; i < kPageSlots; i += 1024)
-    if (pkey[i] != kEmpty32) atomicAdd(p.hist + pkey[i], s_pcnt[i]);
-}
-
-// Partition-first lookup, pass C: attribution workgroup w counts the matched
-// samples among those it routed, per buffer (mem_sampling.c:921-926).
-__global__ __launch_bounds__(1024, 1) void route_tally_kernel(RouteParams rp) {
-  constexpr uint32_t kDescs = 4096;
-  __shared__ uint32_t s_pre[kRouteMaxParts + 1];
-  __shared__ uint32_t s_found[kDescs];
-  const Params& p = rp.p;
-  const uint32_t w = blockIdx.x, tid = threadIdx.x;
-  const uint32_t r0 = p.ranges[w], nd = p.ranges[w + 1] - r0;
-  for (uint32_t j = tid; j < kDescs; j += 1024) s_found[j] = 0;
-  for (uint32_t q = tid; q < p.rparts; q += 1024) s_pre[q + 1] = p.rcnt[uint64_t(w) * p.rparts + q];
-  __syncthreads();
-  if (tid < 64) {
-    const uint32_t per = (p.rparts + 63) / 64, b = min(tid * per, p.rparts), e = min(b + per, p.rparts);
-    uint32_t sum = 0;
-    for (uint32_t q = b; q < e; q++) sum += s_pre[q + 1];
-    uint32_t incl = sum;
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t t = __shfl_up(incl, o, 64);
-      if ((int)tid >= o) incl += t;
-    }
-    uint32_t run = incl - sum;
-    for (uint32_t q = b; q < e; q++) {
-      run += s_pre[q + 1];
-      s_pre[q + 1] = run;
-    }
-    if (tid == 0) s_pre[0] = 0;
-  }
-  __syncthreads();
-  const uint32_t total = s_pre[p.rparts];
-  constexpr int kU = 8;  // records per thread in flight
-  for (uint32_t i0 = tid; i0 < total; i0 += kU * 1024) {
-    uint32_t vs[kU];
-#pragma unroll
-    for (int u = 0; u < kU; u++) {
-      const uint32_t i = i0 + u * 1024;
-      vs[u] = 0;
-      if (i >= total) continue;
-      uint32_t lo = 0, hi = p.rparts;
-      while (hi - lo > 1) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (s_pre[mid] <= i) lo = mid;
-        else hi = mid;
-      }
-      vs[u] = reinterpret_cast<const uint32_t*>(
-          p.rlog + ((uint64_t(w) * p.rparts + lo) * p.rcap + (i - s_pre[lo])) * 4)[0];
-    }
-#pragma unroll
-    for (int u = 0; u < kU; u++) {
-      const uint32_t v = vs[u];
-      if (!(v >> 31)) continue;
-      const uint32_t desc = v & 0x7fffffffu, j = desc - r0;
-      if (j < min(nd, kDescs)) atomicAdd(&s_found[j], 1u);
-      else atomicAdd(p.bufcnt + p.nb_bufs + p.sbufs[desc].pad, 1u);
-    }
-  }
-  __syncthreads();
-  for (uint32_t j = tid; j < min(nd, kDescs); j += 1024)
-    if (s_found[j]) atomicAdd(p.bufcnt + p.nb_bufs + p.sbufs[r0 + j].pad, s_found[j]);
-}
-
 // Adds the launch's packed long-tail object counters into sum64 and clears
 // them (same stream, after attribute_kernel).
 __global__ __launch_bounds__(256) void unpack_kernel(uint64_t* sum64, unsigned long long* pk64, uint32_t nb_entries,
@@ -1491,14 +1220,10 @@ __global__ __launch_bounds__(256) void reset_kernel(ResetParams r) {
 typedef void (*AttributeKernel)(Params);
 
 hipError_t launch_attribute(bool timing, int mode, uint32_t grid, hipStream_t s, const Params& p) {
-  // (routing is built only into the hashed object modes: 5 and 7 never run)
-  static const AttributeKernel k[2][8] = {
-      {attribute_kernel<false, 0>, attribute_kernel<false, 1>, attribute_kernel<false, 2>, attribute_kernel<false, 3>,
-       attribute_kernel<false, 4>, attribute_kernel<false, 1>, attribute_kernel<false, 6>, attribute_kernel<false, 3>},
-      {attribute_kernel<true, 0>, attribute_kernel<true, 1>, attribute_kernel<true, 2>, attribute_kernel<true, 3>,
-       attribute_kernel<true, 4>, attribute_kernel<true, 1>, attribute_kernel<true, 6>, attribute_kernel<true, 3>}};
-  if ((mode & kModeRoute) && (mode & kModeDenseObj)) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k[timing ? 1 : 0][mode & 7], dim3(grid), dim3(kWG), 0, s, p);
+  static const AttributeKernel k[2][4] = {
+      {attribute_kernel<false, 0>, attribute_kernel<false, 1>, attribute_kernel<false, 2>, attribute_kernel<false, 3>},
+      {attribute_kernel<true, 0>, attribute_kernel<true, 1>, attribute_kernel<true, 2>, attribute_kernel<true, 3>}};
+  hipLaunchKernelGGL(k[timing ? 1 : 0][mode & 3], dim3(grid), dim3(kWG), 0, s, p);
   return hipGetLastError();
 }
 
@@ -1517,14 +1242,6 @@ hipError_t launch_tlog_reduce(uint32_t grid, hipStream_t s, const TlogParams& r)
 hipError_t launch_unpack(uint32_t grid, hipStream_t s, uint64_t* sum64, unsigned long long* pk64, uint32_t nb_entries,
                          uint32_t shift) {
   hipLaunchKernelGGL(unpack_kernel, dim3(grid), dim3(256), 0, s, sum64, pk64, nb_entries, shift);
-  return hipGetLastError();
-}
-
-hipError_t launch_route(uint32_t parts, uint32_t grid, hipStream_t s, const RouteParams& r) {
-  hipLaunchKernelGGL(route_resolve_kernel, dim3(parts), dim3(1024), 0, s, r);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(route_tally_kernel, dim3(grid), dim3(1024), 0, s, r);
   return hipGetLastError();
 }
 

@@ -75,9 +75,16 @@ int load_replay(const char* path, Replay& r, std::string& err) {
   r.nb_buffers = get<uint32_t>(p + 24);
   uint64_t cs_len = get<uint64_t>(p + 32), str_len = get<uint64_t>(p + 40);
   size_t off = 64;
-  size_t need = off + 8ull * r.nb_keys + pad8(4ull * (r.nb_keys + 1)) + kEntryBytes * r.nb_entries + 8 * cs_len +
-                pad8(str_len);
-  if (need > r.file.size()) {
+  // every size is checked against the file before it is added to an offset
+  // (header values come from the file and may be anything)
+  const uint64_t fsz = r.file.size();
+  if (cs_len > fsz / 8 || str_len > fsz) {
+    err = "truncated object table";
+    return NMG_ERR_INVALID;
+  }
+  const uint64_t need = off + 8ull * r.nb_keys + pad8(4ull * (r.nb_keys + 1)) + (uint64_t)kEntryBytes * r.nb_entries +
+                        8 * cs_len + pad8(str_len);
+  if (need > fsz) {
     err = "truncated object table";
     return NMG_ERR_INVALID;
   }
@@ -119,7 +126,8 @@ int load_replay(const char* path, Replay& r, std::string& err) {
       m.callstack = nullptr;
     }
     if (caller_off != 0xFFFFFFFFu) {
-      if (caller_off >= str_len) {
+      // the string must end inside the pool (it is printed with %s)
+      if (caller_off >= str_len || !memchr(str_pool + caller_off, 0, str_len - caller_off)) {
         err = "caller string out of range";
         return NMG_ERR_INVALID;
       }
@@ -141,7 +149,7 @@ int load_replay(const char* path, Replay& r, std::string& err) {
     B.head = get<uint64_t>(p + off + 16);
     B.ring = get<uint64_t>(p + off + 24);
     off += 32;
-    if (off + pad8(B.ring) > r.file.size()) {
+    if (B.ring > r.file.size() - off || pad8(B.ring) > r.file.size() - off) {
       err = "truncated ring";
       return NMG_ERR_INVALID;
     }
@@ -156,8 +164,9 @@ int load_replay(const char* path, Replay& r, std::string& err) {
     const uint32_t nm = get<uint32_t>(p + off + 8), nb_names = get<uint32_t>(p + off + 12);
     const uint32_t nb_path = get<uint32_t>(p + off + 16), nb_text = get<uint32_t>(p + off + 20);
     off += 32;
-    const size_t mods_off = off, names_off = mods_off + 32ull * nm, path_off = names_off + pad8(nb_names),
-                 text_off = path_off + pad8(nb_path);
+    // (u32 counts: the sums below cannot overflow 64 bits)
+    const uint64_t mods_off = off, names_off = mods_off + 32ull * nm, path_off = names_off + pad8(nb_names),
+                   text_off = path_off + pad8(nb_path);
     if (text_off + pad8(nb_text) > r.file.size() || (nb_names && p[names_off + nb_names - 1] != 0)) {
       err = "truncated context section";
       return NMG_ERR_INVALID;

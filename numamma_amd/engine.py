@@ -130,6 +130,12 @@ class Engine:
         cnt = self._c(lib.nmg_get_launch_times(self.h, buf, n))
         return [buf[i] for i in range(cnt)]
 
+    def kernel_times(self, n: int = 64):
+        """(attribution kernel ms, whole launch ms) of up to n recent launches."""
+        a, t = (C.c_float * n)(), (C.c_float * n)()
+        cnt = self._c(lib.nmg_get_kernel_times(self.h, a, t, n))
+        return [a[i] for i in range(cnt)], [t[i] for i in range(cnt)]
+
     def last_analyze_ms(self) -> float:
         ms = C.c_float()
         self._c(lib.nmg_last_analyze_ms(self.h, C.byref(ms)))

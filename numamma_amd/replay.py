@@ -392,47 +392,50 @@ def make_table(cfg: SynthConfig, rng: np.random.Generator) -> ObjectTable:
 
     nent = K + int(reused.sum())
     ent = np.zeros(nent, dtype=ENTRY_DTYPE)
-    entry_off = np.zeros(K + 1, dtype=np.uint32)
-    e = 0
-    mem_id = 1
     head_frames = rng.integers(0x7F0000000000, 0x7F0000100000, (nent, 3), dtype=np.uint64)
     alloc_jit = rng.integers(0, HORIZON // 100, (K, 2))
-    for k in range(K):
-        entry_off[k] = e
-        g = int(group[k])
-        n = 2 if reused[k] else 1
-        for j in range(n):  # newest first
-            r = ent[e]
-            r["initial_buffer_size"] = size[k]
-            r["buffer_addr"] = keys[k]
-            r["buffer_size"] = size[k]
-            if realloc[k]:
-                r["buffer_addr"] = keys[k] + np.uint64(16 * int(rng.integers(1, 64)))
-                r["buffer_size"] = size[k] + np.uint64(16 * int(rng.integers(0, 512)))
-            if n == 1:
-                r["alloc_date"] = T0 + alloc_jit[k, 0]
-                r["free_date"] = T0 + HORIZON - alloc_jit[k, 1]
-            elif j == 0:  # newer lifetime: second half
-                r["alloc_date"] = T0 + HORIZON // 2 + alloc_jit[k, 0]
-                r["free_date"] = T0 + HORIZON - alloc_jit[k, 1]
-            else:  # older lifetime: first half
-                r["alloc_date"] = T0 + alloc_jit[k, 0]
-                r["free_date"] = T0 + HORIZON // 2 - alloc_jit[k, 1]
-            r["caller_rip"] = grip[g]
-            r["mem_type"] = MEM_DYNAMIC
-            r["caller_off"] = g_caller_off[g]
-            if gnull[g]:
-                r["has_callstack"] = 0
-                r["callstack_size"] = 0
-            else:
-                cs = np.concatenate([head_frames[e], g_tail[g]])
-                r["has_callstack"] = 1
-                r["callstack_size"] = cs.shape[0]
-                r["callstack_off"] = pool_off
-                pool.append(cs)
-                pool_off += cs.shape[0]
-            e += 1
-    entry_off[K] = e
+    # entries in key order, newest first (vectorised; the only random draws
+    # inside the per-key walk are the realloc'd keys' offsets, taken in key
+    # order as the scalar walk did)
+    nper = np.where(reused, 2, 1)
+    entry_off = np.zeros(K + 1, dtype=np.uint32)
+    entry_off[1:] = np.cumsum(nper)
+    ek = np.repeat(np.arange(K), nper)               # entry -> key
+    ej = np.arange(nent) - entry_off[ek].astype(np.int64)  # 0 = newest
+    eg = group[ek]
+    ent["initial_buffer_size"] = size[ek]
+    ent["buffer_addr"] = keys[ek]
+    ent["buffer_size"] = size[ek]
+    for k in np.flatnonzero(realloc):  # (never reused: one entry)
+        e = int(entry_off[k])
+        ent["buffer_addr"][e] = keys[k] + np.uint64(16 * int(rng.integers(1, 64)))
+        ent["buffer_size"][e] = size[k] + np.uint64(16 * int(rng.integers(0, 512)))
+    j0, j1 = alloc_jit[ek, 0].astype(np.uint64), alloc_jit[ek, 1].astype(np.uint64)
+    two = nper[ek] == 2
+    half = np.uint64(HORIZON // 2)
+    ent["alloc_date"] = np.uint64(T0) + j0 + np.where(two & (ej == 0), half, np.uint64(0))
+    ent["free_date"] = np.uint64(T0) + np.where(two & (ej == 1), half, np.uint64(HORIZON)) - j1
+    ent["caller_rip"] = grip[eg]
+    ent["mem_type"] = MEM_DYNAMIC
+    ent["caller_off"] = g_caller_off[eg]
+    # call stacks: the entry's 3 interposer frames, then its group's tail
+    tl = np.array([t.shape[0] for t in g_tail], dtype=np.int64)
+    toff = np.zeros(G + 1, dtype=np.int64)
+    toff[1:] = np.cumsum(tl)
+    tails = np.concatenate(g_tail) if G else np.zeros(0, dtype=np.uint64)
+    has = ~gnull[eg]
+    clen = np.where(has, 3 + tl[eg], 0)
+    coff = np.zeros(nent + 1, dtype=np.int64)
+    coff[1:] = np.cumsum(clen)
+    ent["has_callstack"] = has.astype(np.uint32)
+    ent["callstack_size"] = clen.astype(np.int32)
+    ent["callstack_off"] = np.where(has, coff[:-1], 0).astype(np.uint32)
+    pe = np.repeat(np.arange(nent), clen)             # pool position -> entry
+    pj = np.arange(coff[-1]) - coff[pe]               # position within the entry's stack
+    pool_arr = np.where(pj < 3, head_frames[pe, np.minimum(pj, 2)],
+                        tails[np.clip(toff[eg[pe]] + pj - 3, 0, max(0, tails.shape[0] - 1))] if tails.shape[0]
+                        else np.uint64(0)).astype(np.uint64)
+    e = nent
     keys_l = [keys]
     ent_l = [ent]
     off_l = [entry_off[:-1].astype(np.int64)]
@@ -481,7 +484,6 @@ def make_table(cfg: SynthConfig, rng: np.random.Generator) -> ObjectTable:
     order = np.argsort(keys_all, kind="stable")
     assert np.all(order == np.arange(order.shape[0])), "regions are laid out in ascending order"
     ent_all["id"] = np.arange(1, ent_all.shape[0] + 1)
-    pool_arr = np.concatenate(pool) if pool else np.zeros(0, dtype=np.uint64)
     return ObjectTable(keys_all, eo, ent_all, pool_arr.astype(np.uint64), bytes(strings))
 
 

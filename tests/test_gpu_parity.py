@@ -146,51 +146,6 @@ def test_long_tail_paths_bit_exact(tmp_path, dbg):
     _same_dirs(odir, edir)
 
 
-ROUTE_CASES = [
-    SynthConfig(nb_samples=300_000, nb_intervals=1_000_000, size_max=64 * 1024, site_ratio=0.002, seed=12),
-    SynthConfig(nb_samples=60_000, nb_intervals=200_000, size_min=8, size_max=512, seed=6),
-    SynthConfig(nb_samples=200_000, nb_intervals=20_000, reuse_frac=0.3, realloc_frac=0.1, nb_threads=5,
-                lost_frac=1e-3, wrap_one=True, seed=18),
-]
-
-
-@pytest.mark.parametrize("cfg", ROUTE_CASES, ids=["k1m", "k200k", "k20k_reuse"])
-def test_partition_first_bit_exact(tmp_path, cfg):
-    """Partition-first lookup for large tables (internal switch 0x8000):
-    samples routed by fence range, matched per range from LDS, tallied per
-    buffer; bit-exact with the oracle, reused addresses and irregular buffers
-    included."""
-    from numamma_amd.engine import Engine
-
-    d = str(tmp_path)
-    rp = generate(cfg)
-    path, odir = _oracle(rp, d)
-    # (the raw dump needs NMG_F_OBJECT_LEVELS, which keeps the direct path: compare
-    # through the getters, the report and the page cells instead)
-    eng = Engine(flags=_lib.NMG_F_DEFAULT | 0x8000, nb_threads=rp.nb_threads)
-    eng.set_objects(rp.table)
-    eng.submit_replay(rp)
-    for _ in range(2):  # reset + analyse twice: the sub-logs are reused
-        eng.reset()
-        eng.analyze()
-    eng.synchronize()
-    edir = os.path.join(d, "engine")
-    eng.report(edir, os.path.join(d, "e.txt"))
-    raw = RawResults.read(os.path.join(d, "oracle_raw.bin"))
-    first, cw = eng.object_counters()
-    g, ns, nf = eng.global_counters()
-    cells = eng.page_cells()
-    nbs, nbf = eng.buffer_counts()
-    eng.close()
-    assert np.array_equal(first, raw.first_ordinal)
-    assert np.array_equal(cw, raw.count_weight)
-    assert np.array_equal(g, raw.global_counters) and (ns, nf) == (raw.nb_samples, raw.nb_found)
-    assert np.array_equal(nbs, raw.buf_samples) and np.array_equal(nbf, raw.buf_found)
-    assert np.array_equal(cells, raw.cells)
-    assert open(os.path.join(d, "oracle_stdout.txt"), "rb").read() == open(os.path.join(d, "e.txt"), "rb").read()
-    _same_dirs(odir, edir)
-
-
 def test_no_match_mode(tmp_path):
     d = str(tmp_path)
     rp = generate(SynthConfig(nb_samples=40_000, nb_intervals=100, seed=8))
@@ -420,6 +375,64 @@ def test_lookup_boundaries_bit_exact(tmp_path, nkeys, cluster):
     d = str(tmp_path)
     path, odir = _oracle(_edge_replay(nkeys, 100 + nkeys, cluster), d)
     edir = _engine_replay(path, d)
+    _assert_raw_equal(os.path.join(d, "oracle_raw.bin"), os.path.join(d, "engine_raw.bin"))
+    _same_dirs(odir, edir)
+
+
+@pytest.mark.parametrize("nkeys,cluster", [(40_000, 0), (20_000, 7)])
+def test_lookup_without_directory_bit_exact(tmp_path, nkeys, cluster):
+    """Large-table buckets with no directory (internal switch 0x8000, the
+    layout of tables beyond 4095 << 16 keys): fence search, then a binary
+    search of the bucket's keys."""
+    d = str(tmp_path)
+    path, odir = _oracle(_edge_replay(nkeys, 200 + nkeys, cluster), d)
+    edir = _engine_replay(path, d, flags=_lib.NMG_F_DEFAULT | 0x8000)
+    _assert_raw_equal(os.path.join(d, "oracle_raw.bin"), os.path.join(d, "engine_raw.bin"))
+    _same_dirs(odir, edir)
+
+
+def _short_sample_replay(n=200_000, seed=61):
+    """One buffer of n PERF_RECORD_SAMPLE records whose header size is 16 B
+    (the reference's byte cursor accepts them, mem_sampling.c:862-918: the
+    32 B of struct mem_sample are read after the header whatever the size),
+    then two 40 B records.  Record i reads ts = its own second word, addr =
+    the next header (0x0010000000000009), weight = the next record's second
+    word: every sample hits one object, and a launch holds 2.5x more samples
+    than nbytes / 40."""
+    from numamma_amd.replay import Buffer, ObjectTable, Replay
+
+    rp = generate(SynthConfig(nb_samples=1000, nb_intervals=3000, seed=seed))
+    t = rp.table
+    special = np.zeros(1, dtype=t.entries.dtype)
+    special[0] = t.entries[t.entry_off[-2]]  # a heap entry as the template
+    special["buffer_addr"] = 0x0010000000000000
+    special["buffer_size"] = special["initial_buffer_size"] = 4096
+    special["alloc_date"] = 0
+    special["free_date"] = 1 << 62
+    special["id"] = t.nb_entries + 1
+    # (2^52 + 9: above every heap, global and [stack] key)
+    tab = ObjectTable(np.concatenate([t.keys, np.array([0x0010000000000000], np.uint64)]),
+                      np.concatenate([t.entry_off, [t.entry_off[-1] + 1]]).astype(np.uint32),
+                      np.concatenate([t.entries, special]), t.callstack_pool, t.string_pool)
+    rng = np.random.default_rng(seed)
+    words = np.zeros(2 * n, dtype=np.uint64)
+    words[0::2] = np.uint64(9) | (np.uint64(16) << np.uint64(48))
+    words[1::2] = rng.integers(1, 2000, n).astype(np.uint64)
+    tail = np.zeros(2, dtype=RECORD_DTYPE)
+    tail["type"], tail["size"], tail["timestamp"], tail["addr"], tail["weight"] = 9, 40, 5, 1, 7
+    raw = np.concatenate([np.frombuffer(words.tobytes(), np.uint8), np.frombuffer(tail.tobytes(), np.uint8)])
+    return Replay(rp.nb_threads, tab, [Buffer(0, 0, raw.copy(), 0, raw.shape[0])])
+
+
+@pytest.mark.parametrize("dbg", [0, 0x2000])
+def test_short_sample_records_bit_exact(tmp_path, dbg):
+    """SAMPLE records shorter than 40 B in the hashed object mode: they stay
+    out of the packed long-tail counters (whose bound counts 40 B records);
+    0x2000 (sub-logs of 2 records) drives every contribution to the overflow
+    paths."""
+    d = str(tmp_path)
+    path, odir = _oracle(_short_sample_replay(), d)
+    edir = _engine_replay(path, d, flags=_lib.NMG_F_DEFAULT | dbg)
     _assert_raw_equal(os.path.join(d, "oracle_raw.bin"), os.path.join(d, "engine_raw.bin"))
     _same_dirs(odir, edir)
 

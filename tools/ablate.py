@@ -27,6 +27,10 @@ WORKLOADS = {
     "c2": dict(nb_samples=10_000_000, nb_intervals=1_000),
     "k100k": dict(nb_samples=10_000_000, nb_intervals=100_000),
     "k1m": dict(nb_samples=10_000_000, nb_intervals=1_000_000, size_max=64 * 1024),
+    "c4": dict(nb_samples=125_000_000, nb_intervals=1_000_000, size_max=64 * 1024),
+    # same table, samples concentrated on few objects (no gap samples): the
+    # lookup's cost when every table line it touches is cache-hot
+    "c4hot": dict(nb_samples=125_000_000, nb_intervals=1_000_000, size_max=64 * 1024, zipf_s=2.0, frac_gap=0.0),
 }
 
 

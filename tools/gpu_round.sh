@@ -73,7 +73,7 @@ for s in $STAGES; do
         i=$((i+1))
         rm -rf $OUT/pmc_${TAG}_$i
         timeout -k 10 400 rocprofv3 --pmc $set --kernel-trace -d $ROOT/$OUT/pmc_${TAG}_$i -o run --output-format csv \
-          -- python3 $ROOT/bench.py --steps 3 --warmup 1 --no-cpu-baseline > $OUT/pmc_${TAG}_$i.log 2>&1 \
+          -- python3 $ROOT/bench.py --workload ${PMC_WL:-c2} --steps 3 --warmup 1 --no-cpu-baseline > $OUT/pmc_${TAG}_$i.log 2>&1 \
           || { echo "pmc pass $i failed"; tail -20 $OUT/pmc_${TAG}_$i.log; exit 1; }
       done
       echo "pmc passes done" ;;
@@ -101,6 +101,11 @@ for s in $STAGES; do
           || { echo "l2 pass $i failed"; tail -20 $OUT/l2_${TAG}_$i.log; exit 1; }
       done
       echo "l2 passes done" ;;
+    alloc)
+      echo "== arena allocation experiment (${ALLOC_WL:-c4})"
+      timeout -k 10 900 python tools/exp_alloc.py --workload ${ALLOC_WL:-c4} > $OUT/alloc_$TAG.json 2> $OUT/alloc_$TAG.err \
+        || { echo "alloc failed"; tail -30 $OUT/alloc_$TAG.err; exit 1; }
+      cat $OUT/alloc_$TAG.json ;;
     ab)
       echo "== A/B variants (${AB_VARIANTS:-base})"
       timeout -k 10 900 python tools/ab.py --variants ${AB_VARIANTS:-base} --workloads ${AB_WL:-c2,k1m} --rounds 2 \
