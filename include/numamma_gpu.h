@@ -137,6 +137,7 @@ struct nmg_engine;
 typedef struct nmg_engine nmg_engine;
 
 const char *nmg_strerror(int status);
+/* text of the last error on h (h == NULL: the calling thread's last failed nmg_create) */
 int nmg_get_last_error_detail(nmg_engine *h, char *buf, size_t len);
 
 int nmg_create(nmg_engine **out, const struct nmg_options *opt);

@@ -16,6 +16,16 @@ if os.environ.get("NMG_LIB_VARIANT"):
     LIB_PATH = os.path.join(_HERE, "build", "variants", "libnumamma_gpu_%s.so" % os.environ["NMG_LIB_VARIANT"])
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "numamma_gpu.h")
 
+# One HIP runtime per process: torch ships its own libamdhip64.so (same
+# soname as /opt/rocm's).  Loaded first, it is the one the engine's
+# libamdhip64.so.7 dependency resolves to; loaded after the engine, torch
+# would bring a second runtime instance into the process, and on some boxes
+# the second one to initialise finds no GPU.
+try:
+    import torch  # noqa: F401
+except ImportError:  # (a process without torch uses /opt/rocm's runtime)
+    pass
+
 if not os.path.exists(LIB_PATH):
     raise ImportError(
         f"{LIB_PATH} is missing: build it with `make -C numamma_amd` or "
@@ -198,10 +208,8 @@ class NmgError(RuntimeError):
 
 def check(rc: int, h=None) -> int:
     if rc < 0:
-        detail = ""
-        if h:
-            buf = C.create_string_buffer(512)
-            lib.nmg_get_last_error_detail(h, buf, 512)
-            detail = buf.value.decode(errors="replace")
+        buf = C.create_string_buffer(512)
+        lib.nmg_get_last_error_detail(h, buf, 512)  # (h None: the last failed nmg_create)
+        detail = buf.value.decode(errors="replace")
         raise NmgError(rc, detail)
     return rc

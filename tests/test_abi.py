@@ -1,6 +1,8 @@
 """The C-ABI library loads, exports every symbol include/numamma_gpu.h
 declares, and fails loudly (no CPU fallback) when no GPU is present."""
 import ctypes as C
+import os
+import subprocess
 
 import pytest
 import torch
@@ -40,3 +42,15 @@ def test_null_arguments_rejected():
     assert _lib.lib.nmg_create(None, None) == -1
     assert _lib.lib.nmg_analyze(None) == -1
     assert _lib.lib.nmg_report_host(None, None, None, None) == -1
+
+
+def test_header_compiles_as_c99(tmp_path):
+    """include/numamma_gpu.h from a plain C99 translation unit: the test host
+    of INTEGRATION.md section 1 (tests/c/nmg_c99_host.c) compiles with
+    -std=c99 -Wall -Wextra -Werror -pedantic and links against the library."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = os.path.join(str(tmp_path), "host")
+    subprocess.run(["gcc", "-std=c99", "-Wall", "-Wextra", "-Werror", "-pedantic",
+                    "-I" + os.path.join(root, "include"), os.path.join(root, "tests", "c", "nmg_c99_host.c"),
+                    "-o", exe, "-L" + os.path.join(root, "numamma_amd"), "-lnumamma_gpu"], check=True)
+    assert os.path.exists(exe)
