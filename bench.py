@@ -127,7 +127,7 @@ def main():
     ap.add_argument("--workload", default="c4", choices=sorted(WORKLOADS))
     ap.add_argument("--secondary", default="c2", help="workload measured after the main one (N=1; '' = none)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-records", type=int, default=10_000_000, help="records in the CPU baseline's sample")
+    ap.add_argument("--cpu-records", type=int, default=200_000, help="records in the CPU baseline's sample")
     args = ap.parse_args()
 
     import torch
@@ -197,6 +197,7 @@ def main():
                          "roofline_frac": s.samples * RECORD_BYTES / (float(np.mean(sa)) * 1e-3) / 1e9 / HBM_PEAK_GBS}}
             s.eng.close()
         if world == 1 and not args.no_cpu_baseline:
+            log(f"[rank 0] cpu baseline: first {args.cpu_records} records")
             out["cpu_baseline"] = cpu_baseline(w.rp, args.cpu_records)
         print(json.dumps(out), flush=True)
     if distributed:
@@ -286,6 +287,7 @@ def cpu_baseline(rp, max_records, target_s=10.0, max_runs=40):
         sub.write(path)
         while runs < max_runs and (runs == 0 or secs < target_s):
             t = pyoracle.run(path, os.path.join(d, "out"), os.path.join(d, "stdout.txt"))
+            log(f"[rank 0] cpu baseline run {runs}: {t['nb_samples']} records in {t['analysis_s']:.2f}s")
             runs += 1
             samples += t["nb_samples"]
             secs += t["analysis_s"]

@@ -28,75 +28,9 @@
 //     bit-exact;
 //   * the long-tail log's range reduce, the packed-counter fold and the
 //     counter reset; the host side is nmg_engine.hip.
-#include "nmg_kernels.h"
+#include "nmg_device.h"
 
 namespace nmg {
-
-__constant__ uint32_t c_level_mask[9] = {0x08,  0x20,  0x40,  0x10,  0x80,
-                                         0x300, 0xC00, 0x1000, 0x2000};
-// order: L1, L2, L3, LFB, LOC_RAM, REM_RAM1|2, REM_CCE1|2, IO, UNC
-// (the bucket order of struct mem_counters, mem_analyzer.h:23-40)
-
-// ---------------------------------------------------------------------------
-// device helpers
-
-__device__ __forceinline__ uint64_t wave_sum(uint64_t v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
-}
-
-// Full-wave u32 sum with DPP (VALU only, no LDS traffic): Hillis-Steele
-// within each 16-lane row, then row_bcast:15 / row_bcast:31; lane 63 holds
-// the total.
-template <int CTRL, int ROW_MASK>
-__device__ __forceinline__ uint32_t dpp0(uint32_t v) {
-  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROW_MASK, 0xf, true);
-}
-__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
-  v += dpp0<0x111, 0xf>(v);  // row_shr:1
-  v += dpp0<0x112, 0xf>(v);  // row_shr:2
-  v += dpp0<0x114, 0xf>(v);  // row_shr:4
-  v += dpp0<0x118, 0xf>(v);  // row_shr:8
-  v += dpp0<0x142, 0xa>(v);  // row_bcast:15 into rows 1 and 3
-  v += dpp0<0x143, 0xc>(v);  // row_bcast:31 into rows 2 and 3
-  return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
-}
-// Sum of per-lane weights; `big` (wave-uniform) = some weight >= 2^26, in
-// which case 64 lanes could overflow 32 bits and the u64 path is taken.
-__device__ __forceinline__ uint64_t wave_sum_w(uint64_t w, bool big) {
-  return big ? wave_sum(w) : (uint64_t)wave_sum_u32((uint32_t)w);
-}
-
-// update_counters' level classification (mem_sampling.c:521-591) as an
-// 18-bit mask: bit g (0..8) = hit bucket of level group g, bit 9+g = miss.
-// Groups: L1, L2, L3, LFB, local RAM, remote RAM 1|2, remote cache 1|2, IO,
-// uncached (the bucket order of struct mem_counters).  HIT beats MISS and
-// every group is independent (quirk Q12).
-__device__ __forceinline__ uint32_t bucket_mask(uint32_t lvl) {
-  uint32_t g = ((lvl >> 3) & 1) | (((lvl >> 5) & 1) << 1) | (((lvl >> 6) & 1) << 2) |
-               (((lvl >> 4) & 1) << 3) | (((lvl >> 7) & 1) << 4) | ((((lvl >> 8) | (lvl >> 9)) & 1) << 5) |
-               ((((lvl >> 10) | (lvl >> 11)) & 1) << 6) | (((lvl >> 12) & 1) << 7) | (((lvl >> 13) & 1) << 8);
-  if (lvl & LVL_HIT) return g;
-  if (lvl & LVL_MISS) return g << 9;
-  return 0;
-}
-
-__device__ __forceinline__ void set_error(Params& p, uint64_t seq, uint32_t off, uint32_t code) {
-  uint64_t w = (seq << 40) | (uint64_t(off) << 8) | code;
-  atomicMin(reinterpret_cast<unsigned long long*>(p.min64 + 36 + p.nb_entries),
-            (unsigned long long)w);
-}
-
-// Descend `levels` levels of an Eytzinger tree (node i has children 2i, 2i+1)
-// from the root and return the index below the last level: one 8 B LDS read
-// per level (reading three levels per round trip was measured slower: more
-// LDS bytes and bank conflicts).  Reads stay below 2^levels.
-__device__ __forceinline__ uint32_t eytz_descend(const uint64_t* F, uint32_t levels, uint64_t addr) {
-  uint32_t i = 1;
-  for (; levels > 0; levels--) i = 2 * i + (F[i] <= addr ? 1u : 0u);
-  return i;
-}
 
 // Largest key <= addr (ht_lower_key, tools/hash.c:63-77) for tables larger
 // than kLdsNodes.  Returns nb_keys when no key <= addr.
@@ -180,30 +114,6 @@ __device__ __forceinline__ uint32_t lower_key(const Params& p, const uint64_t* s
   return lo;
 }
 
-// __ma_find_mem_info_from_sample_generic (mem_analyzer.c:249-286) with
-// is_sample_in_buffer (:141-155): only the lower-bound node, newest entry first.
-__device__ __forceinline__ bool entry_match(uint4 a, uint4 b, uint64_t addr, uint64_t ts) {
-  const uint64_t baddr = (uint64_t(a.y) << 32) | a.x, bend = (uint64_t(a.w) << 32) | a.z;
-  const uint64_t alloc = (uint64_t(b.y) << 32) | b.x, fr = (uint64_t(b.w) << 32) | b.z;
-  return baddr <= addr && addr < bend && alloc <= ts && ts <= fr;
-}
-
-__device__ __forceinline__ void sparse_add(Params& p, uint64_t key, uint64_t seq, uint32_t off, uint32_t cnt) {
-  *p.sparse_dirty = 1u;
-  uint64_t h = (key * 0x9E3779B97F4A7C15ull) >> 20;
-  uint32_t slot = uint32_t(h) & p.sparse_mask;
-  for (uint32_t probe = 0; probe <= p.sparse_mask; probe++) {
-    unsigned long long prev = atomicCAS(reinterpret_cast<unsigned long long*>(p.sparse_keys + slot),
-                                        ~0ull, (unsigned long long)key);
-    if (prev == ~0ull || prev == key) {
-      atomicAdd(p.sparse_vals + slot, cnt);
-      return;
-    }
-    slot = (slot + 1) & p.sparse_mask;
-  }
-  set_error(p, seq, off, kErrCapacity);
-}
-
 // Per-workgroup privatised counters of the stream (access type, thread rank)
 // being analysed.  One stream at a time per workgroup, so (entry) and
 // (entry, page) are the keys of the aggregation tables.
@@ -236,26 +146,6 @@ __device__ __forceinline__ uint32_t obj_bucket(uint32_t e) {
   return (uint32_t)(((uint64_t)(e * 0x9E3779B1u) * kObjBuckets) >> 32);
 }
 
-__device__ __forceinline__ int bucket_slot(unsigned int* slots8, uint32_t key) {
-  const uint4 k0 = reinterpret_cast<const uint4*>(slots8)[0], k1 = reinterpret_cast<const uint4*>(slots8)[1];
-  uint32_t k[8] = {k0.x, k0.y, k0.z, k0.w, k1.x, k1.y, k1.z, k1.w};
-  int j = -1;
-#pragma unroll
-  for (int i = 7; i >= 0; i--) j = k[i] == key ? i : j;
-  if (j >= 0) return j;
-  for (int attempt = 0; attempt < 8; attempt++) {
-    int f = -1;
-#pragma unroll
-    for (int i = 7; i >= 0; i--) f = k[i] == kEmpty32 ? i : f;
-    if (f < 0) return -1;
-    const unsigned prev = atomicCAS(&slots8[f], kEmpty32, key);
-    if (prev == kEmpty32 || prev == key) return f;
-#pragma unroll
-    for (int i = 0; i < 8; i++) k[i] = i == f ? prev : k[i];
-  }
-  return -1;
-}
-
 __device__ __forceinline__ int obj_slot(WgCounters& wc, uint32_t e) {
   const uint32_t hb = obj_bucket(e);
   const int j = bucket_slot(&wc.okey[hb * 8], e);
@@ -281,63 +171,6 @@ __device__ __forceinline__ int page_slot(WgCounters& wc, uint32_t cell) {
   return page_slot_at(wc.pkey4, cell);
 }
 
-// Per-lane privatised mem_counters of the current stream: packed u16 counts
-// and u32 weight sums per bucket, plus total count / weight / N/A.  Bounded:
-// drained at least every kDrainWindows windows (one record per lane per
-// window) and only weights < 2^23 take this path, so nothing overflows
-// (256 x 2^23 = 2^31).
-constexpr uint32_t kDrainWindows = 256;
-constexpr uint64_t kLaneMaxWeight = 1ull << 23;
-static_assert((uint64_t)kDensePageWindows * kWG * kLaneMaxWeight < (1ull << kPackShift), "packed weight");
-// Only the 9 hit buckets live in registers (the common case in PEBS data);
-// miss buckets are updated in LDS directly.
-struct LaneAcc {
-  uint32_t cnt2[5];  // counts of hit buckets 2k (low 16 bits) and 2k+1 (high 16 bits)
-  uint32_t sum[9];
-  uint32_t tc, tw, na;
-};
-
-__device__ __forceinline__ void lane_acc_clear(LaneAcc& a) {
-#pragma unroll
-  for (int k = 0; k < 5; k++) a.cnt2[k] = 0;
-#pragma unroll
-  for (int k = 0; k < 9; k++) a.sum[k] = 0;
-  a.tc = a.tw = a.na = 0;
-}
-
-// exact sum over the wave of a u32 per lane (as two 16-bit halves, DPP)
-__device__ __forceinline__ uint64_t wave_sum_u32x(uint32_t v) {
-  const uint32_t lo = wave_sum_u32(v & 0xffffu), hi = wave_sum_u32(v >> 16);
-  return (uint64_t)lo + ((uint64_t)hi << 16);
-}
-
-// lanes -> workgroup LDS counters (every lane of the wave calls this)
-__device__ __forceinline__ void lane_acc_drain(LaneAcc& a, WgCounters& wc, int lane) {
-  if (__ballot(a.tc != 0) == 0) return;
-  const uint64_t tc = wave_sum_u32x(a.tc), tw = wave_sum_u32x(a.tw), na = wave_sum_u32x(a.na);
-  if (lane == 0) {
-    atomicAdd(&wc.sums[0], (unsigned long long)tc);
-    if (tw) atomicAdd(&wc.sums[1], (unsigned long long)tw);
-    if (na) atomicAdd(&wc.sums[2], (unsigned long long)na);
-  }
-#pragma unroll
-  for (int k = 0; k < 5; k++) {
-    if (__ballot(a.cnt2[k] != 0) == 0) continue;
-    const uint32_t c0 = wave_sum_u32(a.cnt2[k] & 0xffffu), c1 = wave_sum_u32(a.cnt2[k] >> 16);
-    if (lane == 0) {
-      if (c0) atomicAdd(&wc.sums[3 + 2 * (2 * k)], (unsigned long long)c0);
-      if (c1 && 2 * k + 1 < 9) atomicAdd(&wc.sums[3 + 2 * (2 * k + 1)], (unsigned long long)c1);
-    }
-  }
-#pragma unroll
-  for (int k = 0; k < 9; k++) {
-    if (__ballot(a.sum[k] != 0) == 0) continue;
-    const uint64_t sk = wave_sum_u32x(a.sum[k]);
-    if (lane == 0) atomicAdd(&wc.sums[4 + 2 * k], (unsigned long long)sk);
-  }
-  lane_acc_clear(a);
-}
-
 // The object table as the kernel sees it: node records in LDS (small tables)
 // or in global memory (L2/MALL resident) behind the LDS fence table.
 struct Lookup {
@@ -358,27 +191,6 @@ __device__ __forceinline__ bool plog_append(const Params& p, uint32_t* pcur, uin
       (unsigned long long)(cell - (part << p.plog_cshift)) | ((unsigned long long)th << 22) |
       ((unsigned long long)cnt << 32);
   return true;
-}
-
-struct Match {
-  int64_t e;       // entry id, -1 = no match
-  uint64_t baddr;  // the entry's buffer_addr
-  uint64_t hist;   // dense histogram base cell, or kHistSparse
-};
-
-__device__ __forceinline__ void match_older(const Params& p, uint32_t first, uint32_t count, uint64_t addr,
-                                            uint64_t ts, Match& m) {
-  for (uint32_t e = first + 1; e < first + count; e++) {  // older entries of a reused address
-    const uint4* r = reinterpret_cast<const uint4*>(p.entries + e);
-    const uint4 ra = r[0], rb = r[1];
-    if (entry_match(ra, rb, addr, ts)) {
-      const uint4 rc = r[2];
-      m.e = e;
-      m.baddr = (uint64_t(ra.y) << 32) | ra.x;
-      m.hist = (uint64_t(rc.y) << 32) | rc.x;
-      return;
-    }
-  }
 }
 
 // __ma_find_mem_info_from_sample_generic (mem_analyzer.c:249-286): the
@@ -556,7 +368,7 @@ __device__ __forceinline__ void process_sample(Params& p, WgCounters& wc, LaneAc
         p.sum64 + 2 * kGlobalSums + uint64_t(p.nb_entries) * 4 + (uint64_t(e) * 2 + access) * kLevelWords);
     if (lvl & LVL_NA) atomicAdd(lv, 1ull);
     for (int g = 0; g < 9; g++) {
-      if (!(lvl & c_level_mask[g])) continue;
+      if (!(lvl & level_mask(g))) continue;
       int bucket = (lvl & LVL_HIT) ? g : ((lvl & LVL_MISS) ? 9 + g : -1);
       if (bucket < 0) continue;
       atomicAdd(lv + 1 + 2 * bucket, 1ull);
@@ -671,56 +483,6 @@ __device__ __forceinline__ void clear_state(WgCounters& wc, int tid) {
 }
 
 // ---------------------------------------------------------------------------
-// record loads straight into registers
-
-// One 40 B stride slot: 16 B + 16 B + 8 B loads whose offsets depend on the
-// slot's 16 B parity (records are 8-aligned in a 16-aligned buffer), so every
-// lane issues the same three instructions.  Decoded only when consumed, so a
-// prefetched window stays in flight while the current one is processed.
-struct RawRec {
-  uint4 x, y;
-  uint2 z;
-};
-
-__device__ __forceinline__ void load_rec(const uint8_t* base, uint64_t pos, uint64_t len, RawRec& r) {
-  if (pos + kRecBytes <= len) {
-    const uint32_t odd = uint32_t(pos >> 3) & 1;
-    const uint8_t* q = base + pos;
-    r.x = *reinterpret_cast<const uint4*>(q + (odd ? 8 : 0));
-    r.y = *reinterpret_cast<const uint4*>(q + (odd ? 24 : 16));
-    r.z = *reinterpret_cast<const uint2*>(q + (odd ? 0 : 32));
-  } else {
-    r.x = make_uint4(0, 0, 0, 0);
-    r.y = make_uint4(0, 0, 0, 0);
-    r.z = make_uint2(0, 0);
-  }
-}
-
-struct Rec {
-  uint64_t hdr, ts, addr, w, dsrc;
-};
-
-__device__ __forceinline__ uint64_t u64of(uint32_t lo, uint32_t hi) { return (uint64_t(hi) << 32) | lo; }
-
-__device__ __forceinline__ Rec decode_rec(const RawRec& r, uint64_t pos) {
-  Rec d;
-  if ((pos >> 3) & 1) {  // hdr | ts addr | w dsrc
-    d.hdr = u64of(r.z.x, r.z.y);
-    d.ts = u64of(r.x.x, r.x.y);
-    d.addr = u64of(r.x.z, r.x.w);
-    d.w = u64of(r.y.x, r.y.y);
-    d.dsrc = u64of(r.y.z, r.y.w);
-  } else {  // hdr ts | addr w | dsrc
-    d.hdr = u64of(r.x.x, r.x.y);
-    d.ts = u64of(r.x.z, r.x.w);
-    d.addr = u64of(r.y.x, r.y.y);
-    d.w = u64of(r.y.z, r.y.w);
-    d.dsrc = u64of(r.z.x, r.z.y);
-  }
-  return d;
-}
-
-// ---------------------------------------------------------------------------
 // the attribution kernel
 //
 // One 1024-thread workgroup per CU (LDS: fences 8 KiB, node records 40 KiB,
@@ -757,14 +519,6 @@ __device__ __forceinline__ void load_slot(const Params& p, const WinLane& w, con
   const uint64_t off = w.in1 ? d1.offset : d0.offset;
   const uint32_t len = w.cand ? (w.in1 ? d1.len : d0.len) : 0;
   load_rec(p.data + off, w.pos, len, r);
-}
-
-// shader-clock stamp that the scheduler does not move work across
-__device__ __forceinline__ uint64_t stamp() {
-  __builtin_amdgcn_sched_barrier(0);
-  const uint64_t t = __builtin_amdgcn_s_memtime();
-  __builtin_amdgcn_sched_barrier(0);
-  return t;
 }
 
 template <bool TIMING, int MODE>
@@ -1024,7 +778,7 @@ __global__ __launch_bounds__(kWG, 1) void attribute_kernel(Params p) {
     // window's barrier) are flushed here too -- the single flush site
     const bool stream_end = nidx != idx && (nidx >= r1 || nd0.access != cur_access || nd0.thread_rank != cur_thread);
     if (++acc_windows == kDrainWindows || stream_end) {  // keep the per-lane u32 sums bounded
-      lane_acc_drain(acc, wc, lane);
+      lane_acc_drain(acc, wc.sums, lane);
       acc_windows = 0;
     }
     if (nidx != idx) {
