@@ -102,7 +102,7 @@ class Workload:
                     reduce_u64(t, {0: "sum", 1: "min", 2: "max"}[which], dst=0)
 
 
-def timed_run(w, steps, warmup, barrier):
+def timed_run(w, steps, warmup, barrier, agree=None):
     for _ in range(warmup):
         w.step()
     barrier()
@@ -112,6 +112,8 @@ def timed_run(w, steps, warmup, barrier):
         barrier()
         one = time.perf_counter() - t
         steps = int(min(2000, max(20, math.ceil(MIN_TIMED_S / max(one, 1e-6)))))
+        if agree:  # every rank runs rank 0's count (the steps hold collectives)
+            steps = agree(steps)
     t_start = time.perf_counter()
     for _ in range(steps):
         w.step()
@@ -163,7 +165,14 @@ def main():
         torch.cuda.synchronize(device)
         w.eng.synchronize()
 
-    elapsed, steps = timed_run(w, args.steps, args.warmup, barrier)
+    def agree(n):
+        if not distributed:
+            return n
+        t = torch.tensor([n], dtype=torch.int64, device=device if backend == "nccl" else "cpu")
+        dist.broadcast(t, src=0)
+        return int(t.item())
+
+    elapsed, steps = timed_run(w, args.steps, args.warmup, barrier, agree)
     attr_ms, total_ms = w.eng.kernel_times(min(steps, 64))  # HIP events on the engine stream
     if distributed:
         tt = torch.tensor([elapsed], dtype=torch.float64, device=device)

@@ -80,6 +80,19 @@ __device__ __forceinline__ uint32_t eytz_descend(const uint64_t* F, uint32_t lev
 
 // __ma_find_mem_info_from_sample_generic (mem_analyzer.c:249-286) with
 // is_sample_in_buffer (:141-155): only the lower-bound node, newest entry first.
+// Eytzinger node of the largest fence <= addr (0: addr < every fence)
+__device__ __forceinline__ uint32_t fence_node(const uint64_t* s_fences, uint64_t addr) {
+  const uint32_t i = eytz_descend(s_fences, kFenceLevels, addr);
+  return i >> (__builtin_ctz(i) + 1);  // node of the last right turn
+}
+
+// in-order rank (bucket) of Eytzinger node idx >= 1 of the complete
+// kFenceLevels-level fence tree
+__device__ __forceinline__ uint32_t fence_bucket(uint32_t idx) {
+  const uint32_t d = 31 - __builtin_clz(idx);
+  return (((idx - (1u << d)) * 2 + 1) << (kFenceLevels - 1 - d)) - 1;
+}
+
 __device__ __forceinline__ bool entry_match(uint4 a, uint4 b, uint64_t addr, uint64_t ts) {
   const uint64_t baddr = (uint64_t(a.y) << 32) | a.x, bend = (uint64_t(a.w) << 32) | a.z;
   const uint64_t alloc = (uint64_t(b.y) << 32) | b.x, fr = (uint64_t(b.w) << 32) | b.z;

@@ -107,6 +107,28 @@ struct DevEntry {
 };
 static_assert(sizeof(DevEntry) == 64, "DevEntry");
 
+// Large tables (nmg_big.hip): the directory slot of a fence bucket is a
+// "fat" 64 B slot that resolves most lookups by itself: candidate a is the
+// node of the largest key <= the slot start, candidate b the node of the one
+// key inside the slot (if any), each as its newest entry's end, dates, entry
+// id and size.  b's key = b.end - b.sz (its newest entry is not realloc'd).
+struct FatCand {
+  uint64_t end;    // buffer_addr + buffer_size (mod 2^64) of the node's newest entry
+  uint64_t alloc;  // alloc_date
+  uint64_t free;   // free_date
+  uint32_t eid;    // bits 0..30 entry id; bit 31 = slot flag (a: several keys inside; b: present)
+  uint32_t sz;     // bits 0..29 buffer_size, or the node's key index when bit 30 (size >= 2^30)
+                   // or bit 31 (the node has older entries) is set: then the node record decides
+};
+struct FatSlot {
+  FatCand a, b;  // with several keys inside (a.eid bit 31): b.end = first inner key,
+                 // b.eid = its key index, b.sz = number of inner keys
+};
+static_assert(sizeof(FatSlot) == 64, "FatSlot");
+constexpr uint32_t kFatFlag = 0x80000000u;
+constexpr uint32_t kSzOlder = 0x80000000u, kSzBig = 0x40000000u, kSzMask = 0x3fffffffu;
+constexpr uint32_t kDbgOldBig = 0x10000;  // large tables through attribute_kernel (A/B, tests)
+
 struct Params {
   const uint8_t* data;
   const BufDesc* sbufs;    // descriptors in schedule order (sorted by stream; .pad = buffer index)
@@ -161,6 +183,19 @@ struct Params {
   unsigned long long* plog;  // null: off (cells that miss go to global atomics)
   uint32_t* plog_cnt;        // [grid][plog_parts] records written
   uint32_t plog_cap, plog_cshift, plog_parts;
+  // large tables (attribute_big_kernel)
+  const FatSlot* fat;       // [nb_fences << dir_log2]
+  const uint8_t* fatshift;  // [nb_fences] slot width log2 (<= 63), kShiftSearch: no directory
+  const uint32_t* hpre;     // [E + 1] dense cells before entry e (entry e is dense iff hpre[e+1] > hpre[e])
+  uint32_t pbits;           // LDS page key = entry << pbits | page (pages < 2^pbits)
+  uint4* plog16;            // entry-range page log: {entry, page, count, thread}; parts = entry >> plog_pshift
+  uint32_t plog_pshift;
+};
+
+// plog16_reduce_kernel (large tables)
+struct Plog16Params {
+  Params p;
+  uint32_t grid;
 };
 
 // plog_reduce_kernel
@@ -209,5 +244,10 @@ hipError_t launch_unpack(uint32_t grid, hipStream_t s, uint64_t* sum64, unsigned
                          uint32_t nb_entries, uint32_t shift);
 hipError_t launch_reset(uint32_t grid, hipStream_t s, const ResetParams& r);
 hipError_t launch_plog_reduce(uint32_t parts, hipStream_t s, const PlogParams& r);
+// large tables (nmg_big.hip)
+constexpr int kBWG = 512;  // attribute_big_kernel: 8 waves, one workgroup per CU
+hipError_t launch_attribute_big(uint32_t grid, hipStream_t s, const Params& p);
+int attribute_big_blocks_per_cu();
+hipError_t launch_plog16_reduce(uint32_t parts, hipStream_t s, const Plog16Params& r);
 
 }  // namespace nmg

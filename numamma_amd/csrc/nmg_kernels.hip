@@ -53,10 +53,6 @@ struct SpecDir {
   uint2 de;
 };
 
-__device__ __forceinline__ uint32_t fence_node(const uint64_t* s_fences, uint64_t addr) {
-  const uint32_t i = eytz_descend(s_fences, kFenceLevels, addr);
-  return i >> (__builtin_ctz(i) + 1);  // node of the last right turn (0: addr < every fence)
-}
 
 // The directory slot that lower_key reads for (addr, fence node idx), or
 // null when it reads none.

@@ -21,6 +21,9 @@ VARIANTS = {
     "match": 0x1,                       # + object counters
     "full_noflush": 0x3 | 0x400,        # LDS tables filled, never flushed to global
     "full": 0x3,                        # + page histogram (default product path)
+    # large tables through the small-table kernel's directory + node-record path
+    "lookup_only_old": 0x1 | 0x200 | 0x800 | 0x10000,
+    "full_old": 0x3 | 0x10000,
 }
 
 WORKLOADS = {
@@ -38,6 +41,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--workloads", default="c2,k100k,k1m")
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--variants", default=",".join(VARIANTS))
     args = ap.parse_args()
     import torch
 
@@ -51,13 +55,14 @@ def main():
         d = torch.from_numpy(arena).cuda()
         nbytes = int(lens.sum())
         engines = {}
-        for v, f in VARIANTS.items():
+        for v in args.variants.split(","):
+            f = VARIANTS[v]
             e = Engine(flags=f, nb_threads=rp.nb_threads)
             e.set_objects(rp.table)
             e.set_device_buffers(d.data_ptr(), offs, lens, ranks, acc)
             engines[v] = e
         print(f"# {wname}: generated in {time.time() - t0:.1f}s", file=sys.stderr, flush=True)
-        times = {v: [] for v in VARIANTS}
+        times = {v: [] for v in engines}
         for r in range(args.reps + 2):
             for v, e in engines.items():
                 e.reset()

@@ -44,7 +44,7 @@ for s in $STAGES; do
       find $OUT/prof_$TAG -name "*kernel_stats.csv" -exec cat {} \; | head -20 ;;
     ablate)
       echo "== ablation"
-      timeout -k 10 900 python tools/ablate.py --workloads ${ABLATE_WL:-c2,k100k,k1m} > $OUT/ablate_$TAG.json 2> $OUT/ablate_$TAG.err \
+      timeout -k 10 900 python tools/ablate.py --workloads ${ABLATE_WL:-c2,k100k,k1m} ${ABLATE_VARIANTS:+--variants $ABLATE_VARIANTS} > $OUT/ablate_$TAG.json 2> $OUT/ablate_$TAG.err \
         || { echo "ablate failed"; tail -40 $OUT/ablate_$TAG.err; exit 1; }
       cat $OUT/ablate_$TAG.json ;;
     e2e)
