@@ -33,13 +33,21 @@
 
 namespace nmg {
 
-constexpr int kBK = 3;                     // records per lane per window
+#ifndef NMG_BIG_K
+#define NMG_BIG_K 3
+#endif
+constexpr int kBK = NMG_BIG_K;             // records per lane per window
 constexpr uint32_t kBWin = kBWG * kBK;     // 1536 stride slots
 constexpr uint32_t kBDrain = 64;           // windows between lane-accumulator drains
 constexpr uint32_t kBTableWindows = 128;   // hashed LDS tables flushed at least this often
 constexpr uint32_t kBPageBuckets = 768;    // LDS page cells: 8-slot buckets
 constexpr uint32_t kBPageSlots = kBPageBuckets * 8;
 static_assert(kBK * kBDrain <= 256, "lane accumulators: u16 counts, u32 sums of weights < 2^23");
+#ifdef NMG_BIG_EARLY_PREFETCH
+constexpr bool kEarlyPrefetch = true;  // next window's records issued before this window's lookups
+#else
+constexpr bool kEarlyPrefetch = false;
+#endif
 static_assert((uint64_t)kBTableWindows * kBWin < (1u << 20), "flushed slot counts");
 
 struct BigCounters {
@@ -345,6 +353,19 @@ __global__ __launch_bounds__(kBWG, 1) void attribute_big_kernel(Params p) {
     const bool nhas1 = nidx + 1 < r1;
     const bool stream_end = nidx != idx && (nidx >= r1 || nd0.access != cur_access || nd0.thread_rank != cur_thread);
 
+    bool nxt_issued = false;
+    if (kEarlyPrefetch && nidx < r1) {
+      uint32_t m0, m1;
+      geometry((uint32_t)ncur, nd0, nd1, nhas1, m0, m1);
+#pragma unroll
+      for (int k = 0; k < kBK; k++) {
+        const uint32_t s = uint32_t(k) * kBWG + tid;
+        const bool i1 = s >= m0, c = s < m0 + m1;
+        const uint32_t ps = i1 ? (s - m0) * kRecBytes : (uint32_t)ncur + s * kRecBytes;
+        load_rec(p.data + (i1 ? nd1.offset : nd0.offset), ps, c ? (i1 ? nd1.len : nd0.len) : 0, nx[k]);
+      }
+      nxt_issued = true;
+    }
     const uint32_t access = d0.access, th = d0.thread_rank;
     uint64_t vm[kBK], fm[kBK];
     int64_t ent[kBK];
@@ -398,7 +419,6 @@ __global__ __launch_bounds__(kBWG, 1) void attribute_big_kernel(Params p) {
       }
     }
 
-    bool nxt_issued = false;
     if (match_on) {
       // ---- lookup stage 1: LDS fence search for the lane's records, interleaved
       uint32_t ei[kBK];
@@ -450,7 +470,7 @@ __global__ __launch_bounds__(kBWG, 1) void attribute_big_kernel(Params p) {
       }
       // the next window's records: issued after the slot loads, so the wait
       // for a slot never includes the record stream
-      if (nidx < r1) {
+      if (!nxt_issued && nidx < r1) {
         uint32_t m0, m1;
         geometry((uint32_t)ncur, nd0, nd1, nhas1, m0, m1);
 #pragma unroll

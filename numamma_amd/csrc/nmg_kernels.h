@@ -245,7 +245,10 @@ hipError_t launch_unpack(uint32_t grid, hipStream_t s, uint64_t* sum64, unsigned
 hipError_t launch_reset(uint32_t grid, hipStream_t s, const ResetParams& r);
 hipError_t launch_plog_reduce(uint32_t parts, hipStream_t s, const PlogParams& r);
 // large tables (nmg_big.hip)
-constexpr int kBWG = 512;  // attribute_big_kernel: 8 waves, one workgroup per CU
+#ifndef NMG_BIG_WG
+#define NMG_BIG_WG 512
+#endif
+constexpr int kBWG = NMG_BIG_WG;  // attribute_big_kernel: 8 waves, one workgroup per CU
 hipError_t launch_attribute_big(uint32_t grid, hipStream_t s, const Params& p);
 int attribute_big_blocks_per_cu();
 hipError_t launch_plog16_reduce(uint32_t parts, hipStream_t s, const Plog16Params& r);

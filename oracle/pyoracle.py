@@ -108,3 +108,32 @@ def ref():
         lib.ref_size.restype = C.c_int
         _ref = lib
     return _ref
+
+
+# ---- the multi-threaded restatement (oracle/nmg_cpu_mt.cpp)
+class _MtTiming(C.Structure):
+    _fields_ = [("load_s", C.c_double), ("analysis_s", C.c_double), ("merge_s", C.c_double),
+                ("nb_samples", C.c_uint64), ("threads", C.c_int)]
+
+
+_mt = None
+
+
+def run_mt(replay_path: str, raw_path: str | None = None, threads: int = 16, levels: bool = True) -> dict:
+    """Analyse a replay with `threads` host threads (bit-exact with run());
+    returns the timings: load, parallel analysis, merge."""
+    global _mt
+    if _mt is None:
+        so = os.path.join(HERE, "liboracle_mt.so")
+        if not os.path.exists(so):
+            build()
+        _mt = C.CDLL(so)
+        _mt.nmo_mt_run.argtypes = [C.c_char_p, C.c_char_p, C.c_int, C.c_int, C.POINTER(_MtTiming)]
+        _mt.nmo_mt_run.restype = C.c_int
+    t = _MtTiming()
+    rc = _mt.nmo_mt_run(replay_path.encode(), raw_path.encode() if raw_path else None, threads, int(levels),
+                        C.byref(t))
+    if rc:
+        raise RuntimeError(f"multi-threaded restatement failed ({rc})")
+    return {"load_s": t.load_s, "analysis_s": t.analysis_s, "merge_s": t.merge_s, "nb_samples": t.nb_samples,
+            "threads": t.threads}

@@ -108,7 +108,7 @@ for s in $STAGES; do
       cat $OUT/alloc_$TAG.json ;;
     ab)
       echo "== A/B variants (${AB_VARIANTS:-base})"
-      timeout -k 10 900 python tools/ab.py --variants ${AB_VARIANTS:-base} --workloads ${AB_WL:-c2,k1m} --rounds 2 \
+      timeout -k 10 900 python tools/ab.py --variants ${AB_VARIANTS:-base} --workloads ${AB_WL:-c2,k1m} --rounds ${AB_ROUNDS:-2} \
         > $OUT/ab_$TAG.json 2> $OUT/ab_$TAG.err || { echo "ab failed"; tail -30 $OUT/ab_$TAG.err; exit 1; }
       cat $OUT/ab_$TAG.json ;;
     pmc)

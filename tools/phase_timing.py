@@ -28,6 +28,8 @@ WORKLOADS = {
     "c2": dict(nb_samples=10_000_000, nb_intervals=1_000),
     "k100k": dict(nb_samples=10_000_000, nb_intervals=100_000),
     "k1m": dict(nb_samples=10_000_000, nb_intervals=1_000_000, size_max=64 * 1024),
+    "c4": dict(nb_samples=125_000_000, nb_intervals=1_000_000, size_max=64 * 1024),
+    "c4hot": dict(nb_samples=125_000_000, nb_intervals=1_000_000, size_max=64 * 1024, zipf_s=2.0, frac_gap=0.0),
 }
 
 
@@ -49,7 +51,7 @@ def main():
         arena, offs, lens, ranks, acc = rp.packed()
         d = torch.from_numpy(arena).cuda()
         for v, f in VARIANTS.items():
-            e = Engine(flags=f | TIMING, nb_threads=rp.nb_threads)
+            e = Engine(flags=f | TIMING | 0x10000, nb_threads=rp.nb_threads)
             e.set_objects(rp.table)
             e.set_device_buffers(d.data_ptr(), offs, lens, ranks, acc)
             res = []
