@@ -129,7 +129,10 @@ def main():
     ap.add_argument("--workload", default="c4", choices=sorted(WORKLOADS))
     ap.add_argument("--secondary", default="c2", help="workload measured after the main one (N=1; '' = none)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-records", type=int, default=200_000, help="records in the CPU baseline's sample")
+    ap.add_argument("--cpu-records", type=int, default=50_000, help="records in the single-threaded oracle's sample")
+    ap.add_argument("--cpu-mt-records", type=int, default=25_000_000, help="records in the multi-threaded baseline's sample")
+    ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16")),
+                    help="host threads of the multi-threaded CPU baseline")
     args = ap.parse_args()
 
     import torch
@@ -207,7 +210,7 @@ def main():
             s.eng.close()
         if world == 1 and not args.no_cpu_baseline:
             log(f"[rank 0] cpu baseline: first {args.cpu_records} records")
-            out["cpu_baseline"] = cpu_baseline(w.rp, args.cpu_records)
+            out["cpu_baseline"] = cpu_baseline(w.rp, args.cpu_records, args.cpu_mt_records, args.cpu_threads)
         print(json.dumps(out), flush=True)
     if distributed:
         dist.barrier()
@@ -268,18 +271,7 @@ def result_line(args, w, world, steps, ms_per_step, value, attr_ms, total_ms):
     }
 
 
-def cpu_baseline(rp, max_records, target_s=10.0, max_runs=40):
-    """The CPU oracle (a single-threaded C restatement of the reference's
-    offline analysis loop, oracle/nmg_oracle.c) timed on this host on a
-    bounded sample of the same workload: the first buffers (up to
-    `max_records` records) against the full object table, analysed
-    repeatedly until about `target_s` seconds of analysis time have
-    accumulated; rate = records / analysis seconds."""
-    import tempfile
-
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import pyoracle
-
+def _sample_replay(rp, max_records):
     from numamma_amd.replay import Replay
 
     n, recs = 0, 0
@@ -288,27 +280,65 @@ def cpu_baseline(rp, max_records, target_s=10.0, max_runs=40):
             break
         recs += b.linear().shape[0] // RECORD_BYTES
         n += 1
-    n = max(1, n)
-    sub = Replay(rp.nb_threads, rp.table, rp.buffers[:n])
-    runs, samples, secs = 0, 0, 0.0
+    return Replay(rp.nb_threads, rp.table, rp.buffers[:max(1, n)]), max(1, n)
+
+
+def cpu_baseline(rp, max_records, mt_records, threads, target_s=5.0, max_runs=20):
+    """CPU baselines timed on this host on bounded samples of the same
+    workload (the first buffers of the batch, against the full object table):
+
+    * value: the multi-threaded bit-exact C++ restatement
+      (oracle/nmg_cpu_mt.cpp, `threads` host threads) on the first
+      `mt_records` records, analysed repeatedly until about `target_s` seconds
+      of analysis + merge time; rate = records / (analysis + merge seconds);
+    * single_thread_oracle: the single-threaded C restatement of the
+      reference loop (oracle/nmg_oracle.c, which keeps the reference's linear
+      call-site list and page-block lists) on the first `max_records` records."""
+    import tempfile
+
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle
+
+    out = {}
     with tempfile.TemporaryDirectory() as d:
-        path = os.path.join(d, "sample.bin")
+        sub, n = _sample_replay(rp, mt_records)
+        path = os.path.join(d, "mt.bin")
         sub.write(path)
+        del sub
+        pyoracle.run_mt(path, None, threads=threads, levels=False)  # warm-up (first touch of the arrays)
+        runs, samples, secs = 0, 0, 0.0
+        while runs < max_runs and (runs == 0 or secs < target_s):
+            t = pyoracle.run_mt(path, None, threads=threads, levels=False)
+            log(f"[rank 0] cpu baseline (mt) run {runs}: {t['nb_samples']} records, analysis {t['analysis_s']:.2f}s "
+                f"+ merge {t['merge_s']:.2f}s on {t['threads']} threads")
+            runs += 1
+            samples += t["nb_samples"]
+            secs += t["analysis_s"] + t["merge_s"]
+        out = {
+            "value": samples / secs,
+            "unit": "samples/s",
+            "cores": threads,
+            "kind": "port",
+            "sample": f"first {n} of {len(rp.buffers)} buffers ({samples // runs} records, full object table) "
+                      f"analysed {runs}x by the multi-threaded bit-exact restatement (oracle/nmg_cpu_mt.cpp) on "
+                      f"{threads} threads, {secs:.1f}s of analysis + merge; host has {os.cpu_count()} CPUs",
+        }
+        os.remove(path)
+        sub, n = _sample_replay(rp, max_records)
+        path = os.path.join(d, "st.bin")
+        sub.write(path)
+        runs, samples, secs = 0, 0, 0.0
         while runs < max_runs and (runs == 0 or secs < target_s):
             t = pyoracle.run(path, os.path.join(d, "out"), os.path.join(d, "stdout.txt"))
-            log(f"[rank 0] cpu baseline run {runs}: {t['nb_samples']} records in {t['analysis_s']:.2f}s")
+            log(f"[rank 0] cpu baseline (oracle) run {runs}: {t['nb_samples']} records in {t['analysis_s']:.2f}s")
             runs += 1
             samples += t["nb_samples"]
             secs += t["analysis_s"]
-    return {
-        "value": samples / secs,
-        "unit": "samples/s",
-        "cores": 1,
-        "kind": "port",
-        "sample": f"first {n} of {len(rp.buffers)} buffers ({samples // runs} records, full object table) analysed "
-                  f"{runs}x, {secs:.1f}s of analysis loop; single-threaded like the reference "
-                  f"(global mutex, mem_analyzer.c:254); host has {os.cpu_count()} CPUs",
-    }
+        out["single_thread_oracle"] = {
+            "value": samples / secs, "cores": 1,
+            "sample": f"first {n} buffers ({samples // runs} records) analysed {runs}x, {secs:.1f}s of analysis loop; "
+                      "single-threaded like the reference (global mutex, mem_analyzer.c:254)"}
+    return out
 
 
 if __name__ == "__main__":

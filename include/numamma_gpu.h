@@ -99,6 +99,18 @@ struct nmg_options {
   uint32_t copy_threads;     /* host threads for nmg_submit_buffers copies (0 = 1) */
   uint64_t hist_budget_bytes; /* dense page-histogram arena cap (0 = default 4 GiB) */
   uint64_t sparse_capacity;   /* sparse (object, page, thread) slots (0 = default 1<<22) */
+  /* Multi-GPU from one host process: nb_gpus > 1 shards the
+   * submitted buffer list over the GPUs devices[0..nb_gpus) (NULL: device,
+   * device + 1, ...) in contiguous byte-balanced ranges, replicates the
+   * object table, and merges the per-GPU counters into this handle at
+   * nmg_analyze -- RCCL reduces over xGMI (sum / min / max) when the devices
+   * are distinct, a device-side merge when they are one device (testing).
+   * Results, getters and nmg_report read the merged counters.  Such an engine
+   * takes host buffers (nmg_submit_*); device-resident buffers and streaming
+   * stay single-GPU.  0 or 1: one GPU, `device`. */
+  uint32_t nb_gpus;
+  uint32_t reserved;
+  const int32_t *devices;
 };
 
 struct nmg_report_options {

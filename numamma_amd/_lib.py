@@ -93,6 +93,9 @@ class nmg_options(C.Structure):
         ("copy_threads", C.c_uint32),
         ("hist_budget_bytes", C.c_uint64),
         ("sparse_capacity", C.c_uint64),
+        ("nb_gpus", C.c_uint32),
+        ("reserved", C.c_uint32),
+        ("devices", C.POINTER(C.c_int32)),
     ]
 
 

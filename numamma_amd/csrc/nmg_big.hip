@@ -34,7 +34,7 @@
 namespace nmg {
 
 #ifndef NMG_BIG_K
-#define NMG_BIG_K 3
+#define NMG_BIG_K 2
 #endif
 constexpr int kBK = NMG_BIG_K;             // records per lane per window
 constexpr uint32_t kBWin = kBWG * kBK;     // 1536 stride slots
@@ -43,11 +43,7 @@ constexpr uint32_t kBTableWindows = 128;   // hashed LDS tables flushed at least
 constexpr uint32_t kBPageBuckets = 768;    // LDS page cells: 8-slot buckets
 constexpr uint32_t kBPageSlots = kBPageBuckets * 8;
 static_assert(kBK * kBDrain <= 256, "lane accumulators: u16 counts, u32 sums of weights < 2^23");
-#ifdef NMG_BIG_EARLY_PREFETCH
-constexpr bool kEarlyPrefetch = true;  // next window's records issued before this window's lookups
-#else
-constexpr bool kEarlyPrefetch = false;
-#endif
+
 static_assert((uint64_t)kBTableWindows * kBWin < (1u << 20), "flushed slot counts");
 
 struct BigCounters {
@@ -210,24 +206,64 @@ __global__ __launch_bounds__(kBWG, 1) void attribute_big_kernel(Params p) {
     if (hb && n0 < kBWin && b.access == a.access && b.thread_rank == a.thread_rank)
       n1 = min(b.len / kRecBytes + (b.len % kRecBytes != 0), kBWin - n0);
   };
-  RawRec nx[kBK];
-  {
-    uint32_t n0, n1;
-    geometry(0, d0, d1, has1, n0, n1);
+  // the records of the window at (i, c): K stride slots per lane
+  auto issue = [&](uint32_t i, uint32_t c, RawRec (&raw)[kBK]) {
+    BufDesc a, b;
+    uint32_t n0 = 0, n1 = 0;
+    if (i < r1) {
+      a = p.sbufs[i];
+      b = i + 1 < r1 ? p.sbufs[i + 1] : a;
+      geometry(c, a, b, i + 1 < r1, n0, n1);
+    } else {
+      a = b = d0;
+    }
 #pragma unroll
     for (int k = 0; k < kBK; k++) {
       const uint32_t s = uint32_t(k) * kBWG + tid;
       const bool in1 = s >= n0, cand = s < n0 + n1;
-      const uint32_t pos = in1 ? (s - n0) * kRecBytes : s * kRecBytes;
-      load_rec(p.data + (in1 ? d1.offset : d0.offset), pos, cand ? (in1 ? d1.len : d0.len) : 0, nx[k]);
+      const uint32_t pos = in1 ? (s - n0) * kRecBytes : c + s * kRecBytes;
+      load_rec(p.data + (in1 ? b.offset : a.offset), pos, cand ? (in1 ? b.len : a.len) : 0, raw[k]);
     }
-  }
+  };
+  // the position after window (i, c) when that window is regular (the fast
+  // path's successor; a slow-path window ends elsewhere, and the records
+  // loaded for a mispredicted window are reloaded)
+  auto fast_succ = [&](uint32_t i, uint32_t c, const BufDesc& a, const BufDesc& b, bool hb, uint32_t& si, uint32_t& sc) {
+    uint32_t n0, n1;
+    geometry(c, a, b, hb, n0, n1);
+    if (n1) {
+      si = i + 1;
+      sc = n1 * kRecBytes;
+      if (sc >= b.len) {
+        si = i + 2;
+        sc = 0;
+      }
+    } else {
+      si = i;
+      const uint64_t e = uint64_t(c) + uint64_t(n0) * kRecBytes;
+      sc = (uint32_t)e;
+      if (e >= a.len) {
+        si = i + 1;
+        sc = 0;
+      }
+    }
+  };
+  // two windows of records in flight: window w's records were issued during
+  // window w - 2, after its directory loads, so no wait on a directory slot
+  // or on the next window's records includes a freshly issued stream load
+  RawRec nxA[kBK], nxB[kBK];
+  uint32_t pidx, pcur;  // predicted position of the window after the current one
+  issue(idx, 0, nxA);
+  fast_succ(idx, 0, d0, d1, has1, pidx, pcur);
+  issue(pidx, pcur, nxB);
+  bool pred_ok = true;  // the current window's records were loaded at its position
   LaneAcc acc;
   lane_acc_clear(acc);
   uint32_t win = 0, acc_windows = 0, last_flush = 0;
   uint32_t ns0 = 0, nf0 = 0, ns1 = 0, nf1 = 0;  // per-buffer tallies: buffers idx, idx + 1
 
-  while (true) {
+  auto window = [&](RawRec (&craw)[kBK], RawRec (&fraw)[kBK]) -> bool {
+    if (!pred_ok) issue(idx, cur, craw);  // mispredicted (after a slow-path window)
     uint32_t n0, n1;
     geometry(cur, d0, d1, has1, n0, n1);
     // ---- decode; fast-path check: every stride slot holds a whole 40 B record
@@ -241,7 +277,7 @@ __global__ __launch_bounds__(kBWG, 1) void attribute_big_kernel(Params p) {
       in1[k] = s >= n0;
       cand[k] = s < n0 + n1;
       pos[k] = in1[k] ? (s - n0) * kRecBytes : cur + s * kRecBytes;
-      r[k] = decode_rec(nx[k], pos[k]);
+      r[k] = decode_rec(craw[k], pos[k]);
       const uint32_t wlen = in1[k] ? d1.len : d0.len;
       bad |= cand[k] && (uint64_t(pos[k]) + kRecBytes > wlen || (r[k].hdr >> 48) != kRecBytes);
     }
@@ -353,19 +389,13 @@ __global__ __launch_bounds__(kBWG, 1) void attribute_big_kernel(Params p) {
     const bool nhas1 = nidx + 1 < r1;
     const bool stream_end = nidx != idx && (nidx >= r1 || nd0.access != cur_access || nd0.thread_rank != cur_thread);
 
+    // the next window's records (in flight in fraw) were loaded at pidx/pcur;
+    // predict the one after it (loaded into craw once this window's
+    // directory loads are issued)
+    const bool next_ok = nidx == pidx && (uint32_t)ncur == pcur;
+    uint32_t qidx = r1, qcur = 0;
+    if (nidx < r1) fast_succ(nidx, (uint32_t)ncur, nd0, nd1, nhas1, qidx, qcur);
     bool nxt_issued = false;
-    if (kEarlyPrefetch && nidx < r1) {
-      uint32_t m0, m1;
-      geometry((uint32_t)ncur, nd0, nd1, nhas1, m0, m1);
-#pragma unroll
-      for (int k = 0; k < kBK; k++) {
-        const uint32_t s = uint32_t(k) * kBWG + tid;
-        const bool i1 = s >= m0, c = s < m0 + m1;
-        const uint32_t ps = i1 ? (s - m0) * kRecBytes : (uint32_t)ncur + s * kRecBytes;
-        load_rec(p.data + (i1 ? nd1.offset : nd0.offset), ps, c ? (i1 ? nd1.len : nd0.len) : 0, nx[k]);
-      }
-      nxt_issued = true;
-    }
     const uint32_t access = d0.access, th = d0.thread_rank;
     uint64_t vm[kBK], fm[kBK];
     int64_t ent[kBK];
@@ -468,19 +498,9 @@ __global__ __launch_bounds__(kBWG, 1) void attribute_big_kernel(Params p) {
           fs[k][3] = q[3];
         }
       }
-      // the next window's records: issued after the slot loads, so the wait
-      // for a slot never includes the record stream
-      if (!nxt_issued && nidx < r1) {
-        uint32_t m0, m1;
-        geometry((uint32_t)ncur, nd0, nd1, nhas1, m0, m1);
-#pragma unroll
-        for (int k = 0; k < kBK; k++) {
-          const uint32_t s = uint32_t(k) * kBWG + tid;
-          const bool i1 = s >= m0, c = s < m0 + m1;
-          const uint32_t ps = i1 ? (s - m0) * kRecBytes : (uint32_t)ncur + s * kRecBytes;
-          load_rec(p.data + (i1 ? nd1.offset : nd0.offset), ps, c ? (i1 ? nd1.len : nd0.len) : 0, nx[k]);
-        }
-      }
+      // the records of the window after next: issued after the slot loads,
+      // so the wait for a slot never includes them
+      issue(qidx, qcur, craw);
       nxt_issued = true;
       // ---- stage 3: resolve from the slot (FatSlot layout, nmg_kernels.h)
 #pragma unroll
@@ -538,17 +558,7 @@ __global__ __launch_bounds__(kBWG, 1) void attribute_big_kernel(Params p) {
         baddr[k] = m.baddr;
       }
     }
-    if (!nxt_issued && nidx < r1) {
-      uint32_t m0, m1;
-      geometry((uint32_t)ncur, nd0, nd1, nhas1, m0, m1);
-#pragma unroll
-      for (int k = 0; k < kBK; k++) {
-        const uint32_t s = uint32_t(k) * kBWG + tid;
-        const bool i1 = s >= m0, c = s < m0 + m1;
-        const uint32_t ps = i1 ? (s - m0) * kRecBytes : (uint32_t)ncur + s * kRecBytes;
-        load_rec(p.data + (i1 ? nd1.offset : nd0.offset), ps, c ? (i1 ? nd1.len : nd0.len) : 0, nx[k]);
-      }
-    }
+    if (!nxt_issued) issue(qidx, qcur, craw);
 
     // ---- per-buffer tallies (mem_sampling.c:921-926) and the matched samples' counters
 #pragma unroll
@@ -688,7 +698,13 @@ __global__ __launch_bounds__(kBWG, 1) void attribute_big_kernel(Params p) {
     d0 = nd0;
     d1 = nd1;
     has1 = nhas1;
-    if (idx >= r1) break;  // the loop's only exit, after the state update
+    pred_ok = next_ok;
+    pidx = qidx;
+    pcur = qcur;
+    return idx >= r1;  // the loop's only exit, after the state update
+  };
+  // unrolled by two: the raw record buffers alternate without register copies
+  while (!window(nxA, nxB) && !window(nxB, nxA)) {
   }
   __syncthreads();  // the sub-logs' fill (every append of this workgroup is done)
   if (p.tlog)

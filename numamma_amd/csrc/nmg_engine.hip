@@ -3,7 +3,9 @@
 // stream-sorted schedule, the streaming pipeline (copy stream + double-buffered
 // pinned staging), launches and result downloads.  The kernels are in
 // nmg_kernels.hip (DESIGN.md "Kernels").
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <functional>
@@ -188,6 +190,16 @@ struct nmg_engine {
   std::string last_error;
   float last_ms = 0.f;
 
+  // multi-GPU (nmg_options.nb_gpus > 1): this handle holds the submitted
+  // buffers, the table and the merged counters; `workers` (one engine per
+  // device, worker 0 on this handle's device) analyse contiguous ranges
+  std::vector<nmg_engine*> workers;
+  std::vector<int> devices;
+  bool multi = false, multi_distinct = false, multi_pending = false;
+  std::vector<void*> comms;  // ncclComm_t per worker (distinct devices)
+  std::vector<uint8_t*> warena;
+  std::vector<size_t> warena_cap;
+
   // kDbgTiming (internal): per-wave phase cycles of the last launch
   uint64_t* d_dbg = nullptr;
   size_t dbg_cap = 0, dbg_len = 0;
@@ -297,13 +309,16 @@ static void free_table(nmg_engine* h) {
   h->d_dir = nullptr;
 }
 
+static int multi_create(nmg_engine* h, const nmg_options* opt);
+static void multi_destroy(nmg_engine* h);
+
 extern "C" int nmg_create(nmg_engine** out, const nmg_options* opt) {
   if (!out) return NMG_ERR_INVALID;
   *out = nullptr;
   nmg_engine* h = new (std::nothrow) nmg_engine();
   if (!h) return NMG_ERR_NOMEM;
   if (opt) {
-    h->device = opt->device;
+    h->device = opt->nb_gpus > 1 && opt->devices ? opt->devices[0] : opt->device;
     h->flags = opt->flags;
     h->T = opt->nb_threads ? opt->nb_threads : 1;
     h->copy_threads = opt->copy_threads ? opt->copy_threads : 1;
@@ -345,12 +360,21 @@ extern "C" int nmg_create(nmg_engine** out, const nmg_options* opt) {
   }
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, h->device) == hipSuccess) h->num_cus = prop.multiProcessorCount;
+  if (opt && opt->nb_gpus > 1) {
+    const int rc = multi_create(h, opt);
+    if (rc) {
+      g_create_error = h->last_error;
+      nmg_destroy(h);
+      return rc;
+    }
+  }
   *out = h;
   return NMG_OK;
 }
 
 extern "C" void nmg_destroy(nmg_engine* h) {
   if (!h) return;
+  multi_destroy(h);
   (void)hipSetDevice(h->device);
   if (h->stream) (void)hipStreamSynchronize(h->stream);
   free_table(h);
@@ -387,6 +411,10 @@ extern "C" void nmg_destroy(nmg_engine* h) {
 extern "C" int nmg_reset_counters(nmg_engine* h) {
   if (!h) return NMG_ERR_INVALID;
   if (!h->have_table) return fail(h, NMG_ERR_STATE, "nmg_reset_counters before nmg_set_objects");
+  for (nmg_engine* w : h->workers) {
+    const int rc = nmg_reset_counters(w);
+    if (rc) return fail(h, rc, w->last_error);
+  }
   HIP_TRY(h, hipSetDevice(h->device));
   ResetParams r;
   memset(&r, 0, sizeof(r));
@@ -707,6 +735,10 @@ extern "C" int nmg_set_objects(nmg_engine* h, const uint64_t* keys, const uint32
   }
   h->have_table = true;
   HIP_TRY(h, hipStreamSynchronize(h->stream));
+  for (nmg_engine* w : h->workers) {  // multi-GPU: the table on every device
+    const int rc = nmg_set_objects(w, keys, entry_off, nb_keys, entries, nb_entries);
+    if (rc) return fail(h, rc, w->last_error);
+  }
   return nmg_reset_counters(h);
 }
 
@@ -714,7 +746,8 @@ static int stage_reserve(nmg_engine* h, size_t need) {
   if (need <= h->stage_cap) return NMG_OK;
   size_t cap = std::max(need, h->stage_cap * 2 + (1u << 20));
   uint8_t* p = nullptr;
-  HIP_TRY(h, hipHostMalloc((void**)&p, cap, hipHostMallocDefault));
+  // (portable: a multi-GPU engine's workers copy from it on every device)
+  HIP_TRY(h, hipHostMalloc((void**)&p, cap, h->multi ? hipHostMallocPortable : hipHostMallocDefault));
   if (h->stage_len) memcpy(p, h->h_stage, h->stage_len);
   if (h->h_stage) {
     HIP_TRY(h, hipStreamSynchronize(h->stream));
@@ -980,6 +1013,7 @@ static int stream_append(nmg_engine* h, uint64_t len, uint32_t thread_rank, uint
 
 extern "C" int nmg_stream_begin(nmg_engine* h, uint64_t chunk_bytes, uint32_t copy_threads) {
   if (!h || copy_threads == 0) return NMG_ERR_INVALID;
+  if (h->multi) return fail(h, NMG_ERR_STATE, "streaming is single-GPU (nmg_options.nb_gpus <= 1)");
   if (h->external) return fail(h, NMG_ERR_STATE, "device buffers are set; call nmg_clear_buffers first");
   if (h->flags & NMG_F_SAMPLE_MATCHES)
     return fail(h, NMG_ERR_STATE, "dump modes (NMG_F_SAMPLE_MATCHES) need nmg_analyze over submitted buffers");
@@ -1050,6 +1084,7 @@ extern "C" int nmg_set_device_buffers(nmg_engine* h, const void* d_data, const u
                                       const uint32_t* access_types, uint32_t nb_buffers, uint64_t seq_base) {
   if (!h || (nb_buffers && (!d_data || !offsets || !lengths || !thread_ranks || !access_types)))
     return NMG_ERR_INVALID;
+  if (h->multi) return fail(h, NMG_ERR_STATE, "a multi-GPU engine takes host buffers (nmg_submit_*)");
   if (h->streaming || h->streamed) return fail(h, NMG_ERR_STATE, "streaming buffers are set; call nmg_clear_buffers first");
   std::vector<BufDesc> descs;
   std::vector<uint64_t> bytes;
@@ -1094,6 +1129,7 @@ extern "C" int nmg_clear_buffers(nmg_engine* h) {
     h->streamed = false;
     h->bufcnt_stride = 0;  // per-buffer counts restart (the array is kept)
   }
+  for (nmg_engine* w : h->workers) nmg_clear_buffers(w);
   h->descs.clear();
   h->buf_bytes.clear();
   h->stage_len = 0;
@@ -1422,9 +1458,13 @@ static int launch_attribution(nmg_engine* h, const uint8_t* data, const BufDesc*
 
 static int stream_flush(nmg_engine* h);
 
+static int multi_analyze(nmg_engine* h);
+static int multi_finish(nmg_engine* h);
+
 extern "C" int nmg_analyze(nmg_engine* h) {
   if (!h) return NMG_ERR_INVALID;
   if (!h->have_table) return fail(h, NMG_ERR_STATE, "nmg_analyze before nmg_set_objects");
+  if (h->multi) return multi_analyze(h);
   HIP_TRY(h, hipSetDevice(h->device));
   if (h->streaming) return stream_flush(h);  // earlier chunks are already enqueued
   if (h->streamed) return NMG_OK;             // nmg_stream_end flushed everything
@@ -1472,6 +1512,10 @@ static int decode_error_word(nmg_engine* h, uint64_t w) {
 
 extern "C" int nmg_synchronize(nmg_engine* h) {
   if (!h) return NMG_ERR_INVALID;
+  if (h->multi_pending) {
+    const int rc = multi_finish(h);
+    if (rc) return rc;
+  }
   HIP_TRY(h, hipSetDevice(h->device));
   HIP_TRY(h, hipStreamSynchronize(h->stream));
   if (h->launched) {  // the most recent launch's start / end events
@@ -1830,6 +1874,237 @@ extern "C" int nmg_set_buffer_counts(nmg_engine* h, uint32_t nb_buffers, const u
   h->ov_found.assign(nb_found, nb_found + nb_buffers);
   h->ov_bytes.assign(buffer_bytes, buffer_bytes + nb_buffers);
   return NMG_OK;
+}
+
+// ---------------------------------------------------------------------------
+// multi-GPU from one host process (nmg_options.nb_gpus > 1)
+
+// RCCL, loaded at run time (only distinct-device engines use it)
+struct Rccl {
+  void* so = nullptr;
+  decltype(&ncclCommInitAll) init_all = nullptr;
+  decltype(&ncclCommDestroy) destroy = nullptr;
+  decltype(&ncclReduce) reduce = nullptr;
+  decltype(&ncclGroupStart) group_start = nullptr;
+  decltype(&ncclGroupEnd) group_end = nullptr;
+  decltype(&ncclGetErrorString) error_string = nullptr;
+};
+static Rccl* rccl() {
+  static Rccl r;
+  static bool tried = false;
+  if (!tried) {
+    tried = true;
+    r.so = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    if (!r.so) r.so = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    if (r.so) {
+      r.init_all = (decltype(r.init_all))dlsym(r.so, "ncclCommInitAll");
+      r.destroy = (decltype(r.destroy))dlsym(r.so, "ncclCommDestroy");
+      r.reduce = (decltype(r.reduce))dlsym(r.so, "ncclReduce");
+      r.group_start = (decltype(r.group_start))dlsym(r.so, "ncclGroupStart");
+      r.group_end = (decltype(r.group_end))dlsym(r.so, "ncclGroupEnd");
+      r.error_string = (decltype(r.error_string))dlsym(r.so, "ncclGetErrorString");
+    }
+  }
+  return r.so && r.init_all && r.reduce && r.group_start && r.group_end ? &r : nullptr;
+}
+
+static int multi_create(nmg_engine* h, const nmg_options* opt) {
+  const uint32_t n = opt->nb_gpus;
+  for (uint32_t i = 0; i < n; i++) h->devices.push_back(opt->devices ? opt->devices[i] : opt->device + (int)i);
+  bool all_same = true, all_distinct = true;
+  for (uint32_t i = 0; i < n; i++)
+    for (uint32_t j = 0; j < i; j++) {
+      if (h->devices[i] != h->devices[j]) all_same = false;
+      else all_distinct = false;
+    }
+  if (!all_same && !all_distinct)
+    return fail(h, NMG_ERR_INVALID, "nb_gpus: devices must be all distinct (RCCL) or all one device (testing)");
+  for (uint32_t i = 0; i < n; i++) {
+    nmg_options o = *opt;
+    o.nb_gpus = 0;
+    o.devices = nullptr;
+    o.device = h->devices[i];
+    nmg_engine* w = nullptr;
+    const int rc = nmg_create(&w, &o);
+    if (rc) return fail(h, rc, "worker engine on device " + std::to_string(h->devices[i]) + ": " + g_create_error);
+    h->workers.push_back(w);
+  }
+  h->warena.assign(n, nullptr);
+  h->warena_cap.assign(n, 0);
+  h->multi = true;
+  h->multi_distinct = all_distinct;
+  if (all_distinct) {
+    Rccl* r = rccl();
+    if (!r) return fail(h, NMG_ERR_HIP, "librccl.so.1 not loadable (multi-GPU merge)");
+    std::vector<ncclComm_t> c(n);
+    const ncclResult_t e = r->init_all(c.data(), (int)n, h->devices.data());
+    if (e != ncclSuccess) return fail(h, NMG_ERR_HIP, std::string("ncclCommInitAll: ") + r->error_string(e));
+    for (auto x : c) h->comms.push_back(x);
+  }
+  return NMG_OK;
+}
+
+static void multi_destroy(nmg_engine* h) {
+  if (!h->multi) return;
+  for (size_t i = 0; i < h->workers.size(); i++) {
+    if (h->warena[i]) {
+      (void)hipSetDevice(h->workers[i]->device);
+      (void)hipFree(h->warena[i]);
+    }
+  }
+  if (Rccl* r = rccl())
+    for (void* c : h->comms) r->destroy((ncclComm_t)c);
+  for (nmg_engine* w : h->workers) nmg_destroy(w);
+  h->workers.clear();
+  h->comms.clear();
+  h->multi = false;
+}
+
+// Shard the submitted buffers (analysis order) into contiguous byte-balanced
+// ranges, one per worker: H2D from this handle's pinned staging into the
+// worker's arena, analysed there with its global analysis index (seq_base);
+// then merge every worker's counters into this handle (sum / min / max):
+// RCCL reduces to worker 0 then a device add into this handle (distinct
+// devices), or device-side merges (one device).  Per-buffer counts and sparse
+// cells are gathered at nmg_synchronize (multi_finish).
+static int multi_analyze(nmg_engine* h) {
+  if (h->multi_pending) {
+    const int rc = multi_finish(h);
+    if (rc) return rc;
+  }
+  const uint32_t n = (uint32_t)h->workers.size(), nb = (uint32_t)h->descs.size();
+  std::vector<uint64_t> csum(nb + 1, 0);
+  for (uint32_t b = 0; b < nb; b++) csum[b + 1] = csum[b] + h->descs[b].len + 64;
+  std::vector<uint32_t> cut(n + 1, nb);
+  cut[0] = 0;
+  for (uint32_t i = 1; i < n; i++)
+    cut[i] = std::max(cut[i - 1], (uint32_t)(std::lower_bound(csum.begin(), csum.end(), csum[nb] * i / n) - csum.begin()));
+  for (uint32_t i = 0; i < n; i++) {
+    nmg_engine* w = h->workers[i];
+    const uint32_t a = cut[i], b = cut[i + 1];
+    std::vector<uint64_t> offs, lens;
+    std::vector<uint32_t> ranks, acc;
+    const uint64_t base = a < b ? h->descs[a].offset : 0;
+    const uint64_t span = a < b ? h->descs[b - 1].offset + h->descs[b - 1].len - base : 0;
+    for (uint32_t k = a; k < b; k++) {
+      offs.push_back(h->descs[k].offset - base);
+      lens.push_back(h->descs[k].len);
+      ranks.push_back(h->descs[k].thread_rank);
+      acc.push_back(h->descs[k].access);
+    }
+    HIP_TRY(h, hipSetDevice(w->device));
+    if (span + 64 > h->warena_cap[i]) {
+      HIP_TRY(h, hipStreamSynchronize(w->stream));
+      (void)hipFree(h->warena[i]);
+      h->warena[i] = nullptr;
+      h->warena_cap[i] = span + 64;
+      HIP_TRY(h, hipMalloc(&h->warena[i], h->warena_cap[i]));
+    }
+    if (span) HIP_TRY(h, hipMemcpyAsync(h->warena[i], h->h_stage + base, span, hipMemcpyHostToDevice, w->stream));
+    int rc = nmg_set_device_buffers(w, h->warena[i], offs.data(), lens.data(), ranks.data(), acc.data(), b - a, a);
+    if (!rc) rc = nmg_analyze(w);
+    if (rc) return fail(h, rc, w->last_error);
+  }
+  struct Arr {
+    int which, op;
+  };
+  const Arr arrs[4] = {{NMG_ARR_SUM64, 0}, {NMG_ARR_MIN64, 1}, {NMG_ARR_MAX64, 2}, {NMG_ARR_HIST32, 3}};
+  if (h->multi_distinct) {  // RCCL reduce to worker 0 (in place), over xGMI
+    Rccl* r = rccl();
+    HIP_TRY(h, hipSetDevice(h->device));
+    r->group_start();
+    for (const Arr& x : arrs) {
+      for (uint32_t i = 0; i < n; i++) {
+        nmg_engine* w = h->workers[i];
+        size_t bytes = 0;
+        void* p = array_ptr(w, x.which, &bytes);
+        void* root = array_ptr(h->workers[0], x.which, &bytes);
+        if (!bytes) continue;
+        const ncclRedOp_t op = x.op == 1 ? ncclMin : (x.op == 2 ? ncclMax : ncclSum);
+        const ncclDataType_t dt = x.op == 3 ? ncclUint32 : ncclUint64;
+        const size_t count = bytes / (x.op == 3 ? 4 : 8);
+        const ncclResult_t e = r->reduce(p, i == 0 ? root : p, count, dt, op, 0, (ncclComm_t)h->comms[i], w->stream);
+        if (e != ncclSuccess) {
+          r->group_end();
+          return fail(h, NMG_ERR_HIP, std::string("ncclReduce: ") + r->error_string(e));
+        }
+      }
+    }
+    const ncclResult_t e = r->group_end();
+    if (e != ncclSuccess) return fail(h, NMG_ERR_HIP, std::string("ncclGroupEnd: ") + r->error_string(e));
+  }
+  // this handle += worker 0 (distinct: the reduced arrays) or += every worker (one device)
+  HIP_TRY(h, hipSetDevice(h->device));
+  for (uint32_t i = 0; i < (h->multi_distinct ? 1u : n); i++) {
+    nmg_engine* w = h->workers[i];
+    hipEvent_t ev;
+    HIP_TRY(h, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    HIP_TRY(h, hipEventRecord(ev, w->stream));
+    HIP_TRY(h, hipStreamWaitEvent(h->stream, ev, 0));
+    (void)hipEventDestroy(ev);
+    for (const Arr& x : arrs) {
+      size_t bytes = 0, wb = 0;
+      void* dst = array_ptr(h, x.which, &bytes);
+      const void* src = array_ptr(w, x.which, &wb);
+      if (bytes) HIP_TRY(h, launch_merge(h->stream, dst, src, bytes / (x.op == 3 ? 4 : 8), x.op));
+    }
+  }
+  h->multi_pending = true;
+  h->launched = false;
+  return NMG_OK;
+}
+
+// after the merges: per-buffer counts (concatenated in analysis order) and
+// sparse cells (summed by key) into this handle; the workers are reset so
+// that a later nmg_analyze adds only its own samples
+static int multi_finish(nmg_engine* h) {
+  h->multi_pending = false;
+  for (nmg_engine* w : h->workers) {
+    const int rc = nmg_synchronize(w);
+    if (rc) return fail(h, rc, w->last_error);
+  }
+  HIP_TRY(h, hipSetDevice(h->device));
+  HIP_TRY(h, hipStreamSynchronize(h->stream));
+  std::vector<uint32_t> ns, nf;
+  std::vector<uint64_t> keys;
+  std::vector<uint32_t> vals;
+  std::vector<uint64_t> k0;
+  std::vector<uint32_t> v0;
+  int rc = sparse_download(h, k0, v0);
+  if (rc) return rc;
+  keys.insert(keys.end(), k0.begin(), k0.end());
+  vals.insert(vals.end(), v0.begin(), v0.end());
+  for (nmg_engine* w : h->workers) {
+    const uint32_t nb = nmg_get_nb_buffers(w);
+    std::vector<uint32_t> a(nb), b(nb);
+    rc = nmg_get_buffer_counts(w, a.data(), b.data());
+    if (rc) return fail(h, rc, w->last_error);
+    ns.insert(ns.end(), a.begin(), a.end());
+    nf.insert(nf.end(), b.begin(), b.end());
+    rc = sparse_download(w, k0, v0);
+    if (rc) return fail(h, rc, w->last_error);
+    keys.insert(keys.end(), k0.begin(), k0.end());
+    vals.insert(vals.end(), v0.begin(), v0.end());
+    rc = nmg_reset_counters(w);
+    if (rc) return fail(h, rc, w->last_error);
+  }
+  if (h->d_sparse_keys) {
+    std::vector<size_t> ord(keys.size());
+    for (size_t i = 0; i < ord.size(); i++) ord[i] = i;
+    std::sort(ord.begin(), ord.end(), [&](size_t a, size_t b) { return keys[a] < keys[b]; });
+    std::vector<uint64_t> mk;
+    std::vector<uint32_t> mv;
+    for (size_t i : ord) {
+      if (!mk.empty() && mk.back() == keys[i]) mv.back() += vals[i];
+      else {
+        mk.push_back(keys[i]);
+        mv.push_back(vals[i]);
+      }
+    }
+    rc = nmg_sparse_import(h, mk.data(), mv.data(), (int64_t)mk.size());
+    if (rc) return rc;
+  }
+  return nmg_set_buffer_counts(h, (uint32_t)ns.size(), ns.data(), nf.data(), h->buf_bytes.data());
 }
 
 extern "C" int nmg_report(nmg_engine* h, const nmg_object_meta* meta, const nmg_report_options* opts,

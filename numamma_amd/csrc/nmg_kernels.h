@@ -244,6 +244,7 @@ hipError_t launch_unpack(uint32_t grid, hipStream_t s, uint64_t* sum64, unsigned
                          uint32_t nb_entries, uint32_t shift);
 hipError_t launch_reset(uint32_t grid, hipStream_t s, const ResetParams& r);
 hipError_t launch_plog_reduce(uint32_t parts, hipStream_t s, const PlogParams& r);
+hipError_t launch_merge(hipStream_t s, void* dst, const void* src, uint64_t n, int op);
 // large tables (nmg_big.hip)
 #ifndef NMG_BIG_WG
 #define NMG_BIG_WG 512

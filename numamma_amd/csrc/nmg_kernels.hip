@@ -28,6 +28,8 @@
 //     bit-exact;
 //   * the long-tail log's range reduce, the packed-counter fold and the
 //     counter reset; the host side is nmg_engine.hip.
+#include <algorithm>
+
 #include "nmg_device.h"
 
 namespace nmg {
@@ -1063,6 +1065,21 @@ __global__ __launch_bounds__(256) void reset_kernel(ResetParams r) {
   for (uint64_t i = i0; i < r.n_bufcnt; i += stride) r.bufcnt[i] = 0;
 }
 
+// Multi-GPU merge when the shards share one device: dst op= src over n words
+// (op 0: u64 sum, 1: u64 min, 2: u64 max, 3: u32 sum).
+__global__ __launch_bounds__(256) void merge_kernel(void* dst, const void* src, uint64_t n, int op) {
+  const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
+  for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) {
+    if (op == 3) {
+      reinterpret_cast<uint32_t*>(dst)[i] += reinterpret_cast<const uint32_t*>(src)[i];
+    } else {
+      uint64_t& d = reinterpret_cast<uint64_t*>(dst)[i];
+      const uint64_t v = reinterpret_cast<const uint64_t*>(src)[i];
+      d = op == 0 ? d + v : (op == 1 ? min(d, v) : max(d, v));
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------
 // launchers
 
@@ -1096,6 +1113,13 @@ hipError_t launch_unpack(uint32_t grid, hipStream_t s, uint64_t* sum64, unsigned
 
 hipError_t launch_plog_reduce(uint32_t parts, hipStream_t s, const PlogParams& r) {
   hipLaunchKernelGGL(plog_reduce_kernel, dim3(parts), dim3(1024), 0, s, r);
+  return hipGetLastError();
+}
+
+hipError_t launch_merge(hipStream_t s, void* dst, const void* src, uint64_t n, int op) {
+  if (!n) return hipSuccess;
+  const uint32_t grid = (uint32_t)std::min<uint64_t>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(merge_kernel, dim3(grid), dim3(256), 0, s, dst, src, n, op);
   return hipGetLastError();
 }
 

@@ -29,8 +29,14 @@ def counters_to_numpy(c: "_lib.nmg_mem_counters") -> np.ndarray:
 
 class Engine:
     def __init__(self, device: int = 0, flags: int = _lib.NMG_F_DEFAULT, nb_threads: int = 1,
-                 hist_budget_bytes: int = 0, sparse_capacity: int = 0, copy_threads: int = 1):
-        opt = _lib.nmg_options(device, flags, nb_threads, copy_threads, hist_budget_bytes, sparse_capacity)
+                 hist_budget_bytes: int = 0, sparse_capacity: int = 0, copy_threads: int = 1,
+                 devices=None):
+        """devices: a list of GPU ordinals -> one engine sharding its host
+        buffers over those GPUs (nmg_options.nb_gpus / devices)."""
+        devs = (C.c_int32 * max(1, len(devices or [])))(*(devices or [device]))
+        self._devs = devs
+        opt = _lib.nmg_options(device, flags, nb_threads, copy_threads, hist_budget_bytes, sparse_capacity,
+                               len(devices) if devices else 0, 0, devs if devices else None)
         h = _lib.H()
         check(lib.nmg_create(C.byref(h), C.byref(opt)))
         self.h = h
