@@ -72,17 +72,10 @@ __device__ __forceinline__ int big_page_slot(BigCounters& bc, uint32_t key) {
   return j < 0 ? -1 : (int)(hb * 8 + (uint32_t)j);
 }
 
-// one long-tail object contribution (24 B record, tlog_reduce_kernel)
+// one long-tail object contribution (tlog_put, tlog_reduce_kernel)
 __device__ __forceinline__ bool big_tlog_append(const Params& p, BigCounters& bc, uint32_t e, uint32_t a, uint32_t cnt,
                                                 uint64_t wt, uint64_t ord) {
-  const uint32_t part = e >> p.tlog_rshift;
-  const uint32_t k = atomicAdd(&bc.tcur[part], 1u);
-  if (k >= p.tlog_cap) return false;
-  unsigned long long* r = p.tlog + ((uint64_t(blockIdx.x) * p.tlog_parts + part) * p.tlog_cap + k) * 3;
-  r[0] = (unsigned long long)(e | (a << 31)) | ((unsigned long long)cnt << 32);
-  r[1] = wt;
-  r[2] = ord;
-  return true;
+  return tlog_put(p, bc.tcur, e, a, cnt, wt, ord);
 }
 
 // page contribution straight to the histogram (the page log is full or off)

@@ -195,6 +195,30 @@ __device__ __forceinline__ void lane_acc_drain(LaneAcc& a, unsigned long long* s
 }
 
 
+// One long-tail object contribution of this workgroup (kTlogHead layouts,
+// nmg_kernels.h) to the sub-log of entry e's range; false when it is full
+// (the caller then takes the packed or plain atomics).
+__device__ __forceinline__ bool tlog_put(const Params& p, unsigned int* tcur, uint32_t e, uint32_t a, uint32_t cnt,
+                                         uint64_t wt, uint64_t ord) {
+  const uint32_t part = e >> p.tlog_rshift;
+  const bool one = cnt == 1 && wt < (1ull << 32);
+  const uint32_t k = atomicAdd(&tcur[part], one ? 1u : 2u);
+  if (k >= p.tlog_cap) return false;
+  uint4* r = p.tlog + (uint64_t(blockIdx.x) * p.tlog_parts + part) * p.tlog_cap + k;
+  const uint32_t ea = e | (a << 31);
+  if (one) {
+    r[0] = make_uint4(ea, (uint32_t)wt, (uint32_t)ord, (uint32_t)(ord >> 32));
+    return true;
+  }
+  if (k + 1 >= p.tlog_cap) {  // only the last slot left: marked dead (skipped like a continuation)
+    r[0] = make_uint4(0, 0, kTlogCont, 0);
+    return false;
+  }
+  r[0] = make_uint4(ea, cnt, kTlogHead, (uint32_t)(ord >> 32));
+  r[1] = make_uint4((uint32_t)wt, (uint32_t)(wt >> 32), kTlogCont, (uint32_t)ord);
+  return true;
+}
+
 // ---------------------------------------------------------------------------
 // record loads straight into registers
 

@@ -128,7 +128,7 @@ struct nmg_engine {
   uint32_t* d_sparse_dirty = nullptr;  // [2] parity flags (see reset_kernel)
   uint32_t* d_smatch = nullptr;        // NMG_F_SAMPLE_MATCHES: per 8 B of the arena span
   unsigned long long* d_pk64 = nullptr;  // hashed object mode: packed long-tail counters (0 between launches)
-  unsigned long long* d_tlog = nullptr;  // hashed object mode: long-tail log (see Params::tlog)
+  uint4* d_tlog = nullptr;  // hashed object mode: long-tail log (see Params::tlog)
   size_t tlog_bytes = 0;
   uint32_t* d_tlog_cnt = nullptr;
   size_t tlog_cnt_cap = 0;
@@ -1233,8 +1233,9 @@ static void ensure_occupancy(nmg_engine* h) {
   }
 }
 
-// large tables go through attribute_big_kernel (kDbgOldBig: attribute_kernel)
-static bool use_big(const nmg_engine* h) { return h->K > kLdsNodes && !(h->flags & kDbgOldBig); }
+// large tables go through attribute_kernel's directory + node-record path;
+// kDbgBigKernel routes them through attribute_big_kernel (A/B, tests)
+static bool use_big(const nmg_engine* h) { return h->K > kLdsNodes && (h->flags & kDbgBigKernel); }
 
 // persistent grid: one resident workgroup per slot, each with a byte-balanced range
 static uint32_t attribution_grid(nmg_engine* h, uint32_t nb) {
@@ -1285,7 +1286,9 @@ static int launch_attribution(nmg_engine* h, const uint8_t* data, const BufDesc*
   // dense LDS tables when the table is small enough (DESIGN.md "Kernels");
   // large tables: attribute_big_kernel, hashed tables only
   const bool big = use_big(h);
-  int mode = big ? 0 : (h->E <= kObjSlots ? kModeDenseObj : 0) | (h->hist_cells <= kDensePageCells ? kModeDensePage : 0);
+  int mode = big ? 0
+                 : (h->E <= kObjSlots ? kModeDenseObj : 0) | (h->hist_cells <= kDensePageCells ? kModeDensePage : 0) |
+                       (p.lds_nodes ? 0 : kModeLarge);
   if (big) {
     p.fat = h->d_fat;
     p.fatshift = h->d_fatshift;
@@ -1314,8 +1317,8 @@ static int launch_attribution(nmg_engine* h, const uint8_t* data, const BufDesc*
     // sub-log only sends its overflow to the atomics
     const uint64_t cap = (h->flags & kDbgTinyLog)
                              ? 2
-                             : std::min<uint64_t>(1u << 20, (nbytes / kRecBytes) / ((uint64_t)grid * parts) + 32);
-    const size_t need = (size_t)grid * parts * cap * 24;
+                             : std::min<uint64_t>(1u << 20, (nbytes / kRecBytes) / ((uint64_t)grid * parts) * 5 / 4 + 32);
+    const size_t need = (size_t)grid * parts * cap * sizeof(uint4);  // (16 B slots; flushed slots take two)
     if (need > h->tlog_bytes || (size_t)grid * parts > h->tlog_cnt_cap) {
       HIP_TRY(h, hipStreamSynchronize(h->stream));  // an earlier launch may still read the old log
       if (need > h->tlog_bytes) {

@@ -34,6 +34,12 @@ constexpr uint32_t kObjSlots = 2048;           // entry -> (count, weight, first
 // long-tail log (hashed object mode): per workgroup, kLogParts sub-logs by
 // entry range of 24 B records {entry | access << 31, count, weight, ordinal}
 constexpr uint32_t kLogParts = 256;
+// Long-tail log slots (16 B, one store): a sample (count 1, weight < 2^32)
+// is {entry | access << 31, weight, offset, seq}; anything else takes two
+// slots, {entry | access << 31, count, kTlogHead, ord >> 32} then
+// {weight lo, weight hi, kTlogCont, ord & ~0u}.  Offsets are 8-aligned, so
+// the two marks never occur as a sample's offset.
+constexpr uint32_t kTlogHead = 0xFFFFFFFFu, kTlogCont = 0xFFFFFFFEu;
 constexpr uint32_t kLogChunk = 4096;   // entries per LDS pass of tlog_reduce_kernel
 constexpr uint32_t kLogMaxGrid = 1024;  // attribution workgroups a log can serve
 // page-cell log (large tables, hashed page cells): cells that miss the LDS
@@ -56,6 +62,7 @@ constexpr uint32_t kTableWindows = 256;
 //                   kDensePageWindows windows (<= 1024 samples per cell each,
 //                   so a u16 cannot overflow into its neighbour)
 constexpr int kModeDenseObj = 1, kModeDensePage = 2;
+constexpr int kModeLarge = 4;  // more than kLdsNodes keys: LDS fences + directory + node records in global memory
 constexpr uint32_t kDensePageCells = kPageSlots * 4;  // the page table's 56 KiB as u16 cells
 constexpr uint32_t kDensePageWindows = 62;
 constexpr bool kPackObj = true;
@@ -127,7 +134,7 @@ struct FatSlot {
 static_assert(sizeof(FatSlot) == 64, "FatSlot");
 constexpr uint32_t kFatFlag = 0x80000000u;
 constexpr uint32_t kSzOlder = 0x80000000u, kSzBig = 0x40000000u, kSzMask = 0x3fffffffu;
-constexpr uint32_t kDbgOldBig = 0x10000;  // large tables through attribute_kernel (A/B, tests)
+constexpr uint32_t kDbgBigKernel = 0x10000;  // large tables through attribute_big_kernel (A/B, tests)
 
 struct Params {
   const uint8_t* data;
@@ -176,7 +183,7 @@ struct Params {
   // and flushed slots append to sub-log (workgroup, entry >> tlog_rshift);
   // tlog_reduce_kernel sums each entry range from LDS.  A full sub-log falls
   // back to the atomics.
-  unsigned long long* tlog;  // [grid][tlog_parts][tlog_cap][3] u64; null: off
+  uint4* tlog;               // [grid][tlog_parts][tlog_cap] 16 B slots (TlogSlot layouts); null: off
   uint32_t* tlog_cnt;        // [grid][tlog_parts] records written
   uint32_t tlog_cap, tlog_rshift, tlog_parts;
   // page-cell log (see kPlogMaxParts): [grid][plog_parts][plog_cap] records
@@ -209,7 +216,7 @@ struct PlogParams {
 
 // tlog_reduce_kernel (long-tail log, see Params::tlog)
 struct TlogParams {
-  const unsigned long long* tlog;
+  const uint4* tlog;
   const uint32_t* tlog_cnt;
   uint64_t* sum64;
   uint64_t* min64;

@@ -48,11 +48,12 @@ namespace nmg {
 // A lane's lookup of the next window started early (large tables): the fence
 // node of `addr` and, when the lookup needs it, its directory slot, loaded
 // while the current window is processed.  Valid for a record whose address
-// equals `addr` (idx 0: none).
+// on the record the lane processes in that window when it is a fast-path
+// window (`on`; idx 0: none).
 struct SpecDir {
-  uint64_t addr;
   uint32_t idx;
   uint2 de;
+  bool on;
 };
 
 
@@ -73,7 +74,7 @@ __device__ __forceinline__ const uint2* dir_slot(const Params& p, const uint64_t
 
 __device__ __forceinline__ uint32_t lower_key(const Params& p, const uint64_t* s_fences, const uint8_t* s_shift,
                                               uint64_t addr, const SpecDir& sp) {
-  const bool spec = sp.idx != 0 && sp.addr == addr;
+  const bool spec = sp.idx != 0 && sp.on;
   const uint32_t idx = spec ? sp.idx : fence_node(s_fences, addr);
   if (idx == 0) return p.nb_keys;                    // addr < first key
   // in-order rank of Eytzinger node idx at depth d of a complete tree
@@ -194,13 +195,14 @@ __device__ __forceinline__ bool plog_append(const Params& p, uint32_t* pcur, uin
 // __ma_find_mem_info_from_sample_generic (mem_analyzer.c:249-286): the
 // lower-bound node only (ht_lower_key, tools/hash.c:63-77), newest entry
 // first, inclusive timestamp window (is_sample_in_buffer, :141-155).
+template <int MODE>
 __device__ __forceinline__ Match find_entry(const Params& p, const Lookup& L, uint64_t addr, uint64_t ts,
                                             const SpecDir& sp) {
   Match m;
   m.e = -1;
   m.baddr = 0;
   m.hist = kHistSparse;
-  if (p.lds_nodes) {
+  if (!(MODE & kModeLarge)) {
     // Eytzinger tree: node i has children 2i, 2i+1; a fixed number of levels,
     // one LDS read each, branch-free.  The levels above the 7th fit in one
     // 256 B bank row, so the search is conflict-free where every lane reads.
@@ -238,25 +240,34 @@ __device__ __forceinline__ Match find_entry(const Params& p, const Lookup& L, ui
 // when the sub-log is full (the caller then issues the global atomics).
 __device__ __forceinline__ bool tlog_append(const Params& p, WgCounters& wc, uint32_t e, uint32_t a, uint32_t cnt,
                                             uint64_t wt, uint64_t ord) {
-  const uint32_t part = e >> p.tlog_rshift;
-  const uint32_t k = atomicAdd(&wc.tcur[part], 1u);
-  if (k >= p.tlog_cap) return false;
-  unsigned long long* r = p.tlog + ((uint64_t(blockIdx.x) * p.tlog_parts + part) * p.tlog_cap + k) * 3;
-  r[0] = (unsigned long long)(e | (a << 31)) | ((unsigned long long)cnt << 32);
-  r[1] = wt;
-  r[2] = ord;
-  return true;
+  return tlog_put(p, wc.tcur, e, a, cnt, wt, ord);
+}
+
+// kDbgTiming sub-phases of the window's processing (per wave, cycles)
+struct SubTimer {
+  uint64_t acc[7];
+  uint64_t last;
+};
+template <bool TIMING>
+__device__ __forceinline__ void sub_stamp(SubTimer& st, int i) {
+  if (TIMING) {
+    const uint64_t t = stamp();
+    st.acc[i] += t - st.last;
+    st.last = t;
+  }
 }
 
 // Process one decoded record (`valid` = it is a SAMPLE).  Every lane of the
 // wave calls this together (wave-level reductions inside); vmask / fmask are
 // the wave's SAMPLE and matched lanes.
-template <int MODE>
-__device__ __forceinline__ void process_sample(Params& p, WgCounters& wc, LaneAcc& acc, const Lookup& L,
+template <int MODE, bool TIMING>
+__device__ __forceinline__ void process_sample(Params& p, WgCounters& wc, LaneAcc& acc, const Lookup& L, SubTimer& st,
                                                bool valid, bool shortrec, uint64_t ts, uint64_t addr,
                                                uint64_t w, uint64_t dsrc, uint32_t access,
-                                               uint32_t th, uint64_t seq, uint32_t off, uint64_t rbase,
+                                               uint32_t th, const BufDesc& b0, const BufDesc& b1, bool in1, uint32_t off,
                                                uint64_t& vmask, uint64_t& fmask, const SpecDir& sp) {
+  // (the lane's buffer: b1 when in1; selected where used, so no 64-bit
+  // per-lane copy stays live across the window)
   const uint32_t lvl = uint32_t(dsrc >> 5) & 0x3fff;  // data_src.mem_lvl
   // ---- global counters: update_counters(global_counters, ...) (mem_sampling.c:882)
   vmask = __ballot(valid);
@@ -300,17 +311,19 @@ __device__ __forceinline__ void process_sample(Params& p, WgCounters& wc, LaneAc
       }
     }
   }
+  sub_stamp<TIMING>(st, 0);
   if (!(p.flags & NMG_F_MATCH_SAMPLES)) return;
 
   // ---- __match_sample (mem_sampling.c:594-673)
   Match m;
   m.e = -1;
-  if (valid) m = find_entry(p, L, addr, ts, sp);
+  if (valid) m = find_entry<MODE>(p, L, addr, ts, sp);
   const int64_t e = m.e;
   fmask = __ballot(e >= 0);
+  sub_stamp<TIMING>(st, 1);
   // dump modes: every SAMPLE record's match at its arena position (host
   // formats the per-sample lines in analysis order)
-  if (p.smatch && valid) p.smatch[(rbase + off) >> 3] = e >= 0 ? (uint32_t)e + 1u : 0u;
+  if (p.smatch && valid) p.smatch[((in1 ? b1.offset : b0.offset) + off) >> 3] = e >= 0 ? (uint32_t)e + 1u : 0u;
   if (e < 0 || (p.flags & kDbgNoTables)) return;
   // per-object counters, aggregated per stream in LDS.  (Admitting an entry
   // only on its second sample -- a doorkeeper bitset -- was measured slower at
@@ -318,7 +331,7 @@ __device__ __forceinline__ void process_sample(Params& p, WgCounters& wc, LaneAc
   // (with packing, a slot only sums packable weights: its flush is packed too)
   const bool pk = !(MODE & kModeDenseObj) && p.pk64 && w < p.pk_wlim && !shortrec;
   const int os = (MODE & kModeDenseObj) ? (int)e : ((p.pk64 && !pk) ? -1 : obj_slot(wc, (uint32_t)e));
-  const unsigned long long ord = (seq << 32) | off;  // first match in analysis order (quirk Q7)
+  const unsigned long long ord = ((in1 ? b1.seq : b0.seq) << 32) | off;  // first match in analysis order (quirk Q7)
   if ((MODE & kModeDenseObj) && w < kLaneMaxWeight && kPackObj) {
     // one packed add: count in bits 44..63, weight below (bounded by the
     // kDensePageWindows flush cadence: < 2^16 samples of < 2^23 each)
@@ -342,6 +355,7 @@ __device__ __forceinline__ void process_sample(Params& p, WgCounters& wc, LaneAc
     unsigned long long* fp = reinterpret_cast<unsigned long long*>(p.min64 + 36 + e);
     atomicMin(fp, ord);
   }
+  sub_stamp<TIMING>(st, 2);
   if (p.flags & NMG_F_PAGE_HIST) {
     // ma_get_block: page_no = (int)((addr - buffer_addr) / 4096) (mem_analyzer.c:530-531)
     const uint32_t page = uint32_t(int(uint64_t(addr - m.baddr) / kPageSize));
@@ -352,15 +366,16 @@ __device__ __forceinline__ void process_sample(Params& p, WgCounters& wc, LaneAc
       } else {
         const int ps = page_slot(wc, cell);
         if (ps >= 0) atomicAdd(&wc.pcnt[ps], 1u);
-        else if (!(p.plog && plog_append(p, L.pcur, cell, th, 1u)))
+        else if (!((MODE & kModeLarge) && p.plog && plog_append(p, L.pcur, cell, th, 1u)))
           atomicAdd(p.hist + uint64_t(th) * p.hist_cells + cell, 1u);
       }
     } else {
       const uint32_t sidx = p.entries[e].sidx;
       if (sidx != ~0u)  // huge objects ([stack]): hashed cells in global memory
-        sparse_add(p, sparse_key(sidx, th, page), seq, off, 1u);
+        sparse_add(p, sparse_key(sidx, th, page), in1 ? b1.seq : b0.seq, off, 1u);
     }
   }
+  sub_stamp<TIMING>(st, 3);
   if (p.flags & NMG_F_OBJECT_LEVELS) {
     unsigned long long* lv = reinterpret_cast<unsigned long long*>(
         p.sum64 + 2 * kGlobalSums + uint64_t(p.nb_entries) * 4 + (uint64_t(e) * 2 + access) * kLevelWords);
@@ -431,7 +446,8 @@ __device__ __forceinline__ void flush_pages(Params& p, WgCounters& wc, uint32_t*
   for (int i = tid; i < (int)kPageSlots; i += kWG) {
     const uint32_t cell = pkey[i];
     if (cell == kEmpty32) continue;
-    if (write && !(p.plog && plog_append(p, pcur, cell, th, wc.pcnt[i]))) atomicAdd(hrow + cell, wc.pcnt[i]);
+    if (write && !((MODE & kModeLarge) && p.plog && plog_append(p, pcur, cell, th, wc.pcnt[i])))
+      atomicAdd(hrow + cell, wc.pcnt[i]);
     pkey[i] = kEmpty32;
     wc.pcnt[i] = 0;
   }
@@ -535,7 +551,7 @@ __global__ __launch_bounds__(kWG, 1) void attribute_kernel(Params p) {
   // page-cell sub-log cursors after the shifts (large tables only)
   uint32_t* const s_pcur = reinterpret_cast<uint32_t*>(s_tab + (kMaxFences + 1) / 2 + (kMaxFences + 1) / 16);
   static_assert(((kMaxFences + 1) / 2 + (kMaxFences + 1) / 16) * 16 + kPlogMaxParts * 4 <= kTabBytes, "plog cursors");
-  if (p.lds_nodes) {
+  if (!(MODE & kModeLarge)) {
     const uint32_t n = 1u << p.elevels;
     for (uint32_t i = tid; i < n; i += kWG) s_fences[i] = p.efences[i];
     for (uint32_t i = 1 + tid; i < n; i += kWG) {
@@ -588,9 +604,12 @@ __global__ __launch_bounds__(kWG, 1) void attribute_kernel(Params p) {
   uint32_t ns0 = 0, nf0 = 0, ns1 = 0, nf1 = 0;  // per-buffer tallies: buffer idx, idx + 1
   uint64_t tacc[4] = {0, 0, 0, 0}, t_start = 0, t0 = 0, t1 = 0;
   if (TIMING) t_start = t0 = stamp();
-  constexpr bool kSpec = !(MODE & kModeDenseObj);  // large tables come with the hashed object mode
+  constexpr bool kSpec = (MODE & kModeLarge) && !(MODE & kModeDenseObj);
+  SubTimer st;
+  for (int k = 0; k < 7; k++) st.acc[k] = 0;
+  st.last = 0;
   SpecDir sp;
-  sp.addr = 0;
+  sp.on = false;
   sp.idx = 0;
   sp.de = make_uint2(0, 0);
 
@@ -614,6 +633,7 @@ __global__ __launch_bounds__(kWG, 1) void attribute_kernel(Params p) {
     // (LDS broadcasts are made wave-uniform explicitly: the branches below
     // hold barriers and steer the scalar loop state)
     const uint32_t f = __builtin_amdgcn_readfirstlane(s_flags[win % 3]);
+    sp.on = !(f & 1);  // a fast-path window: each lane's record is the one its spec was computed for
     if (tid == 0) s_flags[(win + 2) % 3] = 0;  // last read before the previous barrier
     win++;
     if (TIMING) {
@@ -626,13 +646,12 @@ __global__ __launch_bounds__(kWG, 1) void attribute_kernel(Params p) {
     // the record this lane processes in this window
     Rec rec = r;
     bool valid;
-    uint64_t rseq, rbase;
+    bool rin1;  // the lane's record is in d1
     uint32_t roff;
     bool shortrec = false;  // a SAMPLE record shorter than 40 B (slow path only)
     if (!(f & 1)) {
       valid = wl.cand && uint32_t(r.hdr) == kSampleType;
-      rseq = wl.in1 ? d1.seq : d0.seq;
-      rbase = wl.in1 ? d1.offset : d0.offset;
+      rin1 = wl.in1;
       roff = wl.pos;
       // ---- fast path: one record per lane
       if (wl.n1) {
@@ -707,8 +726,7 @@ __global__ __launch_bounds__(kWG, 1) void attribute_kernel(Params p) {
       roff = valid ? s_list[tid] : 0;
       shortrec = (roff & 1u) != 0;
       roff &= ~1u;
-      rseq = d0.seq;
-      rbase = d0.offset;
+      rin1 = false;
       RawRec rr;
       load_rec(base, roff, valid ? len : 0, rr);
       rec = decode_rec(rr, roff);
@@ -734,7 +752,8 @@ __global__ __launch_bounds__(kWG, 1) void attribute_kernel(Params p) {
       ncand = nl.cand;
     }
 
-    if (TIMING && tid == 0 && win <= 8) {
+    if (TIMING) st.last = stamp();
+    if (TIMING && tid == 0 && win <= 4) {
       unsigned long long* o = p.dbg + uint64_t(blockIdx.x) * (kWG / 64) * kTimingWords + 8 + 2 * (win - 1);
       o[0] = (uint64_t(idx) << 40) | cur;
       o[1] = uint64_t(wl.n0) | (uint64_t(wl.n1) << 11) | (uint64_t(f) << 22) | (uint64_t(nidx) << 24) |
@@ -742,20 +761,22 @@ __global__ __launch_bounds__(kWG, 1) void attribute_kernel(Params p) {
     }
     uint64_t vm = 0, fm = 0;
     if (!(p.flags & kDbgLoadOnly))
-      process_sample<MODE>(p, wc, acc, L, valid, shortrec, rec.ts, rec.addr, rec.w, rec.dsrc, d0.access, d0.thread_rank, rseq, roff,
-                           rbase, vm, fm, sp);
-    if (kSpec && !p.lds_nodes && (p.flags & NMG_F_MATCH_SAMPLES)) {
+      process_sample<MODE, TIMING>(p, wc, acc, L, st, valid, shortrec, rec.ts, rec.addr, rec.w, rec.dsrc, d0.access, d0.thread_rank, d0, d1, rin1,
+                           roff, vm, fm, sp);
+    sub_stamp<TIMING>(st, 4);
+    if (kSpec && (p.flags & NMG_F_MATCH_SAMPLES)) {
       // start the next window's lookup: its record (loaded above, arrived
       // during this window's lookups) -> fence node -> directory slot load,
       // in flight across the flush and the barrier.  Used when the record
       // this lane processes next has the same address (fast-path windows).
       sp.idx = 0;
       if (nidx < r1 && ncand) {
-        sp.addr = decode_rec(nx, npos).addr;
-        sp.idx = fence_node(L.fences, sp.addr);
-        const uint2* ds = dir_slot(p, L.fences, L.shift, sp.addr, sp.idx);
+        const uint64_t saddr = decode_rec(nx, npos).addr;
+        sp.idx = fence_node(L.fences, saddr);
+        const uint2* ds = dir_slot(p, L.fences, L.shift, saddr, sp.idx);
         if (ds) sp.de = *ds;
       }
+      sub_stamp<TIMING>(st, 5);
     }
     {
       // lanes of this wave in buffer idx + 1 (tid >= n0)
@@ -770,6 +791,7 @@ __global__ __launch_bounds__(kWG, 1) void attribute_kernel(Params p) {
       t1 = stamp();
       tacc[2] += t1 - t0;
       t0 = t1;
+      st.acc[6] += t1 - st.last;
     }
     // end of the stream run (or of this workgroup's range): publish the
     // stream's counters; tables over their fill threshold (as of this
@@ -836,6 +858,7 @@ __global__ __launch_bounds__(kWG, 1) void attribute_kernel(Params p) {
   if (TIMING && lane == 0) {
     unsigned long long* o = p.dbg + (uint64_t(blockIdx.x) * (kWG / 64) + tid / 64) * kTimingWords;
     for (int k = 0; k < 4; k++) o[k] = tacc[k];
+    for (int k = 0; k < 7; k++) o[16 + k] = st.acc[k];
     o[4] = stamp() - t_start;
     o[5] = win;
   }
@@ -885,11 +908,13 @@ __global__ __launch_bounds__(1024, 1) void tlog_reduce_kernel(TlogParams r) {
     __syncthreads();
     constexpr int kU = 4;  // records per thread in flight
     for (uint32_t i0 = tid; i0 < total; i0 += kU * 1024) {
-      unsigned long long kv[kU], wv[kU], ov[kU];
+      uint4 sv[kU];
+      const uint4* sq[kU];
 #pragma unroll
       for (int u = 0; u < kU; u++) {
         const uint32_t i = i0 + u * 1024;
-        kv[u] = ~0ull;  // (no record: entry ids are < 2^31)
+        sv[u] = make_uint4(~0u, 0, kTlogCont, 0);  // (no slot: skipped like a continuation)
+        sq[u] = nullptr;
         if (i >= total) continue;
         uint32_t lo = 0, hi = r.grid;  // source workgroup: s_pre[lo] <= i < s_pre[lo + 1]
         while (hi - lo > 1) {
@@ -897,20 +922,27 @@ __global__ __launch_bounds__(1024, 1) void tlog_reduce_kernel(TlogParams r) {
           if (s_pre[mid] <= i) lo = mid;
           else hi = mid;
         }
-        const unsigned long long* q = r.tlog + ((uint64_t(lo) * r.parts + part) * r.cap + (i - s_pre[lo])) * 3;
-        kv[u] = q[0];
-        wv[u] = q[1];
-        ov[u] = q[2];
+        sq[u] = r.tlog + (uint64_t(lo) * r.parts + part) * r.cap + (i - s_pre[lo]);
+        sv[u] = *sq[u];
       }
 #pragma unroll
       for (int u = 0; u < kU; u++) {
-        if (kv[u] == ~0ull) continue;
-        const uint32_t e = uint32_t(kv[u]) & 0x7fffffffu, a = uint32_t(kv[u]) >> 31;
+        const uint4 v = sv[u];
+        if (v.z == kTlogCont) continue;  // second slot of a two-slot record (read with its head)
+        const uint32_t e = v.x & 0x7fffffffu, a = v.x >> 31;
         const uint64_t j = e - base;
         if (e < base || j >= n) continue;
-        atomicAdd(&s_cnt[a][j], uint32_t(kv[u] >> 32));
-        if (wv[u]) atomicAdd(&s_wt[a][j], wv[u]);
-        atomicMin(&s_ord[j], ov[u]);
+        uint32_t cnt = 1;
+        uint64_t wt = v.y, ord = (uint64_t(v.w) << 32) | v.z;
+        if (v.z == kTlogHead) {
+          const uint4 c = sq[u][1];
+          cnt = v.y;
+          wt = (uint64_t(c.y) << 32) | c.x;
+          ord = (uint64_t(v.w) << 32) | c.w;
+        }
+        atomicAdd(&s_cnt[a][j], cnt);
+        if (wt) atomicAdd(&s_wt[a][j], (unsigned long long)wt);
+        atomicMin(&s_ord[j], (unsigned long long)ord);
       }
     }
     __syncthreads();
@@ -1086,10 +1118,12 @@ __global__ __launch_bounds__(256) void merge_kernel(void* dst, const void* src, 
 typedef void (*AttributeKernel)(Params);
 
 hipError_t launch_attribute(bool timing, int mode, uint32_t grid, hipStream_t s, const Params& p) {
-  static const AttributeKernel k[2][4] = {
-      {attribute_kernel<false, 0>, attribute_kernel<false, 1>, attribute_kernel<false, 2>, attribute_kernel<false, 3>},
-      {attribute_kernel<true, 0>, attribute_kernel<true, 1>, attribute_kernel<true, 2>, attribute_kernel<true, 3>}};
-  hipLaunchKernelGGL(k[timing ? 1 : 0][mode & 3], dim3(grid), dim3(kWG), 0, s, p);
+  static const AttributeKernel k[2][8] = {
+      {attribute_kernel<false, 0>, attribute_kernel<false, 1>, attribute_kernel<false, 2>, attribute_kernel<false, 3>,
+       attribute_kernel<false, 4>, attribute_kernel<false, 5>, attribute_kernel<false, 6>, attribute_kernel<false, 7>},
+      {attribute_kernel<true, 0>, attribute_kernel<true, 1>, attribute_kernel<true, 2>, attribute_kernel<true, 3>,
+       attribute_kernel<true, 4>, attribute_kernel<true, 5>, attribute_kernel<true, 6>, attribute_kernel<true, 7>}};
+  hipLaunchKernelGGL(k[timing ? 1 : 0][mode & 7], dim3(grid), dim3(kWG), 0, s, p);
   return hipGetLastError();
 }
 

@@ -101,6 +101,19 @@ for s in $STAGES; do
           || { echo "l2 pass $i failed"; tail -20 $OUT/l2_${TAG}_$i.log; exit 1; }
       done
       echo "l2 passes done" ;;
+    pmcx)
+      # arbitrary counter passes: PMCX_SETS="A B;C D" (one rocprofv3 run per set)
+      echo "== rocprofv3 counter passes (${PMCX_WL:-c4})"
+      i=0
+      IFS=';' read -ra SETS <<< "${PMCX_SETS:-TCC_HIT_sum TCC_MISS_sum}"
+      for set in "${SETS[@]}"; do
+        i=$((i+1))
+        rm -rf $OUT/pmcx_${TAG}_$i
+        NMG_BENCH_DEBUG_FLAGS=${PMCX_FLAGS:-0} timeout -k 10 400 rocprofv3 --pmc $set --kernel-trace -d $ROOT/$OUT/pmcx_${TAG}_$i -o run --output-format csv \
+          -- python3 $ROOT/bench.py --workload ${PMCX_WL:-c4} --secondary "" --steps 3 --warmup 1 --no-cpu-baseline > $OUT/pmcx_${TAG}_$i.log 2>&1 \
+          || { echo "pmcx pass $i failed"; tail -20 $OUT/pmcx_${TAG}_$i.log; exit 1; }
+      done
+      python3 tools/pmc_kernels.py $OUT/pmcx_${TAG}_* ;;
     alloc)
       echo "== arena allocation experiment (${ALLOC_WL:-c4})"
       timeout -k 10 900 python tools/exp_alloc.py --workload ${ALLOC_WL:-c4} > $OUT/alloc_$TAG.json 2> $OUT/alloc_$TAG.err \

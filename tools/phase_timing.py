@@ -9,6 +9,10 @@ window of each phase:
   process     next-window issue + the records' lookup and accumulation
   rest        drain / buffer end / stream flush bookkeeping
 
+and the process phase split (sub_*): global counters, lookup (until the
+node record has arrived), object tables, page cells, levels, the next
+window's speculative fence walk + directory issue, tallies.
+
 The stamps themselves cost a few percent (MI355X_MICROARCH.md constants
 table); compare variants with each other, not with the untimed kernel."""
 import argparse
@@ -51,7 +55,7 @@ def main():
         arena, offs, lens, ranks, acc = rp.packed()
         d = torch.from_numpy(arena).cuda()
         for v, f in VARIANTS.items():
-            e = Engine(flags=f | TIMING | 0x10000, nb_threads=rp.nb_threads)
+            e = Engine(flags=f | TIMING, nb_threads=rp.nb_threads)
             e.set_objects(rp.table)
             e.set_device_buffers(d.data_ptr(), offs, lens, ranks, acc)
             res = []
@@ -64,13 +68,15 @@ def main():
                 buf = np.zeros(n.value, dtype=np.uint64)
                 lib.nmg_debug_timing(e.h, buf.ctypes.data_as(C.POINTER(C.c_uint64)), n.value, C.byref(n))
                 if r:
-                    res.append((buf.reshape(-1, 24)[:, :8].astype(np.float64), e.last_analyze_ms()))
+                    res.append((buf.reshape(-1, 24).astype(np.float64), e.last_analyze_ms()))
             t = np.mean([x[0] for x in res], axis=0)  # [waves][8]
             wins = t[:, 5].sum()
             out = {"workload": wname, "variant": v, "kernel_ms": float(np.median([x[1] for x in res])),
                    "windows_per_wave": float(t[:, 5].mean())}
             for k, name in enumerate(("load_check", "barrier", "process", "rest")):
                 out[name + "_cyc_per_window"] = float(t[:, k].sum() / wins)
+            for k, name in enumerate(("glob", "find", "obj", "page", "levels", "spec", "tail")):
+                out["sub_" + name] = float(t[:, 16 + k].sum() / wins)
             out["total_cyc_per_wave"] = float(t[:, 4].mean())
             out["max_total_cyc"] = float(t[:, 4].max())
             print(json.dumps(out), flush=True)

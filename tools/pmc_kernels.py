@@ -1,0 +1,27 @@
+#!/usr/bin/env python3
+"""Per-kernel averages of rocprofv3 counter-collection CSVs (one directory per
+--pmc pass): prints one JSON line per (kernel, counter) group, values per
+dispatch, for the attribution and reduce kernels."""
+import collections
+import csv
+import glob
+import json
+import os
+import sys
+
+
+def main():
+    agg = collections.defaultdict(lambda: collections.defaultdict(list))
+    for d in sys.argv[1:]:
+        for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+            for r in csv.DictReader(open(f)):
+                agg[r["Kernel_Name"].split("(")[0][:60]][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    for k, v in sorted(agg.items()):
+        if "attribute" not in k and "reduce" not in k:
+            continue
+        print(json.dumps({"kernel": k, **{c: sum(x) / len(x) for c, x in sorted(v.items())},
+                          "dispatches": max(len(x) for x in v.values())}))
+
+
+if __name__ == "__main__":
+    main()
