@@ -1,7 +1,6 @@
-// nmg_device.h -- device helpers shared by the attribution kernels
-// (nmg_kernels.hip: small tables and the reduce / reset kernels; nmg_big.hip:
-// large tables): wave reductions, the level-bucket mask, record loads, the
-// per-lane global counters, hash-bucket slots, entry matching.
+// nmg_device.h -- device helpers of the attribution kernels (nmg_kernels.hip):
+// wave reductions, the level-bucket mask, record loads, the per-lane global
+// counters, hash-bucket slots, the long-tail log, entry matching.
 #pragma once
 
 #include "nmg_kernels.h"

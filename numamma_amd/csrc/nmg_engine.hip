@@ -91,7 +91,7 @@ struct nmg_engine {
   hipEvent_t ringm[kRing] = {};  // after the attribution kernel (before the log reduce)
   uint64_t nlaunch = 0;
   int num_cus = 256;
-  int blocks_per_cu = 0, big_blocks_per_cu = 0;
+  int blocks_per_cu = 0;
   bool launched = false;
 
   // object table
@@ -107,11 +107,6 @@ struct nmg_engine {
   uint8_t* d_fshift = nullptr;
   uint2* d_dir = nullptr;
   uint32_t nb_fences = 0, fence_log2 = 0, dir_log2 = 0;
-  FatSlot* d_fat = nullptr;       // large tables: fat directory (attribute_big_kernel)
-  uint8_t* d_fatshift = nullptr;
-  uint32_t fat_dir_log2 = 0;
-  uint32_t* d_hpre = nullptr;     // [E + 1] dense page cells before each entry
-  uint32_t pbits = 0;
   std::vector<uint64_t> hist_base, npages, buffer_size, entry_addr;
   std::vector<nmg_object> objects;  // the table as given (all_memory_objects.dat)
   std::vector<uint32_t> sparse_entries;
@@ -132,7 +127,7 @@ struct nmg_engine {
   size_t tlog_bytes = 0;
   uint32_t* d_tlog_cnt = nullptr;
   size_t tlog_cnt_cap = 0;
-  unsigned long long* d_plog = nullptr;  // large tables: page-cell log (Params::plog / plog16)
+  unsigned long long* d_plog = nullptr;  // large tables: page-cell log (Params::plog)
   size_t plog_bytes = 0;
   uint32_t* d_plog_cnt = nullptr;
   size_t plog_cnt_cap = 0;
@@ -295,12 +290,6 @@ static void free_table(nmg_engine* h) {
   (void)hipFree(h->d_ffences);
   (void)hipFree(h->d_fshift);
   (void)hipFree(h->d_dir);
-  (void)hipFree(h->d_fat);
-  (void)hipFree(h->d_fatshift);
-  (void)hipFree(h->d_hpre);
-  h->d_fat = nullptr;
-  h->d_fatshift = nullptr;
-  h->d_hpre = nullptr;
   h->d_keys = nullptr;
   h->d_nodes = nullptr;
   h->d_entries = nullptr;
@@ -511,73 +500,6 @@ static void build_big_lookup(const uint64_t* keys, uint32_t K, bool no_dir, BigL
   }
 }
 
-// The fat directory of attribute_big_kernel (FatSlot, nmg_kernels.h): the
-// same fences (every S-th key), per bucket 2^dir_log2 equal slots over the
-// bucket's key span [first key, last key] -- slot widths up to 2^63, so a
-// bucket across a huge gap (heap -> [stack]) keeps its directory -- and per
-// slot the node of the largest key <= the slot start (a) plus the node of the
-// one key inside the slot (b), or, with several keys inside (or an unusual
-// b), the first inner key's index and the number of inner keys.
-struct FatLookup {
-  uint32_t dir_log2 = 0;
-  std::vector<uint8_t> shift;  // [nb_fences]
-  std::vector<FatSlot> slots;  // [nb_fences << dir_log2]
-};
-
-static void build_fat(const uint64_t* keys, uint32_t K, const uint32_t* entry_off, const nmg_object* objs,
-                      const BigLookup& bl, bool no_dir, FatLookup& fl) {
-  const uint32_t S = 1u << bl.fence_log2;
-  fl.shift.assign(bl.nb_fences, kShiftSearch);
-  if (S > (1u << 16) || no_dir) return;  // (kernel: binary search of the bucket)
-  // two slots per key, within 4 GiB of directory
-  fl.dir_log2 = S == 1 ? 0 : bl.fence_log2 + 1;
-  while (fl.dir_log2 > 0 && ((uint64_t)bl.nb_fences << fl.dir_log2) * sizeof(FatSlot) > (4ull << 30)) fl.dir_log2--;
-  const uint32_t D = 1u << fl.dir_log2;
-  fl.slots.assign((size_t)bl.nb_fences << fl.dir_log2, FatSlot{});
-  auto cand = [&](uint32_t k, FatCand& c) {
-    const uint32_t e = entry_off[k];
-    const nmg_object& o = objs[e];
-    c.end = o.buffer_addr + o.buffer_size;  // (mod 2^64, as the reference's pointer sum)
-    c.alloc = o.alloc_date;
-    c.free = o.free_date;
-    c.eid = e;
-    if (entry_off[k + 1] - e > 1) c.sz = kSzOlder | k;
-    else if (o.buffer_size > kSzMask) c.sz = kSzBig | k;
-    else c.sz = (uint32_t)o.buffer_size;
-  };
-  for (uint32_t b = 0; b < bl.nb_fences; b++) {
-    const uint32_t k0 = b * S, k1 = (uint32_t)std::min<uint64_t>((uint64_t)k0 + S, K);
-    const uint64_t f = keys[k0], span = keys[k1 - 1] - f;
-    uint32_t sh = 0;
-    while (sh < 63 && (span >> sh) >= D) sh++;
-    fl.shift[b] = (uint8_t)sh;
-    FatSlot* ds = &fl.slots[(size_t)b << fl.dir_log2];
-    uint32_t k = k0;  // largest key <= slot start
-    for (uint32_t j = 0; j < D; j++) {
-      const uint64_t s0 = (uint64_t)j << sh;  // slot [s0, s0 + 2^sh) relative to f; the last slot is open
-      while (k + 1 < k1 && keys[k + 1] - f <= s0) k++;
-      uint32_t c = 0;
-      while (k + 1 + c < k1 && (j == D - 1 || keys[k + 1 + c] - f - s0 < (1ull << sh))) c++;
-      FatSlot& z = ds[j];
-      cand(k, z.a);
-      if (c == 0) continue;
-      const uint32_t kb = k + 1;
-      const nmg_object& ob = objs[entry_off[kb]];
-      const bool plain = c == 1 && entry_off[kb + 1] - entry_off[kb] == 1 && ob.buffer_addr == keys[kb] &&
-                         ob.buffer_size <= kSzMask;
-      if (plain) {
-        cand(kb, z.b);
-        z.b.eid |= kFatFlag;  // b present; its key = b.end - b.sz
-      } else {
-        z.a.eid |= kFatFlag;  // several keys inside: binary search of [kb, kb + c)
-        z.b.end = keys[kb];
-        z.b.eid = kb;
-        z.b.sz = c;
-      }
-    }
-  }
-}
-
 extern "C" int nmg_set_objects(nmg_engine* h, const uint64_t* keys, const uint32_t* entry_off,
                                uint32_t nb_keys, const nmg_object* entries, uint32_t nb_entries) {
   if (!h || (nb_keys && (!keys || !entry_off)) || (nb_entries && !entries))
@@ -695,20 +617,6 @@ extern "C" int nmg_set_objects(nmg_engine* h, const uint64_t* keys, const uint32
     HIP_TRY(h, alloc_copy((void**)&h->d_ffences, bl.efences.data(), bl.efences.size() * 8));
     HIP_TRY(h, alloc_copy((void**)&h->d_fshift, bl.shift.data(), bl.shift.size()));
     HIP_TRY(h, alloc_copy((void**)&h->d_dir, bl.dir.data(), bl.dir.size() * sizeof(uint2)));
-    FatLookup fl;
-    build_fat(keys, nb_keys, entry_off, entries, bl, (h->flags & kDbgNoDir) != 0, fl);
-    h->fat_dir_log2 = fl.dir_log2;
-    HIP_TRY(h, alloc_copy((void**)&h->d_fatshift, fl.shift.data(), fl.shift.size()));
-    HIP_TRY(h, alloc_copy((void**)&h->d_fat, fl.slots.data(), fl.slots.size() * sizeof(FatSlot)));
-    // dense page cells before each entry (entry e is dense iff hpre[e+1] > hpre[e])
-    std::vector<uint32_t> hpre((size_t)nb_entries + 1, 0);
-    for (uint32_t e = 0; e < nb_entries; e++)
-      hpre[e + 1] = hpre[e] + (h->hist_base[e] != kHistSparse ? (uint32_t)h->npages[e] : 0u);
-    HIP_TRY(h, alloc_copy((void**)&h->d_hpre, hpre.data(), hpre.size() * 4));
-    // LDS page key = entry << pbits | page; entry ids < 2^(32 - pbits) - 1
-    uint32_t ebits = 1;
-    while (ebits < 32 && ((uint64_t)nb_entries >> ebits)) ebits++;
-    h->pbits = ebits < 32 ? 32 - ebits : 0;
   }
   HIP_TRY(h, alloc_copy((void**)&h->d_entries, dev.data(), (size_t)nb_entries * sizeof(DevEntry)));
 
@@ -1229,19 +1137,13 @@ static int build_schedule(nmg_engine* h, uint32_t grid) {
 static void ensure_occupancy(nmg_engine* h) {
   if (h->blocks_per_cu <= 0) {
     h->blocks_per_cu = attribute_blocks_per_cu();
-    h->big_blocks_per_cu = attribute_big_blocks_per_cu();
   }
 }
-
-// large tables go through attribute_kernel's directory + node-record path;
-// kDbgBigKernel routes them through attribute_big_kernel (A/B, tests)
-static bool use_big(const nmg_engine* h) { return h->K > kLdsNodes && (h->flags & kDbgBigKernel); }
 
 // persistent grid: one resident workgroup per slot, each with a byte-balanced range
 static uint32_t attribution_grid(nmg_engine* h, uint32_t nb) {
   ensure_occupancy(h);
-  const int bpc = use_big(h) ? h->big_blocks_per_cu : h->blocks_per_cu;
-  return nb ? std::min<uint32_t>(nb, (uint32_t)(h->num_cus * bpc)) : 0;
+  return nb ? std::min<uint32_t>(nb, (uint32_t)(h->num_cus * h->blocks_per_cu)) : 0;
 }
 
 // One attribution launch over `nb` buffers whose stream-sorted descriptors and
@@ -1284,18 +1186,9 @@ static int launch_attribution(nmg_engine* h, const uint8_t* data, const BufDesc*
   p.sparse_dirty = h->d_sparse_dirty ? h->d_sparse_dirty + (h->nreset & 1) : nullptr;
   p.smatch = (h->flags & NMG_F_SAMPLE_MATCHES) ? h->d_smatch : nullptr;
   // dense LDS tables when the table is small enough (DESIGN.md "Kernels");
-  // large tables: attribute_big_kernel, hashed tables only
-  const bool big = use_big(h);
-  int mode = big ? 0
-                 : (h->E <= kObjSlots ? kModeDenseObj : 0) | (h->hist_cells <= kDensePageCells ? kModeDensePage : 0) |
-                       (p.lds_nodes ? 0 : kModeLarge);
-  if (big) {
-    p.fat = h->d_fat;
-    p.fatshift = h->d_fatshift;
-    p.dir_log2 = h->fat_dir_log2;
-    p.hpre = h->d_hpre;
-    p.pbits = h->pbits;
-  }
+  // large tables: their own kernel instances (fences + directory + node records)
+  const int mode = (h->E <= kObjSlots ? kModeDenseObj : 0) | (h->hist_cells <= kDensePageCells ? kModeDensePage : 0) |
+                   (p.lds_nodes ? 0 : kModeLarge);
   if (!(mode & kModeDenseObj) && h->d_pk64 && !(h->flags & kDbgNoPack)) {
     // < 2^cbits packed samples in this launch (only SAMPLE records of at
     // least 40 B are packed: the kernel keeps shorter ones, which the
@@ -1346,18 +1239,13 @@ static int launch_attribution(nmg_engine* h, const uint8_t* data, const BufDesc*
   // spare part) with hashed page cells
   if (!(mode & kModeDensePage) && !p.lds_nodes && nb && h->hist_cells && grid <= kLogMaxGrid &&
       (h->flags & NMG_F_MATCH_SAMPLES) && (h->flags & NMG_F_PAGE_HIST) && nbytes / 8 < (1ull << 32)) {
-    uint32_t cshift = 0, parts = 0;
-    size_t rec = 8;
-    if (big) {  // entry ranges (plog16_reduce_kernel), 16 B records
-      while (((h->E + (1ull << cshift) - 1) >> cshift) > kPlogMaxParts) cshift++;
-      parts = (uint32_t)((h->E + (1ull << cshift) - 1) >> cshift);
-      rec = 16;
-    } else {  // cell ranges (plog_reduce_kernel), 8 B records
-      while (((h->hist_cells + (1ull << cshift) - 1) >> cshift) > kPlogMaxParts) cshift++;
-      // parts of at least a few hundred cells (fewer, longer sub-logs)
-      while (cshift < 9 && ((uint64_t)h->T << (cshift + 1)) <= kPlogWin) cshift++;
-      parts = (uint32_t)((h->hist_cells + (1ull << cshift) - 1) >> cshift);
-    }
+    // cell ranges (plog_reduce_kernel), 8 B records
+    uint32_t cshift = 0;
+    const size_t rec = 8;
+    while (((h->hist_cells + (1ull << cshift) - 1) >> cshift) > kPlogMaxParts) cshift++;
+    // parts of at least a few hundred cells (fewer, longer sub-logs)
+    while (cshift < 9 && ((uint64_t)h->T << (cshift + 1)) <= kPlogWin) cshift++;
+    const uint32_t parts = (uint32_t)((h->hist_cells + (1ull << cshift) - 1) >> cshift);
     // sized for about every sample of the launch spread evenly over the
     // parts; a full sub-log only sends its overflow to the global atomics
     const uint64_t cap = std::min<uint64_t>(1u << 20, (nbytes / kRecBytes) / ((uint64_t)grid * parts) + 64);
@@ -1379,13 +1267,8 @@ static int launch_attribution(nmg_engine* h, const uint8_t* data, const BufDesc*
         h->plog_cnt_cap = (size_t)grid * parts;
       }
     }
-    if (big) {
-      p.plog16 = reinterpret_cast<uint4*>(h->d_plog);
-      p.plog_pshift = cshift;
-    } else {
-      p.plog = h->d_plog;
-      p.plog_cshift = cshift;
-    }
+    p.plog = h->d_plog;
+    p.plog_cshift = cshift;
     p.plog_cnt = h->d_plog_cnt;
     p.plog_cap = (uint32_t)cap;
     p.plog_parts = parts;
@@ -1398,7 +1281,7 @@ static int launch_attribution(nmg_engine* h, const uint8_t* data, const BufDesc*
   }
   HIP_TRY(h, hipEventRecord(h->ring0[slot], h->stream));
   if (nb) {
-    if ((h->flags & kDbgTiming) && !big) {
+    if (h->flags & kDbgTiming) {
       const size_t n = (size_t)grid * (kWG / 64) * kTimingWords;
       if (n > h->dbg_cap) {
         (void)hipFree(h->d_dbg);
@@ -1411,7 +1294,7 @@ static int launch_attribution(nmg_engine* h, const uint8_t* data, const BufDesc*
       p.dbg = reinterpret_cast<unsigned long long*>(h->d_dbg);
       HIP_TRY(h, launch_attribute(true, mode, grid, h->stream, p));
     } else {
-      HIP_TRY(h, big ? launch_attribute_big(grid, h->stream, p) : launch_attribute(false, mode, grid, h->stream, p));
+      HIP_TRY(h, launch_attribute(false, mode, grid, h->stream, p));
     }
     HIP_TRY(h, hipEventRecord(h->ringm[slot], h->stream));
     if (p.tlog) {  // sums the log per entry range, folds the packed counters
@@ -1431,12 +1314,6 @@ static int launch_attribution(nmg_engine* h, const uint8_t* data, const BufDesc*
     } else if (p.pk64) {
       const uint32_t blocks = (uint32_t)std::min<uint64_t>(2048, (2ull * h->E + 255) / 256);
       HIP_TRY(h, launch_unpack(blocks, h->stream, h->d_sum64, p.pk64, h->E, p.pk_shift));
-    }
-    if (p.plog16) {  // sums the page log per entry range into the histogram
-      Plog16Params r;
-      r.p = p;
-      r.grid = grid;
-      HIP_TRY(h, launch_plog16_reduce(p.plog_parts, h->stream, r));
     }
     if (p.plog) {  // sums the page-cell log per cell range into the histogram
       PlogParams r;

@@ -114,28 +114,6 @@ struct DevEntry {
 };
 static_assert(sizeof(DevEntry) == 64, "DevEntry");
 
-// Large tables (nmg_big.hip): the directory slot of a fence bucket is a
-// "fat" 64 B slot that resolves most lookups by itself: candidate a is the
-// node of the largest key <= the slot start, candidate b the node of the one
-// key inside the slot (if any), each as its newest entry's end, dates, entry
-// id and size.  b's key = b.end - b.sz (its newest entry is not realloc'd).
-struct FatCand {
-  uint64_t end;    // buffer_addr + buffer_size (mod 2^64) of the node's newest entry
-  uint64_t alloc;  // alloc_date
-  uint64_t free;   // free_date
-  uint32_t eid;    // bits 0..30 entry id; bit 31 = slot flag (a: several keys inside; b: present)
-  uint32_t sz;     // bits 0..29 buffer_size, or the node's key index when bit 30 (size >= 2^30)
-                   // or bit 31 (the node has older entries) is set: then the node record decides
-};
-struct FatSlot {
-  FatCand a, b;  // with several keys inside (a.eid bit 31): b.end = first inner key,
-                 // b.eid = its key index, b.sz = number of inner keys
-};
-static_assert(sizeof(FatSlot) == 64, "FatSlot");
-constexpr uint32_t kFatFlag = 0x80000000u;
-constexpr uint32_t kSzOlder = 0x80000000u, kSzBig = 0x40000000u, kSzMask = 0x3fffffffu;
-constexpr uint32_t kDbgBigKernel = 0x10000;  // large tables through attribute_big_kernel (A/B, tests)
-
 struct Params {
   const uint8_t* data;
   const BufDesc* sbufs;    // descriptors in schedule order (sorted by stream; .pad = buffer index)
@@ -183,26 +161,13 @@ struct Params {
   // and flushed slots append to sub-log (workgroup, entry >> tlog_rshift);
   // tlog_reduce_kernel sums each entry range from LDS.  A full sub-log falls
   // back to the atomics.
-  uint4* tlog;               // [grid][tlog_parts][tlog_cap] 16 B slots (TlogSlot layouts); null: off
+  uint4* tlog;               // [grid][tlog_parts][tlog_cap] 16 B slots (kTlogHead layouts); null: off
   uint32_t* tlog_cnt;        // [grid][tlog_parts] records written
   uint32_t tlog_cap, tlog_rshift, tlog_parts;
   // page-cell log (see kPlogMaxParts): [grid][plog_parts][plog_cap] records
   unsigned long long* plog;  // null: off (cells that miss go to global atomics)
   uint32_t* plog_cnt;        // [grid][plog_parts] records written
   uint32_t plog_cap, plog_cshift, plog_parts;
-  // large tables (attribute_big_kernel)
-  const FatSlot* fat;       // [nb_fences << dir_log2]
-  const uint8_t* fatshift;  // [nb_fences] slot width log2 (<= 63), kShiftSearch: no directory
-  const uint32_t* hpre;     // [E + 1] dense cells before entry e (entry e is dense iff hpre[e+1] > hpre[e])
-  uint32_t pbits;           // LDS page key = entry << pbits | page (pages < 2^pbits)
-  uint4* plog16;            // entry-range page log: {entry, page, count, thread}; parts = entry >> plog_pshift
-  uint32_t plog_pshift;
-};
-
-// plog16_reduce_kernel (large tables)
-struct Plog16Params {
-  Params p;
-  uint32_t grid;
 };
 
 // plog_reduce_kernel
@@ -252,13 +217,5 @@ hipError_t launch_unpack(uint32_t grid, hipStream_t s, uint64_t* sum64, unsigned
 hipError_t launch_reset(uint32_t grid, hipStream_t s, const ResetParams& r);
 hipError_t launch_plog_reduce(uint32_t parts, hipStream_t s, const PlogParams& r);
 hipError_t launch_merge(hipStream_t s, void* dst, const void* src, uint64_t n, int op);
-// large tables (nmg_big.hip)
-#ifndef NMG_BIG_WG
-#define NMG_BIG_WG 512
-#endif
-constexpr int kBWG = NMG_BIG_WG;  // attribute_big_kernel: 8 waves, one workgroup per CU
-hipError_t launch_attribute_big(uint32_t grid, hipStream_t s, const Params& p);
-int attribute_big_blocks_per_cu();
-hipError_t launch_plog16_reduce(uint32_t parts, hipStream_t s, const Plog16Params& r);
 
 }  // namespace nmg

@@ -146,24 +146,6 @@ def test_long_tail_paths_bit_exact(tmp_path, dbg):
     _same_dirs(odir, edir)
 
 
-BIG_KERNEL = 0x10000  # internal switch: large tables through attribute_big_kernel
-
-
-@pytest.mark.parametrize("cfg,dbg", [
-    (CONFIGS[1], 0), (CONFIGS[5], 0), (CONFIGS[6], 0), (CONFIGS[3], 0x2000),
-    (SynthConfig(nb_samples=200_000, nb_intervals=20_000, seed=17), 0x2000 | 0x4000),
-], ids=["k5k", "k200k", "k1m", "realloc_tinylog", "k20k_nopack"])
-def test_big_kernel_bit_exact(tmp_path, cfg, dbg):
-    """The alternative large-table kernel (fat directory slots, several
-    records per lane, entry-range page log) agrees with the oracle too."""
-    d = str(tmp_path)
-    path, odir = _oracle(generate(cfg), d)
-    edir = _engine_replay(path, d, flags=_lib.NMG_F_DEFAULT | BIG_KERNEL | dbg)
-    _assert_raw_equal(os.path.join(d, "oracle_raw.bin"), os.path.join(d, "engine_raw.bin"))
-    assert open(os.path.join(d, "oracle_stdout.txt"), "rb").read() == open(os.path.join(d, "engine_stdout.txt"), "rb").read()
-    _same_dirs(odir, edir)
-
-
 def test_no_match_mode(tmp_path):
     d = str(tmp_path)
     rp = generate(SynthConfig(nb_samples=40_000, nb_intervals=100, seed=8))

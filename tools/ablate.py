@@ -21,9 +21,6 @@ VARIANTS = {
     "match": 0x1,                       # + object counters
     "full_noflush": 0x3 | 0x400,        # LDS tables filled, never flushed to global
     "full": 0x3,                        # + page histogram (default product path)
-    # large tables through attribute_big_kernel (fat directory slots, K records per lane)
-    "lookup_only_big": 0x1 | 0x200 | 0x800 | 0x10000,
-    "full_big": 0x3 | 0x10000,
 }
 
 WORKLOADS = {
