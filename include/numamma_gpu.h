@@ -128,7 +128,12 @@ struct nmg_report_options {
    * Dl_info there -- unpinned). */
   const struct nmg_module *modules;
   uint32_t nb_modules;
-  uint32_t reserved;
+  /* --online-analysis (mem_sampling.c:313, :953-954): the counters were
+   * accumulated alarm by alarm (nmg_update_objects), so mem_sampling_finalize
+   * prints nothing, and every object has counters from its creation
+   * (_init_mem_info, mem_analyzer.c:569-572), so ma_finalize passes each one
+   * to update_call_sites (:1832-1834), matched or not. */
+  uint32_t online;
 };
 
 struct nmg_module {
@@ -164,6 +169,24 @@ void nmg_destroy(nmg_engine *h);
  */
 int nmg_set_objects(nmg_engine *h, const uint64_t *keys, const uint32_t *entry_off,
                     uint32_t nb_keys, const struct nmg_object *entries, uint32_t nb_entries);
+
+/*
+ * Online analysis (--online-analysis: __process_samples analyses each alarm's
+ * rings in place, mem_sampling.c:953-954, against the object table as it is
+ * at that alarm): replace the lookup table, keeping every counter.  The
+ * table of nmg_set_objects is the final one (ids, page-histogram layout,
+ * report metadata); this one is the table at the alarm, flattened the same
+ * way: keys[] ascending, key i's entries [entry_off[i], entry_off[i+1]) of
+ * objects[] newest-first, and entry_ids[j] the id (index in the
+ * nmg_set_objects table) of objects[j].  Objects still alive at the alarm
+ * carry free_date 0 (they never match, quirk Q3); objects not yet allocated
+ * are absent.  An object's buffer_size must not exceed its final one (its
+ * page cells were laid out by nmg_set_objects).  In streaming mode the open
+ * chunk is analysed with the previous table first.  Copied; the caller keeps
+ * ownership.
+ */
+int nmg_update_objects(nmg_engine *h, const uint64_t *keys, const uint32_t *entry_off, uint32_t nb_keys,
+                       const uint32_t *entry_ids, const struct nmg_object *objects);
 
 /*
  * Append one captured buffer to the analysis list, in analysis order (the

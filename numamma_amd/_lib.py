@@ -106,7 +106,7 @@ class nmg_module(C.Structure):
 class nmg_report_options(C.Structure):
     _fields_ = [("output_dir", C.c_char_p), ("dump_single_items", C.c_int32), ("dump_flags", C.c_int32),
                 ("maps_path", C.c_char_p), ("maps_text", C.c_char_p),
-                ("modules", C.POINTER(nmg_module)), ("nb_modules", C.c_uint32), ("reserved", C.c_uint32)]
+                ("modules", C.POINTER(nmg_module)), ("nb_modules", C.c_uint32), ("online", C.c_uint32)]
 
 
 def module_array(modules):
@@ -150,6 +150,7 @@ _SIGS = {
     "nmg_create": (C.c_int, [C.POINTER(H), C.POINTER(nmg_options)]),
     "nmg_destroy": (None, [H]),
     "nmg_set_objects": (C.c_int, [H, u64p, u32p, C.c_uint32, C.POINTER(nmg_object), C.c_uint32]),
+    "nmg_update_objects": (C.c_int, [H, u64p, u32p, C.c_uint32, u32p, C.POINTER(nmg_object)]),
     "nmg_submit_ring": (C.c_int, [H, P, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32]),
     "nmg_submit_buffer": (C.c_int, [H, P, C.c_uint64, C.c_uint32, C.c_uint32]),
     "nmg_submit_buffers": (C.c_int, [H, C.c_uint32, C.POINTER(C.c_void_p), u64p, u32p, u32p]),

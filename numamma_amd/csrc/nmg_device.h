@@ -286,12 +286,12 @@ struct Match {
 
 __device__ __forceinline__ void match_older(const Params& p, uint32_t first, uint32_t count, uint64_t addr,
                                             uint64_t ts, Match& m) {
-  for (uint32_t e = first + 1; e < first + count; e++) {  // older entries of a reused address
-    const uint4* r = reinterpret_cast<const uint4*>(p.entries + e);
+  for (uint32_t j = first + 1; j < first + count; j++) {  // older entries of a reused address
+    const uint4* r = reinterpret_cast<const uint4*>(p.chain + j);
     const uint4 ra = r[0], rb = r[1];
     if (entry_match(ra, rb, addr, ts)) {
       const uint4 rc = r[2];
-      m.e = e;
+      m.e = rc.w;  // DevEntry::id
       m.baddr = (uint64_t(ra.y) << 32) | ra.x;
       m.hist = (uint64_t(rc.y) << 32) | rc.x;
       return;

@@ -102,12 +102,15 @@ struct nmg_engine {
   uint64_t* d_efences = nullptr;  // small tables: Eytzinger-ordered keys / node records
   DevEntry* d_enodes = nullptr;
   uint32_t elevels = 0;
-  DevEntry* d_entries = nullptr;
+  DevEntry* d_entries = nullptr;  // by entry id (the nmg_set_objects table)
+  DevEntry* d_chain = nullptr;    // table order of the current lookup table; == d_entries until
+                                  // the first nmg_update_objects
   uint64_t* d_ffences = nullptr;  // large tables: Eytzinger fences, directory shifts, directory
   uint8_t* d_fshift = nullptr;
   uint2* d_dir = nullptr;
   uint32_t nb_fences = 0, fence_log2 = 0, dir_log2 = 0;
   std::vector<uint64_t> hist_base, npages, buffer_size, entry_addr;
+  std::vector<DevEntry> dev_entries;  // host copy of d_entries (nmg_update_objects builds from it)
   std::vector<nmg_object> objects;  // the table as given (all_memory_objects.dat)
   std::vector<uint32_t> sparse_entries;
   uint64_t hist_cells = 0;
@@ -279,23 +282,50 @@ static void free_counters(nmg_engine* h) {
   h->plog_cnt_cap = 0;
 }
 
-static void free_table(nmg_engine* h) {
+// the lookup structures of one table (keys, node records, LDS tree or fences
+// + directory, table-order entries)
+static void free_lookup(nmg_engine* h) {
   (void)hipFree(h->d_keys);
   (void)hipFree(h->d_nodes);
   (void)hipFree(h->d_efences);
   (void)hipFree(h->d_enodes);
-  h->d_efences = nullptr;
-  h->d_enodes = nullptr;
-  (void)hipFree(h->d_entries);
   (void)hipFree(h->d_ffences);
   (void)hipFree(h->d_fshift);
   (void)hipFree(h->d_dir);
+  if (h->d_chain != h->d_entries) (void)hipFree(h->d_chain);
   h->d_keys = nullptr;
   h->d_nodes = nullptr;
-  h->d_entries = nullptr;
+  h->d_efences = nullptr;
+  h->d_enodes = nullptr;
   h->d_ffences = nullptr;
   h->d_fshift = nullptr;
   h->d_dir = nullptr;
+  h->d_chain = nullptr;
+}
+
+static void free_table(nmg_engine* h) {
+  free_lookup(h);
+  (void)hipFree(h->d_entries);
+  h->d_entries = nullptr;
+}
+
+static hipError_t alloc_copy(nmg_engine* h, void** dptr, const void* src, size_t bytes) {
+  hipError_t e = hipMalloc(dptr, bytes ? bytes : 16);
+  if (e != hipSuccess) return e;
+  if (bytes) return hipMemcpyAsync(*dptr, src, bytes, hipMemcpyHostToDevice, h->stream);
+  return hipSuccess;
+}
+
+// keys strictly ascending, every key with >= 1 entry, entry_off a prefix array over n entries
+static int check_table(nmg_engine* h, const uint64_t* keys, const uint32_t* entry_off, uint32_t nb_keys,
+                       uint32_t n) {
+  if (entry_off && (entry_off[0] != 0 || entry_off[nb_keys] != n))
+    return fail(h, NMG_ERR_INVALID, "entry_off[0] must be 0 and entry_off[nb_keys] == the number of entries");
+  for (uint32_t i = 0; i < nb_keys; i++) {
+    if (entry_off[i + 1] <= entry_off[i]) return fail(h, NMG_ERR_INVALID, "every key needs >= 1 entry");
+    if (i && keys[i] <= keys[i - 1]) return fail(h, NMG_ERR_INVALID, "keys must be strictly ascending");
+  }
+  return NMG_OK;
 }
 
 static int multi_create(nmg_engine* h, const nmg_options* opt);
@@ -500,16 +530,76 @@ static void build_big_lookup(const uint64_t* keys, uint32_t K, bool no_dir, BigL
   }
 }
 
+// Lookup structures of a flattened table whose entries, in table order, are
+// chain[] (ids in DevEntry::id): node records, then the LDS Eytzinger tree
+// (<= kLdsNodes keys) or the fences + directory of the large-table path.
+// chain_dev: chain already on the device (the by-id array), else uploaded.
+static int build_lookup(nmg_engine* h, const uint64_t* keys, const uint32_t* entry_off, uint32_t nb_keys,
+                        const std::vector<DevEntry>& chain, DevEntry* chain_dev) {
+  h->K = nb_keys;
+  std::vector<DevEntry> nodes(nb_keys);
+  for (uint32_t k = 0; k < nb_keys; k++) {
+    nodes[k] = chain[entry_off[k]];
+    nodes[k].first = entry_off[k];
+    nodes[k].count = entry_off[k + 1] - entry_off[k];
+  }
+  HIP_TRY(h, alloc_copy(h, (void**)&h->d_keys, keys, (size_t)nb_keys * 8));
+  HIP_TRY(h, alloc_copy(h, (void**)&h->d_nodes, nodes.data(), (size_t)nb_keys * sizeof(DevEntry)));
+  if (chain_dev) h->d_chain = chain_dev;
+  else HIP_TRY(h, alloc_copy(h, (void**)&h->d_chain, chain.data(), chain.size() * sizeof(DevEntry)));
+  if (nb_keys <= kLdsNodes) {
+    // Eytzinger (BFS) order for the LDS search: an in-order walk of the
+    // complete tree of 2^L - 1 nodes hands out the keys in sorted order; the
+    // slots after the last key are ~0 keys carrying a copy of the last node
+    // (reached only for addr == UINT64_MAX, where the last key is the answer)
+    h->elevels = 0;
+    while (((1u << h->elevels) - 1) < nb_keys) h->elevels++;
+    const uint32_t n = 1u << h->elevels;
+    std::vector<uint64_t> ef(n, ~0ull);
+    std::vector<DevEntry> en(n);
+    memset(en.data(), 0, n * sizeof(DevEntry));
+    uint32_t r = 0;
+    std::vector<uint32_t> stack;
+    uint32_t i = 1;
+    while (i < n || !stack.empty()) {  // iterative in-order walk
+      while (i < n) {
+        stack.push_back(i);
+        i = 2 * i;
+      }
+      i = stack.back();
+      stack.pop_back();
+      if (r < nb_keys) {
+        ef[i] = keys[r];
+        en[i] = nodes[r];
+      } else if (nb_keys) {
+        en[i] = nodes[nb_keys - 1];
+      }
+      r++;
+      i = 2 * i + 1;
+    }
+    HIP_TRY(h, alloc_copy(h, (void**)&h->d_efences, ef.data(), n * 8));
+    HIP_TRY(h, alloc_copy(h, (void**)&h->d_enodes, en.data(), n * sizeof(DevEntry)));
+  }
+  h->nb_fences = h->fence_log2 = h->dir_log2 = 0;
+  if (nb_keys > kLdsNodes) {
+    BigLookup bl;
+    build_big_lookup(keys, nb_keys, (h->flags & kDbgNoDir) != 0, bl);
+    h->nb_fences = bl.nb_fences;
+    h->fence_log2 = bl.fence_log2;
+    h->dir_log2 = bl.dir_log2;
+    HIP_TRY(h, alloc_copy(h, (void**)&h->d_ffences, bl.efences.data(), bl.efences.size() * 8));
+    HIP_TRY(h, alloc_copy(h, (void**)&h->d_fshift, bl.shift.data(), bl.shift.size()));
+    HIP_TRY(h, alloc_copy(h, (void**)&h->d_dir, bl.dir.data(), bl.dir.size() * sizeof(uint2)));
+  }
+  return NMG_OK;
+}
+
 extern "C" int nmg_set_objects(nmg_engine* h, const uint64_t* keys, const uint32_t* entry_off,
                                uint32_t nb_keys, const nmg_object* entries, uint32_t nb_entries) {
   if (!h || (nb_keys && (!keys || !entry_off)) || (nb_entries && !entries))
     return NMG_ERR_INVALID;
-  if (entry_off && (entry_off[0] != 0 || entry_off[nb_keys] != nb_entries))
-    return fail(h, NMG_ERR_INVALID, "entry_off[0] must be 0 and entry_off[nb_keys] == nb_entries");
-  for (uint32_t i = 0; i < nb_keys; i++) {
-    if (entry_off[i + 1] <= entry_off[i]) return fail(h, NMG_ERR_INVALID, "every key needs >= 1 entry");
-    if (i && keys[i] <= keys[i - 1]) return fail(h, NMG_ERR_INVALID, "keys must be strictly ascending");
-  }
+  int rc = check_table(h, keys, entry_off, nb_keys, nb_entries);
+  if (rc) return rc;
   if (nb_entries >= (1u << 31)) return fail(h, NMG_ERR_RANGE, "too many entries");
   HIP_TRY(h, hipSetDevice(h->device));
   HIP_TRY(h, hipStreamSynchronize(h->stream));
@@ -546,6 +636,7 @@ extern "C" int nmg_set_objects(nmg_engine* h, const uint64_t* keys, const uint32
     h->entry_addr[e] = o.buffer_addr;
     d.hist = kHistSparse;
     d.sidx = ~0u;
+    d.id = e;
     if (!want_hist) continue;
     // dense cells: histogram index = thread * hist_cells + hist_base(entry) + page
     if (np * T <= max_cells_per_entry && (h->hist_cells + np) * T <= budget_cells &&
@@ -559,66 +650,11 @@ extern "C" int nmg_set_objects(nmg_engine* h, const uint64_t* keys, const uint32
       h->sparse_entries.push_back(e);
     }
   }
-  std::vector<DevEntry> nodes(nb_keys);
-  for (uint32_t k = 0; k < nb_keys; k++) {
-    nodes[k] = dev[entry_off[k]];
-    nodes[k].first = entry_off[k];
-    nodes[k].count = entry_off[k + 1] - entry_off[k];
-  }
+  HIP_TRY(h, alloc_copy(h, (void**)&h->d_entries, dev.data(), (size_t)nb_entries * sizeof(DevEntry)));
+  rc = build_lookup(h, keys, entry_off, nb_keys, dev, h->d_entries);
+  if (rc) return rc;
+  h->dev_entries = std::move(dev);
 
-  auto alloc_copy = [&](void** dptr, const void* src, size_t bytes) -> hipError_t {
-    hipError_t e = hipMalloc(dptr, bytes ? bytes : 16);
-    if (e != hipSuccess) return e;
-    if (bytes) return hipMemcpyAsync(*dptr, src, bytes, hipMemcpyHostToDevice, h->stream);
-    return hipSuccess;
-  };
-  HIP_TRY(h, alloc_copy((void**)&h->d_keys, keys, (size_t)nb_keys * 8));
-  HIP_TRY(h, alloc_copy((void**)&h->d_nodes, nodes.data(), (size_t)nb_keys * sizeof(DevEntry)));
-  if (nb_keys <= kLdsNodes) {
-    // Eytzinger (BFS) order for the LDS search: an in-order walk of the
-    // complete tree of 2^L - 1 nodes hands out the keys in sorted order; the
-    // slots after the last key are ~0 keys carrying a copy of the last node
-    // (reached only for addr == UINT64_MAX, where the last key is the answer)
-    h->elevels = 0;
-    while (((1u << h->elevels) - 1) < nb_keys) h->elevels++;
-    const uint32_t n = 1u << h->elevels;
-    std::vector<uint64_t> ef(n, ~0ull);
-    std::vector<DevEntry> en(n);
-    memset(en.data(), 0, n * sizeof(DevEntry));
-    uint32_t r = 0;
-    std::vector<uint32_t> stack;
-    uint32_t i = 1;
-    while (i < n || !stack.empty()) {  // iterative in-order walk
-      while (i < n) {
-        stack.push_back(i);
-        i = 2 * i;
-      }
-      i = stack.back();
-      stack.pop_back();
-      if (r < nb_keys) {
-        ef[i] = keys[r];
-        en[i] = nodes[r];
-      } else if (nb_keys) {
-        en[i] = nodes[nb_keys - 1];
-      }
-      r++;
-      i = 2 * i + 1;
-    }
-    HIP_TRY(h, alloc_copy((void**)&h->d_efences, ef.data(), n * 8));
-    HIP_TRY(h, alloc_copy((void**)&h->d_enodes, en.data(), n * sizeof(DevEntry)));
-  }
-  h->nb_fences = h->fence_log2 = h->dir_log2 = 0;
-  if (nb_keys > kLdsNodes) {
-    BigLookup bl;
-    build_big_lookup(keys, nb_keys, (h->flags & kDbgNoDir) != 0, bl);
-    h->nb_fences = bl.nb_fences;
-    h->fence_log2 = bl.fence_log2;
-    h->dir_log2 = bl.dir_log2;
-    HIP_TRY(h, alloc_copy((void**)&h->d_ffences, bl.efences.data(), bl.efences.size() * 8));
-    HIP_TRY(h, alloc_copy((void**)&h->d_fshift, bl.shift.data(), bl.shift.size()));
-    HIP_TRY(h, alloc_copy((void**)&h->d_dir, bl.dir.data(), bl.dir.size() * sizeof(uint2)));
-  }
-  HIP_TRY(h, alloc_copy((void**)&h->d_entries, dev.data(), (size_t)nb_entries * sizeof(DevEntry)));
 
   h->n_sum64 = 2 * kGlobalSums + (uint64_t)nb_entries * 4;
   if (h->flags & NMG_F_OBJECT_LEVELS) h->n_sum64 += (uint64_t)nb_entries * 2 * kLevelWords;
@@ -648,6 +684,49 @@ extern "C" int nmg_set_objects(nmg_engine* h, const uint64_t* keys, const uint32
     if (rc) return fail(h, rc, w->last_error);
   }
   return nmg_reset_counters(h);
+}
+
+static int stream_flush(nmg_engine* h);
+
+// --online-analysis: the table at an alarm (entries by their set_objects
+// ids), counters kept (mem_sampling.c:953-954 against the live mem_list)
+extern "C" int nmg_update_objects(nmg_engine* h, const uint64_t* keys, const uint32_t* entry_off,
+                                  uint32_t nb_keys, const uint32_t* entry_ids, const nmg_object* objects) {
+  if (!h || (nb_keys && (!keys || !entry_off || !entry_ids || !objects))) return NMG_ERR_INVALID;
+  if (!h->have_table) return fail(h, NMG_ERR_STATE, "nmg_update_objects before nmg_set_objects");
+  const uint32_t n = nb_keys ? entry_off[nb_keys] : 0;
+  int rc = check_table(h, keys, nb_keys ? entry_off : nullptr, nb_keys, n);
+  if (rc) return rc;
+  std::vector<DevEntry> chain(n);
+  for (uint32_t j = 0; j < n; j++) {
+    const uint32_t id = entry_ids[j];
+    if (id >= h->E) return fail(h, NMG_ERR_RANGE, "entry id past the nmg_set_objects table");
+    const nmg_object& o = objects[j];
+    if (o.buffer_size > h->buffer_size[id])
+      return fail(h, NMG_ERR_RANGE, "object larger than in the nmg_set_objects table (its page cells)");
+    DevEntry& d = chain[j];
+    d = h->dev_entries[id];  // hist, sidx, id of the final table
+    d.addr = o.buffer_addr;
+    d.end = o.buffer_addr + o.buffer_size;
+    d.alloc = o.alloc_date;
+    d.free = o.free_date;
+    d.count = d.first = 0;
+  }
+  HIP_TRY(h, hipSetDevice(h->device));
+  if (h->streaming) {  // the open chunk belongs to the previous alarms' table
+    rc = stream_flush(h);
+    if (rc) return rc;
+  }
+  HIP_TRY(h, hipStreamSynchronize(h->stream));  // launches in flight read the old table
+  free_lookup(h);
+  rc = build_lookup(h, keys, entry_off, nb_keys, chain, nullptr);
+  if (rc) return rc;
+  HIP_TRY(h, hipStreamSynchronize(h->stream));
+  for (nmg_engine* w : h->workers) {  // multi-GPU: the table on every device
+    rc = nmg_update_objects(w, keys, entry_off, nb_keys, entry_ids, objects);
+    if (rc) return fail(h, rc, w->last_error);
+  }
+  return NMG_OK;
 }
 
 static int stage_reserve(nmg_engine* h, size_t need) {
@@ -1161,6 +1240,7 @@ static int launch_attribution(nmg_engine* h, const uint8_t* data, const BufDesc*
   p.keys = h->d_keys;
   p.nodes = h->d_nodes;
   p.entries = h->d_entries;
+  p.chain = h->d_chain;
   p.ffences = h->d_ffences;
   p.fshift = h->d_fshift;
   p.dir = h->d_dir;

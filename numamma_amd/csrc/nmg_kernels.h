@@ -107,9 +107,9 @@ struct DevEntry {
   uint64_t free;   // free_date
   uint64_t hist;   // dense histogram base cell, or kHistSparse
   uint32_t sidx;   // sparse index (valid when hist == kHistSparse && sidx != ~0u)
-  uint32_t first;  // (node records) entry id of the node's newest entry
+  uint32_t id;     // entry id: the counters' index (node records: of the node's newest entry)
   uint32_t count;  // (node records) entries of the node
-  uint32_t pad0;
+  uint32_t first;  // (node records) table position of the newest entry; the older ones follow it
   uint64_t pad1;
 };
 static_assert(sizeof(DevEntry) == 64, "DevEntry");
@@ -122,7 +122,9 @@ struct Params {
   uint32_t nb_keys;
   const uint64_t* keys;      // [nb_keys] sorted unique keys
   const DevEntry* nodes;     // [nb_keys] node records
-  const DevEntry* entries;
+  const DevEntry* entries;   // [nb_entries] by entry id (hist, sidx)
+  const DevEntry* chain;     // entries in table order (node i's: [first, first + count)); the table
+                             // of the last nmg_set_objects / nmg_update_objects
   // large tables (nb_keys > kLdsNodes): fence b = keys[b * fence_step]
   const uint64_t* ffences;   // [2^kFenceLevels] fences in Eytzinger order, [0] unused, ~0 padding
   const uint8_t* fshift;     // [nb_fences] slot width log2 of bucket b's directory, or kShiftSearch

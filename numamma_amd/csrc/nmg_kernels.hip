@@ -217,7 +217,7 @@ __device__ __forceinline__ Match find_entry(const Params& p, const Lookup& L, ui
       m.baddr = (uint64_t(a.y) << 32) | a.x;
       m.hist = inf.x == kEmpty32 ? kHistSparse : (uint64_t)inf.x;
     } else if (inf.y >> 31) {
-      match_older(p, inf.y & 0x7fffffffu, p.enodes[idx].count, addr, ts, m);
+      match_older(p, p.enodes[idx].first, p.enodes[idx].count, addr, ts, m);
     }
     return m;
   }
@@ -232,7 +232,7 @@ __device__ __forceinline__ Match find_entry(const Params& p, const Lookup& L, ui
     return m;
   }
   const uint4 d = q[3];
-  if (d.x > 1) match_older(p, c.w, d.x, addr, ts, m);
+  if (d.x > 1) match_older(p, d.y, d.x, addr, ts, m);  // (count, first)
   return m;
 }
 

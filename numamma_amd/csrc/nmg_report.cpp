@@ -424,21 +424,24 @@ int write_report(const nmg_host_results* r, const nmg_object_meta* meta, const n
     else fflush(out);
   };
 
-  // ---- mem_sampling_finalize's messages (mem_sampling.c:321-344)
+  // ---- mem_sampling_finalize's messages (mem_sampling.c:321-344; none online, :313)
+  const bool online = opts && opts->online;
   const int nbuf = (int)r->nb_buffers;
-  fprintf(out, "Analyzing %d sample buffers\n", nbuf);
+  if (!online) fprintf(out, "Analyzing %d sample buffers\n", nbuf);
   uint64_t so_far = 0, found_total = 0;
   size_t total_bytes = 0;
   for (int b = 0; b < nbuf; b++) {
-    if (b % 10 == 0)
+    if (b % 10 == 0 && !online)
       fprintf(out, "\rAnalyzing sample buffer %d/%d. Total samples so far: %zu", b, nbuf, (size_t)so_far);
-    so_far += (uint64_t)(int64_t)(int32_t)r->buf_samples[b];  // int nb_samples (:325, :334)
+    so_far += (uint64_t)(int64_t)(int32_t)r->buf_samples[b];  // int nb_samples (:325, :334, :934)
     found_total += (uint64_t)(int64_t)(int32_t)r->buf_found[b];
     total_bytes += r->buf_bytes[b];
   }
   const uint64_t nb_samples_total = so_far;
-  fprintf(out, "\n");
-  fprintf(out, "%zu bytes processed\n", total_bytes);
+  if (!online) {
+    fprintf(out, "\n");
+    fprintf(out, "%zu bytes processed\n", total_bytes);
+  }
   fprintf(out, "---------------------------------\n");
   fprintf(out, "         MEM ANALYZER\n");
   fprintf(out, "---------------------------------\n");
@@ -449,7 +452,13 @@ int write_report(const nmg_host_results* r, const nmg_object_meta* meta, const n
   if (r->match_samples) {
     for (uint32_t e = 0; e < E; e++)
       if (r->first_ordinal[e] != ~0ull) matched.push_back(e);
-    for (uint32_t e : matched)
+    // objects that reach update_call_sites: the matched ones, or every one online
+    std::vector<uint32_t> updated;
+    if (online)
+      for (uint32_t e = 0; e < E; e++) updated.push_back(e);
+    else
+      updated = matched;
+    for (uint32_t e : updated)
       if (meta[e].callstack == nullptr && meta[e].callstack_size > 3) {
         close_out();
         err = "entry with NULL callstack and callstack_size > 3 (the reference dereferences NULL)";
@@ -461,9 +470,12 @@ int write_report(const nmg_host_results* r, const nmg_object_meta* meta, const n
               [&](uint32_t a, uint32_t b) { return r->first_ordinal[a] < r->first_ordinal[b]; });
     for (uint32_t e : order)
       if (reg.find(e) < 0) reg.create(e, r->buffer_size[e] / kPageSize + 1);
-    // update_call_sites in FOREACH_HASH order (= flattened order)
-    for (uint32_t e : matched) {
-      Site& site = reg.sites[reg.find(e)];
+    // update_call_sites in FOREACH_HASH order (= flattened order); online, an
+    // object never matched finds or creates its site here
+    for (uint32_t e : updated) {
+      int si = reg.find(e);
+      if (si < 0) si = reg.create(e, r->buffer_size[e] / kPageSize + 1);
+      Site& site = reg.sites[si];
       site.nb_mallocs++;
       const uint64_t* cw = r->count_weight + (uint64_t)e * 4;
       site.read_count += cw[0];

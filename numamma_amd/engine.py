@@ -69,6 +69,16 @@ class Engine:
                                     objs.ctypes.data_as(C.POINTER(_lib.nmg_object)), table.nb_entries))
         self.table = table
 
+    def update_objects(self, keys: np.ndarray, entry_off: np.ndarray, entry_ids: np.ndarray, objs: np.ndarray):
+        """nmg_update_objects: the table at an alarm (--online-analysis); objs in
+        table_objects() layout, entry_ids = their ids in the set_objects table."""
+        keys = np.ascontiguousarray(keys, dtype=np.uint64)
+        off = np.ascontiguousarray(entry_off, dtype=np.uint32)
+        ids = np.ascontiguousarray(entry_ids, dtype=np.uint32)
+        objs = np.ascontiguousarray(objs)
+        self._c(lib.nmg_update_objects(self.h, _ptr(keys, C.c_uint64), _ptr(off, C.c_uint32), keys.shape[0],
+                                       _ptr(ids, C.c_uint32), objs.ctypes.data_as(C.POINTER(_lib.nmg_object))))
+
     def submit_ring(self, ring: np.ndarray, tail: int, head: int, thread_rank: int, access: int):
         ring = np.ascontiguousarray(ring, dtype=np.uint8)
         self._c(lib.nmg_submit_ring(self.h, ring.ctypes.data, ring.shape[0], tail, head, thread_rank, access))
@@ -184,7 +194,7 @@ class Engine:
     # ------------------------------------------------------------------
     def report(self, output_dir: str, stdout_path: Optional[str] = None, dump_single_items: int = 1,
                dump_flags: int = 0, maps_path: Optional[str] = None, maps_text: Optional[str] = None,
-               modules=None):
+               modules=None, online: bool = False):
         """nmg_report; dump_flags = NMG_DUMP_* (engine created with
         NMG_F_SAMPLE_MATCHES | NMG_F_OBJECT_LEVELS); modules = [(lo, hi, fbase,
         fname)], dladdr()'s view of the traced process (all_memory_objects.dat)."""
@@ -192,7 +202,7 @@ class Engine:
         marr, nmods = _lib.module_array(modules)
         ro = _lib.nmg_report_options(output_dir.encode(), dump_single_items, dump_flags,
                                      maps_path.encode() if maps_path else None,
-                                     maps_text.encode() if maps_text else None, marr, nmods)
+                                     maps_text.encode() if maps_text else None, marr, nmods, int(online))
         self._c(lib.nmg_report(self.h, meta, C.byref(ro), stdout_path.encode() if stdout_path else None))
         del keep
 

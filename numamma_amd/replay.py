@@ -631,3 +631,54 @@ def _wrap(b: Buffer, rng) -> Buffer:
     slack = np.full(64, 0xAB, dtype=np.uint8)  # stale ring bytes, never read
     ring = np.concatenate([second, slack, first])
     return Buffer(b.thread_rank, b.access_type, ring, second.shape[0] + 64, second.shape[0])
+
+
+# ---------------------------------------------------------------------------
+# --online-analysis: the object table at an alarm (mem_sampling.c:953-954)
+
+
+def table_at(table: ObjectTable, t: int):
+    """The flattened table as __process_samples sees it at an alarm at time t:
+    an entry exists once it is allocated (alloc_date <= t; globals have 0), it
+    carries its free_date only once freed (free_date <= t), 0 before (quirk Q3:
+    a live object never matches), and a key exists while one of its entries
+    does; entries keep their newest-first order.  Returns (keys, entry_off,
+    entry_ids, ent4) for nmg_update_objects / the oracle's alarms, entry_ids
+    indexing `table` (the final one)."""
+    ent = table.entries
+    present = ent["alloc_date"] <= np.uint64(t)
+    eo = table.entry_off.astype(np.int64)
+    key_of = np.repeat(np.arange(table.nb_keys), np.diff(eo))
+    ids = np.flatnonzero(present).astype(np.uint32)
+    kp = key_of[ids]
+    keys_present = np.unique(kp)
+    keys = table.keys[keys_present].astype(np.uint64)
+    off = np.zeros(keys_present.shape[0] + 1, dtype=np.uint32)
+    off[1:] = np.cumsum(np.bincount(np.searchsorted(keys_present, kp), minlength=keys_present.shape[0]))
+    ent4 = np.zeros((ids.shape[0], 4), dtype=np.uint64)
+    ent4[:, 0] = ent["buffer_addr"][ids]
+    ent4[:, 1] = ent["buffer_size"][ids]
+    ent4[:, 2] = ent["alloc_date"][ids]
+    fr = ent["free_date"][ids]
+    ent4[:, 3] = np.where(fr <= np.uint64(t), fr, np.uint64(0))
+    return keys, off, ids, ent4
+
+
+def online_alarms(replay: Replay, nb_alarms: int):
+    """Split a replay whose buffers are in capture order (oldest first) and
+    hold whole 40 B SAMPLE records into nb_alarms consecutive alarms of about
+    equal buffer counts; each alarm fires just after the last sample it
+    collects.  Returns [(buf_end, alarm_time)]."""
+    nb = len(replay.buffers)
+    lin = [b.linear() for b in replay.buffers]
+    last_ts = np.array([int(x.view(RECORD_DTYPE)["timestamp"].max()) if x.shape[0] else 0 for x in lin],
+                       dtype=np.uint64)
+    cuts = [int(round(nb * (i + 1) / nb_alarms)) for i in range(nb_alarms)]
+    out, b0, t = [], 0, 0
+    for c in cuts:
+        if c <= b0:
+            continue
+        t = max(t, int(last_ts[b0:c].max()) + 1)  # (alarms fire in time order)
+        out.append((c, t))
+        b0 = c
+    return out

@@ -72,7 +72,7 @@ class RawResults:
 
 def report_host(res: RawResults, table, buf_bytes: np.ndarray, output_dir: str,
                 stdout_path: Optional[str], match_samples: bool = True, dump_single_items: int = 1,
-                dump_flags: int = 0, modules=None) -> None:
+                dump_flags: int = 0, modules=None, online: bool = False) -> None:
     """nmg_report_host(): the report from host arrays (no GPU involved).
     dump_flags: NMG_DUMP_ALL writes all_memory_objects.dat (the sample dumps
     need the engine's per-sample matches: nmg_report)."""
@@ -106,7 +106,8 @@ def report_host(res: RawResults, table, buf_bytes: np.ndarray, output_dir: str,
     hr.objects = objs.ctypes.data_as(C.POINTER(_lib.nmg_object))
     meta, kmeta = build_meta(table)
     marr, nmods = _lib.module_array(modules)
-    ro = _lib.nmg_report_options(output_dir.encode(), dump_single_items, dump_flags, None, None, marr, nmods)
+    ro = _lib.nmg_report_options(output_dir.encode(), dump_single_items, dump_flags, None, None, marr, nmods,
+                                 int(online))
     _lib.check(_lib.lib.nmg_report_host(C.byref(hr), meta, C.byref(ro),
                                         stdout_path.encode() if stdout_path else None))
     del keep, kmeta

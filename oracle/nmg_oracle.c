@@ -134,6 +134,8 @@ struct o_state {
   uint32_t *buf_samples, *buf_found;
   struct o_site *call_sites; /* mem_analyzer.c:1300 */
   uint32_t next_call_site_id;
+  /* online analysis: the table at the current alarm (NULL: the replay's) */
+  const struct nmo_alarm *snap;
   /* dump modes (settings.dump / dump_all / dump_unmatched) */
   const struct nmo_settings *set;
   const char *outdir;
@@ -375,11 +377,41 @@ static int o_in_buffer(const struct o_mem *m, uint64_t addr, uint64_t ts) {
 /* __ma_find_mem_info_from_sample_generic -- src/mem_analyzer.c:249-286:
  * only the lower-bound node is examined (no fallback to smaller keys); its
  * entries are scanned newest-first and the first hit wins. */
-static int64_t o_find(const struct o_state *st, uint64_t addr, uint64_t ts) {
+static int64_t o_find(const struct o_state *st, uint64_t addr, uint64_t ts, uint64_t *baddr) {
+  if (st->snap) { /* online: the live mem_list at this alarm */
+    const struct nmo_alarm *a = st->snap;
+    int64_t lo = 0, hi = (int64_t)a->nb_keys - 1, k = -1;
+    while (lo <= hi) {
+      int64_t mid = lo + (hi - lo) / 2;
+      if (a->keys[mid] <= addr) {
+        k = mid;
+        lo = mid + 1;
+      } else {
+        hi = mid - 1;
+      }
+    }
+    if (k < 0) return -1;
+    for (uint32_t j = a->entry_off[k]; j < a->entry_off[k + 1]; j++) {
+      struct o_mem m;
+      memset(&m, 0, sizeof(m));
+      m.buffer_addr = a->ent4[4 * j];
+      m.buffer_size = a->ent4[4 * j + 1];
+      m.alloc_date = a->ent4[4 * j + 2];
+      m.free_date = a->ent4[4 * j + 3];
+      if (o_in_buffer(&m, addr, ts)) {
+        *baddr = m.buffer_addr;
+        return a->entry_ids[j];
+      }
+    }
+    return -1;
+  }
   int64_t k = o_lower_key(st, addr);
   if (k < 0) return -1;
   for (uint32_t e = st->entry_off[k]; e < st->entry_off[k + 1]; e++)
-    if (o_in_buffer(&st->mems[e], addr, ts)) return e;
+    if (o_in_buffer(&st->mems[e], addr, ts)) {
+      *baddr = st->mems[e].buffer_addr;
+      return e;
+    }
   return -1;
 }
 
@@ -432,9 +464,10 @@ static struct o_block *o_get_block(struct o_block *block, unsigned page) {
   return NULL;
 }
 
-/* ma_get_block -- src/mem_analyzer.c:525-534 (page_no is an int) */
-static struct o_block *o_ma_get_block(struct o_mem *m, unsigned th, uint64_t addr) {
-  uint64_t offset = addr - m->buffer_addr;
+/* ma_get_block -- src/mem_analyzer.c:525-534 (page_no is an int); baddr =
+ * the object's buffer_addr when the sample was matched */
+static struct o_block *o_ma_get_block(struct o_mem *m, unsigned th, uint64_t addr, uint64_t baddr) {
+  uint64_t offset = addr - baddr;
   int page_no = (int)(offset / PAGE_SIZE);
   return o_get_block(o_head(m->blocks, th), (unsigned)page_no);
 }
@@ -537,12 +570,13 @@ static void o_update_call_sites(struct o_state *st, struct o_mem *m) {
 static int64_t o_match_sample(struct o_state *st, uint64_t addr, uint64_t ts,
                               uint64_t weight, uint64_t data_src, int access,
                               unsigned th, uint64_t ordinal) {
-  int64_t e = o_find(st, addr, ts);
+  uint64_t baddr = 0;
+  int64_t e = o_find(st, addr, ts, &baddr);
   if (e < 0) return -1;
   struct o_mem *m = &st->mems[e];
   if (!m->blocks) m->blocks = o_allocate_counters();
   if (ordinal < m->first_ordinal) m->first_ordinal = ordinal;
-  struct o_block *block = o_ma_get_block(m, th, addr);
+  struct o_block *block = o_ma_get_block(m, th, addr, baddr);
   o_update_counters(block->counters, weight, data_src, access);
   if (!m->call_site) {
     m->call_site = o_find_call_site(st, m);
@@ -1072,16 +1106,29 @@ int nmo_run(const char *replay_path, const char *outdir, const char *stdout_path
   st.buf_samples = calloc(st.nb_buffers ? st.nb_buffers : 1, 4);
   st.buf_found = calloc(st.nb_buffers ? st.nb_buffers : 1, 4);
 
-  /* mem_sampling_finalize -- src/mem_sampling.c:311-346 */
+  /* mem_sampling_finalize -- src/mem_sampling.c:311-346; online, the
+   * buffers were analysed at the alarms (__process_samples, :929-966) and
+   * finalize prints nothing (:313) */
+  const int online = st.set->nb_alarms > 0;
+  if (online && st.set->alarms[st.set->nb_alarms - 1].buf_end != st.nb_buffers) {
+    if (out != stdout) fclose(out);
+    o_free(&st);
+    return NMO_ERR_FORMAT;
+  }
   double t0 = o_now();
-  fprintf(out, "Analyzing %d sample buffers\n", (int)st.nb_buffers);
+  if (!online) fprintf(out, "Analyzing %d sample buffers\n", (int)st.nb_buffers);
   int nb_blocks = 0;
   size_t total_buffer_size = 0;
+  uint32_t alarm = 0;
   for (uint32_t b = 0; b < st.nb_buffers; b++) {
     uint32_t nb = 0, found = 0;
-    if (nb_blocks % 10 == 0)
+    if (online) {
+      while (b >= st.set->alarms[alarm].buf_end) alarm++;
+      st.snap = &st.set->alarms[alarm];
+    } else if (nb_blocks % 10 == 0) {
       fprintf(out, "\rAnalyzing sample buffer %d/%d. Total samples so far: %zu", nb_blocks,
               (int)st.nb_buffers, (size_t)st.nb_samples_total);
+    }
     rc = o_analyze_buffer(&st, b, match, &nb, &found);
     if (rc) break;
     st.buf_samples[b] = nb;
@@ -1097,16 +1144,22 @@ int nmo_run(const char *replay_path, const char *outdir, const char *stdout_path
     o_free(&st);
     return rc;
   }
-  fprintf(out, "\n");
-  fprintf(out, "%zu bytes processed\n", total_buffer_size);
+  st.snap = NULL;
+  if (!online) {
+    fprintf(out, "\n");
+    fprintf(out, "%zu bytes processed\n", total_buffer_size);
+  }
 
   /* ma_finalize -- src/mem_analyzer.c:1809-1881 */
   fprintf(out, "---------------------------------\n");
   fprintf(out, "         MEM ANALYZER\n");
   fprintf(out, "---------------------------------\n");
   /* FOREACH_HASH: keys ascending, each node's entries newest-first */
-  for (uint32_t e = 0; e < st.nb_entries; e++)
+  for (uint32_t e = 0; e < st.nb_entries; e++) {
+    /* online, every object has counters since _init_mem_info (:569-572) */
+    if (online && match && !st.mems[e].blocks) st.mems[e].blocks = o_allocate_counters();
     if (st.mems[e].blocks) o_update_call_sites(&st, &st.mems[e]);
+  }
   o_print_counters(out, st.global_counters);
   if (outdir) rc = o_print_call_site_summary(&st, out, outdir, dump_single);
   if (!rc && outdir && st.set->dump_all) rc = o_print_object_summary(&st);

@@ -23,6 +23,26 @@ struct nmo_settings {
   const struct nmo_module *modules; /* dladdr() of the traced process (all_memory_objects.dat) */
   uint32_t nb_modules;
   uint32_t reserved2;
+  /* --online-analysis (mem_sampling.c:953-954): nb_alarms > 0 analyses the
+   * buffers alarm by alarm, each against the object table as it stands at
+   * that alarm, and reports as ma_finalize does online */
+  const struct nmo_alarm *alarms;
+  uint32_t nb_alarms;
+  uint32_t reserved3;
+};
+
+/* The object table at one alarm, flattened like the replay's (keys
+ * ascending, entries newest-first), and the buffers analysed with it:
+ * [previous alarm's buf_end, buf_end).  entry_ids[j] = index of entry j in
+ * the replay's (final) table, whose counters it updates; ent4[j] = its
+ * (buffer_addr, buffer_size, alloc_date, free_date) at the alarm. */
+struct nmo_alarm {
+  uint32_t buf_end;
+  uint32_t nb_keys;
+  const uint64_t *keys;
+  const uint32_t *entry_off; /* [nb_keys + 1] */
+  const uint32_t *entry_ids;
+  const uint64_t *ent4;
 };
 
 /* Dl_info of the frames in [lo, hi): dli_fbase, dli_fname */

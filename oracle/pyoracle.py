@@ -25,11 +25,17 @@ class _Module(C.Structure):
     _fields_ = [("lo", C.c_uint64), ("hi", C.c_uint64), ("fbase", C.c_uint64), ("fname", C.c_char_p)]
 
 
+class _Alarm(C.Structure):
+    _fields_ = [("buf_end", C.c_uint32), ("nb_keys", C.c_uint32), ("keys", C.c_void_p), ("entry_off", C.c_void_p),
+                ("entry_ids", C.c_void_p), ("ent4", C.c_void_p)]
+
+
 class _Settings(C.Structure):
     _fields_ = [("match_samples", C.c_int), ("dump_single_items", C.c_int), ("dump", C.c_int),
                 ("dump_all", C.c_int), ("dump_unmatched", C.c_int), ("reserved", C.c_int),
                 ("maps_path", C.c_char_p), ("maps_text", C.c_char_p),
-                ("modules", C.POINTER(_Module)), ("nb_modules", C.c_uint32), ("reserved2", C.c_uint32)]
+                ("modules", C.POINTER(_Module)), ("nb_modules", C.c_uint32), ("reserved2", C.c_uint32),
+                ("alarms", C.POINTER(_Alarm)), ("nb_alarms", C.c_uint32), ("reserved3", C.c_uint32)]
 
 
 class _Timing(C.Structure):
@@ -58,17 +64,29 @@ def oracle():
 def run(replay_path: str, outdir: str, stdout_path: str, raw_path: str | None = None,
         match_samples: bool = True, dump_single_items: bool = True, dump: bool = False,
         dump_all: bool = False, dump_unmatched: bool = False, maps_path: str | None = None,
-        maps_text: str | None = None, modules=None) -> dict:
+        maps_text: str | None = None, modules=None, alarms=None) -> dict:
     """Dump modes (-d / -D / -u) write callsite_dump_<id>.dat, callsite_summary_<id>.dat,
     all_memory_accesses.dat, all_memory_objects.dat and unmatched_samples.log into
     outdir like the reference.  modules = [(lo, hi, fbase, fname)]: dladdr()'s view
-    of the traced process, for all_memory_objects.dat."""
+    of the traced process, for all_memory_objects.dat.  alarms = [(buf_end, keys,
+    entry_off, entry_ids, ent4)]: --online-analysis, each alarm's buffers against
+    the table at that alarm (replay.table_at)."""
+    import numpy as np
+
     lib = oracle()
     mods = list(modules or [])
     marr = (_Module * max(1, len(mods)))(*[_Module(lo, hi, fb, fn.encode()) for lo, hi, fb, fn in mods])
+    keep = []
+    al = list(alarms or [])
+    aarr = (_Alarm * max(1, len(al)))()
+    for i, (buf_end, keys, off, ids, ent4) in enumerate(al):
+        arrs = [np.ascontiguousarray(keys, dtype=np.uint64), np.ascontiguousarray(off, dtype=np.uint32),
+                np.ascontiguousarray(ids, dtype=np.uint32), np.ascontiguousarray(ent4, dtype=np.uint64)]
+        keep += arrs
+        aarr[i] = _Alarm(buf_end, arrs[0].shape[0], *[a.ctypes.data for a in arrs])
     s = _Settings(int(match_samples), int(dump_single_items), int(dump), int(dump_all), int(dump_unmatched), 0,
                   maps_path.encode() if maps_path else None, maps_text.encode() if maps_text else None,
-                  marr, len(mods), 0)
+                  marr, len(mods), 0, aarr, len(al), 0)
     t = _Timing()
     rc = lib.nmo_run(replay_path.encode(), outdir.encode(), stdout_path.encode(),
                      raw_path.encode() if raw_path else None, C.byref(s), C.byref(t))

@@ -1,0 +1,135 @@
+"""--online-analysis parity (mem_sampling.c:929-966, branch :953-954): every
+alarm's rings are attributed against the object table as it stands at that
+alarm -- objects not yet allocated are absent, live ones carry free_date 0 and
+never match (quirk Q3) -- and the counters accumulate across alarms; the
+report is ma_finalize's online one (no finalize lines, every object reaches
+update_call_sites).  The engine gets each alarm's table through
+nmg_update_objects while it streams; the oracle replays the same alarms
+(replay.table_at).  Bit-exact: raw counters, per-buffer tallies, page cells,
+stdout, call_sites.log and every callsite_counters_<id>.dat."""
+import os
+
+import numpy as np
+import pytest
+
+import pyoracle
+from numamma_amd import _lib
+from numamma_amd.replay import SynthConfig, generate, online_alarms, table_at
+from numamma_amd.results import RawResults
+
+pytestmark = pytest.mark.gpu
+
+CASES = [
+    # small table (LDS Eytzinger path), address reuse: entries appear and are freed mid-run
+    (SynthConfig(nb_samples=120_000, nb_intervals=400, nb_threads=4, with_stack=False, reuse_frac=0.3,
+                 buffer_records=300, seed=71), 6, 1 << 20),
+    # large table (fences + directory), one chunk per alarm and several
+    (SynthConfig(nb_samples=200_000, nb_intervals=30_000, nb_threads=8, with_stack=False, reuse_frac=0.2,
+                 realloc_frac=0.05, buffer_records=500, seed=72), 5, 256 << 10),
+    # a single alarm at the end: every object freed by then matches as offline would
+    (SynthConfig(nb_samples=60_000, nb_intervals=2_000, nb_threads=2, with_stack=False, buffer_records=400,
+                 seed=73), 1, 4 << 20),
+]
+
+
+def _ent_objs(ent4):
+    objs = np.zeros(ent4.shape[0], dtype=[("a", "<u8"), ("s", "<u8"), ("al", "<u8"), ("fr", "<u8")])
+    objs["a"], objs["s"], objs["al"], objs["fr"] = ent4[:, 0], ent4[:, 1], ent4[:, 2], ent4[:, 3]
+    return objs
+
+
+def _same_dirs(a, b):
+    fa, fb = sorted(os.listdir(a)), sorted(os.listdir(b))
+    assert fa == fb
+    for f in fa:
+        assert open(os.path.join(a, f), "rb").read() == open(os.path.join(b, f), "rb").read(), f
+
+
+@pytest.mark.parametrize("cfg,nb_alarms,chunk", CASES, ids=["k400", "k30k", "one_alarm"])
+def test_online_analysis_bit_exact(tmp_path, cfg, nb_alarms, chunk):
+    from numamma_amd.engine import Engine
+
+    d = str(tmp_path)
+    rp = generate(cfg)
+    rp.buffers.reverse()  # online: rings are analysed as they are collected, oldest first
+    alarms = online_alarms(rp, nb_alarms)
+    snaps = [(be,) + table_at(rp.table, t) for be, t in alarms]
+    path = os.path.join(d, "replay.bin")
+    rp.write(path)
+    odir = os.path.join(d, "oracle")
+    pyoracle.run(path, odir, os.path.join(d, "o.txt"), os.path.join(d, "o_raw.bin"), alarms=snaps)
+    raw = RawResults.read(os.path.join(d, "o_raw.bin"))
+    assert raw.nb_found > 0  # objects freed before an alarm did match
+
+    eng = Engine(flags=_lib.NMG_F_DEFAULT, nb_threads=rp.nb_threads)
+    eng.set_objects(rp.table)  # the final table: ids, page cells, report metadata
+    eng.stream_begin(chunk_bytes=chunk, copy_threads=2)
+    b0 = 0
+    for be, keys, off, ids, ent4 in snaps:
+        eng.update_objects(keys, off, ids, _ent_objs(ent4))
+        for b in rp.buffers[b0:be]:
+            eng.submit_ring(b.ring, b.data_tail, b.data_head, b.thread_rank, b.access_type)
+        b0 = be
+    eng.analyze()
+    eng.stream_end()
+    eng.synchronize()
+    g, ns, nf = eng.global_counters()
+    assert np.array_equal(g, raw.global_counters) and (ns, nf) == (raw.nb_samples, raw.nb_found)
+    s, f = eng.buffer_counts()
+    assert np.array_equal(s, raw.buf_samples) and np.array_equal(f, raw.buf_found)
+    first, cw = eng.object_counters()
+    assert np.array_equal(first, raw.first_ordinal)
+    assert np.array_equal(cw, raw.count_weight)
+    assert np.array_equal(eng.page_cells(), raw.cells)
+    edir = os.path.join(d, "engine")
+    eng.report(edir, os.path.join(d, "e.txt"), online=True)
+    eng.close()
+    assert open(os.path.join(d, "o.txt"), "rb").read() == open(os.path.join(d, "e.txt"), "rb").read()
+    _same_dirs(odir, edir)
+
+
+def test_online_table_updates_keep_counters(tmp_path):
+    """Updating to the same table between analyses changes nothing: the
+    counters of one stream equal those of the stream split by updates."""
+    from numamma_amd.engine import Engine, table_objects
+
+    rp = generate(SynthConfig(nb_samples=80_000, nb_intervals=3_000, seed=74))
+    t = rp.table
+    lins = rp.linear_buffers()
+    res = []
+    for split in (False, True):
+        eng = Engine(nb_threads=rp.nb_threads)
+        eng.set_objects(t)
+        eng.stream_begin(chunk_bytes=1 << 20, copy_threads=1)
+        for i, (r, a, data) in enumerate(lins):
+            if split and i % 7 == 0:
+                eng.update_objects(t.keys, t.entry_off, np.arange(t.nb_entries, dtype=np.uint32), table_objects(t))
+            eng.submit_buffer(data, r, a)
+        eng.analyze()
+        eng.stream_end()
+        eng.synchronize()
+        res.append((eng.global_counters()[0], eng.object_counters()[1], eng.page_cells()))
+        eng.close()
+    for a, b in zip(*res):
+        assert np.array_equal(a, b)
+
+
+def test_update_objects_rejects_bad_tables():
+    from numamma_amd.engine import Engine, table_objects
+
+    rp = generate(SynthConfig(nb_samples=1_000, nb_intervals=50, seed=75))
+    t = rp.table
+    eng = Engine(nb_threads=rp.nb_threads)
+    eng.set_objects(t)
+    ids = np.arange(t.nb_entries, dtype=np.uint32)
+    objs = table_objects(t)
+    bad = ids.copy()
+    bad[3] = t.nb_entries  # past the set_objects table
+    with pytest.raises(RuntimeError):
+        eng.update_objects(t.keys, t.entry_off, bad, objs)
+    big = objs.copy()
+    big["s"][5] += 1 << 20  # larger than its page cells
+    with pytest.raises(RuntimeError):
+        eng.update_objects(t.keys, t.entry_off, ids, big)
+    eng.update_objects(t.keys[:0], np.zeros(1, dtype=np.uint32), ids[:0], objs[:0])  # empty table at an alarm
+    eng.close()
