@@ -6,6 +6,7 @@
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
+#include <rocprofiler-sdk-roctx/roctx.h>
 
 #include <algorithm>
 #include <functional>
@@ -25,6 +26,15 @@
 // host side
 
 using namespace nmg;
+
+// roctx range over one host-side stage (rocprofv3 --marker-trace): stage,
+// attribution enqueue, merge, table swap, report
+struct Range {
+  explicit Range(const char* what) { roctxRangePushA(what); }
+  ~Range() { roctxRangePop(); }
+  Range(const Range&) = delete;
+  Range& operator=(const Range&) = delete;
+};
 
 // Persistent host threads for the staging copies of nmg_submit_buffers (a
 // batch per alarm in streaming mode would otherwise pay a thread start per
@@ -596,6 +606,7 @@ static int build_lookup(nmg_engine* h, const uint64_t* keys, const uint32_t* ent
 
 extern "C" int nmg_set_objects(nmg_engine* h, const uint64_t* keys, const uint32_t* entry_off,
                                uint32_t nb_keys, const nmg_object* entries, uint32_t nb_entries) {
+  Range range("nmg_set_objects");
   if (!h || (nb_keys && (!keys || !entry_off)) || (nb_entries && !entries))
     return NMG_ERR_INVALID;
   int rc = check_table(h, keys, entry_off, nb_keys, nb_entries);
@@ -692,6 +703,7 @@ static int stream_flush(nmg_engine* h);
 // ids), counters kept (mem_sampling.c:953-954 against the live mem_list)
 extern "C" int nmg_update_objects(nmg_engine* h, const uint64_t* keys, const uint32_t* entry_off,
                                   uint32_t nb_keys, const uint32_t* entry_ids, const nmg_object* objects) {
+  Range range("nmg_update_objects");
   if (!h || (nb_keys && (!keys || !entry_off || !entry_ids || !objects))) return NMG_ERR_INVALID;
   if (!h->have_table) return fail(h, NMG_ERR_STATE, "nmg_update_objects before nmg_set_objects");
   const uint32_t n = nb_keys ? entry_off[nb_keys] : 0;
@@ -904,6 +916,7 @@ static int ensure_bufcnt(nmg_engine* h, size_t need) {
 // the slot's previous kernel released its device arena), then the kernel on
 // the engine stream once the copy has landed.
 static int stream_flush(nmg_engine* h) {
+  Range range("nmg_stream_chunk");
   auto& sl = h->slots[h->cur_slot];
   if (sl.descs.empty()) return NMG_OK;
   const uint32_t nb = (uint32_t)sl.descs.size();
@@ -1128,6 +1141,7 @@ extern "C" int nmg_clear_buffers(nmg_engine* h) {
 }
 
 static int upload_buffers(nmg_engine* h) {
+  Range range("nmg_stage_h2d");
   if (!h->external && h->staged_dirty) {
     if (h->stage_len + 64 > h->arena_cap) {
       HIP_TRY(h, hipStreamSynchronize(h->stream));
@@ -1230,6 +1244,7 @@ static uint32_t attribution_grid(nmg_engine* h, uint32_t nb) {
 // bracketed by the launch-timing events.
 static int launch_attribution(nmg_engine* h, const uint8_t* data, const BufDesc* sdescs, const uint32_t* ranges,
                               uint32_t nb, uint32_t grid, uint64_t nbytes) {
+  Range range("nmg_attribute");
   Params p;
   memset(&p, 0, sizeof(p));
   p.data = data;
@@ -1422,6 +1437,7 @@ static int multi_analyze(nmg_engine* h);
 static int multi_finish(nmg_engine* h);
 
 extern "C" int nmg_analyze(nmg_engine* h) {
+  Range range("nmg_analyze");
   if (!h) return NMG_ERR_INVALID;
   if (!h->have_table) return fail(h, NMG_ERR_STATE, "nmg_analyze before nmg_set_objects");
   if (h->multi) return multi_analyze(h);
@@ -1739,6 +1755,7 @@ static void* array_ptr(nmg_engine* h, int which, size_t* bytes) {
 }
 
 extern "C" int nmg_export_array(nmg_engine* h, int which, void* d_dst) {
+  Range range("nmg_export_array");
   if (!h || !h->have_table) return NMG_ERR_INVALID;
   size_t bytes = 0;
   void* src = array_ptr(h, which, &bytes);
@@ -1751,6 +1768,7 @@ extern "C" int nmg_export_array(nmg_engine* h, int which, void* d_dst) {
 }
 
 extern "C" int nmg_import_array(nmg_engine* h, int which, const void* d_src) {
+  Range range("nmg_import_array");
   if (!h || !h->have_table) return NMG_ERR_INVALID;
   size_t bytes = 0;
   void* dst = array_ptr(h, which, &bytes);
@@ -1928,6 +1946,7 @@ static void multi_destroy(nmg_engine* h) {
 // devices), or device-side merges (one device).  Per-buffer counts and sparse
 // cells are gathered at nmg_synchronize (multi_finish).
 static int multi_analyze(nmg_engine* h) {
+  Range range("nmg_multi_analyze");
   if (h->multi_pending) {
     const int rc = multi_finish(h);
     if (rc) return rc;
@@ -2018,6 +2037,7 @@ static int multi_analyze(nmg_engine* h) {
 // sparse cells (summed by key) into this handle; the workers are reset so
 // that a later nmg_analyze adds only its own samples
 static int multi_finish(nmg_engine* h) {
+  Range range("nmg_multi_merge");
   h->multi_pending = false;
   for (nmg_engine* w : h->workers) {
     const int rc = nmg_synchronize(w);
@@ -2069,6 +2089,7 @@ static int multi_finish(nmg_engine* h) {
 
 extern "C" int nmg_report(nmg_engine* h, const nmg_object_meta* meta, const nmg_report_options* opts,
                           const char* stdout_path) {
+  Range range("nmg_report");
   if (!h || (h->E && !meta)) return NMG_ERR_INVALID;
   if (!h->have_table) return fail(h, NMG_ERR_STATE, "nmg_report before nmg_set_objects");
   HostResults r;

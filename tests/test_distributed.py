@@ -1,11 +1,12 @@
-"""The multi-GPU merge path on CPU: world size 2 over gloo.
-
-Each rank analyses a contiguous, byte-balanced shard of the buffer list (with
-its global seq_base) -- here with the CPU oracle standing in for a rank's GPU
-partial results -- and the product's merge primitives (reduce_u64 with the
-x ^ 2^63 order map for MIN/MAX, variable-length gathers) combine them on rank
-0.  The merged counters must produce a report byte-identical to a single
-unsharded run."""
+"""The merge algebra of the one-process-per-GPU path on CPU (world size 2 over
+gloo, no GPU): each rank's partial counters for a contiguous, byte-balanced
+shard (with its global seq_base) -- computed here by the oracle, since no
+engine runs without a GPU -- are combined by the product's merge primitives
+(reduce_u64 with the x ^ 2^63 order map for MIN/MAX, variable-length gathers,
+merge_sparse) on rank 0, and the merged counters must give a report
+byte-identical to a single unsharded run.  The same chain through the engine
+itself (nmg_export_array -> reduce -> nmg_import_array) runs on the GPU in
+tests/test_gpu_distributed.py."""
 import os
 import socket
 import sys

@@ -1,0 +1,113 @@
+"""The one-process-per-GPU merge through the product: two ranks (gloo, both on
+GPU 0 of the test box) each analyse a contiguous byte-balanced shard of the
+buffer list with its seq_base, then merge_engine runs the engine's
+nmg_export_array -> reduce_u64 / reduce_u32_sum -> nmg_import_array chain and
+the sparse / per-buffer gathers; rank 0 reports.  The merged counters and
+every report file must equal the oracle's single unsharded run."""
+import os
+import socket
+import sys
+import tempfile
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+pytestmark = pytest.mark.gpu
+
+CFGS = {
+    "k700": dict(nb_samples=200_000, nb_intervals=700, lost_frac=1e-3, seed=21),
+    # large-table path, hashed objects, cell log, [stack] sparse cells
+    "k60k": dict(nb_samples=300_000, nb_intervals=60_000, seed=22),
+}
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, workdir, cfg_name, ret):
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "oracle")]
+    try:
+        import torch
+        import torch.distributed as dist
+
+        from numamma_amd.distributed import merge_engine, shard_ranges
+        from numamma_amd.engine import Engine
+        from numamma_amd.replay import SynthConfig, generate
+
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+        rp = generate(SynthConfig(**CFGS[cfg_name]))
+        arena, offs, lens, ranks, acc = rp.packed()
+        lo, hi = shard_ranges(lens, world)[rank]
+        dev = torch.device("cuda", 0)
+        base = int(offs[lo]) if hi > lo else 0
+        end = int(offs[hi - 1] + lens[hi - 1]) if hi > lo else 0
+        d_arena = torch.from_numpy(arena[base:end].copy()).to(dev)
+        eng = Engine(device=0, nb_threads=rp.nb_threads)
+        eng.set_objects(rp.table)
+        eng.set_device_buffers(d_arena.data_ptr(), offs[lo:hi] - base, lens[lo:hi], ranks[lo:hi], acc[lo:hi],
+                               seq_base=lo)
+        eng.analyze()
+        eng.synchronize()
+        merge_engine(eng, dst=0, device=dev)
+        if rank == 0:
+            edir = os.path.join(workdir, "engine")
+            eng.report(edir, os.path.join(workdir, "e.txt"))
+            g, ns, nf = eng.global_counters()
+            first, cw = eng.object_counters()
+            np.savez(os.path.join(workdir, "merged.npz"), g=g, ns=ns, nf=nf, first=first, cw=cw,
+                     cells=eng.page_cells())
+        eng.close()
+        dist.barrier()
+        dist.destroy_process_group()
+        ret.put((rank, "ok"))
+    except Exception as e:  # surfaced by the parent
+        import traceback
+
+        ret.put((rank, traceback.format_exc()))
+        raise
+
+
+@pytest.mark.parametrize("cfg_name", sorted(CFGS))
+def test_two_rank_engine_merge_matches_oracle(cfg_name):
+    import multiprocessing as mp
+
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "oracle")]
+    import pyoracle
+    from numamma_amd.replay import SynthConfig, generate
+    from numamma_amd.results import RawResults
+
+    ctx = mp.get_context("spawn")
+    ret = ctx.Queue()
+    with tempfile.TemporaryDirectory() as d:
+        port = _free_port()
+        procs = [ctx.Process(target=_worker, args=(r, 2, port, d, cfg_name, ret)) for r in range(2)]
+        for p in procs:
+            p.start()
+        msgs = [ret.get(timeout=240) for _ in procs]
+        for p in procs:
+            p.join(timeout=60)
+        for rank, msg in msgs:
+            assert msg == "ok", f"rank {rank}:\n{msg}"
+        assert all(p.exitcode == 0 for p in procs)
+        rp = generate(SynthConfig(**CFGS[cfg_name]))
+        full = os.path.join(d, "full.bin")
+        rp.write(full)
+        pyoracle.run(full, os.path.join(d, "oracle"), os.path.join(d, "o.txt"), os.path.join(d, "o_raw.bin"))
+        raw = RawResults.read(os.path.join(d, "o_raw.bin"))
+        m = np.load(os.path.join(d, "merged.npz"))
+        assert np.array_equal(m["g"], raw.global_counters)
+        assert (int(m["ns"]), int(m["nf"])) == (raw.nb_samples, raw.nb_found)
+        assert np.array_equal(m["first"], raw.first_ordinal)
+        assert np.array_equal(m["cw"], raw.count_weight)
+        assert np.array_equal(m["cells"], raw.cells)
+        assert open(os.path.join(d, "o.txt"), "rb").read() == open(os.path.join(d, "e.txt"), "rb").read()
+        for f in sorted(os.listdir(os.path.join(d, "oracle"))):
+            assert open(os.path.join(d, "oracle", f), "rb").read() == \
+                open(os.path.join(d, "engine", f), "rb").read(), f
