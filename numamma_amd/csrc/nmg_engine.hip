@@ -163,6 +163,7 @@ struct nmg_engine {
   uint32_t* d_ranges = nullptr;  // per-workgroup [begin, end) in d_order
   uint32_t sched_grid = 0;       // grid the current schedule was built for
   bool descs_dirty = false;
+  bool multi_staged = false;  // the workers' arenas hold the current buffers (multi_analyze)
   uint32_t* d_bufcnt = nullptr;
   size_t bufcnt_cap = 0;     // buffers the per-buffer count array holds ([2][bufcnt_stride] u32)
   size_t bufcnt_stride = 0;
@@ -770,6 +771,7 @@ static int append_desc(nmg_engine* h, uint64_t len, uint32_t thread_rank, uint32
   h->stage_len = (h->stage_len + len + 15) & ~size_t(15);
   h->staged_dirty = true;
   h->descs_dirty = true;
+  h->multi_staged = false;
   return NMG_OK;
 }
 
@@ -1111,6 +1113,7 @@ extern "C" int nmg_set_device_buffers(nmg_engine* h, const void* d_data, const u
   h->external = true;
   h->staged_dirty = false;
   h->descs_dirty = true;
+  h->multi_staged = false;
   h->stage_len = 0;
   return NMG_OK;
 }
@@ -1136,6 +1139,7 @@ extern "C" int nmg_clear_buffers(nmg_engine* h) {
   h->external = false;
   h->d_data = nullptr;
   h->descs_dirty = true;
+  h->multi_staged = false;
   h->counts_override = false;
   return NMG_OK;
 }
@@ -1952,6 +1956,8 @@ static int multi_analyze(nmg_engine* h) {
     if (rc) return rc;
   }
   const uint32_t n = (uint32_t)h->workers.size(), nb = (uint32_t)h->descs.size();
+  // the buffers go to the workers once; later steps re-analyse them in place
+  const bool stage = !h->multi_staged;
   std::vector<uint64_t> csum(nb + 1, 0);
   for (uint32_t b = 0; b < nb; b++) csum[b + 1] = csum[b] + h->descs[b].len + 64;
   std::vector<uint32_t> cut(n + 1, nb);
@@ -1972,15 +1978,18 @@ static int multi_analyze(nmg_engine* h) {
       acc.push_back(h->descs[k].access);
     }
     HIP_TRY(h, hipSetDevice(w->device));
-    if (span + 64 > h->warena_cap[i]) {
-      HIP_TRY(h, hipStreamSynchronize(w->stream));
-      (void)hipFree(h->warena[i]);
-      h->warena[i] = nullptr;
-      h->warena_cap[i] = span + 64;
-      HIP_TRY(h, hipMalloc(&h->warena[i], h->warena_cap[i]));
+    int rc = NMG_OK;
+    if (stage) {
+      if (span + 64 > h->warena_cap[i]) {
+        HIP_TRY(h, hipStreamSynchronize(w->stream));
+        (void)hipFree(h->warena[i]);
+        h->warena[i] = nullptr;
+        h->warena_cap[i] = span + 64;
+        HIP_TRY(h, hipMalloc(&h->warena[i], h->warena_cap[i]));
+      }
+      if (span) HIP_TRY(h, hipMemcpyAsync(h->warena[i], h->h_stage + base, span, hipMemcpyHostToDevice, w->stream));
+      rc = nmg_set_device_buffers(w, h->warena[i], offs.data(), lens.data(), ranks.data(), acc.data(), b - a, a);
     }
-    if (span) HIP_TRY(h, hipMemcpyAsync(h->warena[i], h->h_stage + base, span, hipMemcpyHostToDevice, w->stream));
-    int rc = nmg_set_device_buffers(w, h->warena[i], offs.data(), lens.data(), ranks.data(), acc.data(), b - a, a);
     if (!rc) rc = nmg_analyze(w);
     if (rc) return fail(h, rc, w->last_error);
   }
@@ -2028,6 +2037,7 @@ static int multi_analyze(nmg_engine* h) {
       if (bytes) HIP_TRY(h, launch_merge(h->stream, dst, src, bytes / (x.op == 3 ? 4 : 8), x.op));
     }
   }
+  h->multi_staged = true;
   h->multi_pending = true;
   h->launched = false;
   return NMG_OK;

@@ -27,7 +27,7 @@ for s in $STAGES; do
       tail -5 $OUT/pytest_gpu_$TAG.log ;;
     bench)
       echo "== bench"
-      timeout -k 10 600 python bench.py --steps 20 --warmup 3 > $OUT/bench_$TAG.json 2> $OUT/bench_$TAG.err \
+      timeout -k 10 900 python bench.py > $OUT/bench_$TAG.json 2> $OUT/bench_$TAG.err \
         || { echo "bench failed"; tail -40 $OUT/bench_$TAG.err; exit 1; }
       cat $OUT/bench_$TAG.json ;;
     bench3)
@@ -84,11 +84,26 @@ for s in $STAGES; do
       for c in FETCH_SIZE WRITE_SIZE; do
         rm -rf $OUT/traffic_${TAG}_$c
         timeout -k 10 300 rocprofv3 --pmc $c --kernel-trace -d $ROOT/$OUT/traffic_${TAG}_$c -o run --output-format csv \
-          -- python3 $ROOT/bench.py --workload ${TRAFFIC_WL:-c2} --steps 3 --warmup 1 --no-cpu-baseline \
+          -- python3 $ROOT/bench.py --workload ${TRAFFIC_WL:-c2} --secondary "" --steps 3 --warmup 1 --no-cpu-baseline \
           > $OUT/traffic_${TAG}_$c.log 2>&1 || { echo "traffic pass $c failed"; tail -20 $OUT/traffic_${TAG}_$c.log; exit 1; }
       done
+      # the record stream of one launch (40 B records) is the only x2-corrected part
       python3 tools/pmc_summary.py $OUT/traffic_${TAG}_FETCH_SIZE $OUT/traffic_${TAG}_WRITE_SIZE \
+        ${TRAFFIC_STREAM:+--stream-bytes $TRAFFIC_STREAM} \
         > $OUT/pmc_${TRAFFIC_WL:-c2}_$TAG.json && cat $OUT/pmc_${TRAFFIC_WL:-c2}_$TAG.json ;;
+    marker)
+      # roctx ranges (stage, attribute, merge, report) beside the kernel trace
+      echo "== rocprofv3 marker + kernel trace"
+      rm -rf $OUT/marker_$TAG
+      timeout -k 10 600 rocprofv3 --marker-trace --kernel-trace --stats -d $ROOT/$OUT/marker_$TAG -o run --output-format csv \
+        -- python3 $ROOT/bench.py --steps 5 --warmup 1 --no-cpu-baseline --secondary "" > $OUT/marker_$TAG.log 2>&1 \
+        || { echo "marker trace failed"; tail -30 $OUT/marker_$TAG.log; exit 1; }
+      find $OUT/marker_$TAG -name "*marker*" | head ;;
+    merge)
+      echo "== merge timing (${MERGE_WL:-c4})"
+      timeout -k 10 900 python tools/merge_timing.py --workload ${MERGE_WL:-c4} > $OUT/merge_$TAG.json 2> $OUT/merge_$TAG.err \
+        || { echo "merge timing failed"; tail -30 $OUT/merge_$TAG.err; exit 1; }
+      cat $OUT/merge_$TAG.json ;;
     l2)
       # L2 hit rate and memory-side atomics of the attribution kernel
       echo "== rocprofv3 L2 passes (${L2_WL:-k1m})"
