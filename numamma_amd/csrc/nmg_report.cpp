@@ -426,6 +426,11 @@ int write_report(const nmg_host_results* r, const nmg_object_meta* meta, const n
 
   // ---- mem_sampling_finalize's messages (mem_sampling.c:321-344; none online, :313)
   const bool online = opts && opts->online;
+  if (online && opts->dump_flags) {  // the reference's _dump_* read the NULL `samples` list online
+    close_out();
+    err = "dump modes are not available with online analysis (mem_sampling.c:644, 764, 799)";
+    return NMG_ERR_INVALID;
+  }
   const int nbuf = (int)r->nb_buffers;
   if (!online) fprintf(out, "Analyzing %d sample buffers\n", nbuf);
   uint64_t so_far = 0, found_total = 0;

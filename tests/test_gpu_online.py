@@ -114,7 +114,7 @@ def test_online_table_updates_keep_counters(tmp_path):
         assert np.array_equal(a, b)
 
 
-def test_update_objects_rejects_bad_tables():
+def test_update_objects_rejects_bad_tables(tmp_path):
     from numamma_amd.engine import Engine, table_objects
 
     rp = generate(SynthConfig(nb_samples=1_000, nb_intervals=50, seed=75))
@@ -132,4 +132,6 @@ def test_update_objects_rejects_bad_tables():
     with pytest.raises(RuntimeError):
         eng.update_objects(t.keys, t.entry_off, ids, big)
     eng.update_objects(t.keys[:0], np.zeros(1, dtype=np.uint32), ids[:0], objs[:0])  # empty table at an alarm
+    with pytest.raises(RuntimeError):  # dump modes read the NULL `samples` list online in the reference
+        eng.report(str(tmp_path), os.path.join(str(tmp_path), "x.txt"), dump_flags=_lib.NMG_DUMP_ALL, online=True)
     eng.close()
