@@ -221,45 +221,17 @@ __device__ __forceinline__ Match find_entry(const Params& p, const Lookup& L, ui
     }
     return m;
   }
-  return m;
-}
-
-// Large tables, in two halves so that independent work can run while the node
-// record is in flight: node_issue (lower bound + the node record's loads),
-// node_match (the newest entry, then the older ones).
-struct NodePre {
-  uint32_t k;  // lower-bound key index (nb_keys: none)
-  uint4 a, b, c;
-};
-
-__device__ __forceinline__ NodePre node_issue(const Params& p, const Lookup& L, bool valid, uint64_t addr,
-                                              const SpecDir& sp) {
-  NodePre n;
-  n.k = valid ? lower_key(p, L.fences, L.shift, addr, sp) : p.nb_keys;
-  n.a = n.b = n.c = make_uint4(0, 0, 0, 0);
-  if (n.k < p.nb_keys) {
-    const uint4* q = reinterpret_cast<const uint4*>(p.nodes + n.k);
-    n.a = q[0];
-    n.b = q[1];
-    n.c = q[2];
-  }
-  return n;
-}
-
-__device__ __forceinline__ Match node_match(const Params& p, const NodePre& n, uint64_t addr, uint64_t ts) {
-  Match m;
-  m.e = -1;
-  m.baddr = 0;
-  m.hist = kHistSparse;
-  if (n.k >= p.nb_keys) return m;
-  const uint4 a = n.a, b = n.b, c = n.c;
+  const uint32_t k = lower_key(p, L.fences, L.shift, addr, sp);
+  if (k >= p.nb_keys) return m;
+  const uint4* q = reinterpret_cast<const uint4*>(p.nodes + k);
+  const uint4 a = q[0], b = q[1], c = q[2];
   if (entry_match(a, b, addr, ts)) {
     m.e = c.w;
     m.baddr = (uint64_t(a.y) << 32) | a.x;
     m.hist = (uint64_t(c.y) << 32) | c.x;
     return m;
   }
-  const uint4 d = reinterpret_cast<const uint4*>(p.nodes + n.k)[3];
+  const uint4 d = q[3];
   if (d.x > 1) match_older(p, d.y, d.x, addr, ts, m);  // (count, first)
   return m;
 }
@@ -301,10 +273,6 @@ __device__ __forceinline__ void process_sample(Params& p, WgCounters& wc, LaneAc
   vmask = __ballot(valid);
   fmask = 0;
   if (vmask == 0) return;
-  // large tables: the node record's loads go out first; the global counters
-  // below do not depend on them and run while they are in flight
-  NodePre np;
-  if ((MODE & kModeLarge) && (p.flags & NMG_F_MATCH_SAMPLES)) np = node_issue(p, L, valid, addr, sp);
   if (valid && !(p.flags & kDbgNoGlobal)) {
     const uint32_t bm = bucket_mask(lvl);
     if (w < kLaneMaxWeight) {  // register accumulation (no LDS traffic)
@@ -349,11 +317,7 @@ __device__ __forceinline__ void process_sample(Params& p, WgCounters& wc, LaneAc
   // ---- __match_sample (mem_sampling.c:594-673)
   Match m;
   m.e = -1;
-  if (MODE & kModeLarge) {
-    if (valid) m = node_match(p, np, addr, ts);
-  } else if (valid) {
-    m = find_entry<MODE>(p, L, addr, ts, sp);
-  }
+  if (valid) m = find_entry<MODE>(p, L, addr, ts, sp);
   const int64_t e = m.e;
   fmask = __ballot(e >= 0);
   sub_stamp<TIMING>(st, 1);
