@@ -140,10 +140,6 @@ struct nmg_engine {
   size_t tlog_bytes = 0;
   uint32_t* d_tlog_cnt = nullptr;
   size_t tlog_cnt_cap = 0;
-  unsigned long long* d_plog = nullptr;  // large tables: page-cell log (Params::plog)
-  size_t plog_bytes = 0;
-  uint32_t* d_plog_cnt = nullptr;
-  size_t plog_cnt_cap = 0;
   size_t smatch_cap = 0;
   uint64_t nreset = 0;
 
@@ -285,12 +281,6 @@ static void free_counters(nmg_engine* h) {
   (void)hipFree(h->d_tlog_cnt);
   h->d_tlog_cnt = nullptr;
   h->tlog_cnt_cap = 0;
-  (void)hipFree(h->d_plog);
-  h->d_plog = nullptr;
-  h->plog_bytes = 0;
-  (void)hipFree(h->d_plog_cnt);
-  h->d_plog_cnt = nullptr;
-  h->plog_cnt_cap = 0;
 }
 
 // the lookup structures of one table (keys, node records, LDS tree or fences
@@ -1334,44 +1324,6 @@ static int launch_attribution(nmg_engine* h, const uint8_t* data, const BufDesc*
     p.tlog_rshift = rshift;
     p.tlog_parts = parts;
   }
-  // page-cell log: large tables (its cursors live in the lookup LDS region's
-  // spare part) with hashed page cells
-  if (!(mode & kModeDensePage) && !p.lds_nodes && nb && h->hist_cells && grid <= kLogMaxGrid &&
-      (h->flags & NMG_F_MATCH_SAMPLES) && (h->flags & NMG_F_PAGE_HIST) && nbytes / 8 < (1ull << 32)) {
-    // cell ranges (plog_reduce_kernel), 8 B records
-    uint32_t cshift = 0;
-    const size_t rec = 8;
-    while (((h->hist_cells + (1ull << cshift) - 1) >> cshift) > kPlogMaxParts) cshift++;
-    // parts of at least a few hundred cells (fewer, longer sub-logs)
-    while (cshift < 9 && ((uint64_t)h->T << (cshift + 1)) <= kPlogWin) cshift++;
-    const uint32_t parts = (uint32_t)((h->hist_cells + (1ull << cshift) - 1) >> cshift);
-    // sized for about every sample of the launch spread evenly over the
-    // parts; a full sub-log only sends its overflow to the global atomics
-    const uint64_t cap = std::min<uint64_t>(1u << 20, (nbytes / kRecBytes) / ((uint64_t)grid * parts) + 64);
-    const size_t need = (size_t)grid * parts * cap * rec;
-    if (need > h->plog_bytes || (size_t)grid * parts > h->plog_cnt_cap) {
-      HIP_TRY(h, hipStreamSynchronize(h->stream));  // an earlier launch may still read the old log
-      if (need > h->plog_bytes) {
-        (void)hipFree(h->d_plog);
-        h->d_plog = nullptr;
-        h->plog_bytes = 0;
-        HIP_TRY(h, hipMalloc(&h->d_plog, need));
-        h->plog_bytes = need;
-      }
-      if ((size_t)grid * parts > h->plog_cnt_cap) {
-        (void)hipFree(h->d_plog_cnt);
-        h->d_plog_cnt = nullptr;
-        h->plog_cnt_cap = 0;
-        HIP_TRY(h, hipMalloc(&h->d_plog_cnt, (size_t)grid * parts * 4));
-        h->plog_cnt_cap = (size_t)grid * parts;
-      }
-    }
-    p.plog = h->d_plog;
-    p.plog_cshift = cshift;
-    p.plog_cnt = h->d_plog_cnt;
-    p.plog_cap = (uint32_t)cap;
-    p.plog_parts = parts;
-  }
   const int slot = (int)(h->nlaunch % nmg_engine::kRing);
   if (!h->ring0[slot]) {
     HIP_TRY(h, hipEventCreate(&h->ring0[slot]));
@@ -1413,19 +1365,6 @@ static int launch_attribution(nmg_engine* h, const uint8_t* data, const BufDesc*
     } else if (p.pk64) {
       const uint32_t blocks = (uint32_t)std::min<uint64_t>(2048, (2ull * h->E + 255) / 256);
       HIP_TRY(h, launch_unpack(blocks, h->stream, h->d_sum64, p.pk64, h->E, p.pk_shift));
-    }
-    if (p.plog) {  // sums the page-cell log per cell range into the histogram
-      PlogParams r;
-      r.plog = p.plog;
-      r.plog_cnt = p.plog_cnt;
-      r.hist = h->d_hist;
-      r.hist_cells = h->hist_cells;
-      r.grid = grid;
-      r.parts = p.plog_parts;
-      r.cap = p.plog_cap;
-      r.cshift = p.plog_cshift;
-      r.nb_threads = h->T;
-      HIP_TRY(h, launch_plog_reduce(p.plog_parts, h->stream, r));
     }
   }
   if (!nb) HIP_TRY(h, hipEventRecord(h->ringm[slot], h->stream));

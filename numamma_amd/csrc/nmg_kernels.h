@@ -42,13 +42,6 @@ constexpr uint32_t kLogParts = 256;
 constexpr uint32_t kTlogHead = 0xFFFFFFFFu, kTlogCont = 0xFFFFFFFEu;
 constexpr uint32_t kLogChunk = 4096;   // entries per LDS pass of tlog_reduce_kernel
 constexpr uint32_t kLogMaxGrid = 1024;  // attribution workgroups a log can serve
-// page-cell log (large tables, hashed page cells): cells that miss the LDS
-// page table, and the table's flushes, append 8 B records {count, thread,
-// cell - part base} to one of the workgroup's sub-logs by cell range (part
-// = cell >> plog_cshift); plog_reduce_kernel sums each part's cells of every
-// thread in LDS and adds them to the histogram with plain read-modify-writes
-constexpr uint32_t kPlogMaxParts = 2048;  // cursors in the lookup LDS region's spare 12 KiB
-constexpr uint32_t kPlogWin = 16384;      // cells one plog_reduce pass holds in LDS (64 KiB)
 constexpr uint32_t kPageBuckets = 896;         // dense page cell -> count: 8-slot buckets
 constexpr uint32_t kPageSlots = kPageBuckets * 8;  // 7168 cells (56 KiB)
 constexpr uint32_t kObjBuckets = kObjSlots / 8;
@@ -166,19 +159,6 @@ struct Params {
   uint4* tlog;               // [grid][tlog_parts][tlog_cap] 16 B slots (kTlogHead layouts); null: off
   uint32_t* tlog_cnt;        // [grid][tlog_parts] records written
   uint32_t tlog_cap, tlog_rshift, tlog_parts;
-  // page-cell log (see kPlogMaxParts): [grid][plog_parts][plog_cap] records
-  unsigned long long* plog;  // null: off (cells that miss go to global atomics)
-  uint32_t* plog_cnt;        // [grid][plog_parts] records written
-  uint32_t plog_cap, plog_cshift, plog_parts;
-};
-
-// plog_reduce_kernel
-struct PlogParams {
-  const unsigned long long* plog;
-  const uint32_t* plog_cnt;
-  uint32_t* hist;
-  uint64_t hist_cells;
-  uint32_t grid, parts, cap, cshift, nb_threads;
 };
 
 // tlog_reduce_kernel (long-tail log, see Params::tlog)
@@ -217,7 +197,6 @@ hipError_t launch_tlog_reduce(uint32_t grid, hipStream_t s, const TlogParams& r)
 hipError_t launch_unpack(uint32_t grid, hipStream_t s, uint64_t* sum64, unsigned long long* pk64,
                          uint32_t nb_entries, uint32_t shift);
 hipError_t launch_reset(uint32_t grid, hipStream_t s, const ResetParams& r);
-hipError_t launch_plog_reduce(uint32_t parts, hipStream_t s, const PlogParams& r);
 hipError_t launch_merge(hipStream_t s, void* dst, const void* src, uint64_t n, int op);
 
 }  // namespace nmg

@@ -177,20 +177,7 @@ struct Lookup {
   const uint4* nodes;      // LDS (small tables): 2 x uint4 per node: (addr, end), (alloc, free)
   const uint2* ninfo;      // LDS (small tables): (dense histogram base or ~0, entry id | older-entries << 31)
   const uint8_t* shift;    // LDS (large tables): per-bucket directory shift
-  uint32_t* pcur;          // LDS (large tables): page-cell sub-log cursors
 };
-
-// One page-cell contribution to this workgroup's sub-log of the cell's
-// range; false when the sub-log is full (the caller then adds to global).
-__device__ __forceinline__ bool plog_append(const Params& p, uint32_t* pcur, uint32_t cell, uint32_t th, uint32_t cnt) {
-  const uint32_t part = cell >> p.plog_cshift;
-  const uint32_t k = atomicAdd(&pcur[part], 1u);
-  if (k >= p.plog_cap) return false;
-  p.plog[(uint64_t(blockIdx.x) * p.plog_parts + part) * p.plog_cap + k] =
-      (unsigned long long)(cell - (part << p.plog_cshift)) | ((unsigned long long)th << 22) |
-      ((unsigned long long)cnt << 32);
-  return true;
-}
 
 // __ma_find_mem_info_from_sample_generic (mem_analyzer.c:249-286): the
 // lower-bound node only (ht_lower_key, tools/hash.c:63-77), newest entry
@@ -221,17 +208,45 @@ __device__ __forceinline__ Match find_entry(const Params& p, const Lookup& L, ui
     }
     return m;
   }
-  const uint32_t k = lower_key(p, L.fences, L.shift, addr, sp);
-  if (k >= p.nb_keys) return m;
-  const uint4* q = reinterpret_cast<const uint4*>(p.nodes + k);
-  const uint4 a = q[0], b = q[1], c = q[2];
+  return m;
+}
+
+// Large tables, in two halves so that independent work can run while the node
+// record is in flight: node_issue (lower bound + the node record's loads),
+// node_match (the newest entry, then the older ones).
+struct NodePre {
+  uint32_t k;  // lower-bound key index (nb_keys: none)
+  uint4 a, b, c;
+};
+
+__device__ __forceinline__ NodePre node_issue(const Params& p, const Lookup& L, bool valid, uint64_t addr,
+                                              const SpecDir& sp) {
+  NodePre n;
+  n.k = valid ? lower_key(p, L.fences, L.shift, addr, sp) : p.nb_keys;
+  n.a = n.b = n.c = make_uint4(0, 0, 0, 0);
+  if (n.k < p.nb_keys) {
+    const uint4* q = reinterpret_cast<const uint4*>(p.nodes + n.k);
+    n.a = q[0];
+    n.b = q[1];
+    n.c = q[2];
+  }
+  return n;
+}
+
+__device__ __forceinline__ Match node_match(const Params& p, const NodePre& n, uint64_t addr, uint64_t ts) {
+  Match m;
+  m.e = -1;
+  m.baddr = 0;
+  m.hist = kHistSparse;
+  if (n.k >= p.nb_keys) return m;
+  const uint4 a = n.a, b = n.b, c = n.c;
   if (entry_match(a, b, addr, ts)) {
     m.e = c.w;
     m.baddr = (uint64_t(a.y) << 32) | a.x;
     m.hist = (uint64_t(c.y) << 32) | c.x;
     return m;
   }
-  const uint4 d = q[3];
+  const uint4 d = reinterpret_cast<const uint4*>(p.nodes + n.k)[3];
   if (d.x > 1) match_older(p, d.y, d.x, addr, ts, m);  // (count, first)
   return m;
 }
@@ -273,6 +288,10 @@ __device__ __forceinline__ void process_sample(Params& p, WgCounters& wc, LaneAc
   vmask = __ballot(valid);
   fmask = 0;
   if (vmask == 0) return;
+  // large tables: the node record's loads go out first; the global counters
+  // below do not depend on them and run while they are in flight
+  NodePre np;
+  if ((MODE & kModeLarge) && (p.flags & NMG_F_MATCH_SAMPLES)) np = node_issue(p, L, valid, addr, sp);
   if (valid && !(p.flags & kDbgNoGlobal)) {
     const uint32_t bm = bucket_mask(lvl);
     if (w < kLaneMaxWeight) {  // register accumulation (no LDS traffic)
@@ -317,7 +336,11 @@ __device__ __forceinline__ void process_sample(Params& p, WgCounters& wc, LaneAc
   // ---- __match_sample (mem_sampling.c:594-673)
   Match m;
   m.e = -1;
-  if (valid) m = find_entry<MODE>(p, L, addr, ts, sp);
+  if (MODE & kModeLarge) {
+    if (valid) m = node_match(p, np, addr, ts);
+  } else if (valid) {
+    m = find_entry<MODE>(p, L, addr, ts, sp);
+  }
   const int64_t e = m.e;
   fmask = __ballot(e >= 0);
   sub_stamp<TIMING>(st, 1);
@@ -366,7 +389,7 @@ __device__ __forceinline__ void process_sample(Params& p, WgCounters& wc, LaneAc
       } else {
         const int ps = page_slot(wc, cell);
         if (ps >= 0) atomicAdd(&wc.pcnt[ps], 1u);
-        else if (!((MODE & kModeLarge) && p.plog && plog_append(p, L.pcur, cell, th, 1u)))
+        else
           atomicAdd(p.hist + uint64_t(th) * p.hist_cells + cell, 1u);
       }
     } else {
@@ -426,7 +449,7 @@ __device__ __forceinline__ void flush_objects(Params& p, WgCounters& wc, int tid
 }
 
 template <int MODE>
-__device__ __forceinline__ void flush_pages(Params& p, WgCounters& wc, uint32_t* pcur, int tid, uint32_t th) {
+__device__ __forceinline__ void flush_pages(Params& p, WgCounters& wc, int tid, uint32_t th) {
   const bool write = !(p.flags & kDbgNoFlush);
   unsigned int* hrow = p.hist + uint64_t(th) * p.hist_cells;
   if (MODE & kModeDensePage) {  // cells in order: consecutive lanes add to consecutive words
@@ -446,8 +469,7 @@ __device__ __forceinline__ void flush_pages(Params& p, WgCounters& wc, uint32_t*
   for (int i = tid; i < (int)kPageSlots; i += kWG) {
     const uint32_t cell = pkey[i];
     if (cell == kEmpty32) continue;
-    if (write && !((MODE & kModeLarge) && p.plog && plog_append(p, pcur, cell, th, wc.pcnt[i])))
-      atomicAdd(hrow + cell, wc.pcnt[i]);
+    if (write) atomicAdd(hrow + cell, wc.pcnt[i]);
     pkey[i] = kEmpty32;
     wc.pcnt[i] = 0;
   }
@@ -548,9 +570,6 @@ __global__ __launch_bounds__(kWG, 1) void attribute_kernel(Params p) {
   uint4* const s_nodes = s_tab + (kLdsNodes + 1) / 2;                    // after 8 KiB of keys
   uint2* const s_ninfo = reinterpret_cast<uint2*>(s_tab + (kLdsNodes + 1) * 5 / 2);  // after 40 KiB
   uint8_t* const s_shift = reinterpret_cast<uint8_t*>(s_tab + (kMaxFences + 1) / 2);  // after 32 KiB
-  // page-cell sub-log cursors after the shifts (large tables only)
-  uint32_t* const s_pcur = reinterpret_cast<uint32_t*>(s_tab + (kMaxFences + 1) / 2 + (kMaxFences + 1) / 16);
-  static_assert(((kMaxFences + 1) / 2 + (kMaxFences + 1) / 16) * 16 + kPlogMaxParts * 4 <= kTabBytes, "plog cursors");
   if (!(MODE & kModeLarge)) {
     const uint32_t n = 1u << p.elevels;
     for (uint32_t i = tid; i < n; i += kWG) s_fences[i] = p.efences[i];
@@ -569,11 +588,9 @@ __global__ __launch_bounds__(kWG, 1) void attribute_kernel(Params p) {
   constexpr bool kLog = !(MODE & kModeDenseObj);  // the long-tail log serves the hashed object mode
   if (kLog && p.tlog)
     for (uint32_t i = tid; i < kLogParts; i += kWG) wc.tcur[i] = 0;
-  if (p.plog)
-    for (uint32_t i = tid; i < p.plog_parts; i += kWG) s_pcur[i] = 0;
   if (tid < 3) s_flags[tid] = 0;
   __syncthreads();
-  const Lookup L{s_fences, s_nodes, s_ninfo, s_shift, s_pcur};
+  const Lookup L{s_fences, s_nodes, s_ninfo, s_shift};
 
   // A window is (idx, cur): up to kWG stride slots from byte `cur` of buffer
   // idx; when that buffer ends inside the window and the next buffer belongs
@@ -583,8 +600,6 @@ __global__ __launch_bounds__(kWG, 1) void attribute_kernel(Params p) {
   if (r0 >= r1) {
     if (kLog && p.tlog)
       for (uint32_t i = tid; i < p.tlog_parts; i += kWG) p.tlog_cnt[uint64_t(blockIdx.x) * p.tlog_parts + i] = 0;
-    if (p.plog)
-      for (uint32_t i = tid; i < p.plog_parts; i += kWG) p.plog_cnt[uint64_t(blockIdx.x) * p.plog_parts + i] = 0;
     return;
   }
   uint32_t idx = r0;
@@ -825,7 +840,7 @@ __global__ __launch_bounds__(kWG, 1) void attribute_kernel(Params p) {
       __syncthreads();  // every insert and drain of this window is done
       if (stream_end) flush_sums(p, wc, tid, cur_access);
       flush_objects<MODE>(p, wc, tid, cur_access);
-      flush_pages<MODE>(p, wc, s_pcur, tid, cur_thread);
+      flush_pages<MODE>(p, wc, tid, cur_thread);
       last_flush = win;
       __syncthreads();
       if (stream_end) {
@@ -846,14 +861,11 @@ __global__ __launch_bounds__(kWG, 1) void attribute_kernel(Params p) {
     }
     if (idx >= r1) break;  // the loop's only exit, after the state update
   }
-  if ((kLog && p.tlog) || p.plog) {  // the sub-logs' fill (every append of this workgroup is done)
+  if (kLog && p.tlog) {  // the sub-logs' fill (every append of this workgroup is done)
     __syncthreads();
     if (kLog && p.tlog)
       for (uint32_t i = tid; i < p.tlog_parts; i += kWG)
         p.tlog_cnt[uint64_t(blockIdx.x) * p.tlog_parts + i] = min(wc.tcur[i], p.tlog_cap);
-    if (p.plog)
-      for (uint32_t i = tid; i < p.plog_parts; i += kWG)
-        p.plog_cnt[uint64_t(blockIdx.x) * p.plog_parts + i] = min(s_pcur[i], p.plog_cap);
   }
   if (TIMING && lane == 0) {
     unsigned long long* o = p.dbg + (uint64_t(blockIdx.x) * (kWG / 64) + tid / 64) * kTimingWords;
@@ -987,80 +999,6 @@ __global__ __launch_bounds__(1024, 1) void tlog_reduce_kernel(TlogParams r) {
   }
 }
 
-// Sums the page-cell log of one attribution launch: workgroup `part` owns
-// the cells [part << cshift, (part + 1) << cshift) of every thread's row.  It
-// reads that part's sub-log of every attribution workgroup, adds the counts
-// in LDS ([thread][cell], a window of threads per pass when T << cshift
-// exceeds kPlogWin), then adds the window to the histogram with plain
-// read-modify-writes: no other writer of those cells runs meanwhile, and a
-// row's cells are contiguous, so the update is coalesced.
-__global__ __launch_bounds__(1024, 1) void plog_reduce_kernel(PlogParams r) {
-  __shared__ uint32_t s_cnt[kPlogWin];
-  __shared__ uint32_t s_pre[kLogMaxGrid + 1];
-  const uint32_t part = blockIdx.x, tid = threadIdx.x;
-  for (uint32_t w = tid; w < r.grid; w += 1024) s_pre[w + 1] = r.plog_cnt[uint64_t(w) * r.parts + part];
-  __syncthreads();
-  if (tid < 64) {  // prefix over the source workgroups (as in tlog_reduce_kernel)
-    const uint32_t per = (r.grid + 63) / 64, b = min(tid * per, r.grid), e = min(b + per, r.grid);
-    uint32_t sum = 0;
-    for (uint32_t w = b; w < e; w++) sum += s_pre[w + 1];
-    uint32_t incl = sum;
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t t = __shfl_up(incl, o, 64);
-      if ((int)tid >= o) incl += t;
-    }
-    uint32_t run = incl - sum;
-    for (uint32_t w = b; w < e; w++) {
-      run += s_pre[w + 1];
-      s_pre[w + 1] = run;
-    }
-    if (tid == 0) s_pre[0] = 0;
-  }
-  __syncthreads();
-  const uint32_t total = s_pre[r.grid];
-  if (total == 0) return;
-  const uint32_t width = 1u << r.cshift;
-  const uint64_t c0 = uint64_t(part) << r.cshift;
-  const uint32_t ncell = (uint32_t)min((uint64_t)width, r.hist_cells - c0);
-  const uint32_t tw = max(1u, kPlogWin >> r.cshift);  // threads per pass
-  for (uint32_t t0 = 0; t0 < r.nb_threads; t0 += tw) {
-    const uint32_t t1 = min(t0 + tw, r.nb_threads);
-    for (uint32_t j = tid; j < (t1 - t0) << r.cshift; j += 1024) s_cnt[j] = 0;
-    __syncthreads();
-    constexpr int kU = 8;  // records per thread in flight
-    for (uint32_t i0 = tid; i0 < total; i0 += kU * 1024) {
-      unsigned long long v[kU];
-#pragma unroll
-      for (int u = 0; u < kU; u++) {
-        const uint32_t i = i0 + u * 1024;
-        v[u] = 0;
-        if (i >= total) continue;
-        uint32_t lo = 0, hi = r.grid;  // source workgroup: s_pre[lo] <= i < s_pre[lo + 1]
-        while (hi - lo > 1) {
-          const uint32_t mid = (lo + hi) >> 1;
-          if (s_pre[mid] <= i) lo = mid;
-          else hi = mid;
-        }
-        v[u] = r.plog[(uint64_t(lo) * r.parts + part) * r.cap + (i - s_pre[lo])];
-      }
-#pragma unroll
-      for (int u = 0; u < kU; u++) {
-        const uint32_t th = uint32_t(v[u] >> 22) & 0x3ffu, cnt = uint32_t(v[u] >> 32);
-        if (cnt == 0 || th < t0 || th >= t1) continue;
-        atomicAdd(&s_cnt[((th - t0) << r.cshift) + (uint32_t(v[u]) & 0x3fffffu)], cnt);
-      }
-    }
-    __syncthreads();
-    for (uint32_t th = t0; th < t1; th++) {
-      uint32_t* row = r.hist + uint64_t(th) * r.hist_cells + c0;
-      const uint32_t* src = s_cnt + ((th - t0) << r.cshift);
-      for (uint32_t j = tid; j < ncell; j += 1024)
-        if (src[j]) row[j] += src[j];
-    }
-    __syncthreads();
-  }
-}
-
 // Adds the launch's packed long-tail object counters into sum64 and clears
 // them (same stream, after attribute_kernel).
 __global__ __launch_bounds__(256) void unpack_kernel(uint64_t* sum64, unsigned long long* pk64, uint32_t nb_entries,
@@ -1142,11 +1080,6 @@ hipError_t launch_tlog_reduce(uint32_t grid, hipStream_t s, const TlogParams& r)
 hipError_t launch_unpack(uint32_t grid, hipStream_t s, uint64_t* sum64, unsigned long long* pk64, uint32_t nb_entries,
                          uint32_t shift) {
   hipLaunchKernelGGL(unpack_kernel, dim3(grid), dim3(256), 0, s, sum64, pk64, nb_entries, shift);
-  return hipGetLastError();
-}
-
-hipError_t launch_plog_reduce(uint32_t parts, hipStream_t s, const PlogParams& r) {
-  hipLaunchKernelGGL(plog_reduce_kernel, dim3(parts), dim3(1024), 0, s, r);
   return hipGetLastError();
 }
 

@@ -23,6 +23,7 @@ from numamma_amd.replay import SynthConfig, generate
 W = {"c2": dict(nb_samples=10_000_000, nb_intervals=1_000),
      "k100k": dict(nb_samples=10_000_000, nb_intervals=100_000),
      "k1m": dict(nb_samples=10_000_000, nb_intervals=1_000_000, size_max=64 * 1024),
+     "c3": dict(nb_samples=100_000_000, nb_intervals=100_000),
      "c4": dict(nb_samples=125_000_000, nb_intervals=1_000_000, size_max=64 * 1024)}
 for w in sys.argv[3].split(","):
     rp = generate(SynthConfig(seed=1, **W[w]))
