@@ -9,6 +9,8 @@
 #include <rocprofiler-sdk-roctx/roctx.h>
 
 #include <algorithm>
+#include <chrono>
+#include <cinttypes>
 #include <functional>
 #include <cstdio>
 #include <cstdlib>
@@ -2041,15 +2043,22 @@ extern "C" int nmg_report(nmg_engine* h, const nmg_object_meta* meta, const nmg_
   Range range("nmg_report");
   if (!h || (h->E && !meta)) return NMG_ERR_INVALID;
   if (!h->have_table) return fail(h, NMG_ERR_STATE, "nmg_report before nmg_set_objects");
+  const bool timing = getenv("NMG_REPORT_TIMING") != nullptr;  // phase times on stderr
+  auto t0 = std::chrono::steady_clock::now();
   HostResults r;
   int rc = engine_download(h, r);
   if (rc) return rc;
+  auto t1 = std::chrono::steady_clock::now();
   std::vector<uint32_t> rows;
   int64_t ncells = 0;
   if ((h->flags & NMG_F_PAGE_HIST) && (!opts || opts->dump_single_items)) {
     rc = collect_page_cells(h, &rows, &ncells);
     if (rc) return rc;
   }
+  if (timing)
+    fprintf(stderr, "nmg_report: counters D2H %.3f s, page cells D2H + rows %.3f s (%" PRId64 " cells)\n",
+            std::chrono::duration<double>(t1 - t0).count(),
+            std::chrono::duration<double>(std::chrono::steady_clock::now() - t1).count(), ncells);
   nmg_host_results res;
   memset(&res, 0, sizeof(res));
   res.global[0] = r.global[0];

@@ -18,6 +18,11 @@
 #include <sys/stat.h>
 
 #include <algorithm>
+#include <atomic>
+#include <mutex>
+#include <thread>
+#include <chrono>
+#include <cstdlib>
 #include <cinttypes>
 #include <cstdio>
 #include <cstring>
@@ -48,18 +53,19 @@ struct Site {
   std::vector<uint32_t> objects;   // entries attached at finalize
 };
 
+// (the tail points into the caller's callstack pool, alive for the report)
 struct CsKey {
   uint64_t size;
   int32_t cs_size;
-  std::vector<uint64_t> tail;  // callstack[3..cs_size)
-  bool operator==(const CsKey& o) const { return size == o.size && cs_size == o.cs_size && tail == o.tail; }
+  uint32_t n;            // tail length
+  const uint64_t* tail;  // callstack[3..cs_size)
+  uint64_t hash;
+  bool operator==(const CsKey& o) const {
+    return size == o.size && cs_size == o.cs_size && n == o.n && (n == 0 || !memcmp(tail, o.tail, 8ull * n));
+  }
 };
 struct CsKeyHash {
-  size_t operator()(const CsKey& k) const {
-    uint64_t h = k.size * 0x9E3779B97F4A7C15ull ^ (uint64_t)(uint32_t)k.cs_size;
-    for (uint64_t v : k.tail) h = (h ^ v) * 0x100000001B3ull;
-    return (size_t)h;
-  }
+  size_t operator()(const CsKey& k) const { return (size_t)k.hash; }
 };
 struct RipKey {
   uint64_t size, rip;
@@ -111,8 +117,14 @@ class Registry {
 
  private:
   static CsKey cs_key_of(uint64_t size, const uint64_t* cs, int32_t cs_size) {
-    CsKey k{size, cs_size, {}};
-    if (cs && cs_size > 3) k.tail.assign(cs + 3, cs + cs_size);
+    CsKey k{size, cs_size, 0, nullptr, 0};
+    if (cs && cs_size > 3) {
+      k.tail = cs + 3;
+      k.n = (uint32_t)(cs_size - 3);
+    }
+    uint64_t h = size * 0x9E3779B97F4A7C15ull ^ (uint64_t)(uint32_t)cs_size;
+    for (uint32_t i = 0; i < k.n; i++) h = (h ^ k.tail[i]) * 0x100000001B3ull;
+    k.hash = h;
     return k;
   }
  public:
@@ -409,6 +421,15 @@ int write_object_summary(const std::string& path, const nmg_host_results* r, con
 
 int write_report(const nmg_host_results* r, const nmg_object_meta* meta, const nmg_report_options* opts,
                  const char* stdout_path, std::string& err, const DumpInput* dump) {
+  // NMG_REPORT_TIMING=1: phase times on stderr
+  const bool timing = getenv("NMG_REPORT_TIMING") != nullptr;
+  auto t_last = std::chrono::steady_clock::now();
+  auto phase = [&](const char* name) {
+    if (!timing) return;
+    const auto t = std::chrono::steady_clock::now();
+    fprintf(stderr, "nmg_report: %s %.3f s\n", name, std::chrono::duration<double>(t - t_last).count());
+    t_last = t;
+  };
   const uint32_t E = r->nb_entries;
   const uint32_t T = r->nb_threads;
   FILE* out = stdout;
@@ -452,6 +473,7 @@ int write_report(const nmg_host_results* r, const nmg_object_meta* meta, const n
   fprintf(out, "---------------------------------\n");
 
   // ---- call sites
+  phase("buffers");
   Registry reg(meta);
   std::vector<uint32_t> matched;
   if (r->match_samples) {
@@ -473,8 +495,10 @@ int write_report(const nmg_host_results* r, const nmg_object_meta* meta, const n
     std::vector<uint32_t> order(matched);
     std::sort(order.begin(), order.end(),
               [&](uint32_t a, uint32_t b) { return r->first_ordinal[a] < r->first_ordinal[b]; });
+    phase("registry: order");
     for (uint32_t e : order)
       if (reg.find(e) < 0) reg.create(e, r->buffer_size[e] / kPageSize + 1);
+    phase("registry: create");
     // update_call_sites in FOREACH_HASH order (= flattened order); online, an
     // object never matched finds or creates its site here
     for (uint32_t e : updated) {
@@ -491,6 +515,7 @@ int write_report(const nmg_host_results* r, const nmg_object_meta* meta, const n
     }
   }
   std::vector<Site>& sites = reg.sites;
+  phase("call-site registry");
 
   // ---- dump modes (mem_sampling.c:895-914): per SAMPLE record in analysis order
   const char* dir = opts && opts->output_dir ? opts->output_dir : ".";
@@ -577,11 +602,13 @@ int write_report(const nmg_host_results* r, const nmg_object_meta* meta, const n
   }
 
   // ---- ma_finalize prints (mem_analyzer.c:1877-1881)
+  phase("dumps");
   print_counters(out, r->global);
   fprintf(out, "Summary of the call sites:\n");
   fprintf(out, "--------------------------\n");
   fprintf(out, "Sorting call sites\n");
   std::vector<int64_t> order = sort_sites(sites);
+  phase("sort");
   // __remove_site during the sort (mem_analyzer.c:1506-1528): the site the
   // walk stops at -- the removed one when it heads the list, else its
   // predecessor (quirk Q10) -- gets callsite_summary_<id>.dat and its dump
@@ -644,8 +671,7 @@ int write_report(const nmg_host_results* r, const nmg_object_meta* meta, const n
   };
 
   int rc = NMG_OK;
-  std::string line;
-  char cell[16];
+  std::vector<int64_t> jobs;  // sites whose page file is written (in report order)
   for (int64_t idx : order) {
     const Site& s = sites[idx];
     if (!(s.read_count || s.write_count)) continue;
@@ -657,38 +683,63 @@ int write_report(const nmg_host_results* r, const nmg_object_meta* meta, const n
               ", avg weight: %f). %" PRIu64 " wr_access\n",
               (int)s.id, s.caller.c_str(), (size_t)s.buffer_size, (int)s.nb_mallocs, (size_t)s.read_count,
               s.read_weight, avg, s.write_count);
-    if (dump_single && s.mem_type != kMemTypeStack) {
-      // __plot_counters: (buffer_size / 4096 + 1) rows x next_thread_rank columns
-      index_cells();
-      SiteHist sh;
-      uint64_t rows = s.mem_info_buffer_size / kPageSize + 1;
-      sh.init(rows, T);
-      for (uint32_t e : s.objects)
-        for (int64_t i = cell_begin[e]; i < cell_begin[e + 1]; i++) {
-          const uint32_t* c = r->cells + 4 * i;
-          sh.add(c[2], c[1], c[3]);
+    if (dump_single && s.mem_type != kMemTypeStack) jobs.push_back(idx);
+  }
+  if (!jobs.empty()) {
+    // __plot_counters (mem_analyzer.c:1557-1585): one callsite_counters_<id>.dat
+    // per site, (buffer_size / 4096 + 1) rows x next_thread_rank columns.  The
+    // files are independent: written by a pool of host threads
+    // (NMG_REPORT_THREADS, default min(16, cores)).
+    index_cells();
+    unsigned nth = std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
+    if (const char* e = getenv("NMG_REPORT_THREADS")) nth = (unsigned)std::max(1, atoi(e));
+    nth = (unsigned)std::min<size_t>(nth, jobs.size());
+    std::atomic<size_t> next{0};
+    std::mutex mu;
+    auto work = [&]() {
+      std::string line;
+      char cell[16];
+      for (size_t j; (j = next.fetch_add(1)) < jobs.size();) {
+        const Site& s = sites[jobs[j]];
+        SiteHist sh;
+        const uint64_t rows = s.mem_info_buffer_size / kPageSize + 1;
+        sh.init(rows, T);
+        for (uint32_t e : s.objects)
+          for (int64_t i = cell_begin[e]; i < cell_begin[e + 1]; i++) {
+            const uint32_t* c = r->cells + 4 * i;
+            sh.add(c[2], c[1], c[3]);
+          }
+        char fn[4096];
+        snprintf(fn, sizeof(fn), "%s/callsite_counters_%d.dat", dir, (int)s.id);
+        FILE* df = fopen(fn, "w");
+        if (!df) {
+          std::lock_guard<std::mutex> g(mu);
+          if (rc == NMG_OK) {
+            rc = NMG_ERR_IO;
+            err = std::string("cannot open ") + fn;
+          }
+          next = jobs.size();  // stop the pool
+          break;
         }
-      char fn[4096];
-      snprintf(fn, sizeof(fn), "%s/callsite_counters_%d.dat", dir, (int)s.id);
-      FILE* df = fopen(fn, "w");
-      if (!df) {
-        rc = NMG_ERR_IO;
-        err = std::string("cannot open ") + fn;
-        break;
-      }
-      for (uint64_t i = 0; i < rows; i++) {
-        line.clear();
-        for (uint32_t th = 0; th < T; th++) {
-          int n = snprintf(cell, sizeof(cell), "\t%d", (int)sh.get(i, th));
-          line.append(cell, n);
+        for (uint64_t i = 0; i < rows; i++) {
+          line.clear();
+          for (uint32_t th = 0; th < T; th++) {
+            int n = snprintf(cell, sizeof(cell), "\t%d", (int)sh.get(i, th));
+            line.append(cell, n);
+          }
+          line.push_back('\n');
+          fwrite(line.data(), 1, line.size(), df);
         }
-        line.push_back('\n');
-        fwrite(line.data(), 1, line.size(), df);
+        fclose(df);
       }
-      fclose(df);
-    }
+    };
+    std::vector<std::thread> pool;
+    for (unsigned t = 1; t < nth; t++) pool.emplace_back(work);
+    work();
+    for (std::thread& t : pool) t.join();
   }
   fclose(cf);
+  phase("call_sites.log + page files");
   if (!rc && (dflags & NMG_DUMP_ALL)) {
     if (r->objects)
       rc = write_object_summary(std::string(dir) + "/all_memory_objects.dat", r, meta, opts, err);

@@ -275,27 +275,31 @@ def write_replay_c(path: str, replay: Replay) -> None:
 
 
 def build_meta(table: ObjectTable):
-    """nmg_object_meta[] for the call-site registry (+ objects to keep alive)."""
+    """nmg_object_meta[] for the call-site registry (+ objects to keep alive),
+    filled with numpy in the struct's layout (include/numamma_gpu.h)."""
     E = table.nb_entries
-    meta = (_lib.nmg_object_meta * E)()
+    dt = np.dtype([("initial_buffer_size", "<u8"), ("caller_rip", "<u8"), ("callstack", "<u8"),
+                   ("callstack_size", "<i4"), ("mem_type", "<u4"), ("caller", "<u8"), ("id", "<u4"),
+                   ("reserved", "<u4")])
+    assert dt.itemsize == C.sizeof(_lib.nmg_object_meta)
+    arr = np.zeros(max(E, 1), dtype=dt)
     ent = table.entries
     pool = np.ascontiguousarray(table.callstack_pool, dtype=np.uint64)
-    pool_ptr = pool.ctypes.data
     strings = C.create_string_buffer(table.string_pool + b"\0", len(table.string_pool) + 1)
-    sbase = C.addressof(strings)
-    for e in range(E):
-        m = meta[e]
-        r = ent[e]
-        m.initial_buffer_size = int(r["initial_buffer_size"])
-        m.caller_rip = int(r["caller_rip"])
-        m.callstack_size = int(r["callstack_size"])
-        m.mem_type = int(r["mem_type"])
-        m.id = int(r["id"])
-        if r["has_callstack"]:
-            m.callstack = C.cast(C.c_void_p(pool_ptr + 8 * int(r["callstack_off"])), C.POINTER(C.c_uint64))
-        if int(r["caller_off"]) != 0xFFFFFFFF:
-            m.caller = C.cast(C.c_void_p(sbase + int(r["caller_off"])), C.c_char_p)
-    return meta, (pool, strings)
+    if E:
+        arr["initial_buffer_size"][:E] = ent["initial_buffer_size"]
+        arr["caller_rip"][:E] = ent["caller_rip"]
+        arr["callstack_size"][:E] = ent["callstack_size"]
+        arr["mem_type"][:E] = ent["mem_type"]
+        arr["id"][:E] = ent["id"]
+        has_cs = ent["has_callstack"] != 0
+        arr["callstack"][:E] = np.where(has_cs, np.uint64(pool.ctypes.data) + np.uint64(8) *
+                                        ent["callstack_off"].astype(np.uint64), np.uint64(0))
+        has_caller = ent["caller_off"].astype(np.uint64) != 0xFFFFFFFF
+        arr["caller"][:E] = np.where(has_caller, np.uint64(C.addressof(strings)) +
+                                     ent["caller_off"].astype(np.uint64), np.uint64(0))
+    meta = (_lib.nmg_object_meta * E).from_buffer(arr)
+    return meta, (pool, strings, arr)
 
 
 def run_replay(path: str, output_dir: str, stdout_path: Optional[str] = None, raw_path: Optional[str] = None,

@@ -28,6 +28,7 @@ WORKLOADS = {
     "k100k": dict(nb_samples=10_000_000, nb_intervals=100_000),
     "k1m": dict(nb_samples=10_000_000, nb_intervals=1_000_000, size_max=64 * 1024),
     "c4": dict(nb_samples=125_000_000, nb_intervals=1_000_000, size_max=64 * 1024),
+    "c3": dict(nb_samples=100_000_000, nb_intervals=100_000),
     # same table, samples concentrated on few objects (no gap samples): the
     # lookup's cost when every table line it touches is cache-hot
     "c4hot": dict(nb_samples=125_000_000, nb_intervals=1_000_000, size_max=64 * 1024, zipf_s=2.0, frac_gap=0.0),

@@ -14,12 +14,13 @@ everything nmg_report reads).  Modes (one JSON line each):
               batches: each chunk's H2D (copy stream) and kernel (engine
               stream) overlap the copies of the next chunk (configs[4])
 
-    python tools/e2e.py [c2] [--threads 16] [--chunk-mb 64] [--batch 256]
+    python tools/e2e.py [c2|c4shard] [--threads 16] [--chunk-mb 64] [--batch 256]
 """
 import argparse
 import json
 import os
 import sys
+import tempfile
 import time
 
 import numpy as np
@@ -36,12 +37,16 @@ def main():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--reps", type=int, default=4)
     ap.add_argument("--modes", default="per_buffer,batch,stream")
+    ap.add_argument("--report", action="store_true", help="time nmg_report (counters D2H + report files) "
+                    "instead of the raw result getters")
     a = ap.parse_args()
 
     from numamma_amd.engine import Engine
-    from numamma_amd.replay import CONFIGS, generate
+    from numamma_amd.replay import CONFIGS, SynthConfig, generate
 
-    rp = generate(CONFIGS[a.workload])
+    # c4shard: configs[3]'s per-GPU shard (bench.py's default workload)
+    cfgs = dict(CONFIGS, c4shard=SynthConfig(nb_samples=125_000_000, nb_intervals=1_000_000, size_max=64 * 1024))
+    rp = generate(cfgs[a.workload])
     lins = rp.linear_buffers()
     nbytes = sum(x[2].shape[0] for x in lins)
     nsamples = nbytes // 40
@@ -74,7 +79,11 @@ def main():
             eng.analyze()
             eng.synchronize()
             t2 = time.perf_counter()
-            results()
+            if a.report:  # the product's output stage: D2H of the counters + report files
+                with tempfile.TemporaryDirectory() as d:
+                    eng.report(os.path.join(d, "out"), os.path.join(d, "stdout.txt"))
+            else:
+                results()
             t3 = time.perf_counter()
             kern = float(np.sum(eng.launch_times(64 if mode == "stream" else 1))) / 1e3
             if r:
@@ -85,7 +94,8 @@ def main():
             "workload": a.workload, "mode": mode, "records": int(nsamples), "bytes": int(nbytes),
             "copy_threads": a.threads if mode != "per_buffer" else 1,
             "chunk_bytes": (a.chunk_mb << 20) if mode == "stream" else None,
-            "submit_s": submit, "analyze_to_sync_s": tail, "d2h_results_s": d2h, "kernel_s": kern,
+            "submit_s": submit, "analyze_to_sync_s": tail,
+            ("report_s" if a.report else "d2h_results_s"): d2h, "kernel_s": kern,
             "e2e_s": total, "e2e_samples_per_s": nsamples / total,
             "device_resident_samples_per_s": nsamples / kern if kern else None,
         }), flush=True)
