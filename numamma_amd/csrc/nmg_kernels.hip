@@ -886,28 +886,10 @@ __global__ __launch_bounds__(1024, 1) void tlog_reduce_kernel(TlogParams r) {
   __shared__ uint32_t s_cnt[2][kLogChunk];
   __shared__ unsigned long long s_wt[2][kLogChunk];
   __shared__ unsigned long long s_ord[kLogChunk];
-  __shared__ uint32_t s_pre[kLogMaxGrid + 1];
+  __shared__ uint32_t s_pre[kLogMaxGrid];  // slots of each source workgroup's sub-log
   const uint32_t part = blockIdx.x, tid = threadIdx.x;
-  for (uint32_t w = tid; w < r.grid; w += 1024) s_pre[w + 1] = r.tlog_cnt[uint64_t(w) * r.parts + part];
+  for (uint32_t w = tid; w < r.grid; w += 1024) s_pre[w] = r.tlog_cnt[uint64_t(w) * r.parts + part];
   __syncthreads();
-  if (tid < 64) {  // prefix over the source workgroups: a chunk per lane, then a wave scan
-    const uint32_t per = (r.grid + 63) / 64, b = min(tid * per, r.grid), e = min(b + per, r.grid);
-    uint32_t sum = 0;
-    for (uint32_t w = b; w < e; w++) sum += s_pre[w + 1];
-    uint32_t incl = sum;
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t t = __shfl_up(incl, o, 64);
-      if ((int)tid >= o) incl += t;
-    }
-    uint32_t run = incl - sum;
-    for (uint32_t w = b; w < e; w++) {
-      run += s_pre[w + 1];
-      s_pre[w + 1] = run;
-    }
-    if (tid == 0) s_pre[0] = 0;
-  }
-  __syncthreads();
-  const uint32_t total = s_pre[r.grid];
   const uint64_t e0 = uint64_t(part) << r.rshift;
   const uint64_t e1 = min(e0 + (1ull << r.rshift), (uint64_t)r.nb_entries);
   for (uint64_t base = e0; base < e1; base += kLogChunk) {
@@ -918,43 +900,39 @@ __global__ __launch_bounds__(1024, 1) void tlog_reduce_kernel(TlogParams r) {
       s_ord[j] = ~0ull;
     }
     __syncthreads();
-    constexpr int kU = 4;  // records per thread in flight
-    for (uint32_t i0 = tid; i0 < total; i0 += kU * 1024) {
-      uint4 sv[kU];
-      const uint4* sq[kU];
+    // each wave walks whole source sub-logs (contiguous slots), kU slots per
+    // lane in flight; sub-logs are about equally long (byte-balanced schedule)
+    constexpr int kU = 4;
+    const uint32_t wave = tid >> 6, lane = tid & 63;
+    for (uint32_t w = wave; w < r.grid; w += 1024 / 64) {
+      const uint32_t cnt = s_pre[w];
+      const uint4* src = r.tlog + (uint64_t(w) * r.parts + part) * r.cap;
+      for (uint32_t i0 = lane; i0 < cnt; i0 += kU * 64) {
+        uint4 sv[kU];
 #pragma unroll
-      for (int u = 0; u < kU; u++) {
-        const uint32_t i = i0 + u * 1024;
-        sv[u] = make_uint4(~0u, 0, kTlogCont, 0);  // (no slot: skipped like a continuation)
-        sq[u] = nullptr;
-        if (i >= total) continue;
-        uint32_t lo = 0, hi = r.grid;  // source workgroup: s_pre[lo] <= i < s_pre[lo + 1]
-        while (hi - lo > 1) {
-          const uint32_t mid = (lo + hi) >> 1;
-          if (s_pre[mid] <= i) lo = mid;
-          else hi = mid;
+        for (int u = 0; u < kU; u++) {
+          const uint32_t i = i0 + u * 64;
+          sv[u] = i < cnt ? src[i] : make_uint4(~0u, 0, kTlogCont, 0);  // (no slot: skipped like a continuation)
         }
-        sq[u] = r.tlog + (uint64_t(lo) * r.parts + part) * r.cap + (i - s_pre[lo]);
-        sv[u] = *sq[u];
-      }
 #pragma unroll
-      for (int u = 0; u < kU; u++) {
-        const uint4 v = sv[u];
-        if (v.z == kTlogCont) continue;  // second slot of a two-slot record (read with its head)
-        const uint32_t e = v.x & 0x7fffffffu, a = v.x >> 31;
-        const uint64_t j = e - base;
-        if (e < base || j >= n) continue;
-        uint32_t cnt = 1;
-        uint64_t wt = v.y, ord = (uint64_t(v.w) << 32) | v.z;
-        if (v.z == kTlogHead) {
-          const uint4 c = sq[u][1];
-          cnt = v.y;
-          wt = (uint64_t(c.y) << 32) | c.x;
-          ord = (uint64_t(v.w) << 32) | c.w;
+        for (int u = 0; u < kU; u++) {
+          const uint4 v = sv[u];
+          if (v.z == kTlogCont) continue;  // second slot of a two-slot record (read with its head)
+          const uint32_t e = v.x & 0x7fffffffu, a = v.x >> 31;
+          const uint64_t j = e - base;
+          if (e < base || j >= n) continue;
+          uint32_t c = 1;
+          uint64_t wt = v.y, ord = (uint64_t(v.w) << 32) | v.z;
+          if (v.z == kTlogHead) {
+            const uint4 q = src[i0 + u * 64 + 1];
+            c = v.y;
+            wt = (uint64_t(q.y) << 32) | q.x;
+            ord = (uint64_t(v.w) << 32) | q.w;
+          }
+          atomicAdd(&s_cnt[a][j], c);
+          if (wt) atomicAdd(&s_wt[a][j], (unsigned long long)wt);
+          atomicMin(&s_ord[j], (unsigned long long)ord);
         }
-        atomicAdd(&s_cnt[a][j], cnt);
-        if (wt) atomicAdd(&s_wt[a][j], (unsigned long long)wt);
-        atomicMin(&s_ord[j], (unsigned long long)ord);
       }
     }
     __syncthreads();
