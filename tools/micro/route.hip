@@ -1,0 +1,351 @@
+// Partition-first cost model: the two passes of a
+// route-then-attribute design at the configs[3] shard's shape, as a stand-alone
+// measurement (not the product path).
+//   pass 1 (route): stream N 40 B records, find each sample's address range
+//     (partition) in an LDS Eytzinger tree of P - 1 partition bounds, append a
+//     24 B compact record {addr, ts, weight | partition check, position} to the
+//     workgroup's chunk of that partition (LDS cursors);
+//   pass 2 (local): one workgroup per partition at a time: the partition's keys
+//     in LDS, every chunk of the partition read in order, each record's lower
+//     bound found by an LDS search and counted per key in LDS, then flushed.
+//   route <records_M> <keys_K> <partitions> [staged 0/1]
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <random>
+#include <vector>
+
+#define CHECK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); exit(1); } } while (0)
+
+constexpr int kWG = 1024;
+constexpr int kMaxParts = 1024;  // partitions (P <= 1024)
+constexpr int kMaxLocal = 4096;  // keys per partition held in LDS (pass 2); partitions must not be larger
+constexpr int kBatch = 4096;     // staged route: records sorted by partition in LDS per batch
+
+__device__ __forceinline__ uint32_t hash32(uint32_t x) {
+  x ^= x >> 16; x *= 0x7feb352dU; x ^= x >> 15; x *= 0x846ca68bU; x ^= x >> 16; return x;
+}
+
+// synthetic records: Zipf(1.1)-ranked objects (hashed permutation), uniform
+// offset inside the object, 10 % in the gap after a uniform object
+__global__ void gen_kernel(uint64_t* rec, uint64_t n, const uint64_t* keys, const uint32_t* size, uint32_t K) {
+  for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += gridDim.x * 256ull) {
+    uint32_t h = hash32((uint32_t)i * 2654435761u + 17);
+    const float u = (hash32(h) + 1.0f) * 2.3283064e-10f;
+    uint32_t k;
+    uint64_t addr;
+    if ((h & 1023) < 102) {
+      k = hash32(h ^ 0xabcdef) % K;
+      addr = keys[k] + size[k] + (hash32(h + 3) % 4096);
+    } else {
+      const double r = pow((double)u, -10.0);  // P(rank >= r) ~ r^(1 - 1.1)
+      const uint32_t rank = (uint32_t)min(r, (double)K - 1);
+      k = hash32(rank * 0x9E3779B1u + 7) % K;
+      addr = keys[k] + hash32(h + 5) % size[k];
+    }
+    uint64_t* q = rec + 5 * i;
+    q[0] = (40ull << 48) | 9;
+    q[1] = i;
+    q[2] = addr;
+    q[3] = 1 + (h >> 22);
+    q[4] = 0x42;
+  }
+}
+
+__device__ __forceinline__ uint32_t eytz_last_le(const uint64_t* F, uint32_t levels, uint64_t addr) {
+  uint32_t i = 1;
+  for (uint32_t l = 0; l < levels; l++) i = 2 * i + (F[i] <= addr ? 1u : 0u);
+  return i >> (__builtin_ctz(i) + 1);  // 0: below every bound
+}
+
+struct RouteParams {
+  const uint64_t* rec;
+  uint64_t n;
+  const uint64_t* bounds;  // [2^levels] Eytzinger, ~0 padded
+  const uint32_t* rank;    // Eytzinger node -> partition index (in-order rank + 1)
+  uint32_t levels, parts;
+  const uint64_t* off;     // [grid][parts] partition-major output offsets (count pass, untimed)
+  uint32_t* cnt;           // count pass: [grid][parts]
+  uint4* out;              // 16 B + 8 B per record, as two arrays
+  uint2* out2;
+};
+
+template <bool COUNT>
+__global__ __launch_bounds__(kWG, 1) void route_kernel(RouteParams p) {
+  __shared__ uint64_t s_b[kMaxParts];
+  __shared__ uint32_t s_r[kMaxParts];
+  __shared__ uint32_t s_cur[kMaxParts];
+  const uint32_t tid = threadIdx.x;
+  for (uint32_t i = tid; i < (1u << p.levels); i += kWG) {
+    s_b[i] = p.bounds[i];
+    s_r[i] = p.rank[i];
+  }
+  for (uint32_t i = tid; i < p.parts; i += kWG) s_cur[i] = 0;
+  __syncthreads();
+  const uint64_t per = (p.n + gridDim.x - 1) / gridDim.x;
+  const uint64_t r0 = blockIdx.x * per, r1 = min(p.n, r0 + per);
+  const uint64_t* ob = p.off + uint64_t(blockIdx.x) * p.parts;
+  for (uint64_t i = r0 + tid; i < r1; i += kWG) {
+    const uint64_t* q8 = p.rec + 5 * i;
+    const uint64_t ts = q8[1], addr = q8[2], w = q8[3];
+    const uint32_t node = eytz_last_le(s_b, p.levels, addr);
+    const uint32_t part = node ? s_r[node] : 0;  // rank + 1 of the last bound <= addr; 0 below all
+    const uint32_t k = atomicAdd(&s_cur[part], 1u);
+    if (!COUNT) {
+      const uint64_t o = ob[part] + k;
+      p.out[o] = make_uint4((uint32_t)addr, (uint32_t)(addr >> 32), (uint32_t)ts, (uint32_t)(ts >> 32));
+      p.out2[o] = make_uint2((uint32_t)w, (uint32_t)i);
+    }
+  }
+  if (COUNT) {
+    __syncthreads();
+    for (uint32_t i = tid; i < p.parts; i += kWG) p.cnt[uint64_t(blockIdx.x) * p.parts + i] = s_cur[i];
+  }
+}
+
+// Route pass with the batch counting-sorted by partition in LDS first, so
+// that each partition's records of the batch are written as one contiguous run.
+__global__ __launch_bounds__(kWG, 1) void route_staged_kernel(RouteParams p) {
+  __shared__ uint64_t s_b[kMaxParts];
+  __shared__ uint16_t s_r[kMaxParts];
+  __shared__ uint32_t s_hist[kMaxParts], s_start[kMaxParts], s_cur[kMaxParts];
+  __shared__ uint4 s_a[kBatch];
+  __shared__ uint2 s_w[kBatch];
+  __shared__ uint16_t s_p[kBatch];
+  __shared__ uint32_t s_wsum[kWG / 64];
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  for (uint32_t i = tid; i < (1u << p.levels); i += kWG) {
+    s_b[i] = p.bounds[i];
+    s_r[i] = (uint16_t)p.rank[i];
+  }
+  for (uint32_t i = tid; i < kMaxParts; i += kWG) s_cur[i] = s_hist[i] = 0;
+  __syncthreads();
+  const uint64_t per = (p.n + gridDim.x - 1) / gridDim.x;
+  const uint64_t r0 = blockIdx.x * per, r1 = min(p.n, r0 + per);
+  const uint64_t* ob = p.off + uint64_t(blockIdx.x) * p.parts;
+  constexpr int kPer = kBatch / kWG;
+  for (uint64_t b0 = r0; b0 < r1; b0 += kBatch) {
+    uint32_t part[kPer], rk[kPer];
+    uint4 av[kPer];
+    uint2 wv[kPer];
+#pragma unroll
+    for (int u = 0; u < kPer; u++) {
+      const uint64_t i = b0 + tid + u * kWG;
+      part[u] = ~0u;
+      rk[u] = 0;
+      av[u] = make_uint4(0, 0, 0, 0);
+      wv[u] = make_uint2(0, 0);
+      if (i < r1) {
+        const uint64_t* q8 = p.rec + 5 * i;
+        const uint64_t ts = q8[1], addr = q8[2], w = q8[3];
+        const uint32_t node = eytz_last_le(s_b, p.levels, addr);
+        part[u] = node ? s_r[node] : 0;
+        rk[u] = atomicAdd(&s_hist[part[u]], 1u);
+        av[u] = make_uint4((uint32_t)addr, (uint32_t)(addr >> 32), (uint32_t)ts, (uint32_t)(ts >> 32));
+        wv[u] = make_uint2((uint32_t)w, (uint32_t)i);
+      }
+    }
+    __syncthreads();
+    // exclusive scan of the histogram (kMaxParts entries, 4 per thread)
+    uint32_t loc[kMaxParts / kWG], sum = 0;
+#pragma unroll
+    for (int u = 0; u < kMaxParts / kWG; u++) {
+      loc[u] = sum;
+      sum += s_hist[tid * (kMaxParts / kWG) + u];
+    }
+    uint32_t incl = sum;
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t t = __shfl_up(incl, o, 64);
+      if ((int)lane >= o) incl += t;
+    }
+    if (lane == 63) s_wsum[wave] = incl;
+    __syncthreads();
+    uint32_t wbase = 0;
+    for (uint32_t w2 = 0; w2 < wave; w2++) wbase += s_wsum[w2];
+#pragma unroll
+    for (int u = 0; u < kMaxParts / kWG; u++) s_start[tid * (kMaxParts / kWG) + u] = wbase + incl - sum + loc[u];
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < kPer; u++) {
+      if (part[u] == ~0u) continue;
+      const uint32_t j = s_start[part[u]] + rk[u];
+      s_a[j] = av[u];
+      s_w[j] = wv[u];
+      s_p[j] = (uint16_t)part[u];
+    }
+    __syncthreads();
+    const uint32_t nb = (uint32_t)min((uint64_t)kBatch, r1 - b0);
+    for (uint32_t j = tid; j < nb; j += kWG) {
+      const uint32_t q = s_p[j];
+      const uint64_t o = ob[q] + s_cur[q] + (j - s_start[q]);
+      p.out[o] = s_a[j];
+      p.out2[o] = s_w[j];
+    }
+    __syncthreads();
+    for (uint32_t i = tid; i < p.parts; i += kWG) {
+      s_cur[i] += s_hist[i];
+      s_hist[i] = 0;
+    }
+    __syncthreads();
+  }
+}
+
+struct LocalParams {
+  const uint64_t* keys;
+  const uint32_t* pk0;  // [parts + 1] first key of each partition
+  const uint4* in;
+  const uint2* in2;
+  const uint4* items;   // {partition, begin lo, end lo, (begin hi | end hi << 16)}: record ranges of one partition
+  uint32_t nitems;
+  uint32_t* counts;     // [K]
+};
+
+__global__ __launch_bounds__(kWG, 1) void local_kernel(LocalParams p) {
+  __shared__ uint64_t s_k[kMaxLocal];
+  __shared__ uint32_t s_c[kMaxLocal];
+  const uint32_t tid = threadIdx.x;
+  for (uint32_t it = blockIdx.x; it < p.nitems; it += gridDim.x) {
+    const uint4 w = p.items[it];
+    const uint32_t part = w.x;
+    const uint64_t b = w.y | (uint64_t(w.w & 0xffff) << 32), e = w.z | (uint64_t(w.w >> 16) << 32);
+    const uint32_t k0 = p.pk0[part], k1 = p.pk0[part + 1], nk = min(k1 - k0, (uint32_t)kMaxLocal);
+    for (uint32_t i = tid; i < kMaxLocal; i += kWG) {
+      s_k[i] = i < nk ? p.keys[k0 + i] : ~0ull;
+      s_c[i] = 0;
+    }
+    __syncthreads();
+    for (uint64_t i = b + tid; i < e; i += kWG) {
+      const uint4 a = p.in[i];
+      const uint2 c = p.in2[i];
+      const uint64_t addr = (uint64_t(a.y) << 32) | a.x;
+      // largest key <= addr among the partition's keys (binary search in LDS)
+      uint32_t lo = 0, len = kMaxLocal;
+      while (len > 1) {
+        const uint32_t half = len >> 1;
+        lo = s_k[lo + half] <= addr ? lo + half : lo;
+        len -= half;
+      }
+      if (s_k[lo] <= addr) atomicAdd(&s_c[lo], 1u + (c.x & 0));
+    }
+    __syncthreads();
+    for (uint32_t i = tid; i < nk; i += kWG)
+      if (s_c[i]) atomicAdd(p.counts + k0 + i, s_c[i]);
+    __syncthreads();
+  }
+}
+
+int main(int argc, char** argv) {
+  const uint64_t n = (uint64_t)((argc > 1 ? atof(argv[1]) : 125) * 1e6);
+  const uint32_t K = (uint32_t)((argc > 2 ? atof(argv[2]) : 1000) * 1e3);
+  const uint32_t P = argc > 3 ? atoi(argv[3]) : 1024;
+  uint32_t levels = 0;
+  while ((1u << levels) - 1 < P - 1) levels++;
+  // table: log-uniform sizes 64 B .. 64 KiB, gaps up to the size
+  std::mt19937_64 rng(1);
+  std::vector<uint64_t> keys(K);
+  std::vector<uint32_t> size(K);
+  uint64_t a = 0x555555560000ull;
+  for (uint32_t k = 0; k < K; k++) {
+    const double lg = std::uniform_real_distribution<double>(std::log(64.0), std::log(65536.0))(rng);
+    size[k] = (uint32_t)std::exp(lg);
+    keys[k] = a;
+    a += (size[k] + 15) / 16 * 16 + rng() % (size[k] + 1) / 16 * 16 + 16;
+  }
+  // partitions: K / P keys each; bound b = first key of partition b + 1
+  std::vector<uint32_t> pk0(P + 1);
+  for (uint32_t i = 0; i <= P; i++) pk0[i] = (uint32_t)((uint64_t)K * i / P);
+  std::vector<uint64_t> eb(1u << levels, ~0ull);
+  std::vector<uint32_t> er(1u << levels, 0);
+  {
+    uint32_t r = 0, i = 1;
+    std::vector<uint32_t> st;
+    const uint32_t m = 1u << levels;
+    while (i < m || !st.empty()) {
+      while (i < m) { st.push_back(i); i = 2 * i; }
+      i = st.back(); st.pop_back();
+      if (r < P - 1) { eb[i] = keys[pk0[r + 1]]; er[i] = r + 1; }
+      r++;
+      i = 2 * i + 1;
+    }
+  }
+  // partition 0 also takes addresses below the first key (they match nothing)
+  int ncu = 0;
+  CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0));
+  const uint32_t G = ncu;
+  uint64_t *d_rec, *d_keys, *d_b, *d_off;
+  uint32_t *d_size, *d_r, *d_cntwp, *d_pk0, *d_cnt;
+  uint4 *d_out, *d_items;
+  uint2* d_out2;
+  CHECK(hipMalloc(&d_rec, n * 40));
+  CHECK(hipMalloc(&d_keys, K * 8ull));
+  CHECK(hipMalloc(&d_size, K * 4ull));
+  CHECK(hipMalloc(&d_b, eb.size() * 8));
+  CHECK(hipMalloc(&d_r, er.size() * 4));
+  CHECK(hipMalloc(&d_off, (size_t)G * P * 8));
+  CHECK(hipMalloc(&d_cntwp, (size_t)G * P * 4));
+  CHECK(hipMalloc(&d_pk0, (P + 1) * 4));
+  CHECK(hipMalloc(&d_cnt, K * 4ull));
+  CHECK(hipMalloc(&d_out, n * 16));
+  CHECK(hipMalloc(&d_out2, n * 8));
+  CHECK(hipMemcpy(d_keys, keys.data(), K * 8ull, hipMemcpyHostToDevice));
+  CHECK(hipMemcpy(d_size, size.data(), K * 4ull, hipMemcpyHostToDevice));
+  CHECK(hipMemcpy(d_b, eb.data(), eb.size() * 8, hipMemcpyHostToDevice));
+  CHECK(hipMemcpy(d_r, er.data(), er.size() * 4, hipMemcpyHostToDevice));
+  CHECK(hipMemcpy(d_pk0, pk0.data(), (P + 1) * 4, hipMemcpyHostToDevice));
+  hipLaunchKernelGGL(gen_kernel, dim3(4096), dim3(256), 0, 0, d_rec, n, d_keys, d_size, K);
+  CHECK(hipDeviceSynchronize());
+  // untimed count pass -> partition-major offsets and balanced work items
+  RouteParams rp{d_rec, n, d_b, d_r, levels, P, d_off, d_cntwp, d_out, d_out2};
+  hipLaunchKernelGGL(route_kernel<true>, dim3(G), dim3(kWG), 0, 0, rp);
+  CHECK(hipDeviceSynchronize());
+  std::vector<uint32_t> cnt((size_t)G * P);
+  CHECK(hipMemcpy(cnt.data(), d_cntwp, cnt.size() * 4, hipMemcpyDeviceToHost));
+  std::vector<uint64_t> off((size_t)G * P);
+  std::vector<uint4> items;
+  const uint64_t kItem = 65536;
+  uint64_t run = 0, maxpart = 0;
+  for (uint32_t q = 0; q < P; q++) {
+    const uint64_t pb = run;
+    for (uint32_t w = 0; w < G; w++) {
+      off[(size_t)w * P + q] = run;
+      run += cnt[(size_t)w * P + q];
+    }
+    maxpart = std::max(maxpart, run - pb);
+    for (uint64_t b = pb; b < run; b += kItem) {
+      const uint64_t e = std::min(run, b + kItem);
+      items.push_back(make_uint4(q, (uint32_t)b, (uint32_t)e, (uint32_t)(b >> 32) | ((uint32_t)(e >> 32) << 16)));
+    }
+  }
+  CHECK(hipMemcpy(d_off, off.data(), off.size() * 8, hipMemcpyHostToDevice));
+  CHECK(hipMalloc(&d_items, items.size() * 16));
+  CHECK(hipMemcpy(d_items, items.data(), items.size() * 16, hipMemcpyHostToDevice));
+  LocalParams lp{d_keys, d_pk0, d_out, d_out2, d_items, (uint32_t)items.size(), d_cnt};
+  hipEvent_t e0, e1, e2;
+  CHECK(hipEventCreate(&e0)); CHECK(hipEventCreate(&e1)); CHECK(hipEventCreate(&e2));
+  const bool staged = argc > 4 && atoi(argv[4]);
+  float best1 = 1e30f, best2 = 1e30f;
+  for (int rep = 0; rep < 4; rep++) {
+    CHECK(hipMemset(d_cnt, 0, K * 4ull));
+    CHECK(hipEventRecord(e0));
+    if (staged) hipLaunchKernelGGL(route_staged_kernel, dim3(G), dim3(kWG), 0, 0, rp);
+    else hipLaunchKernelGGL(route_kernel<false>, dim3(G), dim3(kWG), 0, 0, rp);
+    CHECK(hipEventRecord(e1));
+    hipLaunchKernelGGL(local_kernel, dim3(G), dim3(kWG), 0, 0, lp);
+    CHECK(hipEventRecord(e2));
+    CHECK(hipEventSynchronize(e2));
+    float t1 = 0, t2 = 0;
+    CHECK(hipEventElapsedTime(&t1, e0, e1));
+    CHECK(hipEventElapsedTime(&t2, e1, e2));
+    if (rep) { best1 = std::min(best1, t1); best2 = std::min(best2, t2); }
+  }
+  printf("{\"staged\": %d, \"records\": %lu, \"keys\": %u, \"partitions\": %u, \"route_ms\": %.3f, \"local_ms\": %.3f, "
+         "\"total_ms\": %.3f, \"Gsamples_s\": %.2f, \"route_GBps\": %.0f, \"work_items\": %zu, "
+         "\"largest_partition_frac\": %.4f}\n",
+         (int)staged, (unsigned long)n, K, P, best1, best2, best1 + best2, n / ((best1 + best2) * 1e6),
+         n * (40.0 + 24.0) / (best1 * 1e6), items.size(), (double)maxpart / n);
+  return 0;
+}
