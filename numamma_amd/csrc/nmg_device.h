@@ -144,19 +144,23 @@ __device__ __forceinline__ int bucket_slot(unsigned int* slots8, uint32_t key) {
 constexpr uint32_t kDrainWindows = 256;
 constexpr uint64_t kLaneMaxWeight = 1ull << 23;
 static_assert((uint64_t)kDensePageWindows * kWG * kLaneMaxWeight < (1ull << kPackShift), "packed weight");
-// Only the 9 hit buckets live in registers (the common case in PEBS data);
-// miss buckets are updated in LDS directly.
+// Only the hit buckets of the first kRegGroups level groups (L1, L2, L3: the
+// common case in PEBS data) live in registers; the other hit buckets and every
+// miss bucket are updated in LDS directly.  (Nine groups in registers left the
+// large-table instance 28 B of scratch per lane; three groups: none spilled
+// where five still spilled 12 B, and c2 -3 %, k1m -1.5 %.)
+constexpr int kRegGroups = 3;
 struct LaneAcc {
-  uint32_t cnt2[5];  // counts of hit buckets 2k (low 16 bits) and 2k+1 (high 16 bits)
-  uint32_t sum[9];
+  uint32_t cnt2[(kRegGroups + 1) / 2];  // counts of hit buckets 2k (low 16 bits) and 2k+1 (high 16 bits)
+  uint32_t sum[kRegGroups];
   uint32_t tc, tw, na;
 };
 
 __device__ __forceinline__ void lane_acc_clear(LaneAcc& a) {
 #pragma unroll
-  for (int k = 0; k < 5; k++) a.cnt2[k] = 0;
+  for (int k = 0; k < (kRegGroups + 1) / 2; k++) a.cnt2[k] = 0;
 #pragma unroll
-  for (int k = 0; k < 9; k++) a.sum[k] = 0;
+  for (int k = 0; k < kRegGroups; k++) a.sum[k] = 0;
   a.tc = a.tw = a.na = 0;
 }
 
@@ -176,16 +180,16 @@ __device__ __forceinline__ void lane_acc_drain(LaneAcc& a, unsigned long long* s
     if (na) atomicAdd(&sums[2], (unsigned long long)na);
   }
 #pragma unroll
-  for (int k = 0; k < 5; k++) {
+  for (int k = 0; k < (kRegGroups + 1) / 2; k++) {
     if (__ballot(a.cnt2[k] != 0) == 0) continue;
     const uint32_t c0 = wave_sum_u32(a.cnt2[k] & 0xffffu), c1 = wave_sum_u32(a.cnt2[k] >> 16);
     if (lane == 0) {
       if (c0) atomicAdd(&sums[3 + 2 * (2 * k)], (unsigned long long)c0);
-      if (c1 && 2 * k + 1 < 9) atomicAdd(&sums[3 + 2 * (2 * k + 1)], (unsigned long long)c1);
+      if (c1 && 2 * k + 1 < kRegGroups) atomicAdd(&sums[3 + 2 * (2 * k + 1)], (unsigned long long)c1);
     }
   }
 #pragma unroll
-  for (int k = 0; k < 9; k++) {
+  for (int k = 0; k < kRegGroups; k++) {
     if (__ballot(a.sum[k] != 0) == 0) continue;
     const uint64_t sk = wave_sum_u32x(a.sum[k]);
     if (lane == 0) atomicAdd(&sums[4 + 2 * k], (unsigned long long)sk);

@@ -300,11 +300,12 @@ __device__ __forceinline__ void process_sample(Params& p, WgCounters& wc, LaneAc
       acc.tw += w32;
       acc.na += lvl & LVL_NA;
 #pragma unroll
-      for (int k = 0; k < 5; k++) acc.cnt2[k] += ((bm >> (2 * k)) & 1) | ((k < 4 ? (bm >> (2 * k + 1)) & 1 : 0) << 16);
+      for (int k = 0; k < (kRegGroups + 1) / 2; k++)
+        acc.cnt2[k] += ((bm >> (2 * k)) & 1) | ((2 * k + 1 < kRegGroups ? (bm >> (2 * k + 1)) & 1 : 0) << 16);
 #pragma unroll
-      for (int k = 0; k < 9; k++) acc.sum[k] += ((bm >> k) & 1) * w32;
-      for (uint32_t m = bm >> 9; m; m &= m - 1) {  // miss buckets
-        const uint32_t b = 9 + (uint32_t)__builtin_ctz(m);
+      for (int k = 0; k < kRegGroups; k++) acc.sum[k] += ((bm >> k) & 1) * w32;
+      for (uint32_t m = bm >> kRegGroups; m; m &= m - 1) {  // rarer hit buckets, miss buckets
+        const uint32_t b = kRegGroups + (uint32_t)__builtin_ctz(m);
         atomicAdd(&wc.sums[3 + 2 * b], 1ull);
         if (w) atomicAdd(&wc.sums[4 + 2 * b], (unsigned long long)w);
       }
