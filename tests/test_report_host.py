@@ -177,3 +177,19 @@ def test_all_memory_objects(tmp_path, cfg):
     assert open(os.path.join(d, "o.txt"), "rb").read() == open(os.path.join(d, "p.txt"), "rb").read()
     for f in ("call_sites.log",):
         assert open(os.path.join(odir, f), "rb").read() == open(os.path.join(pdir, f), "rb").read()
+
+
+def test_report_files_independent_of_writer_threads(tmp_path, monkeypatch):
+    """The per-site page files are written by a thread pool (NMG_REPORT_THREADS):
+    one writer and many give the same bytes, and both match the oracle."""
+    rp = generate(SynthConfig(nb_samples=50_000, nb_intervals=3_000, site_ratio=0.5, seed=5))
+    raw, odir = _run_oracle(rp, str(tmp_path))
+    outs = []
+    for n in ("1", "7"):
+        monkeypatch.setenv("NMG_REPORT_THREADS", n)
+        pdir = str(tmp_path / f"product_{n}")
+        report_host(raw, rp.table, _buf_bytes(rp), pdir, str(tmp_path / f"stdout_{n}.txt"))
+        outs.append(pdir)
+        _compare_dirs(odir, pdir)
+    assert len(os.listdir(outs[0])) > 100  # many call sites: the pool has work to split
+    assert open(tmp_path / "stdout_1.txt", "rb").read() == open(tmp_path / "stdout_7.txt", "rb").read()
