@@ -303,6 +303,9 @@ int nmg_get_kernel_times(nmg_engine *h, float *attribute_ms, float *total_ms, in
  * callsite_counters_<id>.dat in opts->output_dir -- byte-identical formats
  * (mem_analyzer.c:1438-1640, mem_sampling.c:321-361).
  * meta[] parallels the entries passed to nmg_set_objects.
+ * The per-site files are written by up to 16 host threads (environment:
+ * NMG_REPORT_THREADS=n sets the count, NMG_REPORT_TIMING=1 prints phase times
+ * on stderr); the output does not depend on the count.
  */
 int nmg_report(nmg_engine *h, const struct nmg_object_meta *meta,
                const struct nmg_report_options *opts, const char *stdout_path);
