@@ -264,6 +264,9 @@ def result_line(args, w, world, steps, ms_per_step, value, attr_ms, total_ms):
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
             "traffic": traffic,
+            # the HBM bytes the kernel really moves (PMC, per launch) per second: the
+            # lookups' random lines come on top of the 40 B per record
+            "traffic_GBps": (traffic / (avg_attr * 1e-3) / 1e9) if traffic else None,
             "algorithmic_bytes_per_launch": algo,
             "avg_kernel_ms": avg_attr,
             "avg_launch_ms": avg_total,
