@@ -144,6 +144,9 @@ __device__ __forceinline__ int bucket_slot(unsigned int* slots8, uint32_t key) {
 constexpr uint32_t kDrainWindows = 256;
 constexpr uint64_t kLaneMaxWeight = 1ull << 23;
 static_assert((uint64_t)kDensePageWindows * kWG * kLaneMaxWeight < (1ull << kPackShift), "packed weight");
+// hashed object slots: flushed at least every kTableWindows windows
+static_assert((uint64_t)kTableWindows * kWG < (1ull << (64 - kPackShift)), "packed hashed count");
+static_assert((uint64_t)kTableWindows * kWG * kLaneMaxWeight <= (1ull << kPackShift), "packed hashed weight");
 // Only the hit buckets of the first kRegGroups level groups (L1, L2, L3: the
 // common case in PEBS data) live in registers; the other hit buckets and every
 // miss bucket are updated in LDS directly.  (Nine groups in registers left the

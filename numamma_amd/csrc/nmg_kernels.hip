@@ -121,9 +121,8 @@ struct WgCounters {
   unsigned long long mins[18];
   unsigned long long maxs[18];
   alignas(16) unsigned int okey[kObjSlots];  // entry id, 8 per bucket (hashed modes)
-  unsigned int ocnt[kObjSlots];
   unsigned long long ofirst[kObjSlots];  // smallest (seq << 32 | offset): first match
-  unsigned long long owt[kObjSlots];
+  unsigned long long owt[kObjSlots];     // count << kPackShift | weight sum (weights < kLaneMaxWeight)
   union {
     struct {
       uint4 pkey4[kPageSlots / 4];  // dense cell index (hist_base(entry) + page), 8 per bucket
@@ -352,18 +351,17 @@ __device__ __forceinline__ void process_sample(Params& p, WgCounters& wc, LaneAc
   // per-object counters, aggregated per stream in LDS.  (Admitting an entry
   // only on its second sample -- a doorkeeper bitset -- was measured slower at
   // 1M intervals: the per-sample bit test costs more than the flushes it saves.)
-  // (with packing, a slot only sums packable weights: its flush is packed too)
+  // A slot sums (count << kPackShift | weight) in one u64 LDS add, for weights
+  // < kLaneMaxWeight (dense: bounded by the kDensePageWindows cadence, < 2^16
+  // samples; hashed: by kTableWindows, < 2^18 samples).  With the packed
+  // long-tail counters on, a hashed slot only takes weights they can pack too
+  // (its flush is packed as well); any other sample takes the table-full path.
   const bool pk = !(MODE & kModeDenseObj) && p.pk64 && w < p.pk_wlim && !shortrec;
-  const int os = (MODE & kModeDenseObj) ? (int)e : ((p.pk64 && !pk) ? -1 : obj_slot(wc, (uint32_t)e));
+  const bool lds_ok = w < kLaneMaxWeight && (!(MODE & kModeDenseObj) ? (!p.pk64 || pk) : kPackObj);
+  const int os = !lds_ok ? -1 : ((MODE & kModeDenseObj) ? (int)e : obj_slot(wc, (uint32_t)e));
   const unsigned long long ord = ((in1 ? b1.seq : b0.seq) << 32) | off;  // first match in analysis order (quirk Q7)
-  if ((MODE & kModeDenseObj) && w < kLaneMaxWeight && kPackObj) {
-    // one packed add: count in bits 44..63, weight below (bounded by the
-    // kDensePageWindows flush cadence: < 2^16 samples of < 2^23 each)
+  if (os >= 0) {
     atomicAdd(&wc.owt[os], (1ull << kPackShift) | w);
-    if (ord < wc.ofirst[os]) atomicMin(&wc.ofirst[os], ord);
-  } else if (os >= 0 && !((MODE & kModeDenseObj) && kPackObj)) {
-    atomicAdd(&wc.ocnt[os], 1u);
-    if (w) atomicAdd(&wc.owt[os], (unsigned long long)w);
     if (ord < wc.ofirst[os]) atomicMin(&wc.ofirst[os], ord);
   } else if (!(MODE & kModeDenseObj) && p.tlog && tlog_append(p, wc, (uint32_t)e, access, 1u, w, ord)) {
     // table full: logged for tlog_reduce_kernel
@@ -424,10 +422,9 @@ __device__ __forceinline__ void flush_objects(Params& p, WgCounters& wc, int tid
   const int n = (MODE & kModeDenseObj) ? (int)p.nb_entries : (int)kObjSlots;
   for (int i = tid; i < n; i += kWG) {
     const uint32_t e = (MODE & kModeDenseObj) ? (uint32_t)i : wc.okey[i];
-    constexpr bool packed = (MODE & kModeDenseObj) && kPackObj;
-    if ((MODE & kModeDenseObj) ? (packed ? wc.owt[i] == 0 : wc.ocnt[i] == 0) : e == kEmpty32) continue;
-    const uint64_t cnt = packed ? wc.owt[i] >> kPackShift : wc.ocnt[i];
-    const uint64_t wt = packed ? wc.owt[i] & ((1ull << kPackShift) - 1) : wc.owt[i];
+    if ((MODE & kModeDenseObj) ? wc.owt[i] == 0 : e == kEmpty32) continue;
+    const uint64_t cnt = wc.owt[i] >> kPackShift;
+    const uint64_t wt = wc.owt[i] & ((1ull << kPackShift) - 1);
     if (write && !(MODE & kModeDenseObj) && p.tlog && tlog_append(p, wc, e, a, (uint32_t)cnt, wt, wc.ofirst[i])) {
       // logged
     } else if (write && !(MODE & kModeDenseObj) && p.pk64) {
@@ -443,7 +440,6 @@ __device__ __forceinline__ void flush_objects(Params& p, WgCounters& wc, int tid
       atomicMin(fp, wc.ofirst[i]);  // no read first: a returning load would stall the flush
     }
     wc.okey[i] = kEmpty32;
-    wc.ocnt[i] = 0;
     wc.ofirst[i] = kEmpty64;
     wc.owt[i] = 0;
   }
@@ -505,7 +501,6 @@ __device__ __forceinline__ void clear_state(WgCounters& wc, int tid) {
   clear_sums(wc, tid);
   for (int i = tid; i < (int)kObjSlots; i += kWG) {
     wc.okey[i] = kEmpty32;
-    wc.ocnt[i] = 0;
     wc.ofirst[i] = kEmpty64;
     wc.owt[i] = 0;
   }
