@@ -238,10 +238,94 @@ __global__ __launch_bounds__(kWG, 1) void local_kernel(LocalParams p) {
   }
 }
 
+// The second pass with the product's per-sample work (cost model): per work
+// item, the partition's keys and node fields in LDS; per record the lower
+// bound, the end / date check, a packed (count, weight) add and a first-ordinal
+// minimum per object, a u16 page-cell count per (thread, page) of the
+// partition; flushed with global atomics at the end of the item.
+constexpr int kFullKeys = 1024, kFullCells = 14336;  // u16 cells, two per word: [8 threads][kFullCells / 8]
+struct FullParams {
+  const uint64_t* keys;
+  const uint64_t* kend;   // [K] object end
+  const uint2* kdate;     // [K] (alloc, free) as 32-bit
+  const uint32_t* kcell;  // [K] first page cell of the key within its partition
+  const uint32_t* pk0;
+  const uint4* in;
+  const uint2* in2;
+  const uint4* items;
+  uint32_t nitems;
+  unsigned long long* objcw;  // [K] count << 44 | weight
+  unsigned long long* objfirst;
+  uint32_t* pages;            // [P][8][kFullCells / 8]
+};
+
+__global__ __launch_bounds__(kWG, 1) void local_full_kernel(FullParams p) {
+  __shared__ uint64_t s_k[kFullKeys], s_end[kFullKeys];
+  __shared__ uint2 s_d[kFullKeys];
+  __shared__ uint32_t s_cell[kFullKeys];
+  __shared__ unsigned long long s_cw[kFullKeys], s_first[kFullKeys];
+  __shared__ uint32_t s_pg[kFullCells / 2];
+  const uint32_t tid = threadIdx.x;
+  for (uint32_t it = blockIdx.x; it < p.nitems; it += gridDim.x) {
+    const uint4 w = p.items[it];
+    const uint32_t part = w.x;
+    const uint64_t b = w.y | (uint64_t(w.w & 0xffff) << 32), e = w.z | (uint64_t(w.w >> 16) << 32);
+    const uint32_t k0 = p.pk0[part], k1 = p.pk0[part + 1], nk = min(k1 - k0, (uint32_t)kFullKeys);
+    for (uint32_t i = tid; i < kFullKeys; i += kWG) {
+      s_k[i] = i < nk ? p.keys[k0 + i] : ~0ull;
+      s_end[i] = i < nk ? p.kend[k0 + i] : 0;
+      s_d[i] = i < nk ? p.kdate[k0 + i] : make_uint2(1, 0);
+      s_cell[i] = i < nk ? p.kcell[k0 + i] : 0;
+      s_cw[i] = 0;
+      s_first[i] = ~0ull;
+    }
+    for (uint32_t i = tid; i < kFullCells / 2; i += kWG) s_pg[i] = 0;
+    __syncthreads();
+    for (uint64_t i = b + tid; i < e; i += kWG) {
+      const uint4 a = p.in[i];
+      const uint2 c = p.in2[i];
+      const uint64_t addr = (uint64_t(a.y) << 32) | a.x;
+      const uint32_t ts = a.z;
+      uint32_t lo = 0, len = kFullKeys;
+      while (len > 1) {
+        const uint32_t half = len >> 1;
+        lo = s_k[lo + half] <= addr ? lo + half : lo;
+        len -= half;
+      }
+      if (s_k[lo] > addr || addr >= s_end[lo]) continue;
+      const uint2 d = s_d[lo];
+      if (ts < d.x || ts > d.y) continue;
+      atomicAdd(&s_cw[lo], (1ull << 44) | (c.x & 0xffff));
+      const unsigned long long ord = c.y;
+      if (ord < s_first[lo]) atomicMin(&s_first[lo], ord);
+      const uint32_t th = (c.y >> 12) & 7;
+      const uint32_t cell = min(s_cell[lo] + (uint32_t)((addr - s_k[lo]) >> 12), (uint32_t)(kFullCells / 8 - 1));
+      const uint32_t x = th * (kFullCells / 8) + cell;
+      atomicAdd(&s_pg[x >> 1], 1u << (16 * (x & 1)));
+    }
+    __syncthreads();
+    for (uint32_t i = tid; i < nk; i += kWG) {
+      if (s_cw[i]) atomicAdd(p.objcw + k0 + i, s_cw[i]);
+      if (s_first[i] != ~0ull) atomicMin(p.objfirst + k0 + i, s_first[i]);
+    }
+    uint32_t* pg = p.pages + uint64_t(part) * kFullCells;
+    for (uint32_t i = tid; i < kFullCells / 2; i += kWG) {
+      const uint32_t v = s_pg[i];
+      if (v & 0xffff) atomicAdd(pg + 2 * i, v & 0xffff);
+      if (v >> 16) atomicAdd(pg + 2 * i + 1, v >> 16);
+    }
+    __syncthreads();
+  }
+}
+
 int main(int argc, char** argv) {
   const uint64_t n = (uint64_t)((argc > 1 ? atof(argv[1]) : 125) * 1e6);
   const uint32_t K = (uint32_t)((argc > 2 ? atof(argv[2]) : 1000) * 1e3);
   const uint32_t P = argc > 3 ? atoi(argv[3]) : 1024;
+  if (P < 2 || P > (uint32_t)kMaxParts || K / P > (uint32_t)kMaxLocal) {
+    printf("partitions must be in [2, %d] with at most %d keys each\n", kMaxParts, kMaxLocal);
+    return 1;
+  }
   uint32_t levels = 0;
   while ((1u << levels) - 1 < P - 1) levels++;
   // table: log-uniform sizes 64 B .. 64 KiB, gaps up to the size
@@ -324,17 +408,57 @@ int main(int argc, char** argv) {
   CHECK(hipMalloc(&d_items, items.size() * 16));
   CHECK(hipMemcpy(d_items, items.data(), items.size() * 16, hipMemcpyHostToDevice));
   LocalParams lp{d_keys, d_pk0, d_out, d_out2, d_items, (uint32_t)items.size(), d_cnt};
+  // node fields for the full second pass: end, (alloc, free) covering most of
+  // the records' timestamps (record i has ts = i), first page cell per key
+  std::vector<uint64_t> kend(K);
+  std::vector<uint2> kdate(K);
+  std::vector<uint32_t> kcell(K);
+  for (uint32_t q = 0; q < P; q++) {
+    uint32_t c = 0;
+    for (uint32_t k = pk0[q]; k < pk0[q + 1]; k++) {
+      kend[k] = keys[k] + size[k];
+      const uint32_t a0 = (uint32_t)(rng() % (n / 20)), f0 = (uint32_t)(n - rng() % (n / 20));
+      kdate[k] = make_uint2(a0, f0);
+      kcell[k] = c;
+      c += size[k] / 4096 + 1;
+    }
+  }
+  uint64_t* d_kend;
+  uint2* d_kdate;
+  uint32_t *d_kcell, *d_pages;
+  unsigned long long *d_objcw, *d_objfirst;
+  CHECK(hipMalloc(&d_kend, K * 8ull));
+  CHECK(hipMalloc(&d_kdate, K * 8ull));
+  CHECK(hipMalloc(&d_kcell, K * 4ull));
+  CHECK(hipMalloc(&d_objcw, K * 8ull));
+  CHECK(hipMalloc(&d_objfirst, K * 8ull));
+  CHECK(hipMalloc(&d_pages, (size_t)P * kFullCells * 4));
+  CHECK(hipMemcpy(d_kend, kend.data(), K * 8ull, hipMemcpyHostToDevice));
+  CHECK(hipMemcpy(d_kdate, kdate.data(), K * 8ull, hipMemcpyHostToDevice));
+  CHECK(hipMemcpy(d_kcell, kcell.data(), K * 4ull, hipMemcpyHostToDevice));
+  FullParams fp{d_keys, d_kend, d_kdate, d_kcell, d_pk0, d_out, d_out2, d_items, (uint32_t)items.size(),
+                d_objcw, d_objfirst, d_pages};
+  const bool full = K / P <= (uint32_t)kFullKeys;
   hipEvent_t e0, e1, e2;
   CHECK(hipEventCreate(&e0)); CHECK(hipEventCreate(&e1)); CHECK(hipEventCreate(&e2));
   const bool staged = argc > 4 && atoi(argv[4]);
   float best1 = 1e30f, best2 = 1e30f;
   for (int rep = 0; rep < 4; rep++) {
     CHECK(hipMemset(d_cnt, 0, K * 4ull));
+    if (full) {
+      CHECK(hipMemset(d_objcw, 0, K * 8ull));
+      CHECK(hipMemset(d_objfirst, 0xff, K * 8ull));
+      CHECK(hipMemset(d_pages, 0, (size_t)P * kFullCells * 4));
+    }
     CHECK(hipEventRecord(e0));
     if (staged) hipLaunchKernelGGL(route_staged_kernel, dim3(G), dim3(kWG), 0, 0, rp);
     else hipLaunchKernelGGL(route_kernel<false>, dim3(G), dim3(kWG), 0, 0, rp);
     CHECK(hipEventRecord(e1));
-    hipLaunchKernelGGL(local_kernel, dim3(G), dim3(kWG), 0, 0, lp);
+    if (full) {
+      hipLaunchKernelGGL(local_full_kernel, dim3(G), dim3(kWG), 0, 0, fp);
+    } else {
+      hipLaunchKernelGGL(local_kernel, dim3(G), dim3(kWG), 0, 0, lp);
+    }
     CHECK(hipEventRecord(e2));
     CHECK(hipEventSynchronize(e2));
     float t1 = 0, t2 = 0;
@@ -343,9 +467,9 @@ int main(int argc, char** argv) {
     if (rep) { best1 = std::min(best1, t1); best2 = std::min(best2, t2); }
   }
   printf("{\"staged\": %d, \"records\": %lu, \"keys\": %u, \"partitions\": %u, \"route_ms\": %.3f, \"local_ms\": %.3f, "
-         "\"total_ms\": %.3f, \"Gsamples_s\": %.2f, \"route_GBps\": %.0f, \"work_items\": %zu, "
+         "\"second_pass\": \"%s\", \"total_ms\": %.3f, \"Gsamples_s\": %.2f, \"route_GBps\": %.0f, \"work_items\": %zu, "
          "\"largest_partition_frac\": %.4f}\n",
-         (int)staged, (unsigned long)n, K, P, best1, best2, best1 + best2, n / ((best1 + best2) * 1e6),
+         (int)staged, (unsigned long)n, K, P, best1, best2, full ? "full" : "count", best1 + best2, n / ((best1 + best2) * 1e6),
          n * (40.0 + 24.0) / (best1 * 1e6), items.size(), (double)maxpart / n);
   return 0;
 }
