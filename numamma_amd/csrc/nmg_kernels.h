@@ -47,7 +47,7 @@ constexpr uint32_t kPageSlots = kPageBuckets * 8;  // 7168 cells (56 KiB)
 constexpr uint32_t kObjBuckets = kObjSlots / 8;
 // hashed (non-dense) tables are flushed at least every kTableWindows windows:
 // u32 counts stay far from overflow and the first-come slots are re-learnt
-constexpr uint32_t kTableWindows = 256;
+constexpr uint32_t kTableWindows = 128;  // (256: configs[2] +4 %, 64: c4 +3 %; 128 neutral at c4)
 // Dense modes (template flags of attribute_kernel):
 //   kModeDenseObj:  nb_entries <= kObjSlots: slot = entry id, no key check;
 //   kModeDensePage: dense histogram cells per thread <= kDensePageCells: u16

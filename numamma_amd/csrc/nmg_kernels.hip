@@ -353,7 +353,7 @@ __device__ __forceinline__ void process_sample(Params& p, WgCounters& wc, LaneAc
   // 1M intervals: the per-sample bit test costs more than the flushes it saves.)
   // A slot sums (count << kPackShift | weight) in one u64 LDS add, for weights
   // < kLaneMaxWeight (dense: bounded by the kDensePageWindows cadence, < 2^16
-  // samples; hashed: by kTableWindows, < 2^18 samples).  With the packed
+  // samples; hashed: by kTableWindows, < 2^17 samples).  With the packed
   // long-tail counters on, a hashed slot only takes weights they can pack too
   // (its flush is packed as well); any other sample takes the table-full path.
   const bool pk = !(MODE & kModeDenseObj) && p.pk64 && w < p.pk_wlim && !shortrec;
