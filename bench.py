@@ -13,8 +13,8 @@ per-GPU shard): 125M 40-byte PERF_RECORD_SAMPLE records per GPU in 128 KiB
 per-thread buffers, 1M object intervals (+ 8 globals + [stack]), 8 threads.
 Weak scaling: every rank analyses its own 125M-record shard against the same
 table, so --gpus 8 is configs[3] (1B records).  configs[1] (10M records, 1k
-intervals) is measured after it and reported in the same JSON line under
-"secondary".
+intervals) and configs[2] (100M records, 100k intervals, per-page on) are measured
+after it and reported in the same JSON line under "secondary".
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c4|c2|c3|k1m]
     torchrun --nproc-per-node N bench.py --gpus N ...
@@ -130,7 +130,8 @@ def main():
     ap.add_argument("--steps", type=int, default=0, help="timed steps (0: enough for >= 1 s)")
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="c4", choices=sorted(WORKLOADS))
-    ap.add_argument("--secondary", default="c2", help="workload measured after the main one (N=1; '' = none)")
+    ap.add_argument("--secondary", default="c2,c3",
+                    help="workloads measured after the main one, comma-separated (N=1; '' = none)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-records", type=int, default=50_000, help="records in the single-threaded oracle's sample")
     ap.add_argument("--cpu-mt-records", type=int, default=25_000_000, help="records in the multi-threaded baseline's sample")
@@ -197,20 +198,23 @@ def main():
     if rank == 0:
         out = result_line(args, w, world, steps, ms_per_step, value, attr_ms, total_ms)
         if world == 1 and args.secondary:
-            s = Workload(args.secondary, rank, device, False)
+            out["secondary"] = {}
+            for name in args.secondary.split(","):
+                s = Workload(name, rank, device, False)
 
-            def sbar():
-                torch.cuda.synchronize(device)
-                s.eng.synchronize()
+                def sbar():
+                    torch.cuda.synchronize(device)
+                    s.eng.synchronize()
 
-            se, sn = timed_run(s, 0, 3, sbar)
-            sa, st = s.eng.kernel_times(min(sn, 64))
-            out["secondary"] = {
-                s.name: {"workload": WORKLOADS[s.name]["desc"], "value": s.samples / (se / sn), "unit": "samples/s",
-                         "ms_per_step": se * 1e3 / sn, "steps": sn,
-                         "attribute_kernel_ms": float(np.mean(sa)), "launch_ms": float(np.mean(st)),
-                         "roofline_frac": s.samples * RECORD_BYTES / (float(np.mean(sa)) * 1e-3) / 1e9 / HBM_PEAK_GBS}}
-            s.eng.close()
+                se, sn = timed_run(s, 0, 3, sbar)
+                sa, st = s.eng.kernel_times(min(sn, 64))
+                out["secondary"][s.name] = {
+                    "workload": WORKLOADS[s.name]["desc"], "value": s.samples / (se / sn), "unit": "samples/s",
+                    "ms_per_step": se * 1e3 / sn, "steps": sn,
+                    "attribute_kernel_ms": float(np.mean(sa)), "launch_ms": float(np.mean(st)),
+                    "roofline_frac": s.samples * RECORD_BYTES / (float(np.mean(sa)) * 1e-3) / 1e9 / HBM_PEAK_GBS}
+                s.eng.close()
+                del s
         if world == 1 and not args.no_cpu_baseline:
             log(f"[rank 0] cpu baseline: first {args.cpu_records} records")
             out["cpu_baseline"] = cpu_baseline(w.rp, args.cpu_records, args.cpu_mt_records, args.cpu_threads)
