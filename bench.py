@@ -145,13 +145,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world == 1 and args.gpus > 1:  # no launcher: one process drives every GPU through the C-ABI
+        return main_one_process(args)
     # test hooks for the multi-rank path on a one-GPU box (never used by the driver):
     # NMG_BENCH_BACKEND=gloo, NMG_BENCH_SAME_GPU=1 (every rank on GPU 0)
     backend = os.environ.get("NMG_BENCH_BACKEND", "nccl")
     if os.environ.get("NMG_BENCH_SAME_GPU") == "1":
         local = 0
     if world != args.gpus:
-        log(f"warning: WORLD_SIZE={world} but --gpus={args.gpus}; using WORLD_SIZE")
+        log(f"error: WORLD_SIZE={world} but --gpus={args.gpus}")
+        sys.exit(2)
     distributed = world > 1
     if distributed:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -223,6 +226,74 @@ def main():
         dist.barrier()
         dist.destroy_process_group()
     w.eng.close()
+
+
+def main_one_process(args):
+    """--gpus N without a launcher: the reference's shape, one analysing
+    process (mem_sampling.c:324-342), here driving N GPUs through one engine
+    handle (nmg_options.nb_gpus): the buffers of N per-GPU shards are staged
+    once, and a step is reset + nmg_analyze (every GPU analyses its
+    byte-balanced contiguous range, RCCL reduces the counters over xGMI into
+    GPU 0's handle) + the handle's per-buffer count gather.  Exits with status
+    2 when fewer than N GPUs are visible."""
+    import torch
+
+    from numamma_amd.engine import Engine
+    from numamma_amd.replay import SynthConfig, generate
+
+    n = args.gpus
+    visible = torch.cuda.device_count()
+    if visible < n:
+        log(f"error: --gpus {n} but {visible} GPU(s) visible")
+        sys.exit(2)
+    wl = WORKLOADS[args.workload]
+    cfg = SynthConfig(seed=1, sample_seed=1000, **{k: v for k, v in wl.items() if k != "desc"})
+    t0 = time.time()
+    rp = generate(cfg)
+    bufs = [b.linear() for b in rp.buffers]
+    shard = sum(x.nbytes for x in bufs) // RECORD_BYTES
+    log(f"[1 process, {n} GPUs] {args.workload}: shard of {shard} records in {len(bufs)} buffers, generated in "
+        f"{time.time() - t0:.1f}s; every GPU analyses one copy of it")
+    eng = Engine(devices=list(range(n)), nb_threads=rp.nb_threads, copy_threads=16)
+    eng.set_objects(rp.table)
+    subs = [(b.thread_rank, b.access_type, x) for b, x in zip(rp.buffers, bufs) if x.shape[0]]
+    for _ in range(n):  # N shards in analysis order; the handle cuts them into N byte-balanced ranges
+        eng.submit_buffers(subs)
+
+    class W:
+        def step(self):
+            eng.reset()
+            eng.analyze()
+
+    def barrier():
+        eng.synchronize()
+        for d in range(n):
+            torch.cuda.synchronize(d)
+
+    elapsed, steps = timed_run(W(), args.steps, args.warmup, barrier)
+    g, ns, nf = eng.global_counters()
+    assert ns == n * shard, (ns, n * shard)
+    ms_per_step = elapsed * 1e3 / steps
+    out = {
+        "metric": "PEBS samples/s analysed (device-resident)",
+        "value": n * shard / (elapsed / steps),
+        "unit": "samples/s",
+        "n_gpus": n,
+        "steps": steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u64",
+        "data": "synthetic (seeded SURVEY 8(d) generator); one per-GPU shard, analysed by every GPU",
+        "config": {"workload": f"{args.workload}: {wl['desc']}", "records_per_gpu": shard,
+                   "object_intervals": int(cfg.nb_intervals), "threads": rp.nb_threads,
+                   "parallelism": f"one process, nmg_options.nb_gpus={n}: buffers sharded over {n} GPUs, "
+                                  "RCCL reduce of the counters"},
+    }
+    print(json.dumps(out), flush=True)
+    eng.close()
 
 
 def result_line(args, w, world, steps, ms_per_step, value, attr_ms, total_ms):

@@ -55,6 +55,10 @@ extern "C" {
 #define NMG_F_PAGE_HIST 0x2      /* per-(object, page, thread) counts for callsite_counters_<id>.dat */
 #define NMG_F_OBJECT_LEVELS 0x4  /* per-object level buckets (count, sum) for callsite_summary_<id>.dat */
 #define NMG_F_SAMPLE_MATCHES 0x8 /* keep every SAMPLE record's match (object or none) for the dump modes */
+#define NMG_F_SINGLE_PASS 0x10   /* large tables (> 1023 keys): one attribution pass with global lookups instead of
+                                    the partition-first passes; same results.  Needed only for batches
+                                    with a great many SAMPLE records shorter than 40 B (garbage perf data), which
+                                    the partition-first path reports as NMG_ERR_CAPACITY */
 #define NMG_F_DEFAULT (NMG_F_MATCH_SAMPLES | NMG_F_PAGE_HIST)
 
 /* struct count, src/mem_analyzer.h:10-15 */

@@ -38,6 +38,7 @@ NMG_F_MATCH_SAMPLES = 0x1
 NMG_F_PAGE_HIST = 0x2
 NMG_F_OBJECT_LEVELS = 0x4
 NMG_F_SAMPLE_MATCHES = 0x8
+NMG_F_SINGLE_PASS = 0x10  # large tables: single-pass attribute_kernel instead of the partition-first passes
 NMG_F_DEFAULT = NMG_F_MATCH_SAMPLES | NMG_F_PAGE_HIST
 NMG_DUMP_CALLSITES, NMG_DUMP_ALL, NMG_DUMP_UNMATCHED = 0x1, 0x2, 0x4
 NMG_ARR_SUM64, NMG_ARR_MIN64, NMG_ARR_MAX64, NMG_ARR_HIST32 = range(4)

@@ -40,6 +40,16 @@ __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
   v += dpp0<0x143, 0xc>(v);  // row_bcast:31 into rows 2 and 3
   return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
 }
+// Inclusive prefix sum over the wave (DPP, the steps of wave_sum_u32)
+__device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t v) {
+  v += dpp0<0x111, 0xf>(v);  // row_shr:1
+  v += dpp0<0x112, 0xf>(v);  // row_shr:2
+  v += dpp0<0x114, 0xf>(v);  // row_shr:4
+  v += dpp0<0x118, 0xf>(v);  // row_shr:8
+  v += dpp0<0x142, 0xa>(v);  // row_bcast:15 into rows 1 and 3
+  v += dpp0<0x143, 0xc>(v);  // row_bcast:31 into rows 2 and 3
+  return v;
+}
 // Sum of per-lane weights; `big` (wave-uniform) = some weight >= 2^26, in
 // which case 64 lanes could overflow 32 bits and the u64 path is taken.
 __device__ __forceinline__ uint64_t wave_sum_w(uint64_t w, bool big) {
@@ -60,7 +70,7 @@ __device__ __forceinline__ uint32_t bucket_mask(uint32_t lvl) {
   return 0;
 }
 
-__device__ __forceinline__ void set_error(Params& p, uint64_t seq, uint32_t off, uint32_t code) {
+__device__ __forceinline__ void set_error(const Params& p, uint64_t seq, uint32_t off, uint32_t code) {
   uint64_t w = (seq << 40) | (uint64_t(off) << 8) | code;
   atomicMin(reinterpret_cast<unsigned long long*>(p.min64 + 36 + p.nb_entries),
             (unsigned long long)w);
@@ -98,7 +108,7 @@ __device__ __forceinline__ bool entry_match(uint4 a, uint4 b, uint64_t addr, uin
   return baddr <= addr && addr < bend && alloc <= ts && ts <= fr;
 }
 
-__device__ __forceinline__ void sparse_add(Params& p, uint64_t key, uint64_t seq, uint32_t off, uint32_t cnt) {
+__device__ __forceinline__ void sparse_add(const Params& p, uint64_t key, uint64_t seq, uint32_t off, uint32_t cnt) {
   *p.sparse_dirty = 1u;
   uint64_t h = (key * 0x9E3779B97F4A7C15ull) >> 20;
   uint32_t slot = uint32_t(h) & p.sparse_mask;
@@ -200,6 +210,51 @@ __device__ __forceinline__ void lane_acc_drain(LaneAcc& a, unsigned long long* s
   lane_acc_clear(a);
 }
 
+
+// update_counters(global_counters, sample) (mem_sampling.c:517-592) for one
+// SAMPLE of level field `lvl` and weight w: per-lane registers for the common
+// buckets, the workgroup's LDS words (sums [kGlobalSums], mins / maxs [18])
+// for the rest.
+__device__ __forceinline__ void global_count(LaneAcc& acc, unsigned long long* sums, unsigned long long* mins,
+                                             unsigned long long* maxs, uint32_t lvl, uint64_t w) {
+  const uint32_t bm = bucket_mask(lvl);
+  if (w < kLaneMaxWeight) {  // register accumulation (no LDS traffic)
+    const uint32_t w32 = (uint32_t)w;
+    acc.tc += 1;
+    acc.tw += w32;
+    acc.na += lvl & LVL_NA;
+#pragma unroll
+    for (int k = 0; k < (kRegGroups + 1) / 2; k++)
+      acc.cnt2[k] += ((bm >> (2 * k)) & 1) | ((2 * k + 1 < kRegGroups ? (bm >> (2 * k + 1)) & 1 : 0) << 16);
+#pragma unroll
+    for (int k = 0; k < kRegGroups; k++) acc.sum[k] += ((bm >> k) & 1) * w32;
+    for (uint32_t m = bm >> kRegGroups; m; m &= m - 1) {  // rarer hit buckets, miss buckets
+      const uint32_t b = kRegGroups + (uint32_t)__builtin_ctz(m);
+      atomicAdd(&sums[3 + 2 * b], 1ull);
+      if (w) atomicAdd(&sums[4 + 2 * b], (unsigned long long)w);
+    }
+  } else {  // weights >= 2^23 cycles: straight to the LDS counters
+    atomicAdd(&sums[0], 1ull);
+    atomicAdd(&sums[1], (unsigned long long)w);
+    if (lvl & LVL_NA) atomicAdd(&sums[2], 1ull);
+    for (uint32_t m = bm; m; m &= m - 1) {
+      const uint32_t b = (uint32_t)__builtin_ctz(m);
+      atomicAdd(&sums[3 + 2 * b], 1ull);
+      atomicAdd(&sums[4 + 2 * b], (unsigned long long)w);
+    }
+  }
+  // min / max only move monotonically: read first, atomic only on improvement
+  if (bm) {
+    const uint32_t b = (uint32_t)__builtin_ctz(bm);
+    if (w < mins[b]) atomicMin(&mins[b], (unsigned long long)w);
+    if (w > maxs[b]) atomicMax(&maxs[b], (unsigned long long)w);
+    for (uint32_t m = bm & (bm - 1); m; m &= m - 1) {  // several level groups (rare)
+      const uint32_t b2 = (uint32_t)__builtin_ctz(m);
+      if (w < mins[b2]) atomicMin(&mins[b2], (unsigned long long)w);
+      if (w > maxs[b2]) atomicMax(&maxs[b2], (unsigned long long)w);
+    }
+  }
+}
 
 // One long-tail object contribution of this workgroup (kTlogHead layouts,
 // nmg_kernels.h) to the sub-log of entry e's range; false when it is full

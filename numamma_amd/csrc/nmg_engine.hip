@@ -23,6 +23,7 @@
 #include <vector>
 
 #include "nmg_kernels.h"
+#include "nmg_route.h"
 
 // ===========================================================================
 // host side
@@ -207,6 +208,38 @@ struct nmg_engine {
   std::vector<uint8_t*> warena;
   std::vector<size_t> warena_cap;
 
+  // partition-first path for large tables (nmg_route.h): the partitions of
+  // the current table, and the per-analysis chunk pool
+  bool route_ok = false;          // partitions built for the nmg_set_objects table
+  uint32_t nparts = 0;
+  PartInfo* d_parts = nullptr;
+  uint64_t* d_pbounds = nullptr;  // [2^kPartLevels] partition starts, Eytzinger order
+  uint64_t* d_pe_keys = nullptr;  // [nparts][kPartSlots]
+  uint4* d_pe_nodes = nullptr;    // [nparts][kPartSlots][2]
+  uint2* d_pe_info = nullptr;     // [nparts][kPartSlots]
+  uint4* d_rec16 = nullptr;       // chunk pool: [chunks][kChunk] (addr, ts) and X words
+  unsigned long long* d_recx = nullptr;
+  uint32_t* d_cmeta = nullptr;
+  unsigned long long* d_cmatch = nullptr;
+  uint32_t* d_clist = nullptr;
+  size_t route_chunk_cap = 0;
+  uint4* d_items = nullptr;
+  size_t items_cap = 0;
+  uint32_t* d_chunk0 = nullptr;   // [grid + 1]
+  uint32_t* d_used = nullptr;     // [grid]
+  uint32_t* d_pcnt = nullptr;     // [grid][nparts]
+  uint32_t* d_pbase = nullptr;    // [nparts]
+  uint32_t* d_ctl = nullptr;      // [3] items, dequeue head, overflow records
+  uint4* d_ovf16 = nullptr;       // overflow list (route pass, pool exhausted)
+  unsigned long long* d_ovfx = nullptr;
+  size_t ovf_cap = 0;
+  size_t route_grid_cap = 0;
+  bool sched_route = false;       // d_sdescs / d_ranges hold the analysis-order schedule
+  uint32_t route_sched_key = 0;   // nparts (| tiny-pool switch) the pools were sized for
+  bool route_pending = false;     // per-buffer match counts of the last route analysis not yet summed
+  uint32_t route_grid = 0;
+  XLayout route_xl{};
+
   // kDbgTiming (internal): per-wave phase cycles of the last launch
   uint64_t* d_dbg = nullptr;
   size_t dbg_cap = 0, dbg_len = 0;
@@ -306,7 +339,93 @@ static void free_lookup(nmg_engine* h) {
   h->d_chain = nullptr;
 }
 
+// the partitions of the partition-first path (built with the table)
+static void free_route_table(nmg_engine* h) {
+  (void)hipFree(h->d_parts);
+  (void)hipFree(h->d_pbounds);
+  (void)hipFree(h->d_pe_keys);
+  (void)hipFree(h->d_pe_nodes);
+  (void)hipFree(h->d_pe_info);
+  h->d_parts = nullptr;
+  h->d_pbounds = nullptr;
+  h->d_pe_keys = nullptr;
+  h->d_pe_nodes = nullptr;
+  h->d_pe_info = nullptr;
+  h->route_ok = false;
+  h->nparts = 0;
+}
+
+// the per-analysis buffers of the partition-first path
+static void free_route_pool(nmg_engine* h) {
+  for (void* q : {(void*)h->d_rec16, (void*)h->d_recx, (void*)h->d_cmeta, (void*)h->d_cmatch, (void*)h->d_clist,
+                  (void*)h->d_items, (void*)h->d_chunk0, (void*)h->d_used, (void*)h->d_pcnt, (void*)h->d_pbase,
+                  (void*)h->d_ctl, (void*)h->d_ovf16, (void*)h->d_ovfx})
+    (void)hipFree(q);
+  h->d_rec16 = nullptr;
+  h->d_recx = nullptr;
+  h->d_cmeta = nullptr;
+  h->d_cmatch = nullptr;
+  h->d_clist = nullptr;
+  h->d_items = nullptr;
+  h->d_chunk0 = nullptr;
+  h->d_used = nullptr;
+  h->d_pcnt = nullptr;
+  h->d_pbase = nullptr;
+  h->d_ctl = nullptr;
+  h->d_ovf16 = nullptr;
+  h->d_ovfx = nullptr;
+  h->ovf_cap = 0;
+  h->route_chunk_cap = h->items_cap = h->route_grid_cap = 0;
+  h->route_pending = false;
+}
+
+// The lookup structures' pointers and shape, moved out of the engine so that
+// a new table can be built beside them (nmg_update_objects swaps only on
+// success).
+struct LookupSet {
+  uint64_t* keys;
+  DevEntry* nodes;
+  uint64_t* efences;
+  DevEntry* enodes;
+  uint64_t* ffences;
+  uint8_t* fshift;
+  uint2* dir;
+  DevEntry* chain;
+  uint32_t K, elevels, nb_fences, fence_log2, dir_log2;
+};
+
+static LookupSet take_lookup(nmg_engine* h) {
+  LookupSet l{h->d_keys, h->d_nodes, h->d_efences, h->d_enodes, h->d_ffences, h->d_fshift, h->d_dir, h->d_chain,
+              h->K, h->elevels, h->nb_fences, h->fence_log2, h->dir_log2};
+  h->d_keys = nullptr;
+  h->d_nodes = nullptr;
+  h->d_efences = nullptr;
+  h->d_enodes = nullptr;
+  h->d_ffences = nullptr;
+  h->d_fshift = nullptr;
+  h->d_dir = nullptr;
+  h->d_chain = nullptr;
+  return l;
+}
+
+static void put_lookup(nmg_engine* h, const LookupSet& l) {
+  h->d_keys = l.keys;
+  h->d_nodes = l.nodes;
+  h->d_efences = l.efences;
+  h->d_enodes = l.enodes;
+  h->d_ffences = l.ffences;
+  h->d_fshift = l.fshift;
+  h->d_dir = l.dir;
+  h->d_chain = l.chain;
+  h->K = l.K;
+  h->elevels = l.elevels;
+  h->nb_fences = l.nb_fences;
+  h->fence_log2 = l.fence_log2;
+  h->dir_log2 = l.dir_log2;
+}
+
 static void free_table(nmg_engine* h) {
+  free_route_table(h);
   free_lookup(h);
   (void)hipFree(h->d_entries);
   h->d_entries = nullptr;
@@ -340,7 +459,7 @@ extern "C" int nmg_create(nmg_engine** out, const nmg_options* opt) {
   nmg_engine* h = new (std::nothrow) nmg_engine();
   if (!h) return NMG_ERR_NOMEM;
   if (opt) {
-    h->device = opt->nb_gpus > 1 && opt->devices ? opt->devices[0] : opt->device;
+    h->device = opt->nb_gpus >= 1 && opt->devices ? opt->devices[0] : opt->device;
     h->flags = opt->flags;
     h->T = opt->nb_threads ? opt->nb_threads : 1;
     h->copy_threads = opt->copy_threads ? opt->copy_threads : 1;
@@ -382,7 +501,7 @@ extern "C" int nmg_create(nmg_engine** out, const nmg_options* opt) {
   }
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, h->device) == hipSuccess) h->num_cus = prop.multiProcessorCount;
-  if (opt && opt->nb_gpus > 1) {
+  if (opt && (opt->nb_gpus > 1 || (opt->flags & kDbgMultiRccl))) {
     const int rc = multi_create(h, opt);
     if (rc) {
       g_create_error = h->last_error;
@@ -401,6 +520,7 @@ extern "C" void nmg_destroy(nmg_engine* h) {
   if (h->stream) (void)hipStreamSynchronize(h->stream);
   free_table(h);
   free_counters(h);
+  free_route_pool(h);
   (void)hipFree(h->d_arena);
   (void)hipFree(h->d_descs);
   (void)hipFree(h->d_bufcnt);
@@ -430,14 +550,25 @@ extern "C" void nmg_destroy(nmg_engine* h) {
   delete h;
 }
 
+static int multi_finish(nmg_engine* h);
+
 extern "C" int nmg_reset_counters(nmg_engine* h) {
   if (!h) return NMG_ERR_INVALID;
   if (!h->have_table) return fail(h, NMG_ERR_STATE, "nmg_reset_counters before nmg_set_objects");
+  if (h->multi_pending) {  // the merges in flight belong to the counters being reset
+    const int rc = multi_finish(h);
+    if (rc) return rc;
+  }
   for (nmg_engine* w : h->workers) {
     const int rc = nmg_reset_counters(w);
     if (rc) return fail(h, rc, w->last_error);
   }
+  if (h->multi && h->counts_override) {  // merged per-buffer counts (multi_finish)
+    std::fill(h->ov_samples.begin(), h->ov_samples.end(), 0u);
+    std::fill(h->ov_found.begin(), h->ov_found.end(), 0u);
+  }
   HIP_TRY(h, hipSetDevice(h->device));
+  h->route_pending = false;  // the counts found_kernel would add are zeroed here
   ResetParams r;
   memset(&r, 0, sizeof(r));
   r.sum64 = h->d_sum64;
@@ -597,6 +728,108 @@ static int build_lookup(nmg_engine* h, const uint64_t* keys, const uint32_t* ent
   return NMG_OK;
 }
 
+// In-order walk of the complete Eytzinger tree with 2^levels - 1 nodes:
+// visit(slot, rank) for every slot in sorted order.
+template <class F>
+static void eytz_inorder(uint32_t levels, F visit) {
+  const uint32_t n = 1u << levels;
+  std::vector<uint32_t> stack;
+  uint32_t r = 0, i = 1;
+  while (i < n || !stack.empty()) {
+    while (i < n) {
+      stack.push_back(i);
+      i = 2 * i;
+    }
+    i = stack.back();
+    stack.pop_back();
+    visit(i, r++);
+    i = 2 * i + 1;
+  }
+}
+
+// Partitions of the partition-first path (nmg_route.h): runs of consecutive
+// keys, each at most kPartKeys keys and kPartEntries entries, and -- where
+// the keys allow it -- at most kPartCells dense page cells over all threads,
+// so that a partition's lookup tree, node records, object counters and page
+// cells fit one workgroup's LDS.  Only for the offline table (entry id =
+// table position, so a key range owns an id range) of engines that count
+// per object (NMG_F_MATCH_SAMPLES) without the dump modes' per-sample
+// output or per-object levels; otherwise the table keeps attribute_kernel.
+static int build_partitions(nmg_engine* h, const uint64_t* keys, const uint32_t* entry_off, uint32_t K,
+                            const std::vector<DevEntry>& dev) {
+  free_route_table(h);
+  if (K <= kLdsNodes || !(h->flags & NMG_F_MATCH_SAMPLES) || (h->flags & (NMG_F_SAMPLE_MATCHES | NMG_F_OBJECT_LEVELS)))
+    return NMG_OK;
+  const uint64_t T = h->T;
+  std::vector<PartInfo> parts;
+  uint32_t k = 0;
+  while (k < K) {
+    PartInfo pi;
+    memset(&pi, 0, sizeof(pi));
+    pi.k0 = k;
+    pi.e0 = entry_off[k];
+    uint64_t cb = ~0ull, ce = 0;
+    while (k < K && k - pi.k0 < kPartKeys) {
+      const uint32_t ea = entry_off[k], eb = entry_off[k + 1];
+      if (eb - pi.e0 > kPartEntries) {
+        if (k == pi.k0) return NMG_OK;  // one address reused more than kPartEntries times: keep attribute_kernel
+        break;
+      }
+      uint64_t ncb = cb, nce = ce;
+      for (uint32_t e = ea; e < eb; e++)
+        if (dev[e].hist != kHistSparse) {
+          ncb = std::min<uint64_t>(ncb, dev[e].hist);
+          nce = std::max<uint64_t>(nce, dev[e].hist + h->npages[e]);
+        }
+      if (k > pi.k0 && ncb != ~0ull && (nce - ncb) * T > kPartCells) break;  // (one key alone may exceed: global cells)
+      cb = ncb;
+      ce = nce;
+      k++;
+    }
+    pi.nk = k - pi.k0;
+    pi.ne = entry_off[k] - pi.e0;
+    pi.cb = cb == ~0ull ? 0 : cb;
+    pi.span = cb == ~0ull ? 0 : (uint32_t)(ce - cb);
+    pi.pages_lds = pi.span && (uint64_t)pi.span * T <= kPartCells;
+    while (((1u << pi.levels) - 1) < pi.nk) pi.levels++;
+    parts.push_back(pi);
+    if (parts.size() > kMaxParts) return NMG_OK;  // too many partitions for the route pass's LDS tree
+  }
+  const uint32_t P = (uint32_t)parts.size();
+  // per partition: keys, newest-entry node records and info in Eytzinger order;
+  // slots past the last key hold ~0 keys with a copy of the last node
+  std::vector<uint64_t> pk((size_t)P * kPartSlots, ~0ull);
+  std::vector<uint4> pn((size_t)P * kPartSlots * 2, make_uint4(0, 0, 0, 0));
+  std::vector<uint2> pinf((size_t)P * kPartSlots, make_uint2(kEmpty32, 0));
+  for (uint32_t q = 0; q < P; q++) {
+    const PartInfo& pi = parts[q];
+    eytz_inorder(pi.levels, [&](uint32_t slot, uint32_t r) {
+      const uint32_t kk = pi.k0 + std::min(r, pi.nk - 1);
+      const DevEntry& d = dev[entry_off[kk]];
+      const size_t o = (size_t)q * kPartSlots + slot;
+      pk[o] = r < pi.nk ? keys[kk] : ~0ull;
+      pn[2 * o] = make_uint4((uint32_t)d.addr, (uint32_t)(d.addr >> 32), (uint32_t)d.end, (uint32_t)(d.end >> 32));
+      pn[2 * o + 1] = make_uint4((uint32_t)d.alloc, (uint32_t)(d.alloc >> 32), (uint32_t)d.free, (uint32_t)(d.free >> 32));
+      const uint32_t older = entry_off[kk + 1] - entry_off[kk] > 1 ? 0x80000000u : 0u;
+      pinf[o] = make_uint2(d.hist == kHistSparse ? kEmpty32 : (uint32_t)(d.hist - pi.cb), (entry_off[kk] - pi.e0) | older);
+    });
+  }
+  // the route pass's tree: the partitions' first keys
+  std::vector<uint64_t> pb(1u << kPartLevels, ~0ull);
+  eytz_inorder(kPartLevels, [&](uint32_t slot, uint32_t r) {
+    if (r < P) pb[slot] = keys[parts[r].k0];
+  });
+  HIP_TRY(h, alloc_copy(h, (void**)&h->d_parts, parts.data(), parts.size() * sizeof(PartInfo)));
+  HIP_TRY(h, alloc_copy(h, (void**)&h->d_pbounds, pb.data(), pb.size() * 8));
+  HIP_TRY(h, alloc_copy(h, (void**)&h->d_pe_keys, pk.data(), pk.size() * 8));
+  HIP_TRY(h, alloc_copy(h, (void**)&h->d_pe_nodes, pn.data(), pn.size() * sizeof(uint4)));
+  HIP_TRY(h, alloc_copy(h, (void**)&h->d_pe_info, pinf.data(), pinf.size() * sizeof(uint2)));
+  HIP_TRY(h, hipStreamSynchronize(h->stream));  // (pageable sources)
+  h->nparts = P;
+  h->route_ok = true;
+  return NMG_OK;
+}
+
 extern "C" int nmg_set_objects(nmg_engine* h, const uint64_t* keys, const uint32_t* entry_off,
                                uint32_t nb_keys, const nmg_object* entries, uint32_t nb_entries) {
   Range range("nmg_set_objects");
@@ -657,6 +890,8 @@ extern "C" int nmg_set_objects(nmg_engine* h, const uint64_t* keys, const uint32
   HIP_TRY(h, alloc_copy(h, (void**)&h->d_entries, dev.data(), (size_t)nb_entries * sizeof(DevEntry)));
   rc = build_lookup(h, keys, entry_off, nb_keys, dev, h->d_entries);
   if (rc) return rc;
+  rc = build_partitions(h, keys, entry_off, nb_keys, dev);
+  if (rc) return rc;
   h->dev_entries = std::move(dev);
 
 
@@ -691,6 +926,7 @@ extern "C" int nmg_set_objects(nmg_engine* h, const uint64_t* keys, const uint32
 }
 
 static int stream_flush(nmg_engine* h);
+static int route_settle(nmg_engine* h);
 
 // --online-analysis: the table at an alarm (entries by their set_objects
 // ids), counters kept (mem_sampling.c:953-954 against the live mem_list)
@@ -722,11 +958,27 @@ extern "C" int nmg_update_objects(nmg_engine* h, const uint64_t* keys, const uin
     rc = stream_flush(h);
     if (rc) return rc;
   }
-  HIP_TRY(h, hipStreamSynchronize(h->stream));  // launches in flight read the old table
-  free_lookup(h);
-  rc = build_lookup(h, keys, entry_off, nb_keys, chain, nullptr);
+  rc = route_settle(h);  // (reads the pool only, not the table)
   if (rc) return rc;
-  HIP_TRY(h, hipStreamSynchronize(h->stream));
+  HIP_TRY(h, hipStreamSynchronize(h->stream));  // launches in flight read the old table
+  free_route_table(h);  // (the partitions describe the nmg_set_objects table)
+  // build the alarm's lookup beside the current one; keep the current one if that fails
+  const LookupSet prev = take_lookup(h);
+  rc = build_lookup(h, keys, entry_off, nb_keys, chain, nullptr);
+  if (rc == NMG_OK && hipStreamSynchronize(h->stream) != hipSuccess)
+    rc = fail(h, NMG_ERR_HIP, "nmg_update_objects: table upload failed");
+  if (rc) {
+    (void)hipStreamSynchronize(h->stream);
+    free_lookup(h);
+    put_lookup(h, prev);
+    return rc;
+  }
+  {
+    const LookupSet cur = take_lookup(h);
+    put_lookup(h, prev);
+    free_lookup(h);  // (keeps d_chain when it is the by-id entry array)
+    put_lookup(h, cur);
+  }
   for (nmg_engine* w : h->workers) {  // multi-GPU: the table on every device
     rc = nmg_update_objects(w, keys, entry_off, nb_keys, entry_ids, objects);
     if (rc) return fail(h, rc, w->last_error);
@@ -787,10 +1039,14 @@ static int stream_dst(nmg_engine* h, uint64_t len, uint8_t** dst, std::vector<Co
 static void ensure_occupancy(nmg_engine* h);
 static uint32_t attribution_grid(nmg_engine* h, uint32_t nb);
 static void make_schedule(const std::vector<BufDesc>& descs, uint32_t grid, uint32_t index_base, BufDesc* sorted,
-                          uint32_t* ranges);
+                          uint32_t* ranges, bool by_stream = true);
 static int launch_attribution(nmg_engine* h, const uint8_t* data, const BufDesc* sdescs, const uint32_t* ranges,
                               uint32_t nb, uint32_t grid, uint64_t nbytes);
 static int stream_append(nmg_engine* h, uint64_t len, uint32_t thread_rank, uint32_t access);
+static bool route_eligible(nmg_engine* h);
+static int route_prepare(nmg_engine* h, uint32_t grid, const std::vector<uint32_t>& ranges);
+static int route_analyze(nmg_engine* h, uint32_t nb, uint32_t grid);
+static int route_settle(nmg_engine* h);
 
 extern "C" int nmg_submit_buffer(nmg_engine* h, const void* bytes, uint64_t len, uint32_t thread_rank,
                                  uint32_t access_type) {
@@ -1112,6 +1368,10 @@ extern "C" int nmg_set_device_buffers(nmg_engine* h, const void* d_data, const u
 
 extern "C" int nmg_clear_buffers(nmg_engine* h) {
   if (!h) return NMG_ERR_INVALID;
+  if (h->route_pending) {
+    const int rc = route_settle(h);
+    if (rc) return rc;
+  }
   if (h->streaming || h->streamed) {
     HIP_TRY(h, hipSetDevice(h->device));
     HIP_TRY(h, hipStreamSynchronize(h->stream));
@@ -1182,11 +1442,11 @@ static int upload_buffers(nmg_engine* h) {
 // buffer's position in `descs` (its per-buffer count slot), `ranges` = grid + 1
 // cut points of about equal bytes.
 static void make_schedule(const std::vector<BufDesc>& descs, uint32_t grid, uint32_t index_base, BufDesc* sorted,
-                          uint32_t* ranges) {
+                          uint32_t* ranges, bool by_stream) {
   const uint32_t nb = (uint32_t)descs.size();
   std::vector<uint32_t> order(nb);
   for (uint32_t i = 0; i < nb; i++) order[i] = i;
-  std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) {
+  if (by_stream) std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) {
     const BufDesc &x = descs[a], &y = descs[b];
     if (x.access != y.access) return x.access < y.access;
     return x.thread_rank < y.thread_rank;
@@ -1206,11 +1466,13 @@ static void make_schedule(const std::vector<BufDesc>& descs, uint32_t grid, uint
   }
 }
 
-static int build_schedule(nmg_engine* h, uint32_t grid) {
+// by_stream: sorted by (access, thread) for attribute_kernel's per-stream
+// tables; otherwise analysis order (the partition-first route pass)
+static int build_schedule(nmg_engine* h, uint32_t grid, bool by_stream = true) {
   const uint32_t nb = (uint32_t)h->descs.size();
   std::vector<uint32_t> ranges(grid + 1, 0);
   std::vector<BufDesc> sorted(nb);
-  make_schedule(h->descs, grid, 0, sorted.data(), ranges.data());
+  make_schedule(h->descs, grid, 0, sorted.data(), ranges.data(), by_stream);
   (void)hipFree(h->d_sdescs);
   (void)hipFree(h->d_ranges);
   h->d_sdescs = nullptr;
@@ -1220,6 +1482,8 @@ static int build_schedule(nmg_engine* h, uint32_t grid) {
   if (nb) HIP_TRY(h, hipMemcpy(h->d_sdescs, sorted.data(), nb * sizeof(BufDesc), hipMemcpyHostToDevice));
   HIP_TRY(h, hipMemcpy(h->d_ranges, ranges.data(), (grid + 1) * 4, hipMemcpyHostToDevice));
   h->sched_grid = grid;
+  h->sched_route = !by_stream;
+  if (!by_stream) return route_prepare(h, grid, ranges);
   return NMG_OK;
 }
 
@@ -1238,9 +1502,8 @@ static uint32_t attribution_grid(nmg_engine* h, uint32_t nb) {
 // One attribution launch over `nb` buffers whose stream-sorted descriptors and
 // per-workgroup ranges are already on the device, on the engine stream,
 // bracketed by the launch-timing events.
-static int launch_attribution(nmg_engine* h, const uint8_t* data, const BufDesc* sdescs, const uint32_t* ranges,
-                              uint32_t nb, uint32_t grid, uint64_t nbytes) {
-  Range range("nmg_attribute");
+// The kernels' view of the engine: buffers, table, counters.
+static Params base_params(nmg_engine* h, const uint8_t* data, const BufDesc* sdescs, const uint32_t* ranges) {
   Params p;
   memset(&p, 0, sizeof(p));
   p.data = data;
@@ -1276,6 +1539,25 @@ static int launch_attribution(nmg_engine* h, const uint8_t* data, const BufDesc*
   p.sparse_vals = h->d_sparse_vals;
   p.sparse_dirty = h->d_sparse_dirty ? h->d_sparse_dirty + (h->nreset & 1) : nullptr;
   p.smatch = (h->flags & NMG_F_SAMPLE_MATCHES) ? h->d_smatch : nullptr;
+  return p;
+}
+
+// timing events of launch slot nlaunch % kRing (created on first use)
+static int launch_events(nmg_engine* h, int* slot_out) {
+  const int slot = (int)(h->nlaunch % nmg_engine::kRing);
+  if (!h->ring0[slot]) {
+    HIP_TRY(h, hipEventCreate(&h->ring0[slot]));
+    HIP_TRY(h, hipEventCreate(&h->ringm[slot]));
+    HIP_TRY(h, hipEventCreate(&h->ring1[slot]));
+  }
+  *slot_out = slot;
+  return NMG_OK;
+}
+
+static int launch_attribution(nmg_engine* h, const uint8_t* data, const BufDesc* sdescs, const uint32_t* ranges,
+                              uint32_t nb, uint32_t grid, uint64_t nbytes) {
+  Range range("nmg_attribute");
+  Params p = base_params(h, data, sdescs, ranges);
   // dense LDS tables when the table is small enough (DESIGN.md "Kernels");
   // large tables: their own kernel instances (fences + directory + node records)
   const int mode = (h->E <= kObjSlots ? kModeDenseObj : 0) | (h->hist_cells <= kDensePageCells ? kModeDensePage : 0) |
@@ -1326,12 +1608,9 @@ static int launch_attribution(nmg_engine* h, const uint8_t* data, const BufDesc*
     p.tlog_rshift = rshift;
     p.tlog_parts = parts;
   }
-  const int slot = (int)(h->nlaunch % nmg_engine::kRing);
-  if (!h->ring0[slot]) {
-    HIP_TRY(h, hipEventCreate(&h->ring0[slot]));
-    HIP_TRY(h, hipEventCreate(&h->ringm[slot]));
-    HIP_TRY(h, hipEventCreate(&h->ring1[slot]));
-  }
+  int slot = 0;
+  int rc = launch_events(h, &slot);
+  if (rc) return rc;
   HIP_TRY(h, hipEventRecord(h->ring0[slot], h->stream));
   if (nb) {
     if (h->flags & kDbgTiming) {
@@ -1376,6 +1655,209 @@ static int launch_attribution(nmg_engine* h, const uint8_t* data, const BufDesc*
   return NMG_OK;
 }
 
+// ---------------------------------------------------------------------------
+// partition-first path (nmg_route.h): eligibility, pool sizing, launches
+
+static uint32_t bits_for(uint64_t v) {  // smallest b with v < 2^b
+  uint32_t b = 0;
+  while (b < 64 && (v >> b) != 0) b++;
+  return b;
+}
+
+// X word layout of the current buffers; false when the weight field would
+// be narrower than 16 bits (escapes would be common)
+static bool route_layout(nmg_engine* h, XLayout& xl) {
+  uint64_t maxlen = 1;
+  for (const BufDesc& d : h->descs) maxlen = std::max<uint64_t>(maxlen, d.len);
+  xl.gbits = bits_for(h->descs.size() - 1);
+  xl.obits = bits_for((maxlen - 1) / 8);
+  xl.tbits = bits_for(h->T - 1);
+  xl.wshift = xl.gbits + xl.obits + xl.tbits + 1;
+  if (xl.wshift > 64 - 16) return false;
+  xl.wesc = (1ull << (64 - xl.wshift)) - 1;
+  return true;
+}
+
+static bool route_eligible(nmg_engine* h) {
+  constexpr uint32_t kLegacyOnly = kDbgLoadOnly | kDbgNoGlobal | kDbgNoFlush | kDbgNoTables | kDbgTiming |
+                                   kDbgTinyLog | kDbgNoPack | kDbgNoDir | kDbgNoRoute | NMG_F_SINGLE_PASS;
+  if (!h->route_ok || (h->flags & kLegacyOnly) || h->descs.empty()) return false;
+  // the first-match ordinal is rebuilt from the buffer index: seq = seq0 + index
+  uint64_t bytes = 0;
+  for (size_t i = 0; i < h->descs.size(); i++) {
+    if (h->descs[i].seq != h->descs[0].seq + i) return false;
+    bytes += h->descs[i].len;
+  }
+  // chunk ids (route pass LDS: id << 7 | fill) -- an upper bound of the pool
+  const uint64_t chunks = (bytes / kRecBytes + h->descs.size()) / kChunk + (uint64_t)h->num_cus * (h->nparts + 2);
+  if (chunks >= (1ull << kChunkIdBits)) return false;
+  XLayout xl;
+  return route_layout(h, xl);
+}
+
+// per-workgroup private chunk pools for a new schedule: every SAMPLE record
+// of at least 40 B fits (a partition's chunks are full but for its one open
+// chunk); shorter records past that are attributed directly
+static int route_prepare(nmg_engine* h, uint32_t grid, const std::vector<uint32_t>& ranges) {
+  const uint32_t P = h->nparts;
+  std::vector<uint32_t> c0(grid + 1, 0);
+  uint64_t tot = 0;
+  for (uint32_t w = 0; w < grid; w++) {
+    uint64_t rec = 0;
+    for (uint32_t b = ranges[w]; b < ranges[w + 1]; b++) rec += (h->descs[b].len + kRecBytes - 1) / kRecBytes;
+    const uint64_t cap = (h->flags & kDbgTinyPool) ? 2 : (rec + kChunk - 1) / kChunk + P;
+    c0[w] = (uint32_t)tot;
+    tot += cap;
+  }
+  c0[grid] = (uint32_t)tot;
+  if (tot >= (1ull << kChunkIdBits)) return fail(h, NMG_ERR_RANGE, "partition-first chunk pool too large");
+  const size_t items = tot / kItemChunks + P + 1;
+  // overflow list: records past a full pool (only SAMPLE records shorter than
+  // 40 B can get there; kDbgTinyPool sends nearly all of them)
+  uint64_t recs = 0;
+  for (const BufDesc& d : h->descs) recs += (d.len + kRecBytes - 1) / kRecBytes;
+  // (a quarter of the records, plus up to three times them for batches under 4M records)
+  const size_t ovf = (size_t)((h->flags & kDbgTinyPool) ? recs : recs / 4 + std::min<uint64_t>(3 * recs, 4u << 20)) + 65536;
+  if (tot > h->route_chunk_cap || items > h->items_cap || grid > h->route_grid_cap || ovf > h->ovf_cap) {
+    HIP_TRY(h, hipStreamSynchronize(h->stream));  // a launch in flight may still read the old pool
+    const bool pending = h->route_pending;
+    free_route_pool(h);
+    h->route_pending = pending;
+    const size_t cap = std::max<size_t>(tot, 1);
+    HIP_TRY(h, hipMalloc(&h->d_rec16, cap * kChunk * sizeof(uint4)));
+    HIP_TRY(h, hipMalloc(&h->d_recx, cap * kChunk * 8));
+    HIP_TRY(h, hipMalloc(&h->d_cmeta, cap * 4));
+    HIP_TRY(h, hipMalloc(&h->d_cmatch, cap * 8));
+    HIP_TRY(h, hipMalloc(&h->d_clist, cap * 4));
+    HIP_TRY(h, hipMalloc(&h->d_items, items * sizeof(uint4)));
+    HIP_TRY(h, hipMalloc(&h->d_chunk0, (grid + 1) * 4));
+    HIP_TRY(h, hipMalloc(&h->d_used, grid * 4));
+    HIP_TRY(h, hipMalloc(&h->d_pcnt, (size_t)grid * (kMaxParts + 1) * 4));
+    HIP_TRY(h, hipMalloc(&h->d_pbase, (kMaxParts + 1) * 4));
+    HIP_TRY(h, hipMalloc(&h->d_ctl, 3 * 4));
+    HIP_TRY(h, hipMemset(h->d_ctl, 0, 3 * 4));
+    HIP_TRY(h, hipMalloc(&h->d_ovf16, ovf * sizeof(uint4)));
+    HIP_TRY(h, hipMalloc(&h->d_ovfx, ovf * 8));
+    h->ovf_cap = ovf;
+    h->route_chunk_cap = cap;
+    h->items_cap = items;
+    h->route_grid_cap = grid;
+  }
+  HIP_TRY(h, hipMemcpy(h->d_chunk0, c0.data(), (grid + 1) * 4, hipMemcpyHostToDevice));
+  h->route_sched_key = P | ((h->flags & kDbgTinyPool) ? 0x80000000u : 0u);
+  return NMG_OK;
+}
+
+// Route -> plan -> scatter -> local over the buffers of the current schedule
+// (analysis order), bracketed by the launch-timing events.
+static int route_analyze(nmg_engine* h, uint32_t nb, uint32_t grid) {
+  Range range("nmg_route");
+  XLayout xl;
+  if (!route_layout(h, xl)) return fail(h, NMG_ERR_STATE, "route layout");
+  const Params base = base_params(h, h->d_data, h->d_sdescs, h->d_ranges);
+  const uint64_t seq0 = h->descs[0].seq;
+  int slot = 0;
+  int rc = launch_events(h, &slot);
+  if (rc) return rc;
+  HIP_TRY(h, hipEventRecord(h->ring0[slot], h->stream));
+  RouteParams rp;
+  memset(&rp, 0, sizeof(rp));
+  rp.p = base;
+  rp.pbounds = h->d_pbounds;
+  rp.nparts = h->nparts;
+  rp.xl = xl;
+  rp.seq0 = seq0;
+  rp.rec16 = h->d_rec16;
+  rp.recx = h->d_recx;
+  rp.cmeta = h->d_cmeta;
+  rp.chunk0 = h->d_chunk0;
+  rp.used = h->d_used;
+  rp.ovf16 = h->d_ovf16;
+  rp.ovfx = h->d_ovfx;
+  rp.ovf_cnt = h->d_ctl + 2;
+  rp.ovf_cap = (uint32_t)std::min<size_t>(h->ovf_cap, 0xffffffffu);
+  if (h->flags & kDbgRouteTiming) {  // (internal) per-wave phase cycles, read by nmg_debug_timing
+    const size_t n = (size_t)grid * (kWG / 64) * kRouteTimingWords;
+    if (n > h->dbg_cap) {
+      (void)hipFree(h->d_dbg);
+      h->d_dbg = nullptr;
+      HIP_TRY(h, hipMalloc(&h->d_dbg, n * 8));
+      h->dbg_cap = n;
+    }
+    HIP_TRY(h, hipMemsetAsync(h->d_dbg, 0, n * 8, h->stream));
+    h->dbg_len = n;
+    rp.p.dbg = reinterpret_cast<unsigned long long*>(h->d_dbg);
+  }
+  HIP_TRY(h, launch_route(grid, h->stream, rp));
+  HIP_TRY(h, launch_overflow(h->stream, rp));
+  ScatterParams sc;
+  sc.cmeta = h->d_cmeta;
+  sc.chunk0 = h->d_chunk0;
+  sc.used = h->d_used;
+  sc.pcnt = h->d_pcnt;
+  sc.pbase = h->d_pbase;
+  sc.clist = h->d_clist;
+  sc.nparts = h->nparts;
+  HIP_TRY(h, launch_count(grid, h->stream, sc));
+  PlanParams pl;
+  pl.pcnt = h->d_pcnt;
+  pl.pbase = h->d_pbase;
+  pl.items = h->d_items;
+  pl.ctl = h->d_ctl;
+  pl.grid = grid;
+  pl.nparts = h->nparts;
+  HIP_TRY(h, launch_plan(h->stream, pl));
+  HIP_TRY(h, launch_scatter(grid, h->stream, sc));
+  LocalParams lp;
+  memset(&lp, 0, sizeof(lp));
+  lp.p = base;
+  lp.parts = h->d_parts;
+  lp.pe_keys = h->d_pe_keys;
+  lp.pe_nodes = h->d_pe_nodes;
+  lp.pe_info = h->d_pe_info;
+  lp.rec16 = h->d_rec16;
+  lp.recx = h->d_recx;
+  lp.cmeta = h->d_cmeta;
+  lp.clist = h->d_clist;
+  lp.items = h->d_items;
+  lp.ctl = h->d_ctl;
+  lp.cmatch = h->d_cmatch;
+  lp.descs = h->d_sdescs;
+  lp.xl = xl;
+  lp.seq0 = seq0;
+  HIP_TRY(h, launch_local((uint32_t)h->num_cus, h->stream, lp));
+  HIP_TRY(h, hipEventRecord(h->ringm[slot], h->stream));
+  HIP_TRY(h, hipEventRecord(h->ring1[slot], h->stream));
+  h->nlaunch++;
+  h->launched = true;
+  h->route_pending = true;
+  h->route_grid = grid;
+  h->route_xl = xl;
+  (void)nb;
+  return NMG_OK;
+}
+
+// Per-buffer matched-sample counts of the last route analysis (found_kernel),
+// enqueued before anything reads or replaces them.  A reset drops them
+// instead: it zeroes those counts anyway.
+static int route_settle(nmg_engine* h) {
+  if (!h->route_pending) return NMG_OK;
+  h->route_pending = false;
+  FoundParams f;
+  f.ranges = h->d_ranges;
+  f.chunk0 = h->d_chunk0;
+  f.used = h->d_used;
+  f.cmeta = h->d_cmeta;
+  f.cmatch = h->d_cmatch;
+  f.recx = h->d_recx;
+  f.bufcnt = h->d_bufcnt;
+  f.nb_bufs = (uint32_t)h->bufcnt_stride;
+  f.gbits = h->route_xl.gbits;
+  HIP_TRY(h, hipSetDevice(h->device));
+  HIP_TRY(h, launch_found(h->route_grid, h->stream, f));
+  return NMG_OK;
+}
+
 static int stream_flush(nmg_engine* h);
 
 static int multi_analyze(nmg_engine* h);
@@ -1387,10 +1869,12 @@ extern "C" int nmg_analyze(nmg_engine* h) {
   if (!h->have_table) return fail(h, NMG_ERR_STATE, "nmg_analyze before nmg_set_objects");
   if (h->multi) return multi_analyze(h);
   HIP_TRY(h, hipSetDevice(h->device));
+  int rc = route_settle(h);  // the previous analysis' per-buffer counts, before the pool is reused
+  if (rc) return rc;
   if (h->streaming) return stream_flush(h);  // earlier chunks are already enqueued
   if (h->streamed) return NMG_OK;             // nmg_stream_end flushed everything
   const bool resched = h->descs_dirty;
-  int rc = upload_buffers(h);
+  rc = upload_buffers(h);
   if (rc) return rc;
   const uint32_t nb = (uint32_t)h->descs.size();
   if (h->flags & NMG_F_SAMPLE_MATCHES) {  // one u32 per 8 B of the buffers' arena span
@@ -1406,7 +1890,15 @@ extern "C" int nmg_analyze(nmg_engine* h) {
     }
   }
   const uint32_t grid = attribution_grid(h, nb);
-  if (nb && (resched || grid != h->sched_grid)) {
+  if (route_eligible(h)) {
+    if (nb && (resched || grid != h->sched_grid || !h->sched_route ||
+               h->route_sched_key != (h->nparts | ((h->flags & kDbgTinyPool) ? 0x80000000u : 0u)))) {
+      rc = build_schedule(h, grid, false);
+      if (rc) return rc;
+    }
+    return route_analyze(h, nb, grid);
+  }
+  if (nb && (resched || grid != h->sched_grid || h->sched_route)) {
     rc = build_schedule(h, grid);
     if (rc) return rc;
   }
@@ -1427,6 +1919,9 @@ static int decode_error_word(nmg_engine* h, uint64_t w) {
     case kErrTruncated: return fail(h, NMG_ERR_TRUNCATED, std::string(msg) + "truncated record");
     case kErrUnaligned: return fail(h, NMG_ERR_UNALIGNED, std::string(msg) + "unaligned record");
     case kErrCapacity: return fail(h, NMG_ERR_CAPACITY, std::string(msg) + "sparse table full");
+    case kErrRouteOverflow:
+      return fail(h, NMG_ERR_CAPACITY, std::string(msg) + "too many SAMPLE records shorter than 40 B for the "
+                  "partition-first overflow list (use NMG_F_SINGLE_PASS)");
     default: return fail(h, NMG_ERR_RANGE, std::string(msg) + "range error");
   }
 }
@@ -1438,6 +1933,8 @@ extern "C" int nmg_synchronize(nmg_engine* h) {
     if (rc) return rc;
   }
   HIP_TRY(h, hipSetDevice(h->device));
+  const int src = route_settle(h);
+  if (src) return src;
   HIP_TRY(h, hipStreamSynchronize(h->stream));
   if (h->launched) {  // the most recent launch's start / end events
     const int slot = (int)((h->nlaunch - 1) % nmg_engine::kRing);
@@ -1605,13 +2102,18 @@ extern "C" int nmg_get_object_levels(nmg_engine* h, uint64_t* levels) {
   return NMG_OK;
 }
 
+static int sparse_nonempty(nmg_engine* h, bool* out);
+
 static int collect_page_cells(nmg_engine* h, std::vector<uint32_t>* rows, int64_t* count) {
   std::vector<uint32_t> cells;
   int rc = engine_download_hist(h, cells);
   if (rc) return rc;
   // sparse cells grouped per entry
   std::vector<std::vector<std::pair<uint64_t, uint32_t>>> sparse(h->sparse_entries.size());
-  if (h->d_sparse_keys) {
+  bool any_sparse = false;
+  rc = sparse_nonempty(h, &any_sparse);
+  if (rc) return rc;
+  if (any_sparse) {
     std::vector<uint64_t> k(h->sparse_cap);
     std::vector<uint32_t> v(h->sparse_cap);
     HIP_TRY(h, hipMemcpy(k.data(), h->d_sparse_keys, h->sparse_cap * 8, hipMemcpyDeviceToHost));
@@ -1725,10 +2227,26 @@ extern "C" int nmg_import_array(nmg_engine* h, int which, const void* d_src) {
   return NMG_OK;
 }
 
+// The sparse cells can be non-empty only when something was inserted (or
+// imported) since the last reset: that reset cleared the table if it had been
+// written, and the flag of the analyses after it is d_sparse_dirty[nreset & 1]
+// (reset_kernel).  A 4-byte read instead of the whole table.
+static int sparse_nonempty(nmg_engine* h, bool* out) {
+  *out = false;
+  if (!h->d_sparse_keys) return NMG_OK;
+  uint32_t dirty = 1;
+  HIP_TRY(h, hipMemcpy(&dirty, h->d_sparse_dirty + (h->nreset & 1), 4, hipMemcpyDeviceToHost));
+  *out = dirty != 0;
+  return NMG_OK;
+}
+
 static int sparse_download(nmg_engine* h, std::vector<uint64_t>& k, std::vector<uint32_t>& v) {
   int rc = nmg_synchronize(h);
   if (rc) return rc;
-  if (!h->d_sparse_keys) {
+  bool any = false;
+  rc = sparse_nonempty(h, &any);
+  if (rc) return rc;
+  if (!any) {
     k.clear();
     v.clear();
     return NMG_OK;
@@ -1828,11 +2346,11 @@ static Rccl* rccl() {
       r.error_string = (decltype(r.error_string))dlsym(r.so, "ncclGetErrorString");
     }
   }
-  return r.so && r.init_all && r.reduce && r.group_start && r.group_end ? &r : nullptr;
+  return r.so && r.init_all && r.destroy && r.reduce && r.group_start && r.group_end && r.error_string ? &r : nullptr;
 }
 
 static int multi_create(nmg_engine* h, const nmg_options* opt) {
-  const uint32_t n = opt->nb_gpus;
+  const uint32_t n = std::max<uint32_t>(opt->nb_gpus, 1);  // (1: kDbgMultiRccl, a one-rank communicator)
   for (uint32_t i = 0; i < n; i++) h->devices.push_back(opt->devices ? opt->devices[i] : opt->device + (int)i);
   bool all_same = true, all_distinct = true;
   for (uint32_t i = 0; i < n; i++)
@@ -1846,6 +2364,7 @@ static int multi_create(nmg_engine* h, const nmg_options* opt) {
     nmg_options o = *opt;
     o.nb_gpus = 0;
     o.devices = nullptr;
+    o.flags &= ~kDbgMultiRccl;
     o.device = h->devices[i];
     nmg_engine* w = nullptr;
     const int rc = nmg_create(&w, &o);
@@ -2034,6 +2553,15 @@ static int multi_finish(nmg_engine* h) {
     }
     rc = nmg_sparse_import(h, mk.data(), mv.data(), (int64_t)mk.size());
     if (rc) return rc;
+  }
+  // per-buffer counts accumulate across analyses like every other counter
+  // (the workers were reset above); a reset of this handle zeroes them
+  if (h->counts_override && h->ov_samples.size() == ns.size()) {
+    for (size_t b = 0; b < ns.size(); b++) {
+      h->ov_samples[b] += ns[b];
+      h->ov_found[b] += nf[b];
+    }
+    return NMG_OK;
   }
   return nmg_set_buffer_counts(h, (uint32_t)ns.size(), ns.data(), nf.data(), h->buf_bytes.data());
 }

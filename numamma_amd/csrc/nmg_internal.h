@@ -36,6 +36,7 @@ enum ErrCode : uint32_t {
   kErrUnaligned = 3,
   kErrCapacity = 4,
   kErrRange = 5,
+  kErrRouteOverflow = 6,  // partition-first path: more short SAMPLE records than its overflow list holds
 };
 
 struct HostResults {

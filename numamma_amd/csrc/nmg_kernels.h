@@ -73,6 +73,8 @@ constexpr uint32_t kDbgTiming = 0x1000;    // per-wave phase cycle counts (tools
 constexpr uint32_t kDbgTinyLog = 0x2000;   // long-tail sub-logs of 2 records: exercises the overflow path (tests)
 constexpr uint32_t kDbgNoPack = 0x4000;    // overflow through plain atomics, not packed ones (tests)
 constexpr uint32_t kDbgNoDir = 0x8000;     // large tables: no fence-bucket directory, binary search only (tests)
+constexpr uint32_t kDbgMultiRccl = 0x40000;  // nmg_create: a multi-GPU handle even for nb_gpus <= 1, merged through
+                                             // RCCL (a one-rank communicator on a one-GPU box: tests of that branch)
 constexpr int kTimingWords = 24;           // per wave: load+check, barrier, process, rest, total, windows, -, -,
                                            // then (wave 0) 8 x 2 words of window trace
 

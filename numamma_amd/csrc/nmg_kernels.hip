@@ -291,45 +291,7 @@ __device__ __forceinline__ void process_sample(Params& p, WgCounters& wc, LaneAc
   // below do not depend on them and run while they are in flight
   NodePre np;
   if ((MODE & kModeLarge) && (p.flags & NMG_F_MATCH_SAMPLES)) np = node_issue(p, L, valid, addr, sp);
-  if (valid && !(p.flags & kDbgNoGlobal)) {
-    const uint32_t bm = bucket_mask(lvl);
-    if (w < kLaneMaxWeight) {  // register accumulation (no LDS traffic)
-      const uint32_t w32 = (uint32_t)w;
-      acc.tc += 1;
-      acc.tw += w32;
-      acc.na += lvl & LVL_NA;
-#pragma unroll
-      for (int k = 0; k < (kRegGroups + 1) / 2; k++)
-        acc.cnt2[k] += ((bm >> (2 * k)) & 1) | ((2 * k + 1 < kRegGroups ? (bm >> (2 * k + 1)) & 1 : 0) << 16);
-#pragma unroll
-      for (int k = 0; k < kRegGroups; k++) acc.sum[k] += ((bm >> k) & 1) * w32;
-      for (uint32_t m = bm >> kRegGroups; m; m &= m - 1) {  // rarer hit buckets, miss buckets
-        const uint32_t b = kRegGroups + (uint32_t)__builtin_ctz(m);
-        atomicAdd(&wc.sums[3 + 2 * b], 1ull);
-        if (w) atomicAdd(&wc.sums[4 + 2 * b], (unsigned long long)w);
-      }
-    } else {  // weights >= 2^23 cycles: straight to the LDS counters
-      atomicAdd(&wc.sums[0], 1ull);
-      atomicAdd(&wc.sums[1], (unsigned long long)w);
-      if (lvl & LVL_NA) atomicAdd(&wc.sums[2], 1ull);
-      for (uint32_t m = bm; m; m &= m - 1) {
-        const uint32_t b = (uint32_t)__builtin_ctz(m);
-        atomicAdd(&wc.sums[3 + 2 * b], 1ull);
-        atomicAdd(&wc.sums[4 + 2 * b], (unsigned long long)w);
-      }
-    }
-    // min / max only move monotonically: read first, atomic only on improvement
-    if (bm) {
-      const uint32_t b = (uint32_t)__builtin_ctz(bm);
-      if (w < wc.mins[b]) atomicMin(&wc.mins[b], (unsigned long long)w);
-      if (w > wc.maxs[b]) atomicMax(&wc.maxs[b], (unsigned long long)w);
-      for (uint32_t m = bm & (bm - 1); m; m &= m - 1) {  // several level groups (rare)
-        const uint32_t b2 = (uint32_t)__builtin_ctz(m);
-        if (w < wc.mins[b2]) atomicMin(&wc.mins[b2], (unsigned long long)w);
-        if (w > wc.maxs[b2]) atomicMax(&wc.maxs[b2], (unsigned long long)w);
-      }
-    }
-  }
+  if (valid && !(p.flags & kDbgNoGlobal)) global_count(acc, wc.sums, wc.mins, wc.maxs, lvl, w);
   sub_stamp<TIMING>(st, 0);
   if (!(p.flags & NMG_F_MATCH_SAMPLES)) return;
 

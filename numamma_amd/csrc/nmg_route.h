@@ -1,0 +1,157 @@
+// nmg_route.h -- the partition-first path for large object tables (DESIGN.md
+// "Partition-first"): what nmg_route.hip and the host engine share.
+//
+// The reference looks every sample up in one global AVL tree
+// (ma_find_mem_info_from_sample, src/mem_analyzer.c:249-306; ht_lower_key,
+// tools/hash.c:63-77).  At 10^5..10^6 intervals that is one or two random
+// HBM lines per sample on a GPU.  This path first routes the samples by
+// address range, then attributes each range with its slice of the table in
+// LDS:
+//   1. route_kernel   streams the buffers in analysis order (the byte cursor of
+//                     __analyze_buffer, mem_sampling.c:815-927), does the global
+//                     counters (update_counters, :508-592) and the per-buffer
+//                     sample counts, and appends a 24 B compact record of every
+//                     SAMPLE to a chunk of its partition (partition = a run of
+//                     <= kPartKeys consecutive keys; chunks of kChunk records
+//                     from the workgroup's private pool);
+//      overflow_kernel  the records a full pool turned away, with global lookups;
+//   2. count_kernel   chunks per (workgroup, partition), from the chunks' tags;
+//      plan_kernel    per-partition chunk counts -> list offsets and work items;
+//   3. scatter_kernel chunk ids into per-partition lists;
+//   4. local_kernel   one work item (<= kItemChunks chunks of one partition) per
+//                     workgroup at a time: the partition's keys and node records
+//                     in an LDS Eytzinger tree, its object and page counters in
+//                     LDS, flushed once per item (__match_sample, :594-673;
+//                     ma_get_block, mem_analyzer.c:494-534);
+//   5. found_kernel   per-buffer matched-sample counts from the match bits
+//                     local_kernel leaves per chunk (on demand: the reference
+//                     only sums them, mem_sampling.c:334-335, 357-361).
+#pragma once
+
+#include "nmg_kernels.h"
+
+namespace nmg {
+
+constexpr uint32_t kChunk = 64;            // compact records per chunk (one wave processes one chunk)
+constexpr uint32_t kPartLevels = 11;       // route pass: Eytzinger tree of partition starts in LDS
+constexpr uint32_t kMaxParts = (1u << kPartLevels) - 1;
+constexpr uint32_t kPartKeyLevels = 10;    // local pass: <= 1023 keys per partition in LDS
+constexpr uint32_t kPartKeys = (1u << kPartKeyLevels) - 1;
+constexpr uint32_t kPartSlots = 1u << kPartKeyLevels;  // Eytzinger slots per partition (index 0 unused)
+constexpr uint32_t kPartEntries = 1536;    // entries per partition (LDS object counters)
+constexpr uint32_t kPartCells = 28672;     // u16 page cells per partition: nb_threads x cell span
+constexpr uint32_t kRouteWindows = 3;      // windows per LDS sort batch of the route pass
+constexpr uint32_t kRouteBatch = kRouteWindows * kWG;
+constexpr uint32_t kItemChunks = 1023;     // chunks per work item: < 2^16 records, so u16 page cells
+                                           // and the packed object counters cannot overflow
+static_assert(kItemChunks * kChunk < 65536u, "u16 page cells per item");
+static_assert((uint64_t)kItemChunks * kChunk < (1ull << (64 - kPackShift)), "packed count per item");
+constexpr uint32_t kChunkIdBits = 25;      // route pass LDS: chunk id << 7 | fill
+constexpr uint32_t kNoChunk = 0xffffffffu;
+constexpr uint32_t kFoundLds = 16384;      // found_kernel: per-buffer LDS counters of one workgroup
+// internal switches (tests / A/B only)
+constexpr uint32_t kDbgNoRoute = 0x10000;  // large tables: the single-pass attribute_kernel instead
+constexpr uint32_t kDbgTinyPool = 0x20000; // route pass: private pools of 2 chunks, so the pool-overflow
+                                           // (direct attribution) path runs
+// ablation switches (tools/ablate.py; results are wrong with them)
+constexpr uint32_t kDbgRouteNoWrite = 0x100000;  // route pass: batches sorted in LDS, no chunk stores
+constexpr uint32_t kDbgRouteNoBatch = 0x200000;  // route pass: no batch sort or stores at all
+constexpr uint32_t kDbgLocalNoWork = 0x400000;   // local pass: chunk loads only
+constexpr uint32_t kDbgRouteTiming = 0x800000;   // route pass: per-wave phase cycles in Params::dbg
+constexpr int kRouteTimingWords = 12;            // wait+barrier, issue, global, search, rank, scan, alloc+stage, write,
+                                                 // state, windows, batches, -
+
+// One partition: keys [k0, k0 + nk), entries [e0, e0 + ne) (entry ids of the
+// offline table are table positions, so a key range owns an id range), dense
+// page cells [cb, cb + span) of every thread.
+struct PartInfo {
+  uint32_t k0, nk, e0, ne;
+  uint64_t cb;
+  uint32_t span;
+  uint32_t levels;     // Eytzinger levels of the partition's tree (nk <= 2^levels - 1)
+  uint32_t pages_lds;  // nb_threads * span <= kPartCells: page cells in LDS, else global atomics
+  uint32_t pad[3];
+};
+static_assert(sizeof(PartInfo) == 48, "PartInfo");
+
+// compact record X word: g | off8 << gbits | thread << (gbits + obits) |
+// access << (gbits + obits + tbits) | min(weight, escape) << xw_shift
+struct XLayout {
+  uint32_t gbits, obits, tbits, wshift;
+  uint64_t wesc;  // 2^wbits - 1: the weight is re-read from the record
+};
+
+struct RouteParams {
+  Params p;                  // data, sbufs (= descriptors in analysis order, .pad = index), ranges,
+                             // global counters, per-buffer counts, and the table for direct attribution
+  const uint64_t* pbounds;   // [2^kPartLevels] partition start keys in Eytzinger order, ~0 padding
+  uint32_t nparts;
+  XLayout xl;
+  uint64_t seq0;             // analysis index of descriptor 0 (seq = seq0 + index)
+  uint4* rec16;              // [chunks][kChunk] (addr, timestamp)
+  unsigned long long* recx;  // [chunks][kChunk] X words
+  uint32_t* cmeta;           // [chunks] partition | fill << 24
+  const uint32_t* chunk0;    // [grid + 1] private chunk range of each workgroup
+  uint32_t* used;            // [grid] chunks taken
+  uint4* ovf16;              // overflow list: records that found no chunk (overflow_kernel)
+  unsigned long long* ovfx;
+  uint32_t* ovf_cnt;         // (= ctl[2]; zeroed by plan_kernel after overflow_kernel read it)
+  uint32_t ovf_cap;
+};
+
+struct PlanParams {
+  uint32_t* pcnt;        // in: [grid][nparts] chunk counts; out: exclusive prefix over workgroups
+  uint32_t* pbase;       // out: [nparts] first list slot of each partition
+  uint4* items;          // out: {partition, list begin, list end, 0}
+  uint32_t* ctl;         // out: [0] number of items, [1] dequeue head (zeroed), [2] overflow records (zeroed)
+  uint32_t grid, nparts;
+};
+
+struct ScatterParams {
+  const uint32_t* cmeta;
+  const uint32_t* chunk0;
+  const uint32_t* used;
+  const uint32_t* pcnt;   // exclusive prefixes (plan_kernel)
+  const uint32_t* pbase;
+  uint32_t* clist;        // [chunks] chunk id | fill << kChunkIdBits, grouped by partition
+  uint32_t nparts;
+};
+
+struct LocalParams {
+  Params p;                  // table (nodes, chain, entries), counters, hist, sparse, flags
+  const PartInfo* parts;
+  const uint64_t* pe_keys;   // [nparts][kPartSlots] Eytzinger keys, ~0 padding
+  const uint4* pe_nodes;     // [nparts][kPartSlots][2] (addr, end), (alloc, free)
+  const uint2* pe_info;      // [nparts][kPartSlots] (cell - cb or ~0, entry - e0 | older entries << 31)
+  const uint4* rec16;
+  const unsigned long long* recx;
+  const uint32_t* cmeta;
+  const uint32_t* clist;     // chunk id | fill << kChunkIdBits, grouped by partition
+  const uint4* items;
+  uint32_t* ctl;             // [0] items, [1] dequeue head
+  unsigned long long* cmatch;  // [chunks] match bit per record
+  const BufDesc* descs;      // analysis order (escaped weights are re-read from the record)
+  XLayout xl;
+  uint64_t seq0;
+};
+
+struct FoundParams {
+  const uint32_t* ranges;    // [grid + 1] descriptor range of each route workgroup
+  const uint32_t* chunk0;
+  const uint32_t* used;
+  const uint32_t* cmeta;
+  const unsigned long long* cmatch;
+  const unsigned long long* recx;
+  uint32_t* bufcnt;          // [2][nb_bufs]
+  uint32_t nb_bufs, gbits;
+};
+
+hipError_t launch_route(uint32_t grid, hipStream_t s, const RouteParams& r);
+hipError_t launch_overflow(hipStream_t s, const RouteParams& r);
+hipError_t launch_count(uint32_t grid, hipStream_t s, const ScatterParams& r);  // pcnt from cmeta
+hipError_t launch_plan(hipStream_t s, const PlanParams& r);
+hipError_t launch_scatter(uint32_t grid, hipStream_t s, const ScatterParams& r);
+hipError_t launch_local(uint32_t grid, hipStream_t s, const LocalParams& r);
+hipError_t launch_found(uint32_t grid, hipStream_t s, const FoundParams& r);
+
+}  // namespace nmg

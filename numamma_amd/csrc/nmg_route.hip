@@ -1,0 +1,1075 @@
+// nmg_route.hip -- MI355X (gfx950) device code of the partition-first path
+// for large object tables (nmg_route.h; DESIGN.md "Partition-first").
+//
+// Same results as attribute_kernel, bit for bit: every merge is an integer
+// sum, min or max, and the first-match ordinal carries the analysis position
+// (seq << 32 | byte offset), so the order in which samples are attributed
+// changes nothing.  What changes is where the table lookups go: instead of a
+// directory slot and a node record in HBM per sample (two dependent random
+// lines), the route pass finds a sample's partition in a 16 KiB LDS tree and
+// writes a 24 B compact record; the local pass then resolves whole partitions
+// with their keys and node records in LDS.
+#include <algorithm>
+
+#include "nmg_device.h"
+#include "nmg_route.h"
+
+namespace nmg {
+
+static_assert((uint64_t)kItemChunks * kChunk * kLaneMaxWeight < (1ull << kPackShift), "packed weight per item");
+
+// in-order rank of Eytzinger node idx >= 1 of a complete `levels`-level tree
+__device__ __forceinline__ uint32_t eytz_rank(uint32_t idx, uint32_t levels) {
+  const uint32_t d = 31 - __builtin_clz(idx);
+  return (((idx - (1u << d)) * 2 + 1) << (levels - 1 - d)) - 1;
+}
+
+// ---------------------------------------------------------------------------
+// compact records: (addr, timestamp) + X (see XLayout)
+
+struct XRec {
+  uint32_t g, off, th, acc;
+  uint64_t wq;
+};
+
+__device__ __forceinline__ uint64_t x_encode(const XLayout& xl, uint32_t g, uint32_t off, uint32_t th, uint32_t acc,
+                                             uint64_t w) {
+  const uint64_t wq = w < xl.wesc ? w : xl.wesc;
+  return uint64_t(g) | (uint64_t(off >> 3) << xl.gbits) | (uint64_t(th) << (xl.gbits + xl.obits)) |
+         (uint64_t(acc) << (xl.wshift - 1)) | (wq << xl.wshift);
+}
+
+__device__ __forceinline__ XRec x_decode(const XLayout& xl, uint64_t x) {
+  XRec r;
+  r.g = (uint32_t)(x & ((1ull << xl.gbits) - 1));
+  r.off = (uint32_t)((x >> xl.gbits) & ((1ull << xl.obits) - 1)) << 3;
+  r.th = (uint32_t)((x >> (xl.gbits + xl.obits)) & ((1ull << xl.tbits) - 1));
+  r.acc = (uint32_t)((x >> (xl.wshift - 1)) & 1);
+  r.wq = x >> xl.wshift;
+  return r;
+}
+
+// the record's weight: the X field, or (escape) the record itself
+__device__ __forceinline__ uint64_t x_weight(const XLayout& xl, const XRec& r, const uint8_t* data,
+                                             const BufDesc* descs) {
+  if (r.wq != xl.wesc) return r.wq;
+  return *reinterpret_cast<const uint64_t*>(data + descs[r.g].offset + r.off + 24);  // struct mem_sample.weight
+}
+
+// ---------------------------------------------------------------------------
+// direct attribution (overflow_kernel: a route workgroup's chunk pool was
+// exhausted): the lookup of
+// __ma_find_mem_info_from_sample_generic (mem_analyzer.c:249-286) in global
+// memory -- binary search of the keys (ht_lower_key, tools/hash.c:63-77),
+// node record, older entries -- and global atomics.  Correct for any input;
+// only taken when a workgroup's samples outgrow its pool (SAMPLE records
+// shorter than 40 B, or the kDbgTinyPool test switch).
+__device__ __forceinline__ void direct_attribute(const Params& p, uint64_t addr, uint64_t ts, uint64_t w, uint32_t th,
+                                                 uint32_t acc, uint64_t seq, uint32_t off, uint32_t slot) {
+  if (p.nb_keys == 0 || p.keys[0] > addr) return;
+  uint32_t lo = 0, n = p.nb_keys;
+  while (n > 1) {
+    const uint32_t half = n >> 1;
+    if (p.keys[lo + half] <= addr) {
+      lo += half;
+      n -= half;
+    } else {
+      n = half;
+    }
+  }
+  const uint4* q = reinterpret_cast<const uint4*>(p.nodes + lo);
+  const uint4 a = q[0], b = q[1], c = q[2];
+  Match m;
+  m.e = -1;
+  m.baddr = 0;
+  m.hist = kHistSparse;
+  if (entry_match(a, b, addr, ts)) {
+    m.e = c.w;
+    m.baddr = u64of(a.x, a.y);
+    m.hist = u64of(c.x, c.y);
+  } else {
+    const uint4 d = q[3];
+    if (d.x > 1) match_older(p, d.y, d.x, addr, ts, m);
+  }
+  if (m.e < 0) return;
+  const uint64_t e = (uint64_t)m.e;
+  atomicAdd(p.bufcnt + p.nb_bufs + slot, 1u);
+  atomicAdd(reinterpret_cast<unsigned long long*>(p.sum64 + objcw_index(e, acc, 0, p.nb_entries)), 1ull);
+  if (w) atomicAdd(reinterpret_cast<unsigned long long*>(p.sum64 + objcw_index(e, acc, 1, p.nb_entries)),
+                   (unsigned long long)w);
+  atomicMin(reinterpret_cast<unsigned long long*>(p.min64 + 36 + e), (unsigned long long)((seq << 32) | off));
+  if (!(p.flags & NMG_F_PAGE_HIST)) return;
+  const uint32_t page = uint32_t(int(uint64_t(addr - m.baddr) / kPageSize));
+  if (m.hist != kHistSparse) {
+    atomicAdd(p.hist + uint64_t(th) * p.hist_cells + m.hist + page, 1u);
+  } else {
+    const uint32_t sidx = p.entries[e].sidx;
+    if (sidx != ~0u) sparse_add(p, sparse_key(sidx, th, page), seq, off, 1u);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// pass 1: route
+
+// A lane's stride slot in window (cur of d0) [+ head of d1]: unlike
+// attribute_kernel's windows, d1 may belong to another stream (the route
+// pass keeps per-lane stream state), so windows stay full across buffer ends.
+struct RWin {
+  uint32_t pos;     // slot offset within its buffer
+  uint32_t n0, n1;  // slots in d0 / in d1 (uniform)
+  bool in1;
+  bool cand;
+};
+
+__device__ __forceinline__ RWin rwin_lane(int tid, uint32_t cur, const BufDesc& d0, const BufDesc& d1, bool has1) {
+  RWin w;
+  const uint32_t left = d0.len - cur;
+  w.n0 = min(left / kRecBytes + (left % kRecBytes != 0), (uint32_t)kWG);
+  w.n1 = 0;
+  if (has1 && w.n0 < (uint32_t)kWG) w.n1 = min(d1.len / kRecBytes + (d1.len % kRecBytes != 0), (uint32_t)kWG - w.n0);
+  w.in1 = (uint32_t)tid >= w.n0;
+  w.cand = (uint32_t)tid < w.n0 + w.n1;
+  w.pos = w.in1 ? (uint32_t(tid) - w.n0) * kRecBytes : cur + uint32_t(tid) * kRecBytes;
+  return w;
+}
+
+__device__ __forceinline__ void rload_slot(const uint8_t* data, const RWin& w, const BufDesc& d0, const BufDesc& d1,
+                                           RawRec& r) {
+  const uint64_t off = w.in1 ? d1.offset : d0.offset;
+  const uint32_t len = w.cand ? (w.in1 ? d1.len : d0.len) : 0;
+  load_rec(data + off, w.pos, len, r);
+}
+
+// update_counters(global_counters, ...) (mem_sampling.c:517-592) for a
+// wave's records, without per-lane accumulators (the route pass needs its
+// registers for the held records): the common buckets (total count / weight,
+// N/A, L1 / L2 / L3 hits) and their min / max are reduced over the wave
+// (ballots, DPP sums and minima) and added to this wave's own LDS words
+// `wacc` [2 access][kWaveAccWords] by one lane; rarer buckets and weights >=
+// 2^23 update the workgroup's LDS counters per lane, as global_count does.
+constexpr int kWaveAccWords = 12;  // tc, tw, na, 3 x (count, sum), 3 hit-bucket (min, max) below
+// DPP move that keeps the lane's own value where the source lane is out of
+// range (identity for min / max)
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ uint32_t dpp_keep(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, CTRL, ROW_MASK, 0xf, false);
+}
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {  // (the steps of wave_sum_u32)
+  v = min(v, dpp_keep<0x111, 0xf>(v));
+  v = min(v, dpp_keep<0x112, 0xf>(v));
+  v = min(v, dpp_keep<0x114, 0xf>(v));
+  v = min(v, dpp_keep<0x118, 0xf>(v));
+  v = min(v, dpp_keep<0x142, 0xa>(v));
+  v = min(v, dpp_keep<0x143, 0xc>(v));
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+  v = max(v, dpp_keep<0x111, 0xf>(v));
+  v = max(v, dpp_keep<0x112, 0xf>(v));
+  v = max(v, dpp_keep<0x114, 0xf>(v));
+  v = max(v, dpp_keep<0x118, 0xf>(v));
+  v = max(v, dpp_keep<0x142, 0xa>(v));
+  v = max(v, dpp_keep<0x143, 0xc>(v));
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+
+__device__ __forceinline__ void wave_global_count(unsigned long long* wacc, unsigned long long (*sums)[kGlobalSums],
+                                                  unsigned long long (*mins)[18], unsigned long long (*maxs)[18],
+                                                  bool valid, uint32_t acc, uint32_t lvl, uint64_t w, int lane) {
+  const uint32_t bm = valid ? bucket_mask(lvl) : 0u;
+  const bool small = w < kLaneMaxWeight;
+  if (valid) {
+    unsigned long long* S = sums[acc];
+    if (small) {
+      for (uint32_t m = bm >> kRegGroups; m; m &= m - 1) {  // rarer hit buckets, miss buckets
+        const uint32_t b = kRegGroups + (uint32_t)__builtin_ctz(m);
+        atomicAdd(&S[3 + 2 * b], 1ull);
+        if (w) atomicAdd(&S[4 + 2 * b], (unsigned long long)w);
+        if (w < mins[acc][b]) atomicMin(&mins[acc][b], (unsigned long long)w);
+        if (w > maxs[acc][b]) atomicMax(&maxs[acc][b], (unsigned long long)w);
+      }
+    } else {  // weights >= 2^23 cycles: every bucket straight to the LDS counters
+      atomicAdd(&S[0], 1ull);
+      atomicAdd(&S[1], (unsigned long long)w);
+      if (lvl & LVL_NA) atomicAdd(&S[2], 1ull);
+      for (uint32_t m = bm; m; m &= m - 1) {
+        const uint32_t b = (uint32_t)__builtin_ctz(m);
+        atomicAdd(&S[3 + 2 * b], 1ull);
+        atomicAdd(&S[4 + 2 * b], (unsigned long long)w);
+        if (w < mins[acc][b]) atomicMin(&mins[acc][b], (unsigned long long)w);
+        if (w > maxs[acc][b]) atomicMax(&maxs[acc][b], (unsigned long long)w);
+      }
+    }
+  }
+#pragma unroll
+  for (uint32_t a = 0; a < 2; a++) {
+    const bool in = valid && small && acc == a;
+    const uint64_t am = __ballot(in);
+    if (!am) continue;
+    const uint32_t w32 = in ? (uint32_t)w : 0u;  // (< 2^23: a wave's sum fits 32 bits)
+    unsigned long long* W = wacc + a * kWaveAccWords;
+    const uint32_t tc = (uint32_t)__popcll(am), na = (uint32_t)__popcll(__ballot(in && (lvl & LVL_NA)));
+    const uint32_t tw = wave_sum_u32(w32);
+    if (lane == 0) {
+      W[0] += tc;
+      W[1] += tw;
+      W[2] += na;
+    }
+#pragma unroll
+    for (int b = 0; b < kRegGroups; b++) {
+      const bool ib = in && ((bm >> b) & 1);
+      const uint64_t bmask = __ballot(ib);
+      if (!bmask) continue;
+      const uint32_t c = (uint32_t)__popcll(bmask), sw = wave_sum_u32(ib ? w32 : 0u);
+      const uint32_t mn = wave_min_u32(ib ? w32 : 0xffffffffu), mx = wave_max_u32(ib ? w32 : 0u);
+      if (lane == 0) {
+        W[3 + 2 * b] += c;
+        W[4 + 2 * b] += sw;
+        if (mn < mins[a][b]) atomicMin(&mins[a][b], (unsigned long long)mn);
+        if (mx > maxs[a][b]) atomicMax(&maxs[a][b], (unsigned long long)mx);
+      }
+    }
+  }
+}
+
+// kDbgRouteTiming: per-wave cycle accumulators of the route pass's phases
+struct RTimer {
+  uint64_t acc[9];
+  uint64_t last;
+};
+template <bool TIMING>
+__device__ __forceinline__ void rt_stamp(RTimer& t, int i) {
+  if (TIMING) {
+    const uint64_t now = stamp();
+    t.acc[i] += now - t.last;
+    t.last = now;
+  }
+}
+
+// One batch's records held per lane in registers until the batch is sorted:
+// a 3-deep shift register (static indices only: no scratch)
+struct Held {
+  uint4 a;         // addr, timestamp
+  uint64_t x;      // X word
+  uint32_t q;      // partition | batch rank << 11, or kNoChunk (nothing held)
+};
+
+// The route pass's LDS state shared by the batch helpers
+struct RouteLds {
+  uint32_t* hist;     // [P] records of each partition in the batch (rank counters)
+  uint32_t* start;    // [P] first staging slot of each partition's run
+  uint32_t* cur;      // [2][kMaxParts + 1] open chunk id << 7 | fill, double-buffered by batch parity
+  uint32_t* nb;       // [P] first new chunk of the batch (kNoChunk: pool exhausted)
+  uint4* a16;         // staging: (addr, timestamp) in partition order
+  unsigned long long* x;
+  uint16_t* q;
+  uint32_t* wsum;     // [16] per-wave scan totals
+  uint32_t* misc;     // [0] records in the batch, [1] chunks taken, [2] first chunk never handed out
+};
+
+// Sort the batch's held records by partition into the LDS staging area and
+// take chunks for the partitions that outgrow their open chunk: three
+// barriers (after the batch's ranks, after the scan, after the staging).
+// Open-chunk state: batch b reads cur[b & 1] and writes cur[(b + 1) & 1].
+template <bool TIMING>
+__device__ __forceinline__ void route_sort_batch(RTimer& rt, const RouteParams& rp, Held (&h)[kRouteWindows], int tid,
+                                                 const RouteLds& L, uint32_t batch, uint32_t c0, uint32_t cap) {
+  const uint32_t P = rp.nparts;
+  const int lane = tid & 63, wave = tid >> 6;
+  const uint32_t* cur_in = L.cur + (batch & 1) * (kMaxParts + 1);
+  uint32_t* cur_out = L.cur + ((batch + 1) & 1) * (kMaxParts + 1);
+  __syncthreads();  // every rank of the batch taken
+  // exclusive scan of the per-partition counts (two per thread, DPP within a wave)
+  const uint32_t i0 = 2 * (uint32_t)tid;
+  const uint32_t v0 = i0 < P ? L.hist[i0] : 0u, v1 = i0 + 1 < P ? L.hist[i0 + 1] : 0u;
+  const uint32_t s = v0 + v1;
+  const uint32_t inc = wave_incl_scan_u32(s);
+  if (lane == 63) L.wsum[wave] = inc;
+  __syncthreads();
+  uint32_t wb = 0;
+  {
+    const uint4* ws = reinterpret_cast<const uint4*>(L.wsum);
+#pragma unroll
+    for (int k = 0; k < (int)(kWG / 64 / 4); k++) {
+      const uint4 x = ws[k];
+      wb += (4 * k + 0 < wave ? x.x : 0u) + (4 * k + 1 < wave ? x.y : 0u) + (4 * k + 2 < wave ? x.z : 0u) +
+            (4 * k + 3 < wave ? x.w : 0u);
+    }
+  }
+  const uint32_t ex = wb + inc - s;
+  rt_stamp<TIMING>(rt, 5);
+  // chunks for the partitions that outgrow their open chunk (private pool:
+  // workgroup-local atomics only), the next open-chunk state, counts cleared
+  for (uint32_t k = 0; k < 2; k++) {
+    const uint32_t q = i0 + k;
+    if (q >= P) break;
+    const uint32_t n = k ? v1 : v0;
+    L.start[q] = ex + (k ? v0 : 0u);
+    const uint32_t cur = cur_in[q];
+    if (!n) {
+      cur_out[q] = cur;
+      continue;
+    }
+    L.hist[q] = 0;
+    const uint32_t fill = cur & 127u, tot = fill + n;
+    if (tot <= kChunk) {
+      cur_out[q] = (cur & ~127u) | tot;
+      continue;
+    }
+    const uint32_t nn = (tot - kChunk + kChunk - 1) / kChunk;
+    const uint32_t base = atomicAdd(&L.misc[1], nn);
+    if (base + nn > cap) {
+      L.nb[q] = kNoChunk;  // pool exhausted: this batch's overflow of q is attributed directly
+      atomicMin(&L.misc[2], base);  // chunks from here on were never handed out
+      cur_out[q] = (cur & ~127u) | kChunk;
+      continue;
+    }
+    L.nb[q] = c0 + base;
+    for (uint32_t j = 0; j < nn; j++) rp.cmeta[c0 + base + j] = q | (kChunk << 24);
+    cur_out[q] = ((c0 + base + nn - 1) << 7) | (tot - kChunk - kChunk * (nn - 1));
+  }
+  if (tid == kWG - 1) L.misc[0] = wb + inc;  // records in the batch
+  __syncthreads();
+  // the held records into LDS in partition order
+#pragma unroll
+  for (int b = 0; b < (int)kRouteWindows; b++) {
+    if (h[b].q == kNoChunk) continue;
+    const uint32_t q = h[b].q & 2047u;
+    const uint32_t j = L.start[q] + (h[b].q >> 11);
+    L.a16[j] = h[b].a;
+    L.x[j] = h[b].x;
+    L.q[j] = (uint16_t)q;
+    h[b].q = kNoChunk;
+  }
+  __syncthreads();
+  rt_stamp<TIMING>(rt, 6);
+}
+
+// Each partition's run of sorted batch `batch` to its chunks: contiguous
+// slots, coalesced by run.  Run right after the next window's barrier and
+// before its loads are issued: a window waits for its loads with
+// vmcnt(0), which counts stores too, so stores issued behind the loads would
+// make the window wait for them.  (The LDS it reads is rewritten only by the
+// next batch's sort, after that batch's barriers.)
+template <bool TIMING>
+__device__ __forceinline__ void route_write_batch(RTimer& rt, const RouteParams& rp, int tid, const RouteLds& L,
+                                                  uint32_t batch) {
+  const Params& p = rp.p;
+  const uint32_t* cur_in = L.cur + (batch & 1) * (kMaxParts + 1);
+  const uint32_t total = L.misc[0];
+  for (uint32_t j = tid; j < total; j += kWG) {
+    const uint32_t q = L.q[j];
+    const uint32_t cur = cur_in[q];
+    const uint32_t pos = (cur & 127u) + (j - L.start[q]);
+    uint32_t chunk, slot;
+    if (pos < kChunk) {
+      chunk = cur >> 7;
+      slot = pos;
+    } else {
+      const uint32_t nb = L.nb[q];
+      if (nb == kNoChunk) {  // pool exhausted: to the overflow list (overflow_kernel)
+        const uint32_t o = atomicAdd(rp.ovf_cnt, 1u);
+        if (o < rp.ovf_cap) {
+          rp.ovf16[o] = L.a16[j];
+          rp.ovfx[o] = L.x[j];
+        } else {  // (only SAMPLE records shorter than 40 B get here: NMG_F_SINGLE_PASS handles any number)
+          const XRec xr = x_decode(rp.xl, L.x[j]);
+          set_error(p, rp.seq0 + xr.g, xr.off, kErrRouteOverflow);
+        }
+        continue;
+      }
+      chunk = nb + (pos - kChunk) / kChunk;
+      slot = (pos - kChunk) % kChunk;
+    }
+    if (p.flags & kDbgRouteNoWrite) continue;
+    const uint64_t k = uint64_t(chunk) * kChunk + slot;
+    rp.rec16[k] = L.a16[j];
+    rp.recx[k] = L.x[j];
+  }
+  rt_stamp<TIMING>(rt, 7);
+}
+
+// Descriptors of the workgroup's range staged in LDS (offset, len,
+// thread | access << 16): a buffer transition reads LDS instead of waiting on
+// a global load.  Ranges longer than kDescLds read the rest from global
+// memory.  In the analysis-order schedule the count slot (.pad) is the
+// index and seq = seq0 + index.
+constexpr uint32_t kDescLds = 512;
+
+__device__ __forceinline__ BufDesc route_desc(const RouteParams& rp, const uint4* s_desc, uint32_t r0, uint32_t i) {
+  if (i - r0 < kDescLds) {
+    const uint4 v = s_desc[i - r0];
+    BufDesc d;
+    d.offset = u64of(v.x, v.y);
+    d.len = v.z;
+    d.thread_rank = v.w & 0xffffu;
+    d.access = v.w >> 16;
+    d.pad = i;
+    d.seq = rp.seq0 + i;
+    return d;
+  }
+  return rp.p.sbufs[i];
+}
+
+template <bool TIMING>
+__global__ __launch_bounds__(kWG, 1) void route_kernel(RouteParams rp) {
+  __shared__ uint64_t s_bounds[1u << kPartLevels];
+  __shared__ uint32_t s_hist[kMaxParts + 1], s_start[kMaxParts + 1], s_cur[2][kMaxParts + 1], s_nb[kMaxParts + 1];
+  __shared__ uint4 s_desc[kDescLds];
+  __shared__ uint4 s_a16[kRouteBatch];
+  __shared__ unsigned long long s_x[kRouteBatch];
+  __shared__ uint16_t s_q[kRouteBatch];
+  __shared__ unsigned long long s_sums[2][kGlobalSums], s_mins[2][18], s_maxs[2][18];
+  __shared__ unsigned long long s_wacc[kWG / 64][2][kWaveAccWords];  // wave_global_count: one block per wave
+  __shared__ uint32_t s_list[kMaxList];
+  __shared__ uint32_t s_flags[3], s_nlist, s_next, s_err, s_wsum[kWG / 64], s_misc[3];
+
+  Params& p = rp.p;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const uint32_t P = rp.nparts;
+  const uint32_t c0 = rp.chunk0[blockIdx.x];
+  const uint32_t cap = rp.chunk0[blockIdx.x + 1] - c0;
+  for (uint32_t i = tid; i < (1u << kPartLevels); i += kWG) s_bounds[i] = rp.pbounds[i];
+  for (uint32_t i = tid; i < P; i += kWG) {
+    s_hist[i] = 0;
+    s_cur[0][i] = kChunk;  // no open chunk (full)
+  }
+  const uint32_t r0 = p.ranges[blockIdx.x], r1 = p.ranges[blockIdx.x + 1];
+  for (uint32_t i = r0 + tid; i < r1 && i - r0 < kDescLds; i += kWG) {
+    const BufDesc d = p.sbufs[i];
+    s_desc[i - r0] = make_uint4((uint32_t)d.offset, (uint32_t)(d.offset >> 32), d.len, d.thread_rank | (d.access << 16));
+  }
+  const RouteLds L{s_hist, s_start, &s_cur[0][0], s_nb, s_a16, s_x, s_q, s_wsum, s_misc};
+  if (tid < (int)kGlobalSums) s_sums[0][tid] = s_sums[1][tid] = 0;
+  if (tid < 18) {
+    s_mins[0][tid] = s_mins[1][tid] = ~0ull;  // INIT_COUNTER (mem_analyzer.c:415-420)
+    s_maxs[0][tid] = s_maxs[1][tid] = 0;
+  }
+  if (tid < 3) s_flags[tid] = 0;
+  for (uint32_t i = tid; i < (kWG / 64) * 2 * kWaveAccWords; i += kWG) (&s_wacc[0][0][0])[i] = 0;
+  if (tid == 0) {
+    s_misc[1] = 0;
+    s_misc[2] = kNoChunk;
+  }
+  __syncthreads();
+
+  uint32_t nbatches = 0;  // (its parity picks the open-chunk state array)
+  if (r0 < r1) {
+    uint32_t idx = r0;
+    uint32_t cur = 0;  // byte cursor (cur_cpt, mem_sampling.c:836)
+    BufDesc d0 = route_desc(rp, s_desc, r0, idx);
+    BufDesc d1 = idx + 1 < r1 ? route_desc(rp, s_desc, r0, idx + 1) : d0;
+    BufDesc d2 = idx + 2 < r1 ? route_desc(rp, s_desc, r0, idx + 2) : d0;  // read a transition ahead
+    bool has1 = idx + 1 < r1;
+    RawRec nx;
+    {
+      const RWin wl = rwin_lane(tid, 0, d0, d1, has1);
+      rload_slot(p.data, wl, d0, d1, nx);
+    }
+    Held held[kRouteWindows];
+#pragma unroll
+    for (int b = 0; b < (int)kRouteWindows; b++) held[b].q = kNoChunk;
+    uint32_t win = 0, bwin = 0;
+    uint32_t ns0 = 0, ns1 = 0;  // per-buffer SAMPLE tallies: buffer idx, idx + 1
+    RTimer rt;
+#pragma unroll
+    for (int k = 0; k < 9; k++) rt.acc[k] = 0;
+    rt.last = TIMING ? stamp() : 0;
+    bool wpending = false;  // a sorted batch waits for its chunk stores
+
+    while (true) {
+      const RWin wl = rwin_lane(tid, cur, d0, d1, has1);
+      const Rec r = decode_rec(nx, wl.pos);
+      // ---- fast-path check: every 40 B stride slot holds a whole 40 B record
+      const uint32_t wlen = wl.in1 ? d1.len : d0.len;
+      const bool bad =
+          (cur & 7) != 0 || (wl.cand && (uint64_t(wl.pos) + kRecBytes > wlen || (r.hdr >> 48) != kRecBytes));
+      const uint64_t badm = __ballot(bad);
+      if (badm && lane == 0) atomicOr(&s_flags[win % 3], 1u);
+      __syncthreads();
+      const uint32_t f = __builtin_amdgcn_readfirstlane(s_flags[win % 3]);
+      if (tid == 0) s_flags[(win + 2) % 3] = 0;
+      win++;
+      if (TIMING) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (timing: the window's loads count as wait)
+      rt_stamp<TIMING>(rt, 0);
+      uint32_t nidx = idx;
+      uint64_t ncur;
+      Rec rec = r;
+      bool valid, rin1;
+      uint32_t roff;
+      if (!(f & 1)) {
+        valid = wl.cand && uint32_t(r.hdr) == kSampleType;
+        rin1 = wl.in1;
+        roff = wl.pos;
+        if (wl.n1) {
+          nidx = idx + 1;
+          ncur = uint64_t(wl.n1) * kRecBytes;
+          if (ncur >= d1.len) {
+            nidx = idx + 2;
+            ncur = 0;
+          }
+        } else {
+          ncur = cur + uint64_t(wl.n0) * kRecBytes;
+          if (ncur >= d0.len) {
+            nidx = idx + 1;
+            ncur = 0;
+          }
+        }
+      } else {
+        // ---- slow path (buffer idx only), as attribute_kernel: wave 0
+        // follows the header chain (non-SAMPLE records skipped by size,
+        // size 0 / truncation / misalignment flagged), listing SAMPLE offsets
+        const uint8_t* base = p.data + d0.offset;
+        const uint64_t len = d0.len;
+        if (tid < 64) {
+          uint64_t q0 = cur;
+          uint32_t n = 0, err = 0;
+          const uint64_t lim = min(uint64_t(cur) + kWinBytes, len);
+          while (q0 < lim && n + 65 <= kMaxList) {
+            const uint64_t q = q0 + uint64_t(lane) * kRecBytes;
+            const uint64_t hdr = (q + 8 <= len) ? *reinterpret_cast<const uint64_t*>(base + q) : 0;
+            const bool reg = q < lim && q + kRecBytes <= len && (hdr >> 48) == kRecBytes;
+            const uint64_t rm = __ballot(reg);
+            const uint32_t run = ~rm ? (uint32_t)__builtin_ctzll(~rm) : 64u;
+            const bool smp = (uint32_t)lane < run && uint32_t(hdr) == kSampleType;
+            const uint64_t sm = __ballot(smp);
+            if (smp) s_list[n + (uint32_t)__popcll(sm & ((1ull << lane) - 1))] = (uint32_t)q;
+            n += (uint32_t)__popcll(sm);
+            q0 += uint64_t(run) * kRecBytes;
+            if (run == 64 || q0 >= lim) continue;
+            if (q0 + 8 > len) {
+              err = kErrTruncated;
+              break;
+            }
+            const uint64_t h = (uint64_t)__shfl(hdr, (int)run, 64);
+            const uint32_t size = uint32_t(h >> 48);
+            if (size == 0) {  // mem_sampling.c:857-860
+              err = kErrZeroSize;
+              break;
+            }
+            if (size & 7) {
+              err = kErrUnaligned;
+              break;
+            }
+            if (uint32_t(h) == kSampleType) {
+              if (q0 + kRecBytes > len || q0 + size > len) {
+                err = kErrTruncated;
+                break;
+              }
+              if (lane == 0) s_list[n] = (uint32_t)q0;
+              n++;
+            }
+            q0 += size;  // non-SAMPLE records are skipped by their size (:918)
+          }
+          if (lane == 0) {
+            if (err) set_error(p, d0.seq, (uint32_t)q0, err);
+            s_err = err;
+            s_nlist = n;
+            s_next = (uint32_t)min(q0, len);
+          }
+        }
+        __syncthreads();
+        const uint32_t n = __builtin_amdgcn_readfirstlane(s_nlist);
+        const uint32_t serr = __builtin_amdgcn_readfirstlane(s_err);
+        ncur = serr ? len : __builtin_amdgcn_readfirstlane(s_next);
+        if (ncur >= len) {
+          nidx = idx + 1;
+          ncur = 0;
+        }
+        valid = (uint32_t)tid < n;
+        roff = valid ? s_list[tid] : 0;
+        rin1 = false;
+        RawRec rr;
+        load_rec(base, roff, valid ? len : 0, rr);
+        rec = decode_rec(rr, roff);
+      }
+
+      // ---- descriptors of the next window (the one after it is read now
+      // and used a transition later), and its loads: issued before this
+      // window's records are processed -- unless a sorted batch waits for its
+      // chunk stores, which must go out before those loads (see
+      // route_write_batch); then the stores and the loads follow the
+      // processing, when the record's registers are free again
+      BufDesc nd0 = d0, nd1 = d1, nd2 = d2;
+      if (nidx == idx + 1) {
+        nd0 = d1;
+        nd1 = d2;
+        if (nidx + 2 < r1) nd2 = route_desc(rp, s_desc, r0, nidx + 2);
+      } else if (nidx == idx + 2) {
+        nd0 = d2;
+        if (nidx + 1 < r1) nd1 = route_desc(rp, s_desc, r0, nidx + 1);
+        if (nidx + 2 < r1) nd2 = route_desc(rp, s_desc, r0, nidx + 2);
+      }
+      const bool nhas1 = nidx + 1 < r1;
+      if (!wpending && nidx < r1) {
+        const RWin nl = rwin_lane(tid, (uint32_t)ncur, nd0, nd1, nhas1);
+        rload_slot(p.data, nl, nd0, nd1, nx);
+      }
+
+      // ---- this window's record: global counters, then its partition
+      rt_stamp<TIMING>(rt, 1);
+      const uint32_t acc_l = rin1 ? d1.access : d0.access;
+      Held hr;
+      hr.q = kNoChunk;
+      wave_global_count(&s_wacc[tid >> 6][0][0], s_sums, s_mins, s_maxs, valid, acc_l,
+                        uint32_t(rec.dsrc >> 5) & 0x3fff /* data_src.mem_lvl */, rec.w, lane);
+      rt_stamp<TIMING>(rt, 2);
+      uint32_t node = 0;
+      if (valid) {
+        // partition = the last partition whose first key <= addr; below the
+        // first key nothing can match (ht_lower_key finds no node)
+        const uint32_t i = eytz_descend(s_bounds, kPartLevels, rec.addr);
+        node = i >> (__builtin_ctz(i) + 1);
+      }
+      if (TIMING) (void)__builtin_amdgcn_readfirstlane(__ballot(node != 0));  // (the search ends here)
+      rt_stamp<TIMING>(rt, 3);
+      if (valid) {
+        if (node) {
+          const uint32_t q = min(eytz_rank(node, kPartLevels), P - 1);
+          const uint32_t rk = atomicAdd(&s_hist[q], 1u);
+          hr.q = q | (rk << 11);
+          hr.a = make_uint4((uint32_t)rec.addr, (uint32_t)(rec.addr >> 32), (uint32_t)rec.ts, (uint32_t)(rec.ts >> 32));
+          const uint32_t g = rin1 ? d1.pad : d0.pad;
+          const uint32_t th = rin1 ? d1.thread_rank : d0.thread_rank;
+          hr.x = x_encode(rp.xl, g, roff, th, acc_l, rec.w);
+        }
+      }
+#pragma unroll
+      for (int b = (int)kRouteWindows - 1; b > 0; b--) held[b] = held[b - 1];
+      held[0] = hr;
+      if (wpending) {  // the previous batch's chunk stores, then the next window's loads
+        route_write_batch<TIMING>(rt, rp, tid, L, nbatches - 1);
+        wpending = false;
+        if (nidx < r1) {
+          const RWin nl = rwin_lane(tid, (uint32_t)ncur, nd0, nd1, nhas1);
+          rload_slot(p.data, nl, nd0, nd1, nx);
+        }
+      }
+      {
+        // per-buffer SAMPLE tallies (mem_sampling.c:921-926): lanes of this
+        // wave in buffer idx + 1 are tid >= n0
+        const uint64_t vm = __ballot(valid);
+        const uint32_t w0 = uint32_t(tid) & ~63u;
+        const uint64_t m1 = ((f & 1) || wl.n0 >= w0 + 64) ? 0ull : (wl.n0 <= w0 ? ~0ull : (~0ull << (wl.n0 - w0)));
+        ns0 += (uint32_t)__popcll(vm & ~m1);
+        ns1 += (uint32_t)__popcll(vm & m1);
+      }
+      if (nidx != idx) {
+        if (lane == 0) {
+          if (ns0) atomicAdd(p.bufcnt + d0.pad, ns0);
+          if (nidx == idx + 2 && ns1) atomicAdd(p.bufcnt + d1.pad, ns1);
+        }
+        ns0 = nidx == idx + 1 ? ns1 : 0;
+        ns1 = 0;
+      }
+      const bool last = nidx >= r1;
+      rt_stamp<TIMING>(rt, 4);
+      if (p.flags & kDbgRouteNoBatch) {  // (ablation) forget the held records
+        if (++bwin == kRouteWindows || last) {
+          __syncthreads();
+          for (uint32_t q = tid; q < P; q += kWG) s_hist[q] = 0;
+#pragma unroll
+          for (int b = 0; b < (int)kRouteWindows; b++) held[b].q = kNoChunk;
+          bwin = 0;
+        }
+      } else if (++bwin == kRouteWindows || last) {
+        route_sort_batch<TIMING>(rt, rp, held, tid, L, nbatches, c0, cap);
+        bwin = 0;
+        nbatches++;
+        if (last) route_write_batch<TIMING>(rt, rp, tid, L, nbatches - 1);
+        else wpending = true;
+      }
+      idx = nidx;
+      cur = (uint32_t)ncur;
+      d0 = nd0;
+      d1 = nd1;
+      d2 = nd2;
+      has1 = nhas1;
+      if (last) break;
+    }
+    if (TIMING && lane == 0) {
+      unsigned long long* o = p.dbg + (uint64_t(blockIdx.x) * (kWG / 64) + tid / 64) * kRouteTimingWords;
+      for (int k = 0; k < 9; k++) o[k] = rt.acc[k];
+      o[9] = win;
+      o[10] = nbatches;
+    }
+  }
+  __syncthreads();
+  // the waves' blocks into the workgroup's counters (sums; the three hit buckets' min / max)
+  if (tid < 2 * 9) {
+    const uint32_t a = tid / 9, k = tid % 9;  // tc, tw, na, 3 x (count, sum)
+    unsigned long long v = 0;
+    for (int wv = 0; wv < kWG / 64; wv++) v += s_wacc[wv][a][k];
+    s_sums[a][k] += v;  // (word k of struct mem_counters' order: 0..2, then 3 + 2b / 4 + 2b for b < 3)
+  }
+  __syncthreads();
+  // global mem_counters of both access types
+#pragma unroll
+  for (uint32_t a = 0; a < 2; a++) {
+    if (tid < (int)kGlobalSums && s_sums[a][tid])
+      atomicAdd(reinterpret_cast<unsigned long long*>(p.sum64 + gsum_index(a, tid)), s_sums[a][tid]);
+    if (tid < 18 && s_sums[a][3 + 2 * tid]) {
+      atomicMin(reinterpret_cast<unsigned long long*>(p.min64 + a * 18 + tid), s_mins[a][tid]);
+      atomicMax(reinterpret_cast<unsigned long long*>(p.max64 + a * 18 + tid), s_maxs[a][tid]);
+    }
+  }
+  // open chunks' fill, chunk counts per partition, pool use
+  for (uint32_t q = tid; q < P; q += kWG) {
+    const uint32_t cur = s_cur[nbatches & 1][q];
+    if ((cur & 127u) < kChunk) rp.cmeta[cur >> 7] = q | ((cur & 127u) << 24);
+  }
+  if (tid == 0) rp.used[blockIdx.x] = min(min(s_misc[1], cap), s_misc[2]);
+}
+
+// ---------------------------------------------------------------------------
+// records that found no chunk (a workgroup's samples outgrew its pool:
+// SAMPLE records shorter than 40 B, or the kDbgTinyPool switch): attributed
+// one by one with global lookups and atomics
+
+__global__ __launch_bounds__(256) void overflow_kernel(RouteParams rp) {
+  const uint32_t n = min(*rp.ovf_cnt, rp.ovf_cap);
+  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+    const uint4 a = rp.ovf16[i];
+    const XRec xr = x_decode(rp.xl, rp.ovfx[i]);
+    direct_attribute(rp.p, u64of(a.x, a.y), u64of(a.z, a.w), x_weight(rp.xl, xr, rp.p.data, rp.p.sbufs), xr.th,
+                     xr.acc, rp.seq0 + xr.g, xr.off, xr.g);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// pass 2: count, plan (one workgroup) and scatter
+
+// chunks per (route workgroup, partition) from the chunks' partition tags
+__global__ __launch_bounds__(kWG) void count_kernel(ScatterParams r) {
+  __shared__ uint32_t s_cnt[kMaxParts + 1];
+  const uint32_t tid = threadIdx.x, w = blockIdx.x, P = r.nparts;
+  for (uint32_t q = tid; q < P; q += kWG) s_cnt[q] = 0;
+  __syncthreads();
+  const uint32_t c0 = r.chunk0[w], n = r.used[w];
+  for (uint32_t c = c0 + tid; c < c0 + n; c += kWG) atomicAdd(&s_cnt[r.cmeta[c] & 0xffffffu], 1u);
+  __syncthreads();
+  uint32_t* out = const_cast<uint32_t*>(r.pcnt) + uint64_t(w) * P;
+  for (uint32_t q = tid; q < P; q += kWG) out[q] = s_cnt[q];
+}
+
+__global__ __launch_bounds__(kWG) void plan_kernel(PlanParams r) {
+  __shared__ uint32_t s_tot[kMaxParts + 1], s_nit[kMaxParts + 1], s_wsum[2][kWG / 64];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const uint32_t P = r.nparts;
+  for (uint32_t q = tid; q < P; q += kWG) {  // per partition: exclusive prefix over the workgroups
+    uint32_t run = 0;
+    constexpr uint32_t kU = 16;  // loads of kU workgroups in flight before their prefixes are stored
+    for (uint32_t w0 = 0; w0 < r.grid; w0 += kU) {
+      uint32_t v[kU];
+#pragma unroll
+      for (uint32_t u = 0; u < kU; u++) v[u] = w0 + u < r.grid ? r.pcnt[uint64_t(w0 + u) * P + q] : 0u;
+#pragma unroll
+      for (uint32_t u = 0; u < kU; u++) {
+        if (w0 + u < r.grid) r.pcnt[uint64_t(w0 + u) * P + q] = run;
+        run += v[u];
+      }
+    }
+    s_tot[q] = run;
+    s_nit[q] = (run + kItemChunks - 1) / kItemChunks;
+  }
+  __syncthreads();
+  // exclusive scans of the chunk totals and the item counts (two per thread)
+  const uint32_t i0 = 2 * (uint32_t)tid;
+  const uint32_t t0 = i0 < P ? s_tot[i0] : 0u, t1 = i0 + 1 < P ? s_tot[i0 + 1] : 0u;
+  const uint32_t n0 = i0 < P ? s_nit[i0] : 0u, n1 = i0 + 1 < P ? s_nit[i0 + 1] : 0u;
+  uint32_t it = t0 + t1, in = n0 + n1;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t a = __shfl_up(it, o, 64), b = __shfl_up(in, o, 64);
+    if (lane >= o) {
+      it += a;
+      in += b;
+    }
+  }
+  if (lane == 63) {
+    s_wsum[0][wave] = it;
+    s_wsum[1][wave] = in;
+  }
+  __syncthreads();
+  uint32_t wt = 0, wn = 0;
+  for (int w2 = 0; w2 < wave; w2++) {
+    wt += s_wsum[0][w2];
+    wn += s_wsum[1][w2];
+  }
+  const uint32_t tb = wt + it - (t0 + t1), nb = wn + in - (n0 + n1);
+  for (uint32_t k = 0; k < 2; k++) {
+    const uint32_t q = i0 + k;
+    if (q >= P) break;
+    const uint32_t base = tb + (k ? t0 : 0u), ibase = nb + (k ? n0 : 0u), tot = k ? t1 : t0;
+    r.pbase[q] = base;
+    for (uint32_t j = 0; j * kItemChunks < tot; j++)
+      r.items[ibase + j] = make_uint4(q, base + j * kItemChunks, base + min(tot, (j + 1) * kItemChunks), 0);
+  }
+  if (tid == kWG - 1) {
+    r.ctl[0] = wn + in;
+    r.ctl[1] = 0;
+    r.ctl[2] = 0;  // overflow list (read by overflow_kernel before this launch)
+  }
+}
+
+__global__ __launch_bounds__(kWG) void scatter_kernel(ScatterParams r) {
+  __shared__ uint32_t s_cnt[kMaxParts + 1];
+  const uint32_t tid = threadIdx.x, w = blockIdx.x, P = r.nparts;
+  for (uint32_t q = tid; q < P; q += kWG) s_cnt[q] = 0;
+  __syncthreads();
+  const uint32_t c0 = r.chunk0[w], n = r.used[w];
+  const uint32_t* off = r.pcnt + uint64_t(w) * P;
+  for (uint32_t c = c0 + tid; c < c0 + n; c += kWG) {
+    const uint32_t m = r.cmeta[c], q = m & 0xffffffu;
+    const uint32_t k = atomicAdd(&s_cnt[q], 1u);
+    r.clist[r.pbase[q] + off[q] + k] = c | ((m >> 24) << kChunkIdBits);  // chunk id | fill
+  }
+}
+
+// ---------------------------------------------------------------------------
+// pass 3: attribute one partition per workgroup at a time
+
+__global__ __launch_bounds__(kWG, 1) void local_kernel(LocalParams lp) {
+  __shared__ uint64_t s_keys[kPartSlots];
+  __shared__ uint4 s_nodes[2 * kPartSlots];
+  __shared__ uint2 s_info[kPartSlots];
+  __shared__ unsigned long long s_owt[2][kPartEntries];
+  __shared__ unsigned long long s_first[kPartEntries];
+  __shared__ uint32_t s_pg[kPartCells / 2];
+  __shared__ uint32_t s_item;
+
+  Params& p = lp.p;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const uint32_t nitems = lp.ctl[0];
+  const uint32_t T = p.nb_threads;
+  const bool pages = (p.flags & NMG_F_PAGE_HIST) != 0;
+  while (true) {
+    if (tid == 0) s_item = atomicAdd(lp.ctl + 1, 1u);
+    __syncthreads();
+    const uint32_t it = __builtin_amdgcn_readfirstlane(s_item);
+    if (it >= nitems) break;
+    const uint4 item = lp.items[it];
+    const uint32_t q = __builtin_amdgcn_readfirstlane(item.x);
+    const PartInfo pi = lp.parts[q];
+    const uint32_t levels = __builtin_amdgcn_readfirstlane(pi.levels);
+    {
+      const uint32_t ns = 1u << levels;
+      const uint64_t* gk = lp.pe_keys + uint64_t(q) * kPartSlots;
+      const uint4* gn = lp.pe_nodes + uint64_t(q) * kPartSlots * 2;
+      const uint2* gi = lp.pe_info + uint64_t(q) * kPartSlots;
+      for (uint32_t i = tid; i < ns; i += kWG) {
+        s_keys[i] = gk[i];
+        s_nodes[2 * i] = gn[2 * i];
+        s_nodes[2 * i + 1] = gn[2 * i + 1];
+        s_info[i] = gi[i];
+      }
+    }
+    for (uint32_t i = tid; i < pi.ne; i += kWG) {
+      s_owt[0][i] = s_owt[1][i] = 0;
+      s_first[i] = ~0ull;
+    }
+    const uint32_t ncell = (pages && pi.pages_lds) ? T * pi.span : 0u;
+    for (uint32_t i = tid; i < (ncell + 1) / 2; i += kWG) s_pg[i] = 0;
+    __syncthreads();
+
+    // each wave takes every 16th chunk of the item; the next chunk's records
+    // and the list entry after it are in flight while a chunk is processed
+    constexpr uint32_t kStride = kWG / 64;
+    const uint32_t l0 = item.y + (uint32_t)wave, l1 = item.z;
+    uint32_t ce = l0 < l1 ? lp.clist[l0] : 0u;
+    uint4 na16 = make_uint4(0, 0, 0, 0);
+    uint64_t nx = 0;
+    if (l0 < l1 && (uint32_t)lane < (ce >> kChunkIdBits)) {
+      const uint64_t k = uint64_t(ce & ((1u << kChunkIdBits) - 1)) * kChunk + lane;
+      na16 = lp.rec16[k];
+      nx = lp.recx[k];
+    }
+    uint32_t ce2 = l0 + kStride < l1 ? lp.clist[l0 + kStride] : 0u;
+    for (uint32_t l = l0; l < l1; l += kStride) {
+      const uint32_t c = ce & ((1u << kChunkIdBits) - 1), fill = ce >> kChunkIdBits;
+      const bool valid = (uint32_t)lane < fill;
+      const uint4 a16 = na16;
+      const uint64_t x = nx;
+      ce = ce2;
+      if (l + kStride < l1 && (uint32_t)lane < (ce >> kChunkIdBits)) {
+        const uint64_t k = uint64_t(ce & ((1u << kChunkIdBits) - 1)) * kChunk + lane;
+        na16 = lp.rec16[k];
+        nx = lp.recx[k];
+      }
+      ce2 = l + 2 * kStride < l1 ? lp.clist[l + 2 * kStride] : 0u;
+      const uint64_t addr = u64of(a16.x, a16.y), ts = u64of(a16.z, a16.w);
+      if (p.flags & kDbgLocalNoWork) {  // (ablation) loads only
+        if (lane == 0) lp.cmatch[c] = addr ^ ts ^ x;
+        continue;
+      }
+      // lower bound among the partition's keys (the record's address is >= its
+      // first key and < the next partition's): the node of the last right turn
+      const uint32_t i = eytz_descend(s_keys, levels, addr);
+      const uint32_t idx = i >> (__builtin_ctz(i) + 1);
+      int32_t erel = -1;
+      uint64_t baddr = 0;
+      uint32_t hrel = kEmpty32;
+      if (valid && idx) {
+        const uint4 na = s_nodes[2 * idx], nb = s_nodes[2 * idx + 1];
+        const uint2 inf = s_info[idx];
+        if (entry_match(na, nb, addr, ts)) {  // is_sample_in_buffer (mem_analyzer.c:141-155), newest entry
+          erel = (int32_t)(inf.y & 0x7fffffffu);
+          baddr = u64of(na.x, na.y);
+          hrel = inf.x;
+        } else if (inf.y >> 31) {  // older entries of a reused address (LIFO, tools/hash.c:108-114)
+          const uint32_t rank = min(eytz_rank(idx, levels), pi.nk - 1);  // (padding slots copy the last node)
+          const uint4 d = reinterpret_cast<const uint4*>(p.nodes + pi.k0 + rank)[3];  // (count, first)
+          Match m;
+          m.e = -1;
+          match_older(p, d.y, d.x, addr, ts, m);
+          if (m.e >= 0) {
+            erel = (int32_t)(m.e - pi.e0);
+            baddr = m.baddr;
+            hrel = m.hist == kHistSparse ? kEmpty32 : (uint32_t)(m.hist - pi.cb);
+          }
+        }
+      }
+      const uint64_t fm = __ballot(erel >= 0);
+      if (lane == 0) lp.cmatch[c] = fm;
+      if (erel < 0) continue;
+      const XRec xr = x_decode(lp.xl, x);
+      const uint64_t w = x_weight(lp.xl, xr, p.data, lp.descs);
+      if (w < kLaneMaxWeight) {
+        atomicAdd(&s_owt[xr.acc][erel], (1ull << kPackShift) | w);
+      } else {
+        const uint64_t e = pi.e0 + (uint32_t)erel;
+        atomicAdd(reinterpret_cast<unsigned long long*>(p.sum64 + objcw_index(e, xr.acc, 0, p.nb_entries)), 1ull);
+        atomicAdd(reinterpret_cast<unsigned long long*>(p.sum64 + objcw_index(e, xr.acc, 1, p.nb_entries)),
+                  (unsigned long long)w);
+      }
+      // first match in analysis order (quirk Q7)
+      const unsigned long long ord = ((lp.seq0 + xr.g) << 32) | xr.off;
+      if (ord < s_first[erel]) atomicMin(&s_first[erel], ord);
+      if (pages) {
+        // ma_get_block: page_no = (int)((addr - buffer_addr) / 4096) (mem_analyzer.c:530-531)
+        const uint32_t page = uint32_t(int(uint64_t(addr - baddr) / kPageSize));
+        if (hrel != kEmpty32) {
+          const uint32_t rel = hrel + page;
+          if (ncell) {
+            const uint32_t li = xr.th * pi.span + rel;
+            atomicAdd(&s_pg[li >> 1], 1u << (16 * (li & 1)));
+          } else {
+            atomicAdd(p.hist + uint64_t(xr.th) * p.hist_cells + pi.cb + rel, 1u);
+          }
+        } else {
+          const uint32_t sidx = p.entries[pi.e0 + (uint32_t)erel].sidx;
+          if (sidx != ~0u) sparse_add(p, sparse_key(sidx, xr.th, page), lp.seq0 + xr.g, xr.off, 1u);
+        }
+      }
+    }
+    __syncthreads();
+    // the item's counters to global memory: consecutive lanes, consecutive words
+    for (uint32_t i = tid; i < pi.ne; i += kWG) {
+      const uint64_t e = pi.e0 + i;
+#pragma unroll
+      for (uint32_t a = 0; a < 2; a++) {
+        const uint64_t v = s_owt[a][i];
+        if (!v) continue;
+        atomicAdd(reinterpret_cast<unsigned long long*>(p.sum64 + objcw_index(e, a, 0, p.nb_entries)),
+                  (unsigned long long)(v >> kPackShift));
+        const uint64_t wt = v & ((1ull << kPackShift) - 1);
+        if (wt)
+          atomicAdd(reinterpret_cast<unsigned long long*>(p.sum64 + objcw_index(e, a, 1, p.nb_entries)),
+                    (unsigned long long)wt);
+      }
+      const uint64_t fo = s_first[i];
+      if (fo != ~0ull) atomicMin(reinterpret_cast<unsigned long long*>(p.min64 + 36 + e), (unsigned long long)fo);
+    }
+    for (uint32_t j = tid; j < (ncell + 1) / 2; j += kWG) {
+      const uint32_t v = s_pg[j];
+      if (!v) continue;
+#pragma unroll
+      for (uint32_t h = 0; h < 2; h++) {
+        const uint32_t cnt = (v >> (16 * h)) & 0xffffu;
+        if (!cnt) continue;
+        const uint32_t li = 2 * j + h, th = li / pi.span, rel = li - th * pi.span;
+        atomicAdd(p.hist + uint64_t(th) * p.hist_cells + pi.cb + rel, cnt);
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------
+// per-buffer matched-sample counts from the match bits (one workgroup per
+// route workgroup: its chunks hold only its own buffers' records)
+
+__global__ __launch_bounds__(kWG) void found_kernel(FoundParams r) {
+  __shared__ uint32_t s_found[kFoundLds];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const uint32_t w = blockIdx.x;
+  const uint32_t g0 = r.ranges[w], nbuf = r.ranges[w + 1] - g0, nl = min(nbuf, kFoundLds);
+  for (uint32_t i = tid; i < nl; i += kWG) s_found[i] = 0;
+  __syncthreads();
+  const uint64_t k0 = uint64_t(r.chunk0[w]) * kChunk, k1 = k0 + uint64_t(r.used[w]) * kChunk;
+  const uint64_t gmask = (1ull << r.gbits) - 1;
+  // one record per lane, a chunk per wave-instruction: the bit word is a
+  // wave-uniform load, the X words stream (bits past a chunk's fill are 0)
+  constexpr int kU = 4;
+  for (uint64_t k = k0 + tid; k < k1; k += kU * kWG) {
+    uint64_t bits[kU], xw[kU];
+#pragma unroll
+    for (int u = 0; u < kU; u++) {
+      const uint64_t kk = k + u * kWG;
+      bits[u] = kk < k1 ? r.cmatch[kk / kChunk] : 0ull;
+      xw[u] = ((bits[u] >> lane) & 1) ? r.recx[kk] : 0ull;
+    }
+#pragma unroll
+    for (int u = 0; u < kU; u++) {
+      if (!((bits[u] >> lane) & 1)) continue;
+      const uint32_t g = (uint32_t)(xw[u] & gmask);
+      if (g - g0 < nl) atomicAdd(&s_found[g - g0], 1u);
+      else atomicAdd(r.bufcnt + r.nb_bufs + g, 1u);
+    }
+  }
+  __syncthreads();
+  for (uint32_t i = tid; i < nl; i += kWG)
+    if (s_found[i]) atomicAdd(r.bufcnt + r.nb_bufs + g0 + i, s_found[i]);
+}
+
+// ---------------------------------------------------------------------------
+// launchers
+
+hipError_t launch_route(uint32_t grid, hipStream_t s, const RouteParams& r) {
+  if (r.p.flags & kDbgRouteTiming) hipLaunchKernelGGL(route_kernel<true>, dim3(grid), dim3(kWG), 0, s, r);
+  else hipLaunchKernelGGL(route_kernel<false>, dim3(grid), dim3(kWG), 0, s, r);
+  return hipGetLastError();
+}
+
+hipError_t launch_plan(hipStream_t s, const PlanParams& r) {
+  hipLaunchKernelGGL(plan_kernel, dim3(1), dim3(kWG), 0, s, r);
+  return hipGetLastError();
+}
+
+hipError_t launch_overflow(hipStream_t s, const RouteParams& r) {
+  hipLaunchKernelGGL(overflow_kernel, dim3(1024), dim3(256), 0, s, r);
+  return hipGetLastError();
+}
+
+hipError_t launch_count(uint32_t grid, hipStream_t s, const ScatterParams& r) {
+  hipLaunchKernelGGL(count_kernel, dim3(grid), dim3(kWG), 0, s, r);
+  return hipGetLastError();
+}
+
+hipError_t launch_scatter(uint32_t grid, hipStream_t s, const ScatterParams& r) {
+  hipLaunchKernelGGL(scatter_kernel, dim3(grid), dim3(kWG), 0, s, r);
+  return hipGetLastError();
+}
+
+hipError_t launch_local(uint32_t grid, hipStream_t s, const LocalParams& r) {
+  hipLaunchKernelGGL(local_kernel, dim3(grid), dim3(kWG), 0, s, r);
+  return hipGetLastError();
+}
+
+hipError_t launch_found(uint32_t grid, hipStream_t s, const FoundParams& r) {
+  hipLaunchKernelGGL(found_kernel, dim3(grid), dim3(kWG), 0, s, r);
+  return hipGetLastError();
+}
+
+}  // namespace nmg

@@ -33,6 +33,8 @@ class Engine:
                  devices=None):
         """devices: a list of GPU ordinals -> one engine sharding its host
         buffers over those GPUs (nmg_options.nb_gpus / devices)."""
+        if devices is not None and len(devices) == 1:  # one GPU: nmg_options.device (nb_gpus <= 1 ignores devices)
+            device, devices = int(devices[0]), None
         devs = (C.c_int32 * max(1, len(devices or [])))(*(devices or [device]))
         self._devs = devs
         opt = _lib.nmg_options(device, flags, nb_threads, copy_threads, hist_budget_bytes, sparse_capacity,

@@ -1,0 +1,120 @@
+"""The partition-first path for large tables (nmg_route.h) against the oracle
+and against the single-pass kernel: every raw counter, the reports.
+
+Large tables (> 1023 keys) take the partition-first passes by default; these
+tests pin the parts the other parity tests do not reach on purpose:
+
+* the pool-overflow path (internal switch 0x20000: private pools of two
+  chunks, so nearly every record goes through the overflow list and
+  overflow_kernel's global lookups);
+* analyses that accumulate without a reset (the per-buffer match counts of
+  one analysis are summed before the next one reuses the chunk pool);
+* partition shapes: many threads (page cells of a partition too many for
+  LDS: global atomics), objects larger than a partition's LDS cells, heavily
+  reused addresses (older entries), tiny buffers (more buffers than windows);
+* NMG_F_SINGLE_PASS gives the same results."""
+import os
+
+import numpy as np
+import pytest
+
+import pyoracle
+from numamma_amd import _lib
+from numamma_amd.replay import SynthConfig, generate
+from numamma_amd.results import RawResults
+
+pytestmark = pytest.mark.gpu
+
+NO_ROUTE = 0x10000
+TINY_POOL = 0x20000
+
+
+def _oracle(rp, d):
+    path = os.path.join(d, "replay.bin")
+    rp.write(path)
+    odir = os.path.join(d, "oracle")
+    pyoracle.run(path, odir, os.path.join(d, "oracle_stdout.txt"), os.path.join(d, "oracle_raw.bin"))
+    return path, odir
+
+
+def _engine(path, d, flags, tag):
+    from numamma_amd.engine import run_replay
+
+    edir = os.path.join(d, f"engine_{tag}")
+    raw = os.path.join(d, f"engine_{tag}_raw.bin")
+    run_replay(path, edir, os.path.join(d, f"engine_{tag}_stdout.txt"), raw, flags=flags)
+    return edir, raw
+
+
+def _same(a, b):
+    assert open(a, "rb").read() == open(b, "rb").read(), (a, b)
+
+
+def _same_dirs(a, b):
+    fa, fb = sorted(os.listdir(a)), sorted(os.listdir(b))
+    assert fa == fb
+    for f in fa:
+        _same(os.path.join(a, f), os.path.join(b, f))
+
+
+ROUTE_CASES = [
+    # LOST records, a wrapped ring, 8 threads
+    SynthConfig(nb_samples=400_000, nb_intervals=50_000, lost_frac=1e-3, wrap_one=True, seed=71),
+    # 64 threads: partitions' page cells exceed LDS (global cell atomics)
+    SynthConfig(nb_samples=300_000, nb_intervals=20_000, nb_threads=64, seed=72),
+    # objects up to 4 MiB: single keys with more cells than a partition's LDS
+    SynthConfig(nb_samples=300_000, nb_intervals=3_000, size_min=1 << 20, size_max=4 << 20, seed=73),
+    # heavy address reuse and reallocs: older entries of a node
+    SynthConfig(nb_samples=300_000, nb_intervals=10_000, reuse_frac=0.5, realloc_frac=0.2, seed=74),
+    # tiny buffers: more buffers than windows, windows across many buffers
+    SynthConfig(nb_samples=200_000, nb_intervals=5_000, buffer_records=7, seed=75),
+]
+
+
+@pytest.mark.parametrize("cfg", ROUTE_CASES, ids=[f"case{i}" for i in range(len(ROUTE_CASES))])
+@pytest.mark.parametrize("flags", [0, TINY_POOL, _lib.NMG_F_SINGLE_PASS], ids=["route", "tinypool", "single"])
+def test_route_bit_exact(tmp_path, cfg, flags):
+    d = str(tmp_path)
+    path, odir = _oracle(generate(cfg), d)
+    edir, raw = _engine(path, d, _lib.NMG_F_DEFAULT | flags, "e")
+    _same(os.path.join(d, "oracle_raw.bin"), raw)
+    _same(os.path.join(d, "oracle_stdout.txt"), os.path.join(d, "engine_e_stdout.txt"))
+    _same_dirs(odir, edir)
+
+
+def _results(eng):
+    g, ns, nf = eng.global_counters()
+    first, cw = eng.object_counters()
+    bs, bf = eng.buffer_counts()
+    return g, ns, nf, first, cw, bs, bf, eng.page_cells()
+
+
+@pytest.mark.parametrize("extra", [0, TINY_POOL])
+def test_route_accumulates_like_single_pass(extra):
+    """analyze, analyze (no reset), synchronize, analyze: the route path and
+    the single-pass kernel accumulate the same counters, per-buffer match
+    counts included; then a reset and one analysis equals the oracle run."""
+    import torch
+    from numamma_amd.engine import Engine
+
+    rp = generate(SynthConfig(nb_samples=500_000, nb_intervals=80_000, lost_frac=5e-4, seed=76))
+    arena, offs, lens, ranks, acc = rp.packed()
+    dev = torch.from_numpy(arena).cuda()
+    out = []
+    for flags in (_lib.NMG_F_DEFAULT | extra, _lib.NMG_F_DEFAULT | NO_ROUTE):
+        eng = Engine(flags=flags, nb_threads=rp.nb_threads)
+        eng.set_objects(rp.table)
+        eng.set_device_buffers(dev.data_ptr(), offs, lens, ranks, acc)
+        eng.analyze()
+        eng.analyze()
+        eng.synchronize()
+        eng.analyze()
+        res = _results(eng)
+        eng.reset()
+        eng.analyze()
+        out.append((res, _results(eng)))
+        eng.close()
+    (a3, a1), (b3, b1) = out
+    for x, y in zip(a3 + a1, b3 + b1):
+        assert np.array_equal(np.asarray(x), np.asarray(y))
+    assert a3[1] == 3 * a1[1] and a3[2] == 3 * a1[2]

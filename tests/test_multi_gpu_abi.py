@@ -73,3 +73,51 @@ def test_multi_gpu_rejects_device_buffers():
     with pytest.raises(_lib.NmgError):
         eng.stream_begin()
     eng.close()
+
+
+def _all(eng):
+    g, ns, nf = eng.global_counters()
+    first, cw = eng.object_counters()
+    bs, bf = eng.buffer_counts()
+    return [g, np.array([ns, nf]), first, cw, bs, bf, eng.page_cells()]
+
+
+@pytest.mark.parametrize("devices,flags", [([0, 0], 0), (None, 0x40000)], ids=["two_shards", "one_rank_rccl"])
+def test_multi_gpu_accumulates_like_one_engine(tmp_path, devices, flags):
+    """Two analyses without a reset, then a third after nmg_synchronize: a
+    multi-GPU handle accumulates every counter -- per-buffer sample / match
+    counts included -- exactly like a one-GPU engine; after a reset one
+    analysis equals the oracle.  `one_rank_rccl` (internal switch 0x40000) is
+    a multi-GPU handle with one worker whose merge takes the distinct-device
+    branch: librccl dlopen'ed, ncclCommInitAll over one device, the grouped
+    ncclReduce of every array to the root, then the device add."""
+    from numamma_amd.engine import Engine
+
+    d = str(tmp_path)
+    rp = generate(SynthConfig(nb_samples=150_000, nb_intervals=30_000, lost_frac=1e-3, seed=95))
+    path = os.path.join(d, "r.bin")
+    rp.write(path)
+    pyoracle.run(path, os.path.join(d, "o"), os.path.join(d, "o.txt"), os.path.join(d, "o_raw.bin"))
+    got = []
+    for kind in ("multi", "single"):
+        eng = (Engine(nb_threads=rp.nb_threads, devices=devices, flags=_lib.NMG_F_DEFAULT | flags) if kind == "multi"
+               else Engine(nb_threads=rp.nb_threads))
+        eng.set_objects(rp.table)
+        eng.submit_replay(rp)
+        eng.analyze()
+        eng.analyze()
+        eng.synchronize()
+        eng.analyze()
+        got.append(_all(eng))
+        if kind == "multi":
+            eng.reset()
+            eng.analyze()
+            eng.synchronize()
+            _check(d, eng, rp, "after reset")
+            eng.report(os.path.join(d, "e"), os.path.join(d, "e.txt"))
+            assert open(os.path.join(d, "o.txt"), "rb").read() == open(os.path.join(d, "e.txt"), "rb").read()
+        eng.close()
+    for a, b in zip(*got):
+        assert np.array_equal(a, b)
+    raw = RawResults.read(os.path.join(d, "o_raw.bin"))
+    assert got[0][1][0] == 3 * raw.nb_samples and got[0][1][1] == 3 * raw.nb_found

@@ -21,6 +21,13 @@ VARIANTS = {
     "match": 0x1,                       # + object counters
     "full_noflush": 0x3 | 0x400,        # LDS tables filled, never flushed to global
     "full": 0x3,                        # + page histogram (default product path)
+    # large tables: the partition-first path (nmg_route.h) and its parts
+    "legacy": 0x3 | 0x10000,            # attribute_kernel on a large table (kDbgNoRoute)
+    "route": 0x3,                       # route + plan + scatter + local (default for > 1023 keys)
+    "route_nopages": 0x1,               # ... without the page histogram
+    "route_noloc": 0x3 | 0x400000,      # local pass loads its chunks only
+    "route_nowrite": 0x3 | 0x100000 | 0x400000,  # batches sorted in LDS, no chunk stores (local: loads only)
+    "route_nobatch": 0x3 | 0x200000,    # stream + global counters + partition search + batch ranks only
 }
 
 WORKLOADS = {
