@@ -217,6 +217,7 @@ struct nmg_engine {
   uint64_t* d_pe_keys = nullptr;  // [nparts][kPartSlots]
   uint4* d_pe_nodes = nullptr;    // [nparts][kPartSlots][2]
   uint2* d_pe_info = nullptr;     // [nparts][kPartSlots]
+  uint32_t* d_pe_dir = nullptr;   // [nparts][kPartDir]
   uint4* d_rec16 = nullptr;       // chunk pool: [chunks][kChunk] (addr, ts) and X words
   unsigned long long* d_recx = nullptr;
   uint32_t* d_cmeta = nullptr;
@@ -346,6 +347,8 @@ static void free_route_table(nmg_engine* h) {
   (void)hipFree(h->d_pe_keys);
   (void)hipFree(h->d_pe_nodes);
   (void)hipFree(h->d_pe_info);
+  (void)hipFree(h->d_pe_dir);
+  h->d_pe_dir = nullptr;
   h->d_parts = nullptr;
   h->d_pbounds = nullptr;
   h->d_pe_keys = nullptr;
@@ -791,28 +794,43 @@ static int build_partitions(nmg_engine* h, const uint64_t* keys, const uint32_t*
     pi.cb = cb == ~0ull ? 0 : cb;
     pi.span = cb == ~0ull ? 0 : (uint32_t)(ce - cb);
     pi.pages_lds = pi.span && (uint64_t)pi.span * T <= kPartCells;
-    while (((1u << pi.levels) - 1) < pi.nk) pi.levels++;
+    const uint64_t kspan = keys[k - 1] - keys[pi.k0];
+    while (pi.dshift < 63 && (kspan >> pi.dshift) >= kPartDir) pi.dshift++;
     parts.push_back(pi);
     if (parts.size() > kMaxParts) return NMG_OK;  // too many partitions for the route pass's LDS tree
   }
   const uint32_t P = (uint32_t)parts.size();
-  // per partition: keys, newest-entry node records and info in Eytzinger order;
-  // slots past the last key hold ~0 keys with a copy of the last node
+  // per partition: keys ascending with their newest entry's node record and
+  // info, and a directory over the key span: slot j starts at first key + (j
+  // << dshift) and holds the index of the largest key <= that start and the
+  // number of keys inside the slot (the last slot: every key after its start)
   std::vector<uint64_t> pk((size_t)P * kPartSlots, ~0ull);
   std::vector<uint4> pn((size_t)P * kPartSlots * 2, make_uint4(0, 0, 0, 0));
   std::vector<uint2> pinf((size_t)P * kPartSlots, make_uint2(kEmpty32, 0));
+  std::vector<uint32_t> pdir((size_t)P * kPartDir, 0);
   for (uint32_t q = 0; q < P; q++) {
     const PartInfo& pi = parts[q];
-    eytz_inorder(pi.levels, [&](uint32_t slot, uint32_t r) {
-      const uint32_t kk = pi.k0 + std::min(r, pi.nk - 1);
+    for (uint32_t r = 0; r < pi.nk; r++) {
+      const uint32_t kk = pi.k0 + r;
       const DevEntry& d = dev[entry_off[kk]];
-      const size_t o = (size_t)q * kPartSlots + slot;
-      pk[o] = r < pi.nk ? keys[kk] : ~0ull;
+      const size_t o = (size_t)q * kPartSlots + r;
+      pk[o] = keys[kk];
       pn[2 * o] = make_uint4((uint32_t)d.addr, (uint32_t)(d.addr >> 32), (uint32_t)d.end, (uint32_t)(d.end >> 32));
       pn[2 * o + 1] = make_uint4((uint32_t)d.alloc, (uint32_t)(d.alloc >> 32), (uint32_t)d.free, (uint32_t)(d.free >> 32));
       const uint32_t older = entry_off[kk + 1] - entry_off[kk] > 1 ? 0x80000000u : 0u;
       pinf[o] = make_uint2(d.hist == kHistSparse ? kEmpty32 : (uint32_t)(d.hist - pi.cb), (entry_off[kk] - pi.e0) | older);
-    });
+    }
+    const uint64_t f = keys[pi.k0];
+    uint32_t lo = 0;
+    for (uint32_t j = 0; j < kPartDir; j++) {
+      const uint64_t s0 = (uint64_t)j << pi.dshift;  // slot start relative to the first key
+      while (lo + 1 < pi.nk && keys[pi.k0 + lo + 1] - f <= s0) lo++;
+      uint32_t c = 0;
+      while (lo + 1 + c < pi.nk &&
+             (j == kPartDir - 1 || keys[pi.k0 + lo + 1 + c] - f < s0 + (1ull << pi.dshift)))
+        c++;
+      pdir[(size_t)q * kPartDir + j] = lo | (c << 16);
+    }
   }
   // the route pass's tree: the partitions' first keys
   std::vector<uint64_t> pb(1u << kPartLevels, ~0ull);
@@ -824,6 +842,7 @@ static int build_partitions(nmg_engine* h, const uint64_t* keys, const uint32_t*
   HIP_TRY(h, alloc_copy(h, (void**)&h->d_pe_keys, pk.data(), pk.size() * 8));
   HIP_TRY(h, alloc_copy(h, (void**)&h->d_pe_nodes, pn.data(), pn.size() * sizeof(uint4)));
   HIP_TRY(h, alloc_copy(h, (void**)&h->d_pe_info, pinf.data(), pinf.size() * sizeof(uint2)));
+  HIP_TRY(h, alloc_copy(h, (void**)&h->d_pe_dir, pdir.data(), pdir.size() * 4));
   HIP_TRY(h, hipStreamSynchronize(h->stream));  // (pageable sources)
   h->nparts = P;
   h->route_ok = true;
@@ -1665,15 +1684,15 @@ static uint32_t bits_for(uint64_t v) {  // smallest b with v < 2^b
 }
 
 // X word layout of the current buffers; false when the weight field would
-// be narrower than 16 bits (escapes would be common)
+// be narrower than 12 bits (escapes would be common)
 static bool route_layout(nmg_engine* h, XLayout& xl) {
   uint64_t maxlen = 1;
   for (const BufDesc& d : h->descs) maxlen = std::max<uint64_t>(maxlen, d.len);
   xl.gbits = bits_for(h->descs.size() - 1);
   xl.obits = bits_for((maxlen - 1) / 8);
   xl.tbits = bits_for(h->T - 1);
-  xl.wshift = xl.gbits + xl.obits + xl.tbits + 1;
-  if (xl.wshift > 64 - 16) return false;
+  xl.wshift = xl.gbits + xl.obits + xl.tbits + 1 + 14;  // (+ access bit, data_src.mem_lvl)
+  if (xl.wshift > 64 - 12) return false;
   xl.wesc = (1ull << (64 - xl.wshift)) - 1;
   return true;
 }
@@ -1815,6 +1834,7 @@ static int route_analyze(nmg_engine* h, uint32_t nb, uint32_t grid) {
   lp.pe_keys = h->d_pe_keys;
   lp.pe_nodes = h->d_pe_nodes;
   lp.pe_info = h->d_pe_info;
+  lp.pe_dir = h->d_pe_dir;
   lp.rec16 = h->d_rec16;
   lp.recx = h->d_recx;
   lp.cmeta = h->d_cmeta;

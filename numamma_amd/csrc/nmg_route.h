@@ -8,10 +8,9 @@
 // address range, then attributes each range with its slice of the table in
 // LDS:
 //   1. route_kernel   streams the buffers in analysis order (the byte cursor of
-//                     __analyze_buffer, mem_sampling.c:815-927), does the global
-//                     counters (update_counters, :508-592) and the per-buffer
-//                     sample counts, and appends a 24 B compact record of every
-//                     SAMPLE to a chunk of its partition (partition = a run of
+//                     __analyze_buffer, mem_sampling.c:815-927), counts the
+//                     SAMPLEs per buffer, and appends a 24 B compact record of
+//                     every SAMPLE to a chunk of its partition (partition = a run of
 //                     <= kPartKeys consecutive keys; chunks of kChunk records
 //                     from the workgroup's private pool);
 //      overflow_kernel  the records a full pool turned away, with global lookups;
@@ -22,7 +21,8 @@
 //                     workgroup at a time: the partition's keys and node records
 //                     in an LDS Eytzinger tree, its object and page counters in
 //                     LDS, flushed once per item (__match_sample, :594-673;
-//                     ma_get_block, mem_analyzer.c:494-534);
+//                     ma_get_block, mem_analyzer.c:494-534), and the global
+//                     counters of every record (update_counters, :508-592);
 //   5. found_kernel   per-buffer matched-sample counts from the match bits
 //                     local_kernel leaves per chunk (on demand: the reference
 //                     only sums them, mem_sampling.c:334-335, 357-361).
@@ -35,9 +35,9 @@ namespace nmg {
 constexpr uint32_t kChunk = 64;            // compact records per chunk (one wave processes one chunk)
 constexpr uint32_t kPartLevels = 11;       // route pass: Eytzinger tree of partition starts in LDS
 constexpr uint32_t kMaxParts = (1u << kPartLevels) - 1;
-constexpr uint32_t kPartKeyLevels = 10;    // local pass: <= 1023 keys per partition in LDS
-constexpr uint32_t kPartKeys = (1u << kPartKeyLevels) - 1;
-constexpr uint32_t kPartSlots = 1u << kPartKeyLevels;  // Eytzinger slots per partition (index 0 unused)
+constexpr uint32_t kPartKeys = 1023;       // local pass: keys per partition in LDS (sorted)
+constexpr uint32_t kPartSlots = 1024;      // per-partition table stride
+constexpr uint32_t kPartDir = 1024;        // directory slots per partition (radix over its key span)
 constexpr uint32_t kPartEntries = 1536;    // entries per partition (LDS object counters)
 constexpr uint32_t kPartCells = 28672;     // u16 page cells per partition: nb_threads x cell span
 constexpr uint32_t kRouteWindows = 3;      // windows per LDS sort batch of the route pass
@@ -58,6 +58,10 @@ constexpr uint32_t kDbgRouteNoWrite = 0x100000;  // route pass: batches sorted i
 constexpr uint32_t kDbgRouteNoBatch = 0x200000;  // route pass: no batch sort or stores at all
 constexpr uint32_t kDbgLocalNoWork = 0x400000;   // local pass: chunk loads only
 constexpr uint32_t kDbgRouteTiming = 0x800000;   // route pass: per-wave phase cycles in Params::dbg
+constexpr uint32_t kDbgLocalNoObj = 0x1000000;   // local pass: no object counters / first ordinals
+constexpr uint32_t kDbgLocalNoPage = 0x2000000;  // local pass: no page cells
+constexpr uint32_t kDbgLocalNoGlobal = 0x4000000;  // local pass: no global counters
+constexpr uint32_t kDbgLocalNoSearch = 0x8000000;  // local pass: no lookup (nothing matches)
 constexpr int kRouteTimingWords = 12;            // wait+barrier, issue, global, search, rank, scan, alloc+stage, write,
                                                  // state, windows, batches, -
 
@@ -68,17 +72,18 @@ struct PartInfo {
   uint32_t k0, nk, e0, ne;
   uint64_t cb;
   uint32_t span;
-  uint32_t levels;     // Eytzinger levels of the partition's tree (nk <= 2^levels - 1)
+  uint32_t dshift;     // directory slot j covers [first key + (j << dshift), + 2^dshift)
   uint32_t pages_lds;  // nb_threads * span <= kPartCells: page cells in LDS, else global atomics
   uint32_t pad[3];
 };
 static_assert(sizeof(PartInfo) == 48, "PartInfo");
 
-// compact record X word: g | off8 << gbits | thread << (gbits + obits) |
-// access << (gbits + obits + tbits) | min(weight, escape) << xw_shift
+// compact record X word, from bit 0: buffer index g (gbits), byte offset / 8
+// (obits), thread rank (tbits), access type (1), data_src.mem_lvl (14),
+// min(weight, wesc) (the rest, from bit wshift)
 struct XLayout {
   uint32_t gbits, obits, tbits, wshift;
-  uint64_t wesc;  // 2^wbits - 1: the weight is re-read from the record
+  uint64_t wesc;  // 2^(64 - wshift) - 1: the weight is re-read from the record
 };
 
 struct RouteParams {
@@ -120,9 +125,10 @@ struct ScatterParams {
 struct LocalParams {
   Params p;                  // table (nodes, chain, entries), counters, hist, sparse, flags
   const PartInfo* parts;
-  const uint64_t* pe_keys;   // [nparts][kPartSlots] Eytzinger keys, ~0 padding
-  const uint4* pe_nodes;     // [nparts][kPartSlots][2] (addr, end), (alloc, free)
+  const uint64_t* pe_keys;   // [nparts][kPartSlots] keys, ascending
+  const uint4* pe_nodes;     // [nparts][kPartSlots][2] (addr, end), (alloc, free) of each key's newest entry
   const uint2* pe_info;      // [nparts][kPartSlots] (cell - cb or ~0, entry - e0 | older entries << 31)
+  const uint32_t* pe_dir;    // [nparts][kPartDir] largest key index <= slot start | keys inside the slot << 16
   const uint4* rec16;
   const unsigned long long* recx;
   const uint32_t* cmeta;

@@ -28,15 +28,15 @@ __device__ __forceinline__ uint32_t eytz_rank(uint32_t idx, uint32_t levels) {
 // compact records: (addr, timestamp) + X (see XLayout)
 
 struct XRec {
-  uint32_t g, off, th, acc;
+  uint32_t g, off, th, acc, lvl;
   uint64_t wq;
 };
 
 __device__ __forceinline__ uint64_t x_encode(const XLayout& xl, uint32_t g, uint32_t off, uint32_t th, uint32_t acc,
-                                             uint64_t w) {
+                                             uint32_t lvl, uint64_t w) {
   const uint64_t wq = w < xl.wesc ? w : xl.wesc;
   return uint64_t(g) | (uint64_t(off >> 3) << xl.gbits) | (uint64_t(th) << (xl.gbits + xl.obits)) |
-         (uint64_t(acc) << (xl.wshift - 1)) | (wq << xl.wshift);
+         (uint64_t(acc) << (xl.wshift - 15)) | (uint64_t(lvl) << (xl.wshift - 14)) | (wq << xl.wshift);
 }
 
 __device__ __forceinline__ XRec x_decode(const XLayout& xl, uint64_t x) {
@@ -44,7 +44,8 @@ __device__ __forceinline__ XRec x_decode(const XLayout& xl, uint64_t x) {
   r.g = (uint32_t)(x & ((1ull << xl.gbits) - 1));
   r.off = (uint32_t)((x >> xl.gbits) & ((1ull << xl.obits) - 1)) << 3;
   r.th = (uint32_t)((x >> (xl.gbits + xl.obits)) & ((1ull << xl.tbits) - 1));
-  r.acc = (uint32_t)((x >> (xl.wshift - 1)) & 1);
+  r.acc = (uint32_t)((x >> (xl.wshift - 15)) & 1);
+  r.lvl = (uint32_t)((x >> (xl.wshift - 14)) & 0x3fff);
   r.wq = x >> xl.wshift;
   return r;
 }
@@ -65,7 +66,22 @@ __device__ __forceinline__ uint64_t x_weight(const XLayout& xl, const XRec& r, c
 // only taken when a workgroup's samples outgrow its pool (SAMPLE records
 // shorter than 40 B, or the kDbgTinyPool test switch).
 __device__ __forceinline__ void direct_attribute(const Params& p, uint64_t addr, uint64_t ts, uint64_t w, uint32_t th,
-                                                 uint32_t acc, uint64_t seq, uint32_t off, uint32_t slot) {
+                                                 uint32_t acc, uint32_t lvl, uint64_t seq, uint32_t off,
+                                                 uint32_t slot) {
+  // update_counters(global_counters, ...) (mem_sampling.c:517-592), global atomics
+  {
+    unsigned long long* S = reinterpret_cast<unsigned long long*>(p.sum64 + gsum_index(acc, 0));
+    atomicAdd(&S[0], 1ull);
+    if (w) atomicAdd(&S[1], (unsigned long long)w);
+    if (lvl & LVL_NA) atomicAdd(&S[2], 1ull);
+    for (uint32_t m = bucket_mask(lvl); m; m &= m - 1) {
+      const uint32_t b = (uint32_t)__builtin_ctz(m);
+      atomicAdd(&S[3 + 2 * b], 1ull);
+      if (w) atomicAdd(&S[4 + 2 * b], (unsigned long long)w);
+      atomicMin(reinterpret_cast<unsigned long long*>(p.min64 + acc * 18 + b), (unsigned long long)w);
+      atomicMax(reinterpret_cast<unsigned long long*>(p.max64 + acc * 18 + b), (unsigned long long)w);
+    }
+  }
   if (p.nb_keys == 0 || p.keys[0] > addr) return;
   uint32_t lo = 0, n = p.nb_keys;
   while (n > 1) {
@@ -140,96 +156,101 @@ __device__ __forceinline__ void rload_slot(const uint8_t* data, const RWin& w, c
   load_rec(data + off, w.pos, len, r);
 }
 
-// update_counters(global_counters, ...) (mem_sampling.c:517-592) for a
-// wave's records, without per-lane accumulators (the route pass needs its
-// registers for the held records): the common buckets (total count / weight,
-// N/A, L1 / L2 / L3 hits) and their min / max are reduced over the wave
-// (ballots, DPP sums and minima) and added to this wave's own LDS words
-// `wacc` [2 access][kWaveAccWords] by one lane; rarer buckets and weights >=
-// 2^23 update the workgroup's LDS counters per lane, as global_count does.
-constexpr int kWaveAccWords = 12;  // tc, tw, na, 3 x (count, sum), 3 hit-bucket (min, max) below
-// DPP move that keeps the lane's own value where the source lane is out of
-// range (identity for min / max)
-template <int CTRL, int ROW_MASK>
-__device__ __forceinline__ uint32_t dpp_keep(uint32_t v) {
-  return (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, CTRL, ROW_MASK, 0xf, false);
-}
-__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {  // (the steps of wave_sum_u32)
-  v = min(v, dpp_keep<0x111, 0xf>(v));
-  v = min(v, dpp_keep<0x112, 0xf>(v));
-  v = min(v, dpp_keep<0x114, 0xf>(v));
-  v = min(v, dpp_keep<0x118, 0xf>(v));
-  v = min(v, dpp_keep<0x142, 0xa>(v));
-  v = min(v, dpp_keep<0x143, 0xc>(v));
-  return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
-}
-__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
-  v = max(v, dpp_keep<0x111, 0xf>(v));
-  v = max(v, dpp_keep<0x112, 0xf>(v));
-  v = max(v, dpp_keep<0x114, 0xf>(v));
-  v = max(v, dpp_keep<0x118, 0xf>(v));
-  v = max(v, dpp_keep<0x142, 0xa>(v));
-  v = max(v, dpp_keep<0x143, 0xc>(v));
-  return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+// update_counters(global_counters, ...) (mem_sampling.c:517-592) of both
+// access types in one per-lane accumulator, without a branch on the access:
+// counts of reads in the low and writes in the high 16 bits of a word,
+// weights summed per access.  The hit buckets of the first kDualGroups level
+// groups (L1, L2, L3, LFB, local RAM: the common PEBS levels) live here; the
+// other buckets, N/A... see dual_count.  Drained at least every
+// kDrainWindows records per lane (u16 counts; weights < 2^23, 256 x 2^23 <
+// 2^31).
+constexpr int kDualGroups = 5;
+struct DualAcc {
+  uint32_t tc, na;                  // total count, N/A count: read | write << 16
+  uint32_t cnt[kDualGroups];        // hit bucket g counts: read | write << 16
+  uint32_t tw[2], sum[2][kDualGroups];  // weights per access
+};
+
+__device__ __forceinline__ void dual_clear(DualAcc& a) {
+  a.tc = a.na = 0;
+#pragma unroll
+  for (int g = 0; g < kDualGroups; g++) {
+    a.cnt[g] = 0;
+    a.sum[0][g] = a.sum[1][g] = 0;
+  }
+  a.tw[0] = a.tw[1] = 0;
 }
 
-__device__ __forceinline__ void wave_global_count(unsigned long long* wacc, unsigned long long (*sums)[kGlobalSums],
-                                                  unsigned long long (*mins)[18], unsigned long long (*maxs)[18],
-                                                  bool valid, uint32_t acc, uint32_t lvl, uint64_t w, int lane) {
-  const uint32_t bm = valid ? bucket_mask(lvl) : 0u;
-  const bool small = w < kLaneMaxWeight;
-  if (valid) {
-    unsigned long long* S = sums[acc];
-    if (small) {
-      for (uint32_t m = bm >> kRegGroups; m; m &= m - 1) {  // rarer hit buckets, miss buckets
-        const uint32_t b = kRegGroups + (uint32_t)__builtin_ctz(m);
-        atomicAdd(&S[3 + 2 * b], 1ull);
-        if (w) atomicAdd(&S[4 + 2 * b], (unsigned long long)w);
-        if (w < mins[acc][b]) atomicMin(&mins[acc][b], (unsigned long long)w);
-        if (w > maxs[acc][b]) atomicMax(&maxs[acc][b], (unsigned long long)w);
-      }
-    } else {  // weights >= 2^23 cycles: every bucket straight to the LDS counters
-      atomicAdd(&S[0], 1ull);
-      atomicAdd(&S[1], (unsigned long long)w);
-      if (lvl & LVL_NA) atomicAdd(&S[2], 1ull);
-      for (uint32_t m = bm; m; m &= m - 1) {
-        const uint32_t b = (uint32_t)__builtin_ctz(m);
-        atomicAdd(&S[3 + 2 * b], 1ull);
-        atomicAdd(&S[4 + 2 * b], (unsigned long long)w);
-        if (w < mins[acc][b]) atomicMin(&mins[acc][b], (unsigned long long)w);
-        if (w > maxs[acc][b]) atomicMax(&maxs[acc][b], (unsigned long long)w);
-      }
+// one SAMPLE of access `acc`: registers for the common buckets and
+// weights < 2^23; LDS (sums [2][kGlobalSums], mins / maxs [2][18]) for the rest
+__device__ __forceinline__ void dual_count(DualAcc& a, unsigned long long (*sums)[kGlobalSums],
+                                           unsigned long long (*mins)[18], unsigned long long (*maxs)[18],
+                                           uint32_t acc, uint32_t lvl, uint64_t w) {
+  const uint32_t bm = bucket_mask(lvl);
+  if (w < kLaneMaxWeight) {
+    const uint32_t w32 = (uint32_t)w, one = 1u << (16 * acc);
+    const uint32_t wr = acc ? 0u : w32, ww = acc ? w32 : 0u;
+    a.tc += one;
+    a.na += (lvl & LVL_NA) ? one : 0u;
+    a.tw[0] += wr;
+    a.tw[1] += ww;
+#pragma unroll
+    for (int g = 0; g < kDualGroups; g++) {
+      const bool in = (bm >> g) & 1;
+      a.cnt[g] += in ? one : 0u;
+      a.sum[0][g] += in ? wr : 0u;
+      a.sum[1][g] += in ? ww : 0u;
+    }
+    for (uint32_t m = bm >> kDualGroups; m; m &= m - 1) {  // rarer hit buckets, miss buckets
+      const uint32_t b = kDualGroups + (uint32_t)__builtin_ctz(m);
+      atomicAdd(&sums[acc][3 + 2 * b], 1ull);
+      if (w) atomicAdd(&sums[acc][4 + 2 * b], (unsigned long long)w);
+    }
+  } else {  // weights >= 2^23 cycles: straight to the LDS counters
+    atomicAdd(&sums[acc][0], 1ull);
+    atomicAdd(&sums[acc][1], (unsigned long long)w);
+    if (lvl & LVL_NA) atomicAdd(&sums[acc][2], 1ull);
+    for (uint32_t m = bm; m; m &= m - 1) {
+      const uint32_t b = (uint32_t)__builtin_ctz(m);
+      atomicAdd(&sums[acc][3 + 2 * b], 1ull);
+      atomicAdd(&sums[acc][4 + 2 * b], (unsigned long long)w);
     }
   }
-#pragma unroll
-  for (uint32_t a = 0; a < 2; a++) {
-    const bool in = valid && small && acc == a;
-    const uint64_t am = __ballot(in);
-    if (!am) continue;
-    const uint32_t w32 = in ? (uint32_t)w : 0u;  // (< 2^23: a wave's sum fits 32 bits)
-    unsigned long long* W = wacc + a * kWaveAccWords;
-    const uint32_t tc = (uint32_t)__popcll(am), na = (uint32_t)__popcll(__ballot(in && (lvl & LVL_NA)));
-    const uint32_t tw = wave_sum_u32(w32);
+  // min / max only move monotonically: read first, atomic only on improvement
+  for (uint32_t m = bm; m; m &= m - 1) {
+    const uint32_t b = (uint32_t)__builtin_ctz(m);
+    if (w < mins[acc][b]) atomicMin(&mins[acc][b], (unsigned long long)w);
+    if (w > maxs[acc][b]) atomicMax(&maxs[acc][b], (unsigned long long)w);
+  }
+}
+
+// lanes -> the workgroup's LDS counters (every lane of the wave calls this)
+__device__ __forceinline__ void dual_drain(DualAcc& a, unsigned long long (*sums)[kGlobalSums], int lane) {
+  if (__ballot(a.tc != 0) == 0) return;
+  auto add2 = [&](uint32_t packed, int word) {  // read | write << 16 counts
+    if (__ballot(packed != 0) == 0) return;
+    const uint32_t r = wave_sum_u32(packed & 0xffffu), wv = wave_sum_u32(packed >> 16);
     if (lane == 0) {
-      W[0] += tc;
-      W[1] += tw;
-      W[2] += na;
+      if (r) atomicAdd(&sums[0][word], (unsigned long long)r);
+      if (wv) atomicAdd(&sums[1][word], (unsigned long long)wv);
     }
+  };
+  auto addw = [&](uint32_t v, int acc, int word) {
+    if (__ballot(v != 0) == 0) return;
+    const uint64_t t = wave_sum_u32x(v);
+    if (lane == 0) atomicAdd(&sums[acc][word], (unsigned long long)t);
+  };
+  add2(a.tc, 0);
+  add2(a.na, 2);
+  addw(a.tw[0], 0, 1);
+  addw(a.tw[1], 1, 1);
 #pragma unroll
-    for (int b = 0; b < kRegGroups; b++) {
-      const bool ib = in && ((bm >> b) & 1);
-      const uint64_t bmask = __ballot(ib);
-      if (!bmask) continue;
-      const uint32_t c = (uint32_t)__popcll(bmask), sw = wave_sum_u32(ib ? w32 : 0u);
-      const uint32_t mn = wave_min_u32(ib ? w32 : 0xffffffffu), mx = wave_max_u32(ib ? w32 : 0u);
-      if (lane == 0) {
-        W[3 + 2 * b] += c;
-        W[4 + 2 * b] += sw;
-        if (mn < mins[a][b]) atomicMin(&mins[a][b], (unsigned long long)mn);
-        if (mx > maxs[a][b]) atomicMax(&maxs[a][b], (unsigned long long)mx);
-      }
-    }
+  for (int g = 0; g < kDualGroups; g++) {
+    add2(a.cnt[g], 3 + 2 * g);
+    addw(a.sum[0][g], 0, 4 + 2 * g);
+    addw(a.sum[1][g], 1, 4 + 2 * g);
   }
+  dual_clear(a);
 }
 
 // kDbgRouteTiming: per-wave cycle accumulators of the route pass's phases
@@ -246,39 +267,55 @@ __device__ __forceinline__ void rt_stamp(RTimer& t, int i) {
   }
 }
 
-// One batch's records held per lane in registers until the batch is sorted:
-// a 3-deep shift register (static indices only: no scratch)
+// A window's record, held in registers from its processing until the next
+// window's barrier, then stored to its staging slot (so that the stores never
+// race with the delayed write phase of the previous batch, which reads the
+// staging area before that barrier)
 struct Held {
   uint4 a;         // addr, timestamp
   uint64_t x;      // X word
-  uint32_t q;      // partition | batch rank << 11, or kNoChunk (nothing held)
+  uint32_t q;      // partition | batch rank << 11, or kNoChunk (no record)
 };
 
-// The route pass's LDS state shared by the batch helpers
+// The route pass's LDS state shared by the batch helpers.  Records are
+// staged unsorted, window b of the batch at slots [b * kWG, (b + 1) * kWG)
+// (lane-contiguous: conflict-free stores); the sort writes only a 16-bit
+// permutation, and the write phase gathers through it.
 struct RouteLds {
   uint32_t* hist;     // [P] records of each partition in the batch (rank counters)
-  uint32_t* start;    // [P] first staging slot of each partition's run
+  uint32_t* start;    // [P] first sorted position of each partition's run
   uint32_t* cur;      // [2][kMaxParts + 1] open chunk id << 7 | fill, double-buffered by batch parity
   uint32_t* nb;       // [P] first new chunk of the batch (kNoChunk: pool exhausted)
-  uint4* a16;         // staging: (addr, timestamp) in partition order
-  unsigned long long* x;
-  uint16_t* q;
+  uint4* a16;         // [kRouteBatch] staging slot: (addr, timestamp)
+  unsigned long long* x;  // [kRouteBatch] X word
+  uint32_t* uq;       // [kRouteBatch] partition | rank << 11, kNoChunk = empty slot
+  uint16_t* perm;     // [kRouteBatch] sorted position -> staging slot
   uint32_t* wsum;     // [16] per-wave scan totals
   uint32_t* misc;     // [0] records in the batch, [1] chunks taken, [2] first chunk never handed out
 };
 
-// Sort the batch's held records by partition into the LDS staging area and
-// take chunks for the partitions that outgrow their open chunk: three
-// barriers (after the batch's ranks, after the scan, after the staging).
-// Open-chunk state: batch b reads cur[b & 1] and writes cur[(b + 1) & 1].
+__device__ __forceinline__ void route_stage(const RouteLds& L, const Held& h, uint32_t b, int tid) {
+  const uint32_t slot = b * kWG + (uint32_t)tid;
+  L.uq[slot] = h.q;
+  if (h.q != kNoChunk) {
+    L.a16[slot] = h.a;
+    L.x[slot] = h.x;
+  }
+}
+
+// Sort batch `batch` (windows [0, nwin) staged) by partition -- the
+// permutation only -- and take chunks for the partitions that outgrow their
+// open chunk: three barriers (after the batch's ranks and stores, after the
+// scan, after the permutation).  Open-chunk state: batch b reads cur[b & 1]
+// and writes cur[(b + 1) & 1].
 template <bool TIMING>
-__device__ __forceinline__ void route_sort_batch(RTimer& rt, const RouteParams& rp, Held (&h)[kRouteWindows], int tid,
-                                                 const RouteLds& L, uint32_t batch, uint32_t c0, uint32_t cap) {
+__device__ __forceinline__ void route_sort_batch(RTimer& rt, const RouteParams& rp, int tid, const RouteLds& L,
+                                                 uint32_t batch, uint32_t nwin, uint32_t c0, uint32_t cap) {
   const uint32_t P = rp.nparts;
   const int lane = tid & 63, wave = tid >> 6;
   const uint32_t* cur_in = L.cur + (batch & 1) * (kMaxParts + 1);
   uint32_t* cur_out = L.cur + ((batch + 1) & 1) * (kMaxParts + 1);
-  __syncthreads();  // every rank of the batch taken
+  __syncthreads();  // every rank and staging store of the batch done
   // exclusive scan of the per-partition counts (two per thread, DPP within a wave)
   const uint32_t i0 = 2 * (uint32_t)tid;
   const uint32_t v0 = i0 < P ? L.hist[i0] : 0u, v1 = i0 + 1 < P ? L.hist[i0 + 1] : 0u;
@@ -319,7 +356,7 @@ __device__ __forceinline__ void route_sort_batch(RTimer& rt, const RouteParams& 
     const uint32_t nn = (tot - kChunk + kChunk - 1) / kChunk;
     const uint32_t base = atomicAdd(&L.misc[1], nn);
     if (base + nn > cap) {
-      L.nb[q] = kNoChunk;  // pool exhausted: this batch's overflow of q is attributed directly
+      L.nb[q] = kNoChunk;  // pool exhausted: this batch's overflow of q goes to the overflow list
       atomicMin(&L.misc[2], base);  // chunks from here on were never handed out
       cur_out[q] = (cur & ~127u) | kChunk;
       continue;
@@ -330,16 +367,10 @@ __device__ __forceinline__ void route_sort_batch(RTimer& rt, const RouteParams& 
   }
   if (tid == kWG - 1) L.misc[0] = wb + inc;  // records in the batch
   __syncthreads();
-  // the held records into LDS in partition order
-#pragma unroll
-  for (int b = 0; b < (int)kRouteWindows; b++) {
-    if (h[b].q == kNoChunk) continue;
-    const uint32_t q = h[b].q & 2047u;
-    const uint32_t j = L.start[q] + (h[b].q >> 11);
-    L.a16[j] = h[b].a;
-    L.x[j] = h[b].x;
-    L.q[j] = (uint16_t)q;
-    h[b].q = kNoChunk;
+  // the permutation: sorted position of every staged record
+  for (uint32_t b = 0; b < nwin; b++) {
+    const uint32_t slot = b * kWG + (uint32_t)tid, e = L.uq[slot];
+    if (e != kNoChunk) L.perm[L.start[e & 2047u] + (e >> 11)] = (uint16_t)slot;
   }
   __syncthreads();
   rt_stamp<TIMING>(rt, 6);
@@ -349,8 +380,8 @@ __device__ __forceinline__ void route_sort_batch(RTimer& rt, const RouteParams& 
 // slots, coalesced by run.  Run right after the next window's barrier and
 // before its loads are issued: a window waits for its loads with
 // vmcnt(0), which counts stores too, so stores issued behind the loads would
-// make the window wait for them.  (The LDS it reads is rewritten only by the
-// next batch's sort, after that batch's barriers.)
+// make the window wait for them.  (The staging slots it reads are rewritten
+// only after the next window's barrier.)
 template <bool TIMING>
 __device__ __forceinline__ void route_write_batch(RTimer& rt, const RouteParams& rp, int tid, const RouteLds& L,
                                                   uint32_t batch) {
@@ -358,7 +389,10 @@ __device__ __forceinline__ void route_write_batch(RTimer& rt, const RouteParams&
   const uint32_t* cur_in = L.cur + (batch & 1) * (kMaxParts + 1);
   const uint32_t total = L.misc[0];
   for (uint32_t j = tid; j < total; j += kWG) {
-    const uint32_t q = L.q[j];
+    const uint32_t src = L.perm[j];
+    const uint32_t q = L.uq[src] & 2047u;
+    const uint4 a = L.a16[src];
+    const uint64_t x = L.x[src];
     const uint32_t cur = cur_in[q];
     const uint32_t pos = (cur & 127u) + (j - L.start[q]);
     uint32_t chunk, slot;
@@ -370,10 +404,10 @@ __device__ __forceinline__ void route_write_batch(RTimer& rt, const RouteParams&
       if (nb == kNoChunk) {  // pool exhausted: to the overflow list (overflow_kernel)
         const uint32_t o = atomicAdd(rp.ovf_cnt, 1u);
         if (o < rp.ovf_cap) {
-          rp.ovf16[o] = L.a16[j];
-          rp.ovfx[o] = L.x[j];
+          rp.ovf16[o] = a;
+          rp.ovfx[o] = x;
         } else {  // (only SAMPLE records shorter than 40 B get here: NMG_F_SINGLE_PASS handles any number)
-          const XRec xr = x_decode(rp.xl, L.x[j]);
+          const XRec xr = x_decode(rp.xl, x);
           set_error(p, rp.seq0 + xr.g, xr.off, kErrRouteOverflow);
         }
         continue;
@@ -383,8 +417,8 @@ __device__ __forceinline__ void route_write_batch(RTimer& rt, const RouteParams&
     }
     if (p.flags & kDbgRouteNoWrite) continue;
     const uint64_t k = uint64_t(chunk) * kChunk + slot;
-    rp.rec16[k] = L.a16[j];
-    rp.recx[k] = L.x[j];
+    rp.rec16[k] = a;
+    rp.recx[k] = x;
   }
   rt_stamp<TIMING>(rt, 7);
 }
@@ -418,9 +452,8 @@ __global__ __launch_bounds__(kWG, 1) void route_kernel(RouteParams rp) {
   __shared__ uint4 s_desc[kDescLds];
   __shared__ uint4 s_a16[kRouteBatch];
   __shared__ unsigned long long s_x[kRouteBatch];
-  __shared__ uint16_t s_q[kRouteBatch];
-  __shared__ unsigned long long s_sums[2][kGlobalSums], s_mins[2][18], s_maxs[2][18];
-  __shared__ unsigned long long s_wacc[kWG / 64][2][kWaveAccWords];  // wave_global_count: one block per wave
+  __shared__ uint32_t s_uq[kRouteBatch];
+  __shared__ uint16_t s_perm[kRouteBatch];
   __shared__ uint32_t s_list[kMaxList];
   __shared__ uint32_t s_flags[3], s_nlist, s_next, s_err, s_wsum[kWG / 64], s_misc[3];
 
@@ -440,14 +473,8 @@ __global__ __launch_bounds__(kWG, 1) void route_kernel(RouteParams rp) {
     const BufDesc d = p.sbufs[i];
     s_desc[i - r0] = make_uint4((uint32_t)d.offset, (uint32_t)(d.offset >> 32), d.len, d.thread_rank | (d.access << 16));
   }
-  const RouteLds L{s_hist, s_start, &s_cur[0][0], s_nb, s_a16, s_x, s_q, s_wsum, s_misc};
-  if (tid < (int)kGlobalSums) s_sums[0][tid] = s_sums[1][tid] = 0;
-  if (tid < 18) {
-    s_mins[0][tid] = s_mins[1][tid] = ~0ull;  // INIT_COUNTER (mem_analyzer.c:415-420)
-    s_maxs[0][tid] = s_maxs[1][tid] = 0;
-  }
+  const RouteLds L{s_hist, s_start, &s_cur[0][0], s_nb, s_a16, s_x, s_uq, s_perm, s_wsum, s_misc};
   if (tid < 3) s_flags[tid] = 0;
-  for (uint32_t i = tid; i < (kWG / 64) * 2 * kWaveAccWords; i += kWG) (&s_wacc[0][0][0])[i] = 0;
   if (tid == 0) {
     s_misc[1] = 0;
     s_misc[2] = kNoChunk;
@@ -467,9 +494,9 @@ __global__ __launch_bounds__(kWG, 1) void route_kernel(RouteParams rp) {
       const RWin wl = rwin_lane(tid, 0, d0, d1, has1);
       rload_slot(p.data, wl, d0, d1, nx);
     }
-    Held held[kRouteWindows];
-#pragma unroll
-    for (int b = 0; b < (int)kRouteWindows; b++) held[b].q = kNoChunk;
+    Held held;  // the previous window's record, staged after this window's barrier
+    held.q = kNoChunk;
+    bool hheld = false;  // held belongs to window bwin - 1 of the open batch
     uint32_t win = 0, bwin = 0;
     uint32_t ns0 = 0, ns1 = 0;  // per-buffer SAMPLE tallies: buffer idx, idx + 1
     RTimer rt;
@@ -491,6 +518,10 @@ __global__ __launch_bounds__(kWG, 1) void route_kernel(RouteParams rp) {
       const uint32_t f = __builtin_amdgcn_readfirstlane(s_flags[win % 3]);
       if (tid == 0) s_flags[(win + 2) % 3] = 0;
       win++;
+      if (hheld) {  // the previous window's record to its staging slot
+        route_stage(L, held, bwin - 1, tid);
+        hheld = false;
+      }
       if (TIMING) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (timing: the window's loads count as wait)
       rt_stamp<TIMING>(rt, 0);
       uint32_t nidx = idx;
@@ -612,8 +643,7 @@ __global__ __launch_bounds__(kWG, 1) void route_kernel(RouteParams rp) {
       const uint32_t acc_l = rin1 ? d1.access : d0.access;
       Held hr;
       hr.q = kNoChunk;
-      wave_global_count(&s_wacc[tid >> 6][0][0], s_sums, s_mins, s_maxs, valid, acc_l,
-                        uint32_t(rec.dsrc >> 5) & 0x3fff /* data_src.mem_lvl */, rec.w, lane);
+      // (update_counters runs in the local pass, from the record's level field)
       rt_stamp<TIMING>(rt, 2);
       uint32_t node = 0;
       if (valid) {
@@ -625,19 +655,18 @@ __global__ __launch_bounds__(kWG, 1) void route_kernel(RouteParams rp) {
       if (TIMING) (void)__builtin_amdgcn_readfirstlane(__ballot(node != 0));  // (the search ends here)
       rt_stamp<TIMING>(rt, 3);
       if (valid) {
-        if (node) {
-          const uint32_t q = min(eytz_rank(node, kPartLevels), P - 1);
-          const uint32_t rk = atomicAdd(&s_hist[q], 1u);
-          hr.q = q | (rk << 11);
-          hr.a = make_uint4((uint32_t)rec.addr, (uint32_t)(rec.addr >> 32), (uint32_t)rec.ts, (uint32_t)(rec.ts >> 32));
-          const uint32_t g = rin1 ? d1.pad : d0.pad;
-          const uint32_t th = rin1 ? d1.thread_rank : d0.thread_rank;
-          hr.x = x_encode(rp.xl, g, roff, th, acc_l, rec.w);
-        }
+        // (below the first key: partition 0, where the lookup finds no node)
+        const uint32_t q = node ? min(eytz_rank(node, kPartLevels), P - 1) : 0u;
+        const uint32_t rk = atomicAdd(&s_hist[q], 1u);
+        hr.q = q | (rk << 11);
+        hr.a = make_uint4((uint32_t)rec.addr, (uint32_t)(rec.addr >> 32), (uint32_t)rec.ts, (uint32_t)(rec.ts >> 32));
+        const uint32_t g = rin1 ? d1.pad : d0.pad;
+        const uint32_t th = rin1 ? d1.thread_rank : d0.thread_rank;
+        hr.x = x_encode(rp.xl, g, roff, th, acc_l, uint32_t(rec.dsrc >> 5) & 0x3fff /* data_src.mem_lvl */, rec.w);
       }
-#pragma unroll
-      for (int b = (int)kRouteWindows - 1; b > 0; b--) held[b] = held[b - 1];
-      held[0] = hr;
+      held = hr;
+      hheld = true;
+      const bool wrote = wpending;  // (uniform)
       if (wpending) {  // the previous batch's chunk stores, then the next window's loads
         route_write_batch<TIMING>(rt, rp, tid, L, nbatches - 1);
         wpending = false;
@@ -665,16 +694,21 @@ __global__ __launch_bounds__(kWG, 1) void route_kernel(RouteParams rp) {
       }
       const bool last = nidx >= r1;
       rt_stamp<TIMING>(rt, 4);
-      if (p.flags & kDbgRouteNoBatch) {  // (ablation) forget the held records
+      if (p.flags & kDbgRouteNoBatch) {  // (ablation) forget the records
         if (++bwin == kRouteWindows || last) {
           __syncthreads();
           for (uint32_t q = tid; q < P; q += kWG) s_hist[q] = 0;
-#pragma unroll
-          for (int b = 0; b < (int)kRouteWindows; b++) held[b].q = kNoChunk;
+          hheld = false;
           bwin = 0;
         }
       } else if (++bwin == kRouteWindows || last) {
-        route_sort_batch<TIMING>(rt, rp, held, tid, L, nbatches, c0, cap);
+        // the batch's last window to its staging slots -- after every wave has
+        // gathered the previous batch, when that was written in this window
+        // (a one-window batch at the end of the range)
+        if (wrote) __syncthreads();
+        route_stage(L, held, bwin - 1, tid);
+        hheld = false;
+        route_sort_batch<TIMING>(rt, rp, tid, L, nbatches, bwin, c0, cap);
         bwin = 0;
         nbatches++;
         if (last) route_write_batch<TIMING>(rt, rp, tid, L, nbatches - 1);
@@ -696,24 +730,6 @@ __global__ __launch_bounds__(kWG, 1) void route_kernel(RouteParams rp) {
     }
   }
   __syncthreads();
-  // the waves' blocks into the workgroup's counters (sums; the three hit buckets' min / max)
-  if (tid < 2 * 9) {
-    const uint32_t a = tid / 9, k = tid % 9;  // tc, tw, na, 3 x (count, sum)
-    unsigned long long v = 0;
-    for (int wv = 0; wv < kWG / 64; wv++) v += s_wacc[wv][a][k];
-    s_sums[a][k] += v;  // (word k of struct mem_counters' order: 0..2, then 3 + 2b / 4 + 2b for b < 3)
-  }
-  __syncthreads();
-  // global mem_counters of both access types
-#pragma unroll
-  for (uint32_t a = 0; a < 2; a++) {
-    if (tid < (int)kGlobalSums && s_sums[a][tid])
-      atomicAdd(reinterpret_cast<unsigned long long*>(p.sum64 + gsum_index(a, tid)), s_sums[a][tid]);
-    if (tid < 18 && s_sums[a][3 + 2 * tid]) {
-      atomicMin(reinterpret_cast<unsigned long long*>(p.min64 + a * 18 + tid), s_mins[a][tid]);
-      atomicMax(reinterpret_cast<unsigned long long*>(p.max64 + a * 18 + tid), s_maxs[a][tid]);
-    }
-  }
   // open chunks' fill, chunk counts per partition, pool use
   for (uint32_t q = tid; q < P; q += kWG) {
     const uint32_t cur = s_cur[nbatches & 1][q];
@@ -733,7 +749,7 @@ __global__ __launch_bounds__(256) void overflow_kernel(RouteParams rp) {
     const uint4 a = rp.ovf16[i];
     const XRec xr = x_decode(rp.xl, rp.ovfx[i]);
     direct_attribute(rp.p, u64of(a.x, a.y), u64of(a.z, a.w), x_weight(rp.xl, xr, rp.p.data, rp.p.sbufs), xr.th,
-                     xr.acc, rp.seq0 + xr.g, xr.off, xr.g);
+                     xr.acc, xr.lvl, rp.seq0 + xr.g, xr.off, xr.g);
   }
 }
 
@@ -834,16 +850,27 @@ __global__ __launch_bounds__(kWG, 1) void local_kernel(LocalParams lp) {
   __shared__ uint64_t s_keys[kPartSlots];
   __shared__ uint4 s_nodes[2 * kPartSlots];
   __shared__ uint2 s_info[kPartSlots];
+  __shared__ uint32_t s_dir[kPartDir];
   __shared__ unsigned long long s_owt[2][kPartEntries];
   __shared__ unsigned long long s_first[kPartEntries];
   __shared__ uint32_t s_pg[kPartCells / 2];
   __shared__ uint32_t s_item;
+  // the global mem_counters of the records this workgroup attributes
+  __shared__ unsigned long long s_gsums[2][kGlobalSums], s_gmins[2][18], s_gmaxs[2][18];
 
   Params& p = lp.p;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const uint32_t nitems = lp.ctl[0];
   const uint32_t T = p.nb_threads;
   const bool pages = (p.flags & NMG_F_PAGE_HIST) != 0;
+  if (tid < (int)kGlobalSums) s_gsums[0][tid] = s_gsums[1][tid] = 0;
+  if (tid < 18) {
+    s_gmins[0][tid] = s_gmins[1][tid] = ~0ull;  // INIT_COUNTER (mem_analyzer.c:415-420)
+    s_gmaxs[0][tid] = s_gmaxs[1][tid] = 0;
+  }
+  DualAcc gacc;  // per-lane update_counters, drained every kDrainWindows chunks
+  dual_clear(gacc);
+  uint32_t acc_chunks = 0;
   while (true) {
     if (tid == 0) s_item = atomicAdd(lp.ctl + 1, 1u);
     __syncthreads();
@@ -852,18 +879,20 @@ __global__ __launch_bounds__(kWG, 1) void local_kernel(LocalParams lp) {
     const uint4 item = lp.items[it];
     const uint32_t q = __builtin_amdgcn_readfirstlane(item.x);
     const PartInfo pi = lp.parts[q];
-    const uint32_t levels = __builtin_amdgcn_readfirstlane(pi.levels);
+    const uint32_t dshift = __builtin_amdgcn_readfirstlane(pi.dshift);
     {
-      const uint32_t ns = 1u << levels;
+      const uint32_t nk = pi.nk;
       const uint64_t* gk = lp.pe_keys + uint64_t(q) * kPartSlots;
       const uint4* gn = lp.pe_nodes + uint64_t(q) * kPartSlots * 2;
       const uint2* gi = lp.pe_info + uint64_t(q) * kPartSlots;
-      for (uint32_t i = tid; i < ns; i += kWG) {
+      for (uint32_t i = tid; i < nk; i += kWG) {
         s_keys[i] = gk[i];
         s_nodes[2 * i] = gn[2 * i];
         s_nodes[2 * i + 1] = gn[2 * i + 1];
         s_info[i] = gi[i];
       }
+      const uint32_t* gd = lp.pe_dir + uint64_t(q) * kPartDir;
+      for (uint32_t i = tid; i < kPartDir; i += kWG) s_dir[i] = gd[i];
     }
     for (uint32_t i = tid; i < pi.ne; i += kWG) {
       s_owt[0][i] = s_owt[1][i] = 0;
@@ -873,53 +902,87 @@ __global__ __launch_bounds__(kWG, 1) void local_kernel(LocalParams lp) {
     for (uint32_t i = tid; i < (ncell + 1) / 2; i += kWG) s_pg[i] = 0;
     __syncthreads();
 
-    // each wave takes every 16th chunk of the item; the next chunk's records
-    // and the list entry after it are in flight while a chunk is processed
+    // each wave takes every 16th chunk of the item; the records of its next
+    // two chunks and the list entry after them are in flight while a chunk is
+    // processed (a wave's chunk is 1.5 KiB: one in flight per wave leaves
+    // HBM idle)
     constexpr uint32_t kStride = kWG / 64;
     const uint32_t l0 = item.y + (uint32_t)wave, l1 = item.z;
+    auto chunk_load = [&](uint32_t e, uint32_t l, uint4& a, uint64_t& x) {
+      a = make_uint4(0, 0, 0, 0);
+      x = 0;
+      if (l < l1 && (uint32_t)lane < (e >> kChunkIdBits)) {
+        const uint64_t k = uint64_t(e & ((1u << kChunkIdBits) - 1)) * kChunk + lane;
+        a = lp.rec16[k];
+        x = lp.recx[k];
+      }
+    };
     uint32_t ce = l0 < l1 ? lp.clist[l0] : 0u;
-    uint4 na16 = make_uint4(0, 0, 0, 0);
-    uint64_t nx = 0;
-    if (l0 < l1 && (uint32_t)lane < (ce >> kChunkIdBits)) {
-      const uint64_t k = uint64_t(ce & ((1u << kChunkIdBits) - 1)) * kChunk + lane;
-      na16 = lp.rec16[k];
-      nx = lp.recx[k];
-    }
-    uint32_t ce2 = l0 + kStride < l1 ? lp.clist[l0 + kStride] : 0u;
+    uint32_t ce1 = l0 + kStride < l1 ? lp.clist[l0 + kStride] : 0u;
+    uint4 na16, na16b;
+    uint64_t nx, nxb;
+    chunk_load(ce, l0, na16, nx);
+    chunk_load(ce1, l0 + kStride, na16b, nxb);
+    uint32_t ce2 = l0 + 2 * kStride < l1 ? lp.clist[l0 + 2 * kStride] : 0u;
     for (uint32_t l = l0; l < l1; l += kStride) {
       const uint32_t c = ce & ((1u << kChunkIdBits) - 1), fill = ce >> kChunkIdBits;
       const bool valid = (uint32_t)lane < fill;
       const uint4 a16 = na16;
       const uint64_t x = nx;
-      ce = ce2;
-      if (l + kStride < l1 && (uint32_t)lane < (ce >> kChunkIdBits)) {
-        const uint64_t k = uint64_t(ce & ((1u << kChunkIdBits) - 1)) * kChunk + lane;
-        na16 = lp.rec16[k];
-        nx = lp.recx[k];
-      }
-      ce2 = l + 2 * kStride < l1 ? lp.clist[l + 2 * kStride] : 0u;
+      ce = ce1;
+      na16 = na16b;
+      nx = nxb;
+      ce1 = ce2;
+      chunk_load(ce1, l + 2 * kStride, na16b, nxb);
+      ce2 = l + 3 * kStride < l1 ? lp.clist[l + 3 * kStride] : 0u;
       const uint64_t addr = u64of(a16.x, a16.y), ts = u64of(a16.z, a16.w);
       if (p.flags & kDbgLocalNoWork) {  // (ablation) loads only
         if (lane == 0) lp.cmatch[c] = addr ^ ts ^ x;
         continue;
       }
-      // lower bound among the partition's keys (the record's address is >= its
-      // first key and < the next partition's): the node of the last right turn
-      const uint32_t i = eytz_descend(s_keys, levels, addr);
-      const uint32_t idx = i >> (__builtin_ctz(i) + 1);
+      // update_counters(global_counters, sample) (mem_sampling.c:882): every
+      // routed SAMPLE, matched or not
+      const XRec xr = x_decode(lp.xl, x);
+      const uint64_t w = valid ? x_weight(lp.xl, xr, p.data, lp.descs) : 0ull;
+      if (valid && !(p.flags & kDbgLocalNoGlobal)) dual_count(gacc, s_gsums, s_gmins, s_gmaxs, xr.acc, xr.lvl, w);
+      if (++acc_chunks == kDrainWindows) {  // keep the per-lane u16 counts / u32 sums bounded
+        dual_drain(gacc, s_gsums, lane);
+        acc_chunks = 0;
+      }
+      // lower bound among the partition's keys (ht_lower_key, tools/hash.c:63-77):
+      // the record's address is < the next partition's first key; below the
+      // first key (partition 0 only) there is no node.  The directory slot
+      // gives the largest key <= the slot start and the keys inside the slot
+      // (usually 0 or 1; a binary search among them otherwise).
+      const uint64_t k0key = s_keys[0];
+      int32_t r = -1;
+      if (valid && addr >= k0key) {
+        const uint64_t rel = addr - k0key;
+        const uint32_t de = s_dir[(uint32_t)min(rel >> dshift, (uint64_t)(kPartDir - 1))];
+        uint32_t a = de & 0xffffu, n = de >> 16;  // answer in [a, a + n]: keys[a] <= addr
+        while (n) {
+          const uint32_t half = (n + 1) >> 1;
+          if (s_keys[a + half] <= addr) {
+            a += half;
+            n -= half;
+          } else {
+            n = half - 1;
+          }
+        }
+        r = (int32_t)a;
+      }
       int32_t erel = -1;
       uint64_t baddr = 0;
       uint32_t hrel = kEmpty32;
-      if (valid && idx) {
-        const uint4 na = s_nodes[2 * idx], nb = s_nodes[2 * idx + 1];
-        const uint2 inf = s_info[idx];
+      if (r >= 0 && !(p.flags & kDbgLocalNoSearch)) {
+        const uint4 na = s_nodes[2 * r], nb = s_nodes[2 * r + 1];
+        const uint2 inf = s_info[r];
         if (entry_match(na, nb, addr, ts)) {  // is_sample_in_buffer (mem_analyzer.c:141-155), newest entry
           erel = (int32_t)(inf.y & 0x7fffffffu);
           baddr = u64of(na.x, na.y);
           hrel = inf.x;
         } else if (inf.y >> 31) {  // older entries of a reused address (LIFO, tools/hash.c:108-114)
-          const uint32_t rank = min(eytz_rank(idx, levels), pi.nk - 1);  // (padding slots copy the last node)
-          const uint4 d = reinterpret_cast<const uint4*>(p.nodes + pi.k0 + rank)[3];  // (count, first)
+          const uint4 d = reinterpret_cast<const uint4*>(p.nodes + pi.k0 + (uint32_t)r)[3];  // (count, first)
           Match m;
           m.e = -1;
           match_older(p, d.y, d.x, addr, ts, m);
@@ -933,9 +996,8 @@ __global__ __launch_bounds__(kWG, 1) void local_kernel(LocalParams lp) {
       const uint64_t fm = __ballot(erel >= 0);
       if (lane == 0) lp.cmatch[c] = fm;
       if (erel < 0) continue;
-      const XRec xr = x_decode(lp.xl, x);
-      const uint64_t w = x_weight(lp.xl, xr, p.data, lp.descs);
-      if (w < kLaneMaxWeight) {
+      if (p.flags & kDbgLocalNoObj) {
+      } else if (w < kLaneMaxWeight) {
         atomicAdd(&s_owt[xr.acc][erel], (1ull << kPackShift) | w);
       } else {
         const uint64_t e = pi.e0 + (uint32_t)erel;
@@ -945,8 +1007,8 @@ __global__ __launch_bounds__(kWG, 1) void local_kernel(LocalParams lp) {
       }
       // first match in analysis order (quirk Q7)
       const unsigned long long ord = ((lp.seq0 + xr.g) << 32) | xr.off;
-      if (ord < s_first[erel]) atomicMin(&s_first[erel], ord);
-      if (pages) {
+      if (!(p.flags & kDbgLocalNoObj) && ord < s_first[erel]) atomicMin(&s_first[erel], ord);
+      if (pages && !(p.flags & kDbgLocalNoPage)) {
         // ma_get_block: page_no = (int)((addr - buffer_addr) / 4096) (mem_analyzer.c:530-531)
         const uint32_t page = uint32_t(int(uint64_t(addr - baddr) / kPageSize));
         if (hrel != kEmpty32) {
@@ -993,6 +1055,18 @@ __global__ __launch_bounds__(kWG, 1) void local_kernel(LocalParams lp) {
       }
     }
     __syncthreads();
+  }
+  // global mem_counters of both access types
+  dual_drain(gacc, s_gsums, lane);
+  __syncthreads();
+#pragma unroll
+  for (uint32_t a = 0; a < 2; a++) {
+    if (tid < (int)kGlobalSums && s_gsums[a][tid])
+      atomicAdd(reinterpret_cast<unsigned long long*>(p.sum64 + gsum_index(a, tid)), s_gsums[a][tid]);
+    if (tid < 18 && s_gsums[a][3 + 2 * tid]) {
+      atomicMin(reinterpret_cast<unsigned long long*>(p.min64 + a * 18 + tid), s_gmins[a][tid]);
+      atomicMax(reinterpret_cast<unsigned long long*>(p.max64 + a * 18 + tid), s_gmaxs[a][tid]);
+    }
   }
 }
 

@@ -27,7 +27,11 @@ VARIANTS = {
     "route_nopages": 0x1,               # ... without the page histogram
     "route_noloc": 0x3 | 0x400000,      # local pass loads its chunks only
     "route_nowrite": 0x3 | 0x100000 | 0x400000,  # batches sorted in LDS, no chunk stores (local: loads only)
-    "route_nobatch": 0x3 | 0x200000,    # stream + global counters + partition search + batch ranks only
+    "route_nobatch": 0x3 | 0x200000,    # stream + partition search + batch ranks only
+    "local_noobj": 0x3 | 0x1000000,     # local pass without object counters / first ordinals
+    "local_nopage": 0x3 | 0x2000000,    # ... without page cells
+    "local_noglobal": 0x3 | 0x4000000,  # ... without the global counters
+    "local_nosearch": 0x3 | 0x8000000,  # ... without the lookup (nothing matches)
 }
 
 WORKLOADS = {
