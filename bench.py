@@ -133,10 +133,14 @@ def main():
     ap.add_argument("--secondary", default="c2,c3",
                     help="workloads measured after the main one, comma-separated (N=1; '' = none)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-records", type=int, default=50_000, help="records in the single-threaded oracle's sample")
+    ap.add_argument("--cpu-records", type=int, default=100_000,
+                    help="records in the reference-loop oracle's sample (its linear call-site list is quadratic)")
+    ap.add_argument("--cpu-st-records", type=int, default=2_000_000,
+                    help="records in the one-thread run of the multi-threaded restatement")
     ap.add_argument("--cpu-mt-records", type=int, default=25_000_000, help="records in the multi-threaded baseline's sample")
-    ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16")),
-                    help="host threads of the multi-threaded CPU baseline")
+    ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)),
+                    help="host threads of the multi-threaded CPU baseline (default: this job's CPU share, "
+                         "OMP_NUM_THREADS, else every CPU)")
     args = ap.parse_args()
 
     import torch
@@ -184,6 +188,7 @@ def main():
 
     elapsed, steps = timed_run(w, args.steps, args.warmup, barrier, agree)
     attr_ms, total_ms = w.eng.kernel_times(min(steps, 64))  # HIP events on the engine stream
+    phases = w.eng.phase_times(min(steps, 64))
     if distributed:
         tt = torch.tensor([elapsed], dtype=torch.float64, device=device)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -199,7 +204,7 @@ def main():
         merge_engine(w.eng, dst=0)  # full merge once (dense + gathers) for the report
 
     if rank == 0:
-        out = result_line(args, w, world, steps, ms_per_step, value, attr_ms, total_ms)
+        out = result_line(args, w, world, steps, ms_per_step, value, attr_ms, total_ms, phases)
         if world == 1 and args.secondary:
             out["secondary"] = {}
             for name in args.secondary.split(","):
@@ -220,7 +225,8 @@ def main():
                 del s
         if world == 1 and not args.no_cpu_baseline:
             log(f"[rank 0] cpu baseline: first {args.cpu_records} records")
-            out["cpu_baseline"] = cpu_baseline(w.rp, args.cpu_records, args.cpu_mt_records, args.cpu_threads)
+            out["cpu_baseline"] = cpu_baseline(w.rp, args.cpu_records, args.cpu_mt_records, args.cpu_threads,
+                                         args.cpu_st_records)
         print(json.dumps(out), flush=True)
     if distributed:
         dist.barrier()
@@ -296,19 +302,52 @@ def main_one_process(args):
     eng.close()
 
 
-def result_line(args, w, world, steps, ms_per_step, value, attr_ms, total_ms):
+def load_traffic(name):
+    """HBM bytes per launch from profiles/pmc_<name>.json (tools/pmc_pipeline.py),
+    or None with the reason when the file is missing or was measured on other
+    kernel sources than this tree's (numamma_amd/srchash.py)."""
+    from numamma_amd.srchash import kernel_source_hash
+
+    path = os.path.join(ROOT, "profiles", f"pmc_{name}.json")
+    if not os.path.exists(path):
+        return None, None, f"no profiles/pmc_{name}.json"
+    try:
+        pmc = json.load(open(path))
+    except (OSError, ValueError) as e:
+        return None, None, f"profiles/pmc_{name}.json unreadable: {e}"
+    here = kernel_source_hash()
+    if pmc.get("source_hash") != here:
+        return None, None, (f"profiles/pmc_{name}.json was measured on kernel sources {pmc.get('source_hash')}, "
+                            f"this tree is {here}: traffic not reported")
+    return pmc.get("hbm_bytes_per_launch"), pmc, (f"profiles/pmc_{name}.json (sources {here}, "
+                                                 f"commit {pmc.get('commit', '?')})")
+
+
+def result_line(args, w, world, steps, ms_per_step, value, attr_ms, total_ms, phases):
     wl = WORKLOADS[w.name]
     avg_attr = float(np.mean(attr_ms))
     avg_total = float(np.mean(total_ms))
+    first_ms, rest_ms = (float(np.mean(x)) if x else 0.0 for x in phases)
     algo = w.samples * RECORD_BYTES
     achieved = algo / (avg_attr * 1e-3) / 1e9
-    traffic = None
-    pmc_path = os.path.join(ROOT, "profiles", f"pmc_{w.name}.json")
-    if os.path.exists(pmc_path):
-        try:
-            traffic = json.load(open(pmc_path)).get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
+    traffic, pmc, traffic_src = load_traffic(w.name)
+    routed = rest_ms > 0.0  # the partition-first path ran (tables > 1023 keys)
+    kernels = {}
+    if routed:
+        # route_kernel reads every 40 B record and writes a 24 B compact record
+        # per sample; the local pass reads the compact records back
+        kernels["route_kernel"] = {"avg_ms": first_ms, "algorithmic_bytes": w.samples * (RECORD_BYTES + 24)}
+        kernels["overflow+count+plan+scatter+local_kernel"] = {"avg_ms": rest_ms, "algorithmic_bytes": w.samples * 24}
+    else:
+        kernels["attribute_kernel"] = {"avg_ms": first_ms, "algorithmic_bytes": algo}
+    for k, v in kernels.items():
+        v["achieved_GBps"] = v["algorithmic_bytes"] / (v["avg_ms"] * 1e-3) / 1e9 if v["avg_ms"] else None
+        v["frac"] = v["achieved_GBps"] / HBM_PEAK_GBS if v["achieved_GBps"] else None
+        if pmc:
+            names = ["route_kernel"] if k == "route_kernel" else [n for n in pmc["kernels"] if n != "route_kernel"
+                                                                  and not n.startswith("reduce")]
+            v["traffic"] = sum(pmc["kernels"][n]["hbm_read_bytes"] + pmc["kernels"][n]["hbm_write_bytes"]
+                               for n in names if n in pmc["kernels"])
     return {
         "metric": "PEBS samples/s analysed (device-resident)",
         "value": value,
@@ -333,21 +372,22 @@ def result_line(args, w, world, steps, ms_per_step, value, attr_ms, total_ms):
         },
         "roofline": {
             "bound": "hbm",
-            "kernel": "nmg::attribute_kernel",
+            "kernel": ("nmg attribution launch, partition-first: route_kernel -> overflow/count/plan/scatter -> "
+                       "local_kernel" if routed else "nmg::attribute_kernel"),
             "achieved": achieved,
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
             "traffic": traffic,
-            # the HBM bytes the kernel really moves (PMC, per launch) per second: the
-            # lookups' random lines come on top of the 40 B per record
+            # the HBM bytes the launch really moves (PMC, per launch) per second
             "traffic_GBps": (traffic / (avg_attr * 1e-3) / 1e9) if traffic else None,
             "algorithmic_bytes_per_launch": algo,
             "avg_kernel_ms": avg_attr,
             "avg_launch_ms": avg_total,
-            "note": "achieved = 40 B per record / attribution-kernel time (HIP events); the launch adds the "
-                    "long-tail reduce kernel; traffic = PMC FETCH_SIZE + WRITE_SIZE per launch "
-                    f"(profiles/pmc_{w.name}.json, record stream corrected x2)",
+            "kernels": kernels,
+            "note": "achieved = 40 B per record (SURVEY 8(d)) / attribution time, HIP events on the engine stream "
+                    "around the kernels that attribute the records; the launch adds the long-tail reduce; "
+                    f"kernels = the same events split after route_kernel; traffic: {traffic_src}",
         },
     }
 
@@ -364,61 +404,85 @@ def _sample_replay(rp, max_records):
     return Replay(rp.nb_threads, rp.table, rp.buffers[:max(1, n)]), max(1, n)
 
 
-def cpu_baseline(rp, max_records, mt_records, threads, target_s=5.0, max_runs=20):
+def _rate_runs(fn, target_s, max_runs, tag):
+    """fn() -> (records, seconds); repeated until about target_s seconds."""
+    rates, secs, recs = [], 0.0, 0
+    while len(rates) < max_runs and (not rates or secs < target_s):
+        recs, t = fn()
+        log(f"[rank 0] cpu baseline ({tag}) run {len(rates)}: {recs} records in {t:.2f}s")
+        rates.append(recs / t)
+        secs += t
+    return float(np.median(rates)), rates, secs, recs
+
+
+def cpu_baseline(rp, max_records, mt_records, threads, st_records, target_s=20.0, max_runs=15):
     """CPU baselines timed on this host on bounded samples of the same
-    workload (the first buffers of the batch, against the full object table):
+    workload (the first buffers of the batch, against the full object table);
+    each is run repeatedly until about its share of `target_s` seconds of
+    timed work and reports the MEDIAN per-run rate:
 
     * value: the multi-threaded bit-exact C++ restatement
-      (oracle/nmg_cpu_mt.cpp, `threads` host threads) on the first
-      `mt_records` records, analysed repeatedly until about `target_s` seconds
-      of analysis + merge time; rate = records / (analysis + merge seconds);
-    * single_thread_oracle: the single-threaded C restatement of the
-      reference loop (oracle/nmg_oracle.c, which keeps the reference's linear
-      call-site list and page-block lists) on the first `max_records` records."""
+      (oracle/nmg_cpu_mt.cpp) on `threads` host threads, first `mt_records`
+      records; rate = records / (analysis + merge seconds);
+    * single_thread: the same restatement on one thread, first `st_records`;
+    * reference_loop_oracle: the single-threaded C restatement of the
+      reference loop (oracle/nmg_oracle.c), which keeps the reference's
+      linear call-site list (find_call_site, mem_analyzer.c:1302-1331, run at
+      every object's first match) and linear page-block lists: with one call
+      site per object its cost grows with the square of the objects touched,
+      so its sample is `max_records` records (about 10 s)."""
     import tempfile
 
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pyoracle
 
-    out = {}
+    def mt(path, nthreads):
+        t = pyoracle.run_mt(path, None, threads=nthreads, levels=False)
+        return t["nb_samples"], t["analysis_s"] + t["merge_s"]
+
+    def st(path, d):
+        t = pyoracle.run(path, os.path.join(d, "out"), os.path.join(d, "stdout.txt"))
+        return t["nb_samples"], t["analysis_s"]
+
+    host = (f"the host has {os.cpu_count()} CPUs, of which this job's share is OMP_NUM_THREADS="
+            f"{os.environ.get('OMP_NUM_THREADS', 'unset')}")
     with tempfile.TemporaryDirectory() as d:
         sub, n = _sample_replay(rp, mt_records)
         path = os.path.join(d, "mt.bin")
         sub.write(path)
         del sub
-        pyoracle.run_mt(path, None, threads=threads, levels=False)  # warm-up (first touch of the arrays)
-        runs, samples, secs = 0, 0, 0.0
-        while runs < max_runs and (runs == 0 or secs < target_s):
-            t = pyoracle.run_mt(path, None, threads=threads, levels=False)
-            log(f"[rank 0] cpu baseline (mt) run {runs}: {t['nb_samples']} records, analysis {t['analysis_s']:.2f}s "
-                f"+ merge {t['merge_s']:.2f}s on {t['threads']} threads")
-            runs += 1
-            samples += t["nb_samples"]
-            secs += t["analysis_s"] + t["merge_s"]
+        mt(path, threads)  # warm-up (first touch of the arrays)
+        v, rates, secs, recs = _rate_runs(lambda: mt(path, threads), target_s, max_runs, f"{threads} threads")
         out = {
-            "value": samples / secs,
+            "value": v,
             "unit": "samples/s",
             "cores": threads,
             "kind": "port",
-            "sample": f"first {n} of {len(rp.buffers)} buffers ({samples // runs} records, full object table) "
-                      f"analysed {runs}x by the multi-threaded bit-exact restatement (oracle/nmg_cpu_mt.cpp) on "
-                      f"{threads} threads, {secs:.1f}s of analysis + merge; host has {os.cpu_count()} CPUs",
+            "sample": f"first {n} of {len(rp.buffers)} buffers ({recs} records, full object table) analysed "
+                      f"{len(rates)}x by the multi-threaded bit-exact restatement (oracle/nmg_cpu_mt.cpp) on "
+                      f"{threads} threads ({secs:.1f}s of analysis + merge), median run; {host}",
+            "runs": rates,
         }
         os.remove(path)
-        sub, n = _sample_replay(rp, max_records)
+        sub, n = _sample_replay(rp, st_records)
         path = os.path.join(d, "st.bin")
         sub.write(path)
-        runs, samples, secs = 0, 0, 0.0
-        while runs < max_runs and (runs == 0 or secs < target_s):
-            t = pyoracle.run(path, os.path.join(d, "out"), os.path.join(d, "stdout.txt"))
-            log(f"[rank 0] cpu baseline (oracle) run {runs}: {t['nb_samples']} records in {t['analysis_s']:.2f}s")
-            runs += 1
-            samples += t["nb_samples"]
-            secs += t["analysis_s"]
-        out["single_thread_oracle"] = {
-            "value": samples / secs, "cores": 1,
-            "sample": f"first {n} buffers ({samples // runs} records) analysed {runs}x, {secs:.1f}s of analysis loop; "
-                      "single-threaded like the reference (global mutex, mem_analyzer.c:254)"}
+        del sub
+        v, rates, secs, recs = _rate_runs(lambda: mt(path, 1), target_s / 2, max_runs, "1 thread")
+        out["single_thread"] = {
+            "value": v, "cores": 1,
+            "sample": f"first {n} buffers ({recs} records) analysed {len(rates)}x by oracle/nmg_cpu_mt.cpp on one "
+                      f"thread ({secs:.1f}s), median run"}
+        os.remove(path)
+        sub, n = _sample_replay(rp, max_records)
+        path = os.path.join(d, "ref.bin")
+        sub.write(path)
+        v, rates, secs, recs = _rate_runs(lambda: st(path, d), target_s / 4, max_runs, "reference loop")
+        out["reference_loop_oracle"] = {
+            "value": v, "cores": 1,
+            "sample": f"first {n} buffers ({recs} records) analysed {len(rates)}x ({secs:.1f}s of analysis loop), "
+                      "median run; single-threaded like the reference (global mutex, mem_analyzer.c:254), with its "
+                      "linear call-site list (quadratic in the objects touched)"}
     return out
 
 

@@ -11,9 +11,6 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libnumamma_gpu.so")
-# tools/ab.py only: time an alternative in-tree build of the same C-ABI
-if os.environ.get("NMG_LIB_VARIANT"):
-    LIB_PATH = os.path.join(_HERE, "build", "variants", "libnumamma_gpu_%s.so" % os.environ["NMG_LIB_VARIANT"])
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "numamma_gpu.h")
 
 # One HIP runtime per process: torch ships its own libamdhip64.so (same
@@ -184,6 +181,7 @@ _SIGS = {
     "nmg_last_analyze_ms": (C.c_int, [H, C.POINTER(C.c_float)]),
     "nmg_get_launch_times": (C.c_int, [H, C.POINTER(C.c_float), C.c_int]),
     "nmg_get_kernel_times": (C.c_int, [H, C.POINTER(C.c_float), C.POINTER(C.c_float), C.c_int]),
+    "nmg_debug_phase_times": (C.c_int, [H, C.POINTER(C.c_float), C.POINTER(C.c_float), C.c_int]),
     "nmg_report": (C.c_int, [H, C.POINTER(nmg_object_meta), C.POINTER(nmg_report_options), C.c_char_p]),
     "nmg_report_host": (C.c_int, [C.POINTER(nmg_host_results), C.POINTER(nmg_object_meta), C.POINTER(nmg_report_options), C.c_char_p]),
     "nmg_run_replay": (C.c_int, [C.c_char_p, C.c_char_p, C.c_char_p, C.c_char_p, C.c_int, C.c_uint32]),

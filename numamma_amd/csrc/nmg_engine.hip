@@ -102,6 +102,7 @@ struct nmg_engine {
   static constexpr int kRing = 64;  // per-launch timing events (nmg_get_launch_times)
   hipEvent_t ring0[kRing] = {}, ring1[kRing] = {};
   hipEvent_t ringm[kRing] = {};  // after the attribution kernel (before the log reduce)
+  hipEvent_t ringr[kRing] = {};  // after the first kernel (route_kernel / attribute_kernel)
   uint64_t nlaunch = 0;
   int num_cus = 256;
   int blocks_per_cu = 0;
@@ -548,6 +549,7 @@ extern "C" void nmg_destroy(nmg_engine* h) {
     if (h->ring0[i]) (void)hipEventDestroy(h->ring0[i]);
     if (h->ring1[i]) (void)hipEventDestroy(h->ring1[i]);
     if (h->ringm[i]) (void)hipEventDestroy(h->ringm[i]);
+    if (h->ringr[i]) (void)hipEventDestroy(h->ringr[i]);
   }
   if (h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
@@ -1566,6 +1568,7 @@ static int launch_events(nmg_engine* h, int* slot_out) {
   const int slot = (int)(h->nlaunch % nmg_engine::kRing);
   if (!h->ring0[slot]) {
     HIP_TRY(h, hipEventCreate(&h->ring0[slot]));
+    HIP_TRY(h, hipEventCreate(&h->ringr[slot]));
     HIP_TRY(h, hipEventCreate(&h->ringm[slot]));
     HIP_TRY(h, hipEventCreate(&h->ring1[slot]));
   }
@@ -1647,6 +1650,7 @@ static int launch_attribution(nmg_engine* h, const uint8_t* data, const BufDesc*
     } else {
       HIP_TRY(h, launch_attribute(false, mode, grid, h->stream, p));
     }
+    HIP_TRY(h, hipEventRecord(h->ringr[slot], h->stream));
     HIP_TRY(h, hipEventRecord(h->ringm[slot], h->stream));
     if (p.tlog) {  // sums the log per entry range, folds the packed counters
       TlogParams r;
@@ -1667,7 +1671,10 @@ static int launch_attribution(nmg_engine* h, const uint8_t* data, const BufDesc*
       HIP_TRY(h, launch_unpack(blocks, h->stream, h->d_sum64, p.pk64, h->E, p.pk_shift));
     }
   }
-  if (!nb) HIP_TRY(h, hipEventRecord(h->ringm[slot], h->stream));
+  if (!nb) {
+    HIP_TRY(h, hipEventRecord(h->ringr[slot], h->stream));
+    HIP_TRY(h, hipEventRecord(h->ringm[slot], h->stream));
+  }
   HIP_TRY(h, hipEventRecord(h->ring1[slot], h->stream));
   h->nlaunch++;
   h->launched = true;
@@ -1808,6 +1815,7 @@ static int route_analyze(nmg_engine* h, uint32_t nb, uint32_t grid) {
     rp.p.dbg = reinterpret_cast<unsigned long long*>(h->d_dbg);
   }
   HIP_TRY(h, launch_route(grid, h->stream, rp));
+  HIP_TRY(h, hipEventRecord(h->ringr[slot], h->stream));
   HIP_TRY(h, launch_overflow(h->stream, rp));
   ScatterParams sc;
   sc.cmeta = h->d_cmeta;
@@ -2656,6 +2664,24 @@ extern "C" int nmg_report(nmg_engine* h, const nmg_object_meta* meta, const nmg_
   rc = write_report(&res, meta, opts, stdout_path, err, dumps ? &dump : nullptr);
   if (rc && !err.empty()) h->last_error = err;
   return rc;
+}
+
+// Internal (not in include/numamma_gpu.h; bench.py): the first kernel's
+// time (route_kernel, or attribute_kernel) and the rest of the attribution
+// (the partition-first path's overflow, count, plan, scatter and local
+// kernels; the single-pass path's nothing) of up to n recent launches.
+extern "C" int nmg_debug_phase_times(nmg_engine* h, float* first_ms, float* rest_ms, int n) {
+  if (!h || (n > 0 && (!first_ms || !rest_ms))) return NMG_ERR_INVALID;
+  HIP_TRY(h, hipSetDevice(h->device));
+  HIP_TRY(h, hipStreamSynchronize(h->stream));
+  const int avail = (int)std::min<uint64_t>(h->nlaunch, nmg_engine::kRing);
+  const int cnt = std::min(n, avail);
+  for (int i = 0; i < cnt; i++) {
+    const int slot = (int)((h->nlaunch - cnt + i) % nmg_engine::kRing);
+    HIP_TRY(h, hipEventElapsedTime(&first_ms[i], h->ring0[slot], h->ringr[slot]));
+    HIP_TRY(h, hipEventElapsedTime(&rest_ms[i], h->ringr[slot], h->ringm[slot]));
+  }
+  return cnt;
 }
 
 // Internal (not in include/numamma_gpu.h): per-wave phase cycle counts of the

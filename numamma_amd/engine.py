@@ -154,6 +154,14 @@ class Engine:
         cnt = self._c(lib.nmg_get_kernel_times(self.h, a, t, n))
         return [a[i] for i in range(cnt)], [t[i] for i in range(cnt)]
 
+    def phase_times(self, n: int = 64):
+        """(first kernel ms, rest of the attribution ms) of up to n recent launches:
+        route_kernel and the local pass (partition-first path), or
+        attribute_kernel and nothing (single-pass path)."""
+        a, t = (C.c_float * n)(), (C.c_float * n)()
+        cnt = self._c(lib.nmg_debug_phase_times(self.h, a, t, n))
+        return [a[i] for i in range(cnt)], [t[i] for i in range(cnt)]
+
     def last_analyze_ms(self) -> float:
         ms = C.c_float()
         self._c(lib.nmg_last_analyze_ms(self.h, C.byref(ms)))

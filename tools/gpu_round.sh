@@ -87,10 +87,9 @@ for s in $STAGES; do
           -- python3 $ROOT/bench.py --workload ${TRAFFIC_WL:-c2} --secondary "" --steps 3 --warmup 1 --no-cpu-baseline \
           > $OUT/traffic_${TAG}_$c.log 2>&1 || { echo "traffic pass $c failed"; tail -20 $OUT/traffic_${TAG}_$c.log; exit 1; }
       done
-      # the record stream of one launch (40 B records) is the only x2-corrected part
-      python3 tools/pmc_summary.py $OUT/traffic_${TAG}_FETCH_SIZE $OUT/traffic_${TAG}_WRITE_SIZE \
-        ${TRAFFIC_STREAM:+--stream-bytes $TRAFFIC_STREAM} \
-        > $OUT/pmc_${TRAFFIC_WL:-c2}_$TAG.json && cat $OUT/pmc_${TRAFFIC_WL:-c2}_$TAG.json ;;
+      # per kernel of the attribution launch, stamped with the kernel-source hash
+      python3 tools/pmc_pipeline.py --workload ${TRAFFIC_WL:-c2} --fetch $OUT/traffic_${TAG}_FETCH_SIZE \
+        --write $OUT/traffic_${TAG}_WRITE_SIZE --out $OUT/pmc_${TRAFFIC_WL:-c2}_$TAG.json ;;
     marker)
       # roctx ranges (stage, attribute, merge, report) beside the kernel trace
       echo "== rocprofv3 marker + kernel trace"
@@ -134,11 +133,6 @@ for s in $STAGES; do
       timeout -k 10 900 python tools/exp_alloc.py --workload ${ALLOC_WL:-c4} > $OUT/alloc_$TAG.json 2> $OUT/alloc_$TAG.err \
         || { echo "alloc failed"; tail -30 $OUT/alloc_$TAG.err; exit 1; }
       cat $OUT/alloc_$TAG.json ;;
-    ab)
-      echo "== A/B variants (${AB_VARIANTS:-base})"
-      timeout -k 10 900 python tools/ab.py --variants ${AB_VARIANTS:-base} --workloads ${AB_WL:-c2,k1m} --rounds ${AB_ROUNDS:-2} \
-        > $OUT/ab_$TAG.json 2> $OUT/ab_$TAG.err || { echo "ab failed"; tail -30 $OUT/ab_$TAG.err; exit 1; }
-      cat $OUT/ab_$TAG.json ;;
     pmc)
       echo "== rocprofv3 pmc FETCH_SIZE"
       rm -rf $OUT/pmc_$TAG
