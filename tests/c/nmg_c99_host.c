@@ -13,9 +13,27 @@
  * involved.
  *
  *   nmg_c99_host replay.bin output_dir stdout_path
+ *   nmg_c99_host --bridge replay.bin output_dir stdout_path
+ *
+ * Under an LD_PRELOAD allocator interposer (tests/c/nmg_interpose.c, the
+ * hazards of INTEGRATION.md section 2):
+ *  - NMG_HOST_PROTECT=1 raises the interposer's thread-local recursion
+ *    counter (`nmg_interpose_unsafe`, found through dlopen(NULL)) around every
+ *    engine call, as NumaMMa's analysis code runs with is_recurse_unsafe
+ *    raised (numamma.h.in:60-74); unset, the engine's allocations are
+ *    recorded like the application's;
+ *  - --bridge runs the out-of-process fallback instead: the replay is
+ *    recorded through the host-only capture bridge (nmg_replay_open /
+ *    add_ring / close: no HIP call in this process), then LD_PRELOAD is set
+ *    to $NMG_BRIDGE_PRELOAD (the value without the interposer; unset when
+ *    empty, like unset_ld_preload, mem_intercept.c:472-502) and the helper
+ *    $NMG_BRIDGE_HELPER (numamma_amd/bin/nmg_replay) analyses and reports
+ *    it.
  *
  * Exit status 0 on success; otherwise the failing call and nmg_strerror().
  */
+#define _POSIX_C_SOURCE 200809L
+#include <dlfcn.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -66,6 +84,54 @@ static int fail(const char *what, int rc, nmg_engine *h) {
   return 1;
 }
 
+static volatile int *unsafe_flag; /* the interposer's recursion counter (NMG_HOST_PROTECT=1) */
+#define ENGINE(call)            \
+  do {                          \
+    if (unsafe_flag) ++*unsafe_flag; \
+    rc = (call);                \
+    if (unsafe_flag) --*unsafe_flag; \
+  } while (0)
+
+/* --bridge: the capture bridge, then the helper without the interposer */
+static int bridge(const uint8_t *file, size_t off, uint32_t nthreads, const uint64_t *keys, const uint32_t *entry_off,
+                  uint32_t nkeys, const struct nmg_object *obj, const struct nmg_object_meta *meta, uint32_t nent,
+                  uint32_t nbufs, const char *outdir, const char *stdout_path) {
+  char path[4096], cmd[16384];
+  const char *helper = getenv("NMG_BRIDGE_HELPER"), *pre = getenv("NMG_BRIDGE_PRELOAD");
+  nmg_replay_writer *w = NULL;
+  uint32_t b;
+  int rc;
+  if (!helper) {
+    fprintf(stderr, "--bridge needs NMG_BRIDGE_HELPER\n");
+    return 2;
+  }
+  snprintf(path, sizeof path, "%s.replay.bin", outdir);
+  rc = nmg_replay_open(&w, path, nthreads, keys, entry_off, nkeys, obj, meta, nent);
+  if (rc) return fail("nmg_replay_open", rc, NULL);
+  for (b = 0; b < nbufs; b++) {
+    uint32_t rank = rd32(file + off), acc = rd32(file + off + 4);
+    uint64_t tail = rd64(file + off + 8), head = rd64(file + off + 16), ring = rd64(file + off + 24);
+    off += 32;
+    rc = nmg_replay_add_ring(w, file + off, ring, tail, head, rank, acc);
+    if (rc) return fail("nmg_replay_add_ring", rc, NULL);
+    off += pad8((size_t)ring);
+  }
+  rc = nmg_replay_close(w);
+  if (rc) return fail("nmg_replay_close", rc, NULL);
+  if (pre && *pre)
+    setenv("LD_PRELOAD", pre, 1);
+  else
+    unsetenv("LD_PRELOAD");
+  snprintf(cmd, sizeof cmd, "'%s' '%s' '%s' > '%s'", helper, path, outdir, stdout_path);
+  rc = system(cmd);
+  remove(path);
+  if (rc != 0) {
+    fprintf(stderr, "helper failed (%d): %s\n", rc, cmd);
+    return 1;
+  }
+  return 0;
+}
+
 int main(int argc, char **argv) {
   size_t len = 0, off;
   uint8_t *file;
@@ -81,9 +147,24 @@ int main(int argc, char **argv) {
   nmg_engine *h = NULL;
   int rc;
 
+  int use_bridge = argc == 5 && strcmp(argv[1], "--bridge") == 0;
+  const char *prot = getenv("NMG_HOST_PROTECT");
+
+  if (use_bridge) {
+    argv++;
+    argc--;
+  }
   if (argc != 4) {
-    fprintf(stderr, "usage: %s replay.bin output_dir stdout_path\n", argv[0]);
+    fprintf(stderr, "usage: %s [--bridge] replay.bin output_dir stdout_path\n", argv[0]);
     return 2;
+  }
+  if (prot && strcmp(prot, "1") == 0) {
+    void *self = dlopen(NULL, RTLD_LAZY);
+    unsafe_flag = self ? (volatile int *)dlsym(self, "nmg_interpose_unsafe") : NULL;
+    if (!unsafe_flag) {
+      fprintf(stderr, "NMG_HOST_PROTECT=1 but no interposer is loaded\n");
+      return 2;
+    }
   }
   file = slurp(argv[1], &len);
   if (!file || len < 64 || memcmp(file, "NMGRPLY1", 8) != 0) {
@@ -130,31 +211,36 @@ int main(int argc, char **argv) {
     off += (size_t)ENTRY_BYTES * nent + 8 * (size_t)cs_len + pad8((size_t)str_len);
   }
 
+  if (use_bridge)
+    return bridge(file, off, nthreads, keys, entry_off, nkeys, obj, meta, nent, nbufs, argv[2], argv[3]);
+
   memset(&opt, 0, sizeof opt);
   opt.device = 0;
   opt.flags = NMG_F_MATCH_SAMPLES | NMG_F_PAGE_HIST;
   opt.nb_threads = nthreads;
-  rc = nmg_create(&h, &opt);
+  ENGINE(nmg_create(&h, &opt));
   if (rc) return fail("nmg_create", rc, NULL);
-  rc = nmg_set_objects(h, keys, entry_off, nkeys, obj, nent);
+  ENGINE(nmg_set_objects(h, keys, entry_off, nkeys, obj, nent));
   if (rc) return fail("nmg_set_objects", rc, h);
   for (b = 0; b < nbufs; b++) { /* `samples` list order (mem_sampling.c:324) */
     uint32_t rank = rd32(file + off), acc = rd32(file + off + 4);
     uint64_t tail = rd64(file + off + 8), head = rd64(file + off + 16), ring = rd64(file + off + 24);
     off += 32;
-    rc = nmg_submit_ring(h, file + off, ring, tail, head, rank, acc);
+    ENGINE(nmg_submit_ring(h, file + off, ring, tail, head, rank, acc));
     if (rc) return fail("nmg_submit_ring", rc, h);
     off += pad8((size_t)ring);
   }
-  rc = nmg_analyze(h);
-  if (!rc) rc = nmg_synchronize(h);
+  ENGINE(nmg_analyze(h));
+  if (!rc) ENGINE(nmg_synchronize(h));
   if (rc) return fail("nmg_analyze", rc, h);
   memset(&ro, 0, sizeof ro);
   ro.output_dir = argv[2];
   ro.dump_single_items = 1;
-  rc = nmg_report(h, meta, &ro, argv[3]);
+  ENGINE(nmg_report(h, meta, &ro, argv[3]));
   if (rc) return fail("nmg_report", rc, h);
+  if (unsafe_flag) ++*unsafe_flag;
   nmg_destroy(h);
+  if (unsafe_flag) --*unsafe_flag;
   free(file);
   free(keys);
   free(entry_off);

@@ -1,0 +1,58 @@
+"""The engine inside an LD_PRELOAD'ed process, on
+the GPU: bin/nmg_c99_host runs INTEGRATION.md section 1's sequence with
+tests/c/nmg_interpose.c preloaded -- every malloc/new of the HIP runtime, the
+engine, its copy pool and the report's writer threads goes through a 64-byte
+header + canary block, safe allocations are recorded (mutex + backtrace) and
+every pthread_create is trampolined through a per-thread init, as under
+NumaMMa's libnumamma.so (src/mem_intercept.c:75-130, 246-299, 325-387).
+
+* protected: the host raises the interposer's thread-local recursion
+  counter around every engine call (is_recurse_unsafe, numamma.h.in:60-74):
+  the calling thread's allocations are not recorded, the runtime's own
+  threads' are;
+* unprotected: everything recorded;
+* bridge: the out-of-process fallback (capture bridge under the interposer,
+  helper nmg_replay without it, mem_intercept.c:472-502).
+
+Each is byte-identical to the oracle's report."""
+import os
+import subprocess
+
+import pytest
+
+import pyoracle
+from numamma_amd.replay import SynthConfig, generate
+from test_interpose_host import BIN, interposed_env, interposer_stats
+
+pytestmark = pytest.mark.gpu
+
+
+def _compare(d, a, b):
+    assert open(os.path.join(d, a + ".txt"), "rb").read() == open(os.path.join(d, b + ".txt"), "rb").read()
+    fa, fb = sorted(os.listdir(os.path.join(d, a))), sorted(os.listdir(os.path.join(d, b)))
+    assert fa == fb and fa
+    for f in fa:
+        assert open(os.path.join(d, a, f), "rb").read() == open(os.path.join(d, b, f), "rb").read(), f
+
+
+@pytest.mark.parametrize("mode", ["protected", "unprotected", "bridge"])
+def test_engine_under_interposer(tmp_path, mode):
+    d = str(tmp_path)
+    rp = generate(SynthConfig(nb_samples=150_000, nb_intervals=3_000, lost_frac=1e-3, wrap_one=True, seed=83))
+    path = os.path.join(d, "replay.bin")
+    rp.write(path)
+    pyoracle.run(path, os.path.join(d, "o"), os.path.join(d, "o.txt"))
+    args = [os.path.join(BIN, "nmg_c99_host")] + (["--bridge"] if mode == "bridge" else [])
+    extra = {"protected": {"NMG_HOST_PROTECT": "1"}, "unprotected": {},
+             "bridge": {"NMG_BRIDGE_HELPER": os.path.join(BIN, "nmg_replay")}}[mode]
+    r = subprocess.run(args + [path, os.path.join(d, "e"), os.path.join(d, "e.txt")],
+                       env=interposed_env(**extra), capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0, r.stderr[-3000:]
+    st = interposer_stats(r.stderr)
+    print(mode, st)
+    assert st["recorded"] > 0
+    if mode != "bridge":
+        assert st["threads"] > 0  # HIP runtime / copy pool / report writer threads went through the hook
+    if mode == "protected":
+        assert st["unsafe_skips"] > 0
+    _compare(d, "o", "e")

@@ -29,6 +29,9 @@ CASES = [
     # a single alarm at the end: every object freed by then matches as offline would
     (SynthConfig(nb_samples=60_000, nb_intervals=2_000, nb_threads=2, with_stack=False, buffer_records=400,
                  seed=73), 1, 4 << 20),
+    # configs[4] scale: 1.2M records over 48 alarms, 20k intervals (large-table lookup), reuse + realloc
+    (SynthConfig(nb_samples=1_200_000, nb_intervals=20_000, nb_threads=8, with_stack=False, reuse_frac=0.2,
+                 realloc_frac=0.05, buffer_records=1_000, seed=76), 48, 1 << 20),
 ]
 
 
@@ -45,7 +48,7 @@ def _same_dirs(a, b):
         assert open(os.path.join(a, f), "rb").read() == open(os.path.join(b, f), "rb").read(), f
 
 
-@pytest.mark.parametrize("cfg,nb_alarms,chunk", CASES, ids=["k400", "k30k", "one_alarm"])
+@pytest.mark.parametrize("cfg,nb_alarms,chunk", CASES, ids=["k400", "k30k", "one_alarm", "m1_48_alarms"])
 def test_online_analysis_bit_exact(tmp_path, cfg, nb_alarms, chunk):
     from numamma_amd.engine import Engine
 
