@@ -111,11 +111,16 @@ struct nmg_options {
    * are distinct, a device-side merge when they are one device (testing).
    * Results, getters and nmg_report read the merged counters.  Such an engine
    * takes host buffers (nmg_submit_*); device-resident buffers and streaming
-   * stay single-GPU.  0 or 1: one GPU, `device`. */
+   * stay single-GPU.  0 or 1: one GPU, `device`.
+   * The three fields below were added after the first version of this
+   * struct: they are read only when abi_version == NMG_OPTIONS_ABI, so a
+   * caller built against the older, shorter struct (or one that zeroes
+   * them) gets a one-GPU engine instead of reading past its struct. */
   uint32_t nb_gpus;
-  uint32_t reserved;
+  uint32_t abi_version;      /* NMG_OPTIONS_ABI to use nb_gpus / devices */
   const int32_t *devices;
 };
+#define NMG_OPTIONS_ABI 0x4e4d4702u /* "NMG" v2: nmg_options with nb_gpus / abi_version / devices */
 
 struct nmg_report_options {
   const char *output_dir;  /* settings.output_dir; call_sites.log etc. land here */
@@ -178,16 +183,25 @@ int nmg_set_objects(nmg_engine *h, const uint64_t *keys, const uint32_t *entry_o
  * Online analysis (--online-analysis: __process_samples analyses each alarm's
  * rings in place, mem_sampling.c:953-954, against the object table as it is
  * at that alarm): replace the lookup table, keeping every counter.  The
- * table of nmg_set_objects is the final one (ids, page-histogram layout,
- * report metadata); this one is the table at the alarm, flattened the same
- * way: keys[] ascending, key i's entries [entry_off[i], entry_off[i+1]) of
- * objects[] newest-first, and entry_ids[j] the id (index in the
- * nmg_set_objects table) of objects[j].  Objects still alive at the alarm
- * carry free_date 0 (they never match, quirk Q3); objects not yet allocated
- * are absent.  An object's buffer_size must not exceed its final one (its
- * page cells were laid out by nmg_set_objects).  In streaming mode the open
- * chunk is analysed with the previous table first.  Copied; the caller keeps
- * ownership.
+ * table is flattened like nmg_set_objects': keys[] ascending, key i's entries
+ * [entry_off[i], entry_off[i+1]) of objects[] newest-first, and entry_ids[j]
+ * the id of objects[j] -- the index of its counters.  Objects still alive at
+ * the alarm carry free_date 0 (they never match, quirk Q3); objects not yet
+ * allocated are absent.
+ *   Live hosts (mem_info->id - 1 as the id): nmg_set_objects may start empty
+ * (or with the table of the first alarm); an update may list new ids, which
+ * must run consecutively from the current entry count: their counters start
+ * at zero, as _init_mem_info gives a new object counters at creation
+ * (mem_analyzer.c:567-572).  An object whose size grew (ma_record_free,
+ * :1287) keeps its page counts in a larger range.
+ *   Recorded runs: nmg_set_objects with the final table, and alarm tables
+ * listing subsets of its ids.
+ *   The report describes each entry as the latest table listed it, walking
+ * the entries in the order of the latest table that listed every one (at
+ * exit, pass the table ma_finalize walks: nmg_update_objects with the final
+ * table; nmg_report's meta[] then follows that table's order).  In streaming
+ * mode the open chunk is analysed with the previous table first.  Copied; the
+ * caller keeps ownership.
  */
 int nmg_update_objects(nmg_engine *h, const uint64_t *keys, const uint32_t *entry_off, uint32_t nb_keys,
                        const uint32_t *entry_ids, const struct nmg_object *objects);

@@ -83,6 +83,9 @@ class nmg_object_meta(C.Structure):
     ]
 
 
+NMG_OPTIONS_ABI = 0x4E4D4702
+
+
 class nmg_options(C.Structure):
     _fields_ = [
         ("device", C.c_int32),
@@ -92,7 +95,7 @@ class nmg_options(C.Structure):
         ("hist_budget_bytes", C.c_uint64),
         ("sparse_capacity", C.c_uint64),
         ("nb_gpus", C.c_uint32),
-        ("reserved", C.c_uint32),
+        ("abi_version", C.c_uint32),  # NMG_OPTIONS_ABI: nb_gpus / devices are read
         ("devices", C.POINTER(C.c_int32)),
     ]
 

@@ -331,6 +331,12 @@ __device__ __forceinline__ Rec decode_rec(const RawRec& r, uint64_t pos) {
 }
 
 
+// s_waitcnt vmcnt(0) (expcnt / lgkmcnt left alone) as a real waitcnt
+// instruction, which the compiler's own waitcnt pass accounts for: a rare
+// path that issued global memory ops ends with it, so that the waits on the
+// common path after it need not count them
+__device__ __forceinline__ void vm_drain() { __builtin_amdgcn_s_waitcnt(0x0f70); }
+
 // shader-clock stamp that the scheduler does not move work across
 __device__ __forceinline__ uint64_t stamp() {
   __builtin_amdgcn_sched_barrier(0);

@@ -125,7 +125,9 @@ struct nmg_engine {
   uint32_t nb_fences = 0, fence_log2 = 0, dir_log2 = 0;
   std::vector<uint64_t> hist_base, npages, buffer_size, entry_addr;
   std::vector<DevEntry> dev_entries;  // host copy of d_entries (nmg_update_objects builds from it)
-  std::vector<nmg_object> objects;  // the table as given (all_memory_objects.dat)
+  std::vector<nmg_object> objects;  // each entry as the latest table lists it (the report's objects)
+  std::vector<uint32_t> order;      // report walk order (position -> id) when it is not the id order:
+                                    // the latest table that listed every entry (nmg_update_objects)
   std::vector<uint32_t> sparse_entries;
   uint64_t hist_cells = 0;
   uint64_t hist_budget = 4ull << 30;
@@ -462,6 +464,17 @@ extern "C" int nmg_create(nmg_engine** out, const nmg_options* opt) {
   *out = nullptr;
   nmg_engine* h = new (std::nothrow) nmg_engine();
   if (!h) return NMG_ERR_NOMEM;
+  // nb_gpus / devices only from a caller of the current struct (NMG_OPTIONS_ABI):
+  // an older caller's struct ends before them
+  nmg_options o2{};
+  if (opt) {
+    o2 = *opt;
+    if (o2.abi_version != NMG_OPTIONS_ABI) {
+      o2.nb_gpus = 0;
+      o2.devices = nullptr;
+    }
+    opt = &o2;
+  }
   if (opt) {
     h->device = opt->nb_gpus >= 1 && opt->devices ? opt->devices[0] : opt->device;
     h->flags = opt->flags;
@@ -875,6 +888,7 @@ extern "C" int nmg_set_objects(nmg_engine* h, const uint64_t* keys, const uint32
   h->buffer_size.resize(nb_entries);
   h->entry_addr.resize(nb_entries);
   h->objects.assign(entries, entries + nb_entries);
+  h->order.clear();
   h->sparse_entries.clear();
   h->hist_cells = 0;
   std::vector<DevEntry> dev(nb_entries);
@@ -949,8 +963,151 @@ extern "C" int nmg_set_objects(nmg_engine* h, const uint64_t* keys, const uint32
 static int stream_flush(nmg_engine* h);
 static int route_settle(nmg_engine* h);
 
-// --online-analysis: the table at an alarm (entries by their set_objects
-// ids), counters kept (mem_sampling.c:953-954 against the live mem_list)
+// A live --online-analysis table (nmg_update_objects) may hold entries the
+// engine has not seen: objects created since the previous alarm (ids E ..
+// newE - 1, _init_mem_info's next id, mem_analyzer.c:567-568, with their
+// counters from creation, :569-572), and objects whose size at free
+// (ma_record_free, :1287) outgrew their page cells.  New entries get page
+// cells like nmg_set_objects gives them (dense within the budget, sparse
+// otherwise); a dense entry that outgrew its cells moves to a new range with
+// its counts.  Every id-indexed counter array is re-laid out on the device
+// for the new entry count, counters kept.  (The stream is idle here.)
+static int grow_entries(nmg_engine* h, uint32_t newE, const uint32_t* ids, const nmg_object* objs, uint32_t n) {
+  const uint32_t oldE = h->E;
+  const uint64_t T = h->T;
+  const bool want_hist = (h->flags & NMG_F_PAGE_HIST) && (h->flags & NMG_F_MATCH_SAMPLES);
+  const uint64_t max_cells_per_entry = 1ull << 24, budget_cells = h->hist_budget / 4;
+  const uint64_t oldCells = h->hist_cells;
+  uint64_t cells = oldCells;
+  struct Move {
+    uint64_t from, to, np;
+  };
+  std::vector<Move> moves;
+  const size_t nsparse0 = h->sparse_entries.size();
+  h->hist_base.resize(newE, kHistSparse);
+  h->npages.resize(newE, 1);
+  h->buffer_size.resize(newE, 0);
+  h->entry_addr.resize(newE, 0);
+  h->objects.resize(newE, nmg_object{0, 0, 0, 0});
+  h->dev_entries.resize(newE);
+  for (uint32_t e = oldE; e < newE; e++) {
+    DevEntry& d = h->dev_entries[e];
+    memset(&d, 0, sizeof(d));
+    d.hist = kHistSparse;
+    d.sidx = ~0u;
+    d.id = e;
+  }
+  for (uint32_t j = 0; j < n; j++) {
+    const uint32_t id = ids[j];
+    const uint64_t np = objs[j].buffer_size / kPageSize + 1;
+    DevEntry& d = h->dev_entries[id];
+    if (id >= oldE) {
+      h->npages[id] = np;
+      if (!want_hist) continue;
+      if (np * T <= max_cells_per_entry && (cells + np) * T <= budget_cells && cells + np < 0xffffffffull) {
+        d.hist = h->hist_base[id] = cells;
+        cells += np;
+      } else {
+        if (h->sparse_entries.size() >= (1u << 22)) return fail(h, NMG_ERR_CAPACITY, "too many sparse entries");
+        d.sidx = (uint32_t)h->sparse_entries.size();
+        h->sparse_entries.push_back(id);
+      }
+    } else if (np > h->npages[id]) {
+      if (want_hist && h->hist_base[id] != kHistSparse) {
+        if (np * T > max_cells_per_entry || (cells + np) * T > budget_cells || cells + np >= 0xffffffffull)
+          return fail(h, NMG_ERR_CAPACITY, "an object outgrew its page cells past the histogram budget");
+        moves.push_back({h->hist_base[id], cells, h->npages[id]});
+        d.hist = h->hist_base[id] = cells;
+        cells += np;
+      }
+      h->npages[id] = np;
+    }
+  }
+  cells = (cells + 3) & ~uint64_t(3);
+  // id-indexed counters, re-laid out for newE entries
+  const uint64_t n_sum = 2 * kGlobalSums + (uint64_t)newE * 4 +
+                         ((h->flags & NMG_F_OBJECT_LEVELS) ? (uint64_t)newE * 2 * kLevelWords : 0);
+  const uint64_t n_min = 36 + (uint64_t)newE + 1;
+  uint64_t *sum = nullptr, *mn = nullptr;
+  uint32_t* hist = nullptr;
+  unsigned long long* pk = nullptr;
+  DevEntry* ent = nullptr;
+  auto undo = [&](hipError_t e, const char* what) {
+    (void)hipFree(sum);
+    (void)hipFree(mn);
+    (void)hipFree(hist);
+    (void)hipFree(pk);
+    (void)hipFree(ent);
+    return fail(h, NMG_ERR_HIP, std::string("nmg_update_objects: ") + what + ": " + hipGetErrorString(e));
+  };
+  hipError_t e;
+  if ((e = hipMalloc(&sum, n_sum * 8)) != hipSuccess) return undo(e, "counters");
+  if ((e = hipMalloc(&mn, n_min * 8)) != hipSuccess) return undo(e, "ordinals");
+  if (cells && cells * T != oldCells * T && (e = hipMalloc(&hist, cells * T * 4)) != hipSuccess)
+    return undo(e, "page histogram");
+  if (newE > kObjSlots && (e = hipMalloc(&pk, (size_t)newE * 2 * 8)) != hipSuccess) return undo(e, "packed counters");
+  if ((e = hipMalloc(&ent, (size_t)newE * sizeof(DevEntry))) != hipSuccess) return undo(e, "entries");
+  hipStream_t st = h->stream;
+  if ((e = hipMemsetAsync(sum, 0, n_sum * 8, st)) != hipSuccess ||
+      (e = hipMemcpyAsync(sum, h->d_sum64, 2 * kGlobalSums * 8, hipMemcpyDeviceToDevice, st)) != hipSuccess ||
+      (oldE && (e = hipMemcpy2DAsync(sum + 2 * kGlobalSums, (size_t)newE * 8, h->d_sum64 + 2 * kGlobalSums,
+                                     (size_t)oldE * 8, (size_t)oldE * 8, 4, hipMemcpyDeviceToDevice, st)) != hipSuccess) ||
+      ((h->flags & NMG_F_OBJECT_LEVELS) && oldE &&
+       (e = hipMemcpyAsync(sum + 2 * kGlobalSums + (uint64_t)newE * 4, h->d_sum64 + 2 * kGlobalSums + (uint64_t)oldE * 4,
+                           (size_t)oldE * 2 * kLevelWords * 8, hipMemcpyDeviceToDevice, st)) != hipSuccess) ||
+      (e = hipMemsetAsync(mn, 0xff, n_min * 8, st)) != hipSuccess ||
+      (e = hipMemcpyAsync(mn, h->d_min64, (36 + (size_t)oldE) * 8, hipMemcpyDeviceToDevice, st)) != hipSuccess ||
+      (e = hipMemcpyAsync(mn + 36 + newE, h->d_min64 + 36 + oldE, 8, hipMemcpyDeviceToDevice, st)) != hipSuccess ||
+      (pk && (e = hipMemsetAsync(pk, 0, (size_t)newE * 2 * 8, st)) != hipSuccess) ||
+      (e = hipMemcpyAsync(ent, h->dev_entries.data(), (size_t)newE * sizeof(DevEntry), hipMemcpyHostToDevice, st)) !=
+          hipSuccess)
+    return undo(e, "re-layout");
+  if (hist) {  // [thread][cell] rows with the new stride; moved entries' counts to their new range
+    if ((e = hipMemsetAsync(hist, 0, cells * T * 4, st)) != hipSuccess ||
+        (oldCells && (e = hipMemcpy2DAsync(hist, cells * 4, h->d_hist, oldCells * 4, oldCells * 4, T,
+                                           hipMemcpyDeviceToDevice, st)) != hipSuccess))
+      return undo(e, "page histogram re-layout");
+    for (const Move& m : moves)
+      if ((e = hipMemcpy2DAsync(hist + m.to, cells * 4, hist + m.from, cells * 4, m.np * 4, T, hipMemcpyDeviceToDevice,
+                                st)) != hipSuccess ||
+          (e = hipMemset2DAsync(hist + m.from, cells * 4, 0, m.np * 4, T, st)) != hipSuccess)
+        return undo(e, "page cells of a grown object");
+  }
+  if ((e = hipStreamSynchronize(st)) != hipSuccess) return undo(e, "re-layout");
+  (void)hipFree(h->d_sum64);
+  (void)hipFree(h->d_min64);
+  (void)hipFree(h->d_pk64);
+  if (h->d_chain == h->d_entries) h->d_chain = ent;
+  (void)hipFree(h->d_entries);
+  h->d_sum64 = sum;
+  h->d_min64 = mn;
+  h->d_pk64 = pk;
+  h->d_entries = ent;
+  if (hist) {
+    (void)hipFree(h->d_hist);
+    h->d_hist = hist;
+  }
+  h->n_sum64 = n_sum;
+  h->n_min64 = n_min;
+  h->hist_cells = cells;
+  h->E = newE;
+  if (nsparse0 == 0 && !h->sparse_entries.empty() && !h->d_sparse_keys) {  // first sparse entry: its table
+    HIP_TRY(h, hipMalloc(&h->d_sparse_keys, h->sparse_cap * 8));
+    HIP_TRY(h, hipMalloc(&h->d_sparse_vals, h->sparse_cap * 4));
+    HIP_TRY(h, hipMalloc(&h->d_sparse_dirty, 2 * 4));
+    HIP_TRY(h, hipMemsetAsync(h->d_sparse_keys, 0xff, h->sparse_cap * 8, st));
+    HIP_TRY(h, hipMemsetAsync(h->d_sparse_vals, 0, h->sparse_cap * 4, st));
+    HIP_TRY(h, hipMemsetAsync(h->d_sparse_dirty, 0, 2 * 4, st));
+    HIP_TRY(h, hipStreamSynchronize(st));
+  }
+  return NMG_OK;
+}
+
+// --online-analysis: the table at an alarm, counters kept (mem_sampling.c:953-954
+// against the live mem_list).  Entry ids index the counters: ids of the
+// nmg_set_objects table, and (live hosts) ids past it for objects created
+// since (grow_entries).  The report describes each entry as the latest table
+// lists it, in the order of the latest table that lists every entry.
 extern "C" int nmg_update_objects(nmg_engine* h, const uint64_t* keys, const uint32_t* entry_off,
                                   uint32_t nb_keys, const uint32_t* entry_ids, const nmg_object* objects) {
   Range range("nmg_update_objects");
@@ -959,20 +1116,21 @@ extern "C" int nmg_update_objects(nmg_engine* h, const uint64_t* keys, const uin
   const uint32_t n = nb_keys ? entry_off[nb_keys] : 0;
   int rc = check_table(h, keys, nb_keys ? entry_off : nullptr, nb_keys, n);
   if (rc) return rc;
-  std::vector<DevEntry> chain(n);
-  for (uint32_t j = 0; j < n; j++) {
-    const uint32_t id = entry_ids[j];
-    if (id >= h->E) return fail(h, NMG_ERR_RANGE, "entry id past the nmg_set_objects table");
-    const nmg_object& o = objects[j];
-    if (o.buffer_size > h->buffer_size[id])
-      return fail(h, NMG_ERR_RANGE, "object larger than in the nmg_set_objects table (its page cells)");
-    DevEntry& d = chain[j];
-    d = h->dev_entries[id];  // hist, sidx, id of the final table
-    d.addr = o.buffer_addr;
-    d.end = o.buffer_addr + o.buffer_size;
-    d.alloc = o.alloc_date;
-    d.free = o.free_date;
-    d.count = d.first = 0;
+  // ids: each at most once; new ones (>= E) consecutive from E
+  uint32_t newE = h->E;
+  for (uint32_t j = 0; j < n; j++) newE = std::max(newE, entry_ids[j] + 1);
+  if (entry_ids && n && (uint64_t)newE > (1ull << 31)) return fail(h, NMG_ERR_RANGE, "too many entries");
+  uint64_t nb_grown = 0;
+  {
+    std::vector<uint8_t> seen(newE, 0);
+    for (uint32_t j = 0; j < n; j++) {
+      const uint32_t id = entry_ids[j];
+      if (seen[id]) return fail(h, NMG_ERR_INVALID, "an entry id listed twice in one table");
+      seen[id] = 1;
+      if (id < h->E && objects[j].buffer_size / kPageSize + 1 > h->npages[id]) nb_grown++;
+    }
+    for (uint32_t id = h->E; id < newE; id++)
+      if (!seen[id]) return fail(h, NMG_ERR_RANGE, "new entry ids must be consecutive from the current entry count");
   }
   HIP_TRY(h, hipSetDevice(h->device));
   if (h->streaming) {  // the open chunk belongs to the previous alarms' table
@@ -981,7 +1139,27 @@ extern "C" int nmg_update_objects(nmg_engine* h, const uint64_t* keys, const uin
   }
   rc = route_settle(h);  // (reads the pool only, not the table)
   if (rc) return rc;
-  HIP_TRY(h, hipStreamSynchronize(h->stream));  // launches in flight read the old table
+  HIP_TRY(h, hipStreamSynchronize(h->stream));  // launches in flight read the old table and counters
+  if (h->multi_pending) {  // merges in flight write the counters being re-laid out
+    rc = multi_finish(h);
+    if (rc) return rc;
+  }
+  if (newE > h->E || nb_grown) {
+    rc = grow_entries(h, newE, entry_ids, objects, n);
+    if (rc) return rc;
+  }
+  std::vector<DevEntry> chain(n);
+  for (uint32_t j = 0; j < n; j++) {
+    const uint32_t id = entry_ids[j];
+    const nmg_object& o = objects[j];
+    DevEntry& d = chain[j];
+    d = h->dev_entries[id];  // hist, sidx, id
+    d.addr = o.buffer_addr;
+    d.end = o.buffer_addr + o.buffer_size;
+    d.alloc = o.alloc_date;
+    d.free = o.free_date;
+    d.count = d.first = 0;
+  }
   free_route_table(h);  // (the partitions describe the nmg_set_objects table)
   // build the alarm's lookup beside the current one; keep the current one if that fails
   const LookupSet prev = take_lookup(h);
@@ -999,6 +1177,21 @@ extern "C" int nmg_update_objects(nmg_engine* h, const uint64_t* keys, const uin
     put_lookup(h, prev);
     free_lookup(h);  // (keeps d_chain when it is the by-id entry array)
     put_lookup(h, cur);
+  }
+  // the report's view: every listed entry as this table lists it, and this
+  // table's order when it lists every entry (ma_finalize walks the table it
+  // has at exit, FOREACH_HASH, mem_analyzer.c:1381-1383)
+  for (uint32_t j = 0; j < n; j++) {
+    const uint32_t id = entry_ids[j];
+    h->objects[id] = objects[j];
+    h->buffer_size[id] = objects[j].buffer_size;
+    h->entry_addr[id] = objects[j].buffer_addr;
+  }
+  if (n == h->E) {
+    bool identity = true;
+    for (uint32_t j = 0; j < n && identity; j++) identity = entry_ids[j] == j;
+    if (identity) h->order.clear();
+    else h->order.assign(entry_ids, entry_ids + n);
   }
   for (nmg_engine* w : h->workers) {  // multi-GPU: the table on every device
     rc = nmg_update_objects(w, keys, entry_off, nb_keys, entry_ids, objects);
@@ -1853,6 +2046,18 @@ static int route_analyze(nmg_engine* h, uint32_t nb, uint32_t grid) {
   lp.descs = h->d_sdescs;
   lp.xl = xl;
   lp.seq0 = seq0;
+  if ((h->flags & kDbgLocalTiming) && !(h->flags & kDbgRouteTiming)) {  // (internal) per-wave phase cycles
+    const size_t n = (size_t)h->num_cus * (kWG / 64) * kRouteTimingWords;
+    if (n > h->dbg_cap) {
+      (void)hipFree(h->d_dbg);
+      h->d_dbg = nullptr;
+      HIP_TRY(h, hipMalloc(&h->d_dbg, n * 8));
+      h->dbg_cap = n;
+    }
+    HIP_TRY(h, hipMemsetAsync(h->d_dbg, 0, n * 8, h->stream));
+    h->dbg_len = n;
+    lp.p.dbg = reinterpret_cast<unsigned long long*>(h->d_dbg);
+  }
   HIP_TRY(h, launch_local((uint32_t)h->num_cus, h->stream, lp));
   HIP_TRY(h, hipEventRecord(h->ringm[slot], h->stream));
   HIP_TRY(h, hipEventRecord(h->ring1[slot], h->stream));
@@ -2632,6 +2837,45 @@ extern "C" int nmg_report(nmg_engine* h, const nmg_object_meta* meta, const nmg_
   res.nb_threads = h->T;
   res.match_samples = (h->flags & NMG_F_MATCH_SAMPLES) ? 1 : 0;
   res.objects = h->objects.data();
+  // live online tables: entries walked in the order of the latest table that
+  // listed them all (ids are creation order there); meta follows that order
+  std::vector<uint64_t> w_size, w_first, w_cw;
+  std::vector<nmg_object> w_obj;
+  std::vector<uint32_t> w_rows;
+  if (!h->order.empty()) {
+    if (opts && opts->dump_flags) return fail(h, NMG_ERR_STATE, "dump modes need the entries in id order");
+    const uint32_t E = h->E;
+    std::vector<uint32_t> pos(E);
+    w_size.resize(E);
+    w_first.resize(E);
+    w_cw.resize((size_t)E * 4);
+    w_obj.resize(E);
+    for (uint32_t k = 0; k < E; k++) {
+      const uint32_t id = h->order[k];
+      pos[id] = k;
+      w_size[k] = h->buffer_size[id];
+      w_first[k] = r.first[id];
+      for (int q = 0; q < 4; q++) w_cw[(size_t)k * 4 + q] = r.count_weight[(size_t)id * 4 + q];
+      w_obj[k] = h->objects[id];
+    }
+    // page rows (entry, thread, page, count), grouped by walk position
+    std::vector<uint32_t> idx((size_t)ncells);
+    for (uint32_t i = 0; i < (uint32_t)ncells; i++) idx[i] = i;
+    std::stable_sort(idx.begin(), idx.end(), [&](uint32_t a, uint32_t b) { return pos[rows[4 * a]] < pos[rows[4 * b]]; });
+    w_rows.resize(rows.size());
+    for (size_t i = 0; i < idx.size(); i++) {
+      const uint32_t* q = &rows[4 * (size_t)idx[i]];
+      w_rows[4 * i] = pos[q[0]];
+      w_rows[4 * i + 1] = q[1];
+      w_rows[4 * i + 2] = q[2];
+      w_rows[4 * i + 3] = q[3];
+    }
+    res.buffer_size = w_size.data();
+    res.first_ordinal = w_first.data();
+    res.count_weight = w_cw.data();
+    res.cells = w_rows.data();
+    res.objects = w_obj.data();
+  }
   // dump modes: the buffers' bytes (staging, or D2H of device-resident ones)
   // and every SAMPLE record's match
   DumpInput dump;

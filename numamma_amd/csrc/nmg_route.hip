@@ -432,7 +432,10 @@ constexpr uint32_t kDescLds = 512;
 
 __device__ __forceinline__ BufDesc route_desc(const RouteParams& rp, const uint4* s_desc, uint32_t r0, uint32_t i) {
   if (i - r0 < kDescLds) {
-    const uint4 v = s_desc[i - r0];
+    // (uniform: scalar registers, not 8 VGPRs per descriptor)
+    const uint4 l = s_desc[i - r0];
+    const uint4 v = make_uint4(__builtin_amdgcn_readfirstlane(l.x), __builtin_amdgcn_readfirstlane(l.y),
+                               __builtin_amdgcn_readfirstlane(l.z), __builtin_amdgcn_readfirstlane(l.w));
     BufDesc d;
     d.offset = u64of(v.x, v.y);
     d.len = v.z;
@@ -618,10 +621,8 @@ __global__ __launch_bounds__(kWG, 1) void route_kernel(RouteParams rp) {
 
       // ---- descriptors of the next window (the one after it is read now
       // and used a transition later), and its loads: issued before this
-      // window's records are processed -- unless a sorted batch waits for its
-      // chunk stores, which must go out before those loads (see
-      // route_write_batch); then the stores and the loads follow the
-      // processing, when the record's registers are free again
+      // window's records are processed, after the chunk stores of a sorted
+      // batch that waits for them (see route_write_batch)
       BufDesc nd0 = d0, nd1 = d1, nd2 = d2;
       if (nidx == idx + 1) {
         nd0 = d1;
@@ -633,7 +634,12 @@ __global__ __launch_bounds__(kWG, 1) void route_kernel(RouteParams rp) {
         if (nidx + 2 < r1) nd2 = route_desc(rp, s_desc, r0, nidx + 2);
       }
       const bool nhas1 = nidx + 1 < r1;
-      if (!wpending && nidx < r1) {
+      const bool wrote = wpending;  // (uniform)
+      if (wpending) {  // the previous batch's chunk stores go out before the next window's loads
+        route_write_batch<TIMING>(rt, rp, tid, L, nbatches - 1);
+        wpending = false;
+      }
+      if (nidx < r1) {  // (in flight while this window's records are processed)
         const RWin nl = rwin_lane(tid, (uint32_t)ncur, nd0, nd1, nhas1);
         rload_slot(p.data, nl, nd0, nd1, nx);
       }
@@ -666,15 +672,6 @@ __global__ __launch_bounds__(kWG, 1) void route_kernel(RouteParams rp) {
       }
       held = hr;
       hheld = true;
-      const bool wrote = wpending;  // (uniform)
-      if (wpending) {  // the previous batch's chunk stores, then the next window's loads
-        route_write_batch<TIMING>(rt, rp, tid, L, nbatches - 1);
-        wpending = false;
-        if (nidx < r1) {
-          const RWin nl = rwin_lane(tid, (uint32_t)ncur, nd0, nd1, nhas1);
-          rload_slot(p.data, nl, nd0, nd1, nx);
-        }
-      }
       {
         // per-buffer SAMPLE tallies (mem_sampling.c:921-926): lanes of this
         // wave in buffer idx + 1 are tid >= n0
@@ -846,6 +843,7 @@ __global__ __launch_bounds__(kWG) void scatter_kernel(ScatterParams r) {
 // ---------------------------------------------------------------------------
 // pass 3: attribute one partition per workgroup at a time
 
+template <bool TIMING>
 __global__ __launch_bounds__(kWG, 1) void local_kernel(LocalParams lp) {
   __shared__ uint64_t s_keys[kPartSlots];
   __shared__ uint4 s_nodes[2 * kPartSlots];
@@ -854,6 +852,7 @@ __global__ __launch_bounds__(kWG, 1) void local_kernel(LocalParams lp) {
   __shared__ unsigned long long s_owt[2][kPartEntries];
   __shared__ unsigned long long s_first[kPartEntries];
   __shared__ uint32_t s_pg[kPartCells / 2];
+  __shared__ uint32_t s_clist[kItemChunks];  // the item's chunk list entries
   __shared__ uint32_t s_item;
   // the global mem_counters of the records this workgroup attributes
   __shared__ unsigned long long s_gsums[2][kGlobalSums], s_gmins[2][18], s_gmaxs[2][18];
@@ -871,11 +870,18 @@ __global__ __launch_bounds__(kWG, 1) void local_kernel(LocalParams lp) {
   DualAcc gacc;  // per-lane update_counters, drained every kDrainWindows chunks
   dual_clear(gacc);
   uint32_t acc_chunks = 0;
+  RTimer rt;  // (kDbgLocalTiming) per-wave phase cycles
+#pragma unroll
+  for (int k = 0; k < 9; k++) rt.acc[k] = 0;
+  rt.last = TIMING ? stamp() : 0;
+  uint32_t nchunks = 0, nit = 0;
   while (true) {
     if (tid == 0) s_item = atomicAdd(lp.ctl + 1, 1u);
     __syncthreads();
     const uint32_t it = __builtin_amdgcn_readfirstlane(s_item);
+    rt_stamp<TIMING>(rt, 6);
     if (it >= nitems) break;
+    nit++;
     const uint4 item = lp.items[it];
     const uint32_t q = __builtin_amdgcn_readfirstlane(item.x);
     const PartInfo pi = lp.parts[q];
@@ -893,6 +899,7 @@ __global__ __launch_bounds__(kWG, 1) void local_kernel(LocalParams lp) {
       }
       const uint32_t* gd = lp.pe_dir + uint64_t(q) * kPartDir;
       for (uint32_t i = tid; i < kPartDir; i += kWG) s_dir[i] = gd[i];
+      for (uint32_t i = tid; i < item.z - item.y; i += kWG) s_clist[i] = lp.clist[item.y + i];
     }
     for (uint32_t i = tid; i < pi.ne; i += kWG) {
       s_owt[0][i] = s_owt[1][i] = 0;
@@ -901,54 +908,54 @@ __global__ __launch_bounds__(kWG, 1) void local_kernel(LocalParams lp) {
     const uint32_t ncell = (pages && pi.pages_lds) ? T * pi.span : 0u;
     for (uint32_t i = tid; i < (ncell + 1) / 2; i += kWG) s_pg[i] = 0;
     __syncthreads();
+    rt_stamp<TIMING>(rt, 7);
 
-    // each wave takes every 16th chunk of the item; the records of its next
-    // two chunks and the list entry after them are in flight while a chunk is
-    // processed (a wave's chunk is 1.5 KiB: one in flight per wave leaves
-    // HBM idle)
+    // Each wave takes every 16th chunk of the item (the item's list entries
+    // are in LDS); two chunks' records are in flight while one is processed
+    // (a wave's chunk is 1.5 KiB: one in flight per wave leaves HBM idle).
+    // The compiler waits for a chunk's loads with the smallest vmcnt any path
+    // allows, so the loop is shaped for that: unrolled by two (the record
+    // registers are never copied -- a copy of a load in flight waits for it),
+    // every chunk load covers the whole wave (a fixed number of memory ops
+    // between a load and its use), and the rare paths that issue global
+    // memory ops of their own end with vmcnt(0).
     constexpr uint32_t kStride = kWG / 64;
-    const uint32_t l0 = item.y + (uint32_t)wave, l1 = item.z;
-    auto chunk_load = [&](uint32_t e, uint32_t l, uint4& a, uint64_t& x) {
-      a = make_uint4(0, 0, 0, 0);
-      x = 0;
-      if (l < l1 && (uint32_t)lane < (e >> kChunkIdBits)) {
-        const uint64_t k = uint64_t(e & ((1u << kChunkIdBits) - 1)) * kChunk + lane;
-        a = lp.rec16[k];
-        x = lp.recx[k];
-      }
+    const uint32_t nl = item.z - item.y;
+    const uint32_t nmine = nl > (uint32_t)wave ? (nl - (uint32_t)wave + kStride - 1) / kStride : 0u;
+    auto chunk_load = [&](uint32_t k, uint4& a, uint64_t& x) {  // this wave's k-th chunk (any k: no branch)
+      const uint32_t e = k < nmine ? s_clist[(uint32_t)wave + k * kStride] : 0u;
+      const uint64_t i = uint64_t(e & ((1u << kChunkIdBits) - 1)) * kChunk + lane;
+      a = lp.rec16[i];
+      x = lp.recx[i];
     };
-    uint32_t ce = l0 < l1 ? lp.clist[l0] : 0u;
-    uint32_t ce1 = l0 + kStride < l1 ? lp.clist[l0 + kStride] : 0u;
-    uint4 na16, na16b;
-    uint64_t nx, nxb;
-    chunk_load(ce, l0, na16, nx);
-    chunk_load(ce1, l0 + kStride, na16b, nxb);
-    uint32_t ce2 = l0 + 2 * kStride < l1 ? lp.clist[l0 + 2 * kStride] : 0u;
-    for (uint32_t l = l0; l < l1; l += kStride) {
+    auto process = [&](uint32_t k, const uint4 a16, const uint64_t x) {
+      const uint32_t ce = s_clist[(uint32_t)wave + k * kStride];
       const uint32_t c = ce & ((1u << kChunkIdBits) - 1), fill = ce >> kChunkIdBits;
       const bool valid = (uint32_t)lane < fill;
-      const uint4 a16 = na16;
-      const uint64_t x = nx;
-      ce = ce1;
-      na16 = na16b;
-      nx = nxb;
-      ce1 = ce2;
-      chunk_load(ce1, l + 2 * kStride, na16b, nxb);
-      ce2 = l + 3 * kStride < l1 ? lp.clist[l + 3 * kStride] : 0u;
+      if (TIMING) {  // (timing: this chunk's loads count as wait; a match-bit store and two loads are younger)
+        asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+        nchunks++;
+      }
+      rt_stamp<TIMING>(rt, 0);
       const uint64_t addr = u64of(a16.x, a16.y), ts = u64of(a16.z, a16.w);
       if (p.flags & kDbgLocalNoWork) {  // (ablation) loads only
-        if (lane == 0) lp.cmatch[c] = addr ^ ts ^ x;
-        continue;
+        lp.cmatch[c] = __builtin_amdgcn_readfirstlane((uint32_t)(addr ^ ts ^ x));
+        return;
       }
       // update_counters(global_counters, sample) (mem_sampling.c:882): every
       // routed SAMPLE, matched or not
       const XRec xr = x_decode(lp.xl, x);
-      const uint64_t w = valid ? x_weight(lp.xl, xr, p.data, lp.descs) : 0ull;
+      uint64_t w = valid ? xr.wq : 0ull;
+      if (__ballot(valid && xr.wq == lp.xl.wesc)) {  // (rare) escaped weights: re-read from the record
+        if (valid) w = x_weight(lp.xl, xr, p.data, lp.descs);
+        vm_drain();
+      }
       if (valid && !(p.flags & kDbgLocalNoGlobal)) dual_count(gacc, s_gsums, s_gmins, s_gmaxs, xr.acc, xr.lvl, w);
       if (++acc_chunks == kDrainWindows) {  // keep the per-lane u16 counts / u32 sums bounded
         dual_drain(gacc, s_gsums, lane);
         acc_chunks = 0;
       }
+      rt_stamp<TIMING>(rt, 1);
       // lower bound among the partition's keys (ht_lower_key, tools/hash.c:63-77):
       // the record's address is < the next partition's first key; below the
       // first key (partition 0 only) there is no node.  The directory slot
@@ -971,9 +978,12 @@ __global__ __launch_bounds__(kWG, 1) void local_kernel(LocalParams lp) {
         }
         r = (int32_t)a;
       }
+      if (TIMING) (void)__builtin_amdgcn_readfirstlane(__ballot(r >= 0));  // (the search ends here)
+      rt_stamp<TIMING>(rt, 2);
       int32_t erel = -1;
       uint64_t baddr = 0;
       uint32_t hrel = kEmpty32;
+      bool older = false;
       if (r >= 0 && !(p.flags & kDbgLocalNoSearch)) {
         const uint4 na = s_nodes[2 * r], nb = s_nodes[2 * r + 1];
         const uint2 inf = s_info[r];
@@ -981,7 +991,12 @@ __global__ __launch_bounds__(kWG, 1) void local_kernel(LocalParams lp) {
           erel = (int32_t)(inf.y & 0x7fffffffu);
           baddr = u64of(na.x, na.y);
           hrel = inf.x;
-        } else if (inf.y >> 31) {  // older entries of a reused address (LIFO, tools/hash.c:108-114)
+        } else {
+          older = (inf.y >> 31) != 0;
+        }
+      }
+      if (__ballot(older)) {  // (rare) older entries of a reused address (LIFO, tools/hash.c:108-114)
+        if (older) {
           const uint4 d = reinterpret_cast<const uint4*>(p.nodes + pi.k0 + (uint32_t)r)[3];  // (count, first)
           Match m;
           m.e = -1;
@@ -992,40 +1007,60 @@ __global__ __launch_bounds__(kWG, 1) void local_kernel(LocalParams lp) {
             hrel = m.hist == kHistSparse ? kEmpty32 : (uint32_t)(m.hist - pi.cb);
           }
         }
+        vm_drain();
       }
-      const uint64_t fm = __ballot(erel >= 0);
-      if (lane == 0) lp.cmatch[c] = fm;
-      if (erel < 0) continue;
+      // the chunk's match bits (found_kernel): every lane stores the same word
+      lp.cmatch[c] = __ballot(erel >= 0);
+      rt_stamp<TIMING>(rt, 3);
+      if (erel < 0) return;
       if (p.flags & kDbgLocalNoObj) {
       } else if (w < kLaneMaxWeight) {
         atomicAdd(&s_owt[xr.acc][erel], (1ull << kPackShift) | w);
-      } else {
-        const uint64_t e = pi.e0 + (uint32_t)erel;
-        atomicAdd(reinterpret_cast<unsigned long long*>(p.sum64 + objcw_index(e, xr.acc, 0, p.nb_entries)), 1ull);
-        atomicAdd(reinterpret_cast<unsigned long long*>(p.sum64 + objcw_index(e, xr.acc, 1, p.nb_entries)),
-                  (unsigned long long)w);
+      }
+      if (__ballot(erel >= 0 && w >= kLaneMaxWeight && !(p.flags & kDbgLocalNoObj))) {  // (rare) large weights
+        if (w >= kLaneMaxWeight && !(p.flags & kDbgLocalNoObj)) {
+          const uint64_t e = pi.e0 + (uint32_t)erel;
+          atomicAdd(reinterpret_cast<unsigned long long*>(p.sum64 + objcw_index(e, xr.acc, 0, p.nb_entries)), 1ull);
+          atomicAdd(reinterpret_cast<unsigned long long*>(p.sum64 + objcw_index(e, xr.acc, 1, p.nb_entries)),
+                    (unsigned long long)w);
+        }
+        vm_drain();
       }
       // first match in analysis order (quirk Q7)
       const unsigned long long ord = ((lp.seq0 + xr.g) << 32) | xr.off;
       if (!(p.flags & kDbgLocalNoObj) && ord < s_first[erel]) atomicMin(&s_first[erel], ord);
+      rt_stamp<TIMING>(rt, 4);
       if (pages && !(p.flags & kDbgLocalNoPage)) {
         // ma_get_block: page_no = (int)((addr - buffer_addr) / 4096) (mem_analyzer.c:530-531)
         const uint32_t page = uint32_t(int(uint64_t(addr - baddr) / kPageSize));
-        if (hrel != kEmpty32) {
-          const uint32_t rel = hrel + page;
-          if (ncell) {
-            const uint32_t li = xr.th * pi.span + rel;
-            atomicAdd(&s_pg[li >> 1], 1u << (16 * (li & 1)));
-          } else {
-            atomicAdd(p.hist + uint64_t(xr.th) * p.hist_cells + pi.cb + rel, 1u);
+        if (hrel != kEmpty32 && ncell) {
+          const uint32_t li = xr.th * pi.span + hrel + page;
+          atomicAdd(&s_pg[li >> 1], 1u << (16 * (li & 1)));
+        }
+        if (__ballot(hrel == kEmpty32 || !ncell)) {  // (rare) cells in global memory: dense or sparse
+          if (hrel != kEmpty32 && !ncell) {
+            atomicAdd(p.hist + uint64_t(xr.th) * p.hist_cells + pi.cb + hrel + page, 1u);
+          } else if (hrel == kEmpty32) {
+            const uint32_t sidx = p.entries[pi.e0 + (uint32_t)erel].sidx;
+            if (sidx != ~0u) sparse_add(p, sparse_key(sidx, xr.th, page), lp.seq0 + xr.g, xr.off, 1u);
           }
-        } else {
-          const uint32_t sidx = p.entries[pi.e0 + (uint32_t)erel].sidx;
-          if (sidx != ~0u) sparse_add(p, sparse_key(sidx, xr.th, page), lp.seq0 + xr.g, xr.off, 1u);
+          vm_drain();
         }
       }
+      rt_stamp<TIMING>(rt, 5);
+    };
+    uint4 a0, a1;
+    uint64_t x0, x1;
+    chunk_load(0, a0, x0);
+    chunk_load(1, a1, x1);
+    for (uint32_t k = 0; k < nmine; k += 2) {
+      process(k, a0, x0);
+      chunk_load(k + 2, a0, x0);
+      if (k + 1 < nmine) process(k + 1, a1, x1);
+      chunk_load(k + 3, a1, x1);
     }
     __syncthreads();
+    rt_stamp<TIMING>(rt, 8);  // (waiting for the item's slowest wave counts as flush)
     // the item's counters to global memory: consecutive lanes, consecutive words
     for (uint32_t i = tid; i < pi.ne; i += kWG) {
       const uint64_t e = pi.e0 + i;
@@ -1055,6 +1090,13 @@ __global__ __launch_bounds__(kWG, 1) void local_kernel(LocalParams lp) {
       }
     }
     __syncthreads();
+    rt_stamp<TIMING>(rt, 8);
+  }
+  if (TIMING && lane == 0) {
+    unsigned long long* o = p.dbg + (uint64_t(blockIdx.x) * (kWG / 64) + tid / 64) * kRouteTimingWords;
+    for (int k = 0; k < 9; k++) o[k] = rt.acc[k];
+    o[9] = nchunks;
+    o[10] = nit;
   }
   // global mem_counters of both access types
   dual_drain(gacc, s_gsums, lane);
@@ -1137,7 +1179,8 @@ hipError_t launch_scatter(uint32_t grid, hipStream_t s, const ScatterParams& r) 
 }
 
 hipError_t launch_local(uint32_t grid, hipStream_t s, const LocalParams& r) {
-  hipLaunchKernelGGL(local_kernel, dim3(grid), dim3(kWG), 0, s, r);
+  if (r.p.flags & kDbgLocalTiming) hipLaunchKernelGGL(local_kernel<true>, dim3(grid), dim3(kWG), 0, s, r);
+  else hipLaunchKernelGGL(local_kernel<false>, dim3(grid), dim3(kWG), 0, s, r);
   return hipGetLastError();
 }
 

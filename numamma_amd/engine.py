@@ -38,7 +38,7 @@ class Engine:
         devs = (C.c_int32 * max(1, len(devices or [])))(*(devices or [device]))
         self._devs = devs
         opt = _lib.nmg_options(device, flags, nb_threads, copy_threads, hist_budget_bytes, sparse_capacity,
-                               len(devices) if devices else 0, 0, devs if devices else None)
+                               len(devices) if devices else 0, _lib.NMG_OPTIONS_ABI, devs if devices else None)
         h = _lib.H()
         check(lib.nmg_create(C.byref(h), C.byref(opt)))
         self.h = h

@@ -140,6 +140,13 @@ class ObjectTable:
         end = self.string_pool.index(b"\0", off)
         return self.string_pool[off:end].decode()
 
+    @classmethod
+    def empty(cls) -> "ObjectTable":
+        """No objects (a live host's table before the first allocation)."""
+        return cls(keys=np.zeros(0, dtype=np.uint64), entry_off=np.zeros(1, dtype=np.uint32),
+                   entries=np.zeros(0, dtype=ENTRY_DTYPE), callstack_pool=np.zeros(0, dtype=np.uint64),
+                   string_pool=b"")
+
     def validate(self) -> None:
         k = self.keys
         if k.shape[0] > 1 and not np.all(k[1:] > k[:-1]):

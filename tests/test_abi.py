@@ -54,3 +54,14 @@ def test_header_compiles_as_c99(tmp_path):
                     "-I" + os.path.join(root, "include"), os.path.join(root, "tests", "c", "nmg_c99_host.c"),
                     "-o", exe, "-L" + os.path.join(root, "numamma_amd"), "-lnumamma_gpu"], check=True)
     assert os.path.exists(exe)
+
+
+def test_options_abi_version_matches_header():
+    """nmg_options.abi_version gates nb_gpus / devices (older, shorter structs
+    get a one-GPU engine): the binding's layout and magic follow the header."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    hdr = open(os.path.join(root, "include", "numamma_gpu.h")).read()
+    assert "#define NMG_OPTIONS_ABI 0x4e4d4702u" in hdr
+    assert _lib.NMG_OPTIONS_ABI == 0x4E4D4702
+    assert C.sizeof(_lib.nmg_options) == 48
+    assert _lib.nmg_options.abi_version.offset == 36 and _lib.nmg_options.devices.offset == 40

@@ -50,7 +50,7 @@ def _same_dirs(a, b):
 
 @pytest.mark.parametrize("cfg,nb_alarms,chunk", CASES, ids=["k400", "k30k", "one_alarm", "m1_48_alarms"])
 def test_online_analysis_bit_exact(tmp_path, cfg, nb_alarms, chunk):
-    from numamma_amd.engine import Engine
+    from numamma_amd.engine import Engine, table_objects
 
     d = str(tmp_path)
     rp = generate(cfg)
@@ -76,6 +76,9 @@ def test_online_analysis_bit_exact(tmp_path, cfg, nb_alarms, chunk):
     eng.analyze()
     eng.stream_end()
     eng.synchronize()
+    # at exit: the table ma_finalize walks (the report's objects and order)
+    t = rp.table
+    eng.update_objects(t.keys, t.entry_off, np.arange(t.nb_entries, dtype=np.uint32), table_objects(t))
     g, ns, nf = eng.global_counters()
     assert np.array_equal(g, raw.global_counters) and (ns, nf) == (raw.nb_samples, raw.nb_found)
     s, f = eng.buffer_counts()
@@ -127,14 +130,106 @@ def test_update_objects_rejects_bad_tables(tmp_path):
     ids = np.arange(t.nb_entries, dtype=np.uint32)
     objs = table_objects(t)
     bad = ids.copy()
-    bad[3] = t.nb_entries  # past the set_objects table
+    bad[3] = t.nb_entries + 1  # a new id, but not the next one (t.nb_entries is missing)
+    with pytest.raises(RuntimeError):
+        eng.update_objects(t.keys, t.entry_off, bad, objs)
+    bad = ids.copy()
+    bad[3] = bad[4]  # one id twice
     with pytest.raises(RuntimeError):
         eng.update_objects(t.keys, t.entry_off, bad, objs)
     big = objs.copy()
-    big["s"][5] += 1 << 20  # larger than its page cells
-    with pytest.raises(RuntimeError):
-        eng.update_objects(t.keys, t.entry_off, ids, big)
+    big["s"][5] += 1 << 20  # larger than its page cells: they move to a larger range
+    eng.update_objects(t.keys, t.entry_off, ids, big)
     eng.update_objects(t.keys[:0], np.zeros(1, dtype=np.uint32), ids[:0], objs[:0])  # empty table at an alarm
     with pytest.raises(RuntimeError):  # dump modes read the NULL `samples` list online in the reference
         eng.report(str(tmp_path), os.path.join(str(tmp_path), "x.txt"), dump_flags=_lib.NMG_DUMP_ALL, online=True)
     eng.close()
+
+
+def _creation_ids(table):
+    """Live ids: objects numbered in creation order (alloc date, then table
+    position), as _init_mem_info's next_mem_info_id hands them out
+    (mem_analyzer.c:567-568); cid[table position] = id."""
+    ent = table.entries
+    order = np.lexsort((np.arange(table.nb_entries), ent["alloc_date"]))
+    cid = np.empty(table.nb_entries, dtype=np.uint32)
+    cid[order] = np.arange(table.nb_entries, dtype=np.uint32)
+    return cid
+
+
+LIVE_CASES = [
+    (SynthConfig(nb_samples=150_000, nb_intervals=600, nb_threads=4, with_stack=False, reuse_frac=0.3,
+                 buffer_records=300, seed=81), 7, 1 << 20),
+    # hashed object counters (> 2048 entries by the end) and the large-table lookup
+    (SynthConfig(nb_samples=400_000, nb_intervals=20_000, nb_threads=8, with_stack=False, reuse_frac=0.2,
+                 realloc_frac=0.05, buffer_records=800, seed=82), 12, 512 << 10),
+]
+
+
+@pytest.mark.parametrize("cfg,nb_alarms,chunk", LIVE_CASES, ids=["k600", "k20k"])
+def test_online_live_tables_bit_exact(tmp_path, cfg, nb_alarms, chunk):
+    """A live host: the engine never sees the final
+    table before the last alarm.  It starts from an empty table; each alarm's
+    table brings the objects created since (ids in creation order, counters
+    from creation) and objects that grew (every third object is half its
+    final size until it is freed: ma_record_free stamps the final size,
+    mem_analyzer.c:1287); at exit the finalize table gives the report its
+    objects and order.  The oracle replays the same alarm tables with
+    final-table ids: reports byte-identical, raw counters equal through the
+    id map."""
+    from numamma_amd.engine import Engine, table_objects
+    from numamma_amd.replay import ObjectTable
+
+    d = str(tmp_path)
+    rp = generate(cfg)
+    rp.buffers.reverse()
+    alarms = online_alarms(rp, nb_alarms)
+    final = rp.table
+    grows = (np.arange(final.nb_entries) % 3) == 0
+    snaps = []
+    for be, t in alarms:
+        keys, off, ids, ent4 = table_at(final, t)
+        ent4 = ent4.copy()
+        live = (ent4[:, 3] == 0) & grows[ids]
+        ent4[live, 1] = ent4[live, 1] // 2  # size before ma_record_free
+        snaps.append((be, keys, off, ids, ent4))
+    path = os.path.join(d, "replay.bin")
+    rp.write(path)
+    odir = os.path.join(d, "oracle")
+    pyoracle.run(path, odir, os.path.join(d, "o.txt"), os.path.join(d, "o_raw.bin"), alarms=snaps)
+    raw = RawResults.read(os.path.join(d, "o_raw.bin"))
+    assert raw.nb_found > 0
+
+    cid = _creation_ids(final)
+    eng = Engine(flags=_lib.NMG_F_DEFAULT, nb_threads=rp.nb_threads)
+    eng.set_objects(ObjectTable.empty())  # no objects yet
+    eng.stream_begin(chunk_bytes=chunk, copy_threads=2)
+    b0 = 0
+    for be, keys, off, ids, ent4 in snaps:
+        eng.update_objects(keys, off, cid[ids], _ent_objs(ent4))
+        for b in rp.buffers[b0:be]:
+            eng.submit_ring(b.ring, b.data_tail, b.data_head, b.thread_rank, b.access_type)
+        b0 = be
+    eng.analyze()
+    eng.stream_end()
+    eng.synchronize()
+    eng.update_objects(final.keys, final.entry_off, cid, table_objects(final))  # ma_finalize's table
+    eng.table = final  # the report's metadata, in the finalize table's order
+    g, ns, nf = eng.global_counters()
+    assert np.array_equal(g, raw.global_counters) and (ns, nf) == (raw.nb_samples, raw.nb_found)
+    s, f = eng.buffer_counts()
+    assert np.array_equal(s, raw.buf_samples) and np.array_equal(f, raw.buf_found)
+    first, cw = eng.object_counters()
+    assert np.array_equal(first[cid], raw.first_ordinal)
+    assert np.array_equal(cw[cid], raw.count_weight)
+    cells = eng.page_cells().copy()
+    pos = np.empty_like(cid)
+    pos[cid] = np.arange(cid.shape[0], dtype=np.uint32)
+    cells[:, 0] = pos[cells[:, 0]]
+    cells = cells[np.lexsort((cells[:, 2], cells[:, 1], cells[:, 0]))]
+    assert np.array_equal(cells, raw.cells)
+    edir = os.path.join(d, "engine")
+    eng.report(edir, os.path.join(d, "e.txt"), online=True)
+    eng.close()
+    assert open(os.path.join(d, "o.txt"), "rb").read() == open(os.path.join(d, "e.txt"), "rb").read()
+    _same_dirs(odir, edir)
