@@ -331,6 +331,18 @@ __device__ __forceinline__ Rec decode_rec(const RawRec& r, uint64_t pos) {
 }
 
 
+// Workgroup barrier for LDS traffic only: the wave's LDS ops complete before
+// it and the other waves' LDS writes are visible after it, while its global
+// loads and stores stay in flight across it.  (__syncthreads()'s workgroup
+// fence also covers global memory: s_waitcnt vmcnt(0) before every barrier,
+// which drains a window's prefetched loads.)  For the kernels whose waves
+// exchange data through LDS only.
+__device__ __forceinline__ void lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 // s_waitcnt vmcnt(0) (expcnt / lgkmcnt left alone) as a real waitcnt
 // instruction, which the compiler's own waitcnt pass accounts for: a rare
 // path that issued global memory ops ends with it, so that the waits on the

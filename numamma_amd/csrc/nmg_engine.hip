@@ -2018,7 +2018,14 @@ static int route_analyze(nmg_engine* h, uint32_t nb, uint32_t grid) {
   sc.pbase = h->d_pbase;
   sc.clist = h->d_clist;
   sc.nparts = h->nparts;
-  HIP_TRY(h, launch_count(grid, h->stream, sc));
+  CountParams cp;
+  memset(&cp, 0, sizeof(cp));
+  cp.sc = sc;
+  cp.p = base;
+  cp.recx = h->d_recx;
+  cp.descs = h->d_sdescs;
+  cp.xl = xl;
+  HIP_TRY(h, launch_count(grid, h->stream, cp));
   PlanParams pl;
   pl.pcnt = h->d_pcnt;
   pl.pbase = h->d_pbase;
@@ -2337,10 +2344,15 @@ extern "C" int nmg_get_object_levels(nmg_engine* h, uint64_t* levels) {
 
 static int sparse_nonempty(nmg_engine* h, bool* out);
 
+// Every non-zero (entry, thread, page) cell, entries in id order, each
+// entry's cells in (thread, page) order.  Dense cells are counted and
+// compacted into rows on the device (cells_count / cells_emit), so only the
+// rows cross PCIe; the sparse table's cells (entries past the dense budget,
+// e.g. [stack]) are grouped on the host and placed at their entries' offsets.
 static int collect_page_cells(nmg_engine* h, std::vector<uint32_t>* rows, int64_t* count) {
-  std::vector<uint32_t> cells;
-  int rc = engine_download_hist(h, cells);
+  int rc = nmg_synchronize(h);
   if (rc) return rc;
+  const uint32_t E = h->E;
   // sparse cells grouped per entry
   std::vector<std::vector<std::pair<uint64_t, uint32_t>>> sparse(h->sparse_entries.size());
   bool any_sparse = false;
@@ -2359,37 +2371,69 @@ static int collect_page_cells(nmg_engine* h, std::vector<uint32_t>* rows, int64_
       }
     for (auto& l : sparse) std::sort(l.begin(), l.end());
   }
-  std::vector<int64_t> sidx_of(h->E, -1);
+  std::vector<int64_t> sidx_of(E, -1);
   for (size_t s = 0; s < h->sparse_entries.size(); s++) sidx_of[h->sparse_entries[s]] = (int64_t)s;
-  int64_t n = 0;
-  const uint64_t T = h->T;
-  for (uint32_t e = 0; e < h->E; e++) {
-    if (h->hist_base[e] != kHistSparse) {
-      for (uint32_t th = 0; th < T; th++)
-        for (uint64_t pg = 0; pg < h->npages[e]; pg++) {
-          uint32_t v = cells[th * h->hist_cells + h->hist_base[e] + pg];
-          if (!v) continue;
-          if (rows) {
-            rows->push_back(e);
-            rows->push_back(th);
-            rows->push_back((uint32_t)pg);
-            rows->push_back(v);
-          }
-          n++;
-        }
-    } else if (sidx_of[e] >= 0) {
-      for (auto& kv : sparse[sidx_of[e]]) {
-        if (rows) {
-          rows->push_back(e);
-          rows->push_back((uint32_t)(kv.first >> 32));
-          rows->push_back((uint32_t)kv.first);
-          rows->push_back(kv.second);
-        }
-        n++;
-      }
+  std::vector<uint32_t> cnt(E, 0);
+  uint64_t *d_base = nullptr, *d_off = nullptr;
+  uint32_t *d_np = nullptr, *d_cnt = nullptr;
+  uint4* d_rows = nullptr;
+  auto cleanup = [&]() {
+    (void)hipFree(d_base);
+    (void)hipFree(d_off);
+    (void)hipFree(d_np);
+    (void)hipFree(d_cnt);
+    (void)hipFree(d_rows);
+  };
+  auto hip = [&](hipError_t e, const char* what) {
+    if (e == hipSuccess) return NMG_OK;
+    cleanup();
+    return fail(h, NMG_ERR_HIP, std::string("page cells: ") + what + ": " + hipGetErrorString(e));
+  };
+  const bool dense = h->hist_cells && E;
+  if (dense) {
+    std::vector<uint32_t> np(E);
+    for (uint32_t e = 0; e < E; e++) np[e] = h->hist_base[e] == kHistSparse ? 0u : (uint32_t)h->npages[e];
+    if ((rc = hip(hipMalloc(&d_base, (size_t)E * 8), "alloc")) || (rc = hip(hipMalloc(&d_np, (size_t)E * 4), "alloc")) ||
+        (rc = hip(hipMalloc(&d_cnt, (size_t)E * 4), "alloc")) ||
+        (rc = hip(hipMemcpyAsync(d_base, h->hist_base.data(), (size_t)E * 8, hipMemcpyHostToDevice, h->stream), "upload")) ||
+        (rc = hip(hipMemcpyAsync(d_np, np.data(), (size_t)E * 4, hipMemcpyHostToDevice, h->stream), "upload")) ||
+        (rc = hip(launch_cells_count(h->stream, h->d_hist, h->hist_cells, h->T, d_base, d_np, E, d_cnt), "count")) ||
+        (rc = hip(hipMemcpyAsync(cnt.data(), d_cnt, (size_t)E * 4, hipMemcpyDeviceToHost, h->stream), "counts")) ||
+        (rc = hip(hipStreamSynchronize(h->stream), "count")))
+      return rc;
+  }
+  std::vector<uint64_t> off(E);
+  uint64_t n = 0;
+  for (uint32_t e = 0; e < E; e++) {
+    off[e] = n;
+    n += sidx_of[e] >= 0 && h->hist_base[e] == kHistSparse ? sparse[sidx_of[e]].size() : cnt[e];
+  }
+  *count = (int64_t)n;
+  if (!rows) {
+    cleanup();
+    return NMG_OK;
+  }
+  rows->resize(n * 4);
+  if (dense && n) {
+    if ((rc = hip(hipMalloc(&d_off, (size_t)E * 8), "alloc")) || (rc = hip(hipMalloc(&d_rows, n * 16), "alloc")) ||
+        (rc = hip(hipMemcpyAsync(d_off, off.data(), (size_t)E * 8, hipMemcpyHostToDevice, h->stream), "upload")) ||
+        (rc = hip(launch_cells_emit(h->stream, h->d_hist, h->hist_cells, h->T, d_base, d_np, E, d_off, d_rows), "emit")) ||
+        (rc = hip(hipMemcpyAsync(rows->data(), d_rows, n * 16, hipMemcpyDeviceToHost, h->stream), "rows")) ||
+        (rc = hip(hipStreamSynchronize(h->stream), "rows")))
+      return rc;
+  }
+  cleanup();
+  for (uint32_t e = 0; e < E; e++) {
+    if (sidx_of[e] < 0 || h->hist_base[e] != kHistSparse) continue;
+    uint32_t* r = rows->data() + off[e] * 4;
+    for (auto& kv : sparse[sidx_of[e]]) {
+      r[0] = e;
+      r[1] = (uint32_t)(kv.first >> 32);
+      r[2] = (uint32_t)kv.first;
+      r[3] = kv.second;
+      r += 4;
     }
   }
-  *count = n;
   return NMG_OK;
 }
 

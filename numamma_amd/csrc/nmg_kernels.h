@@ -200,5 +200,12 @@ hipError_t launch_unpack(uint32_t grid, hipStream_t s, uint64_t* sum64, unsigned
                          uint32_t nb_entries, uint32_t shift);
 hipError_t launch_reset(uint32_t grid, hipStream_t s, const ResetParams& r);
 hipError_t launch_merge(hipStream_t s, void* dst, const void* src, uint64_t n, int op);
+// page-cell rows on the device (nmg_get_page_cells / nmg_report): per dense
+// entry the number of non-zero cells, then the (entry, thread, page, count)
+// rows at each entry's offset, in (thread, page) order
+hipError_t launch_cells_count(hipStream_t s, const uint32_t* hist, uint64_t hist_cells, uint32_t T,
+                              const uint64_t* base, const uint32_t* np, uint32_t E, uint32_t* cnt);
+hipError_t launch_cells_emit(hipStream_t s, const uint32_t* hist, uint64_t hist_cells, uint32_t T,
+                             const uint64_t* base, const uint32_t* np, uint32_t E, const uint64_t* off, uint4* rows);
 
 }  // namespace nmg

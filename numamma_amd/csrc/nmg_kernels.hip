@@ -547,7 +547,7 @@ __global__ __launch_bounds__(kWG, 1) void attribute_kernel(Params p) {
   if (kLog && p.tlog)
     for (uint32_t i = tid; i < kLogParts; i += kWG) wc.tcur[i] = 0;
   if (tid < 3) s_flags[tid] = 0;
-  __syncthreads();
+  lds_sync();
   const Lookup L{s_fences, s_nodes, s_ninfo, s_shift};
 
   // A window is (idx, cur): up to kWG stride slots from byte `cur` of buffer
@@ -602,7 +602,7 @@ __global__ __launch_bounds__(kWG, 1) void attribute_kernel(Params p) {
     // only on pure 40 B SAMPLE streams -- was timed as an upper bound for a
     // barrier-free protocol: c2 -7.6 %, 1M intervals +6 %: not worth one.)
     if (badm && lane == 0) atomicOr(&s_flags[win % 3], 1u);
-    __syncthreads();
+    lds_sync();
     // (LDS broadcasts are made wave-uniform explicitly: the branches below
     // hold barriers and steer the scalar loop state)
     const uint32_t f = __builtin_amdgcn_readfirstlane(s_flags[win % 3]);
@@ -687,7 +687,7 @@ __global__ __launch_bounds__(kWG, 1) void attribute_kernel(Params p) {
           s_next = (uint32_t)min(q0, len);
         }
       }
-      __syncthreads();
+      lds_sync();
       const uint32_t n = __builtin_amdgcn_readfirstlane(s_nlist);
       const uint32_t serr = __builtin_amdgcn_readfirstlane(s_err);
       ncur = serr ? len : __builtin_amdgcn_readfirstlane(s_next);  // the reference aborts on an error: stop this buffer
@@ -795,12 +795,12 @@ __global__ __launch_bounds__(kWG, 1) void attribute_kernel(Params p) {
     }
     const uint32_t cadence = (MODE & (kModeDensePage | kModeDenseObj)) ? kDensePageWindows : kTableWindows;
     if (stream_end || win - last_flush >= cadence) {
-      __syncthreads();  // every insert and drain of this window is done
+      lds_sync();  // every insert and drain of this window is done
       if (stream_end) flush_sums(p, wc, tid, cur_access);
       flush_objects<MODE>(p, wc, tid, cur_access);
       flush_pages<MODE>(p, wc, tid, cur_thread);
       last_flush = win;
-      __syncthreads();
+      lds_sync();
       if (stream_end) {
         clear_sums(wc, tid);  // (sums are next written after the next window's barrier)
         cur_access = nd0.access;
@@ -820,7 +820,7 @@ __global__ __launch_bounds__(kWG, 1) void attribute_kernel(Params p) {
     if (idx >= r1) break;  // the loop's only exit, after the state update
   }
   if (kLog && p.tlog) {  // the sub-logs' fill (every append of this workgroup is done)
-    __syncthreads();
+    lds_sync();
     if (kLog && p.tlog)
       for (uint32_t i = tid; i < p.tlog_parts; i += kWG)
         p.tlog_cnt[uint64_t(blockIdx.x) * p.tlog_parts + i] = min(wc.tcur[i], p.tlog_cap);
@@ -1010,6 +1010,70 @@ int attribute_blocks_per_cu() {
 
 hipError_t launch_tlog_reduce(uint32_t grid, hipStream_t s, const TlogParams& r) {
   hipLaunchKernelGGL(tlog_reduce_kernel, dim3(grid), dim3(1024), 0, s, r);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Page-cell rows (the report's per-(entry, thread, page) counts): one wave per
+// entry, its T x np cells walked thread-major in 64-cell steps; a ballot
+// gives each non-zero cell its row.  Sparse entries (base == kHistSparse)
+// count 0 here: the host adds their rows from the sparse table.
+
+__global__ __launch_bounds__(256) void cells_count_kernel(const uint32_t* hist, uint64_t hist_cells, uint32_t T,
+                                                          const uint64_t* base, const uint32_t* np, uint32_t E,
+                                                          uint32_t* cnt) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t nw = gridDim.x * (blockDim.x / 64);
+  for (uint32_t e = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64; e < E; e += nw) {
+    const uint64_t b = base[e];
+    uint32_t n = 0;
+    if (b != ~0ull) {
+      const uint32_t pg = np[e], tot = pg * T;
+      for (uint32_t i0 = 0; i0 < tot; i0 += 64) {
+        const uint32_t i = i0 + lane;
+        const uint32_t th = i / pg, p = i - th * pg;
+        const bool nz = i < tot && hist[uint64_t(th) * hist_cells + b + p] != 0;
+        n += (uint32_t)__popcll(__ballot(nz));
+      }
+    }
+    if (lane == 0) cnt[e] = n;
+  }
+}
+
+__global__ __launch_bounds__(256) void cells_emit_kernel(const uint32_t* hist, uint64_t hist_cells, uint32_t T,
+                                                         const uint64_t* base, const uint32_t* np, uint32_t E,
+                                                         const uint64_t* off, uint4* rows) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t nw = gridDim.x * (blockDim.x / 64);
+  for (uint32_t e = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64; e < E; e += nw) {
+    const uint64_t b = base[e];
+    if (b == ~0ull) continue;
+    const uint32_t pg = np[e], tot = pg * T;
+    uint64_t o = off[e];
+    for (uint32_t i0 = 0; i0 < tot; i0 += 64) {
+      const uint32_t i = i0 + lane;
+      const uint32_t th = i / pg, p = i - th * pg;
+      const uint32_t v = i < tot ? hist[uint64_t(th) * hist_cells + b + p] : 0u;
+      const uint64_t m = __ballot(v != 0);
+      if (v) rows[o + __popcll(m & ((1ull << lane) - 1))] = make_uint4(e, th, p, v);
+      o += (uint64_t)__popcll(m);
+    }
+  }
+}
+
+hipError_t launch_cells_count(hipStream_t s, const uint32_t* hist, uint64_t hist_cells, uint32_t T,
+                              const uint64_t* base, const uint32_t* np, uint32_t E, uint32_t* cnt) {
+  const uint32_t grid = (uint32_t)std::min<uint64_t>((E + 3) / 4, 8192);
+  hipLaunchKernelGGL(cells_count_kernel, dim3(std::max<uint32_t>(grid, 1)), dim3(256), 0, s, hist, hist_cells, T,
+                     base, np, E, cnt);
+  return hipGetLastError();
+}
+
+hipError_t launch_cells_emit(hipStream_t s, const uint32_t* hist, uint64_t hist_cells, uint32_t T,
+                             const uint64_t* base, const uint32_t* np, uint32_t E, const uint64_t* off, uint4* rows) {
+  const uint32_t grid = (uint32_t)std::min<uint64_t>((E + 3) / 4, 8192);
+  hipLaunchKernelGGL(cells_emit_kernel, dim3(std::max<uint32_t>(grid, 1)), dim3(256), 0, s, hist, hist_cells, T,
+                     base, np, E, off, rows);
   return hipGetLastError();
 }
 

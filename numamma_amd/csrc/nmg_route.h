@@ -14,15 +14,16 @@
 //                     <= kPartKeys consecutive keys; chunks of kChunk records
 //                     from the workgroup's private pool);
 //      overflow_kernel  the records a full pool turned away, with global lookups;
-//   2. count_kernel   chunks per (workgroup, partition), from the chunks' tags;
+//   2. count_kernel   chunks per (workgroup, partition), from the chunks' tags,
+//                     and the global counters of every routed record from its X
+//                     word (update_counters, mem_sampling.c:508-592);
 //      plan_kernel    per-partition chunk counts -> list offsets and work items;
 //   3. scatter_kernel chunk ids into per-partition lists;
 //   4. local_kernel   one work item (<= kItemChunks chunks of one partition) per
 //                     workgroup at a time: the partition's keys and node records
-//                     in an LDS Eytzinger tree, its object and page counters in
-//                     LDS, flushed once per item (__match_sample, :594-673;
-//                     ma_get_block, mem_analyzer.c:494-534), and the global
-//                     counters of every record (update_counters, :508-592);
+//                     in LDS, its object and page counters in LDS, flushed once
+//                     per item (__match_sample, :594-673; ma_get_block,
+//                     mem_analyzer.c:494-534);
 //   5. found_kernel   per-buffer matched-sample counts from the match bits
 //                     local_kernel leaves per chunk (on demand: the reference
 //                     only sums them, mem_sampling.c:334-335, 357-361).
@@ -157,7 +158,16 @@ struct FoundParams {
 
 hipError_t launch_route(uint32_t grid, hipStream_t s, const RouteParams& r);
 hipError_t launch_overflow(hipStream_t s, const RouteParams& r);
-hipError_t launch_count(uint32_t grid, hipStream_t s, const ScatterParams& r);  // pcnt from cmeta
+// count_kernel: per route workgroup, chunks per partition (pcnt, from the
+// chunks' tags) and update_counters of every routed SAMPLE from its X word
+struct CountParams {
+  ScatterParams sc;
+  Params p;                  // global counters, data (escaped weights), flags
+  const unsigned long long* recx;
+  const BufDesc* descs;      // analysis order (escaped weights are re-read from the record)
+  XLayout xl;
+};
+hipError_t launch_count(uint32_t grid, hipStream_t s, const CountParams& r);
 hipError_t launch_plan(hipStream_t s, const PlanParams& r);
 hipError_t launch_scatter(uint32_t grid, hipStream_t s, const ScatterParams& r);
 hipError_t launch_local(uint32_t grid, hipStream_t s, const LocalParams& r);

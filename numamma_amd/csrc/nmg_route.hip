@@ -68,20 +68,7 @@ __device__ __forceinline__ uint64_t x_weight(const XLayout& xl, const XRec& r, c
 __device__ __forceinline__ void direct_attribute(const Params& p, uint64_t addr, uint64_t ts, uint64_t w, uint32_t th,
                                                  uint32_t acc, uint32_t lvl, uint64_t seq, uint32_t off,
                                                  uint32_t slot) {
-  // update_counters(global_counters, ...) (mem_sampling.c:517-592), global atomics
-  {
-    unsigned long long* S = reinterpret_cast<unsigned long long*>(p.sum64 + gsum_index(acc, 0));
-    atomicAdd(&S[0], 1ull);
-    if (w) atomicAdd(&S[1], (unsigned long long)w);
-    if (lvl & LVL_NA) atomicAdd(&S[2], 1ull);
-    for (uint32_t m = bucket_mask(lvl); m; m &= m - 1) {
-      const uint32_t b = (uint32_t)__builtin_ctz(m);
-      atomicAdd(&S[3 + 2 * b], 1ull);
-      if (w) atomicAdd(&S[4 + 2 * b], (unsigned long long)w);
-      atomicMin(reinterpret_cast<unsigned long long*>(p.min64 + acc * 18 + b), (unsigned long long)w);
-      atomicMax(reinterpret_cast<unsigned long long*>(p.max64 + acc * 18 + b), (unsigned long long)w);
-    }
-  }
+  // (update_counters of this record: the route pass counted it)
   if (p.nb_keys == 0 || p.keys[0] > addr) return;
   uint32_t lo = 0, n = p.nb_keys;
   while (n > 1) {
@@ -127,6 +114,15 @@ __device__ __forceinline__ void direct_attribute(const Params& p, uint64_t addr,
 // ---------------------------------------------------------------------------
 // pass 1: route
 
+// A buffer descriptor of the route pass, in scalar registers (5 dwords):
+// offset in the arena, length, thread rank | access type << 16, analysis index
+struct RDesc {
+  uint64_t offset;
+  uint32_t len, ta, pad;
+  __device__ __forceinline__ uint32_t thread_rank() const { return ta & 0xffffu; }
+  __device__ __forceinline__ uint32_t access() const { return ta >> 16; }
+};
+
 // A lane's stride slot in window (cur of d0) [+ head of d1]: unlike
 // attribute_kernel's windows, d1 may belong to another stream (the route
 // pass keeps per-lane stream state), so windows stay full across buffer ends.
@@ -137,7 +133,7 @@ struct RWin {
   bool cand;
 };
 
-__device__ __forceinline__ RWin rwin_lane(int tid, uint32_t cur, const BufDesc& d0, const BufDesc& d1, bool has1) {
+__device__ __forceinline__ RWin rwin_lane(int tid, uint32_t cur, const RDesc& d0, const RDesc& d1, bool has1) {
   RWin w;
   const uint32_t left = d0.len - cur;
   w.n0 = min(left / kRecBytes + (left % kRecBytes != 0), (uint32_t)kWG);
@@ -149,11 +145,32 @@ __device__ __forceinline__ RWin rwin_lane(int tid, uint32_t cur, const BufDesc& 
   return w;
 }
 
-__device__ __forceinline__ void rload_slot(const uint8_t* data, const RWin& w, const BufDesc& d0, const BufDesc& d1,
+__device__ __forceinline__ void rload_slot(const uint8_t* data, const RWin& w, const RDesc& d0, const RDesc& d1,
                                            RawRec& r) {
   const uint64_t off = w.in1 ? d1.offset : d0.offset;
   const uint32_t len = w.cand ? (w.in1 ? d1.len : d0.len) : 0;
   load_rec(data + off, w.pos, len, r);
+}
+
+// The same loads without a branch: every lane issues its three loads (a lane
+// past its buffer reads the window's first record slot instead and gets
+// zeros), so that the number of memory ops per window is fixed and the
+// compiler's wait for a window's records can leave the next window's loads in
+// flight (route_kernel).
+__device__ __forceinline__ void rload_slot_nb(const uint8_t* data, const RWin& w, const RDesc& d0,
+                                              const RDesc& d1, RawRec& r) {
+  const uint64_t off = w.in1 ? d1.offset : d0.offset;
+  const uint32_t len = w.cand ? (w.in1 ? d1.len : d0.len) : 0;
+  const bool ok = uint64_t(w.pos) + kRecBytes <= len;
+  const uint64_t pos = ok ? w.pos : 0u;
+  const uint8_t* q = data + (ok ? off : d0.offset) + pos;
+  const uint32_t odd = uint32_t(pos >> 3) & 1;
+  const uint4 x = *reinterpret_cast<const uint4*>(q + (odd ? 8 : 0));
+  const uint4 y = *reinterpret_cast<const uint4*>(q + (odd ? 24 : 16));
+  const uint2 z = *reinterpret_cast<const uint2*>(q + (odd ? 0 : 32));
+  r.x = ok ? x : make_uint4(0, 0, 0, 0);
+  r.y = ok ? y : make_uint4(0, 0, 0, 0);
+  r.z = ok ? z : make_uint2(0, 0);
 }
 
 // update_counters(global_counters, ...) (mem_sampling.c:517-592) of both
@@ -217,10 +234,60 @@ __device__ __forceinline__ void dual_count(DualAcc& a, unsigned long long (*sums
     }
   }
   // min / max only move monotonically: read first, atomic only on improvement
+  // (the first bucket's two reads issued together: one LDS round trip)
+  if (bm) {
+    const uint32_t b = (uint32_t)__builtin_ctz(bm);
+    const unsigned long long mn = mins[acc][b], mx = maxs[acc][b];
+    if (w < mn) atomicMin(&mins[acc][b], (unsigned long long)w);
+    if (w > mx) atomicMax(&maxs[acc][b], (unsigned long long)w);
+    for (uint32_t m = bm & (bm - 1); m; m &= m - 1) {  // (several level groups: rare)
+      const uint32_t b2 = (uint32_t)__builtin_ctz(m);
+      if (w < mins[acc][b2]) atomicMin(&mins[acc][b2], (unsigned long long)w);
+      if (w > maxs[acc][b2]) atomicMax(&maxs[acc][b2], (unsigned long long)w);
+    }
+  }
+}
+
+// dual_count for the route pass: the same register buckets, and every
+// minimum / maximum an LDS atomic that returns nothing (no round trip per
+// record; the route pass hides their LDS time behind its memory waits)
+__device__ __forceinline__ void route_count(DualAcc& a, unsigned long long (*sums)[kGlobalSums],
+                                            unsigned long long (*mins)[18], unsigned long long (*maxs)[18],
+                                            uint32_t acc, uint32_t lvl, uint64_t w) {
+  const uint32_t bm = bucket_mask(lvl);
+  if (w < kLaneMaxWeight) {
+    const uint32_t w32 = (uint32_t)w, one = 1u << (16 * acc);
+    const uint32_t wr = acc ? 0u : w32, ww = acc ? w32 : 0u;
+    a.tc += one;
+    a.na += (lvl & LVL_NA) ? one : 0u;
+    a.tw[0] += wr;
+    a.tw[1] += ww;
+#pragma unroll
+    for (int g = 0; g < kDualGroups; g++) {
+      const bool in = (bm >> g) & 1;
+      a.cnt[g] += in ? one : 0u;
+      a.sum[0][g] += in ? wr : 0u;
+      a.sum[1][g] += in ? ww : 0u;
+    }
+    for (uint32_t m = bm >> kDualGroups; m; m &= m - 1) {  // rarer hit buckets, miss buckets
+      const uint32_t b = kDualGroups + (uint32_t)__builtin_ctz(m);
+      atomicAdd(&sums[acc][3 + 2 * b], 1ull);
+      if (w) atomicAdd(&sums[acc][4 + 2 * b], (unsigned long long)w);
+    }
+  } else {  // weights >= 2^23 cycles: straight to the LDS counters
+    atomicAdd(&sums[acc][0], 1ull);
+    atomicAdd(&sums[acc][1], (unsigned long long)w);
+    if (lvl & LVL_NA) atomicAdd(&sums[acc][2], 1ull);
+    for (uint32_t m = bm; m; m &= m - 1) {
+      const uint32_t b = (uint32_t)__builtin_ctz(m);
+      atomicAdd(&sums[acc][3 + 2 * b], 1ull);
+      atomicAdd(&sums[acc][4 + 2 * b], (unsigned long long)w);
+    }
+  }
   for (uint32_t m = bm; m; m &= m - 1) {
     const uint32_t b = (uint32_t)__builtin_ctz(m);
-    if (w < mins[acc][b]) atomicMin(&mins[acc][b], (unsigned long long)w);
-    if (w > maxs[acc][b]) atomicMax(&maxs[acc][b], (unsigned long long)w);
+    atomicMin(&mins[acc][b], (unsigned long long)w);
+    atomicMax(&maxs[acc][b], (unsigned long long)w);
   }
 }
 
@@ -315,14 +382,14 @@ __device__ __forceinline__ void route_sort_batch(RTimer& rt, const RouteParams& 
   const int lane = tid & 63, wave = tid >> 6;
   const uint32_t* cur_in = L.cur + (batch & 1) * (kMaxParts + 1);
   uint32_t* cur_out = L.cur + ((batch + 1) & 1) * (kMaxParts + 1);
-  __syncthreads();  // every rank and staging store of the batch done
+  lds_sync();  // every rank and staging store of the batch done
   // exclusive scan of the per-partition counts (two per thread, DPP within a wave)
   const uint32_t i0 = 2 * (uint32_t)tid;
   const uint32_t v0 = i0 < P ? L.hist[i0] : 0u, v1 = i0 + 1 < P ? L.hist[i0 + 1] : 0u;
   const uint32_t s = v0 + v1;
   const uint32_t inc = wave_incl_scan_u32(s);
   if (lane == 63) L.wsum[wave] = inc;
-  __syncthreads();
+  lds_sync();
   uint32_t wb = 0;
   {
     const uint4* ws = reinterpret_cast<const uint4*>(L.wsum);
@@ -366,13 +433,18 @@ __device__ __forceinline__ void route_sort_batch(RTimer& rt, const RouteParams& 
     cur_out[q] = ((c0 + base + nn - 1) << 7) | (tot - kChunk - kChunk * (nn - 1));
   }
   if (tid == kWG - 1) L.misc[0] = wb + inc;  // records in the batch
-  __syncthreads();
-  // the permutation: sorted position of every staged record
-  for (uint32_t b = 0; b < nwin; b++) {
-    const uint32_t slot = b * kWG + (uint32_t)tid, e = L.uq[slot];
-    if (e != kNoChunk) L.perm[L.start[e & 2047u] + (e >> 11)] = (uint16_t)slot;
-  }
-  __syncthreads();
+  lds_sync();
+  // the permutation: sorted position of every staged record (the reads of
+  // the batch's windows issued together)
+  uint32_t e[kRouteWindows], sp[kRouteWindows];
+#pragma unroll
+  for (uint32_t b = 0; b < kRouteWindows; b++) e[b] = b < nwin ? L.uq[b * kWG + (uint32_t)tid] : kNoChunk;
+#pragma unroll
+  for (uint32_t b = 0; b < kRouteWindows; b++) sp[b] = e[b] != kNoChunk ? L.start[e[b] & 2047u] : 0u;
+#pragma unroll
+  for (uint32_t b = 0; b < kRouteWindows; b++)
+    if (e[b] != kNoChunk) L.perm[sp[b] + (e[b] >> 11)] = (uint16_t)(b * kWG + (uint32_t)tid);
+  lds_sync();
   rt_stamp<TIMING>(rt, 6);
 }
 
@@ -430,22 +502,25 @@ __device__ __forceinline__ void route_write_batch(RTimer& rt, const RouteParams&
 // index and seq = seq0 + index.
 constexpr uint32_t kDescLds = 512;
 
-__device__ __forceinline__ BufDesc route_desc(const RouteParams& rp, const uint4* s_desc, uint32_t r0, uint32_t i) {
+__device__ __forceinline__ RDesc route_desc(const RouteParams& rp, const uint4* s_desc, uint32_t r0, uint32_t i) {
+  RDesc d;
   if (i - r0 < kDescLds) {
-    // (uniform: scalar registers, not 8 VGPRs per descriptor)
+    // (uniform: scalar registers)
     const uint4 l = s_desc[i - r0];
-    const uint4 v = make_uint4(__builtin_amdgcn_readfirstlane(l.x), __builtin_amdgcn_readfirstlane(l.y),
-                               __builtin_amdgcn_readfirstlane(l.z), __builtin_amdgcn_readfirstlane(l.w));
-    BufDesc d;
-    d.offset = u64of(v.x, v.y);
-    d.len = v.z;
-    d.thread_rank = v.w & 0xffffu;
-    d.access = v.w >> 16;
+    d.offset = u64of(__builtin_amdgcn_readfirstlane(l.x), __builtin_amdgcn_readfirstlane(l.y));
+    d.len = __builtin_amdgcn_readfirstlane(l.z);
+    d.ta = __builtin_amdgcn_readfirstlane(l.w);
     d.pad = i;
-    d.seq = rp.seq0 + i;
     return d;
   }
-  return rp.p.sbufs[i];
+  const BufDesc g = rp.p.sbufs[i];
+  vm_drain();  // (rare: ranges past kDescLds; keeps the waits on the common path exact)
+  d.offset = u64of(__builtin_amdgcn_readfirstlane((uint32_t)g.offset),
+                   __builtin_amdgcn_readfirstlane((uint32_t)(g.offset >> 32)));
+  d.len = __builtin_amdgcn_readfirstlane(g.len);
+  d.ta = __builtin_amdgcn_readfirstlane(g.thread_rank | (g.access << 16));
+  d.pad = i;
+  return d;
 }
 
 template <bool TIMING>
@@ -459,6 +534,8 @@ __global__ __launch_bounds__(kWG, 1) void route_kernel(RouteParams rp) {
   __shared__ uint16_t s_perm[kRouteBatch];
   __shared__ uint32_t s_list[kMaxList];
   __shared__ uint32_t s_flags[3], s_nlist, s_next, s_err, s_wsum[kWG / 64], s_misc[3];
+  // the global mem_counters of the records this workgroup routes
+  __shared__ unsigned long long s_gsums[2][kGlobalSums], s_gmins[2][18], s_gmaxs[2][18];
 
   Params& p = rp.p;
   const int tid = threadIdx.x;
@@ -482,24 +559,68 @@ __global__ __launch_bounds__(kWG, 1) void route_kernel(RouteParams rp) {
     s_misc[1] = 0;
     s_misc[2] = kNoChunk;
   }
-  __syncthreads();
+  if (tid < (int)kGlobalSums) s_gsums[0][tid] = s_gsums[1][tid] = 0;
+  if (tid < 18) {
+    s_gmins[0][tid] = s_gmins[1][tid] = ~0ull;  // INIT_COUNTER (mem_analyzer.c:415-420)
+    s_gmaxs[0][tid] = s_gmaxs[1][tid] = 0;
+  }
+  DualAcc gacc;  // per-lane update_counters, drained every kDrainWindows windows
+  dual_clear(gacc);
+  uint32_t gwin = 0;
+  lds_sync();
 
   uint32_t nbatches = 0;  // (its parity picks the open-chunk state array)
   if (r0 < r1) {
+    // Two windows' records are in flight: this window's (A) and the next's
+    // (B), loaded where the next window starts if this one holds only whole
+    // 40 B records -- the fast path; a slow-path window reloads B.  The loop
+    // is unrolled by two (window(A, B), window(B, A)) so that no register of a
+    // load in flight is ever copied.  A window's own chunk stores go out
+    // before the loads two windows ahead, and its wait is a vmcnt that leaves
+    // the next window's loads in flight.
     uint32_t idx = r0;
     uint32_t cur = 0;  // byte cursor (cur_cpt, mem_sampling.c:836)
-    BufDesc d0 = route_desc(rp, s_desc, r0, idx);
-    BufDesc d1 = idx + 1 < r1 ? route_desc(rp, s_desc, r0, idx + 1) : d0;
-    BufDesc d2 = idx + 2 < r1 ? route_desc(rp, s_desc, r0, idx + 2) : d0;  // read a transition ahead
+    RDesc d0 = route_desc(rp, s_desc, r0, idx);
+    RDesc d1 = idx + 1 < r1 ? route_desc(rp, s_desc, r0, idx + 1) : d0;
     bool has1 = idx + 1 < r1;
-    RawRec nx;
+    // descriptor i of the range, given those of the window at idx (LDS reads otherwise)
+    auto desc_at = [&](uint32_t i, uint32_t at, const RDesc& a0, const RDesc& a1) -> RDesc {
+      return i == at ? a0 : i == at + 1 ? a1 : route_desc(rp, s_desc, r0, i);
+    };
+    // the next window's start if a window at (i, c) holds only whole records
+    // (the fast path's cursor update below)
+    auto advance = [&](uint32_t i, uint32_t c, const RDesc& e0, const RDesc& e1, bool h1, uint32_t& ni,
+                       uint32_t& nc) {
+      const uint32_t left = e0.len - c;
+      const uint32_t n0 = min(left / kRecBytes + (left % kRecBytes != 0), (uint32_t)kWG);
+      const uint32_t n1 = (h1 && n0 < (uint32_t)kWG) ? min(e1.len / kRecBytes + (e1.len % kRecBytes != 0),
+                                                            (uint32_t)kWG - n0) : 0u;
+      ni = i;
+      if (n1) {
+        ni = i + 1;
+        nc = n1 * kRecBytes;
+        if (nc >= e1.len) {
+          ni = i + 2;
+          nc = 0;
+        }
+      } else {
+        nc = c + n0 * kRecBytes;
+        if (nc >= e0.len) {
+          ni = i + 1;
+          nc = 0;
+        }
+      }
+    };
+    RawRec ra, rb;
+    uint32_t pidx, pcur;  // where rb was loaded
     {
-      const RWin wl = rwin_lane(tid, 0, d0, d1, has1);
-      rload_slot(p.data, wl, d0, d1, nx);
+      rload_slot_nb(p.data, rwin_lane(tid, 0, d0, d1, has1), d0, d1, ra);
+      advance(idx, 0, d0, d1, has1, pidx, pcur);
+      const bool pin = pidx < r1;  // (always three loads per lane, as in the loop)
+      const RDesc e0 = pin ? desc_at(pidx, idx, d0, d1) : d0;
+      const RDesc e1 = pin && pidx + 1 < r1 ? desc_at(pidx + 1, idx, d0, d1) : e0;
+      rload_slot_nb(p.data, rwin_lane(tid, pin ? pcur : 0u, e0, e1, pin && pidx + 1 < r1), e0, e1, rb);
     }
-    Held held;  // the previous window's record, staged after this window's barrier
-    held.q = kNoChunk;
-    bool hheld = false;  // held belongs to window bwin - 1 of the open batch
     uint32_t win = 0, bwin = 0;
     uint32_t ns0 = 0, ns1 = 0;  // per-buffer SAMPLE tallies: buffer idx, idx + 1
     RTimer rt;
@@ -508,27 +629,25 @@ __global__ __launch_bounds__(kWG, 1) void route_kernel(RouteParams rp) {
     rt.last = TIMING ? stamp() : 0;
     bool wpending = false;  // a sorted batch waits for its chunk stores
 
-    while (true) {
+    // one window: A holds its records, B the next window's (in flight);
+    // returns true after the range's last window
+    auto window = [&](RawRec& A, RawRec& B) -> bool {
       const RWin wl = rwin_lane(tid, cur, d0, d1, has1);
-      const Rec r = decode_rec(nx, wl.pos);
+      const Rec r = decode_rec(A, wl.pos);
       // ---- fast-path check: every 40 B stride slot holds a whole 40 B record
       const uint32_t wlen = wl.in1 ? d1.len : d0.len;
       const bool bad =
           (cur & 7) != 0 || (wl.cand && (uint64_t(wl.pos) + kRecBytes > wlen || (r.hdr >> 48) != kRecBytes));
       const uint64_t badm = __ballot(bad);
       if (badm && lane == 0) atomicOr(&s_flags[win % 3], 1u);
-      __syncthreads();
+      lds_sync();
       const uint32_t f = __builtin_amdgcn_readfirstlane(s_flags[win % 3]);
       if (tid == 0) s_flags[(win + 2) % 3] = 0;
       win++;
-      if (hheld) {  // the previous window's record to its staging slot
-        route_stage(L, held, bwin - 1, tid);
-        hheld = false;
-      }
-      if (TIMING) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (timing: the window's loads count as wait)
+      if (TIMING) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");  // (timing: this window's loads count as wait)
       rt_stamp<TIMING>(rt, 0);
       uint32_t nidx = idx;
-      uint64_t ncur;
+      uint32_t ncur;
       Rec rec = r;
       bool valid, rin1;
       uint32_t roff;
@@ -536,20 +655,7 @@ __global__ __launch_bounds__(kWG, 1) void route_kernel(RouteParams rp) {
         valid = wl.cand && uint32_t(r.hdr) == kSampleType;
         rin1 = wl.in1;
         roff = wl.pos;
-        if (wl.n1) {
-          nidx = idx + 1;
-          ncur = uint64_t(wl.n1) * kRecBytes;
-          if (ncur >= d1.len) {
-            nidx = idx + 2;
-            ncur = 0;
-          }
-        } else {
-          ncur = cur + uint64_t(wl.n0) * kRecBytes;
-          if (ncur >= d0.len) {
-            nidx = idx + 1;
-            ncur = 0;
-          }
-        }
+        advance(idx, cur, d0, d1, has1, nidx, ncur);
       } else {
         // ---- slow path (buffer idx only), as attribute_kernel: wave 0
         // follows the header chain (non-SAMPLE records skipped by size,
@@ -597,16 +703,16 @@ __global__ __launch_bounds__(kWG, 1) void route_kernel(RouteParams rp) {
             q0 += size;  // non-SAMPLE records are skipped by their size (:918)
           }
           if (lane == 0) {
-            if (err) set_error(p, d0.seq, (uint32_t)q0, err);
+            if (err) set_error(p, rp.seq0 + d0.pad, (uint32_t)q0, err);
             s_err = err;
             s_nlist = n;
             s_next = (uint32_t)min(q0, len);
           }
         }
-        __syncthreads();
+        lds_sync();
         const uint32_t n = __builtin_amdgcn_readfirstlane(s_nlist);
         const uint32_t serr = __builtin_amdgcn_readfirstlane(s_err);
-        ncur = serr ? len : __builtin_amdgcn_readfirstlane(s_next);
+        ncur = serr ? (uint32_t)len : __builtin_amdgcn_readfirstlane(s_next);
         if (ncur >= len) {
           nidx = idx + 1;
           ncur = 0;
@@ -617,39 +723,46 @@ __global__ __launch_bounds__(kWG, 1) void route_kernel(RouteParams rp) {
         RawRec rr;
         load_rec(base, roff, valid ? len : 0, rr);
         rec = decode_rec(rr, roff);
+        vm_drain();
       }
 
-      // ---- descriptors of the next window (the one after it is read now
-      // and used a transition later), and its loads: issued before this
-      // window's records are processed, after the chunk stores of a sorted
-      // batch that waits for them (see route_write_batch)
-      BufDesc nd0 = d0, nd1 = d1, nd2 = d2;
-      if (nidx == idx + 1) {
-        nd0 = d1;
-        nd1 = d2;
-        if (nidx + 2 < r1) nd2 = route_desc(rp, s_desc, r0, nidx + 2);
-      } else if (nidx == idx + 2) {
-        nd0 = d2;
-        if (nidx + 1 < r1) nd1 = route_desc(rp, s_desc, r0, nidx + 1);
-        if (nidx + 2 < r1) nd2 = route_desc(rp, s_desc, r0, nidx + 2);
-      }
+      // ---- descriptors of the next window
+      const RDesc nd0 = nidx < r1 ? desc_at(nidx, idx, d0, d1) : d0;
+      const RDesc nd1 = nidx + 1 < r1 ? desc_at(nidx + 1, idx, d0, d1) : nd0;
       const bool nhas1 = nidx + 1 < r1;
-      const bool wrote = wpending;  // (uniform)
-      if (wpending) {  // the previous batch's chunk stores go out before the next window's loads
+      // ---- the previous batch's chunk stores (before any later load: see
+      // route_write_batch), then a barrier: every wave has gathered that
+      // batch from the staging slots this window's records go to
+      if (wpending) {
         route_write_batch<TIMING>(rt, rp, tid, L, nbatches - 1);
         wpending = false;
+        lds_sync();
       }
-      if (nidx < r1) {  // (in flight while this window's records are processed)
-        const RWin nl = rwin_lane(tid, (uint32_t)ncur, nd0, nd1, nhas1);
-        rload_slot(p.data, nl, nd0, nd1, nx);
+      // ---- the next window's loads again if this window was not what B
+      // assumed (slow path), and the loads of the window after it
+      if (nidx < r1 && (nidx != pidx || ncur != pcur)) {
+        rload_slot(p.data, rwin_lane(tid, ncur, nd0, nd1, nhas1), nd0, nd1, B);
+        vm_drain();  // (rare: keeps the waits on the common path exact)
+      }
+      uint32_t qidx = nidx, qcur = 0;
+      if (nidx < r1) advance(nidx, ncur, nd0, nd1, nhas1, qidx, qcur);
+      {  // (always three loads per lane: past the range's end they reread this window's buffer)
+        const bool qin = qidx < r1;
+        const RDesc e0 = !qin ? d0 : desc_at(qidx, nidx, nd0, nd1);
+        const RDesc e1 = qin && qidx + 1 < r1 ? desc_at(qidx + 1, nidx, nd0, nd1) : e0;
+        rload_slot_nb(p.data, rwin_lane(tid, qin ? qcur : 0u, e0, e1, qin && qidx + 1 < r1), e0, e1, A);
       }
 
-      // ---- this window's record: global counters, then its partition
+      // ---- this window's record: update_counters(global_counters, sample)
+      // (mem_sampling.c:882: every SAMPLE, matched or not), its partition, its
+      // batch rank, its slot
       rt_stamp<TIMING>(rt, 1);
-      const uint32_t acc_l = rin1 ? d1.access : d0.access;
-      Held hr;
-      hr.q = kNoChunk;
-      // (update_counters runs in the local pass, from the record's level field)
+      const uint32_t acc_l = rin1 ? d1.access() : d0.access();
+      if (valid) route_count(gacc, s_gsums, s_gmins, s_gmaxs, acc_l, uint32_t(rec.dsrc >> 5) & 0x3fff, rec.w);
+      if (++gwin == kDrainWindows) {  // keep the per-lane u16 counts / u32 sums bounded
+        dual_drain(gacc, s_gsums, lane);
+        gwin = 0;
+      }
       rt_stamp<TIMING>(rt, 2);
       uint32_t node = 0;
       if (valid) {
@@ -660,6 +773,8 @@ __global__ __launch_bounds__(kWG, 1) void route_kernel(RouteParams rp) {
       }
       if (TIMING) (void)__builtin_amdgcn_readfirstlane(__ballot(node != 0));  // (the search ends here)
       rt_stamp<TIMING>(rt, 3);
+      Held hr;
+      hr.q = kNoChunk;
       if (valid) {
         // (below the first key: partition 0, where the lookup finds no node)
         const uint32_t q = node ? min(eytz_rank(node, kPartLevels), P - 1) : 0u;
@@ -667,11 +782,9 @@ __global__ __launch_bounds__(kWG, 1) void route_kernel(RouteParams rp) {
         hr.q = q | (rk << 11);
         hr.a = make_uint4((uint32_t)rec.addr, (uint32_t)(rec.addr >> 32), (uint32_t)rec.ts, (uint32_t)(rec.ts >> 32));
         const uint32_t g = rin1 ? d1.pad : d0.pad;
-        const uint32_t th = rin1 ? d1.thread_rank : d0.thread_rank;
+        const uint32_t th = rin1 ? d1.thread_rank() : d0.thread_rank();
         hr.x = x_encode(rp.xl, g, roff, th, acc_l, uint32_t(rec.dsrc >> 5) & 0x3fff /* data_src.mem_lvl */, rec.w);
       }
-      held = hr;
-      hheld = true;
       {
         // per-buffer SAMPLE tallies (mem_sampling.c:921-926): lanes of this
         // wave in buffer idx + 1 are tid >= n0
@@ -693,31 +806,32 @@ __global__ __launch_bounds__(kWG, 1) void route_kernel(RouteParams rp) {
       rt_stamp<TIMING>(rt, 4);
       if (p.flags & kDbgRouteNoBatch) {  // (ablation) forget the records
         if (++bwin == kRouteWindows || last) {
-          __syncthreads();
+          lds_sync();
           for (uint32_t q = tid; q < P; q += kWG) s_hist[q] = 0;
-          hheld = false;
           bwin = 0;
         }
-      } else if (++bwin == kRouteWindows || last) {
-        // the batch's last window to its staging slots -- after every wave has
-        // gathered the previous batch, when that was written in this window
-        // (a one-window batch at the end of the range)
-        if (wrote) __syncthreads();
-        route_stage(L, held, bwin - 1, tid);
-        hheld = false;
-        route_sort_batch<TIMING>(rt, rp, tid, L, nbatches, bwin, c0, cap);
-        bwin = 0;
-        nbatches++;
-        if (last) route_write_batch<TIMING>(rt, rp, tid, L, nbatches - 1);
-        else wpending = true;
+      } else {
+        route_stage(L, hr, bwin, tid);  // (its batch's staging slot: no wave reads it now)
+        if (++bwin == kRouteWindows || last) {
+          route_sort_batch<TIMING>(rt, rp, tid, L, nbatches, bwin, c0, cap);
+          bwin = 0;
+          nbatches++;
+          if (last) route_write_batch<TIMING>(rt, rp, tid, L, nbatches - 1);
+          else wpending = true;
+        }
       }
       idx = nidx;
-      cur = (uint32_t)ncur;
+      cur = ncur;
       d0 = nd0;
       d1 = nd1;
-      d2 = nd2;
       has1 = nhas1;
-      if (last) break;
+      pidx = qidx;
+      pcur = qcur;
+      return last;
+    };
+    while (true) {
+      if (window(ra, rb)) break;
+      if (window(rb, ra)) break;
     }
     if (TIMING && lane == 0) {
       unsigned long long* o = p.dbg + (uint64_t(blockIdx.x) * (kWG / 64) + tid / 64) * kRouteTimingWords;
@@ -726,7 +840,17 @@ __global__ __launch_bounds__(kWG, 1) void route_kernel(RouteParams rp) {
       o[10] = nbatches;
     }
   }
-  __syncthreads();
+  dual_drain(gacc, s_gsums, lane);
+  lds_sync();
+#pragma unroll
+  for (uint32_t a = 0; a < 2; a++) {  // the global mem_counters of both access types
+    if (tid < (int)kGlobalSums && s_gsums[a][tid])
+      atomicAdd(reinterpret_cast<unsigned long long*>(p.sum64 + gsum_index(a, tid)), s_gsums[a][tid]);
+    if (tid < 18 && s_gsums[a][3 + 2 * tid]) {
+      atomicMin(reinterpret_cast<unsigned long long*>(p.min64 + a * 18 + tid), s_gmins[a][tid]);
+      atomicMax(reinterpret_cast<unsigned long long*>(p.max64 + a * 18 + tid), s_gmaxs[a][tid]);
+    }
+  }
   // open chunks' fill, chunk counts per partition, pool use
   for (uint32_t q = tid; q < P; q += kWG) {
     const uint32_t cur = s_cur[nbatches & 1][q];
@@ -754,8 +878,9 @@ __global__ __launch_bounds__(256) void overflow_kernel(RouteParams rp) {
 // pass 2: count, plan (one workgroup) and scatter
 
 // chunks per (route workgroup, partition) from the chunks' partition tags
-__global__ __launch_bounds__(kWG) void count_kernel(ScatterParams r) {
+__global__ __launch_bounds__(kWG) void count_kernel(CountParams cp) {
   __shared__ uint32_t s_cnt[kMaxParts + 1];
+  const ScatterParams& r = cp.sc;
   const uint32_t tid = threadIdx.x, w = blockIdx.x, P = r.nparts;
   for (uint32_t q = tid; q < P; q += kWG) s_cnt[q] = 0;
   __syncthreads();
@@ -853,23 +978,14 @@ __global__ __launch_bounds__(kWG, 1) void local_kernel(LocalParams lp) {
   __shared__ unsigned long long s_first[kPartEntries];
   __shared__ uint32_t s_pg[kPartCells / 2];
   __shared__ uint32_t s_clist[kItemChunks];  // the item's chunk list entries
+  __shared__ unsigned long long s_cm[kItemChunks];  // the item's chunks' match bits (found_kernel)
   __shared__ uint32_t s_item;
-  // the global mem_counters of the records this workgroup attributes
-  __shared__ unsigned long long s_gsums[2][kGlobalSums], s_gmins[2][18], s_gmaxs[2][18];
 
   Params& p = lp.p;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const uint32_t nitems = lp.ctl[0];
   const uint32_t T = p.nb_threads;
   const bool pages = (p.flags & NMG_F_PAGE_HIST) != 0;
-  if (tid < (int)kGlobalSums) s_gsums[0][tid] = s_gsums[1][tid] = 0;
-  if (tid < 18) {
-    s_gmins[0][tid] = s_gmins[1][tid] = ~0ull;  // INIT_COUNTER (mem_analyzer.c:415-420)
-    s_gmaxs[0][tid] = s_gmaxs[1][tid] = 0;
-  }
-  DualAcc gacc;  // per-lane update_counters, drained every kDrainWindows chunks
-  dual_clear(gacc);
-  uint32_t acc_chunks = 0;
   RTimer rt;  // (kDbgLocalTiming) per-wave phase cycles
 #pragma unroll
   for (int k = 0; k < 9; k++) rt.acc[k] = 0;
@@ -908,17 +1024,20 @@ __global__ __launch_bounds__(kWG, 1) void local_kernel(LocalParams lp) {
     const uint32_t ncell = (pages && pi.pages_lds) ? T * pi.span : 0u;
     for (uint32_t i = tid; i < (ncell + 1) / 2; i += kWG) s_pg[i] = 0;
     __syncthreads();
+    const uint64_t k0key = u64of(__builtin_amdgcn_readfirstlane((uint32_t)s_keys[0]),
+                                 __builtin_amdgcn_readfirstlane((uint32_t)(s_keys[0] >> 32)));
     rt_stamp<TIMING>(rt, 7);
 
     // Each wave takes every 16th chunk of the item (the item's list entries
-    // are in LDS); two chunks' records are in flight while one is processed
-    // (a wave's chunk is 1.5 KiB: one in flight per wave leaves HBM idle).
-    // The compiler waits for a chunk's loads with the smallest vmcnt any path
-    // allows, so the loop is shaped for that: unrolled by two (the record
-    // registers are never copied -- a copy of a load in flight waits for it),
-    // every chunk load covers the whole wave (a fixed number of memory ops
-    // between a load and its use), and the rare paths that issue global
-    // memory ops of their own end with vmcnt(0).
+    // are in LDS) and works on two chunks at a time, their steps interleaved
+    // (the LDS round trips of one cover the other's); the records of the next
+    // two are in flight meanwhile (a wave's chunk is 1.5 KiB).  The compiler
+    // waits for a chunk's loads with the smallest vmcnt any path allows, so
+    // the loop is shaped for that: unrolled (the record registers are never
+    // copied -- a copy of a load in flight waits for it), every chunk load
+    // covers the whole wave (a fixed number of memory ops between a load and
+    // its use), and the rare paths that issue global memory ops of their own
+    // end with vmcnt(0).
     constexpr uint32_t kStride = kWG / 64;
     const uint32_t nl = item.z - item.y;
     const uint32_t nmine = nl > (uint32_t)wave ? (nl - (uint32_t)wave + kStride - 1) / kStride : 0u;
@@ -928,32 +1047,47 @@ __global__ __launch_bounds__(kWG, 1) void local_kernel(LocalParams lp) {
       a = lp.rec16[i];
       x = lp.recx[i];
     };
-    auto process = [&](uint32_t k, const uint4 a16, const uint64_t x) {
-      const uint32_t ce = s_clist[(uint32_t)wave + k * kStride];
-      const uint32_t c = ce & ((1u << kChunkIdBits) - 1), fill = ce >> kChunkIdBits;
-      const bool valid = (uint32_t)lane < fill;
-      if (TIMING) {  // (timing: this chunk's loads count as wait; a match-bit store and two loads are younger)
-        asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-        nchunks++;
+    // chunks k and k + 1 of this wave (k + 1 past the last: no valid lane)
+    auto process2 = [&](uint32_t k, const uint4 (&a16)[2], const uint64_t (&xw)[2]) {
+      uint32_t li[2];
+      bool valid[2];
+      uint64_t addr[2], ts[2], w[2];
+      XRec xr[2];
+#pragma unroll
+      for (int j = 0; j < 2; j++) {
+        li[j] = (uint32_t)wave + (k + j) * kStride;  // (list position in the item)
+        const uint32_t fill = k + j < nmine ? s_clist[li[j]] >> kChunkIdBits : 0u;
+        valid[j] = (uint32_t)lane < fill;
+      }
+      if (TIMING) {  // (timing: these chunks' loads count as wait; the next two chunks' four loads are younger)
+        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        nchunks += 2;
       }
       rt_stamp<TIMING>(rt, 0);
-      const uint64_t addr = u64of(a16.x, a16.y), ts = u64of(a16.z, a16.w);
+#pragma unroll
+      for (int j = 0; j < 2; j++) {
+        addr[j] = u64of(a16[j].x, a16[j].y);
+        ts[j] = u64of(a16[j].z, a16[j].w);
+      }
       if (p.flags & kDbgLocalNoWork) {  // (ablation) loads only
-        lp.cmatch[c] = __builtin_amdgcn_readfirstlane((uint32_t)(addr ^ ts ^ x));
+#pragma unroll
+        for (int j = 0; j < 2; j++)
+          if (lane == 0 && k + j < nmine) s_cm[li[j]] = addr[j] ^ ts[j] ^ xw[j];
         return;
       }
-      // update_counters(global_counters, sample) (mem_sampling.c:882): every
-      // routed SAMPLE, matched or not
-      const XRec xr = x_decode(lp.xl, x);
-      uint64_t w = valid ? xr.wq : 0ull;
-      if (__ballot(valid && xr.wq == lp.xl.wesc)) {  // (rare) escaped weights: re-read from the record
-        if (valid) w = x_weight(lp.xl, xr, p.data, lp.descs);
-        vm_drain();
+      // (update_counters of every routed SAMPLE: count_kernel)
+      bool esc = false;
+#pragma unroll
+      for (int j = 0; j < 2; j++) {
+        xr[j] = x_decode(lp.xl, xw[j]);
+        w[j] = valid[j] ? xr[j].wq : 0ull;
+        esc |= valid[j] && xr[j].wq == lp.xl.wesc;
       }
-      if (valid && !(p.flags & kDbgLocalNoGlobal)) dual_count(gacc, s_gsums, s_gmins, s_gmaxs, xr.acc, xr.lvl, w);
-      if (++acc_chunks == kDrainWindows) {  // keep the per-lane u16 counts / u32 sums bounded
-        dual_drain(gacc, s_gsums, lane);
-        acc_chunks = 0;
+      if (__ballot(esc)) {  // (rare) escaped weights: re-read from the record
+#pragma unroll
+        for (int j = 0; j < 2; j++)
+          if (valid[j] && xr[j].wq == lp.xl.wesc) w[j] = x_weight(lp.xl, xr[j], p.data, lp.descs);
+        vm_drain();
       }
       rt_stamp<TIMING>(rt, 1);
       // lower bound among the partition's keys (ht_lower_key, tools/hash.c:63-77):
@@ -961,106 +1095,156 @@ __global__ __launch_bounds__(kWG, 1) void local_kernel(LocalParams lp) {
       // first key (partition 0 only) there is no node.  The directory slot
       // gives the largest key <= the slot start and the keys inside the slot
       // (usually 0 or 1; a binary search among them otherwise).
-      const uint64_t k0key = s_keys[0];
-      int32_t r = -1;
-      if (valid && addr >= k0key) {
-        const uint64_t rel = addr - k0key;
-        const uint32_t de = s_dir[(uint32_t)min(rel >> dshift, (uint64_t)(kPartDir - 1))];
-        uint32_t a = de & 0xffffu, n = de >> 16;  // answer in [a, a + n]: keys[a] <= addr
+      int32_t r[2];
+      uint32_t sa[2], sn[2];
+#pragma unroll
+      for (int j = 0; j < 2; j++) {
+        r[j] = -1;
+        sa[j] = sn[j] = 0;
+        if (valid[j] && addr[j] >= k0key) {
+          const uint32_t de = s_dir[(uint32_t)min((addr[j] - k0key) >> dshift, (uint64_t)(kPartDir - 1))];
+          sa[j] = de & 0xffffu;  // answer in [a, a + n]: keys[a] <= addr
+          sn[j] = de >> 16;
+          r[j] = 0;
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 2; j++) {
+        uint32_t a = sa[j], n = sn[j];
         while (n) {
           const uint32_t half = (n + 1) >> 1;
-          if (s_keys[a + half] <= addr) {
+          if (s_keys[a + half] <= addr[j]) {
             a += half;
             n -= half;
           } else {
             n = half - 1;
           }
         }
-        r = (int32_t)a;
+        if (r[j] >= 0) r[j] = (int32_t)a;
       }
-      if (TIMING) (void)__builtin_amdgcn_readfirstlane(__ballot(r >= 0));  // (the search ends here)
+      if (TIMING) (void)__builtin_amdgcn_readfirstlane(__ballot(r[0] >= 0 || r[1] >= 0));  // (the search ends here)
       rt_stamp<TIMING>(rt, 2);
-      int32_t erel = -1;
-      uint64_t baddr = 0;
-      uint32_t hrel = kEmpty32;
-      bool older = false;
-      if (r >= 0 && !(p.flags & kDbgLocalNoSearch)) {
-        const uint4 na = s_nodes[2 * r], nb = s_nodes[2 * r + 1];
-        const uint2 inf = s_info[r];
-        if (entry_match(na, nb, addr, ts)) {  // is_sample_in_buffer (mem_analyzer.c:141-155), newest entry
-          erel = (int32_t)(inf.y & 0x7fffffffu);
-          baddr = u64of(na.x, na.y);
-          hrel = inf.x;
-        } else {
-          older = (inf.y >> 31) != 0;
+      int32_t erel[2];
+      uint64_t baddr[2];
+      uint32_t hrel[2];
+      bool older[2];
+#pragma unroll
+      for (int j = 0; j < 2; j++) {
+        erel[j] = -1;
+        baddr[j] = 0;
+        hrel[j] = kEmpty32;
+        older[j] = false;
+        if (r[j] >= 0 && !(p.flags & kDbgLocalNoSearch)) {
+          const uint4 na = s_nodes[2 * r[j]], nb = s_nodes[2 * r[j] + 1];
+          const uint2 inf = s_info[r[j]];
+          if (entry_match(na, nb, addr[j], ts[j])) {  // is_sample_in_buffer (mem_analyzer.c:141-155), newest entry
+            erel[j] = (int32_t)(inf.y & 0x7fffffffu);
+            baddr[j] = u64of(na.x, na.y);
+            hrel[j] = inf.x;
+          } else {
+            older[j] = (inf.y >> 31) != 0;
+          }
         }
       }
-      if (__ballot(older)) {  // (rare) older entries of a reused address (LIFO, tools/hash.c:108-114)
-        if (older) {
-          const uint4 d = reinterpret_cast<const uint4*>(p.nodes + pi.k0 + (uint32_t)r)[3];  // (count, first)
+      if (__ballot(older[0] || older[1])) {  // (rare) older entries of a reused address (LIFO, tools/hash.c:108-114)
+#pragma unroll
+        for (int j = 0; j < 2; j++) {
+          if (!older[j]) continue;
+          const uint4 d = reinterpret_cast<const uint4*>(p.nodes + pi.k0 + (uint32_t)r[j])[3];  // (count, first)
           Match m;
           m.e = -1;
-          match_older(p, d.y, d.x, addr, ts, m);
+          match_older(p, d.y, d.x, addr[j], ts[j], m);
           if (m.e >= 0) {
-            erel = (int32_t)(m.e - pi.e0);
-            baddr = m.baddr;
-            hrel = m.hist == kHistSparse ? kEmpty32 : (uint32_t)(m.hist - pi.cb);
+            erel[j] = (int32_t)(m.e - pi.e0);
+            baddr[j] = m.baddr;
+            hrel[j] = m.hist == kHistSparse ? kEmpty32 : (uint32_t)(m.hist - pi.cb);
           }
         }
         vm_drain();
       }
-      // the chunk's match bits (found_kernel): every lane stores the same word
-      lp.cmatch[c] = __ballot(erel >= 0);
-      rt_stamp<TIMING>(rt, 3);
-      if (erel < 0) return;
-      if (p.flags & kDbgLocalNoObj) {
-      } else if (w < kLaneMaxWeight) {
-        atomicAdd(&s_owt[xr.acc][erel], (1ull << kPackShift) | w);
+      // the chunks' match bits (found_kernel), stored with the item's counters
+#pragma unroll
+      for (int j = 0; j < 2; j++) {
+        const uint64_t fm = __ballot(erel[j] >= 0);
+        if (lane == 0 && k + j < nmine) s_cm[li[j]] = fm;
       }
-      if (__ballot(erel >= 0 && w >= kLaneMaxWeight && !(p.flags & kDbgLocalNoObj))) {  // (rare) large weights
-        if (w >= kLaneMaxWeight && !(p.flags & kDbgLocalNoObj)) {
-          const uint64_t e = pi.e0 + (uint32_t)erel;
-          atomicAdd(reinterpret_cast<unsigned long long*>(p.sum64 + objcw_index(e, xr.acc, 0, p.nb_entries)), 1ull);
-          atomicAdd(reinterpret_cast<unsigned long long*>(p.sum64 + objcw_index(e, xr.acc, 1, p.nb_entries)),
-                    (unsigned long long)w);
+      rt_stamp<TIMING>(rt, 3);
+      const bool noobj = (p.flags & kDbgLocalNoObj) != 0;
+#pragma unroll
+      for (int j = 0; j < 2; j++)
+        if (erel[j] >= 0 && !noobj && w[j] < kLaneMaxWeight)
+          atomicAdd(&s_owt[xr[j].acc][erel[j]], (1ull << kPackShift) | w[j]);
+      if (__ballot((erel[0] >= 0 && w[0] >= kLaneMaxWeight) || (erel[1] >= 0 && w[1] >= kLaneMaxWeight)) &&
+          !noobj) {  // (rare) large weights
+#pragma unroll
+        for (int j = 0; j < 2; j++) {
+          if (erel[j] < 0 || w[j] < kLaneMaxWeight) continue;
+          const uint64_t e = pi.e0 + (uint32_t)erel[j];
+          atomicAdd(reinterpret_cast<unsigned long long*>(p.sum64 + objcw_index(e, xr[j].acc, 0, p.nb_entries)), 1ull);
+          atomicAdd(reinterpret_cast<unsigned long long*>(p.sum64 + objcw_index(e, xr[j].acc, 1, p.nb_entries)),
+                    (unsigned long long)w[j]);
         }
         vm_drain();
       }
       // first match in analysis order (quirk Q7)
-      const unsigned long long ord = ((lp.seq0 + xr.g) << 32) | xr.off;
-      if (!(p.flags & kDbgLocalNoObj) && ord < s_first[erel]) atomicMin(&s_first[erel], ord);
+      if (!noobj) {
+        unsigned long long ord[2], cur[2];
+#pragma unroll
+        for (int j = 0; j < 2; j++) {
+          ord[j] = ((lp.seq0 + xr[j].g) << 32) | xr[j].off;
+          cur[j] = erel[j] >= 0 ? s_first[erel[j]] : 0ull;
+        }
+#pragma unroll
+        for (int j = 0; j < 2; j++)
+          if (erel[j] >= 0 && ord[j] < cur[j]) atomicMin(&s_first[erel[j]], ord[j]);
+      }
       rt_stamp<TIMING>(rt, 4);
       if (pages && !(p.flags & kDbgLocalNoPage)) {
         // ma_get_block: page_no = (int)((addr - buffer_addr) / 4096) (mem_analyzer.c:530-531)
-        const uint32_t page = uint32_t(int(uint64_t(addr - baddr) / kPageSize));
-        if (hrel != kEmpty32 && ncell) {
-          const uint32_t li = xr.th * pi.span + hrel + page;
-          atomicAdd(&s_pg[li >> 1], 1u << (16 * (li & 1)));
+        uint32_t page[2];
+        bool glob = false;
+#pragma unroll
+        for (int j = 0; j < 2; j++) {
+          page[j] = uint32_t(int(uint64_t(addr[j] - baddr[j]) / kPageSize));
+          if (erel[j] >= 0 && hrel[j] != kEmpty32 && ncell) {
+            const uint32_t c = xr[j].th * pi.span + hrel[j] + page[j];
+            atomicAdd(&s_pg[c >> 1], 1u << (16 * (c & 1)));
+          }
+          glob |= erel[j] >= 0 && (hrel[j] == kEmpty32 || !ncell);
         }
-        if (__ballot(hrel == kEmpty32 || !ncell)) {  // (rare) cells in global memory: dense or sparse
-          if (hrel != kEmpty32 && !ncell) {
-            atomicAdd(p.hist + uint64_t(xr.th) * p.hist_cells + pi.cb + hrel + page, 1u);
-          } else if (hrel == kEmpty32) {
-            const uint32_t sidx = p.entries[pi.e0 + (uint32_t)erel].sidx;
-            if (sidx != ~0u) sparse_add(p, sparse_key(sidx, xr.th, page), lp.seq0 + xr.g, xr.off, 1u);
+        if (__ballot(glob)) {  // (rare) cells in global memory: dense or sparse
+#pragma unroll
+          for (int j = 0; j < 2; j++) {
+            if (erel[j] < 0) continue;
+            if (hrel[j] != kEmpty32 && !ncell) {
+              atomicAdd(p.hist + uint64_t(xr[j].th) * p.hist_cells + pi.cb + hrel[j] + page[j], 1u);
+            } else if (hrel[j] == kEmpty32) {
+              const uint32_t sidx = p.entries[pi.e0 + (uint32_t)erel[j]].sidx;
+              if (sidx != ~0u) sparse_add(p, sparse_key(sidx, xr[j].th, page[j]), lp.seq0 + xr[j].g, xr[j].off, 1u);
+            }
           }
           vm_drain();
         }
       }
       rt_stamp<TIMING>(rt, 5);
     };
-    uint4 a0, a1;
-    uint64_t x0, x1;
-    chunk_load(0, a0, x0);
-    chunk_load(1, a1, x1);
-    for (uint32_t k = 0; k < nmine; k += 2) {
-      process(k, a0, x0);
-      chunk_load(k + 2, a0, x0);
-      if (k + 1 < nmine) process(k + 1, a1, x1);
-      chunk_load(k + 3, a1, x1);
+    uint4 A[2], B[2];
+    uint64_t XA[2], XB[2];
+    chunk_load(0, A[0], XA[0]);
+    chunk_load(1, A[1], XA[1]);
+    chunk_load(2, B[0], XB[0]);
+    chunk_load(3, B[1], XB[1]);
+    for (uint32_t k = 0; k < nmine; k += 4) {
+      process2(k, A, XA);
+      chunk_load(k + 4, A[0], XA[0]);
+      chunk_load(k + 5, A[1], XA[1]);
+      if (k + 2 < nmine) process2(k + 2, B, XB);
+      chunk_load(k + 6, B[0], XB[0]);
+      chunk_load(k + 7, B[1], XB[1]);
     }
     __syncthreads();
     rt_stamp<TIMING>(rt, 8);  // (waiting for the item's slowest wave counts as flush)
+    for (uint32_t i = tid; i < nl; i += kWG) lp.cmatch[s_clist[i] & ((1u << kChunkIdBits) - 1)] = s_cm[i];
     // the item's counters to global memory: consecutive lanes, consecutive words
     for (uint32_t i = tid; i < pi.ne; i += kWG) {
       const uint64_t e = pi.e0 + i;
@@ -1097,18 +1281,6 @@ __global__ __launch_bounds__(kWG, 1) void local_kernel(LocalParams lp) {
     for (int k = 0; k < 9; k++) o[k] = rt.acc[k];
     o[9] = nchunks;
     o[10] = nit;
-  }
-  // global mem_counters of both access types
-  dual_drain(gacc, s_gsums, lane);
-  __syncthreads();
-#pragma unroll
-  for (uint32_t a = 0; a < 2; a++) {
-    if (tid < (int)kGlobalSums && s_gsums[a][tid])
-      atomicAdd(reinterpret_cast<unsigned long long*>(p.sum64 + gsum_index(a, tid)), s_gsums[a][tid]);
-    if (tid < 18 && s_gsums[a][3 + 2 * tid]) {
-      atomicMin(reinterpret_cast<unsigned long long*>(p.min64 + a * 18 + tid), s_gmins[a][tid]);
-      atomicMax(reinterpret_cast<unsigned long long*>(p.max64 + a * 18 + tid), s_gmaxs[a][tid]);
-    }
   }
 }
 
@@ -1168,7 +1340,7 @@ hipError_t launch_overflow(hipStream_t s, const RouteParams& r) {
   return hipGetLastError();
 }
 
-hipError_t launch_count(uint32_t grid, hipStream_t s, const ScatterParams& r) {
+hipError_t launch_count(uint32_t grid, hipStream_t s, const CountParams& r) {
   hipLaunchKernelGGL(count_kernel, dim3(grid), dim3(kWG), 0, s, r);
   return hipGetLastError();
 }
