@@ -971,7 +971,10 @@ __global__ __launch_bounds__(kWG) void scatter_kernel(ScatterParams r) {
 template <bool TIMING>
 __global__ __launch_bounds__(kWG, 1) void local_kernel(LocalParams lp) {
   __shared__ uint64_t s_keys[kPartSlots];
-  __shared__ uint4 s_nodes[2 * kPartSlots];
+  // node records split in two 16 B arrays (addr, end) and (alloc, free): a
+  // 16 B stride spreads a wave's random reads over twice the bank groups of
+  // a 32 B one
+  __shared__ uint4 s_nodes[kPartSlots], s_dates[kPartSlots];
   __shared__ uint2 s_info[kPartSlots];
   __shared__ uint32_t s_dir[kPartDir];
   __shared__ unsigned long long s_owt[2][kPartEntries];
@@ -1009,8 +1012,8 @@ __global__ __launch_bounds__(kWG, 1) void local_kernel(LocalParams lp) {
       const uint2* gi = lp.pe_info + uint64_t(q) * kPartSlots;
       for (uint32_t i = tid; i < nk; i += kWG) {
         s_keys[i] = gk[i];
-        s_nodes[2 * i] = gn[2 * i];
-        s_nodes[2 * i + 1] = gn[2 * i + 1];
+        s_nodes[i] = gn[2 * i];
+        s_dates[i] = gn[2 * i + 1];
         s_info[i] = gi[i];
       }
       const uint32_t* gd = lp.pe_dir + uint64_t(q) * kPartDir;
@@ -1135,7 +1138,7 @@ __global__ __launch_bounds__(kWG, 1) void local_kernel(LocalParams lp) {
         hrel[j] = kEmpty32;
         older[j] = false;
         if (r[j] >= 0 && !(p.flags & kDbgLocalNoSearch)) {
-          const uint4 na = s_nodes[2 * r[j]], nb = s_nodes[2 * r[j] + 1];
+          const uint4 na = s_nodes[r[j]], nb = s_dates[r[j]];
           const uint2 inf = s_info[r[j]];
           if (entry_match(na, nb, addr[j], ts[j])) {  // is_sample_in_buffer (mem_analyzer.c:141-155), newest entry
             erel[j] = (int32_t)(inf.y & 0x7fffffffu);
