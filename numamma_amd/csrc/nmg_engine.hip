@@ -2225,12 +2225,15 @@ extern "C" uint32_t nmg_get_nb_buffers(nmg_engine* h) {
 }
 
 namespace nmg {
-int engine_download(nmg_engine* h, HostResults& r) {
+int engine_download(nmg_engine* h, HostResults& r, bool entries) {
   int rc = nmg_synchronize(h);
   if (rc) return rc;
-  std::vector<uint64_t> sum(h->n_sum64), mn(h->n_min64), mx(h->n_max64);
-  HIP_TRY(h, hipMemcpy(sum.data(), h->d_sum64, h->n_sum64 * 8, hipMemcpyDeviceToHost));
-  HIP_TRY(h, hipMemcpy(mn.data(), h->d_min64, h->n_min64 * 8, hipMemcpyDeviceToHost));
+  // (entries == false: the global counters and per-buffer counts only, not
+  // the per-entry arrays -- 40 MB at 1M entries)
+  const uint64_t ns = entries ? h->n_sum64 : 2 * kGlobalSums, nm = entries ? h->n_min64 : 36;
+  std::vector<uint64_t> sum(ns), mn(nm), mx(h->n_max64);
+  HIP_TRY(h, hipMemcpy(sum.data(), h->d_sum64, ns * 8, hipMemcpyDeviceToHost));
+  HIP_TRY(h, hipMemcpy(mn.data(), h->d_min64, nm * 8, hipMemcpyDeviceToHost));
   HIP_TRY(h, hipMemcpy(mx.data(), h->d_max64, h->n_max64 * 8, hipMemcpyDeviceToHost));
   for (int a = 0; a < 2; a++) {
     nmg_mem_counters& c = r.global[a];
@@ -2245,13 +2248,13 @@ int engine_download(nmg_engine* h, HostResults& r) {
       c.b[k].max_weight = mx[a * 18 + k];
     }
   }
-  const uint64_t E = h->E;
+  const uint64_t E = entries ? h->E : 0;
   r.first.assign(mn.begin() + 36, mn.begin() + 36 + E);
   r.count_weight.resize(4 * E);  // SoA [2][2][E] -> [E][2][2]
   for (uint64_t e = 0; e < E; e++)
     for (uint32_t a = 0; a < 2; a++)
       for (uint32_t w = 0; w < 2; w++) r.count_weight[e * 4 + a * 2 + w] = sum[objcw_index(e, a, w, E)];
-  if (h->flags & NMG_F_OBJECT_LEVELS)
+  if ((h->flags & NMG_F_OBJECT_LEVELS) && entries)
     r.levels.assign(sum.begin() + 2 * kGlobalSums + 4 * E, sum.end());
   else
     r.levels.clear();
@@ -2293,7 +2296,7 @@ extern "C" int nmg_get_global_counters(nmg_engine* h, nmg_mem_counters out[2], u
   if (!h || !out) return NMG_ERR_INVALID;
   if (!h->have_table) return fail(h, NMG_ERR_STATE, "no object table");
   HostResults r;
-  int rc = engine_download(h, r);
+  int rc = engine_download(h, r, false);
   if (rc) return rc;
   out[0] = r.global[0];
   out[1] = r.global[1];
@@ -2306,7 +2309,7 @@ extern "C" int nmg_get_buffer_counts(nmg_engine* h, uint32_t* nb_samples, uint32
   if (!h) return NMG_ERR_INVALID;
   if (!h->have_table) return fail(h, NMG_ERR_STATE, "no object table");
   HostResults r;
-  int rc = engine_download(h, r);
+  int rc = engine_download(h, r, false);
   if (rc) return rc;
   if (nb_samples) memcpy(nb_samples, r.buf_samples.data(), r.buf_samples.size() * 4);
   if (nb_found) memcpy(nb_found, r.buf_found.data(), r.buf_found.size() * 4);

@@ -56,7 +56,7 @@ uint32_t engine_flags(nmg_engine* h);
 const std::vector<uint64_t>& engine_hist_base(nmg_engine* h);  // per entry, kHistSparse if sparse/none
 const std::vector<uint64_t>& engine_npages(nmg_engine* h);     // per entry: buffer_size/4096 + 1
 const std::vector<uint32_t>& engine_sparse_entries(nmg_engine* h);  // sparse idx -> entry
-int engine_download(nmg_engine* h, HostResults& out);
+int engine_download(nmg_engine* h, HostResults& out, bool entries = true);  // entries: the per-entry arrays too
 int engine_download_hist(nmg_engine* h, std::vector<uint32_t>& cells);
 void engine_set_error(nmg_engine* h, const std::string& msg);
 

@@ -996,7 +996,7 @@ __global__ __launch_bounds__(kWG, 1) void local_kernel(LocalParams lp) {
   uint32_t nchunks = 0, nit = 0;
   while (true) {
     if (tid == 0) s_item = atomicAdd(lp.ctl + 1, 1u);
-    __syncthreads();
+    lds_sync();
     const uint32_t it = __builtin_amdgcn_readfirstlane(s_item);
     rt_stamp<TIMING>(rt, 6);
     if (it >= nitems) break;
@@ -1026,7 +1026,7 @@ __global__ __launch_bounds__(kWG, 1) void local_kernel(LocalParams lp) {
     }
     const uint32_t ncell = (pages && pi.pages_lds) ? T * pi.span : 0u;
     for (uint32_t i = tid; i < (ncell + 1) / 2; i += kWG) s_pg[i] = 0;
-    __syncthreads();
+    lds_sync();
     const uint64_t k0key = u64of(__builtin_amdgcn_readfirstlane((uint32_t)s_keys[0]),
                                  __builtin_amdgcn_readfirstlane((uint32_t)(s_keys[0] >> 32)));
     rt_stamp<TIMING>(rt, 7);
@@ -1245,7 +1245,7 @@ __global__ __launch_bounds__(kWG, 1) void local_kernel(LocalParams lp) {
       chunk_load(k + 6, B[0], XB[0]);
       chunk_load(k + 7, B[1], XB[1]);
     }
-    __syncthreads();
+    lds_sync();
     rt_stamp<TIMING>(rt, 8);  // (waiting for the item's slowest wave counts as flush)
     for (uint32_t i = tid; i < nl; i += kWG) lp.cmatch[s_clist[i] & ((1u << kChunkIdBits) - 1)] = s_cm[i];
     // the item's counters to global memory: consecutive lanes, consecutive words
@@ -1276,7 +1276,7 @@ __global__ __launch_bounds__(kWG, 1) void local_kernel(LocalParams lp) {
         atomicAdd(p.hist + uint64_t(th) * p.hist_cells + pi.cb + rel, cnt);
       }
     }
-    __syncthreads();
+    lds_sync();
     rt_stamp<TIMING>(rt, 8);
   }
   if (TIMING && lane == 0) {
