@@ -216,7 +216,10 @@ struct nmg_engine {
   bool route_ok = false;          // partitions built for the nmg_set_objects table
   uint32_t nparts = 0;
   PartInfo* d_parts = nullptr;
-  uint64_t* d_pbounds = nullptr;  // [2^kPartLevels] partition starts, Eytzinger order
+  uint64_t* d_pbounds = nullptr;  // [kMaxParts + 1] partition starts, ascending
+  uint16_t* d_pdir = nullptr;     // [kRouteDir] the route pass's directory over them
+  RSeg rsegs[kRouteSegs];         // its segments
+  uint32_t nrsegs = 0;
   uint64_t* d_pe_keys = nullptr;  // [nparts][kPartSlots]
   uint4* d_pe_nodes = nullptr;    // [nparts][kPartSlots][2]
   uint2* d_pe_info = nullptr;     // [nparts][kPartSlots]
@@ -347,6 +350,7 @@ static void free_lookup(nmg_engine* h) {
 static void free_route_table(nmg_engine* h) {
   (void)hipFree(h->d_parts);
   (void)hipFree(h->d_pbounds);
+  (void)hipFree(h->d_pdir);
   (void)hipFree(h->d_pe_keys);
   (void)hipFree(h->d_pe_nodes);
   (void)hipFree(h->d_pe_info);
@@ -354,6 +358,7 @@ static void free_route_table(nmg_engine* h) {
   h->d_pe_dir = nullptr;
   h->d_parts = nullptr;
   h->d_pbounds = nullptr;
+  h->d_pdir = nullptr;
   h->d_pe_keys = nullptr;
   h->d_pe_nodes = nullptr;
   h->d_pe_info = nullptr;
@@ -746,23 +751,59 @@ static int build_lookup(nmg_engine* h, const uint64_t* keys, const uint32_t* ent
   return NMG_OK;
 }
 
-// In-order walk of the complete Eytzinger tree with 2^levels - 1 nodes:
-// visit(slot, rank) for every slot in sorted order.
-template <class F>
-static void eytz_inorder(uint32_t levels, F visit) {
-  const uint32_t n = 1u << levels;
-  std::vector<uint32_t> stack;
-  uint32_t r = 0, i = 1;
-  while (i < n || !stack.empty()) {
-    while (i < n) {
-      stack.push_back(i);
-      i = 2 * i;
+// The route pass's partition search (route_partition, nmg_route.hip) over
+// the P ascending partition starts b: up to kRouteSegs segments, split at the
+// gaps between consecutive starts that dwarf the median gap (address spaces
+// are clustered: globals, heap, mmap'd regions, the stack), each with
+// directory slots in proportion to its partitions.  Slot j of a segment holds
+// the last partition starting at or before the slot start, and how many
+// starts lie inside the slot (saturated at kDirCntSat: search to the
+// segment's last partition).
+static void route_segments(const uint64_t* b, uint32_t P, RSeg* seg, uint32_t* nseg, std::vector<uint16_t>& dir) {
+  std::vector<uint32_t> cuts{0};  // segment k starts at partition cuts[k]
+  if (P > 1) {
+    std::vector<uint64_t> gaps(P - 1);
+    for (uint32_t q = 0; q + 1 < P; q++) gaps[q] = b[q + 1] - b[q];
+    std::vector<uint64_t> med(gaps);
+    std::nth_element(med.begin(), med.begin() + med.size() / 2, med.end());
+    const uint64_t m = std::max<uint64_t>(med[med.size() / 2], 1);
+    std::vector<uint32_t> idx(P - 1);
+    for (uint32_t q = 0; q + 1 < P; q++) idx[q] = q;
+    std::sort(idx.begin(), idx.end(), [&](uint32_t x, uint32_t y) { return gaps[x] > gaps[y]; });
+    for (uint32_t i = 0; i < idx.size() && cuts.size() < kRouteSegs; i++) {
+      if (gaps[idx[i]] / 64 <= m) break;
+      cuts.push_back(idx[i] + 1);
     }
-    i = stack.back();
-    stack.pop_back();
-    visit(i, r++);
-    i = 2 * i + 1;
+    std::sort(cuts.begin(), cuts.end());
   }
+  const uint32_t S = (uint32_t)cuts.size();
+  dir.assign(kRouteDir, 0);
+  uint32_t used = 0;
+  for (uint32_t k = 0; k < kRouteSegs; k++) {
+    if (k >= S) {
+      seg[k] = RSeg{~0ull, 0, 1, 0, 0};
+      continue;
+    }
+    const uint32_t qa = cuts[k], qb = k + 1 < S ? cuts[k + 1] : P;
+    const uint32_t ns = (uint32_t)((uint64_t)(kRouteDir - S) * (qb - qa) / P) + 1;
+    const uint64_t span = b[qb - 1] - b[qa];
+    uint32_t sh = 0;
+    while (sh < 63 && (span >> sh) >= ns) sh++;
+    seg[k] = RSeg{b[qa], used, ns, sh, qb - 1};
+    uint32_t q = qa;
+    for (uint32_t j = 0; j < ns; j++) {
+      // slot [s0, s1) relative to the segment start
+      const unsigned __int128 s0 = (unsigned __int128)j << sh, s1 = (unsigned __int128)(j + 1) << sh;
+      while (q + 1 < qb && (unsigned __int128)(b[q + 1] - b[qa]) <= s0) q++;
+      uint32_t c = 0;
+      if (j == ns - 1) c = qb - 1 - q;
+      else
+        while (q + 1 + c < qb && (unsigned __int128)(b[q + 1 + c] - b[qa]) < s1) c++;
+      dir[used + j] = (uint16_t)(q | (std::min(c, kDirCntSat) << 11));
+    }
+    used += ns;
+  }
+  *nseg = S;
 }
 
 // Partitions of the partition-first path (nmg_route.h): runs of consecutive
@@ -847,13 +888,15 @@ static int build_partitions(nmg_engine* h, const uint64_t* keys, const uint32_t*
       pdir[(size_t)q * kPartDir + j] = lo | (c << 16);
     }
   }
-  // the route pass's tree: the partitions' first keys
-  std::vector<uint64_t> pb(1u << kPartLevels, ~0ull);
-  eytz_inorder(kPartLevels, [&](uint32_t slot, uint32_t r) {
-    if (r < P) pb[slot] = keys[parts[r].k0];
-  });
+  // the route pass's partition search: the partitions' first keys ascending,
+  // and a directory over them (route_segments)
+  std::vector<uint64_t> pb(kMaxParts + 1, ~0ull);
+  for (uint32_t q = 0; q < P; q++) pb[q] = keys[parts[q].k0];
+  std::vector<uint16_t> rdir;
+  route_segments(pb.data(), P, h->rsegs, &h->nrsegs, rdir);
   HIP_TRY(h, alloc_copy(h, (void**)&h->d_parts, parts.data(), parts.size() * sizeof(PartInfo)));
   HIP_TRY(h, alloc_copy(h, (void**)&h->d_pbounds, pb.data(), pb.size() * 8));
+  HIP_TRY(h, alloc_copy(h, (void**)&h->d_pdir, rdir.data(), rdir.size() * 2));
   HIP_TRY(h, alloc_copy(h, (void**)&h->d_pe_keys, pk.data(), pk.size() * 8));
   HIP_TRY(h, alloc_copy(h, (void**)&h->d_pe_nodes, pn.data(), pn.size() * sizeof(uint4)));
   HIP_TRY(h, alloc_copy(h, (void**)&h->d_pe_info, pinf.data(), pinf.size() * sizeof(uint2)));
@@ -1983,6 +2026,9 @@ static int route_analyze(nmg_engine* h, uint32_t nb, uint32_t grid) {
   memset(&rp, 0, sizeof(rp));
   rp.p = base;
   rp.pbounds = h->d_pbounds;
+  rp.pdir = h->d_pdir;
+  for (uint32_t k = 0; k < kRouteSegs; k++) rp.seg[k] = h->rsegs[k];
+  rp.nseg = h->nrsegs;
   rp.nparts = h->nparts;
   rp.xl = xl;
   rp.seq0 = seq0;

@@ -34,8 +34,23 @@
 namespace nmg {
 
 constexpr uint32_t kChunk = 64;            // compact records per chunk (one wave processes one chunk)
-constexpr uint32_t kPartLevels = 11;       // route pass: Eytzinger tree of partition starts in LDS
+constexpr uint32_t kPartLevels = 11;
 constexpr uint32_t kMaxParts = (1u << kPartLevels) - 1;
+// route pass: a sample's partition from a directory over the partition starts
+// (RSeg): its segment by comparisons with the segment starts (kernel
+// arguments), its slot's entry (u16: last partition starting at or before the
+// slot start | starts inside the slot << 11, 31 = to the segment's end), then
+// a binary search over those few starts (sorted, in LDS)
+constexpr uint32_t kRouteDir = 2048;
+constexpr uint32_t kRouteSegs = 8;
+constexpr uint32_t kDirCntSat = 31;
+struct RSeg {
+  uint64_t start;   // first partition start of the segment (~0: unused)
+  uint32_t base;    // first directory slot
+  uint32_t nslots;  // slots (>= 1)
+  uint32_t shift;   // slot j covers [start + (j << shift), + 2^shift); the last slot: to the next segment
+  uint32_t qlast;   // last partition of the segment
+};
 constexpr uint32_t kPartKeys = 1023;       // local pass: keys per partition in LDS (sorted)
 constexpr uint32_t kPartSlots = 1024;      // per-partition table stride
 constexpr uint32_t kPartDir = 1024;        // directory slots per partition (radix over its key span)
@@ -93,7 +108,10 @@ struct XLayout {
 struct RouteParams {
   Params p;                  // data, sbufs (= descriptors in analysis order, .pad = index), ranges,
                              // global counters, per-buffer counts, and the table for direct attribution
-  const uint64_t* pbounds;   // [2^kPartLevels] partition start keys in Eytzinger order, ~0 padding
+  const uint64_t* pbounds;   // [kMaxParts + 1] partition start keys, ascending, ~0 padding
+  const uint16_t* pdir;      // [kRouteDir] directory slots of every segment
+  RSeg seg[kRouteSegs];      // segments of the partition starts, ascending
+  uint32_t nseg;
   uint32_t nparts;
   XLayout xl;
   uint64_t seq0;             // analysis index of descriptor 0 (seq = seq0 + index)

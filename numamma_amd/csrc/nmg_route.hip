@@ -24,6 +24,43 @@ __device__ __forceinline__ uint32_t eytz_rank(uint32_t idx, uint32_t levels) {
   return (((idx - (1u << d)) * 2 + 1) << (levels - 1 - d)) - 1;
 }
 
+// The partition of addr: the last partition whose first key <= addr (0 below
+// the first key, where ht_lower_key finds no node and nothing matches).  Its
+// segment by comparisons with the (uniform) segment starts, one directory
+// slot, then a binary search over the partition starts inside that slot --
+// usually none or one: one to two dependent LDS reads instead of a search over
+// every start.
+__device__ __forceinline__ uint32_t route_partition(const RouteParams& rp, const uint64_t* s_pb,
+                                                    const uint16_t* s_pdir, uint64_t addr) {
+  if (addr < rp.seg[0].start) return 0;
+  uint64_t s0 = rp.seg[0].start;
+  uint32_t base = rp.seg[0].base, ns = rp.seg[0].nslots, sh = rp.seg[0].shift, ql = rp.seg[0].qlast;
+#pragma unroll
+  for (uint32_t k = 1; k < kRouteSegs; k++) {
+    const bool in = addr >= rp.seg[k].start;  // (unused segments start at ~0)
+    s0 = in ? rp.seg[k].start : s0;
+    base = in ? rp.seg[k].base : base;
+    ns = in ? rp.seg[k].nslots : ns;
+    sh = in ? rp.seg[k].shift : sh;
+    ql = in ? rp.seg[k].qlast : ql;
+  }
+  const uint64_t rel = (addr - s0) >> sh;
+  const uint32_t e = s_pdir[base + (rel < ns ? (uint32_t)rel : ns - 1)];
+  uint32_t q = e & 2047u;
+  const uint32_t c = e >> 11;
+  uint32_t n = (c == kDirCntSat ? ql - q : c) + 1;  // candidates q .. q + n - 1; s_pb[q] <= addr
+  while (n > 1) {
+    const uint32_t half = n >> 1;
+    if (s_pb[q + half] <= addr) {
+      q += half;
+      n -= half;
+    } else {
+      n = half;
+    }
+  }
+  return q;
+}
+
 // ---------------------------------------------------------------------------
 // compact records: (addr, timestamp) + X (see XLayout)
 
@@ -350,7 +387,7 @@ struct Held {
 // permutation, and the write phase gathers through it.
 struct RouteLds {
   uint32_t* hist;     // [P] records of each partition in the batch (rank counters)
-  uint32_t* start;    // [P] first sorted position of each partition's run
+  uint16_t* start;    // [P] first sorted position of each partition's run
   uint32_t* cur;      // [2][kMaxParts + 1] open chunk id << 7 | fill, double-buffered by batch parity
   uint32_t* nb;       // [P] first new chunk of the batch (kNoChunk: pool exhausted)
   uint4* a16;         // [kRouteBatch] staging slot: (addr, timestamp)
@@ -525,8 +562,10 @@ __device__ __forceinline__ RDesc route_desc(const RouteParams& rp, const uint4* 
 
 template <bool TIMING>
 __global__ __launch_bounds__(kWG, 1) void route_kernel(RouteParams rp) {
-  __shared__ uint64_t s_bounds[1u << kPartLevels];
-  __shared__ uint32_t s_hist[kMaxParts + 1], s_start[kMaxParts + 1], s_cur[2][kMaxParts + 1], s_nb[kMaxParts + 1];
+  __shared__ uint64_t s_pb[kMaxParts + 1];
+  __shared__ uint16_t s_pdir[kRouteDir];
+  __shared__ uint32_t s_hist[kMaxParts + 1], s_cur[2][kMaxParts + 1], s_nb[kMaxParts + 1];
+  __shared__ uint16_t s_start[kMaxParts + 1];
   __shared__ uint4 s_desc[kDescLds];
   __shared__ uint4 s_a16[kRouteBatch];
   __shared__ unsigned long long s_x[kRouteBatch];
@@ -543,7 +582,8 @@ __global__ __launch_bounds__(kWG, 1) void route_kernel(RouteParams rp) {
   const uint32_t P = rp.nparts;
   const uint32_t c0 = rp.chunk0[blockIdx.x];
   const uint32_t cap = rp.chunk0[blockIdx.x + 1] - c0;
-  for (uint32_t i = tid; i < (1u << kPartLevels); i += kWG) s_bounds[i] = rp.pbounds[i];
+  for (uint32_t i = tid; i < kMaxParts + 1; i += kWG) s_pb[i] = rp.pbounds[i];
+  for (uint32_t i = tid; i < kRouteDir; i += kWG) s_pdir[i] = rp.pdir[i];
   for (uint32_t i = tid; i < P; i += kWG) {
     s_hist[i] = 0;
     s_cur[0][i] = kChunk;  // no open chunk (full)
@@ -764,20 +804,14 @@ __global__ __launch_bounds__(kWG, 1) void route_kernel(RouteParams rp) {
         gwin = 0;
       }
       rt_stamp<TIMING>(rt, 2);
-      uint32_t node = 0;
-      if (valid) {
-        // partition = the last partition whose first key <= addr; below the
-        // first key nothing can match (ht_lower_key finds no node)
-        const uint32_t i = eytz_descend(s_bounds, kPartLevels, rec.addr);
-        node = i >> (__builtin_ctz(i) + 1);
-      }
-      if (TIMING) (void)__builtin_amdgcn_readfirstlane(__ballot(node != 0));  // (the search ends here)
+      // partition = the last partition whose first key <= addr; below the
+      // first key partition 0, where the lookup finds no node
+      const uint32_t q = valid ? route_partition(rp, s_pb, s_pdir, rec.addr) : 0u;
+      if (TIMING) (void)__builtin_amdgcn_readfirstlane(__ballot(q != 0));  // (the search ends here)
       rt_stamp<TIMING>(rt, 3);
       Held hr;
       hr.q = kNoChunk;
       if (valid) {
-        // (below the first key: partition 0, where the lookup finds no node)
-        const uint32_t q = node ? min(eytz_rank(node, kPartLevels), P - 1) : 0u;
         const uint32_t rk = atomicAdd(&s_hist[q], 1u);
         hr.q = q | (rk << 11);
         hr.a = make_uint4((uint32_t)rec.addr, (uint32_t)(rec.addr >> 32), (uint32_t)rec.ts, (uint32_t)(rec.ts >> 32));

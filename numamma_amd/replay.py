@@ -339,6 +339,11 @@ class SynthConfig:
     wrap_one: bool = False
     seed: int = 1
     sample_seed: Optional[int] = None  # None: continue the table's stream
+    # heap keys in `heap_clusters` runs, each `cluster_gap` bytes above the
+    # previous one (mmap'd arenas far apart: the route pass's directory
+    # segments); 1 = one contiguous heap
+    heap_clusters: int = 1
+    cluster_gap: int = 1 << 40
 
 
 # named configurations from BASELINE.json "configs"
@@ -382,6 +387,8 @@ def make_table(cfg: SynthConfig, rng: np.random.Generator) -> ObjectTable:
     keys[0] = HEAP_BASE
     if K > 1:
         keys[1:] = HEAP_BASE + np.cumsum(stride[:-1], dtype=np.uint64)
+    if cfg.heap_clusters > 1:
+        keys += (np.arange(K, dtype=np.uint64) * np.uint64(cfg.heap_clusters) // np.uint64(K)) * np.uint64(cfg.cluster_gap)
     reused = rng.random(K) < cfg.reuse_frac
     realloc = (rng.random(K) < cfg.realloc_frac) & ~reused
 

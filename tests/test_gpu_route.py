@@ -9,6 +9,7 @@ tests pin the parts the other parity tests do not reach on purpose:
   overflow_kernel's global lookups);
 * analyses that accumulate without a reset (the per-buffer match counts of
   one analysis are summed before the next one reuses the chunk pool);
+* the route pass's partition directory over clustered address spaces;
 * partition shapes: many threads (page cells of a partition too many for
   LDS: global atomics), objects larger than a partition's LDS cells, heavily
   reused addresses (older entries), tiny buffers (more buffers than windows);
@@ -68,6 +69,12 @@ ROUTE_CASES = [
     SynthConfig(nb_samples=300_000, nb_intervals=10_000, reuse_frac=0.5, realloc_frac=0.2, seed=74),
     # tiny buffers: more buffers than windows, windows across many buffers
     SynthConfig(nb_samples=200_000, nb_intervals=5_000, buffer_records=7, seed=75),
+    # 10 heap arenas 1 TiB apart (+ globals, stack): more clusters than the
+    # route directory's 8 segments, so some segments span a gap and their
+    # slots hold many partition starts (saturated slot counts)
+    SynthConfig(nb_samples=400_000, nb_intervals=400_000, size_max=4096, heap_clusters=10, seed=77),
+    # 3 arenas: a segment each, dense slots
+    SynthConfig(nb_samples=300_000, nb_intervals=60_000, heap_clusters=3, cluster_gap=1 << 36, seed=78),
 ]
 
 
