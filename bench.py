@@ -34,6 +34,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 RECORD_BYTES = 40
+COMPACT_BYTES = 16  # partition-first path: compact record per routed sample
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 MIN_TIMED_S = 1.0      # default --steps: enough steps for at least this much timed work
 
@@ -334,10 +335,11 @@ def result_line(args, w, world, steps, ms_per_step, value, attr_ms, total_ms, ph
     routed = rest_ms > 0.0  # the partition-first path ran (tables > 1023 keys)
     kernels = {}
     if routed:
-        # route_kernel reads every 40 B record and writes a 24 B compact record
-        # per sample; the local pass reads the compact records back
-        kernels["route_kernel"] = {"avg_ms": first_ms, "algorithmic_bytes": w.samples * (RECORD_BYTES + 24)}
-        kernels["overflow+count+plan+scatter+local_kernel"] = {"avg_ms": rest_ms, "algorithmic_bytes": w.samples * 24}
+        # route_kernel reads every 40 B record and writes a 16 B compact record
+        # per sample (nmg_route.h XLayout); the local pass reads them back
+        kernels["route_kernel"] = {"avg_ms": first_ms, "algorithmic_bytes": w.samples * (RECORD_BYTES + COMPACT_BYTES)}
+        kernels["overflow+count+plan+scatter+local_kernel"] = {"avg_ms": rest_ms,
+                                                               "algorithmic_bytes": w.samples * COMPACT_BYTES}
     else:
         kernels["attribute_kernel"] = {"avg_ms": first_ms, "algorithmic_bytes": algo}
     for k, v in kernels.items():

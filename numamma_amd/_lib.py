@@ -10,7 +10,9 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libnumamma_gpu.so")
+# (NMG_LIB_PATH: another in-tree build of the same library, for A/B timing
+# of two kernel versions on one box; tools/ab_lib.sh)
+LIB_PATH = os.environ.get("NMG_LIB_PATH") or os.path.join(_HERE, "libnumamma_gpu.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "numamma_gpu.h")
 
 # One HIP runtime per process: torch ships its own libamdhip64.so (same

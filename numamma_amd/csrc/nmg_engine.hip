@@ -219,13 +219,13 @@ struct nmg_engine {
   uint64_t* d_pbounds = nullptr;  // [kMaxParts + 1] partition starts, ascending
   uint16_t* d_pdir = nullptr;     // [kRouteDir] the route pass's directory over them
   RSeg rsegs[kRouteSegs];         // its segments
+  uint64_t route_tbase = 0;       // compact records: timestamps relative to this (XLayout)
   uint32_t nrsegs = 0;
   uint64_t* d_pe_keys = nullptr;  // [nparts][kPartSlots]
   uint4* d_pe_nodes = nullptr;    // [nparts][kPartSlots][2]
   uint2* d_pe_info = nullptr;     // [nparts][kPartSlots]
   uint32_t* d_pe_dir = nullptr;   // [nparts][kPartDir]
   uint4* d_rec16 = nullptr;       // chunk pool: [chunks][kChunk] (addr, ts) and X words
-  unsigned long long* d_recx = nullptr;
   uint32_t* d_cmeta = nullptr;
   unsigned long long* d_cmatch = nullptr;
   uint32_t* d_clist = nullptr;
@@ -368,12 +368,11 @@ static void free_route_table(nmg_engine* h) {
 
 // the per-analysis buffers of the partition-first path
 static void free_route_pool(nmg_engine* h) {
-  for (void* q : {(void*)h->d_rec16, (void*)h->d_recx, (void*)h->d_cmeta, (void*)h->d_cmatch, (void*)h->d_clist,
+  for (void* q : {(void*)h->d_rec16, (void*)h->d_cmeta, (void*)h->d_cmatch, (void*)h->d_clist,
                   (void*)h->d_items, (void*)h->d_chunk0, (void*)h->d_used, (void*)h->d_pcnt, (void*)h->d_pbase,
                   (void*)h->d_ctl, (void*)h->d_ovf16, (void*)h->d_ovfx})
     (void)hipFree(q);
   h->d_rec16 = nullptr;
-  h->d_recx = nullptr;
   h->d_cmeta = nullptr;
   h->d_cmatch = nullptr;
   h->d_clist = nullptr;
@@ -829,6 +828,11 @@ static int build_partitions(nmg_engine* h, const uint64_t* keys, const uint32_t*
     pi.e0 = entry_off[k];
     uint64_t cb = ~0ull, ce = 0;
     while (k < K && k - pi.k0 < kPartKeys) {
+      // a partition's keys span less than 2^(kAddrBits - 1) bytes, so that the
+      // compact records' address field (relative to the partition's first key)
+      // holds every address its objects cover: a run of keys across a wide gap
+      // in the address space (the heap, then the stack) starts a new partition
+      if (k > pi.k0 && keys[k] - keys[pi.k0] >= (1ull << (kAddrBits - 1))) break;
       const uint32_t ea = entry_off[k], eb = entry_off[k + 1];
       if (eb - pi.e0 > kPartEntries) {
         if (k == pi.k0) return NMG_OK;  // one address reused more than kPartEntries times: keep attribute_kernel
@@ -856,6 +860,12 @@ static int build_partitions(nmg_engine* h, const uint64_t* keys, const uint32_t*
     if (parts.size() > kMaxParts) return NMG_OK;  // too many partitions for the route pass's LDS tree
   }
   const uint32_t P = (uint32_t)parts.size();
+  // the compact records' timestamp base: the earliest allocation (a sample
+  // before it can only match objects allocated at time 0, and escapes)
+  h->route_tbase = ~0ull;
+  for (const DevEntry& d : dev)
+    if (d.alloc) h->route_tbase = std::min<uint64_t>(h->route_tbase, d.alloc);
+  if (h->route_tbase == ~0ull) h->route_tbase = 0;
   // per partition: keys ascending with their newest entry's node record and
   // info, and a directory over the key span: slot j starts at first key + (j
   // << dshift) and holds the index of the largest key <= that start and the
@@ -1934,9 +1944,11 @@ static bool route_layout(nmg_engine* h, XLayout& xl) {
   xl.gbits = bits_for(h->descs.size() - 1);
   xl.obits = bits_for((maxlen - 1) / 8);
   xl.tbits = bits_for(h->T - 1);
-  xl.wshift = xl.gbits + xl.obits + xl.tbits + 1 + 14;  // (+ access bit, data_src.mem_lvl)
-  if (xl.wshift > 64 - 12) return false;
-  xl.wesc = (1ull << (64 - xl.wshift)) - 1;
+  const uint32_t loc = xl.gbits + xl.obits + xl.tbits + 1;  // (+ access bit)
+  if (loc > 48 - 8 || xl.gbits > 31 || xl.obits > 31 || xl.tbits > 31) return false;
+  xl.wbits = std::min<uint32_t>(48 - loc, 16);  // (the decode reads at most 16 bits of weight)
+  xl.wesc = (1ull << xl.wbits) - 1;
+  xl.tbase = h->route_tbase;
   return true;
 }
 
@@ -1987,7 +1999,6 @@ static int route_prepare(nmg_engine* h, uint32_t grid, const std::vector<uint32_
     h->route_pending = pending;
     const size_t cap = std::max<size_t>(tot, 1);
     HIP_TRY(h, hipMalloc(&h->d_rec16, cap * kChunk * sizeof(uint4)));
-    HIP_TRY(h, hipMalloc(&h->d_recx, cap * kChunk * 8));
     HIP_TRY(h, hipMalloc(&h->d_cmeta, cap * 4));
     HIP_TRY(h, hipMalloc(&h->d_cmatch, cap * 8));
     HIP_TRY(h, hipMalloc(&h->d_clist, cap * 4));
@@ -2033,7 +2044,6 @@ static int route_analyze(nmg_engine* h, uint32_t nb, uint32_t grid) {
   rp.xl = xl;
   rp.seq0 = seq0;
   rp.rec16 = h->d_rec16;
-  rp.recx = h->d_recx;
   rp.cmeta = h->d_cmeta;
   rp.chunk0 = h->d_chunk0;
   rp.used = h->d_used;
@@ -2067,10 +2077,6 @@ static int route_analyze(nmg_engine* h, uint32_t nb, uint32_t grid) {
   CountParams cp;
   memset(&cp, 0, sizeof(cp));
   cp.sc = sc;
-  cp.p = base;
-  cp.recx = h->d_recx;
-  cp.descs = h->d_sdescs;
-  cp.xl = xl;
   HIP_TRY(h, launch_count(grid, h->stream, cp));
   PlanParams pl;
   pl.pcnt = h->d_pcnt;
@@ -2090,7 +2096,6 @@ static int route_analyze(nmg_engine* h, uint32_t nb, uint32_t grid) {
   lp.pe_info = h->d_pe_info;
   lp.pe_dir = h->d_pe_dir;
   lp.rec16 = h->d_rec16;
-  lp.recx = h->d_recx;
   lp.cmeta = h->d_cmeta;
   lp.clist = h->d_clist;
   lp.items = h->d_items;
@@ -2135,10 +2140,11 @@ static int route_settle(nmg_engine* h) {
   f.used = h->d_used;
   f.cmeta = h->d_cmeta;
   f.cmatch = h->d_cmatch;
-  f.recx = h->d_recx;
+  f.rec16 = h->d_rec16;
   f.bufcnt = h->d_bufcnt;
   f.nb_bufs = (uint32_t)h->bufcnt_stride;
   f.gbits = h->route_xl.gbits;
+  f.gshift = 16 + h->route_xl.wbits;
   HIP_TRY(h, hipSetDevice(h->device));
   HIP_TRY(h, launch_found(h->route_grid, h->stream, f));
   return NMG_OK;

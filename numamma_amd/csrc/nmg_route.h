@@ -9,7 +9,7 @@
 // LDS:
 //   1. route_kernel   streams the buffers in analysis order (the byte cursor of
 //                     __analyze_buffer, mem_sampling.c:815-927), counts the
-//                     SAMPLEs per buffer, and appends a 24 B compact record of
+//                     SAMPLEs per buffer, and appends a 16 B compact record of
 //                     every SAMPLE to a chunk of its partition (partition = a run of
 //                     <= kPartKeys consecutive keys; chunks of kChunk records
 //                     from the workgroup's private pool);
@@ -56,7 +56,7 @@ constexpr uint32_t kPartSlots = 1024;      // per-partition table stride
 constexpr uint32_t kPartDir = 1024;        // directory slots per partition (radix over its key span)
 constexpr uint32_t kPartEntries = 1536;    // entries per partition (LDS object counters)
 constexpr uint32_t kPartCells = 28672;     // u16 page cells per partition: nb_threads x cell span
-constexpr uint32_t kRouteWindows = 3;      // windows per LDS sort batch of the route pass
+constexpr uint32_t kRouteWindows = 4;      // windows per LDS sort batch of the route pass
 constexpr uint32_t kRouteBatch = kRouteWindows * kWG;
 constexpr uint32_t kItemChunks = 1023;     // chunks per work item: < 2^16 records, so u16 page cells
                                            // and the packed object counters cannot overflow
@@ -97,12 +97,20 @@ struct PartInfo {
 };
 static_assert(sizeof(PartInfo) == 48, "PartInfo");
 
-// compact record X word, from bit 0: buffer index g (gbits), byte offset / 8
-// (obits), thread rank (tbits), access type (1), data_src.mem_lvl (14),
-// min(weight, wesc) (the rest, from bit wshift)
+// compact record: 16 B, two u64 words (everything the local pass needs; the
+// global counters were done by the route pass)
+//   lo = addr - partition start (kAddrBits) | (ts - tbase) << kAddrBits (low 24 bits)
+//   hi = (ts - tbase) >> 24 (16 bits) | min(weight, wesc) << 16 (wbits)
+//        | location << (16 + wbits): buffer index g (gbits), byte offset / 8
+//        (obits), thread rank (tbits), access type (1)
+// A record whose address, timestamp or weight does not fit carries wesc: the
+// local pass re-reads all three from the raw record (rare).
+constexpr uint32_t kAddrBits = 40;
+constexpr uint32_t kTsBits = 40;
 struct XLayout {
-  uint32_t gbits, obits, tbits, wshift;
-  uint64_t wesc;  // 2^(64 - wshift) - 1: the weight is re-read from the record
+  uint32_t gbits, obits, tbits, wbits;  // wbits = min(48 - (gbits + obits + tbits + 1), 16) >= 8
+  uint64_t wesc;   // 2^wbits - 1
+  uint64_t tbase;  // smallest non-zero alloc_date of the table (earlier samples escape)
 };
 
 struct RouteParams {
@@ -115,13 +123,12 @@ struct RouteParams {
   uint32_t nparts;
   XLayout xl;
   uint64_t seq0;             // analysis index of descriptor 0 (seq = seq0 + index)
-  uint4* rec16;              // [chunks][kChunk] (addr, timestamp)
-  unsigned long long* recx;  // [chunks][kChunk] X words
+  uint4* rec16;              // [chunks][kChunk] compact records
   uint32_t* cmeta;           // [chunks] partition | fill << 24
   const uint32_t* chunk0;    // [grid + 1] private chunk range of each workgroup
   uint32_t* used;            // [grid] chunks taken
   uint4* ovf16;              // overflow list: records that found no chunk (overflow_kernel)
-  unsigned long long* ovfx;
+  unsigned long long* ovfx;  // and their partition's start
   uint32_t* ovf_cnt;         // (= ctl[2]; zeroed by plan_kernel after overflow_kernel read it)
   uint32_t ovf_cap;
 };
@@ -152,7 +159,6 @@ struct LocalParams {
   const uint2* pe_info;      // [nparts][kPartSlots] (cell - cb or ~0, entry - e0 | older entries << 31)
   const uint32_t* pe_dir;    // [nparts][kPartDir] largest key index <= slot start | keys inside the slot << 16
   const uint4* rec16;
-  const unsigned long long* recx;
   const uint32_t* cmeta;
   const uint32_t* clist;     // chunk id | fill << kChunkIdBits, grouped by partition
   const uint4* items;
@@ -169,21 +175,17 @@ struct FoundParams {
   const uint32_t* used;
   const uint32_t* cmeta;
   const unsigned long long* cmatch;
-  const unsigned long long* recx;
+  const uint4* rec16;
   uint32_t* bufcnt;          // [2][nb_bufs]
-  uint32_t nb_bufs, gbits;
+  uint32_t nb_bufs, gbits, gshift;
 };
 
 hipError_t launch_route(uint32_t grid, hipStream_t s, const RouteParams& r);
 hipError_t launch_overflow(hipStream_t s, const RouteParams& r);
 // count_kernel: per route workgroup, chunks per partition (pcnt, from the
-// chunks' tags) and update_counters of every routed SAMPLE from its X word
+// chunks' tags)
 struct CountParams {
   ScatterParams sc;
-  Params p;                  // global counters, data (escaped weights), flags
-  const unsigned long long* recx;
-  const BufDesc* descs;      // analysis order (escaped weights are re-read from the record)
-  XLayout xl;
 };
 hipError_t launch_count(uint32_t grid, hipStream_t s, const CountParams& r);
 hipError_t launch_plan(hipStream_t s, const PlanParams& r);

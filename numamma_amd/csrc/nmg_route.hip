@@ -24,15 +24,14 @@ __device__ __forceinline__ uint32_t eytz_rank(uint32_t idx, uint32_t levels) {
   return (((idx - (1u << d)) * 2 + 1) << (levels - 1 - d)) - 1;
 }
 
-// The partition of addr: the last partition whose first key <= addr (0 below
-// the first key, where ht_lower_key finds no node and nothing matches).  Its
+// The partition of addr >= the first key: the last partition whose first key
+// <= addr.  Its
 // segment by comparisons with the (uniform) segment starts, one directory
 // slot, then a binary search over the partition starts inside that slot --
 // usually none or one: one to two dependent LDS reads instead of a search over
 // every start.
 __device__ __forceinline__ uint32_t route_partition(const RouteParams& rp, const uint64_t* s_pb,
                                                     const uint16_t* s_pdir, uint64_t addr) {
-  if (addr < rp.seg[0].start) return 0;
   uint64_t s0 = rp.seg[0].start;
   uint32_t base = rp.seg[0].base, ns = rp.seg[0].nslots, sh = rp.seg[0].shift, ql = rp.seg[0].qlast;
 #pragma unroll
@@ -62,36 +61,56 @@ __device__ __forceinline__ uint32_t route_partition(const RouteParams& rp, const
 }
 
 // ---------------------------------------------------------------------------
-// compact records: (addr, timestamp) + X (see XLayout)
+// compact records (16 B, see XLayout)
 
 struct XRec {
-  uint32_t g, off, th, acc, lvl;
-  uint64_t wq;
+  uint64_t addr, ts, w;
+  uint32_t g, off, th, acc;
+  bool esc;  // addr, ts and w are still to be re-read from the raw record (x_resolve)
 };
 
-__device__ __forceinline__ uint64_t x_encode(const XLayout& xl, uint32_t g, uint32_t off, uint32_t th, uint32_t acc,
-                                             uint32_t lvl, uint64_t w) {
-  const uint64_t wq = w < xl.wesc ? w : xl.wesc;
-  return uint64_t(g) | (uint64_t(off >> 3) << xl.gbits) | (uint64_t(th) << (xl.gbits + xl.obits)) |
-         (uint64_t(acc) << (xl.wshift - 15)) | (uint64_t(lvl) << (xl.wshift - 14)) | (wq << xl.wshift);
+// the record of a SAMPLE routed to the partition starting at pb (addr >= pb)
+__device__ __forceinline__ uint4 x_encode(const XLayout& xl, uint64_t pb, uint64_t addr, uint64_t ts, uint64_t w,
+                                          uint32_t g, uint32_t off, uint32_t th, uint32_t acc) {
+  const uint64_t ar = addr - pb, tr = ts - xl.tbase;
+  const bool fit = (ar >> kAddrBits) == 0 && ts >= xl.tbase && (tr >> kTsBits) == 0 && w < xl.wesc;
+  const uint64_t a = fit ? ar : 0ull, t = fit ? tr : 0ull, wq = fit ? w : xl.wesc;
+  const uint64_t loc = uint64_t(g) | (uint64_t(off >> 3) << xl.gbits) | (uint64_t(th) << (xl.gbits + xl.obits)) |
+                       (uint64_t(acc) << (xl.gbits + xl.obits + xl.tbits));
+  const uint64_t lo = a | (t << kAddrBits);
+  const uint64_t hi = (t >> (64 - kAddrBits)) | (wq << 16) | (loc << (16 + xl.wbits));
+  return make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
 }
 
-__device__ __forceinline__ XRec x_decode(const XLayout& xl, uint64_t x) {
+// bits [start, start + width) of the 64-bit value hi:lo, width <= 32 (32-bit
+// funnel shifts: the local pass decodes two records per lane per step)
+__device__ __forceinline__ uint32_t bits64(uint32_t lo, uint32_t hi, uint32_t start, uint32_t mask) {
+  return (start < 32 ? __builtin_amdgcn_alignbit(hi, lo, start) : hi >> (start - 32)) & mask;
+}
+
+__device__ __forceinline__ XRec x_decode(const XLayout& xl, uint64_t pb, uint4 v) {
   XRec r;
-  r.g = (uint32_t)(x & ((1ull << xl.gbits) - 1));
-  r.off = (uint32_t)((x >> xl.gbits) & ((1ull << xl.obits) - 1)) << 3;
-  r.th = (uint32_t)((x >> (xl.gbits + xl.obits)) & ((1ull << xl.tbits) - 1));
-  r.acc = (uint32_t)((x >> (xl.wshift - 15)) & 1);
-  r.lvl = (uint32_t)((x >> (xl.wshift - 14)) & 0x3fff);
-  r.wq = x >> xl.wshift;
+  r.addr = pb + u64of(v.x, v.y & 0xffu);
+  r.ts = xl.tbase + u64of(__builtin_amdgcn_alignbit(v.z, v.y, 8), (v.z >> 8) & 0xffu);
+  const uint32_t wesc = (uint32_t)xl.wesc;
+  r.w = __builtin_amdgcn_alignbit(v.w, v.z, 16) & wesc;
+  r.esc = r.w == wesc;
+  // the location from bit 16 + wbits of hi = v.w:v.z
+  const uint32_t l0 = 16 + xl.wbits;
+  r.g = bits64(v.z, v.w, l0, (1u << xl.gbits) - 1);
+  r.off = bits64(v.z, v.w, l0 + xl.gbits, (1u << xl.obits) - 1) << 3;
+  r.th = bits64(v.z, v.w, l0 + xl.gbits + xl.obits, (1u << xl.tbits) - 1);
+  r.acc = bits64(v.z, v.w, l0 + xl.gbits + xl.obits + xl.tbits, 1u);
   return r;
 }
 
-// the record's weight: the X field, or (escape) the record itself
-__device__ __forceinline__ uint64_t x_weight(const XLayout& xl, const XRec& r, const uint8_t* data,
-                                             const BufDesc* descs) {
-  if (r.wq != xl.wesc) return r.wq;
-  return *reinterpret_cast<const uint64_t*>(data + descs[r.g].offset + r.off + 24);  // struct mem_sample.weight
+// an escaped record's address, timestamp and weight from the raw record
+// (struct mem_sample after the 8 B header: timestamp, addr, weight)
+__device__ __forceinline__ void x_resolve(XRec& r, const uint8_t* data, const BufDesc* descs) {
+  const uint64_t* q = reinterpret_cast<const uint64_t*>(data + descs[r.g].offset + r.off);
+  r.ts = q[1];
+  r.addr = q[2];
+  r.w = q[3];
 }
 
 // ---------------------------------------------------------------------------
@@ -376,8 +395,7 @@ __device__ __forceinline__ void rt_stamp(RTimer& t, int i) {
 // race with the delayed write phase of the previous batch, which reads the
 // staging area before that barrier)
 struct Held {
-  uint4 a;         // addr, timestamp
-  uint64_t x;      // X word
+  uint4 a;         // compact record
   uint32_t q;      // partition | batch rank << 11, or kNoChunk (no record)
 };
 
@@ -390,8 +408,8 @@ struct RouteLds {
   uint16_t* start;    // [P] first sorted position of each partition's run
   uint32_t* cur;      // [2][kMaxParts + 1] open chunk id << 7 | fill, double-buffered by batch parity
   uint32_t* nb;       // [P] first new chunk of the batch (kNoChunk: pool exhausted)
-  uint4* a16;         // [kRouteBatch] staging slot: (addr, timestamp)
-  unsigned long long* x;  // [kRouteBatch] X word
+  uint4* a16;         // [kRouteBatch] staging slot: compact record
+  const uint64_t* pb; // [P] partition starts (the overflow list keeps a record's)
   uint32_t* uq;       // [kRouteBatch] partition | rank << 11, kNoChunk = empty slot
   uint16_t* perm;     // [kRouteBatch] sorted position -> staging slot
   uint32_t* wsum;     // [16] per-wave scan totals
@@ -401,10 +419,7 @@ struct RouteLds {
 __device__ __forceinline__ void route_stage(const RouteLds& L, const Held& h, uint32_t b, int tid) {
   const uint32_t slot = b * kWG + (uint32_t)tid;
   L.uq[slot] = h.q;
-  if (h.q != kNoChunk) {
-    L.a16[slot] = h.a;
-    L.x[slot] = h.x;
-  }
+  if (h.q != kNoChunk) L.a16[slot] = h.a;
 }
 
 // Sort batch `batch` (windows [0, nwin) staged) by partition -- the
@@ -501,7 +516,6 @@ __device__ __forceinline__ void route_write_batch(RTimer& rt, const RouteParams&
     const uint32_t src = L.perm[j];
     const uint32_t q = L.uq[src] & 2047u;
     const uint4 a = L.a16[src];
-    const uint64_t x = L.x[src];
     const uint32_t cur = cur_in[q];
     const uint32_t pos = (cur & 127u) + (j - L.start[q]);
     uint32_t chunk, slot;
@@ -514,9 +528,9 @@ __device__ __forceinline__ void route_write_batch(RTimer& rt, const RouteParams&
         const uint32_t o = atomicAdd(rp.ovf_cnt, 1u);
         if (o < rp.ovf_cap) {
           rp.ovf16[o] = a;
-          rp.ovfx[o] = x;
+          rp.ovfx[o] = L.pb[q];
         } else {  // (only SAMPLE records shorter than 40 B get here: NMG_F_SINGLE_PASS handles any number)
-          const XRec xr = x_decode(rp.xl, x);
+          const XRec xr = x_decode(rp.xl, 0, a);
           set_error(p, rp.seq0 + xr.g, xr.off, kErrRouteOverflow);
         }
         continue;
@@ -527,7 +541,6 @@ __device__ __forceinline__ void route_write_batch(RTimer& rt, const RouteParams&
     if (p.flags & kDbgRouteNoWrite) continue;
     const uint64_t k = uint64_t(chunk) * kChunk + slot;
     rp.rec16[k] = a;
-    rp.recx[k] = x;
   }
   rt_stamp<TIMING>(rt, 7);
 }
@@ -568,7 +581,6 @@ __global__ __launch_bounds__(kWG, 1) void route_kernel(RouteParams rp) {
   __shared__ uint16_t s_start[kMaxParts + 1];
   __shared__ uint4 s_desc[kDescLds];
   __shared__ uint4 s_a16[kRouteBatch];
-  __shared__ unsigned long long s_x[kRouteBatch];
   __shared__ uint32_t s_uq[kRouteBatch];
   __shared__ uint16_t s_perm[kRouteBatch];
   __shared__ uint32_t s_list[kMaxList];
@@ -593,7 +605,7 @@ __global__ __launch_bounds__(kWG, 1) void route_kernel(RouteParams rp) {
     const BufDesc d = p.sbufs[i];
     s_desc[i - r0] = make_uint4((uint32_t)d.offset, (uint32_t)(d.offset >> 32), d.len, d.thread_rank | (d.access << 16));
   }
-  const RouteLds L{s_hist, s_start, &s_cur[0][0], s_nb, s_a16, s_x, s_uq, s_perm, s_wsum, s_misc};
+  const RouteLds L{s_hist, s_start, &s_cur[0][0], s_nb, s_a16, s_pb, s_uq, s_perm, s_wsum, s_misc};
   if (tid < 3) s_flags[tid] = 0;
   if (tid == 0) {
     s_misc[1] = 0;
@@ -804,20 +816,23 @@ __global__ __launch_bounds__(kWG, 1) void route_kernel(RouteParams rp) {
         gwin = 0;
       }
       rt_stamp<TIMING>(rt, 2);
-      // partition = the last partition whose first key <= addr; below the
-      // first key partition 0, where the lookup finds no node
-      const uint32_t q = valid ? route_partition(rp, s_pb, s_pdir, rec.addr) : 0u;
-      if (TIMING) (void)__builtin_amdgcn_readfirstlane(__ballot(q != 0));  // (the search ends here)
+      // partition = the last partition whose first key <= addr.  Below the
+      // first key ht_lower_key finds no node and nothing can match: such a
+      // sample has been counted (global and per-buffer counters) and goes no
+      // further.
+      const bool routed = valid && rec.addr >= rp.seg[0].start;
+      const uint32_t q = routed ? route_partition(rp, s_pb, s_pdir, rec.addr) : 0u;
+      const uint64_t pbq = routed ? s_pb[q] : 0ull;
+      if (TIMING) (void)__builtin_amdgcn_readfirstlane(__ballot(pbq != 0));  // (the search ends here)
       rt_stamp<TIMING>(rt, 3);
       Held hr;
       hr.q = kNoChunk;
-      if (valid) {
+      if (routed) {
         const uint32_t rk = atomicAdd(&s_hist[q], 1u);
         hr.q = q | (rk << 11);
-        hr.a = make_uint4((uint32_t)rec.addr, (uint32_t)(rec.addr >> 32), (uint32_t)rec.ts, (uint32_t)(rec.ts >> 32));
         const uint32_t g = rin1 ? d1.pad : d0.pad;
         const uint32_t th = rin1 ? d1.thread_rank() : d0.thread_rank();
-        hr.x = x_encode(rp.xl, g, roff, th, acc_l, uint32_t(rec.dsrc >> 5) & 0x3fff /* data_src.mem_lvl */, rec.w);
+        hr.a = x_encode(rp.xl, pbq, rec.addr, rec.ts, rec.w, g, roff, th, acc_l);
       }
       {
         // per-buffer SAMPLE tallies (mem_sampling.c:921-926): lanes of this
@@ -901,10 +916,9 @@ __global__ __launch_bounds__(kWG, 1) void route_kernel(RouteParams rp) {
 __global__ __launch_bounds__(256) void overflow_kernel(RouteParams rp) {
   const uint32_t n = min(*rp.ovf_cnt, rp.ovf_cap);
   for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
-    const uint4 a = rp.ovf16[i];
-    const XRec xr = x_decode(rp.xl, rp.ovfx[i]);
-    direct_attribute(rp.p, u64of(a.x, a.y), u64of(a.z, a.w), x_weight(rp.xl, xr, rp.p.data, rp.p.sbufs), xr.th,
-                     xr.acc, xr.lvl, rp.seq0 + xr.g, xr.off, xr.g);
+    XRec xr = x_decode(rp.xl, rp.ovfx[i], rp.ovf16[i]);
+    if (xr.esc) x_resolve(xr, rp.p.data, rp.p.sbufs);
+    direct_attribute(rp.p, xr.addr, xr.ts, xr.w, xr.th, xr.acc, 0, rp.seq0 + xr.g, xr.off, xr.g);
   }
 }
 
@@ -1078,14 +1092,12 @@ __global__ __launch_bounds__(kWG, 1) void local_kernel(LocalParams lp) {
     constexpr uint32_t kStride = kWG / 64;
     const uint32_t nl = item.z - item.y;
     const uint32_t nmine = nl > (uint32_t)wave ? (nl - (uint32_t)wave + kStride - 1) / kStride : 0u;
-    auto chunk_load = [&](uint32_t k, uint4& a, uint64_t& x) {  // this wave's k-th chunk (any k: no branch)
+    auto chunk_load = [&](uint32_t k, uint4& a) {  // this wave's k-th chunk (any k: no branch)
       const uint32_t e = k < nmine ? s_clist[(uint32_t)wave + k * kStride] : 0u;
-      const uint64_t i = uint64_t(e & ((1u << kChunkIdBits) - 1)) * kChunk + lane;
-      a = lp.rec16[i];
-      x = lp.recx[i];
+      a = lp.rec16[uint64_t(e & ((1u << kChunkIdBits) - 1)) * kChunk + lane];
     };
     // chunks k and k + 1 of this wave (k + 1 past the last: no valid lane)
-    auto process2 = [&](uint32_t k, const uint4 (&a16)[2], const uint64_t (&xw)[2]) {
+    auto process2 = [&](uint32_t k, const uint4 (&a16)[2]) {
       uint32_t li[2];
       bool valid[2];
       uint64_t addr[2], ts[2], w[2];
@@ -1096,35 +1108,35 @@ __global__ __launch_bounds__(kWG, 1) void local_kernel(LocalParams lp) {
         const uint32_t fill = k + j < nmine ? s_clist[li[j]] >> kChunkIdBits : 0u;
         valid[j] = (uint32_t)lane < fill;
       }
-      if (TIMING) {  // (timing: these chunks' loads count as wait; the next two chunks' four loads are younger)
-        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      if (TIMING) {  // (timing: these chunks' loads count as wait; the next two chunks' two loads are younger)
+        asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
         nchunks += 2;
       }
       rt_stamp<TIMING>(rt, 0);
-#pragma unroll
-      for (int j = 0; j < 2; j++) {
-        addr[j] = u64of(a16[j].x, a16[j].y);
-        ts[j] = u64of(a16[j].z, a16[j].w);
-      }
       if (p.flags & kDbgLocalNoWork) {  // (ablation) loads only
 #pragma unroll
         for (int j = 0; j < 2; j++)
-          if (lane == 0 && k + j < nmine) s_cm[li[j]] = addr[j] ^ ts[j] ^ xw[j];
+          if (lane == 0 && k + j < nmine) s_cm[li[j]] = a16[j].x ^ a16[j].y ^ a16[j].z ^ a16[j].w;
         return;
       }
-      // (update_counters of every routed SAMPLE: count_kernel)
+      // (update_counters of every routed SAMPLE: the route pass)
       bool esc = false;
 #pragma unroll
       for (int j = 0; j < 2; j++) {
-        xr[j] = x_decode(lp.xl, xw[j]);
-        w[j] = valid[j] ? xr[j].wq : 0ull;
-        esc |= valid[j] && xr[j].wq == lp.xl.wesc;
+        xr[j] = x_decode(lp.xl, k0key, a16[j]);
+        esc |= valid[j] && xr[j].esc;
       }
-      if (__ballot(esc)) {  // (rare) escaped weights: re-read from the record
+      if (__ballot(esc)) {  // (rare) escaped records: address, timestamp and weight from the record
 #pragma unroll
         for (int j = 0; j < 2; j++)
-          if (valid[j] && xr[j].wq == lp.xl.wesc) w[j] = x_weight(lp.xl, xr[j], p.data, lp.descs);
+          if (valid[j] && xr[j].esc) x_resolve(xr[j], p.data, lp.descs);
         vm_drain();
+      }
+#pragma unroll
+      for (int j = 0; j < 2; j++) {
+        addr[j] = xr[j].addr;
+        ts[j] = xr[j].ts;
+        w[j] = valid[j] ? xr[j].w : 0ull;
       }
       rt_stamp<TIMING>(rt, 1);
       // lower bound among the partition's keys (ht_lower_key, tools/hash.c:63-77):
@@ -1266,18 +1278,17 @@ __global__ __launch_bounds__(kWG, 1) void local_kernel(LocalParams lp) {
       rt_stamp<TIMING>(rt, 5);
     };
     uint4 A[2], B[2];
-    uint64_t XA[2], XB[2];
-    chunk_load(0, A[0], XA[0]);
-    chunk_load(1, A[1], XA[1]);
-    chunk_load(2, B[0], XB[0]);
-    chunk_load(3, B[1], XB[1]);
+    chunk_load(0, A[0]);
+    chunk_load(1, A[1]);
+    chunk_load(2, B[0]);
+    chunk_load(3, B[1]);
     for (uint32_t k = 0; k < nmine; k += 4) {
-      process2(k, A, XA);
-      chunk_load(k + 4, A[0], XA[0]);
-      chunk_load(k + 5, A[1], XA[1]);
-      if (k + 2 < nmine) process2(k + 2, B, XB);
-      chunk_load(k + 6, B[0], XB[0]);
-      chunk_load(k + 7, B[1], XB[1]);
+      process2(k, A);
+      chunk_load(k + 4, A[0]);
+      chunk_load(k + 5, A[1]);
+      if (k + 2 < nmine) process2(k + 2, B);
+      chunk_load(k + 6, B[0]);
+      chunk_load(k + 7, B[1]);
     }
     lds_sync();
     rt_stamp<TIMING>(rt, 8);  // (waiting for the item's slowest wave counts as flush)
@@ -1343,7 +1354,7 @@ __global__ __launch_bounds__(kWG) void found_kernel(FoundParams r) {
     for (int u = 0; u < kU; u++) {
       const uint64_t kk = k + u * kWG;
       bits[u] = kk < k1 ? r.cmatch[kk / kChunk] : 0ull;
-      xw[u] = ((bits[u] >> lane) & 1) ? r.recx[kk] : 0ull;
+      xw[u] = ((bits[u] >> lane) & 1) ? reinterpret_cast<const uint64_t*>(r.rec16)[2 * kk + 1] >> r.gshift : 0ull;
     }
 #pragma unroll
     for (int u = 0; u < kU; u++) {
