@@ -230,6 +230,22 @@ int nmg_submit_buffers(nmg_engine *h, uint32_t n, const void *const *bytes, cons
                        const uint32_t *thread_ranks, const uint32_t *access_types);
 
 /*
+ * Host memory the kernels read in place: [ptr, ptr + bytes) is pinned and
+ * mapped for the device (hipHostRegister) once -- e.g. a thread's mmap'd
+ * perf ring (numap; the ring nmg_submit_ring reads at every alarm,
+ * mem_sampling.c:675-738).  A buffer later given to nmg_submit_buffer(s) or
+ * nmg_submit_ring (unwrapped segment) that lies inside such a range and
+ * starts 16-byte aligned is not copied: nmg_analyze's kernels read it over
+ * PCIe, so it must stay unchanged until nmg_synchronize.  Batch path of a
+ * single-GPU engine without the dump modes only (streaming, dump modes and
+ * multi-GPU handles copy as before).  Ranges must not overlap.
+ * nmg_unregister_host takes the ptr given at registration; buffers inside
+ * the range must have been dropped (nmg_clear_buffers) first.
+ */
+int nmg_register_host(nmg_engine *h, void *ptr, uint64_t bytes);
+int nmg_unregister_host(nmg_engine *h, void *ptr);
+
+/*
  * Streaming (BASELINE configs[4]; the online branch of __process_samples,
  * mem_sampling.c:953-957, fed at each alarm, :130-177): buffers submitted
  * after nmg_stream_begin are uploaded and analysed in chunks of about

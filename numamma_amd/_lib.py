@@ -157,6 +157,8 @@ _SIGS = {
     "nmg_submit_ring": (C.c_int, [H, P, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32]),
     "nmg_submit_buffer": (C.c_int, [H, P, C.c_uint64, C.c_uint32, C.c_uint32]),
     "nmg_submit_buffers": (C.c_int, [H, C.c_uint32, C.POINTER(C.c_void_p), u64p, u32p, u32p]),
+    "nmg_register_host": (C.c_int, [H, C.c_void_p, C.c_uint64]),
+    "nmg_unregister_host": (C.c_int, [H, C.c_void_p]),
     "nmg_stream_begin": (C.c_int, [H, C.c_uint64, C.c_uint32]),
     "nmg_stream_end": (C.c_int, [H]),
     "nmg_replay_open": (C.c_int, [C.POINTER(C.c_void_p), C.c_char_p, C.c_uint32, u64p, u32p, C.c_uint32,

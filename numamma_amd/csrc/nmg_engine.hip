@@ -110,6 +110,29 @@ struct nmg_engine {
 
   // object table
   bool have_table = false;
+  // results epoch: bumped by every call that can change a counter; the page
+  // cells counted by nmg_count_page_cells stay on the device (cells_*) until
+  // nmg_get_page_cells of the same epoch copies them out
+  uint64_t epoch = 1, cells_epoch = 0;
+  // host memory registered with nmg_register_host (device-visible, pinned):
+  // a submitted buffer inside it is read by the kernels in place over PCIe
+  // (zc_dev[i] = its device address, 0 = staged)
+  struct HostReg {
+    uintptr_t lo, hi;  // the caller's range
+    uint64_t dev;      // device address of lo
+    void* pages;       // the registered whole pages around it
+  };
+  std::vector<HostReg> hostregs;
+  std::vector<uint64_t> zc_dev;
+  int64_t cells_n = 0;
+  void* d_cells_rows = nullptr;  // uint4 [cells_n] dense rows (sparse rows: cells_sparse)
+  size_t cells_rows_cap = 0;
+  struct SparseRows {
+    uint64_t off;  // first row
+    uint32_t e;
+    std::vector<std::pair<uint64_t, uint32_t>> cells;  // ((thread << 32 | page), count)
+  };
+  std::vector<SparseRows> cells_sparse;
   uint32_t K = 0, E = 0;
   uint64_t* d_keys = nullptr;
   DevEntry* d_nodes = nullptr;
@@ -542,6 +565,8 @@ extern "C" void nmg_destroy(nmg_engine* h) {
   free_table(h);
   free_counters(h);
   free_route_pool(h);
+  for (const auto& r : h->hostregs) (void)hipHostUnregister(r.pages);
+  (void)hipFree(h->d_cells_rows);
   (void)hipFree(h->d_arena);
   (void)hipFree(h->d_descs);
   (void)hipFree(h->d_bufcnt);
@@ -575,6 +600,7 @@ extern "C" void nmg_destroy(nmg_engine* h) {
 static int multi_finish(nmg_engine* h);
 
 extern "C" int nmg_reset_counters(nmg_engine* h) {
+  if (h) h->epoch++;
   if (!h) return NMG_ERR_INVALID;
   if (!h->have_table) return fail(h, NMG_ERR_STATE, "nmg_reset_counters before nmg_set_objects");
   if (h->multi_pending) {  // the merges in flight belong to the counters being reset
@@ -919,6 +945,7 @@ static int build_partitions(nmg_engine* h, const uint64_t* keys, const uint32_t*
 
 extern "C" int nmg_set_objects(nmg_engine* h, const uint64_t* keys, const uint32_t* entry_off,
                                uint32_t nb_keys, const nmg_object* entries, uint32_t nb_entries) {
+  if (h) h->epoch++;
   Range range("nmg_set_objects");
   if (!h || (nb_keys && (!keys || !entry_off)) || (nb_entries && !entries))
     return NMG_ERR_INVALID;
@@ -1163,6 +1190,7 @@ static int grow_entries(nmg_engine* h, uint32_t newE, const uint32_t* ids, const
 // lists it, in the order of the latest table that lists every entry.
 extern "C" int nmg_update_objects(nmg_engine* h, const uint64_t* keys, const uint32_t* entry_off,
                                   uint32_t nb_keys, const uint32_t* entry_ids, const nmg_object* objects) {
+  if (h) h->epoch++;
   Range range("nmg_update_objects");
   if (!h || (nb_keys && (!keys || !entry_off || !entry_ids || !objects))) return NMG_ERR_INVALID;
   if (!h->have_table) return fail(h, NMG_ERR_STATE, "nmg_update_objects before nmg_set_objects");
@@ -1270,6 +1298,7 @@ static int stage_reserve(nmg_engine* h, size_t need) {
 }
 
 static int append_desc(nmg_engine* h, uint64_t len, uint32_t thread_rank, uint32_t access) {
+  if (!h->zc_dev.empty()) h->zc_dev.push_back(0);
   BufDesc d;
   d.offset = h->stage_len;
   d.len = (uint32_t)len;
@@ -1281,6 +1310,40 @@ static int append_desc(nmg_engine* h, uint64_t len, uint32_t thread_rank, uint32
   h->buf_bytes.push_back(len);
   h->stage_len = (h->stage_len + len + 15) & ~size_t(15);
   h->staged_dirty = true;
+  h->descs_dirty = true;
+  h->multi_staged = false;
+  return NMG_OK;
+}
+
+// The device address of [p, p + len) when it lies in memory registered with
+// nmg_register_host and starts 16-byte aligned (the kernels' record loads);
+// 0 otherwise.  Only for the batch path of a single-GPU engine without the
+// dump modes (their per-record arrays are indexed by staging offsets).
+static uint64_t zero_copy_dev(nmg_engine* h, const void* p, uint64_t len) {
+  if (h->hostregs.empty() || h->streaming || h->multi || (h->flags & NMG_F_SAMPLE_MATCHES)) return 0;
+  const uintptr_t a = (uintptr_t)p;
+  for (const auto& r : h->hostregs)
+    if (a >= r.lo && a + len <= r.hi) {
+      const uint64_t dev = r.dev + (a - r.lo);
+      return (dev & 15) ? 0 : dev;
+    }
+  return 0;
+}
+
+// a buffer read in place (zero_copy_dev): its offset is fixed up against the
+// arena base at upload (upload_buffers)
+static int append_desc_zc(nmg_engine* h, uint64_t dev, uint64_t len, uint32_t thread_rank, uint32_t access) {
+  if (h->zc_dev.size() < h->descs.size()) h->zc_dev.resize(h->descs.size(), 0);
+  h->zc_dev.push_back(dev);
+  BufDesc d;
+  d.offset = 0;
+  d.len = (uint32_t)len;
+  d.thread_rank = thread_rank;
+  d.access = access;
+  d.pad = 0;
+  d.seq = h->descs.size();
+  h->descs.push_back(d);
+  h->buf_bytes.push_back(len);
   h->descs_dirty = true;
   h->multi_staged = false;
   return NMG_OK;
@@ -1315,12 +1378,49 @@ static int route_prepare(nmg_engine* h, uint32_t grid, const std::vector<uint32_
 static int route_analyze(nmg_engine* h, uint32_t nb, uint32_t grid);
 static int route_settle(nmg_engine* h);
 
+extern "C" int nmg_register_host(nmg_engine* h, void* ptr, uint64_t bytes) {
+  if (!h || !ptr || !bytes) return NMG_ERR_INVALID;
+  if (h->multi) return fail(h, NMG_ERR_STATE, "nmg_register_host: single-GPU engines only");
+  const uintptr_t a = (uintptr_t)ptr;
+  for (const auto& r : h->hostregs)  // (pages: two ranges must not share one)
+    if ((a & ~uintptr_t(4095)) < ((r.hi + 4095) & ~uintptr_t(4095)) && ((uintptr_t)r.pages) < a + bytes)
+      return fail(h, NMG_ERR_INVALID, "nmg_register_host: overlaps (shares a page with) a registered range");
+  // whole pages (every page holding a byte of the range is mapped)
+  const uintptr_t pg = 4096, p0 = a & ~(pg - 1), p1 = (a + bytes + pg - 1) & ~(pg - 1);
+  HIP_TRY(h, hipSetDevice(h->device));
+  HIP_TRY(h, hipHostRegister((void*)p0, p1 - p0, hipHostRegisterMapped));
+  void* dev = nullptr;
+  if (hipHostGetDevicePointer(&dev, (void*)p0, 0) != hipSuccess || !dev) {
+    (void)hipHostUnregister((void*)p0);
+    return fail(h, NMG_ERR_HIP, "nmg_register_host: no device address for the range");
+  }
+  h->hostregs.push_back({a, a + bytes, (uint64_t)(uintptr_t)dev + (a - p0), (void*)p0});
+  return NMG_OK;
+}
+
+extern "C" int nmg_unregister_host(nmg_engine* h, void* ptr) {
+  if (!h || !ptr) return NMG_ERR_INVALID;
+  for (size_t i = 0; i < h->hostregs.size(); i++) {
+    if (h->hostregs[i].lo != (uintptr_t)ptr) continue;
+    HIP_TRY(h, hipSetDevice(h->device));
+    HIP_TRY(h, hipStreamSynchronize(h->stream));  // (a launch in flight may still read it)
+    for (uint64_t z : h->zc_dev)
+      if (z && z - h->hostregs[i].dev < h->hostregs[i].hi - h->hostregs[i].lo)
+        return fail(h, NMG_ERR_STATE, "nmg_unregister_host: submitted buffers lie in the range; nmg_clear_buffers first");
+    HIP_TRY(h, hipHostUnregister(h->hostregs[i].pages));
+    h->hostregs.erase(h->hostregs.begin() + i);
+    return NMG_OK;
+  }
+  return fail(h, NMG_ERR_INVALID, "nmg_unregister_host: not a registered range");
+}
+
 extern "C" int nmg_submit_buffer(nmg_engine* h, const void* bytes, uint64_t len, uint32_t thread_rank,
                                  uint32_t access_type) {
   if (!h || (len && !bytes)) return NMG_ERR_INVALID;
   int rc = check_buffer_args(h, len, thread_rank, access_type);
   if (rc) return rc;
   if (len == 0) return NMG_OK;  // __copy_buffer drops empty segments (mem_sampling.c:680-682)
+  if (const uint64_t dev = zero_copy_dev(h, bytes, len)) return append_desc_zc(h, dev, len, thread_rank, access_type);
   if (h->streaming) {
     uint8_t* dst = nullptr;
     rc = stream_dst(h, len, &dst, nullptr);
@@ -1342,6 +1442,9 @@ extern "C" int nmg_submit_ring(nmg_engine* h, const void* ring, uint64_t ring_si
   if (data_head < data_tail) len = ring_size - data_tail + data_head;  // :687-694
   int rc = check_buffer_args(h, len, thread_rank, access_type);
   if (rc) return rc;
+  if (data_head > data_tail)  // one segment: in place if the ring is registered
+    if (const uint64_t dev = zero_copy_dev(h, (const uint8_t*)ring + data_tail, len))
+      return append_desc_zc(h, dev, len, thread_rank, access_type);
   uint8_t* dst = nullptr;
   if (h->streaming) {
     rc = stream_dst(h, len, &dst, nullptr);
@@ -1433,6 +1536,7 @@ static int ensure_bufcnt(nmg_engine* h, size_t need) {
 // the slot's previous kernel released its device arena), then the kernel on
 // the engine stream once the copy has landed.
 static int stream_flush(nmg_engine* h) {
+  if (h) h->epoch++;
   Range range("nmg_stream_chunk");
   auto& sl = h->slots[h->cur_slot];
   if (sl.descs.empty()) return NMG_OK;
@@ -1578,6 +1682,10 @@ extern "C" int nmg_submit_buffers(nmg_engine* h, uint32_t n, const void* const* 
     if (rc) return rc;
     for (uint32_t i = 0; i < n; i++) {
       if (!lens[i]) continue;
+      if (const uint64_t dev = zero_copy_dev(h, bytes[i], lens[i])) {
+        append_desc_zc(h, dev, lens[i], thread_ranks[i], access_types[i]);
+        continue;
+      }
       tasks.push_back({h->h_stage + h->stage_len, (const uint8_t*)bytes[i], lens[i]});
       append_desc(h, lens[i], thread_ranks[i], access_types[i]);
     }
@@ -1623,6 +1731,7 @@ extern "C" int nmg_set_device_buffers(nmg_engine* h, const void* d_data, const u
     bytes.push_back(lengths[b]);
   }
   h->descs.swap(descs);
+  h->zc_dev.clear();
   h->buf_bytes.swap(bytes);
   h->d_data = (const uint8_t*)d_data;
   h->external = true;
@@ -1654,6 +1763,7 @@ extern "C" int nmg_clear_buffers(nmg_engine* h) {
   for (nmg_engine* w : h->workers) nmg_clear_buffers(w);
   h->descs.clear();
   h->buf_bytes.clear();
+  h->zc_dev.clear();
   h->stage_len = 0;
   h->external = false;
   h->d_data = nullptr;
@@ -1679,6 +1789,9 @@ static int upload_buffers(nmg_engine* h) {
   }
   if (h->descs_dirty) {
     size_t n = h->descs.size();
+    // in-place buffers: offsets against the arena base (u64 arithmetic, as the kernels' data + offset)
+    for (size_t i = 0; i < h->zc_dev.size() && i < n; i++)
+      if (h->zc_dev[i]) h->descs[i].offset = h->zc_dev[i] - (uint64_t)(uintptr_t)h->d_data;
     if (n > h->descs_cap) {
       HIP_TRY(h, hipStreamSynchronize(h->stream));
       (void)hipFree(h->d_descs);
@@ -2156,6 +2269,7 @@ static int multi_analyze(nmg_engine* h);
 static int multi_finish(nmg_engine* h);
 
 extern "C" int nmg_analyze(nmg_engine* h) {
+  if (h) h->epoch++;
   Range range("nmg_analyze");
   if (!h) return NMG_ERR_INVALID;
   if (!h->have_table) return fail(h, NMG_ERR_STATE, "nmg_analyze before nmg_set_objects");
@@ -2401,10 +2515,14 @@ static int sparse_nonempty(nmg_engine* h, bool* out);
 
 // Every non-zero (entry, thread, page) cell, entries in id order, each
 // entry's cells in (thread, page) order.  Dense cells are counted and
-// compacted into rows on the device (cells_count / cells_emit), so only the
-// rows cross PCIe; the sparse table's cells (entries past the dense budget,
-// e.g. [stack]) are grouped on the host and placed at their entries' offsets.
-static int collect_page_cells(nmg_engine* h, std::vector<uint32_t>* rows, int64_t* count) {
+// compacted into rows on the device (cells_count / cells_emit); the rows stay
+// there (d_cells_rows) until copied out, so only they cross PCIe, once.  The
+// sparse table's cells (entries past the dense budget, e.g. [stack]) are
+// grouped on the host and placed at their entries' offsets.  Cached per
+// results epoch: nmg_count_page_cells then nmg_get_page_cells does the work
+// once.
+static int cells_prepare(nmg_engine* h) {
+  if (h->cells_epoch == h->epoch) return NMG_OK;
   int rc = nmg_synchronize(h);
   if (rc) return rc;
   const uint32_t E = h->E;
@@ -2431,13 +2549,11 @@ static int collect_page_cells(nmg_engine* h, std::vector<uint32_t>* rows, int64_
   std::vector<uint32_t> cnt(E, 0);
   uint64_t *d_base = nullptr, *d_off = nullptr;
   uint32_t *d_np = nullptr, *d_cnt = nullptr;
-  uint4* d_rows = nullptr;
   auto cleanup = [&]() {
     (void)hipFree(d_base);
     (void)hipFree(d_off);
     (void)hipFree(d_np);
     (void)hipFree(d_cnt);
-    (void)hipFree(d_rows);
   };
   auto hip = [&](hipError_t e, const char* what) {
     if (e == hipSuccess) return NMG_OK;
@@ -2459,30 +2575,48 @@ static int collect_page_cells(nmg_engine* h, std::vector<uint32_t>* rows, int64_
   }
   std::vector<uint64_t> off(E);
   uint64_t n = 0;
+  h->cells_sparse.clear();
   for (uint32_t e = 0; e < E; e++) {
     off[e] = n;
-    n += sidx_of[e] >= 0 && h->hist_base[e] == kHistSparse ? sparse[sidx_of[e]].size() : cnt[e];
+    if (sidx_of[e] >= 0 && h->hist_base[e] == kHistSparse) {
+      auto& l = sparse[sidx_of[e]];
+      const uint64_t k = l.size();
+      if (k) h->cells_sparse.push_back({n, e, std::move(l)});
+      n += k;
+    } else {
+      n += cnt[e];
+    }
   }
-  *count = (int64_t)n;
-  if (!rows) {
-    cleanup();
-    return NMG_OK;
-  }
-  rows->resize(n * 4);
   if (dense && n) {
-    if ((rc = hip(hipMalloc(&d_off, (size_t)E * 8), "alloc")) || (rc = hip(hipMalloc(&d_rows, n * 16), "alloc")) ||
+    if (n > h->cells_rows_cap) {
+      (void)hipFree(h->d_cells_rows);
+      h->d_cells_rows = nullptr;
+      h->cells_rows_cap = 0;
+      if ((rc = hip(hipMalloc(&h->d_cells_rows, n * 16), "alloc"))) return rc;
+      h->cells_rows_cap = n;
+    }
+    if ((rc = hip(hipMalloc(&d_off, (size_t)E * 8), "alloc")) ||
         (rc = hip(hipMemcpyAsync(d_off, off.data(), (size_t)E * 8, hipMemcpyHostToDevice, h->stream), "upload")) ||
-        (rc = hip(launch_cells_emit(h->stream, h->d_hist, h->hist_cells, h->T, d_base, d_np, E, d_off, d_rows), "emit")) ||
-        (rc = hip(hipMemcpyAsync(rows->data(), d_rows, n * 16, hipMemcpyDeviceToHost, h->stream), "rows")) ||
-        (rc = hip(hipStreamSynchronize(h->stream), "rows")))
+        (rc = hip(launch_cells_emit(h->stream, h->d_hist, h->hist_cells, h->T, d_base, d_np, E, d_off,
+                                    (uint4*)h->d_cells_rows), "emit")) ||
+        (rc = hip(hipStreamSynchronize(h->stream), "emit")))
       return rc;
   }
   cleanup();
-  for (uint32_t e = 0; e < E; e++) {
-    if (sidx_of[e] < 0 || h->hist_base[e] != kHistSparse) continue;
-    uint32_t* r = rows->data() + off[e] * 4;
-    for (auto& kv : sparse[sidx_of[e]]) {
-      r[0] = e;
+  h->cells_n = (int64_t)n;
+  h->cells_epoch = h->epoch;
+  return NMG_OK;
+}
+
+// the prepared rows into rows[cells_n * 4]: dense rows D2H, sparse rows placed
+static int cells_fill(nmg_engine* h, uint32_t* rows) {
+  const bool dense = h->hist_cells && h->E;
+  if (dense && h->cells_n)
+    HIP_TRY(h, hipMemcpy(rows, h->d_cells_rows, (size_t)h->cells_n * 16, hipMemcpyDeviceToHost));
+  for (const auto& g : h->cells_sparse) {
+    uint32_t* r = rows + g.off * 4;
+    for (const auto& kv : g.cells) {
+      r[0] = g.e;
       r[1] = (uint32_t)(kv.first >> 32);
       r[2] = (uint32_t)kv.first;
       r[3] = kv.second;
@@ -2491,23 +2625,26 @@ static int collect_page_cells(nmg_engine* h, std::vector<uint32_t>* rows, int64_
   }
   return NMG_OK;
 }
+static int collect_page_cells(nmg_engine* h, std::vector<uint32_t>* rows, int64_t* count) {
+  int rc = cells_prepare(h);
+  if (rc) return rc;
+  *count = h->cells_n;
+  rows->resize((size_t)h->cells_n * 4);
+  return cells_fill(h, rows->data());
+}
 
 extern "C" int64_t nmg_count_page_cells(nmg_engine* h) {
   if (!h || !h->have_table) return NMG_ERR_INVALID;
-  int64_t n = 0;
-  int rc = collect_page_cells(h, nullptr, &n);
-  return rc ? rc : n;
+  int rc = cells_prepare(h);
+  return rc ? rc : h->cells_n;
 }
 
 extern "C" int nmg_get_page_cells(nmg_engine* h, uint32_t* rows, int64_t n) {
   if (!h || !h->have_table || (n && !rows)) return NMG_ERR_INVALID;
-  std::vector<uint32_t> r;
-  int64_t cnt = 0;
-  int rc = collect_page_cells(h, &r, &cnt);
+  int rc = cells_prepare(h);
   if (rc) return rc;
-  if (cnt != n) return fail(h, NMG_ERR_INVALID, "row count mismatch");
-  if (n) memcpy(rows, r.data(), r.size() * 4);
-  return NMG_OK;
+  if (h->cells_n != n) return fail(h, NMG_ERR_INVALID, "row count mismatch");
+  return n ? cells_fill(h, rows) : NMG_OK;
 }
 
 // ---- multi-GPU merge support
@@ -2547,6 +2684,7 @@ extern "C" int nmg_export_array(nmg_engine* h, int which, void* d_dst) {
 }
 
 extern "C" int nmg_import_array(nmg_engine* h, int which, const void* d_src) {
+  if (h) h->epoch++;
   Range range("nmg_import_array");
   if (!h || !h->have_table) return NMG_ERR_INVALID;
   size_t bytes = 0;
@@ -2618,6 +2756,7 @@ extern "C" int nmg_sparse_export(nmg_engine* h, uint64_t* keys, uint32_t* counts
 }
 
 extern "C" int nmg_sparse_import(nmg_engine* h, const uint64_t* keys, const uint32_t* counts, int64_t n) {
+  if (h) h->epoch++;
   // Re-inserts merged (key, count) pairs into an empty table on this rank.
   if (!h || !h->have_table || (n && (!keys || !counts))) return NMG_ERR_INVALID;
   if (!h->d_sparse_keys) return n ? fail(h, NMG_ERR_STATE, "no sparse table") : NMG_OK;
@@ -2641,6 +2780,7 @@ extern "C" int nmg_sparse_import(nmg_engine* h, const uint64_t* keys, const uint
 
 extern "C" int nmg_set_buffer_counts(nmg_engine* h, uint32_t nb_buffers, const uint32_t* nb_samples,
                                      const uint32_t* nb_found, const uint64_t* buffer_bytes) {
+  if (h) h->epoch++;
   if (!h || (nb_buffers && (!nb_samples || !nb_found || !buffer_bytes))) return NMG_ERR_INVALID;
   h->counts_override = true;
   h->ov_samples.assign(nb_samples, nb_samples + nb_buffers);

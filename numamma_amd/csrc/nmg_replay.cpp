@@ -281,6 +281,14 @@ extern "C" int nmg_run_replay(const char* replay_path, const char* output_dir, c
   };
   rc = nmg_set_objects(h, r.keys, r.entry_off, r.nb_keys, r.objects.data(), r.nb_entries);
   if (rc) return bail(rc);
+  // NMG_REPLAY_REGISTER=1: the loaded replay (every ring) registered with
+  // nmg_register_host, so 16-byte aligned unwrapped buffers are read in place
+  const char* reg = getenv("NMG_REPLAY_REGISTER");
+  const bool registered = reg && atoi(reg) && !r.file.empty();
+  if (registered) {
+    rc = nmg_register_host(h, r.file.data(), r.file.size());
+    if (rc) return bail(rc);
+  }
   if (stream && *stream) {
     if (chunk) {
       rc = nmg_stream_begin(h, chunk, threads ? threads : 1);

@@ -107,6 +107,14 @@ class Engine:
                                        _ptr(acc, C.c_uint32)))
         self.buffer_bytes.extend(int(x) for x in lens if x)
 
+    def register_host(self, arr: np.ndarray):
+        """nmg_register_host over a host array the caller keeps alive: buffers
+        submitted from inside it are read in place by the kernels (no copy)."""
+        self._c(lib.nmg_register_host(self.h, C.c_void_p(arr.ctypes.data), arr.nbytes))
+
+    def unregister_host(self, arr: np.ndarray):
+        self._c(lib.nmg_unregister_host(self.h, C.c_void_p(arr.ctypes.data)))
+
     def stream_begin(self, chunk_bytes: int = 64 << 20, copy_threads: int = 1):
         """Streaming mode (configs[4]): chunks are uploaded and analysed while
         buffers keep arriving; analyze() flushes the last one."""

@@ -466,6 +466,77 @@ def test_streaming_bit_exact_vs_oracle(tmp_path, monkeypatch, cfg, mode):
     _same_dirs(odir, edir)
 
 
+ZERO_COPY_CASES = [
+    # (replay config, NMG_REPLAY_STREAM: "" = nmg_submit_ring per buffer, "0:4:16" = nmg_submit_buffers batches)
+    (SynthConfig(nb_samples=150_000, nb_intervals=2_000, lost_frac=1e-3, wrap_one=True, seed=41), ""),
+    (SynthConfig(nb_samples=150_000, nb_intervals=2_000, lost_frac=1e-3, wrap_one=True, seed=42), "0:4:16"),
+    (SynthConfig(nb_samples=300_000, nb_intervals=60_000, lost_frac=1e-3, seed=43), "0:4:64"),  # partition-first
+    (SynthConfig(nb_samples=100_000, nb_intervals=3_000, buffer_records=97, seed=44), ""),  # odd buffer sizes
+]
+
+
+@pytest.mark.parametrize("cfg,mode", ZERO_COPY_CASES, ids=[f"zc{i}" for i in range(len(ZERO_COPY_CASES))])
+def test_zero_copy_bit_exact_vs_oracle(tmp_path, monkeypatch, cfg, mode):
+    """nmg_register_host over the loaded replay: unwrapped buffers that start
+    16-byte aligned are read in place by the kernels over PCIe, the rest
+    (wrapped rings, unaligned starts) are staged; byte-identical to the
+    oracle either way."""
+    d = str(tmp_path)
+    path, odir = _oracle(generate(cfg), d)
+    monkeypatch.setenv("NMG_REPLAY_REGISTER", "1")
+    if mode:
+        monkeypatch.setenv("NMG_REPLAY_STREAM", mode)
+    edir = _engine_replay(path, d)
+    _assert_raw_equal(os.path.join(d, "oracle_raw.bin"), os.path.join(d, "engine_raw.bin"))
+    assert open(os.path.join(d, "oracle_stdout.txt"), "rb").read() == open(os.path.join(d, "engine_stdout.txt"), "rb").read()
+    _same_dirs(odir, edir)
+
+
+def test_register_host_api(tmp_path):
+    """Registration rules: overlapping ranges are refused, a range holding
+    submitted buffers cannot be unregistered before nmg_clear_buffers, and
+    a registered engine gives the same counters as a copying one."""
+    from numamma_amd.engine import Engine
+    from numamma_amd.replay import RECORD_DTYPE
+
+    rp = generate(SynthConfig(nb_samples=100_000, nb_intervals=1_500, seed=45))
+    lins = rp.linear_buffers()
+    # one arena, buffers at 16-byte aligned offsets (one deliberately at +8: staged)
+    offs, o = [], 0
+    for i, (_, _, b) in enumerate(lins):
+        o = (o + 15) // 16 * 16 + (8 if i == 3 else 0)
+        offs.append(o)
+        o += b.shape[0]
+    arena = np.zeros(o + 64, dtype=np.uint8)
+    for (_, _, b), off in zip(lins, offs):
+        arena[off:off + b.shape[0]] = b
+    views = [(r, a, arena[off:off + b.shape[0]]) for (r, a, b), off in zip(lins, offs)]
+    out = []
+    for register in (False, True):
+        eng = Engine(nb_threads=rp.nb_threads)
+        eng.set_objects(rp.table)
+        if register:
+            eng.register_host(arena)
+            with pytest.raises(_lib.NmgError):
+                eng.register_host(arena[100:])  # overlap
+        eng.submit_buffers(views)
+        eng.analyze()
+        eng.synchronize()
+        g, ns, nf = eng.global_counters()
+        first, cw = eng.object_counters()
+        bs, bf = eng.buffer_counts()
+        out.append((g, ns, nf, first, cw, bs, bf, eng.page_cells()))
+        if register:
+            with pytest.raises(_lib.NmgError):
+                eng.unregister_host(arena)  # buffers still submitted
+            eng.clear_buffers()
+            eng.unregister_host(arena)
+        eng.close()
+    for x, y in zip(*out):
+        assert np.array_equal(np.asarray(x), np.asarray(y))
+    assert out[0][1] == sum(int((b.view(RECORD_DTYPE)["type"] == 9).sum()) for _, _, b in lins)
+
+
 def test_streaming_python_api_repeat(tmp_path):
     """Engine.stream_begin + submit_buffers in alarm-sized batches, analysed,
     then cleared and streamed again on the same engine (state reuse), equal to

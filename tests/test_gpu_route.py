@@ -125,3 +125,31 @@ def test_route_accumulates_like_single_pass(extra):
     for x, y in zip(a3 + a1, b3 + b1):
         assert np.array_equal(np.asarray(x), np.asarray(y))
     assert a3[1] == 3 * a1[1] and a3[2] == 3 * a1[2]
+
+
+def test_route_escaped_records_bit_exact(tmp_path):
+    """Compact records that cannot hold a sample (nmg_route.h XLayout) carry
+    the escape mark and the local pass re-reads the raw record: timestamps
+    before the table's first allocation (some still match the globals, alloc
+    date 0) or 2^41 ns past it, addresses 2^40 bytes and more above their
+    partition's first key, weights past the 14-bit field."""
+    from numamma_amd.replay import RECORD_DTYPE, T0
+
+    d = str(tmp_path)
+    rp = generate(SynthConfig(nb_samples=300_000, nb_intervals=30_000, seed=79))
+    rng = np.random.default_rng(79)
+    for b in rp.buffers:
+        rec = b.ring.view(RECORD_DTYPE)  # pure 40 B SAMPLE streams (lost_frac = 0, no wrap)
+        u = rng.random(rec.shape[0])
+        early, late = u < 0.03, (u >= 0.03) & (u < 0.05)
+        far, heavy = (u >= 0.05) & (u < 0.07), (u >= 0.07) & (u < 0.08)
+        rec["timestamp"][early] = rng.integers(1, T0, int(early.sum()), dtype=np.uint64)
+        rec["timestamp"][late] += np.uint64(1 << 41)
+        rec["addr"][far] = np.uint64(0x600000000000) + rng.integers(0, 1 << 41, int(far.sum()), dtype=np.uint64)
+        rec["weight"][heavy] = rng.integers(1 << 14, 1 << 20, int(heavy.sum()), dtype=np.uint64)
+    path, odir = _oracle(rp, d)
+    for tag, flags in (("route", 0), ("tiny", TINY_POOL)):
+        edir, raw = _engine(path, d, _lib.NMG_F_DEFAULT | flags, tag)
+        _same(os.path.join(d, "oracle_raw.bin"), raw)
+        _same(os.path.join(d, "oracle_stdout.txt"), os.path.join(d, f"engine_{tag}_stdout.txt"))
+        _same_dirs(odir, edir)

@@ -13,6 +13,10 @@ everything nmg_report reads).  Modes (one JSON line each):
   stream      nmg_stream_begin(chunk, T) and nmg_submit_buffers in alarm-sized
               batches: each chunk's H2D (copy stream) and kernel (engine
               stream) overlap the copies of the next chunk (configs[4])
+  zerocopy    the buffers live in one host arena registered once with
+              nmg_register_host (like perf rings pinned at thread start; the
+              registration is timed apart, register_s): one nmg_submit_buffers
+              call copies nothing, the kernels read the arena over PCIe
 
     python tools/e2e.py [c2|c4shard] [--threads 16] [--chunk-mb 64] [--batch 256]
 """
@@ -53,13 +57,30 @@ def main():
     eng = Engine(nb_threads=rp.nb_threads, copy_threads=a.threads)
     eng.set_objects(rp.table)
 
-    def results():  # D2H of everything the report reads
-        eng.global_counters()
-        eng.buffer_counts()
-        eng.object_counters()
-        eng.page_cells()
+    split = {}
 
+    def results():  # D2H of everything the report reads (each getter timed: split)
+        for name, f in (("global", eng.global_counters), ("buffers", eng.buffer_counts),
+                        ("objects", eng.object_counters), ("page_cells", eng.page_cells)):
+            t = time.perf_counter()
+            f()
+            split.setdefault(name, []).append(time.perf_counter() - t)
+
+    zc_views, reg_s = None, None
     for mode in a.modes.split(","):
+        if mode == "zerocopy" and zc_views is None:
+            offs, o = [], 0
+            for _, _, b in lins:
+                offs.append(o)
+                o = (o + b.shape[0] + 15) // 16 * 16
+            arena = np.empty(o + 4096, dtype=np.uint8)
+            base = (-arena.ctypes.data) % 16
+            for (_, _, b), off in zip(lins, offs):
+                arena[base + off:base + off + b.shape[0]] = b
+            zc_views = [(r, acc, arena[base + off:base + off + b.shape[0]]) for (r, acc, b), off in zip(lins, offs)]
+            t = time.perf_counter()
+            eng.register_host(arena)
+            reg_s = time.perf_counter() - t
         reps = []
         for r in range(a.reps + 1):
             eng.clear_buffers()
@@ -71,6 +92,8 @@ def main():
                     eng.submit_buffer(data, rank, acc)
             elif mode == "batch":
                 eng.submit_buffers(lins)
+            elif mode == "zerocopy":
+                eng.submit_buffers(zc_views)
             else:
                 eng.stream_begin(chunk_bytes=a.chunk_mb << 20, copy_threads=a.threads)
                 for i in range(0, len(lins), a.batch):
@@ -92,13 +115,16 @@ def main():
         total = submit + tail + d2h
         print(json.dumps({
             "workload": a.workload, "mode": mode, "records": int(nsamples), "bytes": int(nbytes),
-            "copy_threads": a.threads if mode != "per_buffer" else 1,
+            "copy_threads": a.threads if mode in ("batch", "stream") else (0 if mode == "zerocopy" else 1),
             "chunk_bytes": (a.chunk_mb << 20) if mode == "stream" else None,
             "submit_s": submit, "analyze_to_sync_s": tail,
             ("report_s" if a.report else "d2h_results_s"): d2h, "kernel_s": kern,
             "e2e_s": total, "e2e_samples_per_s": nsamples / total,
             "device_resident_samples_per_s": nsamples / kern if kern else None,
+            "d2h_split_s": {k: float(np.median(v[1:] if len(v) > 1 else v)) for k, v in split.items()},
+            **({"register_s": reg_s} if mode == "zerocopy" else {}),
         }), flush=True)
+        split.clear()
     eng.close()
 
 

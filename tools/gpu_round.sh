@@ -49,7 +49,7 @@ for s in $STAGES; do
       cat $OUT/ablate_$TAG.json ;;
     e2e)
       echo "== end-to-end (host buffers, PCIe)"
-      timeout -k 10 600 python tools/e2e.py c2 --threads ${E2E_THREADS:-16} --chunk-mb ${E2E_CHUNK:-64} > $OUT/e2e_$TAG.json 2> $OUT/e2e_$TAG.err \
+      timeout -k 10 600 python tools/e2e.py ${E2E_WL:-c2} --modes ${E2E_MODES:-per_buffer,batch,stream} --threads ${E2E_THREADS:-16} --chunk-mb ${E2E_CHUNK:-64} > $OUT/e2e_$TAG.json 2> $OUT/e2e_$TAG.err \
         || { echo "e2e failed"; tail -30 $OUT/e2e_$TAG.err; exit 1; }
       cat $OUT/e2e_$TAG.json ;;
     phases)
