@@ -238,7 +238,9 @@ int nmg_submit_buffers(nmg_engine *h, uint32_t n, const void *const *bytes, cons
  * starts 16-byte aligned is not copied: nmg_analyze's kernels read it over
  * PCIe, so it must stay unchanged until nmg_synchronize.  Batch path of a
  * single-GPU engine without the dump modes only (streaming, dump modes and
- * multi-GPU handles copy as before).  Ranges must not overlap.
+ * multi-GPU handles copy as before).  ptr must be page-aligned (4 KiB) and
+ * the pages up to ptr + bytes rounded up belong to the caller alone: whole
+ * pages are registered.  Ranges must not overlap.
  * nmg_unregister_host takes the ptr given at registration; buffers inside
  * the range must have been dropped (nmg_clear_buffers) first.
  */

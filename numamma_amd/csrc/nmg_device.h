@@ -62,9 +62,12 @@ __device__ __forceinline__ uint64_t wave_sum_w(uint64_t w, bool big) {
 // uncached (the bucket order of struct mem_counters).  HIT beats MISS and
 // every group is independent (quirk Q12).
 __device__ __forceinline__ uint32_t bucket_mask(uint32_t lvl) {
-  uint32_t g = ((lvl >> 3) & 1) | (((lvl >> 5) & 1) << 1) | (((lvl >> 6) & 1) << 2) |
-               (((lvl >> 4) & 1) << 3) | (((lvl >> 7) & 1) << 4) | ((((lvl >> 8) | (lvl >> 9)) & 1) << 5) |
-               ((((lvl >> 10) | (lvl >> 11)) & 1) << 6) | (((lvl >> 12) & 1) << 7) | (((lvl >> 13) & 1) << 8);
+  // group bits from x = lvl >> 3 (L1 L2 L3 LFB LOC_RAM REM_RAM1|2 REM_CCE1|2 IO UNC, from x0 x2 x3
+  // x1 x4 x5|x6 x7|x8 x9 x10): six masked moves instead of one shift per bit
+  // (lvl < 2^14; equal for every such value)
+  const uint32_t x = lvl >> 3, y = x | (x >> 1);
+  const uint32_t g = (x & 0x11u) | ((x >> 1) & 0x6u) | ((x & 2u) << 2) | (y & 0x20u) | ((y >> 1) & 0x40u) |
+                     ((x >> 2) & 0x180u);
   if (lvl & LVL_HIT) return g;
   if (lvl & LVL_MISS) return g << 9;
   return 0;

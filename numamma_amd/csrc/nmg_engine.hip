@@ -1381,12 +1381,15 @@ static int route_settle(nmg_engine* h);
 extern "C" int nmg_register_host(nmg_engine* h, void* ptr, uint64_t bytes) {
   if (!h || !ptr || !bytes) return NMG_ERR_INVALID;
   if (h->multi) return fail(h, NMG_ERR_STATE, "nmg_register_host: single-GPU engines only");
+  // whole pages are pinned and mapped, and HIP then treats every address in
+  // them as this registration's: they must be the caller's alone (another
+  // allocation sharing the last page would be misread by later copies)
+  if ((uintptr_t)ptr & 4095) return fail(h, NMG_ERR_INVALID, "nmg_register_host: ptr must be page-aligned (4 KiB)");
   const uintptr_t a = (uintptr_t)ptr;
   for (const auto& r : h->hostregs)  // (pages: two ranges must not share one)
     if ((a & ~uintptr_t(4095)) < ((r.hi + 4095) & ~uintptr_t(4095)) && ((uintptr_t)r.pages) < a + bytes)
       return fail(h, NMG_ERR_INVALID, "nmg_register_host: overlaps (shares a page with) a registered range");
-  // whole pages (every page holding a byte of the range is mapped)
-  const uintptr_t pg = 4096, p0 = a & ~(pg - 1), p1 = (a + bytes + pg - 1) & ~(pg - 1);
+  const uintptr_t pg = 4096, p0 = a, p1 = (a + bytes + pg - 1) & ~(pg - 1);
   HIP_TRY(h, hipSetDevice(h->device));
   HIP_TRY(h, hipHostRegister((void*)p0, p1 - p0, hipHostRegisterMapped));
   void* dev = nullptr;

@@ -19,8 +19,29 @@ namespace {
 
 constexpr size_t kEntryBytes = 72;
 
+// page-aligned, page-padded storage for the loaded replay (NMG_REPLAY_REGISTER:
+// nmg_register_host pins whole pages, which must hold nothing else)
+template <class T>
+struct PageAlloc {
+  using value_type = T;
+  PageAlloc() = default;
+  template <class U>
+  PageAlloc(const PageAlloc<U>&) {}
+  T* allocate(size_t n) {
+    void* p = nullptr;
+    const size_t b = std::max<size_t>((n * sizeof(T) + 4095) & ~size_t(4095), 4096);
+    if (posix_memalign(&p, 4096, b)) throw std::bad_alloc();
+    return static_cast<T*>(p);
+  }
+  void deallocate(T* p, size_t) { free(p); }
+  template <class U>
+  bool operator==(const PageAlloc<U>&) const { return true; }
+  template <class U>
+  bool operator!=(const PageAlloc<U>&) const { return false; }
+};
+
 struct Replay {
-  std::vector<uint8_t> file;
+  std::vector<uint8_t, PageAlloc<uint8_t>> file;
   uint32_t nb_threads = 0, nb_keys = 0, nb_entries = 0, nb_buffers = 0;
   const uint64_t* keys = nullptr;
   const uint32_t* entry_off = nullptr;

@@ -34,9 +34,8 @@ __device__ __forceinline__ uint32_t route_partition(const RouteParams& rp, const
                                                     const uint16_t* s_pdir, uint64_t addr) {
   uint64_t s0 = rp.seg[0].start;
   uint32_t base = rp.seg[0].base, ns = rp.seg[0].nslots, sh = rp.seg[0].shift, ql = rp.seg[0].qlast;
-#pragma unroll
-  for (uint32_t k = 1; k < kRouteSegs; k++) {
-    const bool in = addr >= rp.seg[k].start;  // (unused segments start at ~0)
+  for (uint32_t k = 1; k < rp.nseg; k++) {  // (uniform bound: only the table's segments; 7 unrolled
+    const bool in = addr >= rp.seg[k].start;   // selects cost the route pass 6 %)
     s0 = in ? rp.seg[k].start : s0;
     base = in ? rp.seg[k].base : base;
     ns = in ? rp.seg[k].nslots : ns;

@@ -27,6 +27,15 @@ def counters_to_numpy(c: "_lib.nmg_mem_counters") -> np.ndarray:
     return np.frombuffer(bytes(c), dtype="<u8").copy()
 
 
+def page_aligned_empty(nbytes: int) -> np.ndarray:
+    """A u8 array of nbytes starting on a 4 KiB page, its last page its own
+    (what nmg_register_host pins: whole pages)."""
+    n = max(4096, (nbytes + 4095) // 4096 * 4096)
+    buf = np.empty(n + 4096, dtype=np.uint8)
+    off = (-buf.ctypes.data) % 4096
+    return buf[off:off + n][:nbytes]
+
+
 class Engine:
     def __init__(self, device: int = 0, flags: int = _lib.NMG_F_DEFAULT, nb_threads: int = 1,
                  hist_budget_bytes: int = 0, sparse_capacity: int = 0, copy_threads: int = 1,
@@ -108,8 +117,9 @@ class Engine:
         self.buffer_bytes.extend(int(x) for x in lens if x)
 
     def register_host(self, arr: np.ndarray):
-        """nmg_register_host over a host array the caller keeps alive: buffers
-        submitted from inside it are read in place by the kernels (no copy)."""
+        """nmg_register_host over a host array the caller keeps alive (page
+        aligned, its pages its own: page_aligned_empty): buffers submitted from
+        inside it are read in place by the kernels (no copy)."""
         self._c(lib.nmg_register_host(self.h, C.c_void_p(arr.ctypes.data), arr.nbytes))
 
     def unregister_host(self, arr: np.ndarray):

@@ -507,7 +507,10 @@ def test_register_host_api(tmp_path):
         o = (o + 15) // 16 * 16 + (8 if i == 3 else 0)
         offs.append(o)
         o += b.shape[0]
-    arena = np.zeros(o + 64, dtype=np.uint8)
+    from numamma_amd.engine import page_aligned_empty
+
+    arena = page_aligned_empty(o + 64)
+    arena[:] = 0
     for (_, _, b), off in zip(lins, offs):
         arena[off:off + b.shape[0]] = b
     views = [(r, a, arena[off:off + b.shape[0]]) for (r, a, b), off in zip(lins, offs)]
@@ -518,7 +521,9 @@ def test_register_host_api(tmp_path):
         if register:
             eng.register_host(arena)
             with pytest.raises(_lib.NmgError):
-                eng.register_host(arena[100:])  # overlap
+                eng.register_host(arena[4096:])  # overlap
+            with pytest.raises(_lib.NmgError):
+                eng.register_host(arena[100:])  # not page-aligned
         eng.submit_buffers(views)
         eng.analyze()
         eng.synchronize()

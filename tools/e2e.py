@@ -73,8 +73,10 @@ def main():
             for _, _, b in lins:
                 offs.append(o)
                 o = (o + b.shape[0] + 15) // 16 * 16
-            arena = np.empty(o + 4096, dtype=np.uint8)
-            base = (-arena.ctypes.data) % 16
+            from numamma_amd.engine import page_aligned_empty
+
+            arena = page_aligned_empty(o + 64)
+            base = 0
             for (_, _, b), off in zip(lins, offs):
                 arena[base + off:base + off + b.shape[0]] = b
             zc_views = [(r, acc, arena[base + off:base + off + b.shape[0]]) for (r, acc, b), off in zip(lins, offs)]
