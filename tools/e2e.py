@@ -101,6 +101,8 @@ def main():
                 for i in range(0, len(lins), a.batch):
                     eng.submit_buffers(lins[i:i + a.batch])
             t1 = time.perf_counter()
+            if mode == "stream":
+                eng.stream_end()  # (flushes the last chunk; the engine leaves streaming mode)
             eng.analyze()
             eng.synchronize()
             t2 = time.perf_counter()
