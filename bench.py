@@ -78,6 +78,8 @@ class Workload:
         # (NMG_BENCH_DEBUG_FLAGS: internal ablation switches for counter
         # passes, tools/gpu_round.sh pmcx; never set for a reported number)
         dbg = int(os.environ.get("NMG_BENCH_DEBUG_FLAGS", "0"), 0)
+        if dbg:
+            os.environ["NMG_INTERNAL_FLAGS"] = "1"
         self.eng = Engine(device=device.index, flags=_lib.NMG_F_DEFAULT | dbg, nb_threads=self.rp.nb_threads)
         self.eng.set_objects(self.rp.table)
         # global analysis order: rank-major (seq_base)

@@ -56,10 +56,10 @@ extern "C" {
 #define NMG_F_OBJECT_LEVELS 0x4  /* per-object level buckets (count, sum) for callsite_summary_<id>.dat */
 #define NMG_F_SAMPLE_MATCHES 0x8 /* keep every SAMPLE record's match (object or none) for the dump modes */
 #define NMG_F_SINGLE_PASS 0x10   /* large tables (> 1023 keys): one attribution pass with global lookups instead of
-                                    the partition-first passes; same results.  Needed only for batches
-                                    with a great many SAMPLE records shorter than 40 B (garbage perf data), which
-                                    the partition-first path reports as NMG_ERR_CAPACITY */
+                                    the partition-first passes; same results (A/B and tests) */
 #define NMG_F_DEFAULT (NMG_F_MATCH_SAMPLES | NMG_F_PAGE_HIST)
+/* every public flag: nmg_create rejects any other bit with NMG_ERR_INVALID */
+#define NMG_F_ALL (NMG_F_MATCH_SAMPLES | NMG_F_PAGE_HIST | NMG_F_OBJECT_LEVELS | NMG_F_SAMPLE_MATCHES | NMG_F_SINGLE_PASS)
 
 /* struct count, src/mem_analyzer.h:10-15 */
 struct nmg_count {
@@ -113,14 +113,18 @@ struct nmg_options {
    * takes host buffers (nmg_submit_*); device-resident buffers and streaming
    * stay single-GPU.  0 or 1: one GPU, `device`.
    * The three fields below were added after the first version of this
-   * struct: they are read only when abi_version == NMG_OPTIONS_ABI, so a
-   * caller built against the older, shorter struct (or one that zeroes
-   * them) gets a one-GPU engine instead of reading past its struct. */
+   * struct (which ended at sparse_capacity, NMG_OPTIONS_V1_SIZE bytes).
+   * nmg_create reads the whole current struct: zero-initialise it.  A
+   * caller built against the first version passes its own struct size to
+   * nmg_create_ex, which reads only that many bytes.  nb_gpus / devices are
+   * used only with abi_version == NMG_OPTIONS_ABI; nb_gpus > 1 without it is
+   * NMG_ERR_INVALID (not a silent one-GPU engine). */
   uint32_t nb_gpus;
   uint32_t abi_version;      /* NMG_OPTIONS_ABI to use nb_gpus / devices */
   const int32_t *devices;
 };
 #define NMG_OPTIONS_ABI 0x4e4d4702u /* "NMG" v2: nmg_options with nb_gpus / abi_version / devices */
+#define NMG_OPTIONS_V1_SIZE 32      /* bytes of the first struct version: device .. sparse_capacity */
 
 struct nmg_report_options {
   const char *output_dir;  /* settings.output_dir; call_sites.log etc. land here */
@@ -166,7 +170,11 @@ const char *nmg_strerror(int status);
 /* text of the last error on h (h == NULL: the calling thread's last failed nmg_create) */
 int nmg_get_last_error_detail(nmg_engine *h, char *buf, size_t len);
 
+/* opt == NULL: defaults.  Flags outside NMG_F_ALL are NMG_ERR_INVALID. */
 int nmg_create(nmg_engine **out, const struct nmg_options *opt);
+/* The same, reading only the first opt_size bytes of *opt (the rest as
+ * zero): NMG_OPTIONS_V1_SIZE for a caller of the first struct version. */
+int nmg_create_ex(nmg_engine **out, const struct nmg_options *opt, size_t opt_size);
 void nmg_destroy(nmg_engine *h);
 
 /*

@@ -39,6 +39,8 @@ NMG_F_OBJECT_LEVELS = 0x4
 NMG_F_SAMPLE_MATCHES = 0x8
 NMG_F_SINGLE_PASS = 0x10  # large tables: single-pass attribute_kernel instead of the partition-first passes
 NMG_F_DEFAULT = NMG_F_MATCH_SAMPLES | NMG_F_PAGE_HIST
+NMG_F_ALL = NMG_F_MATCH_SAMPLES | NMG_F_PAGE_HIST | NMG_F_OBJECT_LEVELS | NMG_F_SAMPLE_MATCHES | NMG_F_SINGLE_PASS
+NMG_OPTIONS_V1_SIZE = 32
 NMG_DUMP_CALLSITES, NMG_DUMP_ALL, NMG_DUMP_UNMATCHED = 0x1, 0x2, 0x4
 NMG_ARR_SUM64, NMG_ARR_MIN64, NMG_ARR_MAX64, NMG_ARR_HIST32 = range(4)
 ERRORS = {
@@ -151,6 +153,7 @@ _SIGS = {
     "nmg_strerror": (C.c_char_p, [C.c_int]),
     "nmg_get_last_error_detail": (C.c_int, [H, C.c_char_p, C.c_size_t]),
     "nmg_create": (C.c_int, [C.POINTER(H), C.POINTER(nmg_options)]),
+    "nmg_create_ex": (C.c_int, [C.POINTER(H), C.c_void_p, C.c_size_t]),
     "nmg_destroy": (None, [H]),
     "nmg_set_objects": (C.c_int, [H, u64p, u32p, C.c_uint32, C.POINTER(nmg_object), C.c_uint32]),
     "nmg_update_objects": (C.c_int, [H, u64p, u32p, C.c_uint32, u32p, C.POINTER(nmg_object)]),

@@ -14,6 +14,7 @@
 #include <functional>
 #include <cstdio>
 #include <cstdlib>
+#include <cstddef>
 #include <cstring>
 #include <condition_variable>
 #include <memory>
@@ -160,6 +161,7 @@ struct nmg_engine {
   uint64_t *d_sum64 = nullptr, *d_min64 = nullptr, *d_max64 = nullptr;
   uint64_t n_sum64 = 0, n_min64 = 0, n_max64 = 0;
   uint32_t* d_hist = nullptr;
+  unsigned long long* d_found = nullptr;  // matched SAMPLEs since the last reset (Params::found)
   uint64_t* d_sparse_keys = nullptr;
   uint32_t* d_sparse_vals = nullptr;
   uint32_t* d_sparse_dirty = nullptr;  // [2] parity flags (see reset_kernel)
@@ -486,22 +488,51 @@ static int check_table(nmg_engine* h, const uint64_t* keys, const uint32_t* entr
 static int multi_create(nmg_engine* h, const nmg_options* opt);
 static void multi_destroy(nmg_engine* h);
 
+static_assert(offsetof(nmg_options, nb_gpus) == NMG_OPTIONS_V1_SIZE, "first nmg_options version");
+
+// internal (ablation / test) flag bits are accepted only with NMG_INTERNAL_FLAGS
+// set in the environment: they change what the kernels compute
+static bool internal_flags_allowed() {
+  const char* e = getenv("NMG_INTERNAL_FLAGS");
+  return e && *e && strcmp(e, "0") != 0;
+}
+
 extern "C" int nmg_create(nmg_engine** out, const nmg_options* opt) {
+  return nmg_create_ex(out, opt, sizeof(nmg_options));
+}
+
+extern "C" int nmg_create_ex(nmg_engine** out, const nmg_options* opt_in, size_t opt_size) {
   if (!out) return NMG_ERR_INVALID;
   *out = nullptr;
-  nmg_engine* h = new (std::nothrow) nmg_engine();
-  if (!h) return NMG_ERR_NOMEM;
-  // nb_gpus / devices only from a caller of the current struct (NMG_OPTIONS_ABI):
-  // an older caller's struct ends before them
+  // only the caller's bytes of the struct are read (a first-version caller's
+  // struct ends at NMG_OPTIONS_V1_SIZE); the rest is zero
   nmg_options o2{};
-  if (opt) {
-    o2 = *opt;
+  const nmg_options* opt = nullptr;
+  if (opt_in) {
+    if (opt_size < NMG_OPTIONS_V1_SIZE) {
+      g_create_error = "nmg_create_ex: opt_size smaller than the first nmg_options version";
+      return NMG_ERR_INVALID;
+    }
+    memcpy(&o2, opt_in, std::min(opt_size, sizeof(nmg_options)));
+    opt = &o2;
+    if ((o2.flags & ~(uint32_t)NMG_F_ALL) && !internal_flags_allowed()) {
+      char msg[128];
+      snprintf(msg, sizeof(msg), "nmg_create: flags 0x%x outside NMG_F_ALL (0x%x)", o2.flags & ~(uint32_t)NMG_F_ALL,
+               (uint32_t)NMG_F_ALL);
+      g_create_error = msg;
+      return NMG_ERR_INVALID;
+    }
     if (o2.abi_version != NMG_OPTIONS_ABI) {
+      if (o2.nb_gpus > 1) {  // (an older multi-GPU caller: not silently one GPU)
+        g_create_error = "nmg_create: nb_gpus > 1 needs abi_version = NMG_OPTIONS_ABI";
+        return NMG_ERR_INVALID;
+      }
       o2.nb_gpus = 0;
       o2.devices = nullptr;
     }
-    opt = &o2;
   }
+  nmg_engine* h = new (std::nothrow) nmg_engine();
+  if (!h) return NMG_ERR_NOMEM;
   if (opt) {
     h->device = opt->nb_gpus >= 1 && opt->devices ? opt->devices[0] : opt->device;
     h->flags = opt->flags;
@@ -570,6 +601,7 @@ extern "C" void nmg_destroy(nmg_engine* h) {
   (void)hipFree(h->d_arena);
   (void)hipFree(h->d_descs);
   (void)hipFree(h->d_bufcnt);
+  (void)hipFree(h->d_found);
   (void)hipFree(h->d_sdescs);
   (void)hipFree(h->d_ranges);
   (void)hipFree(h->d_dbg);
@@ -625,6 +657,7 @@ extern "C" int nmg_reset_counters(nmg_engine* h) {
   r.n_min64 = h->n_min64;
   r.max64 = h->d_max64;
   r.n_max64 = h->n_max64;
+  r.found = h->d_found;
   const uint64_t hist_bytes = h->hist_cells * h->T * 4;
   if (hist_bytes & 15) HIP_TRY(h, hipMemsetAsync(h->d_hist, 0, hist_bytes, h->stream));  // (16 B multiple always)
   r.hist = reinterpret_cast<uint4*>(h->d_hist);
@@ -1017,6 +1050,7 @@ extern "C" int nmg_set_objects(nmg_engine* h, const uint64_t* keys, const uint32
   HIP_TRY(h, hipMalloc(&h->d_sum64, h->n_sum64 * 8));
   HIP_TRY(h, hipMalloc(&h->d_min64, h->n_min64 * 8));
   HIP_TRY(h, hipMalloc(&h->d_max64, h->n_max64 * 8));
+  if (!h->d_found) HIP_TRY(h, hipMalloc(&h->d_found, 8));
   if (nb_entries > kObjSlots) {  // hashed object mode (see launch_attribution)
     HIP_TRY(h, hipMalloc(&h->d_pk64, (size_t)nb_entries * 2 * 8));
     HIP_TRY(h, hipMemset(h->d_pk64, 0, (size_t)nb_entries * 2 * 8));
@@ -1064,6 +1098,33 @@ static int grow_entries(nmg_engine* h, uint32_t newE, const uint32_t* ids, const
   };
   std::vector<Move> moves;
   const size_t nsparse0 = h->sparse_entries.size();
+  // Host state is changed in place below; every error return first undoes
+  // it (the sizes before the call, and the old fields of the entries that
+  // moved), so that a failed update keeps the engine as it was.
+  struct Old {
+    uint32_t id;
+    uint64_t hist, np;
+    DevEntry d;
+  };
+  std::vector<Old> changed;
+  auto rollback = [&]() {
+    for (auto it = changed.rbegin(); it != changed.rend(); ++it) {
+      h->hist_base[it->id] = it->hist;
+      h->npages[it->id] = it->np;
+      h->dev_entries[it->id] = it->d;
+    }
+    h->hist_base.resize(oldE);
+    h->npages.resize(oldE);
+    h->buffer_size.resize(oldE);
+    h->entry_addr.resize(oldE);
+    h->objects.resize(oldE);
+    h->dev_entries.resize(oldE);
+    h->sparse_entries.resize(nsparse0);
+  };
+  auto fail_rb = [&](int code, const std::string& msg) {
+    rollback();
+    return fail(h, code, msg);
+  };
   h->hist_base.resize(newE, kHistSparse);
   h->npages.resize(newE, 1);
   h->buffer_size.resize(newE, 0);
@@ -1088,14 +1149,15 @@ static int grow_entries(nmg_engine* h, uint32_t newE, const uint32_t* ids, const
         d.hist = h->hist_base[id] = cells;
         cells += np;
       } else {
-        if (h->sparse_entries.size() >= (1u << 22)) return fail(h, NMG_ERR_CAPACITY, "too many sparse entries");
+        if (h->sparse_entries.size() >= (1u << 22)) return fail_rb(NMG_ERR_CAPACITY, "too many sparse entries");
         d.sidx = (uint32_t)h->sparse_entries.size();
         h->sparse_entries.push_back(id);
       }
     } else if (np > h->npages[id]) {
+      changed.push_back({id, h->hist_base[id], h->npages[id], d});
       if (want_hist && h->hist_base[id] != kHistSparse) {
         if (np * T > max_cells_per_entry || (cells + np) * T > budget_cells || cells + np >= 0xffffffffull)
-          return fail(h, NMG_ERR_CAPACITY, "an object outgrew its page cells past the histogram budget");
+          return fail_rb(NMG_ERR_CAPACITY, "an object outgrew its page cells past the histogram budget");
         moves.push_back({h->hist_base[id], cells, h->npages[id]});
         d.hist = h->hist_base[id] = cells;
         cells += np;
@@ -1112,13 +1174,20 @@ static int grow_entries(nmg_engine* h, uint32_t newE, const uint32_t* ids, const
   uint32_t* hist = nullptr;
   unsigned long long* pk = nullptr;
   DevEntry* ent = nullptr;
+  uint64_t* skeys = nullptr;
+  uint32_t *svals = nullptr, *sdirty = nullptr;
+  const bool new_sparse = nsparse0 == 0 && !h->sparse_entries.empty() && !h->d_sparse_keys;
   auto undo = [&](hipError_t e, const char* what) {
+    (void)hipStreamSynchronize(h->stream);
     (void)hipFree(sum);
     (void)hipFree(mn);
     (void)hipFree(hist);
     (void)hipFree(pk);
     (void)hipFree(ent);
-    return fail(h, NMG_ERR_HIP, std::string("nmg_update_objects: ") + what + ": " + hipGetErrorString(e));
+    (void)hipFree(skeys);
+    (void)hipFree(svals);
+    (void)hipFree(sdirty);
+    return fail_rb(NMG_ERR_HIP, std::string("nmg_update_objects: ") + what + ": " + hipGetErrorString(e));
   };
   hipError_t e;
   if ((e = hipMalloc(&sum, n_sum * 8)) != hipSuccess) return undo(e, "counters");
@@ -1128,6 +1197,13 @@ static int grow_entries(nmg_engine* h, uint32_t newE, const uint32_t* ids, const
   if (newE > kObjSlots && (e = hipMalloc(&pk, (size_t)newE * 2 * 8)) != hipSuccess) return undo(e, "packed counters");
   if ((e = hipMalloc(&ent, (size_t)newE * sizeof(DevEntry))) != hipSuccess) return undo(e, "entries");
   hipStream_t st = h->stream;
+  if (new_sparse) {  // the first sparse entry: its table
+    if ((e = hipMalloc(&skeys, h->sparse_cap * 8)) != hipSuccess || (e = hipMalloc(&svals, h->sparse_cap * 4)) != hipSuccess ||
+        (e = hipMalloc(&sdirty, 2 * 4)) != hipSuccess || (e = hipMemsetAsync(skeys, 0xff, h->sparse_cap * 8, st)) != hipSuccess ||
+        (e = hipMemsetAsync(svals, 0, h->sparse_cap * 4, st)) != hipSuccess ||
+        (e = hipMemsetAsync(sdirty, 0, 2 * 4, st)) != hipSuccess)
+      return undo(e, "sparse page table");
+  }
   if ((e = hipMemsetAsync(sum, 0, n_sum * 8, st)) != hipSuccess ||
       (e = hipMemcpyAsync(sum, h->d_sum64, 2 * kGlobalSums * 8, hipMemcpyDeviceToDevice, st)) != hipSuccess ||
       (oldE && (e = hipMemcpy2DAsync(sum + 2 * kGlobalSums, (size_t)newE * 8, h->d_sum64 + 2 * kGlobalSums,
@@ -1171,14 +1247,10 @@ static int grow_entries(nmg_engine* h, uint32_t newE, const uint32_t* ids, const
   h->n_min64 = n_min;
   h->hist_cells = cells;
   h->E = newE;
-  if (nsparse0 == 0 && !h->sparse_entries.empty() && !h->d_sparse_keys) {  // first sparse entry: its table
-    HIP_TRY(h, hipMalloc(&h->d_sparse_keys, h->sparse_cap * 8));
-    HIP_TRY(h, hipMalloc(&h->d_sparse_vals, h->sparse_cap * 4));
-    HIP_TRY(h, hipMalloc(&h->d_sparse_dirty, 2 * 4));
-    HIP_TRY(h, hipMemsetAsync(h->d_sparse_keys, 0xff, h->sparse_cap * 8, st));
-    HIP_TRY(h, hipMemsetAsync(h->d_sparse_vals, 0, h->sparse_cap * 4, st));
-    HIP_TRY(h, hipMemsetAsync(h->d_sparse_dirty, 0, 2 * 4, st));
-    HIP_TRY(h, hipStreamSynchronize(st));
+  if (new_sparse) {
+    h->d_sparse_keys = skeys;
+    h->d_sparse_vals = svals;
+    h->d_sparse_dirty = sdirty;
   }
   return NMG_OK;
 }
@@ -1273,6 +1345,10 @@ extern "C" int nmg_update_objects(nmg_engine* h, const uint64_t* keys, const uin
     for (uint32_t j = 0; j < n && identity; j++) identity = entry_ids[j] == j;
     if (identity) h->order.clear();
     else h->order.assign(entry_ids, entry_ids + n);
+  } else if (!h->order.empty()) {
+    // a partial table that brought new entries: they follow the known ones,
+    // in id order, until a table lists every entry
+    for (uint32_t id = (uint32_t)h->order.size(); id < h->E; id++) h->order.push_back(id);
   }
   for (nmg_engine* w : h->workers) {  // multi-GPU: the table on every device
     rc = nmg_update_objects(w, keys, entry_off, nb_keys, entry_ids, objects);
@@ -1918,6 +1994,7 @@ static Params base_params(nmg_engine* h, const uint8_t* data, const BufDesc* sde
   p.max64 = h->d_max64;
   p.hist = h->d_hist;
   p.bufcnt = h->d_bufcnt;
+  p.found = h->d_found;
   p.sparse_keys = h->d_sparse_keys;
   p.sparse_vals = h->d_sparse_vals;
   p.sparse_dirty = h->d_sparse_dirty ? h->d_sparse_dirty + (h->nreset & 1) : nullptr;
@@ -2342,8 +2419,6 @@ extern "C" int nmg_synchronize(nmg_engine* h) {
     if (rc) return rc;
   }
   HIP_TRY(h, hipSetDevice(h->device));
-  const int src = route_settle(h);
-  if (src) return src;
   HIP_TRY(h, hipStreamSynchronize(h->stream));
   if (h->launched) {  // the most recent launch's start / end events
     const int slot = (int)((h->nlaunch - 1) % nmg_engine::kRing);
@@ -2394,7 +2469,15 @@ extern "C" uint32_t nmg_get_nb_buffers(nmg_engine* h) {
 }
 
 namespace nmg {
-int engine_download(nmg_engine* h, HostResults& r, bool entries) {
+int engine_download(nmg_engine* h, HostResults& r, bool entries, bool buffer_found) {
+  if (buffer_found && !h->counts_override && !h->multi) {
+    // per-buffer matched counts of the partition-first path: found_kernel
+    // over the match bits (only for callers of the per-buffer counts; the
+    // total below is counted by the analysis itself)
+    HIP_TRY(h, hipSetDevice(h->device));
+    const int rc = route_settle(h);
+    if (rc) return rc;
+  }
   int rc = nmg_synchronize(h);
   if (rc) return rc;
   // (entries == false: the global counters and per-buffer counts only, not
@@ -2427,27 +2510,31 @@ int engine_download(nmg_engine* h, HostResults& r, bool entries) {
     r.levels.assign(sum.begin() + 2 * kGlobalSums + 4 * E, sum.end());
   else
     r.levels.clear();
+  // mem_sampling_finalize accumulates the per-buffer int counters (:334-335);
+  // a buffer holds < 2^29 records (< 4 GiB, Q14), so their sum is the
+  // matched-sample total the kernels count (Params::found)
+  r.nb_samples_total = 0;
+  r.nb_found_total = 0;
   if (h->counts_override) {
     r.buf_samples = h->ov_samples;
     r.buf_found = h->ov_found;
     r.buf_bytes = h->ov_bytes;
+    for (size_t b = 0; b < r.buf_found.size(); b++) r.nb_found_total += (uint64_t)(int64_t)(int32_t)r.buf_found[b];
   } else {
     const size_t n = h->descs.size();
     r.buf_samples.assign(n, 0);
     r.buf_found.assign(n, 0);
     if (n) {
       HIP_TRY(h, hipMemcpy(r.buf_samples.data(), h->d_bufcnt, n * 4, hipMemcpyDeviceToHost));
-      HIP_TRY(h, hipMemcpy(r.buf_found.data(), h->d_bufcnt + h->bufcnt_stride, n * 4, hipMemcpyDeviceToHost));
+      if (buffer_found)
+        HIP_TRY(h, hipMemcpy(r.buf_found.data(), h->d_bufcnt + h->bufcnt_stride, n * 4, hipMemcpyDeviceToHost));
     }
     r.buf_bytes = h->buf_bytes;
+    uint64_t found = 0;
+    if (h->d_found) HIP_TRY(h, hipMemcpy(&found, h->d_found, 8, hipMemcpyDeviceToHost));
+    r.nb_found_total = found;
   }
-  // mem_sampling_finalize accumulates the per-buffer int counters (:334-335)
-  r.nb_samples_total = 0;
-  r.nb_found_total = 0;
-  for (size_t b = 0; b < r.buf_samples.size(); b++) {
-    r.nb_samples_total += (uint64_t)(int64_t)(int32_t)r.buf_samples[b];
-    r.nb_found_total += (uint64_t)(int64_t)(int32_t)r.buf_found[b];
-  }
+  for (size_t b = 0; b < r.buf_samples.size(); b++) r.nb_samples_total += (uint64_t)(int64_t)(int32_t)r.buf_samples[b];
   return NMG_OK;
 }
 
@@ -2465,7 +2552,7 @@ extern "C" int nmg_get_global_counters(nmg_engine* h, nmg_mem_counters out[2], u
   if (!h || !out) return NMG_ERR_INVALID;
   if (!h->have_table) return fail(h, NMG_ERR_STATE, "no object table");
   HostResults r;
-  int rc = engine_download(h, r, false);
+  int rc = engine_download(h, r, false, false);
   if (rc) return rc;
   out[0] = r.global[0];
   out[1] = r.global[1];
@@ -2478,7 +2565,7 @@ extern "C" int nmg_get_buffer_counts(nmg_engine* h, uint32_t* nb_samples, uint32
   if (!h) return NMG_ERR_INVALID;
   if (!h->have_table) return fail(h, NMG_ERR_STATE, "no object table");
   HostResults r;
-  int rc = engine_download(h, r, false);
+  int rc = engine_download(h, r, false, true);
   if (rc) return rc;
   if (nb_samples) memcpy(nb_samples, r.buf_samples.data(), r.buf_samples.size() * 4);
   if (nb_found) memcpy(nb_found, r.buf_found.data(), r.buf_found.size() * 4);
@@ -3049,7 +3136,7 @@ extern "C" int nmg_report(nmg_engine* h, const nmg_object_meta* meta, const nmg_
   const bool timing = getenv("NMG_REPORT_TIMING") != nullptr;  // phase times on stderr
   auto t0 = std::chrono::steady_clock::now();
   HostResults r;
-  int rc = engine_download(h, r);
+  int rc = engine_download(h, r, true, false);  // (the total only: no found_kernel)
   if (rc) return rc;
   auto t1 = std::chrono::steady_clock::now();
   std::vector<uint32_t> rows;
@@ -3087,6 +3174,7 @@ extern "C" int nmg_report(nmg_engine* h, const nmg_object_meta* meta, const nmg_
   if (!h->order.empty()) {
     if (opts && opts->dump_flags) return fail(h, NMG_ERR_STATE, "dump modes need the entries in id order");
     const uint32_t E = h->E;
+    if (h->order.size() != E) return fail(h, NMG_ERR_STATE, "report walk order does not cover every entry");
     std::vector<uint32_t> pos(E);
     w_size.resize(E);
     w_first.resize(E);
@@ -3147,7 +3235,7 @@ extern "C" int nmg_report(nmg_engine* h, const nmg_object_meta* meta, const nmg_
     dump.levels = r.levels.data();
   }
   std::string err;
-  rc = write_report(&res, meta, opts, stdout_path, err, dumps ? &dump : nullptr);
+  rc = write_report(&res, meta, opts, stdout_path, err, dumps ? &dump : nullptr, &r.nb_found_total);
   if (rc && !err.empty()) h->last_error = err;
   return rc;
 }

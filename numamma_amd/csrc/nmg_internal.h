@@ -56,7 +56,9 @@ uint32_t engine_flags(nmg_engine* h);
 const std::vector<uint64_t>& engine_hist_base(nmg_engine* h);  // per entry, kHistSparse if sparse/none
 const std::vector<uint64_t>& engine_npages(nmg_engine* h);     // per entry: buffer_size/4096 + 1
 const std::vector<uint32_t>& engine_sparse_entries(nmg_engine* h);  // sparse idx -> entry
-int engine_download(nmg_engine* h, HostResults& out, bool entries = true);  // entries: the per-entry arrays too
+// entries: the per-entry arrays too; buffer_found: the per-buffer matched
+// counts too (the report needs only their total, nb_found_total)
+int engine_download(nmg_engine* h, HostResults& out, bool entries = true, bool buffer_found = true);
 int engine_download_hist(nmg_engine* h, std::vector<uint32_t>& cells);
 void engine_set_error(nmg_engine* h, const std::string& msg);
 
@@ -82,7 +84,10 @@ struct DumpInput {
 };
 
 // ---- report writer (nmg_report.cpp)
+// found_total: the matched-sample total when r->buf_found is not filled in
+// (the engine's report: the analysis counts it, Params::found)
 int write_report(const nmg_host_results* r, const nmg_object_meta* meta, const nmg_report_options* opts,
-                 const char* stdout_path, std::string& err, const DumpInput* dump = nullptr);
+                 const char* stdout_path, std::string& err, const DumpInput* dump = nullptr,
+                 const uint64_t* found_total = nullptr);
 
 }  // namespace nmg

@@ -142,6 +142,10 @@ struct Params {
   uint64_t* max64;
   uint32_t* hist;
   uint32_t* bufcnt;  // [2][nb_bufs]: samples, found
+  // matched SAMPLEs of every analysis since the last reset (the report's
+  // nb_found_samples_total, mem_sampling.c:335, 357-360): added by each kernel
+  // that attributes, so that an analysis leaves it final
+  unsigned long long* found;
   uint64_t* sparse_keys;
   uint32_t* sparse_vals;
   uint32_t* sparse_dirty;  // set on any sparse insert: the next reset must clear the table
@@ -190,6 +194,7 @@ struct ResetParams {
   uint32_t* sparse_clear;       // the flag the analyses after this reset will set
   uint32_t* bufcnt;
   uint64_t n_bufcnt;
+  unsigned long long* found;  // zeroed
 };
 
 // Launchers (nmg_kernels.hip).  `mode` = kModeDenseObj | kModeDensePage.

@@ -779,10 +779,16 @@ __global__ __launch_bounds__(kWG, 1) void attribute_kernel(Params p) {
       // tallies (mem_sampling.c:921-926)
       if (lane == 0) {
         if (ns0) atomicAdd(p.bufcnt + d0.pad, ns0);
-        if (nf0) atomicAdd(p.bufcnt + p.nb_bufs + d0.pad, nf0);
+        if (nf0) {
+          atomicAdd(p.bufcnt + p.nb_bufs + d0.pad, nf0);
+          atomicAdd(p.found, (unsigned long long)nf0);
+        }
         if (nidx == idx + 2) {
           if (ns1) atomicAdd(p.bufcnt + d1.pad, ns1);
-          if (nf1) atomicAdd(p.bufcnt + p.nb_bufs + d1.pad, nf1);
+          if (nf1) {
+            atomicAdd(p.bufcnt + p.nb_bufs + d1.pad, nf1);
+            atomicAdd(p.found, (unsigned long long)nf1);
+          }
         }
       }
       if (nidx == idx + 1) {
@@ -969,6 +975,7 @@ __global__ __launch_bounds__(256) void reset_kernel(ResetParams r) {
     r.sparse_vals[i] = 0;
   }
   for (uint64_t i = i0; i < r.n_bufcnt; i += stride) r.bufcnt[i] = 0;
+  if (i0 == 0 && r.found) *r.found = 0;
 }
 
 // Multi-GPU merge when the shards share one device: dst op= src over n words

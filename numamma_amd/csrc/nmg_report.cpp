@@ -420,7 +420,7 @@ int write_object_summary(const std::string& path, const nmg_host_results* r, con
 }  // namespace
 
 int write_report(const nmg_host_results* r, const nmg_object_meta* meta, const nmg_report_options* opts,
-                 const char* stdout_path, std::string& err, const DumpInput* dump) {
+                 const char* stdout_path, std::string& err, const DumpInput* dump, const uint64_t* found_override) {
   // NMG_REPORT_TIMING=1: phase times on stderr
   const bool timing = getenv("NMG_REPORT_TIMING") != nullptr;
   auto t_last = std::chrono::steady_clock::now();
@@ -464,6 +464,7 @@ int write_report(const nmg_host_results* r, const nmg_object_meta* meta, const n
     total_bytes += r->buf_bytes[b];
   }
   const uint64_t nb_samples_total = so_far;
+  if (found_override) found_total = *found_override;
   if (!online) {
     fprintf(out, "\n");
     fprintf(out, "%zu bytes processed\n", total_bytes);

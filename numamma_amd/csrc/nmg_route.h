@@ -78,6 +78,7 @@ constexpr uint32_t kDbgLocalNoObj = 0x1000000;   // local pass: no object counte
 constexpr uint32_t kDbgLocalNoPage = 0x2000000;  // local pass: no page cells
 constexpr uint32_t kDbgLocalNoGlobal = 0x4000000;  // local pass: no global counters
 constexpr uint32_t kDbgLocalNoSearch = 0x8000000;  // local pass: no lookup (nothing matches)
+constexpr uint32_t kDbgRouteV2 = 0x20000000;      // route pass: per-wave record streams (route2_kernel)
 constexpr uint32_t kDbgLocalTiming = 0x10000000;  // local pass: per-wave phase cycles in Params::dbg
                                                    // (wait, global, search, match, object, page per chunk;
                                                    // dequeue, setup, flush per item; chunks, items)

@@ -152,6 +152,7 @@ __device__ __forceinline__ void direct_attribute(const Params& p, uint64_t addr,
   if (m.e < 0) return;
   const uint64_t e = (uint64_t)m.e;
   atomicAdd(p.bufcnt + p.nb_bufs + slot, 1u);
+  atomicAdd(p.found, 1ull);
   atomicAdd(reinterpret_cast<unsigned long long*>(p.sum64 + objcw_index(e, acc, 0, p.nb_entries)), 1ull);
   if (w) atomicAdd(reinterpret_cast<unsigned long long*>(p.sum64 + objcw_index(e, acc, 1, p.nb_entries)),
                    (unsigned long long)w);
@@ -528,9 +529,11 @@ __device__ __forceinline__ void route_write_batch(RTimer& rt, const RouteParams&
         if (o < rp.ovf_cap) {
           rp.ovf16[o] = a;
           rp.ovfx[o] = L.pb[q];
-        } else {  // (only SAMPLE records shorter than 40 B get here: NMG_F_SINGLE_PASS handles any number)
-          const XRec xr = x_decode(rp.xl, 0, a);
-          set_error(p, rp.seq0 + xr.g, xr.off, kErrRouteOverflow);
+        } else {  // (only SAMPLE records shorter than 40 B get here) attributed at once, like
+                  // overflow_kernel does, so the default path accepts what the single-pass kernel does
+          XRec xr = x_decode(rp.xl, L.pb[q], a);
+          if (xr.esc) x_resolve(xr, p.data, p.sbufs);
+          direct_attribute(p, xr.addr, xr.ts, xr.w, xr.th, xr.acc, 0, rp.seq0 + xr.g, xr.off, xr.g);
         }
         continue;
       }
@@ -886,6 +889,349 @@ __global__ __launch_bounds__(kWG, 1) void route_kernel(RouteParams rp) {
       for (int k = 0; k < 9; k++) o[k] = rt.acc[k];
       o[9] = win;
       o[10] = nbatches;
+    }
+  }
+  dual_drain(gacc, s_gsums, lane);
+  lds_sync();
+#pragma unroll
+  for (uint32_t a = 0; a < 2; a++) {  // the global mem_counters of both access types
+    if (tid < (int)kGlobalSums && s_gsums[a][tid])
+      atomicAdd(reinterpret_cast<unsigned long long*>(p.sum64 + gsum_index(a, tid)), s_gsums[a][tid]);
+    if (tid < 18 && s_gsums[a][3 + 2 * tid]) {
+      atomicMin(reinterpret_cast<unsigned long long*>(p.min64 + a * 18 + tid), s_gmins[a][tid]);
+      atomicMax(reinterpret_cast<unsigned long long*>(p.max64 + a * 18 + tid), s_gmaxs[a][tid]);
+    }
+  }
+  // open chunks' fill, chunk counts per partition, pool use
+  for (uint32_t q = tid; q < P; q += kWG) {
+    const uint32_t cur = s_cur[nbatches & 1][q];
+    if ((cur & 127u) < kChunk) rp.cmeta[cur >> 7] = q | ((cur & 127u) << 24);
+  }
+  if (tid == 0) rp.used[blockIdx.x] = min(min(s_misc[1], cap), s_misc[2]);
+}
+
+// ---------------------------------------------------------------------------
+// pass 1 with per-wave record streams (route2_kernel; kDbgRouteV2 for now).
+//
+// route_kernel moves one workgroup-wide byte cursor: every window of 1024
+// stride slots ends in a barrier (the fast-path check), and the batch sort
+// adds four more per four windows.  Here each wave owns whole buffers,
+// dequeued from the workgroup's range through an LDS counter, and walks them
+// with its own cursor in windows of 64 stride slots (__analyze_buffer's byte
+// cursor, mem_sampling.c:836-926, per buffer as the reference does it): the
+// fast-path check is a ballot, the slow path (LOST / short / irregular
+// records) is the wave's own header walk, and the per-buffer SAMPLE tally is
+// the wave's.  Only the batch sort synchronises the workgroup: after four
+// windows of every wave (4096 stride slots) the batch is sorted by partition
+// and written to the chunks exactly as in route_kernel.  The next window's
+// loads stay in flight across the window and the batch phases.
+
+constexpr uint32_t kWaves = kWG / 64;
+constexpr uint32_t kWaveWinBytes = 64 * kRecBytes;  // one wave window: 64 stride slots
+constexpr uint32_t kNoBuf = 0xffffffffu;            // RDesc::pad of "no buffer"
+
+__device__ __forceinline__ RDesc no_buf() {
+  RDesc d;
+  d.offset = 0;
+  d.len = 0;
+  d.ta = 0;
+  d.pad = kNoBuf;
+  return d;
+}
+
+// The three record loads of a lane's stride slot of the wave window at
+// (d, c), branch-free (a fixed number of memory ops per window, as
+// rload_slot_nb): a slot that is not a whole record inside the buffer reads
+// `safe` (a valid address) and gets zeros.
+__device__ __forceinline__ void wload(const uint8_t* data, uint64_t safe, uint64_t off, uint32_t len, uint32_t c,
+                                      int lane, RawRec& r) {
+  const uint32_t pos = c + uint32_t(lane) * kRecBytes;
+  const bool ok = uint64_t(pos) + kRecBytes <= len;
+  const uint64_t a = ok ? off + pos : safe;
+  const uint8_t* q = data + a;
+  const uint32_t odd = ok ? (pos >> 3) & 1 : 0u;
+  const uint4 x = *reinterpret_cast<const uint4*>(q + (odd ? 8 : 0));
+  const uint4 y = *reinterpret_cast<const uint4*>(q + (odd ? 24 : 16));
+  const uint2 z = *reinterpret_cast<const uint2*>(q + (odd ? 0 : 32));
+  r.x = ok ? x : make_uint4(0, 0, 0, 0);
+  r.y = ok ? y : make_uint4(0, 0, 0, 0);
+  r.z = ok ? z : make_uint2(0, 0);
+}
+
+// route_partition with the segment table in LDS (uniform reads) instead of
+// kernel arguments, which the compiler would keep in scalar registers
+struct SegL {
+  uint4 a;  // start lo, start hi, base, nslots
+  uint4 b;  // shift, qlast
+};
+__device__ __forceinline__ uint32_t route_partition_l(const SegL* s_seg, uint32_t nseg, const uint64_t* s_pb,
+                                                      const uint16_t* s_pdir, uint64_t addr) {
+  uint4 a = s_seg[0].a;
+  uint4 b = s_seg[0].b;
+  for (uint32_t k = 1; k < nseg; k++) {
+    const uint4 ak = s_seg[k].a, bk = s_seg[k].b;
+    const bool in = addr >= u64of(ak.x, ak.y);
+    a = in ? ak : a;
+    b = in ? bk : b;
+  }
+  const uint64_t rel = (addr - u64of(a.x, a.y)) >> b.x;
+  const uint32_t ns = a.w;
+  const uint32_t e = s_pdir[a.z + (rel < ns ? (uint32_t)rel : ns - 1)];
+  uint32_t q = e & 2047u;
+  const uint32_t c = e >> 11;
+  uint32_t n = (c == kDirCntSat ? b.y - q : c) + 1;  // candidates q .. q + n - 1; s_pb[q] <= addr
+  while (n > 1) {
+    const uint32_t half = n >> 1;
+    if (s_pb[q + half] <= addr) {
+      q += half;
+      n -= half;
+    } else {
+      n = half;
+    }
+  }
+  return q;
+}
+
+__global__ __launch_bounds__(kWG, 1) void route2_kernel(RouteParams rp) {
+  __shared__ uint64_t s_pb[kMaxParts + 1];
+  __shared__ uint16_t s_pdir[kRouteDir];
+  __shared__ uint32_t s_hist[kMaxParts + 1], s_cur[2][kMaxParts + 1], s_nb[kMaxParts + 1];
+  __shared__ uint16_t s_start[kMaxParts + 1];
+  __shared__ uint4 s_desc[kDescLds];
+  __shared__ uint4 s_a16[kRouteBatch];
+  __shared__ uint32_t s_uq[kRouteBatch];
+  __shared__ uint16_t s_perm[kRouteBatch];
+  __shared__ uint32_t s_wlist[kWaves][64];  // slow path: the wave window's SAMPLE offsets
+  __shared__ uint32_t s_wsum[kWG / 64], s_misc[3], s_bnext, s_more[2];
+  __shared__ unsigned long long s_gsums[2][kGlobalSums], s_gmins[2][18], s_gmaxs[2][18];
+  __shared__ SegL s_seg[kRouteSegs];
+
+  Params& p = rp.p;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  if (tid < (int)kRouteSegs) {
+    const RSeg g = rp.seg[tid];
+    s_seg[tid].a = make_uint4((uint32_t)g.start, (uint32_t)(g.start >> 32), g.base, g.nslots);
+    s_seg[tid].b = make_uint4(g.shift, g.qlast, 0, 0);
+  }
+  const uint32_t nseg = rp.nseg;
+  const uint64_t first_start = rp.seg[0].start;
+  const uint32_t P = rp.nparts;
+  const uint32_t c0 = rp.chunk0[blockIdx.x];
+  const uint32_t cap = rp.chunk0[blockIdx.x + 1] - c0;
+  for (uint32_t i = tid; i < kMaxParts + 1; i += kWG) s_pb[i] = rp.pbounds[i];
+  for (uint32_t i = tid; i < kRouteDir; i += kWG) s_pdir[i] = rp.pdir[i];
+  for (uint32_t i = tid; i < P; i += kWG) {
+    s_hist[i] = 0;
+    s_cur[0][i] = kChunk;  // no open chunk (full)
+  }
+  const uint32_t r0 = p.ranges[blockIdx.x], r1 = p.ranges[blockIdx.x + 1];
+  for (uint32_t i = r0 + tid; i < r1 && i - r0 < kDescLds; i += kWG) {
+    const BufDesc d = p.sbufs[i];
+    s_desc[i - r0] = make_uint4((uint32_t)d.offset, (uint32_t)(d.offset >> 32), d.len, d.thread_rank | (d.access << 16));
+  }
+  const RouteLds L{s_hist, s_start, &s_cur[0][0], s_nb, s_a16, s_pb, s_uq, s_perm, s_wsum, s_misc};
+  if (tid == 0) {
+    s_misc[1] = 0;
+    s_misc[2] = kNoChunk;
+    s_bnext = r0;
+    s_more[0] = s_more[1] = 0;
+  }
+  if (tid < (int)kGlobalSums) s_gsums[0][tid] = s_gsums[1][tid] = 0;
+  if (tid < 18) {
+    s_gmins[0][tid] = s_gmins[1][tid] = ~0ull;  // INIT_COUNTER (mem_analyzer.c:415-420)
+    s_gmaxs[0][tid] = s_gmaxs[1][tid] = 0;
+  }
+  DualAcc gacc;  // per-lane update_counters, drained every kDrainWindows windows
+  dual_clear(gacc);
+  uint32_t gwin = 0;
+  lds_sync();
+
+  uint32_t nbatches = 0;
+  if (r0 < r1) {
+    // a valid address for the loads of slots that hold no record
+    const uint64_t safe = __builtin_amdgcn_readfirstlane((uint32_t)p.sbufs[r0].offset) |
+                          (uint64_t(__builtin_amdgcn_readfirstlane((uint32_t)(p.sbufs[r0].offset >> 32))) << 32);
+    auto dequeue = [&]() -> RDesc {
+      uint32_t i = 0;
+      if (lane == 0) i = atomicAdd(&s_bnext, 1u);
+      i = __builtin_amdgcn_readfirstlane(i);
+      return i < r1 ? route_desc(rp, s_desc, r0, i) : no_buf();
+    };
+    // the wave's stream: buffer d0 at cursor cur; d1 = the buffer after it
+    // once dequeued (have1): dequeued only when a window of d1 is prefetched,
+    // so that a wave never holds a buffer it is not about to read
+    RDesc d0 = dequeue(), d1 = no_buf();
+    bool have1 = false;
+    uint32_t cur = 0;
+    uint32_t ns = 0;  // SAMPLEs of d0 so far (mem_sampling.c:921-926)
+    // the window after (b, c) if the window at (b, c) holds only whole 40 B
+    // records (the fast path): its buffer and cursor
+    uint32_t pidx, pcur;
+    auto predict = [&]() -> RDesc {
+      if (d0.pad == kNoBuf) {
+        pidx = kNoBuf;
+        pcur = 0;
+        return d0;
+      }
+      if (cur + kWaveWinBytes < d0.len) {
+        pidx = d0.pad;
+        pcur = cur + kWaveWinBytes;
+        return d0;
+      }
+      if (!have1) {
+        d1 = dequeue();
+        have1 = true;
+      }
+      pidx = d1.pad;
+      pcur = 0;
+      return d1;
+    };
+    RawRec ra, rb;
+    wload(p.data, safe, d0.offset, d0.len, 0, lane, ra);
+    {
+      const RDesc e = predict();
+      wload(p.data, safe, e.offset, e.len, pcur, lane, rb);
+    }
+
+    // one window of this wave: A holds its slots, B the next window's (in
+    // flight); k = the window's place in the batch (staging slots)
+    auto window = [&](RawRec& A, RawRec& B, uint32_t k) {
+      const RDesc dw = d0;  // this window's buffer
+      const uint32_t pos = cur + uint32_t(lane) * kRecBytes;
+      const bool cand = pos < dw.len;
+      Rec rec = decode_rec(A, pos);
+      const bool bad = cand && (uint64_t(pos) + kRecBytes > dw.len || (rec.hdr >> 48) != kRecBytes);
+      bool valid;
+      uint32_t roff = pos, ncur;
+      if (!__ballot(bad) && !(cur & 7)) {
+        valid = cand && uint32_t(rec.hdr) == kSampleType;
+        ncur = cur + kWaveWinBytes;
+      } else {
+        // ---- slow path: the wave follows the header chain from cur
+        // (non-SAMPLE records skipped by size, size 0 / truncation /
+        // misalignment flagged), listing up to 64 SAMPLE offsets
+        const uint8_t* base = p.data + dw.offset;
+        const uint64_t len = dw.len;
+        uint64_t q0 = cur;
+        uint32_t n = 0, err = 0;
+        if (cur & 7) err = kErrUnaligned;
+        while (!err && q0 < len && n < 64) {
+          const uint64_t q = q0 + uint64_t(lane) * kRecBytes;
+          const uint64_t hdr = (q + 8 <= len) ? *reinterpret_cast<const uint64_t*>(base + q) : 0;
+          const bool reg = q + kRecBytes <= len && (hdr >> 48) == kRecBytes;
+          const uint64_t rm = __ballot(reg);
+          const uint32_t run = ~rm ? (uint32_t)__builtin_ctzll(~rm) : 64u;
+          const uint32_t take = min(run, 64u - n);
+          const bool smp = (uint32_t)lane < take && uint32_t(hdr) == kSampleType;
+          const uint64_t sm = __ballot(smp);
+          if (smp) s_wlist[wave][n + (uint32_t)__popcll(sm & ((1ull << lane) - 1))] = (uint32_t)q;
+          n += (uint32_t)__popcll(sm);
+          q0 += uint64_t(take) * kRecBytes;
+          if (take < run || run == 64 || q0 >= len || n >= 64) continue;
+          if (q0 + 8 > len) {
+            err = kErrTruncated;
+            break;
+          }
+          const uint64_t h = (uint64_t)__shfl(hdr, (int)run, 64);
+          const uint32_t size = uint32_t(h >> 48);
+          if (size == 0) {  // mem_sampling.c:857-860
+            err = kErrZeroSize;
+            break;
+          }
+          if (size & 7) {
+            err = kErrUnaligned;
+            break;
+          }
+          if (uint32_t(h) == kSampleType) {
+            if (q0 + kRecBytes > len || q0 + size > len) {
+              err = kErrTruncated;
+              break;
+            }
+            if (lane == 0) s_wlist[wave][n] = (uint32_t)q0;
+            n++;
+          }
+          q0 += size;  // non-SAMPLE records are skipped by their size (:918)
+        }
+        if (err && lane == 0) set_error(p, rp.seq0 + dw.pad, (uint32_t)q0, err);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+        ncur = err ? (uint32_t)len : (uint32_t)min(q0, len);
+        valid = (uint32_t)lane < n;
+        roff = valid ? s_wlist[wave][lane] : 0u;
+        RawRec rr;
+        load_rec(base, roff, valid ? len : 0, rr);
+        rec = decode_rec(rr, roff);
+        vm_drain();
+      }
+      ns += (uint32_t)__popcll(__ballot(valid));
+      // ---- advance the stream; dw's tally when it is done
+      if (dw.pad != kNoBuf) {
+        if (ncur >= dw.len) {
+          if (lane == 0 && ns) atomicAdd(p.bufcnt + dw.pad, ns);
+          ns = 0;
+          cur = 0;
+          if (have1) {
+            d0 = d1;
+          } else {
+            d0 = dequeue();
+          }
+          have1 = false;
+          d1 = no_buf();
+        } else {
+          cur = ncur;
+        }
+      }
+      // ---- the next window's loads again if it is not where B was loaded
+      // (after a slow-path window), then the loads of the window after it
+      if (d0.pad != pidx || (d0.pad != kNoBuf && cur != pcur)) {
+        wload(p.data, safe, d0.offset, d0.len, cur, lane, B);
+        vm_drain();  // (rare: keeps the waits on the common path exact)
+      }
+      {
+        const RDesc e = predict();
+        wload(p.data, safe, e.offset, e.len, pcur, lane, A);
+      }
+
+      // ---- this window's records: update_counters(global_counters, sample)
+      // (mem_sampling.c:882: every SAMPLE, matched or not), partition, batch
+      // rank, staging slot
+      const uint32_t acc_l = dw.access();
+      if (valid) route_count(gacc, s_gsums, s_gmins, s_gmaxs, acc_l, uint32_t(rec.dsrc >> 5) & 0x3fff, rec.w);
+      if (++gwin == kDrainWindows) {
+        dual_drain(gacc, s_gsums, lane);
+        gwin = 0;
+      }
+      // below the first key ht_lower_key finds no node: counted, not routed
+      const bool routed = valid && rec.addr >= first_start;
+      const uint32_t q = routed ? route_partition_l(s_seg, nseg, s_pb, s_pdir, rec.addr) : 0u;
+      Held hr;
+      hr.q = kNoChunk;
+      if (routed) {
+        const uint64_t pbq = s_pb[q];
+        const uint32_t rk = atomicAdd(&s_hist[q], 1u);
+        hr.q = q | (rk << 11);
+        hr.a = x_encode(rp.xl, pbq, rec.addr, rec.ts, rec.w, dw.pad, roff, dw.thread_rank(), acc_l);
+      }
+      route_stage(L, hr, k, tid);
+    };
+
+    RTimer rt;  // (unused: no timing instance)
+    while (true) {
+      for (uint32_t k = 0; k < kRouteWindows; k += 2) {
+        window(ra, rb, k);
+        window(rb, ra, k + 1);
+      }
+      if (lane == 0 && d0.pad != kNoBuf) atomicOr(&s_more[nbatches & 1], 1u);
+      route_sort_batch<false>(rt, rp, tid, L, nbatches, kRouteWindows, c0, cap);
+      const uint32_t more = __builtin_amdgcn_readfirstlane(s_more[nbatches & 1]);
+      if (tid == 0) s_more[(nbatches + 1) & 1] = 0;
+      vm_drain();  // (the prefetched window has long arrived: the chunk stores alone stay in flight)
+      route_write_batch<false>(rt, rp, tid, L, nbatches);
+      nbatches++;
+      lds_sync();  // every wave has gathered the batch from the staging slots
+      if (!more) break;
     }
   }
   dual_drain(gacc, s_gsums, lane);
@@ -1291,7 +1637,18 @@ __global__ __launch_bounds__(kWG, 1) void local_kernel(LocalParams lp) {
     }
     lds_sync();
     rt_stamp<TIMING>(rt, 8);  // (waiting for the item's slowest wave counts as flush)
-    for (uint32_t i = tid; i < nl; i += kWG) lp.cmatch[s_clist[i] & ((1u << kChunkIdBits) - 1)] = s_cm[i];
+    {  // the chunks' match bits (per-buffer counts, found_kernel) and the item's matched total
+      uint32_t nf = 0;
+      for (uint32_t i = tid; i < nl; i += kWG) {
+        const unsigned long long m = s_cm[i];
+        lp.cmatch[s_clist[i] & ((1u << kChunkIdBits) - 1)] = m;
+        nf += (uint32_t)__popcll(m);
+      }
+      if (__ballot(nf != 0)) {
+        const uint32_t t = wave_sum_u32(nf);
+        if (lane == 0 && t) atomicAdd(p.found, (unsigned long long)t);
+      }
+    }
     // the item's counters to global memory: consecutive lanes, consecutive words
     for (uint32_t i = tid; i < pi.ne; i += kWG) {
       const uint64_t e = pi.e0 + i;
@@ -1372,7 +1729,8 @@ __global__ __launch_bounds__(kWG) void found_kernel(FoundParams r) {
 // launchers
 
 hipError_t launch_route(uint32_t grid, hipStream_t s, const RouteParams& r) {
-  if (r.p.flags & kDbgRouteTiming) hipLaunchKernelGGL(route_kernel<true>, dim3(grid), dim3(kWG), 0, s, r);
+  if (r.p.flags & kDbgRouteV2) hipLaunchKernelGGL(route2_kernel, dim3(grid), dim3(kWG), 0, s, r);
+  else if (r.p.flags & kDbgRouteTiming) hipLaunchKernelGGL(route_kernel<true>, dim3(grid), dim3(kWG), 0, s, r);
   else hipLaunchKernelGGL(route_kernel<false>, dim3(grid), dim3(kWG), 0, s, r);
   return hipGetLastError();
 }

@@ -5,6 +5,9 @@ import sys
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+# the tests drive internal switches (pool sizes, route variants, ...) through
+# nmg_options.flags; the library accepts bits outside NMG_F_ALL only with this
+os.environ.setdefault("NMG_INTERNAL_FLAGS", "1")
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "oracle"))
 sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))

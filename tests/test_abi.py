@@ -3,6 +3,7 @@ declares, and fails loudly (no CPU fallback) when no GPU is present."""
 import ctypes as C
 import os
 import subprocess
+import sys
 
 import pytest
 import torch
@@ -65,3 +66,82 @@ def test_options_abi_version_matches_header():
     assert _lib.NMG_OPTIONS_ABI == 0x4E4D4702
     assert C.sizeof(_lib.nmg_options) == 48
     assert _lib.nmg_options.abi_version.offset == 36 and _lib.nmg_options.devices.offset == 40
+
+
+def _opts(**kw):
+    o = _lib.nmg_options()
+    o.device = 0
+    o.flags = _lib.NMG_F_DEFAULT
+    o.nb_threads = 8
+    for k, v in kw.items():
+        setattr(o, k, v)
+    return o
+
+
+def _create(o, size=None):
+    h = C.c_void_p()
+    if size is None:
+        rc = _lib.lib.nmg_create(C.byref(h), C.byref(o))
+    else:
+        rc = _lib.lib.nmg_create_ex(C.byref(h), C.byref(o), size)
+    if rc == 0:
+        _lib.lib.nmg_destroy(h)
+    return rc
+
+
+def test_internal_flag_bits_rejected(monkeypatch):
+    """Bits outside NMG_F_ALL (the internal ablation switches, e.g. 0x200 no
+    global counters, 0x1000000 no object counters) are refused with
+    NMG_ERR_INVALID before any GPU call, unless NMG_INTERNAL_FLAGS is set."""
+    monkeypatch.delenv("NMG_INTERNAL_FLAGS", raising=False)
+    for bad in (0x200, 0x1000000, 0x8000000, 0x20, 0x80000000):
+        assert _create(_opts(flags=_lib.NMG_F_DEFAULT | bad)) == -1, hex(bad)
+    detail = C.create_string_buffer(512)
+    _lib.lib.nmg_get_last_error_detail(None, detail, 512)
+    assert b"NMG_F_ALL" in detail.value
+    # public flags pass validation (then: an engine, or NMG_ERR_HIP without a GPU)
+    assert _create(_opts(flags=_lib.NMG_F_ALL)) in (0, -2)
+    monkeypatch.setenv("NMG_INTERNAL_FLAGS", "1")
+    assert _create(_opts(flags=_lib.NMG_F_DEFAULT | 0x20000)) in (0, -2)
+
+
+def test_multi_gpu_without_abi_version_rejected(monkeypatch):
+    """nb_gpus > 1 is used only with abi_version = NMG_OPTIONS_ABI; without it
+    nmg_create fails instead of building a silent one-GPU engine."""
+    devs = (C.c_int32 * 2)(0, 1)
+    assert _create(_opts(nb_gpus=2, devices=devs)) == -1
+    assert _create(_opts(nb_gpus=2, abi_version=0x4E4D4701, devices=devs)) == -1
+    assert _create(_opts(nb_gpus=1)) in (0, -2)  # one GPU: nothing to gate
+
+
+def test_create_ex_reads_only_the_first_struct_version(tmp_path):
+    """A first-version caller's 32-byte nmg_options placed right before an
+    unreadable page: nmg_create_ex(opt, NMG_OPTIONS_V1_SIZE) reads only those
+    bytes (an over-read would fault the child process)."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = r"""
+import ctypes as C, mmap, sys
+sys.path.insert(0, %r)
+from numamma_amd import _lib
+libc = C.CDLL(None)
+m = mmap.mmap(-1, 2 * mmap.PAGESIZE)
+base = C.addressof(C.c_char.from_buffer(m))
+assert libc.mprotect(C.c_void_p(base + mmap.PAGESIZE), C.c_size_t(mmap.PAGESIZE), 0) == 0
+o = _lib.nmg_options(); o.device = 0; o.flags = _lib.NMG_F_DEFAULT; o.nb_threads = 4
+p = base + mmap.PAGESIZE - _lib.NMG_OPTIONS_V1_SIZE
+C.memmove(p, C.addressof(o), _lib.NMG_OPTIONS_V1_SIZE)
+h = C.c_void_p()
+rc = _lib.lib.nmg_create_ex(C.byref(h), C.c_void_p(p), _lib.NMG_OPTIONS_V1_SIZE)
+if rc == 0: _lib.lib.nmg_destroy(h)
+bad = _lib.nmg_options(); bad.flags = 0x200
+C.memmove(p, C.addressof(bad), _lib.NMG_OPTIONS_V1_SIZE)
+rc2 = _lib.lib.nmg_create_ex(C.byref(h), C.c_void_p(p), _lib.NMG_OPTIONS_V1_SIZE)
+rc3 = _lib.lib.nmg_create_ex(C.byref(h), C.c_void_p(p), 16)
+print(rc, rc2, rc3)
+""" % root
+    env = dict(os.environ)
+    env.pop("NMG_INTERNAL_FLAGS", None)
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=env, timeout=120)
+    assert out.returncode == 0, out.stderr[-2000:]
+    rc, rc2, rc3 = map(int, out.stdout.split()[-3:])
+    assert rc in (0, -2) and rc2 == -1 and rc3 == -1

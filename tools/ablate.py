@@ -11,6 +11,7 @@ import time
 import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+os.environ.setdefault("NMG_INTERNAL_FLAGS", "1")  # (internal ablation / timing switches)
 sys.path.insert(0, ROOT)
 
 VARIANTS = {
@@ -24,6 +25,7 @@ VARIANTS = {
     # large tables: the partition-first path (nmg_route.h) and its parts
     "legacy": 0x3 | 0x10000,            # attribute_kernel on a large table (kDbgNoRoute)
     "route": 0x3,                       # route + plan + scatter + local (default for > 1023 keys)
+    "route_v2": 0x3 | 0x20000000,       # ... with the per-wave route pass (route2_kernel)
     "route_nopages": 0x1,               # ... without the page histogram
     "route_noloc": 0x3 | 0x400000,      # local pass loads its chunks only
     "route_nowrite": 0x3 | 0x100000 | 0x400000,  # batches sorted in LDS, no chunk stores (local: loads only)
@@ -72,6 +74,7 @@ def main():
             engines[v] = e
         print(f"# {wname}: generated in {time.time() - t0:.1f}s", file=sys.stderr, flush=True)
         times = {v: [] for v in engines}
+        first = {v: [] for v in engines}
         for r in range(args.reps + 2):
             for v, e in engines.items():
                 e.reset()
@@ -79,9 +82,11 @@ def main():
                 e.synchronize()
                 if r >= 2:
                     times[v].append(e.last_analyze_ms())
+                    first[v].append(e.phase_times(1)[0][-1])
         for v, ts in times.items():
             med = float(np.median(ts))
             print(json.dumps({"workload": wname, "variant": v, "median_ms": med, "min_ms": float(np.min(ts)),
+                              "first_kernel_ms": float(np.median(first[v])),
                               "GBps": nbytes / med / 1e6, "Gsamples_s": nbytes / 40 / med / 1e6}), flush=True)
         for e in engines.values():
             e.close()

@@ -14,6 +14,7 @@ import time
 import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+os.environ.setdefault("NMG_INTERNAL_FLAGS", "1")  # (internal ablation / timing switches)
 sys.path.insert(0, ROOT)
 
 VARIANTS = {"load_only": 0x100, "lookup_only": 0x1 | 0x200 | 0x800, "full": 0x3}

@@ -21,6 +21,7 @@ import time
 import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+os.environ.setdefault("NMG_INTERNAL_FLAGS", "1")  # (internal switches: one-rank RCCL branch)
 sys.path.insert(0, ROOT)
 
 WORKLOADS = {
