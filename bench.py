@@ -224,6 +224,9 @@ def main():
                     "ms_per_step": se * 1e3 / sn, "steps": sn,
                     "attribute_kernel_ms": float(np.mean(sa)), "launch_ms": float(np.mean(st)),
                     "roofline_frac": s.samples * RECORD_BYTES / (float(np.mean(sa)) * 1e-3) / 1e9 / HBM_PEAK_GBS}
+                if s.name == "c2" and not args.no_cpu_baseline:
+                    # BASELINE.md:34-38: the reference loop timed at configs[1], the whole workload
+                    out["secondary"][s.name]["cpu_reference_loop"] = reference_loop_full(s.rp)
                 s.eng.close()
                 del s
         if world == 1 and not args.no_cpu_baseline:
@@ -419,6 +422,33 @@ def _rate_runs(fn, target_s, max_runs, tag):
     return float(np.median(rates)), rates, secs, recs
 
 
+def reference_loop_full(rp, target_s=10.0, max_runs=5):
+    """The single-threaded C restatement of the reference loop
+    (oracle/nmg_oracle.c: mem_sampling_finalize's while(samples) loop,
+    mem_sampling.c:311-346, with the reference's linear call-site and page
+    lists) over a WHOLE workload (configs[1]: 10M records, 1k intervals),
+    analysis loop timed, repeated to about target_s seconds; median rate."""
+    import tempfile
+
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle
+
+    with tempfile.TemporaryDirectory() as d:
+        path = os.path.join(d, "full.bin")
+        rp.write(path)
+
+        def run():
+            t = pyoracle.run(path, os.path.join(d, "out"), os.path.join(d, "stdout.txt"))
+            return t["nb_samples"], t["analysis_s"]
+
+        v, rates, secs, recs = _rate_runs(run, target_s, max_runs, "reference loop, whole workload")
+    return {"value": v, "unit": "samples/s", "cores": 1, "kind": "port", "runs": rates,
+            "spread": [float(min(rates)), float(max(rates))],
+            "sample": f"the whole workload ({recs} records, {len(rp.buffers)} buffers) analysed {len(rates)}x by the "
+                      f"single-threaded restatement of the reference loop ({secs:.1f}s), median run; 1 core of "
+                      f"{os.cpu_count()} (OMP_NUM_THREADS={os.environ.get('OMP_NUM_THREADS', 'unset')})"}
+
+
 def cpu_baseline(rp, max_records, mt_records, threads, st_records, target_s=20.0, max_runs=15):
     """CPU baselines timed on this host on bounded samples of the same
     workload (the first buffers of the batch, against the full object table);
@@ -466,6 +496,7 @@ def cpu_baseline(rp, max_records, mt_records, threads, st_records, target_s=20.0
                       f"{len(rates)}x by the multi-threaded bit-exact restatement (oracle/nmg_cpu_mt.cpp) on "
                       f"{threads} threads ({secs:.1f}s of analysis + merge), median run; {host}",
             "runs": rates,
+            "spread": [float(min(rates)), float(max(rates))],
         }
         os.remove(path)
         sub, n = _sample_replay(rp, st_records)

@@ -25,6 +25,15 @@
  *    per-thread init first (a 64 KiB per-thread buffer, like
  *    mem_sampling_thread_init's sample rings; mem_intercept.c:325-387).
  *
+ *  - NMG_INTERPOSE_CANARY_CHECK=0 reproduces NumaMMa's default setting
+ *    (settings.canary_check = 0, numamma.h.in:41): CANARY_OK is then always
+ *    true (mem_intercept.h:68), so free() and realloc() take every pointer
+ *    for one of theirs and read its header (mem_intercept.c:266-298,
+ *    159-183) -- a block the interposer did not allocate (memalign & co,
+ *    which it does not wrap either) hands a garbage pointer to libc.  With
+ *    the check on (the default here, NumaMMa's --canary-check), free() passes
+ *    such a block to libc, and realloc() aborts on it like the reference.
+ *
  * At exit it prints one line on stderr:
  *   nmg_interpose: {"recorded": R, "freed": F, "foreign_frees": X, "hand_made": H,
  *                   "threads": T, "unsafe_skips": S}
@@ -74,6 +83,7 @@ static size_t hand_next;
 static __thread int in_dlsym;
 
 static unsigned long n_recorded, n_freed, n_foreign, n_hand, n_threads, n_skips;
+static int canary_check = 1; /* NMG_INTERPOSE_CANARY_CHECK (read once, in resolve) */
 
 /* records: open addressing on the user pointer, mmap'ed (not the wrapped allocator) */
 struct rec {
@@ -98,6 +108,10 @@ static void resolve(void) {
   real_pthread_create = (int (*)(pthread_t *, const pthread_attr_t *, void *(*)(void *), void *))dlsym(
       RTLD_NEXT, "pthread_create");
   in_dlsym--;
+  {
+    const char *e = getenv("NMG_INTERPOSE_CANARY_CHECK");
+    canary_check = !(e && e[0] == '0');
+  }
   if (!real_malloc || !real_free || !real_calloc || !real_realloc) {
     static const char m[] = "nmg_interpose: dlsym failed\n";
     (void)!write(2, m, sizeof m - 1);
@@ -130,6 +144,15 @@ static void *hand_made(size_t size) {
 static int ours(void *user) {
   if (!user || ((uintptr_t)user & 15)) return 0;
   return ((struct blk_head *)((unsigned char *)user - HEAD))->canary == CANARY;
+}
+
+/* CANARY_OK (mem_intercept.h:68): always true without the canary check */
+static int canary_ok(void *user) {
+  if (!canary_check) {
+    if (!ours(user)) __atomic_fetch_add(&n_foreign, 1, __ATOMIC_RELAXED); /* (counted, then trusted) */
+    return 1;
+  }
+  return ours(user);
 }
 
 static size_t slot_of(void *p) { return (size_t)(((uintptr_t)p >> 4) * 0x9E3779B97F4A7C15ull >> 42) & (REC_SLOTS - 1); }
@@ -224,19 +247,19 @@ void free(void *ptr) {
   struct blk_head *h;
   if (!ptr) return;
   resolve();
-  if (!ours(ptr)) { /* not ours (memalign & co): libc's */
+  if (!canary_ok(ptr)) { /* not ours (memalign & co): libc's */
     __atomic_fetch_add(&n_foreign, 1, __ATOMIC_RELAXED);
     real_free(ptr);
     return;
   }
   h = (struct blk_head *)((unsigned char *)ptr - HEAD);
-  if (memcmp(h->tail, &(uint64_t){CANARY}, 8) != 0) {
+  if (canary_check && memcmp(h->tail, &(uint64_t){CANARY}, 8) != 0) {
     static const char m[] = "nmg_interpose: tail canary erased\n";
     (void)!write(2, m, sizeof m - 1);
     abort();
   }
   if (h->kind == KIND_HAND) return;
-  if (nmg_interpose_unsafe == 0) record_free(h);
+  if (nmg_interpose_unsafe == 0 && (h->kind == KIND_MALLOC || h->kind == KIND_NEW)) record_free(h);
   h->canary = 0;
   real_free(h->raw);
 }
@@ -260,7 +283,11 @@ void *realloc(void *ptr, size_t size) {
     return NULL;
   }
   resolve();
-  if (!ours(ptr)) return real_realloc(ptr, size);
+  if (!canary_ok(ptr)) { /* mem_intercept.c:159-166: "I can't find this pointer !" */
+    static const char m[] = "nmg_interpose: realloc of a block it did not allocate\n";
+    (void)!write(2, m, sizeof m - 1);
+    abort();
+  }
   h = (struct blk_head *)((unsigned char *)ptr - HEAD);
   if (h->kind == KIND_HAND) { /* emulate: copy out of the arena */
     void *p = malloc(size);

@@ -11,7 +11,13 @@
   come from one run and one replay reproduces both;
 * readme_callsite_summary.dat -- README.md:159-175, a `callsite_summary_<id>.dat`
   of the dump mode (-d): one site's read counters per memory level (L1, L2,
-  L3, LFB, local RAM hits, with their total weights) and 12040 L1 write hits.
+  L3, LFB, local RAM hits, with their total weights) and 12040 L1 write hits;
+* readme_callsite_dump.dat -- README.md:141-148, a `callsite_dump_<id>.dat` of
+  the dump mode: six samples of one site, one row each (thread, timestamp,
+  offset in the object, get_data_src_level string, weight).  The README
+  predates the trailing access_type column that _dump_call_site prints
+  (mem_sampling.c:792-804), so the first five columns and the header without
+  that column are compared (dump_rows).
 
 Everything these blocks print is a per-site aggregate, so any sample stream
 with those aggregates reproduces them; the builders below choose one
@@ -46,6 +52,7 @@ SRC = "/home/trahay/Soft/opt/numamma/test/mat_mul.c"
 CALL_SITES = os.path.join(HERE, "readme_call_sites.log")
 COUNTERS_3 = os.path.join(HERE, "readme_callsite_counters_3.dat")
 SUMMARY = os.path.join(HERE, "readme_callsite_summary.dat")
+DUMP = os.path.join(HERE, "readme_callsite_dump.dat")
 
 READ, WRITE = 0, 1
 PAGE = 4096
@@ -275,6 +282,39 @@ def build_summary() -> Replay:
           np.full(SUMMARY_WRITES, LVL_L1 | LVL_HIT, dtype=np.uint64))
     buffers = _buffers(L.records(0, READ, rng), 0, READ) + _buffers(L.records(0, WRITE, rng), 0, WRITE)
     return Replay(1, table, buffers, {"fixture": "README.md:159-175"})
+
+
+# callsite_dump (README.md:141-148): thread 0, (timestamp, offset, level, weight) in analysis order
+DUMP_ROWS = [(14087247746057, 5864, LVL_L1, 0), (14087248615826, 3872, LVL_L1, 0), (14087249526638, 1888, LVL_L1, 0),
+             (14087250387561, 7912, LVL_L1, 0), (14088660667040, 5776, LVL_L3, 50), (14088923322555, 6376, LVL_L2, 46)]
+
+
+def build_dump() -> Replay:
+    """README.md:141-148: one 12000-byte object of one heap site, six read
+    samples of thread 0 in one buffer; analysed in dump mode (-d) the site
+    (id 1: the first and only one matched) gets callsite_dump_1.dat."""
+    table, _ = _table([("74", 1, 0, 0, 0)], OBJ_SIZE)
+    table.entries["alloc_date"][0] = 14_000_000_000_000
+    table.entries["free_date"][0] = 14_100_000_000_000
+    base = np.uint64(table.keys[0])
+    rec = np.zeros(len(DUMP_ROWS), dtype=RECORD_DTYPE)
+    rec["type"] = 9  # PERF_RECORD_SAMPLE
+    rec["misc"] = 2
+    rec["size"] = 40
+    for i, (ts, off, lvl, w) in enumerate(DUMP_ROWS):
+        rec["timestamp"][i] = ts
+        rec["addr"][i] = base + np.uint64(off)
+        rec["weight"][i] = w
+        rec["data_src"][i] = (np.uint64(lvl | LVL_HIT) << np.uint64(5)) | np.uint64(MEM_OP_LOAD)
+    return Replay(1, table, _buffers(rec, 0, READ), {"fixture": "README.md:141-148"})
+
+
+def dump_rows(path):
+    """A callsite_dump file as the README shows it: the header without
+    ' access_type', each row's first five columns."""
+    lines = [x for x in open(path).read().splitlines() if x.strip()]
+    head = lines[0].replace(" access_type", "")
+    return [head] + [" ".join(x.split()[:5]) for x in lines[1:]]
 
 
 def expected(path):

@@ -1,7 +1,7 @@
-"""README golden vectors on the GPU (README.md:115-131, 159-175; replays from
+"""README golden vectors on the GPU (README.md:115-131, 141-148, 159-175; replays from
 tests/golden/readme_sites_fixture.py): the engine's call_sites.log,
-callsite_counters_3.dat and dump-mode callsite_summary_1.dat equal the README
-blocks, and every output file equals the oracle's byte for byte."""
+callsite_counters_3.dat and dump-mode callsite_dump_1.dat / callsite_summary_1.dat
+equal the README blocks, and every output file equals the oracle's byte for byte."""
 import os
 
 import pytest
@@ -58,5 +58,30 @@ def test_readme_callsite_summary_on_gpu(tmp_path):
     eng.report(edir, os.path.join(d, "e.txt"), dump_flags=_lib.NMG_DUMP_CALLSITES)
     eng.close()
     assert F.produced(os.path.join(edir, "callsite_summary_1.dat")) == F.expected(F.SUMMARY)
+    assert open(os.path.join(d, "o.txt"), "rb").read() == open(os.path.join(d, "e.txt"), "rb").read()
+    _same_dirs(odir, edir)
+
+
+def test_readme_callsite_dump_on_gpu(tmp_path):
+    """Dump mode (-d): the six README rows of callsite_dump_1.dat from the
+    engine's per-record matches (first five columns; the README has no
+    access_type column)."""
+    from numamma_amd.engine import Engine
+
+    d = str(tmp_path)
+    rp = F.build_dump()
+    path = os.path.join(d, "r.bin")
+    rp.write(path)
+    odir, edir = os.path.join(d, "o"), os.path.join(d, "e")
+    pyoracle.run(path, odir, os.path.join(d, "o.txt"), dump=True)
+    eng = Engine(flags=_lib.NMG_F_DEFAULT | _lib.NMG_F_SAMPLE_MATCHES | _lib.NMG_F_OBJECT_LEVELS,
+                 nb_threads=rp.nb_threads)
+    eng.set_objects(rp.table)
+    eng.submit_replay(rp)
+    eng.analyze()
+    eng.synchronize()
+    eng.report(edir, os.path.join(d, "e.txt"), dump_flags=_lib.NMG_DUMP_CALLSITES)
+    eng.close()
+    assert F.dump_rows(os.path.join(edir, "callsite_dump_1.dat")) == F.dump_rows(F.DUMP)
     assert open(os.path.join(d, "o.txt"), "rb").read() == open(os.path.join(d, "e.txt"), "rb").read()
     _same_dirs(odir, edir)

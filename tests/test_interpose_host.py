@@ -10,6 +10,8 @@ import json
 import os
 import subprocess
 
+import pytest
+
 import pyoracle
 from numamma_amd.replay import SynthConfig, generate
 
@@ -33,7 +35,12 @@ def interposer_stats(stderr: str):
     return json.loads(lines[-1][len("nmg_interpose: "):])
 
 
-def test_capture_bridge_under_interposer(tmp_path):
+@pytest.mark.parametrize("canary_check", ["1", "0"])
+def test_capture_bridge_under_interposer(tmp_path, canary_check):
+    """canary_check "0" is NumaMMa's default (numamma.h.in:41): free() trusts
+    every pointer's header (mem_intercept.h:68), so the process must free
+    nothing it did not allocate through the wrapped malloc -- the capture
+    bridge frees none."""
     d = str(tmp_path)
     rp = generate(SynthConfig(nb_samples=60_000, nb_intervals=800, lost_frac=1e-3, wrap_one=True, seed=81))
     path = os.path.join(d, "replay.bin")
@@ -45,10 +52,12 @@ def test_capture_bridge_under_interposer(tmp_path):
         f.write("#!/bin/sh\ncase \"$LD_PRELOAD\" in *libnmg_interpose*) exit 3;; esac\ncp \"$1\" \"$2\"\n")
     os.chmod(helper, 0o755)
     r = subprocess.run([os.path.join(BIN, "nmg_c99_host"), "--bridge", path, copy, os.path.join(d, "h.txt")],
-                       env=interposed_env(NMG_BRIDGE_HELPER=helper), capture_output=True, text=True, timeout=120)
+                       env=interposed_env(NMG_BRIDGE_HELPER=helper, NMG_INTERPOSE_CANARY_CHECK=canary_check),
+                       capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr
     st = interposer_stats(r.stderr)
     assert st["recorded"] > 0 and st["hand_made"] >= 0
+    assert st["foreign_frees"] == 0
     pyoracle.run(path, os.path.join(d, "o"), os.path.join(d, "o.txt"))
     pyoracle.run(copy, os.path.join(d, "c"), os.path.join(d, "c.txt"))
     assert open(os.path.join(d, "o.txt"), "rb").read() == open(os.path.join(d, "c.txt"), "rb").read()

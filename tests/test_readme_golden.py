@@ -1,6 +1,7 @@
-"""Golden vectors from the reference README (README.md:115-131, 159-175), on
-the CPU: the oracle reproduces call_sites.log, callsite_counters_3.dat and a
-dump-mode callsite_summary_<id>.dat block exactly (tests/golden/
+"""Golden vectors from the reference README (README.md:115-131, 141-148,
+159-175), on the CPU: the oracle reproduces call_sites.log,
+callsite_counters_3.dat and the dump-mode callsite_dump_<id>.dat and
+callsite_summary_<id>.dat blocks exactly (tests/golden/
 readme_sites_fixture.py builds the replays), and the product's report writer
 (numamma_amd.results.report_host, the C++ report of the C-ABI) prints the same
 call_sites.log and callsite_counters files from the oracle's raw counters."""
@@ -40,3 +41,12 @@ def test_readme_callsite_summary(tmp_path):
     odir = os.path.join(d, "o")
     pyoracle.run(path, odir, os.path.join(d, "o.txt"), dump=True)
     assert F.produced(os.path.join(odir, "callsite_summary_1.dat")) == F.expected(F.SUMMARY)
+
+
+def test_readme_callsite_dump(tmp_path):
+    d = str(tmp_path)
+    path = os.path.join(d, "r.bin")
+    F.build_dump().write(path)
+    odir = os.path.join(d, "o")
+    pyoracle.run(path, odir, os.path.join(d, "o.txt"), dump=True)
+    assert F.dump_rows(os.path.join(odir, "callsite_dump_1.dat")) == F.dump_rows(F.DUMP)
