@@ -232,6 +232,7 @@ struct nmg_engine {
   std::vector<nmg_engine*> workers;
   std::vector<int> devices;
   bool multi = false, multi_distinct = false, multi_pending = false;
+  uint64_t multi_found = 0;  // matched SAMPLEs of the workers (multi_finish)
   std::vector<void*> comms;  // ncclComm_t per worker (distinct devices)
   std::vector<uint8_t*> warena;
   std::vector<size_t> warena_cap;
@@ -635,9 +636,15 @@ extern "C" int nmg_reset_counters(nmg_engine* h) {
   if (h) h->epoch++;
   if (!h) return NMG_ERR_INVALID;
   if (!h->have_table) return fail(h, NMG_ERR_STATE, "nmg_reset_counters before nmg_set_objects");
-  if (h->multi_pending) {  // the merges in flight belong to the counters being reset
-    const int rc = multi_finish(h);
-    if (rc) return rc;
+  if (h->multi_pending) {  // the merges in flight write the arrays being reset: let them finish (their
+                           // per-buffer gathers are not needed)
+    h->multi_pending = false;
+    for (nmg_engine* w : h->workers) {
+      HIP_TRY(h, hipSetDevice(w->device));
+      HIP_TRY(h, hipStreamSynchronize(w->stream));
+    }
+    HIP_TRY(h, hipSetDevice(h->device));
+    HIP_TRY(h, hipStreamSynchronize(h->stream));
   }
   for (nmg_engine* w : h->workers) {
     const int rc = nmg_reset_counters(w);
@@ -647,6 +654,7 @@ extern "C" int nmg_reset_counters(nmg_engine* h) {
     std::fill(h->ov_samples.begin(), h->ov_samples.end(), 0u);
     std::fill(h->ov_found.begin(), h->ov_found.end(), 0u);
   }
+  h->multi_found = 0;
   HIP_TRY(h, hipSetDevice(h->device));
   h->route_pending = false;  // the counts found_kernel would add are zeroed here
   ResetParams r;
@@ -2347,6 +2355,7 @@ static int stream_flush(nmg_engine* h);
 
 static int multi_analyze(nmg_engine* h);
 static int multi_finish(nmg_engine* h);
+static int multi_buffer_found(nmg_engine* h, std::vector<uint32_t>& nf);
 
 extern "C" int nmg_analyze(nmg_engine* h) {
   if (h) h->epoch++;
@@ -2515,7 +2524,16 @@ int engine_download(nmg_engine* h, HostResults& r, bool entries, bool buffer_fou
   // matched-sample total the kernels count (Params::found)
   r.nb_samples_total = 0;
   r.nb_found_total = 0;
-  if (h->counts_override) {
+  if (h->multi) {
+    r.buf_samples = h->ov_samples;
+    r.buf_bytes = h->ov_bytes;
+    r.buf_found.assign(r.buf_samples.size(), 0);
+    if (buffer_found && !r.buf_samples.empty()) {
+      const int frc = multi_buffer_found(h, r.buf_found);
+      if (frc) return frc;
+    }
+    r.nb_found_total = h->multi_found;
+  } else if (h->counts_override) {
     r.buf_samples = h->ov_samples;
     r.buf_found = h->ov_found;
     r.buf_bytes = h->ov_bytes;
@@ -3019,20 +3037,25 @@ static int multi_analyze(nmg_engine* h) {
     int which, op;
   };
   const Arr arrs[4] = {{NMG_ARR_SUM64, 0}, {NMG_ARR_MIN64, 1}, {NMG_ARR_MAX64, 2}, {NMG_ARR_HIST32, 3}};
-  if (h->multi_distinct) {  // RCCL reduce to worker 0 (in place), over xGMI
+  // The workers' counters accumulate like this handle's would (they are
+  // reset only with it), so the handle's arrays are rebuilt as the merge of
+  // the workers' -- no pass of its own over the old values.
+  if (h->multi_distinct) {  // one RCCL reduce per array, straight into this handle's array (rank 0), over xGMI
     Rccl* r = rccl();
     HIP_TRY(h, hipSetDevice(h->device));
     r->group_start();
     for (const Arr& x : arrs) {
+      size_t hb = 0;
+      void* root = array_ptr(h, x.which, &hb);
       for (uint32_t i = 0; i < n; i++) {
         nmg_engine* w = h->workers[i];
         size_t bytes = 0;
         void* p = array_ptr(w, x.which, &bytes);
-        void* root = array_ptr(h->workers[0], x.which, &bytes);
         if (!bytes) continue;
         const ncclRedOp_t op = x.op == 1 ? ncclMin : (x.op == 2 ? ncclMax : ncclSum);
         const ncclDataType_t dt = x.op == 3 ? ncclUint32 : ncclUint64;
         const size_t count = bytes / (x.op == 3 ? 4 : 8);
+        // (recvbuff is read on the root only)
         const ncclResult_t e = r->reduce(p, i == 0 ? root : p, count, dt, op, 0, (ncclComm_t)h->comms[i], w->stream);
         if (e != ncclSuccess) {
           r->group_end();
@@ -3042,21 +3065,30 @@ static int multi_analyze(nmg_engine* h) {
     }
     const ncclResult_t e = r->group_end();
     if (e != ncclSuccess) return fail(h, NMG_ERR_HIP, std::string("ncclGroupEnd: ") + r->error_string(e));
-  }
-  // this handle += worker 0 (distinct: the reduced arrays) or += every worker (one device)
-  HIP_TRY(h, hipSetDevice(h->device));
-  for (uint32_t i = 0; i < (h->multi_distinct ? 1u : n); i++) {
-    nmg_engine* w = h->workers[i];
+    // the handle's stream (report downloads) after worker 0's, which carries the root's reduces
+    HIP_TRY(h, hipSetDevice(h->device));
     hipEvent_t ev;
     HIP_TRY(h, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-    HIP_TRY(h, hipEventRecord(ev, w->stream));
+    HIP_TRY(h, hipEventRecord(ev, h->workers[0]->stream));
     HIP_TRY(h, hipStreamWaitEvent(h->stream, ev, 0));
     (void)hipEventDestroy(ev);
-    for (const Arr& x : arrs) {
-      size_t bytes = 0, wb = 0;
-      void* dst = array_ptr(h, x.which, &bytes);
-      const void* src = array_ptr(w, x.which, &wb);
-      if (bytes) HIP_TRY(h, launch_merge(h->stream, dst, src, bytes / (x.op == 3 ? 4 : 8), x.op));
+  } else {  // workers on one device (tests): this handle = worker 0, then op= every other worker
+    HIP_TRY(h, hipSetDevice(h->device));
+    for (uint32_t i = 0; i < n; i++) {
+      nmg_engine* w = h->workers[i];
+      hipEvent_t ev;
+      HIP_TRY(h, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+      HIP_TRY(h, hipEventRecord(ev, w->stream));
+      HIP_TRY(h, hipStreamWaitEvent(h->stream, ev, 0));
+      (void)hipEventDestroy(ev);
+      for (const Arr& x : arrs) {
+        size_t bytes = 0, wb = 0;
+        void* dst = array_ptr(h, x.which, &bytes);
+        const void* src = array_ptr(w, x.which, &wb);
+        if (!bytes) continue;
+        if (i == 0) HIP_TRY(h, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, h->stream));
+        else HIP_TRY(h, launch_merge(h->stream, dst, src, bytes / (x.op == 3 ? 4 : 8), x.op));
+      }
     }
   }
   h->multi_staged = true;
@@ -3077,29 +3109,34 @@ static int multi_finish(nmg_engine* h) {
   }
   HIP_TRY(h, hipSetDevice(h->device));
   HIP_TRY(h, hipStreamSynchronize(h->stream));
-  std::vector<uint32_t> ns, nf;
+  // per-buffer SAMPLE counts (concatenated in analysis order), matched-sample
+  // totals and sparse cells (summed by key) of the workers, whose counters are
+  // cumulative: the per-buffer matched counts are gathered only when asked
+  // (engine_download), the report needs their total
+  std::vector<uint32_t> ns;
   std::vector<uint64_t> keys;
   std::vector<uint32_t> vals;
   std::vector<uint64_t> k0;
   std::vector<uint32_t> v0;
-  int rc = sparse_download(h, k0, v0);
-  if (rc) return rc;
-  keys.insert(keys.end(), k0.begin(), k0.end());
-  vals.insert(vals.end(), v0.begin(), v0.end());
+  uint64_t found = 0;
+  int rc = NMG_OK;
   for (nmg_engine* w : h->workers) {
     const uint32_t nb = nmg_get_nb_buffers(w);
-    std::vector<uint32_t> a(nb), b(nb);
-    rc = nmg_get_buffer_counts(w, a.data(), b.data());
-    if (rc) return fail(h, rc, w->last_error);
+    std::vector<uint32_t> a(nb);
+    if (nb) {
+      HIP_TRY(h, hipSetDevice(w->device));
+      HIP_TRY(h, hipMemcpy(a.data(), w->d_bufcnt, nb * 4, hipMemcpyDeviceToHost));
+    }
     ns.insert(ns.end(), a.begin(), a.end());
-    nf.insert(nf.end(), b.begin(), b.end());
+    uint64_t f = 0;
+    if (w->d_found) HIP_TRY(h, hipMemcpy(&f, w->d_found, 8, hipMemcpyDeviceToHost));
+    found += f;
     rc = sparse_download(w, k0, v0);
     if (rc) return fail(h, rc, w->last_error);
     keys.insert(keys.end(), k0.begin(), k0.end());
     vals.insert(vals.end(), v0.begin(), v0.end());
-    rc = nmg_reset_counters(w);
-    if (rc) return fail(h, rc, w->last_error);
   }
+  HIP_TRY(h, hipSetDevice(h->device));
   if (h->d_sparse_keys) {
     std::vector<size_t> ord(keys.size());
     for (size_t i = 0; i < ord.size(); i++) ord[i] = i;
@@ -3116,16 +3153,24 @@ static int multi_finish(nmg_engine* h) {
     rc = nmg_sparse_import(h, mk.data(), mv.data(), (int64_t)mk.size());
     if (rc) return rc;
   }
-  // per-buffer counts accumulate across analyses like every other counter
-  // (the workers were reset above); a reset of this handle zeroes them
-  if (h->counts_override && h->ov_samples.size() == ns.size()) {
-    for (size_t b = 0; b < ns.size(); b++) {
-      h->ov_samples[b] += ns[b];
-      h->ov_found[b] += nf[b];
-    }
-    return NMG_OK;
+  std::vector<uint32_t> nf(ns.size(), 0);
+  rc = nmg_set_buffer_counts(h, (uint32_t)ns.size(), ns.data(), nf.data(), h->buf_bytes.data());
+  if (rc) return rc;
+  h->multi_found = found;
+  return NMG_OK;
+}
+
+// per-buffer matched counts of a multi-GPU handle: the workers' (cumulative)
+static int multi_buffer_found(nmg_engine* h, std::vector<uint32_t>& nf) {
+  nf.clear();
+  for (nmg_engine* w : h->workers) {
+    const uint32_t nb = nmg_get_nb_buffers(w);
+    std::vector<uint32_t> a(nb), b(nb);
+    const int rc = nmg_get_buffer_counts(w, a.data(), b.data());
+    if (rc) return fail(h, rc, w->last_error);
+    nf.insert(nf.end(), b.begin(), b.end());
   }
-  return nmg_set_buffer_counts(h, (uint32_t)ns.size(), ns.data(), nf.data(), h->buf_bytes.data());
+  return NMG_OK;
 }
 
 extern "C" int nmg_report(nmg_engine* h, const nmg_object_meta* meta, const nmg_report_options* opts,

@@ -1335,7 +1335,8 @@ __global__ __launch_bounds__(kWG) void plan_kernel(PlanParams r) {
     const uint32_t base = tb + (k ? t0 : 0u), ibase = nb + (k ? n0 : 0u), tot = k ? t1 : t0;
     r.pbase[q] = base;
     for (uint32_t j = 0; j * kItemChunks < tot; j++)
-      r.items[ibase + j] = make_uint4(q, base + j * kItemChunks, base + min(tot, (j + 1) * kItemChunks), 0);
+      r.items[ibase + j] = make_uint4(q, base + j * kItemChunks, base + min(tot, (j + 1) * kItemChunks),
+                                      tot <= kItemChunks ? 1u : 0u);  // .w: the partition's only item
   }
   if (tid == kWG - 1) {
     r.ctl[0] = wn + in;
@@ -1361,6 +1362,12 @@ __global__ __launch_bounds__(kWG) void scatter_kernel(ScatterParams r) {
 // ---------------------------------------------------------------------------
 // pass 3: attribute one partition per workgroup at a time
 
+// a load served by L2, never by this CU's L1 (global_load ... sc1)
+template <typename T>
+__device__ __forceinline__ T l2_load(const T* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 template <bool TIMING>
 __global__ __launch_bounds__(kWG, 1) void local_kernel(LocalParams lp) {
   __shared__ uint64_t s_keys[kPartSlots];
@@ -1374,7 +1381,6 @@ __global__ __launch_bounds__(kWG, 1) void local_kernel(LocalParams lp) {
   __shared__ unsigned long long s_first[kPartEntries];
   __shared__ uint32_t s_pg[kPartCells / 2];
   __shared__ uint32_t s_clist[kItemChunks];  // the item's chunk list entries
-  __shared__ unsigned long long s_cm[kItemChunks];  // the item's chunks' match bits (found_kernel)
   __shared__ uint32_t s_item;
 
   Params& p = lp.p;
@@ -1387,6 +1393,13 @@ __global__ __launch_bounds__(kWG, 1) void local_kernel(LocalParams lp) {
   for (int k = 0; k < 9; k++) rt.acc[k] = 0;
   rt.last = TIMING ? stamp() : 0;
   uint32_t nchunks = 0, nit = 0;
+  uint32_t nfound = 0;  // this wave's matched records (Params::found, added once at the end)
+  // the item counters start zeroed; every flush re-zeroes what it reads
+  for (uint32_t i = tid; i < kPartEntries; i += kWG) {
+    s_owt[0][i] = s_owt[1][i] = 0;
+    s_first[i] = ~0ull;
+  }
+  for (uint32_t i = tid; i < kPartCells / 2; i += kWG) s_pg[i] = 0;
   while (true) {
     if (tid == 0) s_item = atomicAdd(lp.ctl + 1, 1u);
     lds_sync();
@@ -1413,12 +1426,8 @@ __global__ __launch_bounds__(kWG, 1) void local_kernel(LocalParams lp) {
       for (uint32_t i = tid; i < kPartDir; i += kWG) s_dir[i] = gd[i];
       for (uint32_t i = tid; i < item.z - item.y; i += kWG) s_clist[i] = lp.clist[item.y + i];
     }
-    for (uint32_t i = tid; i < pi.ne; i += kWG) {
-      s_owt[0][i] = s_owt[1][i] = 0;
-      s_first[i] = ~0ull;
-    }
     const uint32_t ncell = (pages && pi.pages_lds) ? T * pi.span : 0u;
-    for (uint32_t i = tid; i < (ncell + 1) / 2; i += kWG) s_pg[i] = 0;
+    const bool excl = item.w != 0;  // no other workgroup writes this partition's counters
     lds_sync();
     const uint64_t k0key = u64of(__builtin_amdgcn_readfirstlane((uint32_t)s_keys[0]),
                                  __builtin_amdgcn_readfirstlane((uint32_t)(s_keys[0] >> 32)));
@@ -1461,7 +1470,8 @@ __global__ __launch_bounds__(kWG, 1) void local_kernel(LocalParams lp) {
       if (p.flags & kDbgLocalNoWork) {  // (ablation) loads only
 #pragma unroll
         for (int j = 0; j < 2; j++)
-          if (lane == 0 && k + j < nmine) s_cm[li[j]] = a16[j].x ^ a16[j].y ^ a16[j].z ^ a16[j].w;
+          if (lane == 0 && k + j < nmine)
+            lp.cmatch[s_clist[li[j]] & ((1u << kChunkIdBits) - 1)] = a16[j].x ^ a16[j].y ^ a16[j].z ^ a16[j].w;
         return;
       }
       // (update_counters of every routed SAMPLE: the route pass)
@@ -1556,11 +1566,13 @@ __global__ __launch_bounds__(kWG, 1) void local_kernel(LocalParams lp) {
         }
         vm_drain();
       }
-      // the chunks' match bits (found_kernel), stored with the item's counters
+      // the chunks' match bits (per-buffer counts, found_kernel) straight to
+      // global memory, and this wave's matched total
 #pragma unroll
       for (int j = 0; j < 2; j++) {
         const uint64_t fm = __ballot(erel[j] >= 0);
-        if (lane == 0 && k + j < nmine) s_cm[li[j]] = fm;
+        nfound += (uint32_t)__popcll(fm);
+        if (lane == 0 && k + j < nmine) lp.cmatch[s_clist[li[j]] & ((1u << kChunkIdBits) - 1)] = fm;
       }
       rt_stamp<TIMING>(rt, 3);
       const bool noobj = (p.flags & kDbgLocalNoObj) != 0;
@@ -1637,49 +1649,55 @@ __global__ __launch_bounds__(kWG, 1) void local_kernel(LocalParams lp) {
     }
     lds_sync();
     rt_stamp<TIMING>(rt, 8);  // (waiting for the item's slowest wave counts as flush)
-    {  // the chunks' match bits (per-buffer counts, found_kernel) and the item's matched total
-      uint32_t nf = 0;
-      for (uint32_t i = tid; i < nl; i += kWG) {
-        const unsigned long long m = s_cm[i];
-        lp.cmatch[s_clist[i] & ((1u << kChunkIdBits) - 1)] = m;
-        nf += (uint32_t)__popcll(m);
-      }
-      if (__ballot(nf != 0)) {
-        const uint32_t t = wave_sum_u32(nf);
-        if (lane == 0 && t) atomicAdd(p.found, (unsigned long long)t);
-      }
-    }
-    // the item's counters to global memory: consecutive lanes, consecutive words
+    // the item's counters to global memory, consecutive lanes on consecutive
+    // words, each LDS word zeroed for the next item as it is read; the only
+    // item of its partition adds with plain loads and stores (no other
+    // workgroup writes these words during the launch), the others with
+    // atomics
     for (uint32_t i = tid; i < pi.ne; i += kWG) {
       const uint64_t e = pi.e0 + i;
 #pragma unroll
       for (uint32_t a = 0; a < 2; a++) {
         const uint64_t v = s_owt[a][i];
         if (!v) continue;
-        atomicAdd(reinterpret_cast<unsigned long long*>(p.sum64 + objcw_index(e, a, 0, p.nb_entries)),
-                  (unsigned long long)(v >> kPackShift));
-        const uint64_t wt = v & ((1ull << kPackShift) - 1);
-        if (wt)
-          atomicAdd(reinterpret_cast<unsigned long long*>(p.sum64 + objcw_index(e, a, 1, p.nb_entries)),
-                    (unsigned long long)wt);
+        s_owt[a][i] = 0;
+        const uint64_t cnt = v >> kPackShift, wt = v & ((1ull << kPackShift) - 1);
+        uint64_t* pc = p.sum64 + objcw_index(e, a, 0, p.nb_entries);
+        uint64_t* pw = p.sum64 + objcw_index(e, a, 1, p.nb_entries);
+        if (excl) {  // (loads past L1: this workgroup's own large-weight atomics went to L2)
+          *pc = l2_load(pc) + cnt;
+          if (wt) *pw = l2_load(pw) + wt;
+        } else {
+          atomicAdd(reinterpret_cast<unsigned long long*>(pc), (unsigned long long)cnt);
+          if (wt) atomicAdd(reinterpret_cast<unsigned long long*>(pw), (unsigned long long)wt);
+        }
       }
       const uint64_t fo = s_first[i];
-      if (fo != ~0ull) atomicMin(reinterpret_cast<unsigned long long*>(p.min64 + 36 + e), (unsigned long long)fo);
+      if (fo != ~0ull) {
+        s_first[i] = ~0ull;
+        uint64_t* pf = p.min64 + 36 + e;
+        if (excl) *pf = min(l2_load(pf), fo);
+        else atomicMin(reinterpret_cast<unsigned long long*>(pf), (unsigned long long)fo);
+      }
     }
     for (uint32_t j = tid; j < (ncell + 1) / 2; j += kWG) {
       const uint32_t v = s_pg[j];
       if (!v) continue;
+      s_pg[j] = 0;
 #pragma unroll
       for (uint32_t h = 0; h < 2; h++) {
         const uint32_t cnt = (v >> (16 * h)) & 0xffffu;
         if (!cnt) continue;
         const uint32_t li = 2 * j + h, th = li / pi.span, rel = li - th * pi.span;
-        atomicAdd(p.hist + uint64_t(th) * p.hist_cells + pi.cb + rel, cnt);
+        uint32_t* pc = p.hist + uint64_t(th) * p.hist_cells + pi.cb + rel;
+        if (excl) *pc = l2_load(pc) + cnt;
+        else atomicAdd(pc, cnt);
       }
     }
     lds_sync();
     rt_stamp<TIMING>(rt, 8);
   }
+  if (lane == 0 && nfound) atomicAdd(p.found, (unsigned long long)nfound);
   if (TIMING && lane == 0) {
     unsigned long long* o = p.dbg + (uint64_t(blockIdx.x) * (kWG / 64) + tid / 64) * kRouteTimingWords;
     for (int k = 0; k < 9; k++) o[k] = rt.acc[k];

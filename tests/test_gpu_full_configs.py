@@ -84,3 +84,41 @@ def test_config4_shard_bit_exact(tmp_path):
     """configs[3]'s per-GPU shard: 125M records, 1M intervals."""
     _run(tmp_path, SynthConfig(nb_samples=125_000_000, nb_intervals=1_000_000, size_max=64 * 1024,
                                site_ratio=0.002, seed=44, sample_seed=1003))
+
+
+def test_config4_shard_one_rank_rccl_handle(tmp_path):
+    """The configs[3] shard through the multi-GPU handle's RCCL branch (a
+    one-rank communicator on a one-GPU box, internal switch 0x40000): host
+    buffers staged to the worker, the worker's analysis, the grouped
+    ncclReduce of every dense array straight into the handle, the handle's
+    gathers.  Every counter equals the bit-exact restatement
+    (oracle/nmg_cpu_mt.cpp, pinned against the oracle in test_cpu_mt.py),
+    after a reset + analysis as well as after the first one."""
+    from numamma_amd.engine import Engine
+
+    d = str(tmp_path)
+    rp = generate(SynthConfig(nb_samples=125_000_000, nb_intervals=1_000_000, size_max=64 * 1024,
+                              site_ratio=0.002, seed=45, sample_seed=1004))
+    path = os.path.join(d, "replay.bin")
+    rp.write(path)
+    pyoracle.run_mt(path, os.path.join(d, "mt_raw.bin"), threads=16, levels=False)
+    os.remove(path)
+    raw = RawResults.read(os.path.join(d, "mt_raw.bin"))
+    eng = Engine(nb_threads=rp.nb_threads, flags=_lib.NMG_F_DEFAULT | 0x40000, copy_threads=16)
+    eng.set_objects(rp.table)
+    eng.submit_buffers(rp.linear_buffers())
+    del rp
+    for rep in range(2):
+        eng.reset()
+        eng.analyze()
+        eng.synchronize()
+        g, ns, nf = eng.global_counters()
+        first, cw = eng.object_counters()
+        nbs, nbf = eng.buffer_counts()
+        cells = eng.page_cells()
+        assert np.array_equal(g, raw.global_counters) and (ns, nf) == (raw.nb_samples, raw.nb_found), rep
+        assert np.array_equal(nbs, raw.buf_samples) and np.array_equal(nbf, raw.buf_found), rep
+        assert np.array_equal(first, raw.first_ordinal), rep
+        assert np.array_equal(cw, raw.count_weight), rep
+        assert np.array_equal(cells, raw.cells), rep
+    eng.close()

@@ -96,21 +96,23 @@ def main():
     if args.skip_multi:
         return
     lins = rp.linear_buffers()
-    for devices in (None, [0, 0]):
-        e = Engine(nb_threads=rp.nb_threads, devices=devices, copy_threads=8)
+    for devices, flags, tag in ((None, 0, "single"), ([0, 0], 0, "two_shards_one_device"),
+                                (None, 0x40000, "one_rank_rccl_handle")):
+        e = Engine(nb_threads=rp.nb_threads, devices=devices, copy_threads=8, flags=_lib.NMG_F_DEFAULT | flags)
         e.set_objects(rp.table)
         e.submit_buffers(lins)
         ts = []
         for r in range(args.reps // 2 + 1):
-            e.reset()
             t0 = time.perf_counter()
+            e.reset()
             e.analyze()
             e.synchronize()
             if r:
                 ts.append((time.perf_counter() - t0) * 1e3)
-        print(json.dumps({"measure": "abi_multi_gpu_step", "workload": args.workload,
+        print(json.dumps({"measure": "abi_multi_gpu_step", "workload": args.workload, "handle": tag,
                           "nb_gpus": len(devices) if devices else 1, "same_device": bool(devices),
-                          "analyze_sync_ms": float(np.median(ts))}), flush=True)
+                          "reset_analyze_sync_ms": float(np.median(ts)),
+                          "analysis_launch_ms": e.last_analyze_ms() if not (devices or flags) else None}), flush=True)
         e.close()
 
 
