@@ -966,20 +966,25 @@ struct SegL {
 };
 __device__ __forceinline__ uint32_t route_partition_l(const SegL* s_seg, uint32_t nseg, const uint64_t* s_pb,
                                                       const uint16_t* s_pdir, uint64_t addr) {
-  uint4 a = s_seg[0].a;
-  uint4 b = s_seg[0].b;
+  // (field by field: a select of whole structs goes through scratch memory)
+  const uint4 a0 = s_seg[0].a, b0 = s_seg[0].b;
+  uint64_t s0 = u64of(a0.x, a0.y);
+  uint32_t base = a0.z, ns = a0.w, sh = b0.x, ql = b0.y;
   for (uint32_t k = 1; k < nseg; k++) {
     const uint4 ak = s_seg[k].a, bk = s_seg[k].b;
-    const bool in = addr >= u64of(ak.x, ak.y);
-    a = in ? ak : a;
-    b = in ? bk : b;
+    const uint64_t sk = u64of(ak.x, ak.y);
+    const bool in = addr >= sk;
+    s0 = in ? sk : s0;
+    base = in ? ak.z : base;
+    ns = in ? ak.w : ns;
+    sh = in ? bk.x : sh;
+    ql = in ? bk.y : ql;
   }
-  const uint64_t rel = (addr - u64of(a.x, a.y)) >> b.x;
-  const uint32_t ns = a.w;
-  const uint32_t e = s_pdir[a.z + (rel < ns ? (uint32_t)rel : ns - 1)];
+  const uint64_t rel = (addr - s0) >> sh;
+  const uint32_t e = s_pdir[base + (rel < ns ? (uint32_t)rel : ns - 1)];
   uint32_t q = e & 2047u;
   const uint32_t c = e >> 11;
-  uint32_t n = (c == kDirCntSat ? b.y - q : c) + 1;  // candidates q .. q + n - 1; s_pb[q] <= addr
+  uint32_t n = (c == kDirCntSat ? ql - q : c) + 1;  // candidates q .. q + n - 1; s_pb[q] <= addr
   while (n > 1) {
     const uint32_t half = n >> 1;
     if (s_pb[q + half] <= addr) {
@@ -992,6 +997,7 @@ __device__ __forceinline__ uint32_t route_partition_l(const SegL* s_seg, uint32_
   return q;
 }
 
+template <bool TIMING>
 __global__ __launch_bounds__(kWG, 1) void route2_kernel(RouteParams rp) {
   __shared__ uint64_t s_pb[kMaxParts + 1];
   __shared__ uint16_t s_pdir[kRouteDir];
@@ -1052,47 +1058,60 @@ __global__ __launch_bounds__(kWG, 1) void route2_kernel(RouteParams rp) {
     // a valid address for the loads of slots that hold no record
     const uint64_t safe = __builtin_amdgcn_readfirstlane((uint32_t)p.sbufs[r0].offset) |
                           (uint64_t(__builtin_amdgcn_readfirstlane((uint32_t)(p.sbufs[r0].offset >> 32))) << 32);
-    auto dequeue = [&]() -> RDesc {
+    // (descriptors are assigned, never selected as whole structs: a select of
+    // structs goes through scratch memory)
+    auto dequeue = [&](RDesc& d) {
       uint32_t i = 0;
       if (lane == 0) i = atomicAdd(&s_bnext, 1u);
       i = __builtin_amdgcn_readfirstlane(i);
-      return i < r1 ? route_desc(rp, s_desc, r0, i) : no_buf();
+      if (i < r1) d = route_desc(rp, s_desc, r0, i);
+      else d = no_buf();
     };
     // the wave's stream: buffer d0 at cursor cur; d1 = the buffer after it
     // once dequeued (have1): dequeued only when a window of d1 is prefetched,
     // so that a wave never holds a buffer it is not about to read
-    RDesc d0 = dequeue(), d1 = no_buf();
+    RDesc d0, d1 = no_buf();
+    dequeue(d0);
     bool have1 = false;
     uint32_t cur = 0;
     uint32_t ns = 0;  // SAMPLEs of d0 so far (mem_sampling.c:921-926)
     // the window after (b, c) if the window at (b, c) holds only whole 40 B
     // records (the fast path): its buffer and cursor
     uint32_t pidx, pcur;
-    auto predict = [&]() -> RDesc {
+    uint64_t eoff;  // the predicted window's buffer (offset, length)
+    uint32_t elen;
+    auto predict = [&]() {
       if (d0.pad == kNoBuf) {
         pidx = kNoBuf;
         pcur = 0;
-        return d0;
-      }
-      if (cur + kWaveWinBytes < d0.len) {
+        eoff = 0;
+        elen = 0;
+      } else if (cur + kWaveWinBytes < d0.len) {
         pidx = d0.pad;
         pcur = cur + kWaveWinBytes;
-        return d0;
+        eoff = d0.offset;
+        elen = d0.len;
+      } else {
+        if (!have1) {
+          dequeue(d1);
+          have1 = true;
+        }
+        pidx = d1.pad;
+        pcur = 0;
+        eoff = d1.offset;
+        elen = d1.len;
       }
-      if (!have1) {
-        d1 = dequeue();
-        have1 = true;
-      }
-      pidx = d1.pad;
-      pcur = 0;
-      return d1;
     };
     RawRec ra, rb;
     wload(p.data, safe, d0.offset, d0.len, 0, lane, ra);
-    {
-      const RDesc e = predict();
-      wload(p.data, safe, e.offset, e.len, pcur, lane, rb);
-    }
+    predict();
+    wload(p.data, safe, eoff, elen, pcur, lane, rb);
+
+    RTimer rt;  // (TIMING) per-wave phase cycles
+#pragma unroll
+    for (int k = 0; k < 9; k++) rt.acc[k] = 0;
+    rt.last = TIMING ? stamp() : 0;
+    uint32_t nwin = 0;
 
     // one window of this wave: A holds its slots, B the next window's (in
     // flight); k = the window's place in the batch (staging slots)
@@ -1100,6 +1119,11 @@ __global__ __launch_bounds__(kWG, 1) void route2_kernel(RouteParams rp) {
       const RDesc dw = d0;  // this window's buffer
       const uint32_t pos = cur + uint32_t(lane) * kRecBytes;
       const bool cand = pos < dw.len;
+      if (TIMING) {
+        asm volatile("s_waitcnt vmcnt(3)" ::: "memory");  // (this window's loads count as wait)
+        nwin++;
+      }
+      rt_stamp<TIMING>(rt, 0);
       Rec rec = decode_rec(A, pos);
       const bool bad = cand && (uint64_t(pos) + kRecBytes > dw.len || (rec.hdr >> 48) != kRecBytes);
       bool valid;
@@ -1175,7 +1199,7 @@ __global__ __launch_bounds__(kWG, 1) void route2_kernel(RouteParams rp) {
           if (have1) {
             d0 = d1;
           } else {
-            d0 = dequeue();
+            dequeue(d0);
           }
           have1 = false;
           d1 = no_buf();
@@ -1189,23 +1213,25 @@ __global__ __launch_bounds__(kWG, 1) void route2_kernel(RouteParams rp) {
         wload(p.data, safe, d0.offset, d0.len, cur, lane, B);
         vm_drain();  // (rare: keeps the waits on the common path exact)
       }
-      {
-        const RDesc e = predict();
-        wload(p.data, safe, e.offset, e.len, pcur, lane, A);
-      }
+      predict();
+      wload(p.data, safe, eoff, elen, pcur, lane, A);
 
       // ---- this window's records: update_counters(global_counters, sample)
       // (mem_sampling.c:882: every SAMPLE, matched or not), partition, batch
       // rank, staging slot
+      rt_stamp<TIMING>(rt, 1);
       const uint32_t acc_l = dw.access();
       if (valid) route_count(gacc, s_gsums, s_gmins, s_gmaxs, acc_l, uint32_t(rec.dsrc >> 5) & 0x3fff, rec.w);
       if (++gwin == kDrainWindows) {
         dual_drain(gacc, s_gsums, lane);
         gwin = 0;
       }
+      rt_stamp<TIMING>(rt, 2);
       // below the first key ht_lower_key finds no node: counted, not routed
       const bool routed = valid && rec.addr >= first_start;
       const uint32_t q = routed ? route_partition_l(s_seg, nseg, s_pb, s_pdir, rec.addr) : 0u;
+      if (TIMING) (void)__builtin_amdgcn_readfirstlane(__ballot(q != 0));  // (the search ends here)
+      rt_stamp<TIMING>(rt, 3);
       Held hr;
       hr.q = kNoChunk;
       if (routed) {
@@ -1215,23 +1241,34 @@ __global__ __launch_bounds__(kWG, 1) void route2_kernel(RouteParams rp) {
         hr.a = x_encode(rp.xl, pbq, rec.addr, rec.ts, rec.w, dw.pad, roff, dw.thread_rank(), acc_l);
       }
       route_stage(L, hr, k, tid);
+      rt_stamp<TIMING>(rt, 4);
     };
 
-    RTimer rt;  // (unused: no timing instance)
     while (true) {
       for (uint32_t k = 0; k < kRouteWindows; k += 2) {
         window(ra, rb, k);
         window(rb, ra, k + 1);
       }
       if (lane == 0 && d0.pad != kNoBuf) atomicOr(&s_more[nbatches & 1], 1u);
-      route_sort_batch<false>(rt, rp, tid, L, nbatches, kRouteWindows, c0, cap);
+      if (TIMING) {  // (the wait at the batch's first barrier)
+        lds_sync();
+        rt_stamp<TIMING>(rt, 8);
+      }
+      route_sort_batch<TIMING>(rt, rp, tid, L, nbatches, kRouteWindows, c0, cap);
       const uint32_t more = __builtin_amdgcn_readfirstlane(s_more[nbatches & 1]);
       if (tid == 0) s_more[(nbatches + 1) & 1] = 0;
       vm_drain();  // (the prefetched window has long arrived: the chunk stores alone stay in flight)
-      route_write_batch<false>(rt, rp, tid, L, nbatches);
+      route_write_batch<TIMING>(rt, rp, tid, L, nbatches);
       nbatches++;
       lds_sync();  // every wave has gathered the batch from the staging slots
+      rt_stamp<TIMING>(rt, 8);
       if (!more) break;
+    }
+    if (TIMING && lane == 0) {
+      unsigned long long* o = p.dbg + (uint64_t(blockIdx.x) * (kWG / 64) + tid / 64) * kRouteTimingWords;
+      for (int k = 0; k < 9; k++) o[k] = rt.acc[k];
+      o[9] = nwin;
+      o[10] = nbatches;
     }
   }
   dual_drain(gacc, s_gsums, lane);
@@ -1747,7 +1784,9 @@ __global__ __launch_bounds__(kWG) void found_kernel(FoundParams r) {
 // launchers
 
 hipError_t launch_route(uint32_t grid, hipStream_t s, const RouteParams& r) {
-  if (r.p.flags & kDbgRouteV2) hipLaunchKernelGGL(route2_kernel, dim3(grid), dim3(kWG), 0, s, r);
+  if ((r.p.flags & kDbgRouteV2) && (r.p.flags & kDbgRouteTiming))
+    hipLaunchKernelGGL(route2_kernel<true>, dim3(grid), dim3(kWG), 0, s, r);
+  else if (r.p.flags & kDbgRouteV2) hipLaunchKernelGGL(route2_kernel<false>, dim3(grid), dim3(kWG), 0, s, r);
   else if (r.p.flags & kDbgRouteTiming) hipLaunchKernelGGL(route_kernel<true>, dim3(grid), dim3(kWG), 0, s, r);
   else hipLaunchKernelGGL(route_kernel<false>, dim3(grid), dim3(kWG), 0, s, r);
   return hipGetLastError();
