@@ -2138,7 +2138,7 @@ static uint32_t bits_for(uint64_t v) {  // smallest b with v < 2^b
 }
 
 // X word layout of the current buffers; false when the weight field would
-// be narrower than 12 bits (escapes would be common)
+// be narrower than kMinWeightBits (escapes would be common)
 static bool route_layout(nmg_engine* h, XLayout& xl) {
   uint64_t maxlen = 1;
   for (const BufDesc& d : h->descs) maxlen = std::max<uint64_t>(maxlen, d.len);
@@ -2146,7 +2146,7 @@ static bool route_layout(nmg_engine* h, XLayout& xl) {
   xl.obits = bits_for((maxlen - 1) / 8);
   xl.tbits = bits_for(h->T - 1);
   const uint32_t loc = xl.gbits + xl.obits + xl.tbits + 1;  // (+ access bit)
-  if (loc > 48 - 8 || xl.gbits > 31 || xl.obits > 31 || xl.tbits > 31) return false;
+  if (loc > 48 - kMinWeightBits || xl.gbits > 31 || xl.obits > 31 || xl.tbits > 31) return false;
   xl.wbits = std::min<uint32_t>(48 - loc, 16);  // (the decode reads at most 16 bits of weight)
   xl.wesc = (1ull << xl.wbits) - 1;
   xl.tbase = h->route_tbase;

@@ -107,9 +107,13 @@ static_assert(sizeof(PartInfo) == 48, "PartInfo");
 // A record whose address, timestamp or weight does not fit carries wesc: the
 // local pass re-reads all three from the raw record (rare).
 constexpr uint32_t kAddrBits = 40;
+// narrowest weight field of a compact record: weights up to 2046 cycles (the
+// bulk of PEBS load latencies) never escape; a buffer set whose location
+// fields leave fewer bits keeps the single-pass kernel (route_layout)
+constexpr uint32_t kMinWeightBits = 11;
 constexpr uint32_t kTsBits = 40;
 struct XLayout {
-  uint32_t gbits, obits, tbits, wbits;  // wbits = min(48 - (gbits + obits + tbits + 1), 16) >= 8
+  uint32_t gbits, obits, tbits, wbits;  // wbits = min(48 - (gbits + obits + tbits + 1), 16) >= kMinWeightBits
   uint64_t wesc;   // 2^wbits - 1
   uint64_t tbase;  // smallest non-zero alloc_date of the table (earlier samples escape)
 };
