@@ -324,6 +324,18 @@ int nmg_get_page_cells(nmg_engine *h, uint32_t *rows /* [n][4] */, int64_t n);
 uint64_t nmg_array_size(nmg_engine *h, int which);
 int nmg_export_array(nmg_engine *h, int which, void *d_dst);
 int nmg_import_array(nmg_engine *h, int which, const void *d_src);
+/* The page histogram packed for the merge (NMG_ARR_HIST32 is most of the
+ * payload: 98 of 140 MB per rank at 1M intervals).  nmg_hist_pack writes
+ * every cell of at most `threshold` (<= 255) as one byte to d_u8 (device,
+ * nmg_array_size(HIST32) bytes; larger cells as 0) and each larger cell as
+ * (cell << 32 | count) to d_ovf (device, ovf_cap u64); *n_ovf = their number
+ * (> ovf_cap: the list is incomplete -- merge NMG_ARR_HIST32 instead).  With
+ * threshold <= 255 / ranks the byte arrays of all ranks add up without
+ * overflow (a u8 SUM reduce); the root then calls nmg_hist_unpack with the
+ * summed bytes and every rank's overflow entries (entries with count 0 are
+ * padding): histogram = bytes + overflow, exactly the u32 sum. */
+int nmg_hist_pack(nmg_engine *h, uint32_t threshold, void *d_u8, void *d_ovf, uint64_t ovf_cap, uint64_t *n_ovf);
+int nmg_hist_unpack(nmg_engine *h, const void *d_u8, const void *d_ovf, uint64_t n_ovf);
 /* sparse (object, page, thread) cells: export as (key, count) pairs on host */
 int64_t nmg_sparse_count(nmg_engine *h);
 int nmg_sparse_export(nmg_engine *h, uint64_t *keys, uint32_t *counts, int64_t n);

@@ -162,6 +162,7 @@ struct nmg_engine {
   uint64_t n_sum64 = 0, n_min64 = 0, n_max64 = 0;
   uint32_t* d_hist = nullptr;
   unsigned long long* d_found = nullptr;  // matched SAMPLEs since the last reset (Params::found)
+  uint64_t* d_scratch = nullptr;          // [2] small device results (nmg_hist_pack / unpack)
   uint64_t* d_sparse_keys = nullptr;
   uint32_t* d_sparse_vals = nullptr;
   uint32_t* d_sparse_dirty = nullptr;  // [2] parity flags (see reset_kernel)
@@ -603,6 +604,7 @@ extern "C" void nmg_destroy(nmg_engine* h) {
   (void)hipFree(h->d_descs);
   (void)hipFree(h->d_bufcnt);
   (void)hipFree(h->d_found);
+  (void)hipFree(h->d_scratch);
   (void)hipFree(h->d_sdescs);
   (void)hipFree(h->d_ranges);
   (void)hipFree(h->d_dbg);
@@ -2802,6 +2804,51 @@ extern "C" int nmg_import_array(nmg_engine* h, int which, const void* d_src) {
   HIP_TRY(h, hipSetDevice(h->device));
   HIP_TRY(h, hipMemcpyAsync(dst, d_src, bytes, hipMemcpyDeviceToDevice, h->stream));
   HIP_TRY(h, hipStreamSynchronize(h->stream));
+  return NMG_OK;
+}
+
+static int scratch_u64(nmg_engine* h) {
+  if (!h->d_scratch) HIP_TRY(h, hipMalloc(&h->d_scratch, 2 * 8));
+  return NMG_OK;
+}
+
+extern "C" int nmg_hist_pack(nmg_engine* h, uint32_t threshold, void* d_u8, void* d_ovf, uint64_t ovf_cap,
+                             uint64_t* n_ovf) {
+  Range range("nmg_hist_pack");
+  if (!h || !h->have_table || !n_ovf || threshold > 255) return NMG_ERR_INVALID;
+  const uint64_t cells = h->hist_cells * h->T;
+  *n_ovf = 0;
+  if (!cells) return NMG_OK;
+  if (!d_u8 || (ovf_cap && !d_ovf)) return NMG_ERR_INVALID;
+  if (cells > (1ull << 32)) return fail(h, NMG_ERR_RANGE, "nmg_hist_pack: more than 2^32 cells");
+  int rc = scratch_u64(h);
+  if (rc) return rc;
+  HIP_TRY(h, hipSetDevice(h->device));
+  HIP_TRY(h, hipMemsetAsync(h->d_scratch, 0, 8, h->stream));
+  HIP_TRY(h, launch_hist_pack(h->stream, h->d_hist, cells, threshold, d_u8, d_ovf, ovf_cap,
+                              reinterpret_cast<unsigned long long*>(h->d_scratch)));
+  HIP_TRY(h, hipMemcpyAsync(n_ovf, h->d_scratch, 8, hipMemcpyDeviceToHost, h->stream));
+  HIP_TRY(h, hipStreamSynchronize(h->stream));
+  return NMG_OK;
+}
+
+extern "C" int nmg_hist_unpack(nmg_engine* h, const void* d_u8, const void* d_ovf, uint64_t n_ovf) {
+  if (h) h->epoch++;
+  Range range("nmg_hist_unpack");
+  if (!h || !h->have_table || (n_ovf && !d_ovf)) return NMG_ERR_INVALID;
+  const uint64_t cells = h->hist_cells * h->T;
+  if (!cells) return NMG_OK;
+  if (!d_u8) return NMG_ERR_INVALID;
+  int rc = scratch_u64(h);
+  if (rc) return rc;
+  HIP_TRY(h, hipSetDevice(h->device));
+  HIP_TRY(h, hipMemsetAsync(h->d_scratch + 1, 0, 8, h->stream));
+  HIP_TRY(h, launch_hist_unpack(h->stream, h->d_hist, cells, d_u8, d_ovf, n_ovf,
+                                reinterpret_cast<unsigned long long*>(h->d_scratch + 1)));
+  uint64_t bad = 0;
+  HIP_TRY(h, hipMemcpyAsync(&bad, h->d_scratch + 1, 8, hipMemcpyDeviceToHost, h->stream));
+  HIP_TRY(h, hipStreamSynchronize(h->stream));
+  if (bad) return fail(h, NMG_ERR_RANGE, "nmg_hist_unpack: overflow entries outside the histogram");
   return NMG_OK;
 }
 

@@ -993,6 +993,72 @@ __global__ __launch_bounds__(256) void merge_kernel(void* dst, const void* src, 
   }
 }
 
+// Packed page histogram for the multi-GPU merge (nmg_hist_pack): cells of at
+// most `thr` as bytes (4 per thread, one 16 B load), larger ones to the
+// overflow list as (cell << 32 | count), compacted per wave (one counter add).
+__global__ __launch_bounds__(256) void hist_pack_kernel(const uint4* hist, uint64_t n4, uint32_t thr, uint32_t* u8x4,
+                                                        unsigned long long* ovf, uint64_t cap,
+                                                        unsigned long long* cnt) {
+  const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
+  const int lane = threadIdx.x & 63;
+  for (uint64_t base = uint64_t(blockIdx.x) * blockDim.x; base < n4; base += stride) {
+    const uint64_t i = base + threadIdx.x;
+    const uint4 v = i < n4 ? hist[i] : make_uint4(0, 0, 0, 0);
+    const uint32_t c[4] = {v.x, v.y, v.z, v.w};
+    uint32_t packed = 0, nbig = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const bool small = c[k] <= thr;
+      packed |= (small ? c[k] : 0u) << (8 * k);
+      nbig += small ? 0u : 1u;
+    }
+    if (i < n4) u8x4[i] = packed;
+    const uint64_t any = __ballot(nbig != 0);
+    if (!any) continue;
+    // this wave's overflow entries: an exclusive scan of nbig, one counter add
+    uint32_t pre = nbig;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t t = __shfl_up(pre, o, 64);
+      if (lane >= o) pre += t;
+    }
+    const uint32_t tot = __shfl(pre, 63, 64);
+    unsigned long long at = 0;
+    if (lane == 0) at = atomicAdd(cnt, (unsigned long long)tot);
+    at = __shfl(at, 0, 64);
+    uint64_t slot = at + pre - nbig;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      if (c[k] <= thr) continue;
+      if (slot < cap) ovf[slot] = ((unsigned long long)(4 * i + k) << 32) | c[k];
+      slot++;
+    }
+  }
+}
+
+// nmg_hist_unpack: hist = summed bytes, then += every overflow entry
+__global__ __launch_bounds__(256) void hist_unpack_kernel(uint4* hist, uint64_t n4, const uint32_t* u8x4) {
+  const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
+  for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    const uint32_t p = u8x4[i];
+    hist[i] = make_uint4(p & 0xffu, (p >> 8) & 0xffu, (p >> 16) & 0xffu, p >> 24);
+  }
+}
+
+__global__ __launch_bounds__(256) void hist_ovf_add_kernel(uint32_t* hist, uint64_t ncells,
+                                                           const unsigned long long* ovf, uint64_t n,
+                                                           unsigned long long* bad) {
+  const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
+  for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const unsigned long long e = ovf[i];
+    const uint64_t cell = e >> 32;
+    const uint32_t c = (uint32_t)e;
+    if (!c) continue;  // (padding)
+    if (cell < ncells) atomicAdd(hist + cell, c);
+    else atomicAdd(bad, 1ull);
+  }
+}
+
 // ---------------------------------------------------------------------------
 // launchers
 
@@ -1087,6 +1153,32 @@ hipError_t launch_cells_emit(hipStream_t s, const uint32_t* hist, uint64_t hist_
 hipError_t launch_unpack(uint32_t grid, hipStream_t s, uint64_t* sum64, unsigned long long* pk64, uint32_t nb_entries,
                          uint32_t shift) {
   hipLaunchKernelGGL(unpack_kernel, dim3(grid), dim3(256), 0, s, sum64, pk64, nb_entries, shift);
+  return hipGetLastError();
+}
+
+hipError_t launch_hist_pack(hipStream_t s, const uint32_t* hist, uint64_t ncells, uint32_t thr, void* u8,
+                            void* ovf, uint64_t cap, unsigned long long* cnt) {
+  const uint64_t n4 = ncells / 4;
+  if (!n4) return hipSuccess;
+  const uint32_t grid = (uint32_t)std::min<uint64_t>((n4 + 255) / 256, 4096);
+  hipLaunchKernelGGL(hist_pack_kernel, dim3(grid), dim3(256), 0, s, reinterpret_cast<const uint4*>(hist), n4, thr,
+                     reinterpret_cast<uint32_t*>(u8), reinterpret_cast<unsigned long long*>(ovf), cap, cnt);
+  return hipGetLastError();
+}
+
+hipError_t launch_hist_unpack(hipStream_t s, uint32_t* hist, uint64_t ncells, const void* u8, const void* ovf,
+                              uint64_t n, unsigned long long* bad) {
+  const uint64_t n4 = ncells / 4;
+  if (n4) {
+    const uint32_t grid = (uint32_t)std::min<uint64_t>((n4 + 255) / 256, 4096);
+    hipLaunchKernelGGL(hist_unpack_kernel, dim3(grid), dim3(256), 0, s, reinterpret_cast<uint4*>(hist), n4,
+                       reinterpret_cast<const uint32_t*>(u8));
+  }
+  if (n) {
+    const uint32_t grid = (uint32_t)std::min<uint64_t>((n + 255) / 256, 4096);
+    hipLaunchKernelGGL(hist_ovf_add_kernel, dim3(grid), dim3(256), 0, s, hist, ncells,
+                       reinterpret_cast<const unsigned long long*>(ovf), n, bad);
+  }
   return hipGetLastError();
 }
 

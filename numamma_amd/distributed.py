@@ -13,6 +13,9 @@ The only exchange step is the merge of the counters:
 * u64 mins (global bucket min_weight, first-match ordinals, error word) -> MIN
 * u64 maxes (global bucket max_weight)                                 -> MAX
 * u32 page histogram                                                   -> SUM
+  (packed, merge_hist_packed: bytes of the cells <= 255 / world summed as
+  u8, the larger cells gathered as (cell, count) lists -- 98 -> ~26 MB per
+  rank at 1M intervals)
 * sparse page cells, per-buffer counts: variable length -> gathered to the root
 
 RCCL reduces int64, not uint64: sums are bit-identical under two's
@@ -84,6 +87,67 @@ def reduce_u32_sum(t, dst: Optional[int] = 0, group=None):
     return _collective(t, dist.ReduceOp.SUM, dst, group)
 
 
+class HistPacker:
+    """Buffers of the packed page-histogram merge of one engine (allocated
+    once; the overflow list holds up to `ovf_frac` of the cells)."""
+
+    def __init__(self, eng, device, ovf_frac: float = 0.125):
+        import torch
+
+        from . import _lib
+
+        self.eng = eng
+        self.cells = eng.array_size(_lib.NMG_ARR_HIST32)
+        self.cap = max(1024, int(self.cells * ovf_frac))
+        self.u8 = torch.empty(max(self.cells, 4), dtype=torch.uint8, device=device)
+        self.ovf = torch.zeros(self.cap, dtype=torch.int64, device=device)
+        self.n = torch.zeros(1, dtype=torch.int64, device=device)
+        self.dense = None  # fallback: the u32 histogram (a list longer than cap)
+
+    def merge(self, dst: int = 0, group=None) -> int:
+        """Merge every rank's histogram into rank dst's engine; returns the
+        bytes this rank contributed to the collectives."""
+        import torch
+        import torch.distributed as dist
+
+        from . import _lib
+
+        if not self.cells:
+            return 0
+        world = dist.get_world_size(group)
+        rank = dist.get_rank(group)
+        thr = 255 // world
+        n = self.eng.hist_pack(thr, self.u8.data_ptr(), self.ovf.data_ptr(), self.cap)
+        self.n.fill_(n)
+        _collective(self.n, dist.ReduceOp.MAX, None, group)  # every rank: the longest list
+        nmax = int(self.n.item())
+        if nmax > self.cap:  # some list does not fit: the plain u32 reduce
+            if self.dense is None:
+                self.dense = torch.empty(self.cells, dtype=torch.int32, device=self.u8.device)
+            self.eng.export_array(_lib.NMG_ARR_HIST32, self.dense.data_ptr())
+            reduce_u32_sum(self.dense, dst=dst, group=group)
+            if rank == dst:
+                torch.cuda.synchronize(self.u8.device)
+                self.eng.import_array(_lib.NMG_ARR_HIST32, self.dense.data_ptr())
+            return self.cells * 4
+        if n < nmax:
+            self.ovf[n:nmax].zero_()  # (padding: count 0)
+        _collective(self.u8[:self.cells], dist.ReduceOp.SUM, dst, group)
+        part = self.ovf[:nmax]
+        if dist.get_backend(group) == "nccl":
+            out = [torch.empty_like(part) for _ in range(world)] if rank == dst else None
+            dist.gather(part, out, dst=dst, group=group)
+        else:  # (gloo test runs: host staging)
+            cpu = part.cpu()
+            out = [torch.empty_like(cpu) for _ in range(world)] if rank == dst else None
+            dist.gather(cpu, out, dst=dst, group=group)
+        if rank == dst:
+            allovf = torch.cat([o.to(self.u8.device) for o in out]) if nmax else self.ovf[:0]
+            torch.cuda.synchronize(self.u8.device)
+            self.eng.hist_unpack(self.u8.data_ptr(), allovf.data_ptr() if nmax else 0, allovf.numel())
+        return self.cells + nmax * 8
+
+
 def gather_arrays(a: np.ndarray, dst: int = 0, group=None):
     """Variable-length gather of a numpy array; returns the list on dst."""
     import torch.distributed as dist
@@ -105,9 +169,10 @@ def merge_sparse(parts) -> Tuple[np.ndarray, np.ndarray]:
     return u, (s & 0xFFFFFFFF).astype(np.uint32)
 
 
-def merge_engine(eng, dst: int = 0, group=None, device=None) -> None:
+def merge_engine(eng, dst: int = 0, group=None, device=None, packed_hist: bool = False) -> None:
     """Merge every rank's partial counters into rank dst's engine (RCCL reduce
-    of the dense arrays over xGMI; gathers of the small variable-length ones)."""
+    of the dense arrays over xGMI; gathers of the small variable-length ones).
+    packed_hist: the page histogram through HistPacker (bytes + overflow)."""
     import torch
     import torch.distributed as dist
 
@@ -126,7 +191,9 @@ def merge_engine(eng, dst: int = 0, group=None, device=None) -> None:
             torch.cuda.synchronize(dev)
             eng.import_array(which, t.data_ptr())
     n = eng.array_size(_lib.NMG_ARR_HIST32)
-    if n:
+    if n and packed_hist:
+        HistPacker(eng, dev).merge(dst=dst, group=group)
+    elif n:
         t = torch.empty(n, dtype=torch.int32, device=dev)
         eng.export_array(_lib.NMG_ARR_HIST32, t.data_ptr())
         reduce_u32_sum(t, dst=dst, group=group)

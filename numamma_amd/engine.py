@@ -244,6 +244,16 @@ class Engine:
     def import_array(self, which: int, d_src: int):
         self._c(lib.nmg_import_array(self.h, which, C.c_void_p(d_src)))
 
+    def hist_pack(self, threshold: int, d_u8: int, d_ovf: int, ovf_cap: int) -> int:
+        """nmg_hist_pack: returns the number of overflow entries (> ovf_cap:
+        the list is incomplete)."""
+        n = C.c_uint64(0)
+        self._c(lib.nmg_hist_pack(self.h, threshold, C.c_void_p(d_u8), C.c_void_p(d_ovf), ovf_cap, C.byref(n)))
+        return n.value
+
+    def hist_unpack(self, d_u8: int, d_ovf: int, n_ovf: int):
+        self._c(lib.nmg_hist_unpack(self.h, C.c_void_p(d_u8), C.c_void_p(d_ovf), n_ovf))
+
     def sparse_export(self):
         n = lib.nmg_sparse_count(self.h)
         self._c(n)

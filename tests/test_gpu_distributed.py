@@ -3,7 +3,9 @@ GPU 0 of the test box) each analyse a contiguous byte-balanced shard of the
 buffer list with its seq_base, then merge_engine runs the engine's
 nmg_export_array -> reduce_u64 / reduce_u32_sum -> nmg_import_array chain and
 the sparse / per-buffer gathers; rank 0 reports.  The merged counters and
-every report file must equal the oracle's single unsharded run."""
+every report file must equal the oracle's single unsharded run.  `packed`
+merges the page histogram through nmg_hist_pack / nmg_hist_unpack (bytes of
+the cells <= 255 / world summed as u8, the larger cells gathered)."""
 import os
 import socket
 import sys
@@ -31,7 +33,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, workdir, cfg_name, ret):
+def _worker(rank, world, port, workdir, cfg_name, ret, packed=False):
     sys.path[:0] = [ROOT, os.path.join(ROOT, "oracle")]
     try:
         import torch
@@ -55,7 +57,7 @@ def _worker(rank, world, port, workdir, cfg_name, ret):
                                seq_base=lo)
         eng.analyze()
         eng.synchronize()
-        merge_engine(eng, dst=0, device=dev)
+        merge_engine(eng, dst=0, device=dev, packed_hist=packed)
         if rank == 0:
             edir = os.path.join(workdir, "engine")
             eng.report(edir, os.path.join(workdir, "e.txt"))
@@ -74,8 +76,9 @@ def _worker(rank, world, port, workdir, cfg_name, ret):
         raise
 
 
+@pytest.mark.parametrize("packed", [False, True], ids=["dense", "packed"])
 @pytest.mark.parametrize("cfg_name", sorted(CFGS))
-def test_two_rank_engine_merge_matches_oracle(cfg_name):
+def test_two_rank_engine_merge_matches_oracle(cfg_name, packed):
     import multiprocessing as mp
 
     sys.path[:0] = [ROOT, os.path.join(ROOT, "oracle")]
@@ -87,7 +90,7 @@ def test_two_rank_engine_merge_matches_oracle(cfg_name):
     ret = ctx.Queue()
     with tempfile.TemporaryDirectory() as d:
         port = _free_port()
-        procs = [ctx.Process(target=_worker, args=(r, 2, port, d, cfg_name, ret)) for r in range(2)]
+        procs = [ctx.Process(target=_worker, args=(r, 2, port, d, cfg_name, ret, packed)) for r in range(2)]
         for p in procs:
             p.start()
         msgs = [ret.get(timeout=240) for _ in procs]
@@ -111,3 +114,42 @@ def test_two_rank_engine_merge_matches_oracle(cfg_name):
         for f in sorted(os.listdir(os.path.join(d, "oracle"))):
             assert open(os.path.join(d, "oracle", f), "rb").read() == \
                 open(os.path.join(d, "engine", f), "rb").read(), f
+
+
+@pytest.mark.parametrize("threshold", [0, 1, 31, 127, 255])
+def test_hist_pack_round_trip(threshold):
+    """nmg_hist_pack then nmg_hist_unpack on one engine gives back every
+    page cell (bytes <= threshold + overflow list); a list longer than its
+    capacity reports its full length."""
+    import torch
+
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "oracle")]
+    from numamma_amd import _lib
+    from numamma_amd.engine import Engine
+    from numamma_amd.replay import SynthConfig, generate
+
+    rp = generate(SynthConfig(nb_samples=400_000, nb_intervals=20_000, seed=23))
+    eng = Engine(device=0, nb_threads=rp.nb_threads)
+    eng.set_objects(rp.table)
+    eng.submit_replay(rp)
+    eng.analyze()
+    eng.synchronize()
+    cells = eng.array_size(_lib.NMG_ARR_HIST32)
+    dev = torch.device("cuda", 0)
+    before = torch.empty(cells, dtype=torch.int32, device=dev)
+    eng.export_array(_lib.NMG_ARR_HIST32, before.data_ptr())
+    ref = before.cpu().numpy().view(np.uint32)
+    u8 = torch.empty(cells, dtype=torch.uint8, device=dev)
+    ovf = torch.zeros(cells, dtype=torch.int64, device=dev)
+    n = eng.hist_pack(threshold, u8.data_ptr(), ovf.data_ptr(), cells)
+    assert n == int((ref > threshold).sum())
+    b = u8.cpu().numpy()
+    assert np.array_equal(b, np.where(ref <= threshold, ref, 0).astype(np.uint8))
+    if n > 1:
+        assert eng.hist_pack(threshold, u8.data_ptr(), ovf.data_ptr(), n - 1) == n  # (capacity short)
+        eng.hist_pack(threshold, u8.data_ptr(), ovf.data_ptr(), cells)
+    eng.hist_unpack(u8.data_ptr(), ovf.data_ptr(), n)
+    after = torch.empty(cells, dtype=torch.int32, device=dev)
+    eng.export_array(_lib.NMG_ARR_HIST32, after.data_ptr())
+    assert np.array_equal(after.cpu().numpy().view(np.uint32), ref)
+    eng.close()
