@@ -547,6 +547,110 @@ __device__ __forceinline__ void route_write_batch(RTimer& rt, const RouteParams&
   rt_stamp<TIMING>(rt, 7);
 }
 
+// The direct form of a batch (route2_kernel): no sort.  Every staged record
+// already carries its rank within its partition's records of the batch, so
+// once each partition's chunks are allocated the lane that staged a record
+// computes its slot (open chunk fill + rank) and stores it: one barrier for
+// the counts, one for the chunk state, no permutation and no gather.  The
+// slots a record takes are the ones the sorted form gives the same ranks.
+//
+// Chunk allocation: each thread takes two partitions; a wave scan of the new
+// chunks they need and one LDS atomic per wave give their first chunks
+// (route_sort_batch takes one atomic per partition).  Open-chunk state:
+// batch b reads cur[b & 1] and writes cur[(b + 1) & 1].
+__device__ __forceinline__ void route_alloc_direct(const RouteParams& rp, int tid, const RouteLds& L, uint32_t batch,
+                                                   uint32_t c0, uint32_t cap) {
+  const uint32_t P = rp.nparts;
+  const int lane = tid & 63;
+  const uint32_t* cur_in = L.cur + (batch & 1) * (kMaxParts + 1);
+  uint32_t* cur_out = L.cur + ((batch + 1) & 1) * (kMaxParts + 1);
+  const uint32_t i0 = 2 * (uint32_t)tid;
+  uint32_t n[2], c[2], nn[2];
+#pragma unroll
+  for (uint32_t k = 0; k < 2; k++) {
+    const uint32_t q = i0 + k;
+    n[k] = q < P ? L.hist[q] : 0u;
+    c[k] = q < P ? cur_in[q] : 0u;
+    const uint32_t tot = (c[k] & 127u) + n[k];
+    nn[k] = tot > kChunk ? (tot - 1) / kChunk : 0u;  // chunks past the open one
+  }
+  const uint32_t need = nn[0] + nn[1];
+  uint32_t base = 0;
+  if (__ballot(need != 0)) {
+    const uint32_t inc = wave_incl_scan_u32(need);
+    const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
+    uint32_t wb = 0;
+    if (lane == 63) wb = atomicAdd(&L.misc[1], tot);
+    wb = (uint32_t)__builtin_amdgcn_readlane((int)wb, 63);
+    base = wb + inc - need;
+  }
+#pragma unroll
+  for (uint32_t k = 0; k < 2; k++) {
+    const uint32_t q = i0 + k;
+    if (q >= P) continue;
+    const uint32_t b = base + (k ? nn[0] : 0u);
+    if (!n[k]) {
+      cur_out[q] = c[k];
+      continue;
+    }
+    L.hist[q] = 0;
+    const uint32_t tot = (c[k] & 127u) + n[k];
+    if (!nn[k]) {
+      cur_out[q] = (c[k] & ~127u) | tot;
+      continue;
+    }
+    if (b + nn[k] > cap) {
+      L.nb[q] = kNoChunk;  // pool exhausted: this batch's overflow of q goes to the overflow list
+      atomicMin(&L.misc[2], b);  // chunks from here on were never handed out
+      cur_out[q] = (c[k] & ~127u) | kChunk;
+      continue;
+    }
+    L.nb[q] = c0 + b;
+    for (uint32_t j = 0; j < nn[k]; j++) rp.cmeta[c0 + b + j] = q | (kChunk << 24);
+    cur_out[q] = ((c0 + b + nn[k] - 1) << 7) | (tot - kChunk * nn[k]);
+  }
+}
+
+// every lane stores the records it staged (slots k * kWG + tid) to their
+// chunk slots: (open chunk fill + rank)
+__device__ __forceinline__ void route_store_direct(const RouteParams& rp, int tid, const RouteLds& L, uint32_t batch) {
+  const Params& p = rp.p;
+  const uint32_t* cur_in = L.cur + (batch & 1) * (kMaxParts + 1);
+  uint32_t e[kRouteWindows];
+#pragma unroll
+  for (uint32_t b = 0; b < kRouteWindows; b++) e[b] = L.uq[b * kWG + (uint32_t)tid];
+#pragma unroll
+  for (uint32_t b = 0; b < kRouteWindows; b++) {
+    if (e[b] == kNoChunk) continue;
+    const uint32_t q = e[b] & 2047u, rk = e[b] >> 11;
+    const uint4 a = L.a16[b * kWG + (uint32_t)tid];
+    const uint32_t cur = cur_in[q];
+    const uint32_t pos = (cur & 127u) + rk;
+    uint32_t chunk, slot;
+    if (pos < kChunk) {
+      chunk = cur >> 7;
+      slot = pos;
+    } else {
+      const uint32_t nb = L.nb[q];
+      if (nb == kNoChunk) {  // pool exhausted: to the overflow list (overflow_kernel)
+        const uint32_t o = atomicAdd(rp.ovf_cnt, 1u);
+        if (o < rp.ovf_cap) {
+          rp.ovf16[o] = a;
+          rp.ovfx[o] = L.pb[q];
+        } else {  // (only SAMPLE records shorter than 40 B get here) attributed at once
+          XRec xr = x_decode(rp.xl, L.pb[q], a);
+          if (xr.esc) x_resolve(xr, p.data, p.sbufs);
+          direct_attribute(p, xr.addr, xr.ts, xr.w, xr.th, xr.acc, 0, rp.seq0 + xr.g, xr.off, xr.g);
+        }
+        continue;
+      }
+      chunk = nb + (pos - kChunk) / kChunk;
+      slot = (pos - kChunk) % kChunk;
+    }
+    rp.rec16[uint64_t(chunk) * kChunk + slot] = a;
+  }
+}
+
 // Descriptors of the workgroup's range staged in LDS (offset, len,
 // thread | access << 16): a buffer transition reads LDS instead of waiting on
 // a global load.  Ranges longer than kDescLds read the rest from global
@@ -1254,13 +1358,30 @@ __global__ __launch_bounds__(kWG, 1) void route2_kernel(RouteParams rp) {
         lds_sync();
         rt_stamp<TIMING>(rt, 8);
       }
-      route_sort_batch<TIMING>(rt, rp, tid, L, nbatches, kRouteWindows, c0, cap);
-      const uint32_t more = __builtin_amdgcn_readfirstlane(s_more[nbatches & 1]);
-      if (tid == 0) s_more[(nbatches + 1) & 1] = 0;
-      vm_drain();  // (the prefetched window has long arrived: the chunk stores alone stay in flight)
-      route_write_batch<TIMING>(rt, rp, tid, L, nbatches);
-      nbatches++;
-      lds_sync();  // every wave has gathered the batch from the staging slots
+      uint32_t more;
+      if (p.flags & kDbgRouteSorted) {
+        route_sort_batch<TIMING>(rt, rp, tid, L, nbatches, kRouteWindows, c0, cap);
+        more = __builtin_amdgcn_readfirstlane(s_more[nbatches & 1]);
+        if (tid == 0) s_more[(nbatches + 1) & 1] = 0;
+        vm_drain();  // (the prefetched window has long arrived: the chunk stores alone stay in flight)
+        route_write_batch<TIMING>(rt, rp, tid, L, nbatches);
+        nbatches++;
+        lds_sync();  // every wave has gathered the batch from the staging slots
+      } else {
+        lds_sync();  // every rank and staging store of the batch done
+        rt_stamp<TIMING>(rt, 5);
+        route_alloc_direct(rp, tid, L, nbatches, c0, cap);
+        more = __builtin_amdgcn_readfirstlane(s_more[nbatches & 1]);
+        if (tid == 0) s_more[(nbatches + 1) & 1] = 0;
+        lds_sync();  // chunk state of every partition set
+        rt_stamp<TIMING>(rt, 6);
+        vm_drain();  // (the prefetched window has long arrived: the chunk stores alone stay in flight)
+        route_store_direct(rp, tid, L, nbatches);
+        rt_stamp<TIMING>(rt, 7);
+        nbatches++;
+        // (no barrier: a lane reads back only its own staging slots, and the
+        // chunk state it reads changes after the next batch's first barrier)
+      }
       rt_stamp<TIMING>(rt, 8);
       if (!more) break;
     }
@@ -1464,7 +1585,8 @@ __global__ __launch_bounds__(kWG, 1) void local_kernel(LocalParams lp) {
       for (uint32_t i = tid; i < item.z - item.y; i += kWG) s_clist[i] = lp.clist[item.y + i];
     }
     const uint32_t ncell = (pages && pi.pages_lds) ? T * pi.span : 0u;
-    const bool excl = item.w != 0;  // no other workgroup writes this partition's counters
+    const bool excl = item.w != 0 && !(p.flags & kDbgLocalAtomics);  // no other workgroup writes this partition's
+                                                                     // counters
     lds_sync();
     const uint64_t k0key = u64of(__builtin_amdgcn_readfirstlane((uint32_t)s_keys[0]),
                                  __builtin_amdgcn_readfirstlane((uint32_t)(s_keys[0] >> 32)));
