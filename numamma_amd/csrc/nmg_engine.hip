@@ -1460,6 +1460,24 @@ static int launch_attribution(nmg_engine* h, const uint8_t* data, const BufDesc*
                               uint32_t nb, uint32_t grid, uint64_t nbytes);
 static int stream_append(nmg_engine* h, uint64_t len, uint32_t thread_rank, uint32_t access);
 static bool route_eligible(nmg_engine* h);
+// One partition-first analysis: a buffer set in HBM with its analysis-order
+// schedule (the submitted buffers, or a streamed chunk whose per-buffer count
+// slots start at index_base; a chunk settles its per-buffer matched counts at
+// once, before the next chunk reuses the pool).
+struct RouteJob {
+  const std::vector<BufDesc>* descs;
+  const uint8_t* data;
+  const BufDesc* sdescs;
+  const uint32_t* ranges;
+  const uint32_t* chunk0;
+  uint32_t grid, index_base;
+  bool settle_now;
+};
+
+static int route_analyze_job(nmg_engine* h, const RouteJob& job);
+static bool route_eligible(nmg_engine* h, const std::vector<BufDesc>& descs);
+static int route_pool(nmg_engine* h, const std::vector<BufDesc>& descs, uint32_t grid, const uint32_t* ranges,
+                      std::vector<uint32_t>& c0);
 static int route_prepare(nmg_engine* h, uint32_t grid, const std::vector<uint32_t>& ranges);
 static int route_analyze(nmg_engine* h, uint32_t nb, uint32_t grid);
 static int route_settle(nmg_engine* h);
@@ -1633,7 +1651,10 @@ static int stream_flush(nmg_engine* h) {
   const uint32_t grid = attribution_grid(h, nb);
   int rc = ensure_bufcnt(h, h->descs.size());
   if (rc) return rc;
-  const size_t sched_bytes = nb * sizeof(BufDesc) + (grid + 1) * 4;
+  // large tables: the partition-first passes over the chunk (analysis-order
+  // schedule, then the ranges and the workgroups' chunk pools)
+  const bool route = route_eligible(h, sl.descs);
+  const size_t sched_bytes = nb * sizeof(BufDesc) + (grid + 1) * 4 * (route ? 2 : 1);
   if (sched_bytes > sl.hs_cap) {  // (slot acquired: its previous H2D is done)
     if (sl.h_sdescs) (void)hipHostFree(sl.h_sdescs);
     sl.h_sdescs = nullptr;
@@ -1642,7 +1663,13 @@ static int stream_flush(nmg_engine* h) {
   }
   const uint32_t index_base = (uint32_t)(h->descs.size() - nb);
   uint32_t* h_ranges = reinterpret_cast<uint32_t*>(sl.h_sdescs + nb);
-  make_schedule(sl.descs, grid, index_base, sl.h_sdescs, h_ranges);
+  make_schedule(sl.descs, grid, index_base, sl.h_sdescs, h_ranges, !route);
+  if (route) {
+    std::vector<uint32_t> c0;
+    rc = route_pool(h, sl.descs, grid, h_ranges, c0);  // (may wait for the stream to grow the pool)
+    if (rc) return rc;
+    memcpy(h_ranges + grid + 1, c0.data(), (grid + 1) * 4);
+  }
   if (sl.len + 64 > sl.dcap || sched_bytes > sl.ds_cap) {  // grow the device side: wait for its last kernel
     if (sl.used) HIP_TRY(h, hipEventSynchronize(sl.done));
     if (sl.len + 64 > sl.dcap) {
@@ -1663,8 +1690,13 @@ static int stream_flush(nmg_engine* h) {
   HIP_TRY(h, hipMemcpyAsync(sl.d_sdescs, sl.h_sdescs, sched_bytes, hipMemcpyHostToDevice, h->copy_stream));
   HIP_TRY(h, hipEventRecord(sl.copied, h->copy_stream));
   HIP_TRY(h, hipStreamWaitEvent(h->stream, sl.copied, 0));
-  rc = launch_attribution(h, sl.d_arena, sl.d_sdescs, reinterpret_cast<const uint32_t*>(sl.d_sdescs + nb), nb, grid,
-                          sl.len);
+  const uint32_t* d_ranges = reinterpret_cast<const uint32_t*>(sl.d_sdescs + nb);
+  if (route) {
+    const RouteJob job{&sl.descs, sl.d_arena, sl.d_sdescs, d_ranges, d_ranges + grid + 1, grid, index_base, true};
+    rc = route_analyze_job(h, job);
+  } else {
+    rc = launch_attribution(h, sl.d_arena, sl.d_sdescs, d_ranges, nb, grid, sl.len);
+  }
   if (rc) return rc;
   HIP_TRY(h, hipEventRecord(sl.done, h->stream));
   sl.used = true;
@@ -2141,10 +2173,10 @@ static uint32_t bits_for(uint64_t v) {  // smallest b with v < 2^b
 
 // X word layout of the current buffers; false when the weight field would
 // be narrower than kMinWeightBits (escapes would be common)
-static bool route_layout(nmg_engine* h, XLayout& xl) {
+static bool route_layout(nmg_engine* h, const std::vector<BufDesc>& descs, XLayout& xl) {
   uint64_t maxlen = 1;
-  for (const BufDesc& d : h->descs) maxlen = std::max<uint64_t>(maxlen, d.len);
-  xl.gbits = bits_for(h->descs.size() - 1);
+  for (const BufDesc& d : descs) maxlen = std::max<uint64_t>(maxlen, d.len);
+  xl.gbits = bits_for(descs.size() - 1);
   xl.obits = bits_for((maxlen - 1) / 8);
   xl.tbits = bits_for(h->T - 1);
   const uint32_t loc = xl.gbits + xl.obits + xl.tbits + 1;  // (+ access bit)
@@ -2155,33 +2187,37 @@ static bool route_layout(nmg_engine* h, XLayout& xl) {
   return true;
 }
 
-static bool route_eligible(nmg_engine* h) {
+// the partition-first path for this buffer set (the submitted buffers, or a
+// streamed chunk of them)
+static bool route_eligible(nmg_engine* h, const std::vector<BufDesc>& descs) {
   constexpr uint32_t kLegacyOnly = kDbgLoadOnly | kDbgNoGlobal | kDbgNoFlush | kDbgNoTables | kDbgTiming |
                                    kDbgTinyLog | kDbgNoPack | kDbgNoDir | kDbgNoRoute | NMG_F_SINGLE_PASS;
-  if (!h->route_ok || (h->flags & kLegacyOnly) || h->descs.empty()) return false;
+  if (!h->route_ok || (h->flags & kLegacyOnly) || descs.empty()) return false;
   // the first-match ordinal is rebuilt from the buffer index: seq = seq0 + index
   uint64_t bytes = 0;
-  for (size_t i = 0; i < h->descs.size(); i++) {
-    if (h->descs[i].seq != h->descs[0].seq + i) return false;
-    bytes += h->descs[i].len;
+  for (size_t i = 0; i < descs.size(); i++) {
+    if (descs[i].seq != descs[0].seq + i) return false;
+    bytes += descs[i].len;
   }
   // chunk ids (route pass LDS: id << 7 | fill) -- an upper bound of the pool
-  const uint64_t chunks = (bytes / kRecBytes + h->descs.size()) / kChunk + (uint64_t)h->num_cus * (h->nparts + 2);
+  const uint64_t chunks = (bytes / kRecBytes + descs.size()) / kChunk + (uint64_t)h->num_cus * (h->nparts + 2);
   if (chunks >= (1ull << kChunkIdBits)) return false;
   XLayout xl;
-  return route_layout(h, xl);
+  return route_layout(h, descs, xl);
 }
+static bool route_eligible(nmg_engine* h) { return route_eligible(h, h->descs); }
 
 // per-workgroup private chunk pools for a new schedule: every SAMPLE record
 // of at least 40 B fits (a partition's chunks are full but for its one open
 // chunk); shorter records past that are attributed directly
-static int route_prepare(nmg_engine* h, uint32_t grid, const std::vector<uint32_t>& ranges) {
+static int route_pool(nmg_engine* h, const std::vector<BufDesc>& descs, uint32_t grid, const uint32_t* ranges,
+                      std::vector<uint32_t>& c0) {
   const uint32_t P = h->nparts;
-  std::vector<uint32_t> c0(grid + 1, 0);
+  c0.assign(grid + 1, 0);
   uint64_t tot = 0;
   for (uint32_t w = 0; w < grid; w++) {
     uint64_t rec = 0;
-    for (uint32_t b = ranges[w]; b < ranges[w + 1]; b++) rec += (h->descs[b].len + kRecBytes - 1) / kRecBytes;
+    for (uint32_t b = ranges[w]; b < ranges[w + 1]; b++) rec += (descs[b].len + kRecBytes - 1) / kRecBytes;
     const uint64_t cap = (h->flags & kDbgTinyPool) ? 2 : (rec + kChunk - 1) / kChunk + P;
     c0[w] = (uint32_t)tot;
     tot += cap;
@@ -2192,7 +2228,7 @@ static int route_prepare(nmg_engine* h, uint32_t grid, const std::vector<uint32_
   // overflow list: records past a full pool (only SAMPLE records shorter than
   // 40 B can get there; kDbgTinyPool sends nearly all of them)
   uint64_t recs = 0;
-  for (const BufDesc& d : h->descs) recs += (d.len + kRecBytes - 1) / kRecBytes;
+  for (const BufDesc& d : descs) recs += (d.len + kRecBytes - 1) / kRecBytes;
   // (a quarter of the records, plus up to three times them for batches under 4M records)
   const size_t ovf = (size_t)((h->flags & kDbgTinyPool) ? recs : recs / 4 + std::min<uint64_t>(3 * recs, 4u << 20)) + 65536;
   if (tot > h->route_chunk_cap || items > h->items_cap || grid > h->route_grid_cap || ovf > h->ovf_cap) {
@@ -2219,19 +2255,36 @@ static int route_prepare(nmg_engine* h, uint32_t grid, const std::vector<uint32_
     h->items_cap = items;
     h->route_grid_cap = grid;
   }
-  HIP_TRY(h, hipMemcpy(h->d_chunk0, c0.data(), (grid + 1) * 4, hipMemcpyHostToDevice));
-  h->route_sched_key = P | ((h->flags & kDbgTinyPool) ? 0x80000000u : 0u);
   return NMG_OK;
 }
+
+static int route_prepare(nmg_engine* h, uint32_t grid, const std::vector<uint32_t>& ranges) {
+  std::vector<uint32_t> c0;
+  const int rc = route_pool(h, h->descs, grid, ranges.data(), c0);
+  if (rc) return rc;
+  HIP_TRY(h, hipMemcpy(h->d_chunk0, c0.data(), (grid + 1) * 4, hipMemcpyHostToDevice));
+  h->route_sched_key = h->nparts | ((h->flags & kDbgTinyPool) ? 0x80000000u : 0u);
+  return NMG_OK;
+}
+
+
 
 // Route -> plan -> scatter -> local over the buffers of the current schedule
 // (analysis order), bracketed by the launch-timing events.
 static int route_analyze(nmg_engine* h, uint32_t nb, uint32_t grid) {
+  (void)nb;
+  RouteJob job{&h->descs, h->d_data, h->d_sdescs, h->d_ranges, h->d_chunk0, grid, 0, false};
+  return route_analyze_job(h, job);
+}
+
+static int route_analyze_job(nmg_engine* h, const RouteJob& job) {
   Range range("nmg_route");
   XLayout xl;
-  if (!route_layout(h, xl)) return fail(h, NMG_ERR_STATE, "route layout");
-  const Params base = base_params(h, h->d_data, h->d_sdescs, h->d_ranges);
-  const uint64_t seq0 = h->descs[0].seq;
+  if (!route_layout(h, *job.descs, xl)) return fail(h, NMG_ERR_STATE, "route layout");
+  const uint32_t grid = job.grid;
+  Params base = base_params(h, job.data, job.sdescs, job.ranges);
+  base.bufcnt = h->d_bufcnt + job.index_base;  // (count slots of the set's first buffer)
+  const uint64_t seq0 = (*job.descs)[0].seq;
   int slot = 0;
   int rc = launch_events(h, &slot);
   if (rc) return rc;
@@ -2248,7 +2301,7 @@ static int route_analyze(nmg_engine* h, uint32_t nb, uint32_t grid) {
   rp.seq0 = seq0;
   rp.rec16 = h->d_rec16;
   rp.cmeta = h->d_cmeta;
-  rp.chunk0 = h->d_chunk0;
+  rp.chunk0 = job.chunk0;
   rp.used = h->d_used;
   rp.ovf16 = h->d_ovf16;
   rp.ovfx = h->d_ovfx;
@@ -2271,7 +2324,7 @@ static int route_analyze(nmg_engine* h, uint32_t nb, uint32_t grid) {
   HIP_TRY(h, launch_overflow(h->stream, rp));
   ScatterParams sc;
   sc.cmeta = h->d_cmeta;
-  sc.chunk0 = h->d_chunk0;
+  sc.chunk0 = job.chunk0;
   sc.used = h->d_used;
   sc.pcnt = h->d_pcnt;
   sc.pbase = h->d_pbase;
@@ -2304,7 +2357,7 @@ static int route_analyze(nmg_engine* h, uint32_t nb, uint32_t grid) {
   lp.items = h->d_items;
   lp.ctl = h->d_ctl;
   lp.cmatch = h->d_cmatch;
-  lp.descs = h->d_sdescs;
+  lp.descs = job.sdescs;
   lp.xl = xl;
   lp.seq0 = seq0;
   if ((h->flags & kDbgLocalTiming) && !(h->flags & kDbgRouteTiming)) {  // (internal) per-wave phase cycles
@@ -2324,10 +2377,24 @@ static int route_analyze(nmg_engine* h, uint32_t nb, uint32_t grid) {
   HIP_TRY(h, hipEventRecord(h->ring1[slot], h->stream));
   h->nlaunch++;
   h->launched = true;
+  if (job.settle_now) {  // (a streamed chunk: the next one reuses the pool)
+    FoundParams f;
+    f.ranges = job.ranges;
+    f.chunk0 = job.chunk0;
+    f.used = h->d_used;
+    f.cmeta = h->d_cmeta;
+    f.cmatch = h->d_cmatch;
+    f.rec16 = h->d_rec16;
+    f.bufcnt = h->d_bufcnt + job.index_base;
+    f.nb_bufs = (uint32_t)h->bufcnt_stride;
+    f.gbits = xl.gbits;
+    f.gshift = 16 + xl.wbits;
+    HIP_TRY(h, launch_found(grid, h->stream, f));
+    return NMG_OK;
+  }
   h->route_pending = true;
   h->route_grid = grid;
   h->route_xl = xl;
-  (void)nb;
   return NMG_OK;
 }
 
