@@ -308,6 +308,15 @@ def main_one_process(args):
                    "parallelism": f"one process, nmg_options.nb_gpus={n}: buffers sharded over {n} GPUs, "
                                   "RCCL reduce of the counters"},
     }
+    # per GPU: its shard's 40 B records over the whole step (analysis, the
+    # RCCL reduce of the counters into GPU 0's handle, the handle's gathers)
+    achieved = shard * RECORD_BYTES / (ms_per_step * 1e-3) / 1e9
+    out["roofline"] = {
+        "bound": "hbm", "kernel": "whole step per GPU: nmg_analyze on every GPU + RCCL reduce + gathers",
+        "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+        "traffic": None, "algorithmic_bytes_per_launch": shard * RECORD_BYTES,
+        "note": "achieved = one GPU's shard (40 B per record, SURVEY 8(d)) / the step's wall time; the single-GPU "
+                "line's kernel split and PMC traffic apply per GPU"}
     print(json.dumps(out), flush=True)
     eng.close()
 

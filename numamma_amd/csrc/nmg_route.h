@@ -80,8 +80,6 @@ constexpr uint32_t kDbgLocalNoGlobal = 0x4000000;  // local pass: no global coun
 constexpr uint32_t kDbgLocalNoSearch = 0x8000000;  // local pass: no lookup (nothing matches)
 constexpr uint32_t kDbgRouteV2 = 0x20000000;      // route pass: per-wave record streams (route2_kernel)
 constexpr uint32_t kDbgLocalAtomics = 0x80000000u;  // local pass: every flush through atomics (A/B)
-constexpr uint32_t kDbgRouteSorted = 0x40000000;  // route2_kernel: batches sorted in LDS (else each lane stores its
-                                                  // own records to their slots)
 constexpr uint32_t kDbgLocalTiming = 0x10000000;  // local pass: per-wave phase cycles in Params::dbg
                                                    // (wait, global, search, match, object, page per chunk;
                                                    // dequeue, setup, flush per item; chunks, items)

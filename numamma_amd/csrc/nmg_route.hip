@@ -307,6 +307,7 @@ __device__ __forceinline__ void dual_count(DualAcc& a, unsigned long long (*sums
 // dual_count for the route pass: the same register buckets, and every
 // minimum / maximum an LDS atomic that returns nothing (no round trip per
 // record; the route pass hides their LDS time behind its memory waits)
+template <bool READ_FIRST = false>
 __device__ __forceinline__ void route_count(DualAcc& a, unsigned long long (*sums)[kGlobalSums],
                                             unsigned long long (*mins)[18], unsigned long long (*maxs)[18],
                                             uint32_t acc, uint32_t lvl, uint64_t w) {
@@ -339,6 +340,20 @@ __device__ __forceinline__ void route_count(DualAcc& a, unsigned long long (*sum
       atomicAdd(&sums[acc][3 + 2 * b], 1ull);
       atomicAdd(&sums[acc][4 + 2 * b], (unsigned long long)w);
     }
+  }
+  if (READ_FIRST) {  // (dual_count's form: an atomic only when the record moves the bound)
+    if (bm) {
+      const uint32_t b = (uint32_t)__builtin_ctz(bm);
+      const unsigned long long mn = mins[acc][b], mx = maxs[acc][b];
+      if (w < mn) atomicMin(&mins[acc][b], (unsigned long long)w);
+      if (w > mx) atomicMax(&maxs[acc][b], (unsigned long long)w);
+      for (uint32_t m = bm & (bm - 1); m; m &= m - 1) {
+        const uint32_t b2 = (uint32_t)__builtin_ctz(m);
+        atomicMin(&mins[acc][b2], (unsigned long long)w);
+        atomicMax(&maxs[acc][b2], (unsigned long long)w);
+      }
+    }
+    return;
   }
   for (uint32_t m = bm; m; m &= m - 1) {
     const uint32_t b = (uint32_t)__builtin_ctz(m);
@@ -378,7 +393,7 @@ __device__ __forceinline__ void dual_drain(DualAcc& a, unsigned long long (*sums
 
 // kDbgRouteTiming: per-wave cycle accumulators of the route pass's phases
 struct RTimer {
-  uint64_t acc[9];
+  uint64_t acc[10];
   uint64_t last;
 };
 template <bool TIMING>
@@ -416,8 +431,9 @@ struct RouteLds {
   uint32_t* misc;     // [0] records in the batch, [1] chunks taken, [2] first chunk never handed out
 };
 
+template <uint32_t WG = kWG>
 __device__ __forceinline__ void route_stage(const RouteLds& L, const Held& h, uint32_t b, int tid) {
-  const uint32_t slot = b * kWG + (uint32_t)tid;
+  const uint32_t slot = b * WG + (uint32_t)tid;
   L.uq[slot] = h.q;
   if (h.q != kNoChunk) L.a16[slot] = h.a;
 }
@@ -545,110 +561,6 @@ __device__ __forceinline__ void route_write_batch(RTimer& rt, const RouteParams&
     rp.rec16[k] = a;
   }
   rt_stamp<TIMING>(rt, 7);
-}
-
-// The direct form of a batch (route2_kernel): no sort.  Every staged record
-// already carries its rank within its partition's records of the batch, so
-// once each partition's chunks are allocated the lane that staged a record
-// computes its slot (open chunk fill + rank) and stores it: one barrier for
-// the counts, one for the chunk state, no permutation and no gather.  The
-// slots a record takes are the ones the sorted form gives the same ranks.
-//
-// Chunk allocation: each thread takes two partitions; a wave scan of the new
-// chunks they need and one LDS atomic per wave give their first chunks
-// (route_sort_batch takes one atomic per partition).  Open-chunk state:
-// batch b reads cur[b & 1] and writes cur[(b + 1) & 1].
-__device__ __forceinline__ void route_alloc_direct(const RouteParams& rp, int tid, const RouteLds& L, uint32_t batch,
-                                                   uint32_t c0, uint32_t cap) {
-  const uint32_t P = rp.nparts;
-  const int lane = tid & 63;
-  const uint32_t* cur_in = L.cur + (batch & 1) * (kMaxParts + 1);
-  uint32_t* cur_out = L.cur + ((batch + 1) & 1) * (kMaxParts + 1);
-  const uint32_t i0 = 2 * (uint32_t)tid;
-  uint32_t n[2], c[2], nn[2];
-#pragma unroll
-  for (uint32_t k = 0; k < 2; k++) {
-    const uint32_t q = i0 + k;
-    n[k] = q < P ? L.hist[q] : 0u;
-    c[k] = q < P ? cur_in[q] : 0u;
-    const uint32_t tot = (c[k] & 127u) + n[k];
-    nn[k] = tot > kChunk ? (tot - 1) / kChunk : 0u;  // chunks past the open one
-  }
-  const uint32_t need = nn[0] + nn[1];
-  uint32_t base = 0;
-  if (__ballot(need != 0)) {
-    const uint32_t inc = wave_incl_scan_u32(need);
-    const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
-    uint32_t wb = 0;
-    if (lane == 63) wb = atomicAdd(&L.misc[1], tot);
-    wb = (uint32_t)__builtin_amdgcn_readlane((int)wb, 63);
-    base = wb + inc - need;
-  }
-#pragma unroll
-  for (uint32_t k = 0; k < 2; k++) {
-    const uint32_t q = i0 + k;
-    if (q >= P) continue;
-    const uint32_t b = base + (k ? nn[0] : 0u);
-    if (!n[k]) {
-      cur_out[q] = c[k];
-      continue;
-    }
-    L.hist[q] = 0;
-    const uint32_t tot = (c[k] & 127u) + n[k];
-    if (!nn[k]) {
-      cur_out[q] = (c[k] & ~127u) | tot;
-      continue;
-    }
-    if (b + nn[k] > cap) {
-      L.nb[q] = kNoChunk;  // pool exhausted: this batch's overflow of q goes to the overflow list
-      atomicMin(&L.misc[2], b);  // chunks from here on were never handed out
-      cur_out[q] = (c[k] & ~127u) | kChunk;
-      continue;
-    }
-    L.nb[q] = c0 + b;
-    for (uint32_t j = 0; j < nn[k]; j++) rp.cmeta[c0 + b + j] = q | (kChunk << 24);
-    cur_out[q] = ((c0 + b + nn[k] - 1) << 7) | (tot - kChunk * nn[k]);
-  }
-}
-
-// every lane stores the records it staged (slots k * kWG + tid) to their
-// chunk slots: (open chunk fill + rank)
-__device__ __forceinline__ void route_store_direct(const RouteParams& rp, int tid, const RouteLds& L, uint32_t batch) {
-  const Params& p = rp.p;
-  const uint32_t* cur_in = L.cur + (batch & 1) * (kMaxParts + 1);
-  uint32_t e[kRouteWindows];
-#pragma unroll
-  for (uint32_t b = 0; b < kRouteWindows; b++) e[b] = L.uq[b * kWG + (uint32_t)tid];
-#pragma unroll
-  for (uint32_t b = 0; b < kRouteWindows; b++) {
-    if (e[b] == kNoChunk) continue;
-    const uint32_t q = e[b] & 2047u, rk = e[b] >> 11;
-    const uint4 a = L.a16[b * kWG + (uint32_t)tid];
-    const uint32_t cur = cur_in[q];
-    const uint32_t pos = (cur & 127u) + rk;
-    uint32_t chunk, slot;
-    if (pos < kChunk) {
-      chunk = cur >> 7;
-      slot = pos;
-    } else {
-      const uint32_t nb = L.nb[q];
-      if (nb == kNoChunk) {  // pool exhausted: to the overflow list (overflow_kernel)
-        const uint32_t o = atomicAdd(rp.ovf_cnt, 1u);
-        if (o < rp.ovf_cap) {
-          rp.ovf16[o] = a;
-          rp.ovfx[o] = L.pb[q];
-        } else {  // (only SAMPLE records shorter than 40 B get here) attributed at once
-          XRec xr = x_decode(rp.xl, L.pb[q], a);
-          if (xr.esc) x_resolve(xr, p.data, p.sbufs);
-          direct_attribute(p, xr.addr, xr.ts, xr.w, xr.th, xr.acc, 0, rp.seq0 + xr.g, xr.off, xr.g);
-        }
-        continue;
-      }
-      chunk = nb + (pos - kChunk) / kChunk;
-      slot = (pos - kChunk) % kChunk;
-    }
-    rp.rec16[uint64_t(chunk) * kChunk + slot] = a;
-  }
 }
 
 // Descriptors of the workgroup's range staged in LDS (offset, len,
@@ -1015,7 +927,8 @@ __global__ __launch_bounds__(kWG, 1) void route_kernel(RouteParams rp) {
 }
 
 // ---------------------------------------------------------------------------
-// pass 1 with per-wave record streams (route2_kernel; kDbgRouteV2 for now).
+// pass 1 with per-wave record streams and no batches (route2_kernel;
+// kDbgRouteV2 for now).
 //
 // route_kernel moves one workgroup-wide byte cursor: every window of 1024
 // stride slots ends in a barrier (the fast-path check), and the batch sort
@@ -1025,12 +938,29 @@ __global__ __launch_bounds__(kWG, 1) void route_kernel(RouteParams rp) {
 // cursor, mem_sampling.c:836-926, per buffer as the reference does it): the
 // fast-path check is a ballot, the slow path (LOST / short / irregular
 // records) is the wave's own header walk, and the per-buffer SAMPLE tally is
-// the wave's.  Only the batch sort synchronises the workgroup: after four
-// windows of every wave (4096 stride slots) the batch is sorted by partition
-// and written to the chunks exactly as in route_kernel.  The next window's
-// loads stay in flight across the window and the batch phases.
+// the wave's.  Nothing synchronises the workgroup between its first and last
+// barrier: each record claims a slot of its partition's open chunk with one
+// LDS atomic and is stored from its registers in the window that read it
+// (the chunk protocol is at the claim).  The next window's loads stay in
+// flight across the window.
 
-constexpr uint32_t kWaves = kWG / 64;
+// route2_kernel's workgroup: 12 waves (three per SIMD); the kernel fits 128
+// VGPRs, so 16 waves are an A/B away (NMG_R2WG=1024)
+#ifndef NMG_R2WG
+#define NMG_R2WG 768
+#endif
+constexpr uint32_t kR2WG = NMG_R2WG;
+#ifndef NMG_R2MMREAD
+#define NMG_R2MMREAD 1
+#endif
+// (A/B builds only: route2 without its global counters (1), with a hash in
+// place of the partition search (2), without the record stores (4), without
+// the chunk claims (8: every lane stores to a fixed slot of its workgroup's
+// pool); results are wrong, and 4 / 8 hand the local pass no chunk)
+#ifndef NMG_R2_ABL
+#define NMG_R2_ABL 0
+#endif
+constexpr uint32_t kWaves = kR2WG / 64;
 constexpr uint32_t kWaveWinBytes = 64 * kRecBytes;  // one wave window: 64 stride slots
 constexpr uint32_t kNoBuf = 0xffffffffu;            // RDesc::pad of "no buffer"
 
@@ -1044,22 +974,24 @@ __device__ __forceinline__ RDesc no_buf() {
 }
 
 // The three record loads of a lane's stride slot of the wave window at
-// (d, c), branch-free (a fixed number of memory ops per window, as
-// rload_slot_nb): a slot that is not a whole record inside the buffer reads
-// `safe` (a valid address) and gets zeros.
-__device__ __forceinline__ void wload(const uint8_t* data, uint64_t safe, uint64_t off, uint32_t len, uint32_t c,
-                                      int lane, RawRec& r) {
+// (off, c): buffer loads through a resource covering exactly the buffer
+// [off, off + len), so a slot past its end reads zeros without a branch or a
+// select (a select of a loaded value, or a load the compiler sinks into a
+// branch, would make the number of loads in flight path-dependent and every
+// later wait a full drain).  A slot partly inside the buffer reads part of
+// the record; the window's check sends it to the slow path.
+__device__ __forceinline__ void wload(const uint8_t* data, uint64_t off, uint32_t len, uint32_t c, int lane,
+                                      RawRec& r) {
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(data + off), (short)0, (int)len, 0x00020000);
   const uint32_t pos = c + uint32_t(lane) * kRecBytes;
-  const bool ok = uint64_t(pos) + kRecBytes <= len;
-  const uint64_t a = ok ? off + pos : safe;
-  const uint8_t* q = data + a;
-  const uint32_t odd = ok ? (pos >> 3) & 1 : 0u;
-  const uint4 x = *reinterpret_cast<const uint4*>(q + (odd ? 8 : 0));
-  const uint4 y = *reinterpret_cast<const uint4*>(q + (odd ? 24 : 16));
-  const uint2 z = *reinterpret_cast<const uint2*>(q + (odd ? 0 : 32));
-  r.x = ok ? x : make_uint4(0, 0, 0, 0);
-  r.y = ok ? y : make_uint4(0, 0, 0, 0);
-  r.z = ok ? z : make_uint2(0, 0);
+  const uint32_t odd = (pos >> 3) & 1;  // 16 B aligned pieces, as load_rec
+  const auto x = __builtin_amdgcn_raw_buffer_load_b128(rs, pos + (odd ? 8 : 0), 0, 0);
+  const auto y = __builtin_amdgcn_raw_buffer_load_b128(rs, pos + (odd ? 24 : 16), 0, 0);
+  const auto z = __builtin_amdgcn_raw_buffer_load_b64(rs, pos + (odd ? 0 : 32), 0, 0);
+  r.x = make_uint4(x[0], x[1], x[2], x[3]);
+  r.y = make_uint4(y[0], y[1], y[2], y[3]);
+  r.z = make_uint2(z[0], z[1]);
 }
 
 // route_partition with the segment table in LDS (uniform reads) instead of
@@ -1101,18 +1033,54 @@ __device__ __forceinline__ uint32_t route_partition_l(const SegL* s_seg, uint32_
   return q;
 }
 
+// route2's per-partition chunk state, one LDS word: open chunk (20 bits,
+// index in the workgroup's pool) | next chunk (20) | generation (8) | claims
+// (16).  Claim f < 64 takes slot f of the open chunk, 64 <= f < 128 slot
+// f - 64 of the next one, which is opened in advance; claim 96 takes a new
+// chunk from the pool and advances the generation (open <- next <- new,
+// claims -= 64, by compare-and-swap, so claims past 128 made meanwhile are
+// void: those lanes wait for the generation and claim again).  So every
+// chunk's slots are taken by exactly the claims that map to them (no hole),
+// and a claim needs one LDS round trip unless the partition is so hot that
+// 32 claims arrive while one lane takes a chunk.  Chunk ids kStNone (before
+// the partition's first claim) and kStOvf (pool exhausted: the overflow list).
+constexpr uint32_t kStNone = 0xfffffu, kStOvf = 0xffffeu, kStMaxLocal = 0xffffdu;
+__device__ __forceinline__ uint32_t st_cnt(uint64_t s) { return uint32_t(s) & 0xffffu; }
+__device__ __forceinline__ uint32_t st_gen(uint64_t s) { return (uint32_t(s) >> 16) & 0xffu; }
+__device__ __forceinline__ uint32_t st_next(uint64_t s) { return uint32_t(s >> 24) & 0xfffffu; }
+__device__ __forceinline__ uint32_t st_cur(uint64_t s) { return uint32_t(s >> 44); }
+__device__ __forceinline__ uint64_t st_pack(uint32_t cur, uint32_t next, uint32_t gen, uint32_t cnt) {
+  return (uint64_t(cur) << 44) | (uint64_t(next) << 24) | (uint64_t(gen & 0xffu) << 16) | cnt;
+}
+// a chunk of the workgroup's pool (its pool index), or kStOvf
+__device__ __forceinline__ uint32_t route2_take(uint32_t& taken, uint32_t cap) {
+  const uint32_t t = atomicAdd(&taken, 1u);
+  return t < cap ? t : kStOvf;
+}
+// generation g -> g + 1 of one partition: open <- next (or n1 on its first
+// claim), next <- n2, claims -> min(claims, 128) - 64 (first claim: 1, the
+// opener's own slot 0)
+__device__ __forceinline__ void route2_advance(unsigned long long* st, uint32_t g, uint32_t n1, uint32_t n2,
+                                               bool first) {
+  unsigned long long cur = __hip_atomic_load(st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  while (true) {
+    const uint32_t f = st_cnt(cur);
+    const unsigned long long nw = first ? st_pack(n1, n2, g + 1, 1u)
+                                        : st_pack(st_next(cur), n2, g + 1, min(f, 2 * kChunk) - kChunk);
+    const unsigned long long prev = atomicCAS(st, cur, nw);
+    if (prev == cur) break;
+    cur = prev;
+  }
+}
+
 template <bool TIMING>
-__global__ __launch_bounds__(kWG, 1) void route2_kernel(RouteParams rp) {
+__global__ __launch_bounds__(kR2WG, 1) void route2_kernel(RouteParams rp) {
   __shared__ uint64_t s_pb[kMaxParts + 1];
   __shared__ uint16_t s_pdir[kRouteDir];
-  __shared__ uint32_t s_hist[kMaxParts + 1], s_cur[2][kMaxParts + 1], s_nb[kMaxParts + 1];
-  __shared__ uint16_t s_start[kMaxParts + 1];
+  __shared__ unsigned long long s_state[kMaxParts + 1];  // open chunk << 32 | slots claimed in it
   __shared__ uint4 s_desc[kDescLds];
-  __shared__ uint4 s_a16[kRouteBatch];
-  __shared__ uint32_t s_uq[kRouteBatch];
-  __shared__ uint16_t s_perm[kRouteBatch];
   __shared__ uint32_t s_wlist[kWaves][64];  // slow path: the wave window's SAMPLE offsets
-  __shared__ uint32_t s_wsum[kWG / 64], s_misc[3], s_bnext, s_more[2];
+  __shared__ uint32_t s_taken, s_bnext;
   __shared__ unsigned long long s_gsums[2][kGlobalSums], s_gmins[2][18], s_gmaxs[2][18];
   __shared__ SegL s_seg[kRouteSegs];
 
@@ -1129,23 +1097,18 @@ __global__ __launch_bounds__(kWG, 1) void route2_kernel(RouteParams rp) {
   const uint32_t P = rp.nparts;
   const uint32_t c0 = rp.chunk0[blockIdx.x];
   const uint32_t cap = rp.chunk0[blockIdx.x + 1] - c0;
-  for (uint32_t i = tid; i < kMaxParts + 1; i += kWG) s_pb[i] = rp.pbounds[i];
-  for (uint32_t i = tid; i < kRouteDir; i += kWG) s_pdir[i] = rp.pdir[i];
-  for (uint32_t i = tid; i < P; i += kWG) {
-    s_hist[i] = 0;
-    s_cur[0][i] = kChunk;  // no open chunk (full)
-  }
+  const uint32_t capl = min(cap, kStMaxLocal + 1);  // (pool indices fit the state's 20-bit fields)
+  for (uint32_t i = tid; i < kMaxParts + 1; i += kR2WG) s_pb[i] = rp.pbounds[i];
+  for (uint32_t i = tid; i < kRouteDir; i += kR2WG) s_pdir[i] = rp.pdir[i];
+  for (uint32_t i = tid; i < P; i += kR2WG) s_state[i] = st_pack(kStNone, kStNone, 0, 2 * kChunk);
   const uint32_t r0 = p.ranges[blockIdx.x], r1 = p.ranges[blockIdx.x + 1];
-  for (uint32_t i = r0 + tid; i < r1 && i - r0 < kDescLds; i += kWG) {
+  for (uint32_t i = r0 + tid; i < r1 && i - r0 < kDescLds; i += kR2WG) {
     const BufDesc d = p.sbufs[i];
     s_desc[i - r0] = make_uint4((uint32_t)d.offset, (uint32_t)(d.offset >> 32), d.len, d.thread_rank | (d.access << 16));
   }
-  const RouteLds L{s_hist, s_start, &s_cur[0][0], s_nb, s_a16, s_pb, s_uq, s_perm, s_wsum, s_misc};
   if (tid == 0) {
-    s_misc[1] = 0;
-    s_misc[2] = kNoChunk;
+    s_taken = 0;
     s_bnext = r0;
-    s_more[0] = s_more[1] = 0;
   }
   if (tid < (int)kGlobalSums) s_gsums[0][tid] = s_gsums[1][tid] = 0;
   if (tid < 18) {
@@ -1157,11 +1120,7 @@ __global__ __launch_bounds__(kWG, 1) void route2_kernel(RouteParams rp) {
   uint32_t gwin = 0;
   lds_sync();
 
-  uint32_t nbatches = 0;
   if (r0 < r1) {
-    // a valid address for the loads of slots that hold no record
-    const uint64_t safe = __builtin_amdgcn_readfirstlane((uint32_t)p.sbufs[r0].offset) |
-                          (uint64_t(__builtin_amdgcn_readfirstlane((uint32_t)(p.sbufs[r0].offset >> 32))) << 32);
     // (descriptors are assigned, never selected as whole structs: a select of
     // structs goes through scratch memory)
     auto dequeue = [&](RDesc& d) {
@@ -1207,9 +1166,9 @@ __global__ __launch_bounds__(kWG, 1) void route2_kernel(RouteParams rp) {
       }
     };
     RawRec ra, rb;
-    wload(p.data, safe, d0.offset, d0.len, 0, lane, ra);
+    wload(p.data, d0.offset, d0.len, 0, lane, ra);
     predict();
-    wload(p.data, safe, eoff, elen, pcur, lane, rb);
+    wload(p.data, eoff, elen, pcur, lane, rb);
 
     RTimer rt;  // (TIMING) per-wave phase cycles
 #pragma unroll
@@ -1219,7 +1178,7 @@ __global__ __launch_bounds__(kWG, 1) void route2_kernel(RouteParams rp) {
 
     // one window of this wave: A holds its slots, B the next window's (in
     // flight); k = the window's place in the batch (staging slots)
-    auto window = [&](RawRec& A, RawRec& B, uint32_t k) {
+    auto window = [&](RawRec& A, RawRec& B) {
       const RDesc dw = d0;  // this window's buffer
       const uint32_t pos = cur + uint32_t(lane) * kRecBytes;
       const bool cand = pos < dw.len;
@@ -1314,18 +1273,19 @@ __global__ __launch_bounds__(kWG, 1) void route2_kernel(RouteParams rp) {
       // ---- the next window's loads again if it is not where B was loaded
       // (after a slow-path window), then the loads of the window after it
       if (d0.pad != pidx || (d0.pad != kNoBuf && cur != pcur)) {
-        wload(p.data, safe, d0.offset, d0.len, cur, lane, B);
+        wload(p.data, d0.offset, d0.len, cur, lane, B);
         vm_drain();  // (rare: keeps the waits on the common path exact)
       }
       predict();
-      wload(p.data, safe, eoff, elen, pcur, lane, A);
+      wload(p.data, eoff, elen, pcur, lane, A);
 
       // ---- this window's records: update_counters(global_counters, sample)
-      // (mem_sampling.c:882: every SAMPLE, matched or not), partition, batch
-      // rank, staging slot
+      // (mem_sampling.c:882: every SAMPLE, matched or not), partition, chunk
+      // slot, store
       rt_stamp<TIMING>(rt, 1);
       const uint32_t acc_l = dw.access();
-      if (valid) route_count(gacc, s_gsums, s_gmins, s_gmaxs, acc_l, uint32_t(rec.dsrc >> 5) & 0x3fff, rec.w);
+      if (valid && !(NMG_R2_ABL & 1))
+        route_count<NMG_R2MMREAD != 0>(gacc, s_gsums, s_gmins, s_gmaxs, acc_l, uint32_t(rec.dsrc >> 5) & 0x3fff, rec.w);
       if (++gwin == kDrainWindows) {
         dual_drain(gacc, s_gsums, lane);
         gwin = 0;
@@ -1333,63 +1293,90 @@ __global__ __launch_bounds__(kWG, 1) void route2_kernel(RouteParams rp) {
       rt_stamp<TIMING>(rt, 2);
       // below the first key ht_lower_key finds no node: counted, not routed
       const bool routed = valid && rec.addr >= first_start;
-      const uint32_t q = routed ? route_partition_l(s_seg, nseg, s_pb, s_pdir, rec.addr) : 0u;
+      const uint32_t q = !routed ? 0u
+                         : (NMG_R2_ABL & 2) ? uint32_t(rec.addr >> 12) % P
+                                            : route_partition_l(s_seg, nseg, s_pb, s_pdir, rec.addr);
       if (TIMING) (void)__builtin_amdgcn_readfirstlane(__ballot(q != 0));  // (the search ends here)
       rt_stamp<TIMING>(rt, 3);
-      Held hr;
-      hr.q = kNoChunk;
+      uint4 a = make_uint4(0, 0, 0, 0);
+      uint64_t pbq = 0;
       if (routed) {
-        const uint64_t pbq = s_pb[q];
-        const uint32_t rk = atomicAdd(&s_hist[q], 1u);
-        hr.q = q | (rk << 11);
-        hr.a = x_encode(rp.xl, pbq, rec.addr, rec.ts, rec.w, dw.pad, roff, dw.thread_rank(), acc_l);
+        pbq = s_pb[q];
+        a = x_encode(rp.xl, pbq, rec.addr, rec.ts, rec.w, dw.pad, roff, dw.thread_rank(), acc_l);
       }
-      route_stage(L, hr, k, tid);
       rt_stamp<TIMING>(rt, 4);
+      // ---- a slot in q's open chunks: one LDS atomic on the partition's
+      // state (route2_claim).  No barrier: the waves run on their own streams.
+      uint64_t dst = ~0ull;  // rec16 slot, or ~0: no slot (not routed / overflow list)
+      bool ovf = false;
+      {
+        bool todo = routed && !(NMG_R2_ABL & 8), spin = false;
+        if (NMG_R2_ABL & 8) dst = routed ? uint64_t(c0) * kChunk + (uint32_t)tid % max(cap * kChunk, 1u) : ~0ull;
+        uint32_t waitg = 0;
+        while (__ballot(todo)) {
+          if (todo) {
+            if (!spin) {
+              const uint64_t old = atomicAdd(&s_state[q], 1ull);
+              const uint32_t f = st_cnt(old), g = st_gen(old), cu = st_cur(old), nx = st_next(old);
+              if (cu != kStNone && f < 2 * kChunk) {  // a slot of the open chunk or of the next one
+                const uint32_t c = f < kChunk ? cu : nx;
+                if (c == kStOvf) ovf = true;
+                else dst = uint64_t(c0 + c) * kChunk + (f & (kChunk - 1));
+                todo = false;
+                if (f == kChunk + kChunk / 2) {  // half of the next chunk claimed: open the one after it
+                  const uint32_t n2 = route2_take(s_taken, capl);
+                  if (n2 != kStOvf && !(NMG_R2_ABL & 12)) rp.cmeta[c0 + n2] = q | (kChunk << 24);
+                  route2_advance(&s_state[q], g, n2, n2, false);
+                }
+              } else if (cu == kStNone && f == 2 * kChunk) {  // q's first claim: open two chunks
+                const uint32_t n1 = route2_take(s_taken, capl);
+                const uint32_t n2 = n1 == kStOvf ? kStOvf : route2_take(s_taken, capl);
+                if (!(NMG_R2_ABL & 12)) {
+                  if (n1 != kStOvf) rp.cmeta[c0 + n1] = q | (kChunk << 24);
+                  if (n2 != kStOvf) rp.cmeta[c0 + n2] = q | (kChunk << 24);
+                }
+                route2_advance(&s_state[q], g, n1, n2, true);
+                if (n1 == kStOvf) ovf = true;
+                else dst = uint64_t(c0 + n1) * kChunk;
+                todo = false;
+              } else {  // void claim (past the next chunk): wait for the next generation
+                spin = true;
+                waitg = g;
+              }
+            } else {
+              const uint64_t st = __hip_atomic_load(&s_state[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+              spin = st_gen(st) == waitg;
+            }
+          }
+        }
+      }
+      if (dst != ~0ull && !(NMG_R2_ABL & 4)) rp.rec16[dst] = a;
+      if (__ballot(ovf)) {  // (rare) a workgroup's pool outgrown: SAMPLEs shorter than 40 B
+        if (ovf) {
+          const uint32_t o = atomicAdd(rp.ovf_cnt, 1u);
+          if (o < rp.ovf_cap) {
+            rp.ovf16[o] = a;
+            rp.ovfx[o] = pbq;
+          } else {  // attributed at once
+            XRec xr = x_decode(rp.xl, pbq, a);
+            if (xr.esc) x_resolve(xr, p.data, p.sbufs);
+            direct_attribute(p, xr.addr, xr.ts, xr.w, xr.th, xr.acc, 0, rp.seq0 + xr.g, xr.off, xr.g);
+          }
+        }
+        vm_drain();  // (rare: nothing of this path stays pending where it joins the window)
+      }
+      rt_stamp<TIMING>(rt, 5);
     };
 
-    while (true) {
-      for (uint32_t k = 0; k < kRouteWindows; k += 2) {
-        window(ra, rb, k);
-        window(rb, ra, k + 1);
-      }
-      if (lane == 0 && d0.pad != kNoBuf) atomicOr(&s_more[nbatches & 1], 1u);
-      if (TIMING) {  // (the wait at the batch's first barrier)
-        lds_sync();
-        rt_stamp<TIMING>(rt, 8);
-      }
-      uint32_t more;
-      if (p.flags & kDbgRouteSorted) {
-        route_sort_batch<TIMING>(rt, rp, tid, L, nbatches, kRouteWindows, c0, cap);
-        more = __builtin_amdgcn_readfirstlane(s_more[nbatches & 1]);
-        if (tid == 0) s_more[(nbatches + 1) & 1] = 0;
-        vm_drain();  // (the prefetched window has long arrived: the chunk stores alone stay in flight)
-        route_write_batch<TIMING>(rt, rp, tid, L, nbatches);
-        nbatches++;
-        lds_sync();  // every wave has gathered the batch from the staging slots
-      } else {
-        lds_sync();  // every rank and staging store of the batch done
-        rt_stamp<TIMING>(rt, 5);
-        route_alloc_direct(rp, tid, L, nbatches, c0, cap);
-        more = __builtin_amdgcn_readfirstlane(s_more[nbatches & 1]);
-        if (tid == 0) s_more[(nbatches + 1) & 1] = 0;
-        lds_sync();  // chunk state of every partition set
-        rt_stamp<TIMING>(rt, 6);
-        vm_drain();  // (the prefetched window has long arrived: the chunk stores alone stay in flight)
-        route_store_direct(rp, tid, L, nbatches);
-        rt_stamp<TIMING>(rt, 7);
-        nbatches++;
-        // (no barrier: a lane reads back only its own staging slots, and the
-        // chunk state it reads changes after the next batch's first barrier)
-      }
-      rt_stamp<TIMING>(rt, 8);
-      if (!more) break;
-    }
+    do {  // (d0: the wave's stream, uniform)
+      window(ra, rb);
+      window(rb, ra);
+    } while (d0.pad != kNoBuf);
     if (TIMING && lane == 0) {
       unsigned long long* o = p.dbg + (uint64_t(blockIdx.x) * (kWG / 64) + tid / 64) * kRouteTimingWords;
       for (int k = 0; k < 9; k++) o[k] = rt.acc[k];
       o[9] = nwin;
-      o[10] = nbatches;
+      o[10] = 0;
     }
   }
   dual_drain(gacc, s_gsums, lane);
@@ -1403,12 +1390,17 @@ __global__ __launch_bounds__(kWG, 1) void route2_kernel(RouteParams rp) {
       atomicMax(reinterpret_cast<unsigned long long*>(p.max64 + a * 18 + tid), s_gmaxs[a][tid]);
     }
   }
-  // open chunks' fill, chunk counts per partition, pool use
-  for (uint32_t q = tid; q < P; q += kWG) {
-    const uint32_t cur = s_cur[nbatches & 1][q];
-    if ((cur & 127u) < kChunk) rp.cmeta[cur >> 7] = q | ((cur & 127u) << 24);
+  // the open and next chunks' fill (claims end below 96: the 96th advanced
+  // the generation); a next chunk nothing reached keeps fill 0, which the
+  // count and scatter passes skip; pool use
+  for (uint32_t q = tid; q < P; q += kR2WG) {
+    const unsigned long long st = s_state[q];
+    const uint32_t f = st_cnt(st), cu = st_cur(st), nx = st_next(st);
+    if (cu == kStNone || (NMG_R2_ABL & 12)) continue;
+    if (cu != kStOvf) rp.cmeta[c0 + cu] = q | (min(f, kChunk) << 24);
+    if (nx != kStOvf) rp.cmeta[c0 + nx] = q | ((f > kChunk ? f - kChunk : 0u) << 24);
   }
-  if (tid == 0) rp.used[blockIdx.x] = min(min(s_misc[1], cap), s_misc[2]);
+  if (tid == 0) rp.used[blockIdx.x] = (NMG_R2_ABL & 12) ? 0u : min(s_taken, capl);
 }
 
 // ---------------------------------------------------------------------------
@@ -1436,7 +1428,10 @@ __global__ __launch_bounds__(kWG) void count_kernel(CountParams cp) {
   for (uint32_t q = tid; q < P; q += kWG) s_cnt[q] = 0;
   __syncthreads();
   const uint32_t c0 = r.chunk0[w], n = r.used[w];
-  for (uint32_t c = c0 + tid; c < c0 + n; c += kWG) atomicAdd(&s_cnt[r.cmeta[c] & 0xffffffu], 1u);
+  for (uint32_t c = c0 + tid; c < c0 + n; c += kWG) {
+    const uint32_t m = r.cmeta[c];
+    if (m >> 24) atomicAdd(&s_cnt[m & 0xffffffu], 1u);  // (fill 0: a chunk route2 opened and nothing reached)
+  }
   __syncthreads();
   uint32_t* out = const_cast<uint32_t*>(r.pcnt) + uint64_t(w) * P;
   for (uint32_t q = tid; q < P; q += kWG) out[q] = s_cnt[q];
@@ -1512,6 +1507,7 @@ __global__ __launch_bounds__(kWG) void scatter_kernel(ScatterParams r) {
   const uint32_t* off = r.pcnt + uint64_t(w) * P;
   for (uint32_t c = c0 + tid; c < c0 + n; c += kWG) {
     const uint32_t m = r.cmeta[c], q = m & 0xffffffu;
+    if (!(m >> 24)) continue;
     const uint32_t k = atomicAdd(&s_cnt[q], 1u);
     r.clist[r.pbase[q] + off[q] + k] = c | ((m >> 24) << kChunkIdBits);  // chunk id | fill
   }
@@ -1548,7 +1544,7 @@ __global__ __launch_bounds__(kWG, 1) void local_kernel(LocalParams lp) {
   const bool pages = (p.flags & NMG_F_PAGE_HIST) != 0;
   RTimer rt;  // (kDbgLocalTiming) per-wave phase cycles
 #pragma unroll
-  for (int k = 0; k < 9; k++) rt.acc[k] = 0;
+  for (int k = 0; k < 10; k++) rt.acc[k] = 0;
   rt.last = TIMING ? stamp() : 0;
   uint32_t nchunks = 0, nit = 0;
   uint32_t nfound = 0;  // this wave's matched records (Params::found, added once at the end)
@@ -1807,7 +1803,7 @@ __global__ __launch_bounds__(kWG, 1) void local_kernel(LocalParams lp) {
       chunk_load(k + 7, B[1]);
     }
     lds_sync();
-    rt_stamp<TIMING>(rt, 8);  // (waiting for the item's slowest wave counts as flush)
+    rt_stamp<TIMING>(rt, 9);  // (waiting for the item's slowest wave)
     // the item's counters to global memory, consecutive lanes on consecutive
     // words, each LDS word zeroed for the next item as it is read; the only
     // item of its partition adds with plain loads and stores (no other
@@ -1862,6 +1858,7 @@ __global__ __launch_bounds__(kWG, 1) void local_kernel(LocalParams lp) {
     for (int k = 0; k < 9; k++) o[k] = rt.acc[k];
     o[9] = nchunks;
     o[10] = nit;
+    o[11] = rt.acc[9];
   }
 }
 
@@ -1907,8 +1904,8 @@ __global__ __launch_bounds__(kWG) void found_kernel(FoundParams r) {
 
 hipError_t launch_route(uint32_t grid, hipStream_t s, const RouteParams& r) {
   if ((r.p.flags & kDbgRouteV2) && (r.p.flags & kDbgRouteTiming))
-    hipLaunchKernelGGL(route2_kernel<true>, dim3(grid), dim3(kWG), 0, s, r);
-  else if (r.p.flags & kDbgRouteV2) hipLaunchKernelGGL(route2_kernel<false>, dim3(grid), dim3(kWG), 0, s, r);
+    hipLaunchKernelGGL(route2_kernel<true>, dim3(grid), dim3(kR2WG), 0, s, r);
+  else if (r.p.flags & kDbgRouteV2) hipLaunchKernelGGL(route2_kernel<false>, dim3(grid), dim3(kR2WG), 0, s, r);
   else if (r.p.flags & kDbgRouteTiming) hipLaunchKernelGGL(route_kernel<true>, dim3(grid), dim3(kWG), 0, s, r);
   else hipLaunchKernelGGL(route_kernel<false>, dim3(grid), dim3(kWG), 0, s, r);
   return hipGetLastError();

@@ -233,3 +233,79 @@ def test_online_live_tables_bit_exact(tmp_path, cfg, nb_alarms, chunk):
     eng.close()
     assert open(os.path.join(d, "o.txt"), "rb").read() == open(os.path.join(d, "e.txt"), "rb").read()
     _same_dirs(odir, edir)
+
+
+def test_failed_growth_keeps_state(tmp_path):
+    """nmg_update_objects that would grow an object past the page-histogram
+    budget fails with NMG_ERR_CAPACITY and leaves the engine as it was: the
+    analysis after it, nmg_get_page_cells and nmg_report equal an engine that
+    never saw the update."""
+    from numamma_amd.engine import Engine, table_objects
+
+    d = str(tmp_path)
+    rp = generate(SynthConfig(nb_samples=60_000, nb_intervals=2_000, with_stack=False, seed=78))
+    t = rp.table
+    ids = np.arange(t.nb_entries, dtype=np.uint32)
+    objs = table_objects(t)
+    cells = int((t.entries["buffer_size"] // 4096 + 1).sum())
+    budget = (cells + 8) * rp.nb_threads * 4  # every object dense, no room to grow one by 1 MiB
+    outs = []
+    for fail_first in (True, False):
+        eng = Engine(nb_threads=rp.nb_threads, hist_budget_bytes=budget)
+        eng.set_objects(t)
+        if fail_first:
+            big = objs.copy()
+            big["s"][5] += 1 << 20
+            with pytest.raises(_lib.NmgError) as ei:
+                eng.update_objects(t.keys, t.entry_off, ids, big)
+            assert ei.value.code == -8  # NMG_ERR_CAPACITY
+        eng.submit_replay(rp)
+        eng.analyze()
+        eng.synchronize()
+        edir = os.path.join(d, f"e{int(fail_first)}")
+        eng.report(edir, os.path.join(d, f"e{int(fail_first)}.txt"))
+        outs.append((eng.page_cells().copy(), eng.object_counters()[1].copy(), edir))
+        eng.close()
+    assert np.array_equal(outs[0][0], outs[1][0]) and np.array_equal(outs[0][1], outs[1][1])
+    assert open(os.path.join(d, "e1.txt"), "rb").read() == open(os.path.join(d, "e0.txt"), "rb").read()
+    _same_dirs(outs[0][2], outs[1][2])
+
+
+def test_partial_update_after_permuted_table(tmp_path):
+    """A live table listing every entry in a non-identity order, then a
+    partial table that brings new objects: the report walks the known entries
+    in the first table's order and the new ones after them (the walk order
+    always covers every entry)."""
+    from numamma_amd.engine import Engine, table_objects
+    from numamma_amd.replay import ObjectTable
+
+    rp = generate(SynthConfig(nb_samples=40_000, nb_intervals=500, with_stack=False, seed=79))
+    t = rp.table
+    E = t.nb_entries
+    objs = table_objects(t)
+    perm = np.random.default_rng(79).permutation(E).astype(np.uint32)
+    eng = Engine(nb_threads=rp.nb_threads)
+    eng.set_objects(ObjectTable.empty())
+    eng.update_objects(t.keys, t.entry_off, perm, objs)  # every entry, ids permuted
+    # two new objects past the table (ids E, E + 1), one key each
+    top = int(t.keys[-1]) + (1 << 30)
+    keys = np.array([top, top + (1 << 20)], dtype=np.uint64)
+    new = np.zeros(2, dtype=objs.dtype)
+    new["a"], new["s"], new["al"], new["fr"] = keys, 4096, 1, 2
+    eng.update_objects(keys, np.array([0, 1, 2], dtype=np.uint32), np.array([E, E + 1], dtype=np.uint32), new)
+    eng.submit_replay(rp)
+    eng.analyze()
+    eng.synchronize()
+    # the report's metadata in walk order: the table's entries, then the two new objects
+    ent = np.concatenate([t.entries, t.entries[:2].copy()])
+    ent["buffer_addr"][E:] = keys
+    ent["buffer_size"][E:] = 4096
+    ent["initial_buffer_size"][E:] = 4096
+    ent["alloc_date"][E:], ent["free_date"][E:] = 1, 2
+    eng.table = ObjectTable(np.concatenate([t.keys, keys]), np.concatenate([t.entry_off, [E + 1, E + 2]]).astype(np.uint32),
+                            ent, t.callstack_pool, t.string_pool)
+    eng.report(str(tmp_path), os.path.join(str(tmp_path), "x.txt"), online=True)
+    assert os.path.exists(os.path.join(str(tmp_path), "call_sites.log"))
+    g, ns, nf = eng.global_counters()
+    assert ns > 0
+    eng.close()

@@ -29,7 +29,6 @@ pytestmark = pytest.mark.gpu
 NO_ROUTE = 0x10000
 TINY_POOL = 0x20000
 ROUTE_V2 = 0x20000000  # (internal) route pass with per-wave record streams
-ROUTE_SORTED = 0x40000000  # (internal) ... its batches sorted in LDS instead of stored by the staging lane
 
 
 def _oracle(rp, d):
@@ -81,9 +80,8 @@ ROUTE_CASES = [
 
 
 @pytest.mark.parametrize("cfg", ROUTE_CASES, ids=[f"case{i}" for i in range(len(ROUTE_CASES))])
-@pytest.mark.parametrize("flags", [0, TINY_POOL, _lib.NMG_F_SINGLE_PASS, ROUTE_V2, ROUTE_V2 | TINY_POOL,
-                                   ROUTE_V2 | ROUTE_SORTED],
-                         ids=["route", "tinypool", "single", "v2", "v2tiny", "v2sorted"])
+@pytest.mark.parametrize("flags", [0, TINY_POOL, _lib.NMG_F_SINGLE_PASS, ROUTE_V2, ROUTE_V2 | TINY_POOL],
+                         ids=["route", "tinypool", "single", "v2", "v2tiny"])
 def test_route_bit_exact(tmp_path, cfg, flags):
     d = str(tmp_path)
     path, odir = _oracle(generate(cfg), d)

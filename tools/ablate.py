@@ -26,7 +26,6 @@ VARIANTS = {
     "legacy": 0x3 | 0x10000,            # attribute_kernel on a large table (kDbgNoRoute)
     "route": 0x3,                       # route + plan + scatter + local (default for > 1023 keys)
     "route_v2": 0x3 | 0x20000000,       # ... with the per-wave route pass (route2_kernel)
-    "route_v2s": 0x3 | 0x60000000,      # ... its batches sorted in LDS (route_sort_batch / route_write_batch)
     "route_v2_atomics": 0x3 | 0xA0000000,  # route_v2 with every local-pass flush through atomics
     "route_nopages": 0x1,               # ... without the page histogram
     "route_noloc": 0x3 | 0x400000,      # local pass loads its chunks only

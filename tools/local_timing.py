@@ -76,8 +76,9 @@ def main():
         for k, name in enumerate(PHASES):
             per = ch if k < 6 else it
             out[f"{name}_cyc_per_{'chunk' if k < 6 else 'item'}"] = float(a[:, k].sum() / per)
-        out["total_cyc_per_wave"] = float(a[:, :9].sum(axis=1).mean())
-        out["max_total_cyc_per_wave"] = float(a[:, :9].sum(axis=1).max())
+        out["imbalance_cyc_per_item"] = float(a[:, 11].sum() / it)  # waiting for the item's slowest wave
+        out["total_cyc_per_wave"] = float((a[:, :9].sum(axis=1) + a[:, 11]).mean())
+        out["max_total_cyc_per_wave"] = float((a[:, :9].sum(axis=1) + a[:, 11]).max())
         print(json.dumps(out), flush=True)
         e.close()
         del d

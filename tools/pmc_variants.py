@@ -53,7 +53,7 @@ def parse(args):
         names = {}
         for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
             for r in csv.DictReader(open(f)):
-                if "attribute_kernel" not in r["Kernel_Name"]:
+                if args.kernel not in r["Kernel_Name"]:
                     continue
                 i = int(r["Dispatch_Id"])
                 rows[i][r["Counter_Name"]] += float(r["Counter_Value"])
@@ -78,6 +78,7 @@ def main():
     ap.add_argument("--workload", default="c4")
     ap.add_argument("--variants", default="full,match")
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--kernel", default="attribute_kernel", help="kernel-name substring of the dispatches to count")
     args = ap.parse_args()
     run(args) if args.cmd == "run" else parse(args)
 

@@ -15,4 +15,6 @@ for s in "${SS[@]}"; do
     || { echo "pass $i failed"; tail -20 $d.log; exit 1; }
   dirs="$dirs $d"
 done
-python3 tools/pmc_variants.py parse $dirs --variants $VARS --reps $REPS | tee $OUT/pmcv_$TAG.jsonl
+for K in ${KERNELS:-attribute_kernel}; do
+  python3 tools/pmc_variants.py parse $dirs --variants $VARS --reps $REPS --kernel $K | sed "s/^{/{\"k\": \"$K\", /"
+done | tee $OUT/pmcv_$TAG.jsonl

@@ -30,7 +30,7 @@ TIMING = 0x800000
 WORDS = 12
 PHASES = ["wait", "issue", "global", "search", "rank", "scan", "alloc", "write", "state"]
 # route2_kernel (flag 0x20000000): per-wave windows; the last word is the batch barriers' wait
-PHASES_V2 = ["wait", "check_loads", "global", "search", "encode_rank", "scan", "alloc_perm", "write", "barrier"]
+PHASES_V2 = ["wait", "check_loads", "global", "search", "encode", "claim_store"]
 WORKLOADS = {
     "c4": dict(nb_samples=125_000_000, nb_intervals=1_000_000, size_max=64 * 1024),
     "c3": dict(nb_samples=100_000_000, nb_intervals=100_000),
@@ -75,8 +75,8 @@ def main():
         out = {"workload": wname, "flags": hex(args.flags), "analyze_ms": float(np.median(ms)),
                "windows_per_wave": float(a[:, 9].mean()), "batches_per_wave": float(a[:, 10].mean())}
         for k, name in enumerate(PHASES_V2 if args.flags & 0x20000000 else PHASES):
-            per = win if k < 5 else bat
-            out[f"{name}_cyc_per_{'window' if k < 5 else 'batch'}"] = float(a[:, k].sum() / per)
+            per = win if (k < 5 or args.flags & 0x20000000) else bat
+            out[f"{name}_cyc_per_{'window' if per is win else 'batch'}"] = float(a[:, k].sum() / per)
         out["total_cyc_per_wave"] = float(a[:, :9].sum(axis=1).mean())
         print(json.dumps(out), flush=True)
         e.close()
