@@ -78,7 +78,8 @@ constexpr uint32_t kDbgLocalNoObj = 0x1000000;   // local pass: no object counte
 constexpr uint32_t kDbgLocalNoPage = 0x2000000;  // local pass: no page cells
 constexpr uint32_t kDbgLocalNoGlobal = 0x4000000;  // local pass: no global counters
 constexpr uint32_t kDbgLocalNoSearch = 0x8000000;  // local pass: no lookup (nothing matches)
-constexpr uint32_t kDbgRouteV2 = 0x20000000;      // route pass: per-wave record streams (route2_kernel)
+constexpr uint32_t kDbgRouteV1 = 0x20000000;      // route pass: route_kernel (one workgroup-wide stream, batch
+                                                  // sort) instead of route2_kernel (A/B and tests)
 constexpr uint32_t kDbgLocalAtomics = 0x80000000u;  // local pass: every flush through atomics (A/B)
 constexpr uint32_t kDbgLocalTiming = 0x10000000;  // local pass: per-wave phase cycles in Params::dbg
                                                    // (wait, global, search, match, object, page per chunk;

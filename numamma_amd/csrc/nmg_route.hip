@@ -927,8 +927,8 @@ __global__ __launch_bounds__(kWG, 1) void route_kernel(RouteParams rp) {
 }
 
 // ---------------------------------------------------------------------------
-// pass 1 with per-wave record streams and no batches (route2_kernel;
-// kDbgRouteV2 for now).
+// pass 1 with per-wave record streams and no batches (route2_kernel, the
+// default; kDbgRouteV1 selects route_kernel).
 //
 // route_kernel moves one workgroup-wide byte cursor: every window of 1024
 // stride slots ends in a barrier (the fast-path check), and the batch sort
@@ -1535,10 +1535,10 @@ __global__ __launch_bounds__(kWG, 1) void local_kernel(LocalParams lp) {
   __shared__ unsigned long long s_first[kPartEntries];
   __shared__ uint32_t s_pg[kPartCells / 2];
   __shared__ uint32_t s_clist[kItemChunks];  // the item's chunk list entries
-  __shared__ uint32_t s_item;
+  __shared__ uint32_t s_item, s_cnext;
 
   Params& p = lp.p;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
   const uint32_t nitems = lp.ctl[0];
   const uint32_t T = p.nb_threads;
   const bool pages = (p.flags & NMG_F_PAGE_HIST) != 0;
@@ -1580,6 +1580,7 @@ __global__ __launch_bounds__(kWG, 1) void local_kernel(LocalParams lp) {
       for (uint32_t i = tid; i < kPartDir; i += kWG) s_dir[i] = gd[i];
       for (uint32_t i = tid; i < item.z - item.y; i += kWG) s_clist[i] = lp.clist[item.y + i];
     }
+    if (tid == 0) s_cnext = 0;
     const uint32_t ncell = (pages && pi.pages_lds) ? T * pi.span : 0u;
     const bool excl = item.w != 0 && !(p.flags & kDbgLocalAtomics);  // no other workgroup writes this partition's
                                                                      // counters
@@ -1588,8 +1589,9 @@ __global__ __launch_bounds__(kWG, 1) void local_kernel(LocalParams lp) {
                                  __builtin_amdgcn_readfirstlane((uint32_t)(s_keys[0] >> 32)));
     rt_stamp<TIMING>(rt, 7);
 
-    // Each wave takes every 16th chunk of the item (the item's list entries
-    // are in LDS) and works on two chunks at a time, their steps interleaved
+    // Each wave takes pairs of consecutive chunks of the item's list (in
+    // LDS) from an LDS counter, so the waves end within a pair of each other
+    // at the item's barrier, and works on two chunks at a time, their steps interleaved
     // (the LDS round trips of one cover the other's); the records of the next
     // two are in flight meanwhile (a wave's chunk is 1.5 KiB).  The compiler
     // waits for a chunk's loads with the smallest vmcnt any path allows, so
@@ -1598,23 +1600,21 @@ __global__ __launch_bounds__(kWG, 1) void local_kernel(LocalParams lp) {
     // covers the whole wave (a fixed number of memory ops between a load and
     // its use), and the rare paths that issue global memory ops of their own
     // end with vmcnt(0).
-    constexpr uint32_t kStride = kWG / 64;
     const uint32_t nl = item.z - item.y;
-    const uint32_t nmine = nl > (uint32_t)wave ? (nl - (uint32_t)wave + kStride - 1) / kStride : 0u;
-    auto chunk_load = [&](uint32_t k, uint4& a) {  // this wave's k-th chunk (any k: no branch)
-      const uint32_t e = k < nmine ? s_clist[(uint32_t)wave + k * kStride] : 0u;
+    auto chunk_load = [&](uint32_t l, uint4& a) {  // the chunk at list position l (l >= nl: none; no branch)
+      const uint32_t e = l < nl ? s_clist[l] : 0u;
       a = lp.rec16[uint64_t(e & ((1u << kChunkIdBits) - 1)) * kChunk + lane];
     };
-    // chunks k and k + 1 of this wave (k + 1 past the last: no valid lane)
-    auto process2 = [&](uint32_t k, const uint4 (&a16)[2]) {
+    // the chunks at list positions l0 and l1 (past the list: no valid lane)
+    auto process2 = [&](uint32_t l0, uint32_t l1, const uint4 (&a16)[2]) {
       uint32_t li[2];
       bool valid[2];
       uint64_t addr[2], ts[2], w[2];
       XRec xr[2];
 #pragma unroll
       for (int j = 0; j < 2; j++) {
-        li[j] = (uint32_t)wave + (k + j) * kStride;  // (list position in the item)
-        const uint32_t fill = k + j < nmine ? s_clist[li[j]] >> kChunkIdBits : 0u;
+        li[j] = j ? l1 : l0;
+        const uint32_t fill = li[j] < nl ? s_clist[li[j]] >> kChunkIdBits : 0u;
         valid[j] = (uint32_t)lane < fill;
       }
       if (TIMING) {  // (timing: these chunks' loads count as wait; the next two chunks' two loads are younger)
@@ -1625,7 +1625,7 @@ __global__ __launch_bounds__(kWG, 1) void local_kernel(LocalParams lp) {
       if (p.flags & kDbgLocalNoWork) {  // (ablation) loads only
 #pragma unroll
         for (int j = 0; j < 2; j++)
-          if (lane == 0 && k + j < nmine)
+          if (lane == 0 && li[j] < nl)
             lp.cmatch[s_clist[li[j]] & ((1u << kChunkIdBits) - 1)] = a16[j].x ^ a16[j].y ^ a16[j].z ^ a16[j].w;
         return;
       }
@@ -1727,7 +1727,7 @@ __global__ __launch_bounds__(kWG, 1) void local_kernel(LocalParams lp) {
       for (int j = 0; j < 2; j++) {
         const uint64_t fm = __ballot(erel[j] >= 0);
         nfound += (uint32_t)__popcll(fm);
-        if (lane == 0 && k + j < nmine) lp.cmatch[s_clist[li[j]] & ((1u << kChunkIdBits) - 1)] = fm;
+        if (lane == 0 && li[j] < nl) lp.cmatch[s_clist[li[j]] & ((1u << kChunkIdBits) - 1)] = fm;
       }
       rt_stamp<TIMING>(rt, 3);
       const bool noobj = (p.flags & kDbgLocalNoObj) != 0;
@@ -1790,17 +1790,25 @@ __global__ __launch_bounds__(kWG, 1) void local_kernel(LocalParams lp) {
       rt_stamp<TIMING>(rt, 5);
     };
     uint4 A[2], B[2];
-    chunk_load(0, A[0]);
-    chunk_load(1, A[1]);
-    chunk_load(2, B[0]);
-    chunk_load(3, B[1]);
-    for (uint32_t k = 0; k < nmine; k += 4) {
-      process2(k, A);
-      chunk_load(k + 4, A[0]);
-      chunk_load(k + 5, A[1]);
-      if (k + 2 < nmine) process2(k + 2, B);
-      chunk_load(k + 6, B[0]);
-      chunk_load(k + 7, B[1]);
+    auto grab = [&]() -> uint32_t {
+      uint32_t t = 0;
+      if (lane == 0) t = atomicAdd(&s_cnext, 2u);
+      return __builtin_amdgcn_readfirstlane(t);
+    };
+    uint32_t la = grab(), lb = grab();
+    chunk_load(la, A[0]);
+    chunk_load(la + 1, A[1]);
+    chunk_load(lb, B[0]);
+    chunk_load(lb + 1, B[1]);
+    while (la < nl) {
+      process2(la, la + 1, A);
+      la = grab();
+      chunk_load(la, A[0]);
+      chunk_load(la + 1, A[1]);
+      if (lb < nl) process2(lb, lb + 1, B);
+      lb = grab();
+      chunk_load(lb, B[0]);
+      chunk_load(lb + 1, B[1]);
     }
     lds_sync();
     rt_stamp<TIMING>(rt, 9);  // (waiting for the item's slowest wave)
@@ -1883,7 +1891,9 @@ __global__ __launch_bounds__(kWG) void found_kernel(FoundParams r) {
 #pragma unroll
     for (int u = 0; u < kU; u++) {
       const uint64_t kk = k + u * kWG;
-      bits[u] = kk < k1 ? r.cmatch[kk / kChunk] : 0ull;
+      // (a chunk of fill 0 -- route2 opened it and nothing reached it -- was
+      // never given to the local pass: its match bits are stale)
+      bits[u] = kk < k1 && (r.cmeta[kk / kChunk] >> 24) ? r.cmatch[kk / kChunk] : 0ull;
       xw[u] = ((bits[u] >> lane) & 1) ? reinterpret_cast<const uint64_t*>(r.rec16)[2 * kk + 1] >> r.gshift : 0ull;
     }
 #pragma unroll
@@ -1903,9 +1913,9 @@ __global__ __launch_bounds__(kWG) void found_kernel(FoundParams r) {
 // launchers
 
 hipError_t launch_route(uint32_t grid, hipStream_t s, const RouteParams& r) {
-  if ((r.p.flags & kDbgRouteV2) && (r.p.flags & kDbgRouteTiming))
+  if (!(r.p.flags & kDbgRouteV1) && (r.p.flags & kDbgRouteTiming))
     hipLaunchKernelGGL(route2_kernel<true>, dim3(grid), dim3(kR2WG), 0, s, r);
-  else if (r.p.flags & kDbgRouteV2) hipLaunchKernelGGL(route2_kernel<false>, dim3(grid), dim3(kR2WG), 0, s, r);
+  else if (!(r.p.flags & kDbgRouteV1)) hipLaunchKernelGGL(route2_kernel<false>, dim3(grid), dim3(kR2WG), 0, s, r);
   else if (r.p.flags & kDbgRouteTiming) hipLaunchKernelGGL(route_kernel<true>, dim3(grid), dim3(kWG), 0, s, r);
   else hipLaunchKernelGGL(route_kernel<false>, dim3(grid), dim3(kWG), 0, s, r);
   return hipGetLastError();

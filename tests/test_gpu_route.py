@@ -28,7 +28,7 @@ pytestmark = pytest.mark.gpu
 
 NO_ROUTE = 0x10000
 TINY_POOL = 0x20000
-ROUTE_V2 = 0x20000000  # (internal) route pass with per-wave record streams
+ROUTE_V1 = 0x20000000  # (internal) route_kernel instead of the default route2_kernel
 
 
 def _oracle(rp, d):
@@ -80,7 +80,7 @@ ROUTE_CASES = [
 
 
 @pytest.mark.parametrize("cfg", ROUTE_CASES, ids=[f"case{i}" for i in range(len(ROUTE_CASES))])
-@pytest.mark.parametrize("flags", [0, TINY_POOL, _lib.NMG_F_SINGLE_PASS, ROUTE_V2, ROUTE_V2 | TINY_POOL],
+@pytest.mark.parametrize("flags", [0, TINY_POOL, _lib.NMG_F_SINGLE_PASS, ROUTE_V1, ROUTE_V1 | TINY_POOL],
                          ids=["route", "tinypool", "single", "v2", "v2tiny"])
 def test_route_bit_exact(tmp_path, cfg, flags):
     d = str(tmp_path)
@@ -98,7 +98,7 @@ def _results(eng):
     return g, ns, nf, first, cw, bs, bf, eng.page_cells()
 
 
-@pytest.mark.parametrize("extra", [0, TINY_POOL, ROUTE_V2])
+@pytest.mark.parametrize("extra", [0, TINY_POOL, ROUTE_V1])
 def test_route_accumulates_like_single_pass(extra):
     """analyze, analyze (no reset), synchronize, analyze: the route path and
     the single-pass kernel accumulate the same counters, per-buffer match
@@ -150,7 +150,7 @@ def test_route_escaped_records_bit_exact(tmp_path):
         rec["addr"][far] = np.uint64(0x600000000000) + rng.integers(0, 1 << 41, int(far.sum()), dtype=np.uint64)
         rec["weight"][heavy] = rng.integers(1 << 14, 1 << 20, int(heavy.sum()), dtype=np.uint64)
     path, odir = _oracle(rp, d)
-    for tag, flags in (("route", 0), ("tiny", TINY_POOL), ("v2", ROUTE_V2), ("v2tiny", ROUTE_V2 | TINY_POOL)):
+    for tag, flags in (("route", 0), ("tiny", TINY_POOL), ("v1", ROUTE_V1), ("v1tiny", ROUTE_V1 | TINY_POOL)):
         edir, raw = _engine(path, d, _lib.NMG_F_DEFAULT | flags, tag)
         _same(os.path.join(d, "oracle_raw.bin"), raw)
         _same(os.path.join(d, "oracle_stdout.txt"), os.path.join(d, f"engine_{tag}_stdout.txt"))

@@ -24,9 +24,9 @@ VARIANTS = {
     "full": 0x3,                        # + page histogram (default product path)
     # large tables: the partition-first path (nmg_route.h) and its parts
     "legacy": 0x3 | 0x10000,            # attribute_kernel on a large table (kDbgNoRoute)
-    "route": 0x3,                       # route + plan + scatter + local (default for > 1023 keys)
-    "route_v2": 0x3 | 0x20000000,       # ... with the per-wave route pass (route2_kernel)
-    "route_v2_atomics": 0x3 | 0xA0000000,  # route_v2 with every local-pass flush through atomics
+    "route": 0x3,                       # route2 + count + plan + scatter + local (default for > 1023 keys)
+    "route_v1": 0x3 | 0x20000000,       # ... with route_kernel (workgroup-wide stream, batch sort)
+    "route_atomics": 0x3 | 0x80000000,  # every local-pass flush through atomics
     "route_nopages": 0x1,               # ... without the page histogram
     "route_noloc": 0x3 | 0x400000,      # local pass loads its chunks only
     "route_nowrite": 0x3 | 0x100000 | 0x400000,  # batches sorted in LDS, no chunk stores (local: loads only)
