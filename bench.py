@@ -352,10 +352,12 @@ def result_line(args, w, world, steps, ms_per_step, value, attr_ms, total_ms, ph
     traffic, pmc, traffic_src = load_traffic(w.name)
     routed = rest_ms > 0.0  # the partition-first path ran (tables > 1023 keys)
     kernels = {}
+    # the route pass: route2_kernel, or route_kernel under the internal switch 0x20000000
+    route = "route_kernel" if int(os.environ.get("NMG_BENCH_DEBUG_FLAGS", "0"), 0) & 0x20000000 else "route2_kernel"
     if routed:
-        # route_kernel reads every 40 B record and writes a 16 B compact record
-        # per sample (nmg_route.h XLayout); the local pass reads them back
-        kernels["route_kernel"] = {"avg_ms": first_ms, "algorithmic_bytes": w.samples * (RECORD_BYTES + COMPACT_BYTES)}
+        # the route pass reads every 40 B record and writes a 16 B compact
+        # record per sample (nmg_route.h XLayout); the local pass reads them back
+        kernels[route] = {"avg_ms": first_ms, "algorithmic_bytes": w.samples * (RECORD_BYTES + COMPACT_BYTES)}
         kernels["overflow+count+plan+scatter+local_kernel"] = {"avg_ms": rest_ms,
                                                                "algorithmic_bytes": w.samples * COMPACT_BYTES}
     else:
@@ -364,8 +366,8 @@ def result_line(args, w, world, steps, ms_per_step, value, attr_ms, total_ms, ph
         v["achieved_GBps"] = v["algorithmic_bytes"] / (v["avg_ms"] * 1e-3) / 1e9 if v["avg_ms"] else None
         v["frac"] = v["achieved_GBps"] / HBM_PEAK_GBS if v["achieved_GBps"] else None
         if pmc:
-            names = ["route_kernel"] if k == "route_kernel" else [n for n in pmc["kernels"] if n != "route_kernel"
-                                                                  and not n.startswith("reduce")]
+            names = [k] if k == route else [n for n in pmc["kernels"] if n not in ("route_kernel", "route2_kernel")
+                                           and not n.startswith("reduce")]
             v["traffic"] = sum(pmc["kernels"][n]["hbm_read_bytes"] + pmc["kernels"][n]["hbm_write_bytes"]
                                for n in names if n in pmc["kernels"])
     return {
@@ -392,7 +394,7 @@ def result_line(args, w, world, steps, ms_per_step, value, attr_ms, total_ms, ph
         },
         "roofline": {
             "bound": "hbm",
-            "kernel": ("nmg attribution launch, partition-first: route_kernel -> overflow/count/plan/scatter -> "
+            "kernel": (f"nmg attribution launch, partition-first: {route} -> overflow/count/plan/scatter -> "
                        "local_kernel" if routed else "nmg::attribute_kernel"),
             "achieved": achieved,
             "peak": HBM_PEAK_GBS,
@@ -407,7 +409,7 @@ def result_line(args, w, world, steps, ms_per_step, value, attr_ms, total_ms, ph
             "kernels": kernels,
             "note": "achieved = 40 B per record (SURVEY 8(d)) / attribution time, HIP events on the engine stream "
                     "around the kernels that attribute the records; the launch adds the long-tail reduce; "
-                    f"kernels = the same events split after route_kernel; traffic: {traffic_src}",
+                    f"kernels = the same events split after {route}; traffic: {traffic_src}",
         },
     }
 

@@ -1517,6 +1517,9 @@ __global__ __launch_bounds__(kWG) void scatter_kernel(ScatterParams r) {
 // pass 3: attribute one partition per workgroup at a time
 
 // a load served by L2, never by this CU's L1 (global_load ... sc1)
+#ifndef NMG_FLUSH_PIPE
+#define NMG_FLUSH_PIPE 0
+#endif
 template <typename T>
 __device__ __forceinline__ T l2_load(const T* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1843,6 +1846,41 @@ __global__ __launch_bounds__(kWG, 1) void local_kernel(LocalParams lp) {
         else atomicMin(reinterpret_cast<unsigned long long*>(pf), (unsigned long long)fo);
       }
     }
+#if NMG_FLUSH_PIPE
+    // the cells kU words per thread at a time: every load of the group in
+    // flight before the adds are stored (one L2 round trip per group, not per
+    // word), the row of a cell by a multiply-high (li * span < 2^32: exact)
+    {
+      const uint32_t nw = (ncell + 1) / 2, span = pi.span;
+      const uint32_t smag = span ? 0xffffffffu / span + 1u : 0u;
+      constexpr uint32_t kU = 4;
+      for (uint32_t j0 = tid; j0 < nw; j0 += kU * kWG) {
+        uint32_t cnt[kU][2], old[kU][2];
+        uint32_t* pc[kU][2];
+#pragma unroll
+        for (uint32_t u = 0; u < kU; u++) {
+          const uint32_t j = j0 + u * kWG;
+          const uint32_t v = j < nw ? s_pg[j] : 0u;
+          if (v) s_pg[j] = 0;
+#pragma unroll
+          for (uint32_t h = 0; h < 2; h++) {
+            cnt[u][h] = (v >> (16 * h)) & 0xffffu;
+            const uint32_t li = 2 * j + h, th = __umulhi(li, smag), rel = li - th * span;
+            pc[u][h] = p.hist + uint64_t(th) * p.hist_cells + pi.cb + rel;
+            old[u][h] = (excl && cnt[u][h]) ? l2_load(pc[u][h]) : 0u;
+          }
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < kU; u++)
+#pragma unroll
+          for (uint32_t h = 0; h < 2; h++) {
+            if (!cnt[u][h]) continue;
+            if (excl) *pc[u][h] = old[u][h] + cnt[u][h];
+            else atomicAdd(pc[u][h], cnt[u][h]);
+          }
+      }
+    }
+#else
     for (uint32_t j = tid; j < (ncell + 1) / 2; j += kWG) {
       const uint32_t v = s_pg[j];
       if (!v) continue;
@@ -1857,6 +1895,7 @@ __global__ __launch_bounds__(kWG, 1) void local_kernel(LocalParams lp) {
         else atomicAdd(pc, cnt);
       }
     }
+#endif
     lds_sync();
     rt_stamp<TIMING>(rt, 8);
   }

@@ -91,6 +91,33 @@ def main():
                       "export_ms": float(np.median(t_exp)), "reduce_2way_ms": float(np.median(t_red)),
                       "import_ms": float(np.median(t_imp)), "attribute_step_ms": eng.last_analyze_ms()}),
           flush=True)
+    # the packed page histogram of the one-process-per-GPU merge (distributed.HistPacker):
+    # cells <= 255 // world as bytes (u8 reduce), the rest as (cell, count) words (gather)
+    cells = eng.array_size(_lib.NMG_ARR_HIST32)
+    if cells:
+        u8 = torch.empty(cells, dtype=torch.uint8, device=dev)
+        cap = max(1024, cells // 8)
+        ovf = torch.zeros(cap, dtype=torch.int64, device=dev)
+        for world in (2, 8):
+            thr = 255 // world
+            tp, tu = [], []
+            for _ in range(args.reps):
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                n = eng.hist_pack(thr, u8.data_ptr(), ovf.data_ptr(), cap)
+                torch.cuda.synchronize()
+                t1 = time.perf_counter()
+                if n <= cap:  # (a longer list: the u32 reduce instead)
+                    eng.hist_unpack(u8.data_ptr(), ovf.data_ptr(), n)
+                eng.synchronize()
+                t2 = time.perf_counter()
+                tp.append((t1 - t0) * 1e3)
+                tu.append((t2 - t1) * 1e3)
+            dense = sum(a.numel() * a.element_size() for w, a, _ in arrays if w != _lib.NMG_ARR_HIST32)
+            print(json.dumps({"measure": "hist_packed", "workload": args.workload, "world": world, "cells": cells,
+                              "hist_u32_bytes": cells * 4, "overflow_cells": n, "packed_bytes": cells + 8 * n,
+                              "bytes_per_rank_packed": dense + cells + 8 * n, "pack_ms": float(np.median(tp)),
+                              "unpack_ms": float(np.median(tu))}), flush=True)
     eng.close()
     del d_arena
     if args.skip_multi:

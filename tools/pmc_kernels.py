@@ -17,7 +17,7 @@ def main():
             for r in csv.DictReader(open(f)):
                 agg[r["Kernel_Name"].split("(")[0][:60]][r["Counter_Name"]].append(float(r["Counter_Value"]))
     for k, v in sorted(agg.items()):
-        if not any(s in k for s in ("attribute", "reduce", "route_kernel", "local_kernel", "found_kernel")):
+        if not any(s in k for s in ("attribute", "reduce", "route_kernel", "route2_kernel", "local_kernel", "found_kernel")):
             continue
         print(json.dumps({"kernel": k, **{c: sum(x) / len(x) for c, x in sorted(v.items())},
                           "dispatches": max(len(x) for x in v.values())}))

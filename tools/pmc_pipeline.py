@@ -23,9 +23,9 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-PIPELINE = ("route_kernel", "overflow_kernel", "count_kernel", "plan_kernel", "scatter_kernel", "local_kernel",
+PIPELINE = ("route2_kernel", "route_kernel", "overflow_kernel", "count_kernel", "plan_kernel", "scatter_kernel", "local_kernel",
             "attribute_kernel", "reduce")
-STREAMING = ("route_kernel", "local_kernel", "attribute_kernel")
+STREAMING = ("route2_kernel", "route_kernel", "local_kernel", "attribute_kernel")
 
 
 def per_kernel(d):
@@ -52,7 +52,7 @@ def main():
     from numamma_amd.srchash import kernel_source_hash
 
     fetch, write = per_kernel(args.fetch), per_kernel(args.write)
-    first = "route_kernel" if "route_kernel" in fetch else "attribute_kernel"
+    first = next(k for k in ("route2_kernel", "route_kernel", "attribute_kernel") if k in fetch)
     launches = fetch[first][1]
     wlaunches = write[first][1]
     kernels = {}
