@@ -140,6 +140,9 @@ def main():
     ap.add_argument("--secondary", default="c2,c3",
                     help="workloads measured after the main one, comma-separated (N=1; '' = none)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--handle", action="store_true",
+                    help="without a launcher, drive the GPUs through one engine handle even for --gpus 1 "
+                         "(host-staged buffers, as --gpus N > 1 does), so a 1 -> N curve compares one path")
     ap.add_argument("--cpu-records", type=int, default=100_000,
                     help="records in the reference-loop oracle's sample (its linear call-site list is quadratic)")
     ap.add_argument("--cpu-st-records", type=int, default=2_000_000,
@@ -156,7 +159,7 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world == 1 and args.gpus > 1:  # no launcher: one process drives every GPU through the C-ABI
+    if world == 1 and (args.gpus > 1 or args.handle):  # no launcher: one process drives every GPU through the C-ABI
         return main_one_process(args)
     # test hooks for the multi-rank path on a one-GPU box (never used by the driver):
     # NMG_BENCH_BACKEND=gloo, NMG_BENCH_SAME_GPU=1 (every rank on GPU 0)

@@ -2200,7 +2200,7 @@ static bool route_eligible(nmg_engine* h, const std::vector<BufDesc>& descs) {
     bytes += descs[i].len;
   }
   // chunk ids (route pass LDS: id << 7 | fill) -- an upper bound of the pool
-  const uint64_t chunks = (bytes / kRecBytes + descs.size()) / kChunk + (uint64_t)h->num_cus * (h->nparts + 2);
+  const uint64_t chunks = (bytes / kRecBytes + descs.size()) / kChunk + (uint64_t)h->num_cus * (2 * h->nparts + 2);
   if (chunks >= (1ull << kChunkIdBits)) return false;
   XLayout xl;
   return route_layout(h, descs, xl);
@@ -2208,8 +2208,8 @@ static bool route_eligible(nmg_engine* h, const std::vector<BufDesc>& descs) {
 static bool route_eligible(nmg_engine* h) { return route_eligible(h, h->descs); }
 
 // per-workgroup private chunk pools for a new schedule: every SAMPLE record
-// of at least 40 B fits (a partition's chunks are full but for its one open
-// chunk); shorter records past that are attributed directly
+// of at least 40 B fits (a partition's chunks are full but for its open and
+// next chunks); shorter records past that are attributed directly
 static int route_pool(nmg_engine* h, const std::vector<BufDesc>& descs, uint32_t grid, const uint32_t* ranges,
                       std::vector<uint32_t>& c0) {
   const uint32_t P = h->nparts;
@@ -2218,7 +2218,9 @@ static int route_pool(nmg_engine* h, const std::vector<BufDesc>& descs, uint32_t
   for (uint32_t w = 0; w < grid; w++) {
     uint64_t rec = 0;
     for (uint32_t b = ranges[w]; b < ranges[w + 1]; b++) rec += (descs[b].len + kRecBytes - 1) / kRecBytes;
-    const uint64_t cap = (h->flags & kDbgTinyPool) ? 2 : (rec + kChunk - 1) / kChunk + P;
+    // (route2_kernel keeps two chunks open per partition: the open one and
+    // the next, opened ahead)
+    const uint64_t cap = (h->flags & kDbgTinyPool) ? 2 : (rec + kChunk - 1) / kChunk + 2 * P;
     c0[w] = (uint32_t)tot;
     tot += cap;
   }

@@ -1517,9 +1517,6 @@ __global__ __launch_bounds__(kWG) void scatter_kernel(ScatterParams r) {
 // pass 3: attribute one partition per workgroup at a time
 
 // a load served by L2, never by this CU's L1 (global_load ... sc1)
-#ifndef NMG_FLUSH_PIPE
-#define NMG_FLUSH_PIPE 0
-#endif
 template <typename T>
 __device__ __forceinline__ T l2_load(const T* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1846,7 +1843,6 @@ __global__ __launch_bounds__(kWG, 1) void local_kernel(LocalParams lp) {
         else atomicMin(reinterpret_cast<unsigned long long*>(pf), (unsigned long long)fo);
       }
     }
-#if NMG_FLUSH_PIPE
     // the cells kU words per thread at a time: every load of the group in
     // flight before the adds are stored (one L2 round trip per group, not per
     // word), the row of a cell by a multiply-high (li * span < 2^32: exact)
@@ -1880,22 +1876,6 @@ __global__ __launch_bounds__(kWG, 1) void local_kernel(LocalParams lp) {
           }
       }
     }
-#else
-    for (uint32_t j = tid; j < (ncell + 1) / 2; j += kWG) {
-      const uint32_t v = s_pg[j];
-      if (!v) continue;
-      s_pg[j] = 0;
-#pragma unroll
-      for (uint32_t h = 0; h < 2; h++) {
-        const uint32_t cnt = (v >> (16 * h)) & 0xffffu;
-        if (!cnt) continue;
-        const uint32_t li = 2 * j + h, th = li / pi.span, rel = li - th * pi.span;
-        uint32_t* pc = p.hist + uint64_t(th) * p.hist_cells + pi.cb + rel;
-        if (excl) *pc = l2_load(pc) + cnt;
-        else atomicAdd(pc, cnt);
-      }
-    }
-#endif
     lds_sync();
     rt_stamp<TIMING>(rt, 8);
   }
