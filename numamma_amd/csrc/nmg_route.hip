@@ -982,6 +982,12 @@ __device__ __forceinline__ RDesc no_buf() {
 // the record; the window's check sends it to the slow path.
 __device__ __forceinline__ void wload(const uint8_t* data, uint64_t off, uint32_t len, uint32_t c, int lane,
                                       RawRec& r) {
+  // (the stream's fields are wave-uniform but may live in vector registers:
+  // read them into scalars, or every load becomes a waterfall loop over the
+  // resource)
+  off = u64of(__builtin_amdgcn_readfirstlane((uint32_t)off), __builtin_amdgcn_readfirstlane((uint32_t)(off >> 32)));
+  len = __builtin_amdgcn_readfirstlane(len);
+  c = __builtin_amdgcn_readfirstlane(c);
   const __amdgpu_buffer_rsrc_t rs =
       __builtin_amdgcn_make_buffer_rsrc((void*)(data + off), (short)0, (int)len, 0x00020000);
   const uint32_t pos = c + uint32_t(lane) * kRecBytes;
