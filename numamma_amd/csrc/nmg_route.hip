@@ -1066,9 +1066,11 @@ __device__ __forceinline__ uint32_t route2_take(uint32_t& taken, uint32_t cap) {
 // generation g -> g + 1 of one partition: open <- next (or n1 on its first
 // claim), next <- n2, claims -> min(claims, 128) - 64 (first claim: 1, the
 // opener's own slot 0)
+// (hint: the word after this lane's own claim, the value when no other claim
+// came in between -- the first compare-and-swap usually succeeds)
 __device__ __forceinline__ void route2_advance(unsigned long long* st, uint32_t g, uint32_t n1, uint32_t n2,
-                                               bool first) {
-  unsigned long long cur = __hip_atomic_load(st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                                               bool first, unsigned long long hint) {
+  unsigned long long cur = hint;
   while (true) {
     const uint32_t f = st_cnt(cur);
     const unsigned long long nw = first ? st_pack(n1, n2, g + 1, 1u)
@@ -1184,7 +1186,21 @@ __global__ __launch_bounds__(kR2WG, 1) void route2_kernel(RouteParams rp) {
 
     // one window of this wave: A holds its slots, B the next window's (in
     // flight); k = the window's place in the batch (staging slots)
+    // (the stream state is wave-uniform, but values merged across branches
+    // may be kept in vector registers, and then every test of them is an
+    // exec-mask branch: read them back into scalars once per window)
+    auto uni = [&](RDesc& d) {
+      d.offset = u64of(__builtin_amdgcn_readfirstlane((uint32_t)d.offset),
+                       __builtin_amdgcn_readfirstlane((uint32_t)(d.offset >> 32)));
+      d.len = __builtin_amdgcn_readfirstlane(d.len);
+      d.ta = __builtin_amdgcn_readfirstlane(d.ta);
+      d.pad = __builtin_amdgcn_readfirstlane(d.pad);
+    };
     auto window = [&](RawRec& A, RawRec& B) {
+      uni(d0);
+      uni(d1);
+      cur = __builtin_amdgcn_readfirstlane(cur);
+      ns = __builtin_amdgcn_readfirstlane(ns);
       const RDesc dw = d0;  // this window's buffer
       const uint32_t pos = cur + uint32_t(lane) * kRecBytes;
       const bool cand = pos < dw.len;
@@ -1332,7 +1348,7 @@ __global__ __launch_bounds__(kR2WG, 1) void route2_kernel(RouteParams rp) {
                 if (f == kChunk + kChunk / 2) {  // half of the next chunk claimed: open the one after it
                   const uint32_t n2 = route2_take(s_taken, capl);
                   if (n2 != kStOvf && !(NMG_R2_ABL & 12)) rp.cmeta[c0 + n2] = q | (kChunk << 24);
-                  route2_advance(&s_state[q], g, n2, n2, false);
+                  route2_advance(&s_state[q], g, n2, n2, false, old + 1);
                 }
               } else if (cu == kStNone && f == 2 * kChunk) {  // q's first claim: open two chunks
                 const uint32_t n1 = route2_take(s_taken, capl);
@@ -1341,7 +1357,7 @@ __global__ __launch_bounds__(kR2WG, 1) void route2_kernel(RouteParams rp) {
                   if (n1 != kStOvf) rp.cmeta[c0 + n1] = q | (kChunk << 24);
                   if (n2 != kStOvf) rp.cmeta[c0 + n2] = q | (kChunk << 24);
                 }
-                route2_advance(&s_state[q], g, n1, n2, true);
+                route2_advance(&s_state[q], g, n1, n2, true, old + 1);
                 if (n1 == kStOvf) ovf = true;
                 else dst = uint64_t(c0 + n1) * kChunk;
                 todo = false;
