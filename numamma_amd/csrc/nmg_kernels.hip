@@ -520,7 +520,7 @@ __global__ __launch_bounds__(kWG, 1) void attribute_kernel(Params p) {
   __shared__ uint4 s_tab[kTabBytes / 16];  // lookup structure (layouts at kTabBytes)
   __shared__ uint32_t s_list[kMaxList];
   __shared__ WgCounters wc;
-  __shared__ uint32_t s_flags[3], s_nlist, s_next, s_err;
+  __shared__ uint32_t s_flags[3], s_nlist, s_next, s_err, s_nfound;
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -575,6 +575,11 @@ __global__ __launch_bounds__(kWG, 1) void attribute_kernel(Params p) {
   lane_acc_clear(acc);
   uint32_t win = 0, acc_windows = 0, last_flush = 0;
   uint32_t ns0 = 0, nf0 = 0, ns1 = 0, nf1 = 0;  // per-buffer tallies: buffer idx, idx + 1
+  // this wave's matched samples; Params::found gets one add per workgroup at
+  // the end (an add per buffer from every wave, all on that one word, made
+  // the kernel 3.4x slower at configs[1])
+  uint32_t nfound = 0;
+  if (tid == 0) s_nfound = 0;  // (read after the loop's barriers)
   uint64_t tacc[4] = {0, 0, 0, 0}, t_start = 0, t0 = 0, t1 = 0;
   if (TIMING) t_start = t0 = stamp();
   constexpr bool kSpec = (MODE & kModeLarge) && !(MODE & kModeDenseObj);
@@ -779,16 +784,12 @@ __global__ __launch_bounds__(kWG, 1) void attribute_kernel(Params p) {
       // tallies (mem_sampling.c:921-926)
       if (lane == 0) {
         if (ns0) atomicAdd(p.bufcnt + d0.pad, ns0);
-        if (nf0) {
-          atomicAdd(p.bufcnt + p.nb_bufs + d0.pad, nf0);
-          atomicAdd(p.found, (unsigned long long)nf0);
-        }
+        if (nf0) atomicAdd(p.bufcnt + p.nb_bufs + d0.pad, nf0);
+        nfound += nf0;
         if (nidx == idx + 2) {
           if (ns1) atomicAdd(p.bufcnt + d1.pad, ns1);
-          if (nf1) {
-            atomicAdd(p.bufcnt + p.nb_bufs + d1.pad, nf1);
-            atomicAdd(p.found, (unsigned long long)nf1);
-          }
+          if (nf1) atomicAdd(p.bufcnt + p.nb_bufs + d1.pad, nf1);
+          nfound += nf1;
         }
       }
       if (nidx == idx + 1) {
@@ -825,6 +826,9 @@ __global__ __launch_bounds__(kWG, 1) void attribute_kernel(Params p) {
     }
     if (idx >= r1) break;  // the loop's only exit, after the state update
   }
+  if (lane == 0 && nfound) atomicAdd(&s_nfound, nfound);
+  lds_sync();
+  if (tid == 0 && s_nfound) atomicAdd(p.found, (unsigned long long)s_nfound);
   if (kLog && p.tlog) {  // the sub-logs' fill (every append of this workgroup is done)
     lds_sync();
     if (kLog && p.tlog)

@@ -1557,7 +1557,7 @@ __global__ __launch_bounds__(kWG, 1) void local_kernel(LocalParams lp) {
   __shared__ unsigned long long s_first[kPartEntries];
   __shared__ uint32_t s_pg[kPartCells / 2];
   __shared__ uint32_t s_clist[kItemChunks];  // the item's chunk list entries
-  __shared__ uint32_t s_item, s_cnext;
+  __shared__ uint32_t s_item, s_cnext, s_nfound;
 
   Params& p = lp.p;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -1569,7 +1569,8 @@ __global__ __launch_bounds__(kWG, 1) void local_kernel(LocalParams lp) {
   for (int k = 0; k < 10; k++) rt.acc[k] = 0;
   rt.last = TIMING ? stamp() : 0;
   uint32_t nchunks = 0, nit = 0;
-  uint32_t nfound = 0;  // this wave's matched records (Params::found, added once at the end)
+  uint32_t nfound = 0;  // this wave's matched records (Params::found, added once per workgroup at the end)
+  if (tid == 0) s_nfound = 0;  // (read after the item loop's barriers)
   // the item counters start zeroed; every flush re-zeroes what it reads
   for (uint32_t i = tid; i < kPartEntries; i += kWG) {
     s_owt[0][i] = s_owt[1][i] = 0;
@@ -1901,7 +1902,9 @@ __global__ __launch_bounds__(kWG, 1) void local_kernel(LocalParams lp) {
     lds_sync();
     rt_stamp<TIMING>(rt, 8);
   }
-  if (lane == 0 && nfound) atomicAdd(p.found, (unsigned long long)nfound);
+  if (lane == 0 && nfound) atomicAdd(&s_nfound, nfound);  // (one add to Params::found per workgroup)
+  lds_sync();
+  if (tid == 0 && s_nfound) atomicAdd(p.found, (unsigned long long)s_nfound);
   if (TIMING && lane == 0) {
     unsigned long long* o = p.dbg + (uint64_t(blockIdx.x) * (kWG / 64) + tid / 64) * kRouteTimingWords;
     for (int k = 0; k < 9; k++) o[k] = rt.acc[k];
