@@ -94,6 +94,11 @@ def main():
     # the packed page histogram of the one-process-per-GPU merge (distributed.HistPacker):
     # cells <= 255 // world as bytes (u8 reduce), the rest as (cell, count) words (gather)
     cells = eng.array_size(_lib.NMG_ARR_HIST32)
+    # (the reduce loop above doubled the counters at every repetition: one
+    # fresh analysis for the packed form)
+    eng.reset()
+    eng.analyze()
+    eng.synchronize()
     if cells:
         u8 = torch.empty(cells, dtype=torch.uint8, device=dev)
         cap = max(1024, cells // 8)
