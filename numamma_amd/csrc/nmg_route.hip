@@ -1539,13 +1539,25 @@ __global__ __launch_bounds__(kWG) void scatter_kernel(ScatterParams r) {
 // pass 3: attribute one partition per workgroup at a time
 
 // a load served by L2, never by this CU's L1 (global_load ... sc1)
+// local pass: workgroup size and chunks per interleaved group (a wave holds
+// two groups: one being attributed, the other's records in flight)
+#ifndef NMG_LWG
+#define NMG_LWG 1024
+#endif
+#ifndef NMG_LC
+#define NMG_LC 2
+#endif
+#define NMG_STR2(x) #x
+#define NMG_STR(x) NMG_STR2(x)
+constexpr uint32_t kLWG = NMG_LWG;
+constexpr int kLC = NMG_LC;
 template <typename T>
 __device__ __forceinline__ T l2_load(const T* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 template <bool TIMING>
-__global__ __launch_bounds__(kWG, 1) void local_kernel(LocalParams lp) {
+__global__ __launch_bounds__(kLWG, 1) void local_kernel(LocalParams lp) {
   __shared__ uint64_t s_keys[kPartSlots];
   // node records split in two 16 B arrays (addr, end) and (alloc, free): a
   // 16 B stride spreads a wave's random reads over twice the bank groups of
@@ -1572,11 +1584,11 @@ __global__ __launch_bounds__(kWG, 1) void local_kernel(LocalParams lp) {
   uint32_t nfound = 0;  // this wave's matched records (Params::found, added once per workgroup at the end)
   if (tid == 0) s_nfound = 0;  // (read after the item loop's barriers)
   // the item counters start zeroed; every flush re-zeroes what it reads
-  for (uint32_t i = tid; i < kPartEntries; i += kWG) {
+  for (uint32_t i = tid; i < kPartEntries; i += kLWG) {
     s_owt[0][i] = s_owt[1][i] = 0;
     s_first[i] = ~0ull;
   }
-  for (uint32_t i = tid; i < kPartCells / 2; i += kWG) s_pg[i] = 0;
+  for (uint32_t i = tid; i < kPartCells / 2; i += kLWG) s_pg[i] = 0;
   while (true) {
     if (tid == 0) s_item = atomicAdd(lp.ctl + 1, 1u);
     lds_sync();
@@ -1593,15 +1605,15 @@ __global__ __launch_bounds__(kWG, 1) void local_kernel(LocalParams lp) {
       const uint64_t* gk = lp.pe_keys + uint64_t(q) * kPartSlots;
       const uint4* gn = lp.pe_nodes + uint64_t(q) * kPartSlots * 2;
       const uint2* gi = lp.pe_info + uint64_t(q) * kPartSlots;
-      for (uint32_t i = tid; i < nk; i += kWG) {
+      for (uint32_t i = tid; i < nk; i += kLWG) {
         s_keys[i] = gk[i];
         s_nodes[i] = gn[2 * i];
         s_dates[i] = gn[2 * i + 1];
         s_info[i] = gi[i];
       }
       const uint32_t* gd = lp.pe_dir + uint64_t(q) * kPartDir;
-      for (uint32_t i = tid; i < kPartDir; i += kWG) s_dir[i] = gd[i];
-      for (uint32_t i = tid; i < item.z - item.y; i += kWG) s_clist[i] = lp.clist[item.y + i];
+      for (uint32_t i = tid; i < kPartDir; i += kLWG) s_dir[i] = gd[i];
+      for (uint32_t i = tid; i < item.z - item.y; i += kLWG) s_clist[i] = lp.clist[item.y + i];
     }
     if (tid == 0) s_cnext = 0;
     const uint32_t ncell = (pages && pi.pages_lds) ? T * pi.span : 0u;
@@ -1628,26 +1640,26 @@ __global__ __launch_bounds__(kWG, 1) void local_kernel(LocalParams lp) {
       const uint32_t e = l < nl ? s_clist[l] : 0u;
       a = lp.rec16[uint64_t(e & ((1u << kChunkIdBits) - 1)) * kChunk + lane];
     };
-    // the chunks at list positions l0 and l1 (past the list: no valid lane)
-    auto process2 = [&](uint32_t l0, uint32_t l1, const uint4 (&a16)[2]) {
-      uint32_t li[2];
-      bool valid[2];
-      uint64_t addr[2], ts[2], w[2];
-      XRec xr[2];
+    // the kLC chunks at list positions l0, l0 + 1, ... (past the list: no valid lane)
+    auto process = [&](uint32_t l0, const uint4 (&a16)[kLC]) {
+      uint32_t li[kLC];
+      bool valid[kLC];
+      uint64_t addr[kLC], ts[kLC], w[kLC];
+      XRec xr[kLC];
 #pragma unroll
-      for (int j = 0; j < 2; j++) {
-        li[j] = j ? l1 : l0;
+      for (int j = 0; j < kLC; j++) {
+        li[j] = l0 + j;
         const uint32_t fill = li[j] < nl ? s_clist[li[j]] >> kChunkIdBits : 0u;
         valid[j] = (uint32_t)lane < fill;
       }
-      if (TIMING) {  // (timing: these chunks' loads count as wait; the next two chunks' two loads are younger)
-        asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-        nchunks += 2;
+      if (TIMING) {  // (timing: these chunks' loads count as wait; the other group's kLC loads are younger)
+        asm volatile("s_waitcnt vmcnt(" NMG_STR(NMG_LC) ")" ::: "memory");
+        nchunks += kLC;
       }
       rt_stamp<TIMING>(rt, 0);
       if (p.flags & kDbgLocalNoWork) {  // (ablation) loads only
 #pragma unroll
-        for (int j = 0; j < 2; j++)
+        for (int j = 0; j < kLC; j++)
           if (lane == 0 && li[j] < nl)
             lp.cmatch[s_clist[li[j]] & ((1u << kChunkIdBits) - 1)] = a16[j].x ^ a16[j].y ^ a16[j].z ^ a16[j].w;
         return;
@@ -1655,18 +1667,18 @@ __global__ __launch_bounds__(kWG, 1) void local_kernel(LocalParams lp) {
       // (update_counters of every routed SAMPLE: the route pass)
       bool esc = false;
 #pragma unroll
-      for (int j = 0; j < 2; j++) {
+      for (int j = 0; j < kLC; j++) {
         xr[j] = x_decode(lp.xl, k0key, a16[j]);
         esc |= valid[j] && xr[j].esc;
       }
       if (__ballot(esc)) {  // (rare) escaped records: address, timestamp and weight from the record
 #pragma unroll
-        for (int j = 0; j < 2; j++)
+        for (int j = 0; j < kLC; j++)
           if (valid[j] && xr[j].esc) x_resolve(xr[j], p.data, lp.descs);
         vm_drain();
       }
 #pragma unroll
-      for (int j = 0; j < 2; j++) {
+      for (int j = 0; j < kLC; j++) {
         addr[j] = xr[j].addr;
         ts[j] = xr[j].ts;
         w[j] = valid[j] ? xr[j].w : 0ull;
@@ -1677,10 +1689,10 @@ __global__ __launch_bounds__(kWG, 1) void local_kernel(LocalParams lp) {
       // first key (partition 0 only) there is no node.  The directory slot
       // gives the largest key <= the slot start and the keys inside the slot
       // (usually 0 or 1; a binary search among them otherwise).
-      int32_t r[2];
-      uint32_t sa[2], sn[2];
+      int32_t r[kLC];
+      uint32_t sa[kLC], sn[kLC];
 #pragma unroll
-      for (int j = 0; j < 2; j++) {
+      for (int j = 0; j < kLC; j++) {
         r[j] = -1;
         sa[j] = sn[j] = 0;
         if (valid[j] && addr[j] >= k0key) {
@@ -1691,7 +1703,7 @@ __global__ __launch_bounds__(kWG, 1) void local_kernel(LocalParams lp) {
         }
       }
 #pragma unroll
-      for (int j = 0; j < 2; j++) {
+      for (int j = 0; j < kLC; j++) {
         uint32_t a = sa[j], n = sn[j];
         while (n) {
           const uint32_t half = (n + 1) >> 1;
@@ -1704,14 +1716,19 @@ __global__ __launch_bounds__(kWG, 1) void local_kernel(LocalParams lp) {
         }
         if (r[j] >= 0) r[j] = (int32_t)a;
       }
-      if (TIMING) (void)__builtin_amdgcn_readfirstlane(__ballot(r[0] >= 0 || r[1] >= 0));  // (the search ends here)
-      rt_stamp<TIMING>(rt, 2);
-      int32_t erel[2];
-      uint64_t baddr[2];
-      uint32_t hrel[2];
-      bool older[2];
+      if (TIMING) {  // (the search ends here)
+        bool any = false;
 #pragma unroll
-      for (int j = 0; j < 2; j++) {
+        for (int j = 0; j < kLC; j++) any |= r[j] >= 0;
+        (void)__builtin_amdgcn_readfirstlane(__ballot(any));
+      }
+      rt_stamp<TIMING>(rt, 2);
+      int32_t erel[kLC];
+      uint64_t baddr[kLC];
+      uint32_t hrel[kLC];
+      bool older[kLC];
+#pragma unroll
+      for (int j = 0; j < kLC; j++) {
         erel[j] = -1;
         baddr[j] = 0;
         hrel[j] = kEmpty32;
@@ -1728,9 +1745,12 @@ __global__ __launch_bounds__(kWG, 1) void local_kernel(LocalParams lp) {
           }
         }
       }
-      if (__ballot(older[0] || older[1])) {  // (rare) older entries of a reused address (LIFO, tools/hash.c:108-114)
+      bool anyold = false;
 #pragma unroll
-        for (int j = 0; j < 2; j++) {
+      for (int j = 0; j < kLC; j++) anyold |= older[j];
+      if (__ballot(anyold)) {  // (rare) older entries of a reused address (LIFO, tools/hash.c:108-114)
+#pragma unroll
+        for (int j = 0; j < kLC; j++) {
           if (!older[j]) continue;
           const uint4 d = reinterpret_cast<const uint4*>(p.nodes + pi.k0 + (uint32_t)r[j])[3];  // (count, first)
           Match m;
@@ -1747,7 +1767,7 @@ __global__ __launch_bounds__(kWG, 1) void local_kernel(LocalParams lp) {
       // the chunks' match bits (per-buffer counts, found_kernel) straight to
       // global memory, and this wave's matched total
 #pragma unroll
-      for (int j = 0; j < 2; j++) {
+      for (int j = 0; j < kLC; j++) {
         const uint64_t fm = __ballot(erel[j] >= 0);
         nfound += (uint32_t)__popcll(fm);
         if (lane == 0 && li[j] < nl) lp.cmatch[s_clist[li[j]] & ((1u << kChunkIdBits) - 1)] = fm;
@@ -1755,13 +1775,15 @@ __global__ __launch_bounds__(kWG, 1) void local_kernel(LocalParams lp) {
       rt_stamp<TIMING>(rt, 3);
       const bool noobj = (p.flags & kDbgLocalNoObj) != 0;
 #pragma unroll
-      for (int j = 0; j < 2; j++)
+      for (int j = 0; j < kLC; j++)
         if (erel[j] >= 0 && !noobj && w[j] < kLaneMaxWeight)
           atomicAdd(&s_owt[xr[j].acc][erel[j]], (1ull << kPackShift) | w[j]);
-      if (__ballot((erel[0] >= 0 && w[0] >= kLaneMaxWeight) || (erel[1] >= 0 && w[1] >= kLaneMaxWeight)) &&
-          !noobj) {  // (rare) large weights
+      bool anybig = false;
 #pragma unroll
-        for (int j = 0; j < 2; j++) {
+      for (int j = 0; j < kLC; j++) anybig |= erel[j] >= 0 && w[j] >= kLaneMaxWeight;
+      if (__ballot(anybig) && !noobj) {  // (rare) large weights
+#pragma unroll
+        for (int j = 0; j < kLC; j++) {
           if (erel[j] < 0 || w[j] < kLaneMaxWeight) continue;
           const uint64_t e = pi.e0 + (uint32_t)erel[j];
           atomicAdd(reinterpret_cast<unsigned long long*>(p.sum64 + objcw_index(e, xr[j].acc, 0, p.nb_entries)), 1ull);
@@ -1771,24 +1793,24 @@ __global__ __launch_bounds__(kWG, 1) void local_kernel(LocalParams lp) {
         vm_drain();
       }
       // first match in analysis order (quirk Q7)
-      if (!noobj) {
-        unsigned long long ord[2], cur[2];
+      if (!noobj) {  // (read first: an unconditional LDS min per match was 9 % slower, hot entries)
+        unsigned long long ord[kLC], cur[kLC];
 #pragma unroll
-        for (int j = 0; j < 2; j++) {
+        for (int j = 0; j < kLC; j++) {
           ord[j] = ((lp.seq0 + xr[j].g) << 32) | xr[j].off;
           cur[j] = erel[j] >= 0 ? s_first[erel[j]] : 0ull;
         }
 #pragma unroll
-        for (int j = 0; j < 2; j++)
+        for (int j = 0; j < kLC; j++)
           if (erel[j] >= 0 && ord[j] < cur[j]) atomicMin(&s_first[erel[j]], ord[j]);
       }
       rt_stamp<TIMING>(rt, 4);
       if (pages && !(p.flags & kDbgLocalNoPage)) {
         // ma_get_block: page_no = (int)((addr - buffer_addr) / 4096) (mem_analyzer.c:530-531)
-        uint32_t page[2];
+        uint32_t page[kLC];
         bool glob = false;
 #pragma unroll
-        for (int j = 0; j < 2; j++) {
+        for (int j = 0; j < kLC; j++) {
           page[j] = uint32_t(int(uint64_t(addr[j] - baddr[j]) / kPageSize));
           if (erel[j] >= 0 && hrel[j] != kEmpty32 && ncell) {
             const uint32_t c = xr[j].th * pi.span + hrel[j] + page[j];
@@ -1798,7 +1820,7 @@ __global__ __launch_bounds__(kWG, 1) void local_kernel(LocalParams lp) {
         }
         if (__ballot(glob)) {  // (rare) cells in global memory: dense or sparse
 #pragma unroll
-          for (int j = 0; j < 2; j++) {
+          for (int j = 0; j < kLC; j++) {
             if (erel[j] < 0) continue;
             if (hrel[j] != kEmpty32 && !ncell) {
               atomicAdd(p.hist + uint64_t(xr[j].th) * p.hist_cells + pi.cb + hrel[j] + page[j], 1u);
@@ -1812,26 +1834,26 @@ __global__ __launch_bounds__(kWG, 1) void local_kernel(LocalParams lp) {
       }
       rt_stamp<TIMING>(rt, 5);
     };
-    uint4 A[2], B[2];
+    uint4 A[kLC], B[kLC];
     auto grab = [&]() -> uint32_t {
       uint32_t t = 0;
-      if (lane == 0) t = atomicAdd(&s_cnext, 2u);
+      if (lane == 0) t = atomicAdd(&s_cnext, (uint32_t)kLC);
       return __builtin_amdgcn_readfirstlane(t);
     };
     uint32_t la = grab(), lb = grab();
-    chunk_load(la, A[0]);
-    chunk_load(la + 1, A[1]);
-    chunk_load(lb, B[0]);
-    chunk_load(lb + 1, B[1]);
+#pragma unroll
+    for (int j = 0; j < kLC; j++) chunk_load(la + j, A[j]);
+#pragma unroll
+    for (int j = 0; j < kLC; j++) chunk_load(lb + j, B[j]);
     while (la < nl) {
-      process2(la, la + 1, A);
+      process(la, A);
       la = grab();
-      chunk_load(la, A[0]);
-      chunk_load(la + 1, A[1]);
-      if (lb < nl) process2(lb, lb + 1, B);
+#pragma unroll
+      for (int j = 0; j < kLC; j++) chunk_load(la + j, A[j]);
+      if (lb < nl) process(lb, B);
       lb = grab();
-      chunk_load(lb, B[0]);
-      chunk_load(lb + 1, B[1]);
+#pragma unroll
+      for (int j = 0; j < kLC; j++) chunk_load(lb + j, B[j]);
     }
     lds_sync();
     rt_stamp<TIMING>(rt, 9);  // (waiting for the item's slowest wave)
@@ -1840,7 +1862,7 @@ __global__ __launch_bounds__(kWG, 1) void local_kernel(LocalParams lp) {
     // item of its partition adds with plain loads and stores (no other
     // workgroup writes these words during the launch), the others with
     // atomics
-    for (uint32_t i = tid; i < pi.ne; i += kWG) {
+    for (uint32_t i = tid; i < pi.ne; i += kLWG) {
       const uint64_t e = pi.e0 + i;
 #pragma unroll
       for (uint32_t a = 0; a < 2; a++) {
@@ -1873,12 +1895,12 @@ __global__ __launch_bounds__(kWG, 1) void local_kernel(LocalParams lp) {
       const uint32_t nw = (ncell + 1) / 2, span = pi.span;
       const uint32_t smag = span ? 0xffffffffu / span + 1u : 0u;
       constexpr uint32_t kU = 4;
-      for (uint32_t j0 = tid; j0 < nw; j0 += kU * kWG) {
+      for (uint32_t j0 = tid; j0 < nw; j0 += kU * kLWG) {
         uint32_t cnt[kU][2], old[kU][2];
         uint32_t* pc[kU][2];
 #pragma unroll
         for (uint32_t u = 0; u < kU; u++) {
-          const uint32_t j = j0 + u * kWG;
+          const uint32_t j = j0 + u * kLWG;
           const uint32_t v = j < nw ? s_pg[j] : 0u;
           if (v) s_pg[j] = 0;
 #pragma unroll
@@ -1986,8 +2008,8 @@ hipError_t launch_scatter(uint32_t grid, hipStream_t s, const ScatterParams& r) 
 }
 
 hipError_t launch_local(uint32_t grid, hipStream_t s, const LocalParams& r) {
-  if (r.p.flags & kDbgLocalTiming) hipLaunchKernelGGL(local_kernel<true>, dim3(grid), dim3(kWG), 0, s, r);
-  else hipLaunchKernelGGL(local_kernel<false>, dim3(grid), dim3(kWG), 0, s, r);
+  if (r.p.flags & kDbgLocalTiming) hipLaunchKernelGGL(local_kernel<true>, dim3(grid), dim3(kLWG), 0, s, r);
+  else hipLaunchKernelGGL(local_kernel<false>, dim3(grid), dim3(kLWG), 0, s, r);
   return hipGetLastError();
 }
 
