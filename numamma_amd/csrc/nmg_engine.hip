@@ -2877,7 +2877,7 @@ extern "C" int nmg_import_array(nmg_engine* h, int which, const void* d_src) {
 }
 
 static int scratch_u64(nmg_engine* h) {
-  if (!h->d_scratch) HIP_TRY(h, hipMalloc(&h->d_scratch, 2 * 8));
+  if (!h->d_scratch) HIP_TRY(h, hipMalloc(&h->d_scratch, 2 * 8 + 1024 * 4));  // + nmg_hist_pack's range counts
   return NMG_OK;
 }
 
@@ -2895,7 +2895,8 @@ extern "C" int nmg_hist_pack(nmg_engine* h, uint32_t threshold, void* d_u8, void
   HIP_TRY(h, hipSetDevice(h->device));
   HIP_TRY(h, hipMemsetAsync(h->d_scratch, 0, 8, h->stream));
   HIP_TRY(h, launch_hist_pack(h->stream, h->d_hist, cells, threshold, d_u8, d_ovf, ovf_cap,
-                              reinterpret_cast<unsigned long long*>(h->d_scratch)));
+                              reinterpret_cast<unsigned long long*>(h->d_scratch),
+                              reinterpret_cast<uint32_t*>(h->d_scratch + 2)));
   HIP_TRY(h, hipMemcpyAsync(n_ovf, h->d_scratch, 8, hipMemcpyDeviceToHost, h->stream));
   HIP_TRY(h, hipStreamSynchronize(h->stream));
   return NMG_OK;

@@ -207,7 +207,7 @@ hipError_t launch_reset(uint32_t grid, hipStream_t s, const ResetParams& r);
 hipError_t launch_merge(hipStream_t s, void* dst, const void* src, uint64_t n, int op);
 // packed page histogram (nmg_hist_pack / nmg_hist_unpack); ncells a multiple of 4
 hipError_t launch_hist_pack(hipStream_t s, const uint32_t* hist, uint64_t ncells, uint32_t thr, void* u8, void* ovf,
-                            uint64_t cap, unsigned long long* cnt);
+                            uint64_t cap, unsigned long long* cnt, uint32_t* wgcnt);  // wgcnt: [1024] workspace
 hipError_t launch_hist_unpack(hipStream_t s, uint32_t* hist, uint64_t ncells, const void* u8, const void* ovf,
                               uint64_t n, unsigned long long* bad);
 // page-cell rows on the device (nmg_get_page_cells / nmg_report): per dense

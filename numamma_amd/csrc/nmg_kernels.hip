@@ -999,53 +999,113 @@ __global__ __launch_bounds__(256) void merge_kernel(void* dst, const void* src, 
 
 // Packed page histogram for the multi-GPU merge (nmg_hist_pack): cells of at
 // most `thr` as bytes (4 per thread, one 16 B load), larger ones to the
-// overflow list as (cell << 32 | count), compacted per wave (one counter add).
-__global__ __launch_bounds__(256) void hist_pack_kernel(const uint4* hist, uint64_t n4, uint32_t thr, uint32_t* u8x4,
-                                                        unsigned long long* ovf, uint64_t cap,
-                                                        unsigned long long* cnt) {
-  const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
-  const int lane = threadIdx.x & 63;
-  for (uint64_t base = uint64_t(blockIdx.x) * blockDim.x; base < n4; base += stride) {
-    const uint64_t i = base + threadIdx.x;
-    const uint4 v = i < n4 ? hist[i] : make_uint4(0, 0, 0, 0);
+// overflow list as (cell << 32 | count), in cell order.  Two passes over
+// contiguous per-workgroup ranges, no shared counter: hist_count_kernel
+// counts each range's large cells, hist_pack_kernel takes its range's offset
+// as the sum of the earlier ranges' counts (one reservation per wave on a
+// shared word had serialised ~10^5 atomics: 0.8 ms at the c4 shard).
+constexpr uint32_t kPackGrid = 1024, kPackWG = 256;
+
+__device__ __forceinline__ uint32_t big_cells(uint4 v, uint32_t thr) {
+  return (v.x > thr) + (v.y > thr) + (v.z > thr) + (v.w > thr);
+}
+// cells 4i .. 4i + 3 (those past ncells read as 0; the last, partial quad by
+// single loads)
+__device__ __forceinline__ uint4 load_quad(const uint32_t* hist, uint64_t i, uint64_t ncells) {
+  if (4 * i + 3 < ncells) return reinterpret_cast<const uint4*>(hist)[i];
+  uint32_t c[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++) c[k] = 4 * i + k < ncells ? hist[4 * i + k] : 0u;
+  return make_uint4(c[0], c[1], c[2], c[3]);
+}
+
+__global__ __launch_bounds__(kPackWG) void hist_count_kernel(const uint32_t* hist, uint64_t ncells, uint32_t thr,
+                                                             uint32_t* wgcnt) {
+  const uint64_t n4 = (ncells + 3) / 4;
+  __shared__ uint32_t s_sum[kPackWG / 64];
+  const uint64_t per = (n4 + kPackGrid - 1) / kPackGrid, i0 = uint64_t(blockIdx.x) * per;
+  const uint64_t i1 = min(i0 + per, n4);
+  uint32_t nbig = 0;
+  for (uint64_t i = i0 + threadIdx.x; i < i1; i += kPackWG) nbig += big_cells(load_quad(hist, i, ncells), thr);
+  nbig = wave_sum_u32(nbig);
+  if ((threadIdx.x & 63) == 0) s_sum[threadIdx.x >> 6] = nbig;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t t = 0;
+    for (uint32_t w = 0; w < kPackWG / 64; w++) t += s_sum[w];
+    wgcnt[blockIdx.x] = t;
+  }
+}
+
+__global__ __launch_bounds__(kPackWG) void hist_pack_kernel(const uint32_t* hist, uint64_t ncells, uint32_t thr,
+                                                            uint8_t* u8, unsigned long long* ovf, uint64_t cap,
+                                                            const uint32_t* wgcnt, unsigned long long* cnt) {
+  const uint64_t n4 = (ncells + 3) / 4;
+  __shared__ uint32_t s_w[kPackWG / 64];
+  __shared__ unsigned long long s_base;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const uint64_t per = (n4 + kPackGrid - 1) / kPackGrid, i0 = uint64_t(blockIdx.x) * per;
+  const uint64_t i1 = min(i0 + per, n4);
+  // this range's first overflow slot: the earlier ranges' counts
+  uint32_t pre = 0;
+  for (uint32_t w = tid; w < blockIdx.x; w += kPackWG) pre += wgcnt[w];
+  pre = wave_sum_u32(pre);
+  if (lane == 0) s_w[wave] = pre;
+  __syncthreads();
+  if (tid == 0) {
+    unsigned long long t = 0;
+    for (uint32_t w = 0; w < kPackWG / 64; w++) t += s_w[w];
+    s_base = t;
+    if (blockIdx.x == gridDim.x - 1) *cnt = t + wgcnt[blockIdx.x];  // (the list's length)
+  }
+  __syncthreads();
+  unsigned long long base = s_base;
+  for (uint64_t j = i0; j < i1; j += kPackWG) {  // (uniform trip count: the scans below are workgroup-wide)
+    const uint64_t i = j + tid;
+    const uint4 v = i < i1 ? load_quad(hist, i, ncells) : make_uint4(0, 0, 0, 0);
     const uint32_t c[4] = {v.x, v.y, v.z, v.w};
-    uint32_t packed = 0, nbig = 0;
+    uint32_t packed = 0;
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
-      const bool small = c[k] <= thr;
-      packed |= (small ? c[k] : 0u) << (8 * k);
-      nbig += small ? 0u : 1u;
+    for (int k = 0; k < 4; k++) packed |= (c[k] <= thr ? c[k] : 0u) << (8 * k);
+    if (i < i1) {
+      if (4 * i + 3 < ncells) {
+        reinterpret_cast<uint32_t*>(u8)[i] = packed;
+      } else {  // (the partial last quad: the byte buffer holds ncells bytes)
+        for (uint32_t k = 0; 4 * i + k < ncells; k++) u8[4 * i + k] = uint8_t(packed >> (8 * k));
+      }
     }
-    if (i < n4) u8x4[i] = packed;
-    const uint64_t any = __ballot(nbig != 0);
-    if (!any) continue;
-    // this wave's overflow entries: an exclusive scan of nbig, one counter add
-    uint32_t pre = nbig;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t t = __shfl_up(pre, o, 64);
-      if (lane >= o) pre += t;
+    const uint32_t nbig = i < i1 ? big_cells(v, thr) : 0u;
+    // workgroup-wide exclusive scan of nbig (cell order)
+    const uint32_t inc = wave_incl_scan_u32(nbig);
+    __syncthreads();  // (s_w of the previous iteration read by every wave)
+    if (lane == 63) s_w[wave] = inc;
+    __syncthreads();
+    uint32_t wpre = 0, tot = 0;
+    for (int w = 0; w < kPackWG / 64; w++) {
+      wpre += w < wave ? s_w[w] : 0u;
+      tot += s_w[w];
     }
-    const uint32_t tot = __shfl(pre, 63, 64);
-    unsigned long long at = 0;
-    if (lane == 0) at = atomicAdd(cnt, (unsigned long long)tot);
-    at = __shfl(at, 0, 64);
-    uint64_t slot = at + pre - nbig;
+    uint64_t slot = base + wpre + inc - nbig;
 #pragma unroll
     for (int k = 0; k < 4; k++) {
       if (c[k] <= thr) continue;
       if (slot < cap) ovf[slot] = ((unsigned long long)(4 * i + k) << 32) | c[k];
       slot++;
     }
+    base += tot;
   }
 }
 
 // nmg_hist_unpack: hist = summed bytes, then += every overflow entry
-__global__ __launch_bounds__(256) void hist_unpack_kernel(uint4* hist, uint64_t n4, const uint32_t* u8x4) {
-  const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
+__global__ __launch_bounds__(256) void hist_unpack_kernel(uint32_t* hist, uint64_t ncells, const uint8_t* u8) {
+  const uint64_t stride = uint64_t(gridDim.x) * blockDim.x, n4 = (ncells + 3) / 4;
   for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n4; i += stride) {
-    const uint32_t p = u8x4[i];
-    hist[i] = make_uint4(p & 0xffu, (p >> 8) & 0xffu, (p >> 16) & 0xffu, p >> 24);
+    if (4 * i + 3 < ncells) {
+      const uint32_t p = reinterpret_cast<const uint32_t*>(u8)[i];
+      reinterpret_cast<uint4*>(hist)[i] = make_uint4(p & 0xffu, (p >> 8) & 0xffu, (p >> 16) & 0xffu, p >> 24);
+    } else {
+      for (uint64_t c = 4 * i; c < ncells; c++) hist[c] = u8[c];
+    }
   }
 }
 
@@ -1161,22 +1221,21 @@ hipError_t launch_unpack(uint32_t grid, hipStream_t s, uint64_t* sum64, unsigned
 }
 
 hipError_t launch_hist_pack(hipStream_t s, const uint32_t* hist, uint64_t ncells, uint32_t thr, void* u8,
-                            void* ovf, uint64_t cap, unsigned long long* cnt) {
-  const uint64_t n4 = ncells / 4;
-  if (!n4) return hipSuccess;
-  const uint32_t grid = (uint32_t)std::min<uint64_t>((n4 + 255) / 256, 4096);
-  hipLaunchKernelGGL(hist_pack_kernel, dim3(grid), dim3(256), 0, s, reinterpret_cast<const uint4*>(hist), n4, thr,
-                     reinterpret_cast<uint32_t*>(u8), reinterpret_cast<unsigned long long*>(ovf), cap, cnt);
+                            void* ovf, uint64_t cap, unsigned long long* cnt, uint32_t* wgcnt) {
+  if (!ncells) return hipSuccess;
+  hipLaunchKernelGGL(hist_count_kernel, dim3(kPackGrid), dim3(kPackWG), 0, s, hist, ncells, thr, wgcnt);
+  hipLaunchKernelGGL(hist_pack_kernel, dim3(kPackGrid), dim3(kPackWG), 0, s, hist, ncells, thr,
+                     reinterpret_cast<uint8_t*>(u8), reinterpret_cast<unsigned long long*>(ovf), cap, wgcnt, cnt);
   return hipGetLastError();
 }
 
 hipError_t launch_hist_unpack(hipStream_t s, uint32_t* hist, uint64_t ncells, const void* u8, const void* ovf,
                               uint64_t n, unsigned long long* bad) {
-  const uint64_t n4 = ncells / 4;
+  const uint64_t n4 = (ncells + 3) / 4;
   if (n4) {
     const uint32_t grid = (uint32_t)std::min<uint64_t>((n4 + 255) / 256, 4096);
-    hipLaunchKernelGGL(hist_unpack_kernel, dim3(grid), dim3(256), 0, s, reinterpret_cast<uint4*>(hist), n4,
-                       reinterpret_cast<const uint32_t*>(u8));
+    hipLaunchKernelGGL(hist_unpack_kernel, dim3(grid), dim3(256), 0, s, hist, ncells,
+                       reinterpret_cast<const uint8_t*>(u8));
   }
   if (n) {
     const uint32_t grid = (uint32_t)std::min<uint64_t>((n + 255) / 256, 4096);

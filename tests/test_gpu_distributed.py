@@ -116,11 +116,12 @@ def test_two_rank_engine_merge_matches_oracle(cfg_name, packed):
                 open(os.path.join(d, "engine", f), "rb").read(), f
 
 
-@pytest.mark.parametrize("threshold", [0, 1, 31, 127, 255])
-def test_hist_pack_round_trip(threshold):
+@pytest.mark.parametrize("threshold,threads", [(0, 8), (1, 8), (31, 8), (127, 8), (255, 8), (1, 3), (31, 7)])
+def test_hist_pack_round_trip(threshold, threads):
     """nmg_hist_pack then nmg_hist_unpack on one engine gives back every
-    page cell (bytes <= threshold + overflow list); a list longer than its
-    capacity reports its full length."""
+    page cell (bytes <= threshold + overflow list, in cell order); a list
+    longer than its capacity reports its full length.  Odd thread counts give
+    cell counts that are not a multiple of 4 (the partial last quad)."""
     import torch
 
     sys.path[:0] = [ROOT, os.path.join(ROOT, "oracle")]
@@ -128,7 +129,7 @@ def test_hist_pack_round_trip(threshold):
     from numamma_amd.engine import Engine
     from numamma_amd.replay import SynthConfig, generate
 
-    rp = generate(SynthConfig(nb_samples=400_000, nb_intervals=20_000, seed=23))
+    rp = generate(SynthConfig(nb_samples=400_000, nb_intervals=20_000, nb_threads=threads, seed=23))
     eng = Engine(device=0, nb_threads=rp.nb_threads)
     eng.set_objects(rp.table)
     eng.submit_replay(rp)
@@ -145,6 +146,9 @@ def test_hist_pack_round_trip(threshold):
     assert n == int((ref > threshold).sum())
     b = u8.cpu().numpy()
     assert np.array_equal(b, np.where(ref <= threshold, ref, 0).astype(np.uint8))
+    big = np.nonzero(ref > threshold)[0].astype(np.uint64)
+    want = (big << np.uint64(32)) | ref[big].astype(np.uint64)
+    assert np.array_equal(ovf[:n].cpu().numpy().view(np.uint64), want)
     if n > 1:
         assert eng.hist_pack(threshold, u8.data_ptr(), ovf.data_ptr(), n - 1) == n  # (capacity short)
         eng.hist_pack(threshold, u8.data_ptr(), ovf.data_ptr(), cells)
