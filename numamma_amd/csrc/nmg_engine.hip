@@ -165,6 +165,7 @@ struct nmg_engine {
   uint64_t* d_scratch = nullptr;          // [2] small device results (nmg_hist_pack / unpack)
   uint64_t* d_sparse_keys = nullptr;
   uint32_t* d_sparse_vals = nullptr;
+  uint64_t* d_sparse_ck = nullptr;  // [sparse_cap + 1] compacted (key, count) words + the count (sparse_download)
   uint32_t* d_sparse_dirty = nullptr;  // [2] parity flags (see reset_kernel)
   uint32_t* d_smatch = nullptr;        // NMG_F_SAMPLE_MATCHES: per 8 B of the arena span
   unsigned long long* d_pk64 = nullptr;  // hashed object mode: packed long-tail counters (0 between launches)
@@ -340,6 +341,8 @@ static void free_counters(nmg_engine* h) {
   h->d_hist = nullptr;
   h->d_sparse_keys = nullptr;
   h->d_sparse_vals = nullptr;
+  (void)hipFree(h->d_sparse_ck);
+  h->d_sparse_ck = nullptr;
   (void)hipFree(h->d_sparse_dirty);
   h->d_sparse_dirty = nullptr;
   (void)hipFree(h->d_pk64);
@@ -2691,6 +2694,7 @@ extern "C" int nmg_get_object_levels(nmg_engine* h, uint64_t* levels) {
 }
 
 static int sparse_nonempty(nmg_engine* h, bool* out);
+static int sparse_download(nmg_engine* h, std::vector<uint64_t>& k, std::vector<uint32_t>& v);
 
 // Every non-zero (entry, thread, page) cell, entries in id order, each
 // entry's cells in (thread, page) order.  Dense cells are counted and
@@ -2711,10 +2715,10 @@ static int cells_prepare(nmg_engine* h) {
   rc = sparse_nonempty(h, &any_sparse);
   if (rc) return rc;
   if (any_sparse) {
-    std::vector<uint64_t> k(h->sparse_cap);
-    std::vector<uint32_t> v(h->sparse_cap);
-    HIP_TRY(h, hipMemcpy(k.data(), h->d_sparse_keys, h->sparse_cap * 8, hipMemcpyDeviceToHost));
-    HIP_TRY(h, hipMemcpy(v.data(), h->d_sparse_vals, h->sparse_cap * 4, hipMemcpyDeviceToHost));
+    std::vector<uint64_t> k;
+    std::vector<uint32_t> v;
+    rc = sparse_download(h, k, v);
+    if (rc) return rc;
     for (size_t i = 0; i < k.size(); i++)
       if (k[i] != ~0ull && v[i]) {
         uint32_t s = sparse_key_idx(k[i]);
@@ -2946,17 +2950,24 @@ static int sparse_download(nmg_engine* h, std::vector<uint64_t>& k, std::vector<
     v.clear();
     return NMG_OK;
   }
-  std::vector<uint64_t> kk(h->sparse_cap);
-  std::vector<uint32_t> vv(h->sparse_cap);
-  HIP_TRY(h, hipMemcpy(kk.data(), h->d_sparse_keys, h->sparse_cap * 8, hipMemcpyDeviceToHost));
-  HIP_TRY(h, hipMemcpy(vv.data(), h->d_sparse_vals, h->sparse_cap * 4, hipMemcpyDeviceToHost));
-  k.clear();
-  v.clear();
-  for (size_t i = 0; i < kk.size(); i++)
-    if (kk[i] != ~0ull && vv[i]) {
-      k.push_back(kk[i]);
-      v.push_back(vv[i]);
-    }
+  // the used slots compacted on the device (key, count pairs), so only they
+  // cross PCIe (the whole table is 12 MB at the default capacity)
+  HIP_TRY(h, hipSetDevice(h->device));
+  if (!h->d_sparse_ck) HIP_TRY(h, hipMalloc(&h->d_sparse_ck, (h->sparse_cap * 2 + 1) * 8));
+  unsigned long long* cnt = reinterpret_cast<unsigned long long*>(h->d_sparse_ck + 2 * h->sparse_cap);
+  HIP_TRY(h, hipMemsetAsync(cnt, 0, 8, h->stream));
+  HIP_TRY(h, launch_sparse_compact(h->stream, h->d_sparse_keys, h->d_sparse_vals, h->sparse_cap, h->d_sparse_ck, cnt));
+  uint64_t n = 0;
+  HIP_TRY(h, hipMemcpyAsync(&n, cnt, 8, hipMemcpyDeviceToHost, h->stream));
+  HIP_TRY(h, hipStreamSynchronize(h->stream));
+  std::vector<uint64_t> kv(2 * n);
+  if (n) HIP_TRY(h, hipMemcpy(kv.data(), h->d_sparse_ck, 2 * n * 8, hipMemcpyDeviceToHost));
+  k.resize(n);
+  v.resize(n);
+  for (uint64_t i = 0; i < n; i++) {
+    k[i] = kv[2 * i];
+    v[i] = (uint32_t)kv[2 * i + 1];
+  }
   return NMG_OK;
 }
 
@@ -2986,18 +2997,25 @@ extern "C" int nmg_sparse_import(nmg_engine* h, const uint64_t* keys, const uint
   if (!h || !h->have_table || (n && (!keys || !counts))) return NMG_ERR_INVALID;
   if (!h->d_sparse_keys) return n ? fail(h, NMG_ERR_STATE, "no sparse table") : NMG_OK;
   if ((uint64_t)n > h->sparse_cap) return fail(h, NMG_ERR_CAPACITY, "sparse table too small");
-  std::vector<uint64_t> k(h->sparse_cap, ~0ull);
-  std::vector<uint32_t> v(h->sparse_cap, 0);
-  for (int64_t i = 0; i < n; i++) {
-    uint64_t hh = (keys[i] * 0x9E3779B97F4A7C15ull) >> 20;
-    uint64_t slot = hh & (h->sparse_cap - 1);
-    while (k[slot] != ~0ull && k[slot] != keys[i]) slot = (slot + 1) & (h->sparse_cap - 1);
-    k[slot] = keys[i];
-    v[slot] += counts[i];
-  }
+  // the table cleared and the pairs inserted on the device (sparse_add's hash
+  // and probing): only the pairs cross PCIe
   HIP_TRY(h, hipSetDevice(h->device));
-  HIP_TRY(h, hipMemcpy(h->d_sparse_keys, k.data(), h->sparse_cap * 8, hipMemcpyHostToDevice));
-  HIP_TRY(h, hipMemcpy(h->d_sparse_vals, v.data(), h->sparse_cap * 4, hipMemcpyHostToDevice));
+  int rc = nmg_synchronize(h);
+  if (rc) return rc;
+  if (!h->d_sparse_ck) HIP_TRY(h, hipMalloc(&h->d_sparse_ck, (h->sparse_cap * 2 + 1) * 8));
+  HIP_TRY(h, hipMemsetAsync(h->d_sparse_keys, 0xff, h->sparse_cap * 8, h->stream));
+  HIP_TRY(h, hipMemsetAsync(h->d_sparse_vals, 0, h->sparse_cap * 4, h->stream));
+  if (n) {
+    std::vector<uint64_t> kv(2 * (size_t)n);
+    for (int64_t i = 0; i < n; i++) {
+      kv[2 * i] = keys[i];
+      kv[2 * i + 1] = counts[i];
+    }
+    HIP_TRY(h, hipMemcpyAsync(h->d_sparse_ck, kv.data(), kv.size() * 8, hipMemcpyHostToDevice, h->stream));
+    HIP_TRY(h, launch_sparse_insert(h->stream, h->d_sparse_keys, h->d_sparse_vals, h->sparse_cap, h->d_sparse_ck,
+                                    (uint64_t)n));
+    HIP_TRY(h, hipStreamSynchronize(h->stream));  // (kv is pageable)
+  }
   const uint32_t one = 1;  // imported cells: the next reset must clear the table
   HIP_TRY(h, hipMemcpy(h->d_sparse_dirty + (h->nreset & 1), &one, 4, hipMemcpyHostToDevice));
   return NMG_OK;

@@ -206,6 +206,11 @@ hipError_t launch_unpack(uint32_t grid, hipStream_t s, uint64_t* sum64, unsigned
 hipError_t launch_reset(uint32_t grid, hipStream_t s, const ResetParams& r);
 hipError_t launch_merge(hipStream_t s, void* dst, const void* src, uint64_t n, int op);
 // packed page histogram (nmg_hist_pack / nmg_hist_unpack); ncells a multiple of 4
+// sparse_download: the used slots of the sparse table as (key, count) u64 pairs, *cnt of them
+hipError_t launch_sparse_compact(hipStream_t s, const uint64_t* keys, const uint32_t* vals, uint64_t cap,
+                                 uint64_t* out, unsigned long long* cnt);
+hipError_t launch_sparse_insert(hipStream_t s, uint64_t* keys, uint32_t* vals, uint64_t cap, const uint64_t* pairs,
+                                uint64_t n);
 hipError_t launch_hist_pack(hipStream_t s, const uint32_t* hist, uint64_t ncells, uint32_t thr, void* u8, void* ovf,
                             uint64_t cap, unsigned long long* cnt, uint32_t* wgcnt);  // wgcnt: [1024] workspace
 hipError_t launch_hist_unpack(hipStream_t s, uint32_t* hist, uint64_t ncells, const void* u8, const void* ovf,

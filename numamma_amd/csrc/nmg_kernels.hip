@@ -1123,6 +1123,51 @@ __global__ __launch_bounds__(256) void hist_ovf_add_kernel(uint32_t* hist, uint6
   }
 }
 
+// The sparse table's used slots as (key, count) pairs (order: any; the host
+// sorts), one counter add per wave that holds one.
+__global__ __launch_bounds__(256) void sparse_compact_kernel(const uint64_t* keys, const uint32_t* vals, uint64_t cap,
+                                                             uint64_t* out, unsigned long long* cnt) {
+  const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
+  const int lane = threadIdx.x & 63;
+  for (uint64_t base = uint64_t(blockIdx.x) * blockDim.x; base < cap; base += stride) {
+    const uint64_t i = base + threadIdx.x;
+    const uint64_t key = i < cap ? keys[i] : ~0ull;
+    const uint32_t v = i < cap ? vals[i] : 0u;
+    const bool used = key != ~0ull && v != 0;
+    const uint64_t m = __ballot(used);
+    if (!m) continue;
+    unsigned long long at = 0;
+    if (lane == 0) at = atomicAdd(cnt, (unsigned long long)__popcll(m));
+    at = __shfl(at, 0, 64);
+    if (used) {
+      const uint64_t slot = at + __popcll(m & ((1ull << lane) - 1));
+      out[2 * slot] = key;
+      out[2 * slot + 1] = v;
+    }
+  }
+}
+
+// nmg_sparse_import: (key, count) pairs into a cleared table, with
+// sparse_add's hash and linear probing (n <= cap: every probe sequence ends)
+__global__ __launch_bounds__(256) void sparse_insert_kernel(uint64_t* keys, uint32_t* vals, uint64_t mask,
+                                                            const uint64_t* pairs, uint64_t n) {
+  const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
+  for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const uint64_t key = pairs[2 * i];
+    const uint32_t cnt = (uint32_t)pairs[2 * i + 1];
+    uint64_t slot = ((key * 0x9E3779B97F4A7C15ull) >> 20) & mask;
+    for (uint64_t probe = 0; probe <= mask; probe++) {
+      const unsigned long long prev =
+          atomicCAS(reinterpret_cast<unsigned long long*>(keys + slot), ~0ull, (unsigned long long)key);
+      if (prev == ~0ull || prev == key) {
+        atomicAdd(vals + slot, cnt);
+        break;
+      }
+      slot = (slot + 1) & mask;
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------
 // launchers
 
@@ -1242,6 +1287,22 @@ hipError_t launch_hist_unpack(hipStream_t s, uint32_t* hist, uint64_t ncells, co
     hipLaunchKernelGGL(hist_ovf_add_kernel, dim3(grid), dim3(256), 0, s, hist, ncells,
                        reinterpret_cast<const unsigned long long*>(ovf), n, bad);
   }
+  return hipGetLastError();
+}
+
+hipError_t launch_sparse_compact(hipStream_t s, const uint64_t* keys, const uint32_t* vals, uint64_t cap,
+                                 uint64_t* out, unsigned long long* cnt) {
+  if (!cap) return hipSuccess;
+  const uint32_t grid = (uint32_t)std::min<uint64_t>((cap + 255) / 256, 2048);
+  hipLaunchKernelGGL(sparse_compact_kernel, dim3(grid), dim3(256), 0, s, keys, vals, cap, out, cnt);
+  return hipGetLastError();
+}
+
+hipError_t launch_sparse_insert(hipStream_t s, uint64_t* keys, uint32_t* vals, uint64_t cap, const uint64_t* pairs,
+                                uint64_t n) {
+  if (!n) return hipSuccess;
+  const uint32_t grid = (uint32_t)std::min<uint64_t>((n + 255) / 256, 2048);
+  hipLaunchKernelGGL(sparse_insert_kernel, dim3(grid), dim3(256), 0, s, keys, vals, cap - 1, pairs, n);
   return hipGetLastError();
 }
 
