@@ -1465,7 +1465,7 @@ __global__ __launch_bounds__(kWG) void plan_kernel(PlanParams r) {
   const uint32_t P = r.nparts;
   for (uint32_t q = tid; q < P; q += kWG) {  // per partition: exclusive prefix over the workgroups
     uint32_t run = 0;
-    constexpr uint32_t kU = 16;  // loads of kU workgroups in flight before their prefixes are stored
+    constexpr uint32_t kU = 32;  // loads of kU workgroups in flight before their prefixes are stored
     for (uint32_t w0 = 0; w0 < r.grid; w0 += kU) {
       uint32_t v[kU];
 #pragma unroll
