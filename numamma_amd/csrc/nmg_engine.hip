@@ -2312,6 +2312,7 @@ static int route_analyze_job(nmg_engine* h, const RouteJob& job) {
   rp.ovfx = h->d_ovfx;
   rp.ovf_cnt = h->d_ctl + 2;
   rp.ovf_cap = (uint32_t)std::min<size_t>(h->ovf_cap, 0xffffffffu);
+  if (h->flags & kDbgTinyOvf) rp.ovf_cap = std::min<uint32_t>(rp.ovf_cap, 64);  // (tests: the direct attribution past a full list)
   if (h->flags & kDbgRouteTiming) {  // (internal) per-wave phase cycles, read by nmg_debug_timing
     const size_t n = (size_t)grid * (kWG / 64) * kRouteTimingWords;
     if (n > h->dbg_cap) {

@@ -70,6 +70,8 @@ constexpr uint32_t kDbgNoRoute = 0x10000;  // large tables: the single-pass attr
 constexpr uint32_t kDbgTinyPool = 0x20000; // route pass: private pools of 2 chunks, so the pool-overflow
                                            // (direct attribution) path runs
 // ablation switches (tools/ablate.py; results are wrong with them)
+constexpr uint32_t kDbgTinyOvf = 0x80000;  // route pass: an overflow list of 64 records, the rest attributed directly
+                                           // (tests, with kDbgTinyPool)
 constexpr uint32_t kDbgRouteNoWrite = 0x100000;  // route pass: batches sorted in LDS, no chunk stores
 constexpr uint32_t kDbgRouteNoBatch = 0x200000;  // route pass: no batch sort or stores at all
 constexpr uint32_t kDbgLocalNoWork = 0x400000;   // local pass: chunk loads only

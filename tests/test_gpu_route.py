@@ -28,6 +28,7 @@ pytestmark = pytest.mark.gpu
 
 NO_ROUTE = 0x10000
 TINY_POOL = 0x20000
+TINY_OVF = 0x80000  # (internal, with TINY_POOL) an overflow list of 64 records: the rest attributed in the route pass
 ROUTE_V1 = 0x20000000  # (internal) route_kernel instead of the default route2_kernel
 
 
@@ -80,8 +81,9 @@ ROUTE_CASES = [
 
 
 @pytest.mark.parametrize("cfg", ROUTE_CASES, ids=[f"case{i}" for i in range(len(ROUTE_CASES))])
-@pytest.mark.parametrize("flags", [0, TINY_POOL, _lib.NMG_F_SINGLE_PASS, ROUTE_V1, ROUTE_V1 | TINY_POOL],
-                         ids=["route", "tinypool", "single", "v2", "v2tiny"])
+@pytest.mark.parametrize("flags", [0, TINY_POOL, TINY_POOL | TINY_OVF, _lib.NMG_F_SINGLE_PASS, ROUTE_V1,
+                                   ROUTE_V1 | TINY_POOL, ROUTE_V1 | TINY_POOL | TINY_OVF],
+                         ids=["route", "tinypool", "tinyovf", "single", "v1", "v1tiny", "v1tinyovf"])
 def test_route_bit_exact(tmp_path, cfg, flags):
     d = str(tmp_path)
     path, odir = _oracle(generate(cfg), d)
