@@ -308,8 +308,9 @@ def main_one_process(args):
         "data": "synthetic (seeded SURVEY 8(d) generator); one per-GPU shard, analysed by every GPU",
         "config": {"workload": f"{args.workload}: {wl['desc']}", "records_per_gpu": shard,
                    "object_intervals": int(cfg.nb_intervals), "threads": rp.nb_threads,
-                   "parallelism": f"one process, nmg_options.nb_gpus={n}: buffers sharded over {n} GPUs, "
-                                  "RCCL reduce of the counters"},
+                   "parallelism": (f"one process, nmg_options.nb_gpus={n}: buffers sharded over {n} GPUs, "
+                                   "RCCL reduce of the counters" if n > 1 else
+                                   "one process, one engine handle over host-staged buffers (the --gpus N path at N=1)")},
     }
     # per GPU: its shard's 40 B records over the whole step (analysis, the
     # RCCL reduce of the counters into GPU 0's handle, the handle's gathers)
