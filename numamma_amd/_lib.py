@@ -194,6 +194,7 @@ _SIGS = {
     "nmg_get_launch_times": (C.c_int, [H, C.POINTER(C.c_float), C.c_int]),
     "nmg_get_kernel_times": (C.c_int, [H, C.POINTER(C.c_float), C.POINTER(C.c_float), C.c_int]),
     "nmg_debug_phase_times": (C.c_int, [H, C.POINTER(C.c_float), C.POINTER(C.c_float), C.c_int]),
+    "nmg_debug_route_count": (C.c_int, [H, u64p]),
     "nmg_report": (C.c_int, [H, C.POINTER(nmg_object_meta), C.POINTER(nmg_report_options), C.c_char_p]),
     "nmg_report_host": (C.c_int, [C.POINTER(nmg_host_results), C.POINTER(nmg_object_meta), C.POINTER(nmg_report_options), C.c_char_p]),
     "nmg_run_replay": (C.c_int, [C.c_char_p, C.c_char_p, C.c_char_p, C.c_char_p, C.c_int, C.c_uint32]),

@@ -241,7 +241,8 @@ struct nmg_engine {
 
   // partition-first path for large tables (nmg_route.h): the partitions of
   // the current table, and the per-analysis chunk pool
-  bool route_ok = false;          // partitions built for the nmg_set_objects table
+  bool route_ok = false;          // partitions built for the current table
+  uint64_t route_launches = 0;    // analyses (or streamed chunks) that took the partition-first path
   uint32_t nparts = 0;
   PartInfo* d_parts = nullptr;
   uint64_t* d_pbounds = nullptr;  // [kMaxParts + 1] partition starts, ascending
@@ -253,6 +254,7 @@ struct nmg_engine {
   uint4* d_pe_nodes = nullptr;    // [nparts][kPartSlots][2]
   uint2* d_pe_info = nullptr;     // [nparts][kPartSlots]
   uint32_t* d_pe_dir = nullptr;   // [nparts][kPartDir]
+  uint32_t* d_pe_ids = nullptr;   // [table entries] entry id per table position (online tables; else null)
   uint4* d_rec16 = nullptr;       // chunk pool: [chunks][kChunk] (addr, ts) and X words
   uint32_t* d_cmeta = nullptr;
   unsigned long long* d_cmatch = nullptr;
@@ -385,7 +387,9 @@ static void free_route_table(nmg_engine* h) {
   (void)hipFree(h->d_pe_nodes);
   (void)hipFree(h->d_pe_info);
   (void)hipFree(h->d_pe_dir);
+  (void)hipFree(h->d_pe_ids);
   h->d_pe_dir = nullptr;
+  h->d_pe_ids = nullptr;
   h->d_parts = nullptr;
   h->d_pbounds = nullptr;
   h->d_pdir = nullptr;
@@ -881,15 +885,24 @@ static void route_segments(const uint64_t* b, uint32_t P, RSeg* seg, uint32_t* n
 // keys, each at most kPartKeys keys and kPartEntries entries, and -- where
 // the keys allow it -- at most kPartCells dense page cells over all threads,
 // so that a partition's lookup tree, node records, object counters and page
-// cells fit one workgroup's LDS.  Only for the offline table (entry id =
-// table position, so a key range owns an id range) of engines that count
-// per object (NMG_F_MATCH_SAMPLES) without the dump modes' per-sample
-// output or per-object levels; otherwise the table keeps attribute_kernel.
+// cells fit one workgroup's LDS.  A key range owns a range of table
+// positions; `ids` (an online table, nmg_update_objects) maps a position to
+// its entry id (null: the id is the position).  An online table's entries
+// have their page cells in id order, scattered over the address order, so
+// its partitions are not cut by cells (the cells of a partition whose span is
+// too wide for LDS take global atomics).  Only for engines that count per
+// object (NMG_F_MATCH_SAMPLES) without the dump modes' per-sample output or
+// per-object levels; otherwise the table keeps attribute_kernel.
 static int build_partitions(nmg_engine* h, const uint64_t* keys, const uint32_t* entry_off, uint32_t K,
-                            const std::vector<DevEntry>& dev) {
+                            const std::vector<DevEntry>& dev, const uint32_t* ids) {
   free_route_table(h);
   if (K <= kLdsNodes || !(h->flags & NMG_F_MATCH_SAMPLES) || (h->flags & (NMG_F_SAMPLE_MATCHES | NMG_F_OBJECT_LEVELS)))
     return NMG_OK;
+  if (ids) {  // the identity map is the offline case
+    uint32_t e = 0;
+    while (e < entry_off[K] && ids[e] == e) e++;
+    if (e == entry_off[K]) ids = nullptr;
+  }
   const uint64_t T = h->T;
   std::vector<PartInfo> parts;
   uint32_t k = 0;
@@ -916,7 +929,8 @@ static int build_partitions(nmg_engine* h, const uint64_t* keys, const uint32_t*
           ncb = std::min<uint64_t>(ncb, dev[e].hist);
           nce = std::max<uint64_t>(nce, dev[e].hist + h->npages[e]);
         }
-      if (k > pi.k0 && ncb != ~0ull && (nce - ncb) * T > kPartCells) break;  // (one key alone may exceed: global cells)
+      if (k > pi.k0 && ncb != ~0ull && (ids ? nce - ncb >= (1ull << 31) : (nce - ncb) * T > kPartCells))
+        break;  // (one key alone may exceed: global cells; cell offsets within a partition stay 32-bit)
       cb = ncb;
       ce = nce;
       k++;
@@ -983,6 +997,7 @@ static int build_partitions(nmg_engine* h, const uint64_t* keys, const uint32_t*
   HIP_TRY(h, alloc_copy(h, (void**)&h->d_pe_nodes, pn.data(), pn.size() * sizeof(uint4)));
   HIP_TRY(h, alloc_copy(h, (void**)&h->d_pe_info, pinf.data(), pinf.size() * sizeof(uint2)));
   HIP_TRY(h, alloc_copy(h, (void**)&h->d_pe_dir, pdir.data(), pdir.size() * 4));
+  if (ids) HIP_TRY(h, alloc_copy(h, (void**)&h->d_pe_ids, ids, (size_t)entry_off[K] * 4));
   HIP_TRY(h, hipStreamSynchronize(h->stream));  // (pageable sources)
   h->nparts = P;
   h->route_ok = true;
@@ -1051,7 +1066,7 @@ extern "C" int nmg_set_objects(nmg_engine* h, const uint64_t* keys, const uint32
   HIP_TRY(h, alloc_copy(h, (void**)&h->d_entries, dev.data(), (size_t)nb_entries * sizeof(DevEntry)));
   rc = build_lookup(h, keys, entry_off, nb_keys, dev, h->d_entries);
   if (rc) return rc;
-  rc = build_partitions(h, keys, entry_off, nb_keys, dev);
+  rc = build_partitions(h, keys, entry_off, nb_keys, dev, nullptr);
   if (rc) return rc;
   h->dev_entries = std::move(dev);
 
@@ -1326,7 +1341,7 @@ extern "C" int nmg_update_objects(nmg_engine* h, const uint64_t* keys, const uin
     d.free = o.free_date;
     d.count = d.first = 0;
   }
-  free_route_table(h);  // (the partitions describe the nmg_set_objects table)
+  free_route_table(h);  // (the partitions describe the previous table)
   // build the alarm's lookup beside the current one; keep the current one if that fails
   const LookupSet prev = take_lookup(h);
   rc = build_lookup(h, keys, entry_off, nb_keys, chain, nullptr);
@@ -1362,6 +1377,12 @@ extern "C" int nmg_update_objects(nmg_engine* h, const uint64_t* keys, const uin
     // a partial table that brought new entries: they follow the known ones,
     // in id order, until a table lists every entry
     for (uint32_t id = (uint32_t)h->order.size(); id < h->E; id++) h->order.push_back(id);
+  }
+  // the alarm table's partitions (a failure leaves attribute_kernel for it)
+  rc = build_partitions(h, keys, entry_off, nb_keys, chain, entry_ids);
+  if (rc) {
+    free_route_table(h);
+    return rc;
   }
   for (nmg_engine* w : h->workers) {  // multi-GPU: the table on every device
     rc = nmg_update_objects(w, keys, entry_off, nb_keys, entry_ids, objects);
@@ -2290,6 +2311,7 @@ static int route_analyze_job(nmg_engine* h, const RouteJob& job) {
   Params base = base_params(h, job.data, job.sdescs, job.ranges);
   base.bufcnt = h->d_bufcnt + job.index_base;  // (count slots of the set's first buffer)
   const uint64_t seq0 = (*job.descs)[0].seq;
+  h->route_launches++;
   int slot = 0;
   int rc = launch_events(h, &slot);
   if (rc) return rc;
@@ -2357,6 +2379,7 @@ static int route_analyze_job(nmg_engine* h, const RouteJob& job) {
   lp.pe_nodes = h->d_pe_nodes;
   lp.pe_info = h->d_pe_info;
   lp.pe_dir = h->d_pe_dir;
+  lp.pe_ids = h->d_pe_ids;
   lp.rec16 = h->d_rec16;
   lp.cmeta = h->d_cmeta;
   lp.clist = h->d_clist;
@@ -3437,6 +3460,14 @@ extern "C" int nmg_debug_phase_times(nmg_engine* h, float* first_ms, float* rest
     HIP_TRY(h, hipEventElapsedTime(&rest_ms[i], h->ringr[slot], h->ringm[slot]));
   }
   return cnt;
+}
+
+// Internal (not in include/numamma_gpu.h): analyses (streamed chunks) that
+// took the partition-first path so far (tests)
+extern "C" int nmg_debug_route_count(nmg_engine* h, uint64_t* n) {
+  if (!h || !n) return NMG_ERR_INVALID;
+  *n = h->route_launches;
+  return NMG_OK;
 }
 
 // Internal (not in include/numamma_gpu.h): per-wave phase cycle counts of the

@@ -165,8 +165,10 @@ struct LocalParams {
   const PartInfo* parts;
   const uint64_t* pe_keys;   // [nparts][kPartSlots] keys, ascending
   const uint4* pe_nodes;     // [nparts][kPartSlots][2] (addr, end), (alloc, free) of each key's newest entry
-  const uint2* pe_info;      // [nparts][kPartSlots] (cell - cb or ~0, entry - e0 | older entries << 31)
+  const uint2* pe_info;      // [nparts][kPartSlots] (cell - cb or ~0, table position - e0 | older entries << 31)
   const uint32_t* pe_dir;    // [nparts][kPartDir] largest key index <= slot start | keys inside the slot << 16
+  const uint32_t* pe_ids;    // [table entries] entry id of each table position (an online table,
+                             // nmg_update_objects), or null: the id is the position (nmg_set_objects)
   const uint4* rec16;
   const uint32_t* cmeta;
   const uint32_t* clist;     // chunk id | fill << kChunkIdBits, grouped by partition

@@ -1556,6 +1556,30 @@ __device__ __forceinline__ T l2_load(const T* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// A partition owns a range of table positions; the counters are indexed by
+// entry id, which is the position for the nmg_set_objects table and
+// pe_ids[position] for an online table (nmg_update_objects).
+__device__ __forceinline__ uint64_t entry_id(const LocalParams& lp, uint32_t pos) {
+  return lp.pe_ids ? lp.pe_ids[pos] : pos;
+}
+
+// match_older (nmg_device.h) giving the matching entry's table position
+// (-1: none), its buffer_addr and its histogram base
+__device__ __forceinline__ int32_t match_older_pos(const Params& p, uint32_t first, uint32_t count, uint64_t addr,
+                                                   uint64_t ts, uint64_t& baddr, uint64_t& hist) {
+  for (uint32_t j = first + 1; j < first + count; j++) {  // older entries of a reused address
+    const uint4* r = reinterpret_cast<const uint4*>(p.chain + j);
+    const uint4 ra = r[0], rb = r[1];
+    if (entry_match(ra, rb, addr, ts)) {
+      const uint4 rc = r[2];
+      baddr = u64of(ra.x, ra.y);
+      hist = u64of(rc.x, rc.y);
+      return (int32_t)j;
+    }
+  }
+  return -1;
+}
+
 template <bool TIMING>
 __global__ __launch_bounds__(kLWG, 1) void local_kernel(LocalParams lp) {
   __shared__ uint64_t s_keys[kPartSlots];
@@ -1753,13 +1777,11 @@ __global__ __launch_bounds__(kLWG, 1) void local_kernel(LocalParams lp) {
         for (int j = 0; j < kLC; j++) {
           if (!older[j]) continue;
           const uint4 d = reinterpret_cast<const uint4*>(p.nodes + pi.k0 + (uint32_t)r[j])[3];  // (count, first)
-          Match m;
-          m.e = -1;
-          match_older(p, d.y, d.x, addr[j], ts[j], m);
-          if (m.e >= 0) {
-            erel[j] = (int32_t)(m.e - pi.e0);
-            baddr[j] = m.baddr;
-            hrel[j] = m.hist == kHistSparse ? kEmpty32 : (uint32_t)(m.hist - pi.cb);
+          uint64_t hist = kHistSparse;
+          const int32_t pos = match_older_pos(p, d.y, d.x, addr[j], ts[j], baddr[j], hist);
+          if (pos >= 0) {
+            erel[j] = pos - (int32_t)pi.e0;
+            hrel[j] = hist == kHistSparse ? kEmpty32 : (uint32_t)(hist - pi.cb);
           }
         }
         vm_drain();
@@ -1785,7 +1807,7 @@ __global__ __launch_bounds__(kLWG, 1) void local_kernel(LocalParams lp) {
 #pragma unroll
         for (int j = 0; j < kLC; j++) {
           if (erel[j] < 0 || w[j] < kLaneMaxWeight) continue;
-          const uint64_t e = pi.e0 + (uint32_t)erel[j];
+          const uint64_t e = entry_id(lp, pi.e0 + (uint32_t)erel[j]);
           atomicAdd(reinterpret_cast<unsigned long long*>(p.sum64 + objcw_index(e, xr[j].acc, 0, p.nb_entries)), 1ull);
           atomicAdd(reinterpret_cast<unsigned long long*>(p.sum64 + objcw_index(e, xr[j].acc, 1, p.nb_entries)),
                     (unsigned long long)w[j]);
@@ -1825,7 +1847,7 @@ __global__ __launch_bounds__(kLWG, 1) void local_kernel(LocalParams lp) {
             if (hrel[j] != kEmpty32 && !ncell) {
               atomicAdd(p.hist + uint64_t(xr[j].th) * p.hist_cells + pi.cb + hrel[j] + page[j], 1u);
             } else if (hrel[j] == kEmpty32) {
-              const uint32_t sidx = p.entries[pi.e0 + (uint32_t)erel[j]].sidx;
+              const uint32_t sidx = p.entries[entry_id(lp, pi.e0 + (uint32_t)erel[j])].sidx;
               if (sidx != ~0u) sparse_add(p, sparse_key(sidx, xr[j].th, page[j]), lp.seq0 + xr[j].g, xr[j].off, 1u);
             }
           }
@@ -1863,7 +1885,7 @@ __global__ __launch_bounds__(kLWG, 1) void local_kernel(LocalParams lp) {
     // workgroup writes these words during the launch), the others with
     // atomics
     for (uint32_t i = tid; i < pi.ne; i += kLWG) {
-      const uint64_t e = pi.e0 + i;
+      const uint64_t e = entry_id(lp, pi.e0 + i);
 #pragma unroll
       for (uint32_t a = 0; a < 2; a++) {
         const uint64_t v = s_owt[a][i];

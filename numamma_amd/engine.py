@@ -55,6 +55,7 @@ class Engine:
         self.nb_threads = nb_threads
         self._keep = []
         self.table: Optional[ObjectTable] = None
+        self.nb_entries = 0
         self.buffer_bytes: list = []  # lengths of the analysed (non-empty) buffers
 
     def close(self):
@@ -79,6 +80,7 @@ class Engine:
         self._c(lib.nmg_set_objects(self.h, _ptr(keys, C.c_uint64), _ptr(off, C.c_uint32), keys.shape[0],
                                     objs.ctypes.data_as(C.POINTER(_lib.nmg_object)), table.nb_entries))
         self.table = table
+        self.nb_entries = table.nb_entries  # (the engine's entry count: update_objects may add ids)
 
     def update_objects(self, keys: np.ndarray, entry_off: np.ndarray, entry_ids: np.ndarray, objs: np.ndarray):
         """nmg_update_objects: the table at an alarm (--online-analysis); objs in
@@ -89,6 +91,8 @@ class Engine:
         objs = np.ascontiguousarray(objs)
         self._c(lib.nmg_update_objects(self.h, _ptr(keys, C.c_uint64), _ptr(off, C.c_uint32), keys.shape[0],
                                        _ptr(ids, C.c_uint32), objs.ctypes.data_as(C.POINTER(_lib.nmg_object))))
+        if ids.shape[0]:
+            self.nb_entries = max(self.nb_entries, int(ids.max()) + 1)
 
     def submit_ring(self, ring: np.ndarray, tail: int, head: int, thread_rank: int, access: int):
         ring = np.ascontiguousarray(ring, dtype=np.uint8)
@@ -180,6 +184,13 @@ class Engine:
         cnt = self._c(lib.nmg_debug_phase_times(self.h, a, t, n))
         return [a[i] for i in range(cnt)], [t[i] for i in range(cnt)]
 
+    def route_count(self) -> int:
+        """Analyses (streamed chunks) that took the partition-first path so far
+        (internal; tests)."""
+        n = C.c_uint64()
+        self._c(lib.nmg_debug_route_count(self.h, C.byref(n)))
+        return n.value
+
     def last_analyze_ms(self) -> float:
         ms = C.c_float()
         self._c(lib.nmg_last_analyze_ms(self.h, C.byref(ms)))
@@ -200,14 +211,14 @@ class Engine:
         return s, f
 
     def object_counters(self):
-        E = self.table.nb_entries
+        E = max(self.table.nb_entries, self.nb_entries)
         first = np.zeros(E, dtype=np.uint64)
         cw = np.zeros((E, 2, 2), dtype=np.uint64)
         self._c(lib.nmg_get_object_counters(self.h, _ptr(first, C.c_uint64), _ptr(cw, C.c_uint64)))
         return first, cw
 
     def object_levels(self):
-        E = self.table.nb_entries
+        E = max(self.table.nb_entries, self.nb_entries)
         lv = np.zeros((E, 2, 37), dtype=np.uint64)
         self._c(lib.nmg_get_object_levels(self.h, _ptr(lv, C.c_uint64)))
         return lv

@@ -76,6 +76,8 @@ def test_online_analysis_bit_exact(tmp_path, cfg, nb_alarms, chunk):
     eng.analyze()
     eng.stream_end()
     eng.synchronize()
+    if cfg.nb_intervals > 10_000:  # large alarm tables take the partition-first path
+        assert eng.route_count() > 0
     # at exit: the table ma_finalize walks (the report's objects and order)
     t = rp.table
     eng.update_objects(t.keys, t.entry_off, np.arange(t.nb_entries, dtype=np.uint32), table_objects(t))
@@ -213,6 +215,8 @@ def test_online_live_tables_bit_exact(tmp_path, cfg, nb_alarms, chunk):
     eng.analyze()
     eng.stream_end()
     eng.synchronize()
+    if cfg.nb_intervals > 10_000:  # partitions over ids in creation order (an id map)
+        assert eng.route_count() > 0
     eng.update_objects(final.keys, final.entry_off, cid, table_objects(final))  # ma_finalize's table
     eng.table = final  # the report's metadata, in the finalize table's order
     g, ns, nf = eng.global_counters()
@@ -309,3 +313,35 @@ def test_partial_update_after_permuted_table(tmp_path):
     g, ns, nf = eng.global_counters()
     assert ns > 0
     eng.close()
+
+
+def test_online_route_matches_single_pass():
+    """A large table given through nmg_update_objects with permuted ids (a
+    partition's table positions map to scattered entry ids and page cells):
+    the partition-first path and the single-pass kernel give the same
+    counters, page cells and per-buffer counts, older entries of reused
+    addresses included."""
+    from numamma_amd.engine import Engine, table_objects
+    from numamma_amd.replay import ObjectTable
+
+    rp = generate(SynthConfig(nb_samples=400_000, nb_intervals=60_000, reuse_frac=0.3, realloc_frac=0.1, seed=83))
+    t = rp.table
+    perm = np.random.default_rng(83).permutation(t.nb_entries).astype(np.uint32)
+    out = []
+    for flags in (_lib.NMG_F_DEFAULT, _lib.NMG_F_DEFAULT | 0x10000):  # (internal 0x10000: no partition-first path)
+        eng = Engine(flags=flags, nb_threads=rp.nb_threads)
+        eng.set_objects(ObjectTable.empty())
+        eng.update_objects(t.keys, t.entry_off, perm, table_objects(t))
+        eng.submit_replay(rp)
+        eng.analyze()
+        eng.synchronize()
+        g, ns, nf = eng.global_counters()
+        first, cw = eng.object_counters()
+        bs, bf = eng.buffer_counts()
+        out.append(((g, ns, nf, first, cw, bs, bf, eng.page_cells().copy()), eng.route_count()))
+        eng.close()
+    (a, na), (b, nb) = out
+    assert na > 0 and nb == 0
+    assert a[2] > 0
+    for x, y in zip(a, b):
+        assert np.array_equal(np.asarray(x), np.asarray(y))
