@@ -255,6 +255,8 @@ struct nmg_engine {
   uint2* d_pe_info = nullptr;     // [nparts][kPartSlots]
   uint32_t* d_pe_dir = nullptr;   // [nparts][kPartDir]
   uint32_t* d_pe_ids = nullptr;   // [table entries] entry id per table position (online tables; else null)
+  uint32_t* d_pe_lrel = nullptr;  // [table entries] first packed LDS cell (online tables)
+  uint32_t* d_pe_cmap = nullptr;  // packed cell -> histogram cell (online tables)
   uint4* d_rec16 = nullptr;       // chunk pool: [chunks][kChunk] (addr, ts) and X words
   uint32_t* d_cmeta = nullptr;
   unsigned long long* d_cmatch = nullptr;
@@ -388,8 +390,12 @@ static void free_route_table(nmg_engine* h) {
   (void)hipFree(h->d_pe_info);
   (void)hipFree(h->d_pe_dir);
   (void)hipFree(h->d_pe_ids);
+  (void)hipFree(h->d_pe_lrel);
+  (void)hipFree(h->d_pe_cmap);
   h->d_pe_dir = nullptr;
   h->d_pe_ids = nullptr;
+  h->d_pe_lrel = nullptr;
+  h->d_pe_cmap = nullptr;
   h->d_parts = nullptr;
   h->d_pbounds = nullptr;
   h->d_pdir = nullptr;
@@ -903,15 +909,22 @@ static int build_partitions(nmg_engine* h, const uint64_t* keys, const uint32_t*
     while (e < entry_off[K] && ids[e] == e) e++;
     if (e == entry_off[K]) ids = nullptr;
   }
+  if (ids && h->hist_cells >= (1ull << 31)) return NMG_OK;  // (cell indices of an online table: 32-bit)
   const uint64_t T = h->T;
   std::vector<PartInfo> parts;
+  // an online table: the partition's dense cells packed in LDS in table
+  // order (lrel: an entry's first LDS cell per table position; cmap: the
+  // histogram cell of every packed cell, per partition from PartInfo::cmap)
+  std::vector<uint32_t> lrel, cmap;
+  if (ids) lrel.assign(entry_off[K], kEmpty32);
   uint32_t k = 0;
   while (k < K) {
     PartInfo pi;
     memset(&pi, 0, sizeof(pi));
     pi.k0 = k;
     pi.e0 = entry_off[k];
-    uint64_t cb = ~0ull, ce = 0;
+    pi.cmap = ~0u;
+    uint64_t cb = ~0ull, ce = 0, cc = 0;  // dense cells in [cb, ce), cc of them
     while (k < K && k - pi.k0 < kPartKeys) {
       // a partition's keys span less than 2^(kAddrBits - 1) bytes, so that the
       // compact records' address field (relative to the partition's first key)
@@ -923,16 +936,19 @@ static int build_partitions(nmg_engine* h, const uint64_t* keys, const uint32_t*
         if (k == pi.k0) return NMG_OK;  // one address reused more than kPartEntries times: keep attribute_kernel
         break;
       }
-      uint64_t ncb = cb, nce = ce;
+      uint64_t ncb = cb, nce = ce, ncc = cc;
       for (uint32_t e = ea; e < eb; e++)
         if (dev[e].hist != kHistSparse) {
+          const uint64_t np = h->npages[dev[e].id];
           ncb = std::min<uint64_t>(ncb, dev[e].hist);
-          nce = std::max<uint64_t>(nce, dev[e].hist + h->npages[e]);
+          nce = std::max<uint64_t>(nce, dev[e].hist + np);
+          ncc += np;
         }
-      if (k > pi.k0 && ncb != ~0ull && (ids ? nce - ncb >= (1ull << 31) : (nce - ncb) * T > kPartCells))
-        break;  // (one key alone may exceed: global cells; cell offsets within a partition stay 32-bit)
+      if (k > pi.k0 && ncb != ~0ull && (ids ? ncc : nce - ncb) * T > kPartCells)
+        break;  // (one key alone may exceed: global cells)
       cb = ncb;
       ce = nce;
+      cc = ncc;
       k++;
     }
     pi.nk = k - pi.k0;
@@ -940,6 +956,19 @@ static int build_partitions(nmg_engine* h, const uint64_t* keys, const uint32_t*
     pi.cb = cb == ~0ull ? 0 : cb;
     pi.span = cb == ~0ull ? 0 : (uint32_t)(ce - cb);
     pi.pages_lds = pi.span && (uint64_t)pi.span * T <= kPartCells;
+    if (ids && cc && cc * T <= kPartCells) {  // online: the cells packed (cmap), always in LDS
+      pi.cmap = (uint32_t)cmap.size();
+      pi.span = (uint32_t)cc;
+      pi.pages_lds = 1;
+      uint32_t off = 0;
+      for (uint32_t e = pi.e0; e < pi.e0 + pi.ne; e++)
+        if (dev[e].hist != kHistSparse) {
+          const uint32_t np = (uint32_t)h->npages[dev[e].id];
+          lrel[e] = off;
+          for (uint32_t g = 0; g < np; g++) cmap.push_back((uint32_t)(dev[e].hist + g));
+          off += np;
+        }
+    }
     const uint64_t kspan = keys[k - 1] - keys[pi.k0];
     while (pi.dshift < 63 && (kspan >> pi.dshift) >= kPartDir) pi.dshift++;
     parts.push_back(pi);
@@ -970,7 +999,10 @@ static int build_partitions(nmg_engine* h, const uint64_t* keys, const uint32_t*
       pn[2 * o] = make_uint4((uint32_t)d.addr, (uint32_t)(d.addr >> 32), (uint32_t)d.end, (uint32_t)(d.end >> 32));
       pn[2 * o + 1] = make_uint4((uint32_t)d.alloc, (uint32_t)(d.alloc >> 32), (uint32_t)d.free, (uint32_t)(d.free >> 32));
       const uint32_t older = entry_off[kk + 1] - entry_off[kk] > 1 ? 0x80000000u : 0u;
-      pinf[o] = make_uint2(d.hist == kHistSparse ? kEmpty32 : (uint32_t)(d.hist - pi.cb), (entry_off[kk] - pi.e0) | older);
+      const uint32_t hrel = d.hist == kHistSparse ? kEmpty32
+                            : pi.cmap != ~0u         ? lrel[entry_off[kk]]
+                                                     : (uint32_t)(d.hist - pi.cb);
+      pinf[o] = make_uint2(hrel, (entry_off[kk] - pi.e0) | older);
     }
     const uint64_t f = keys[pi.k0];
     uint32_t lo = 0;
@@ -997,7 +1029,11 @@ static int build_partitions(nmg_engine* h, const uint64_t* keys, const uint32_t*
   HIP_TRY(h, alloc_copy(h, (void**)&h->d_pe_nodes, pn.data(), pn.size() * sizeof(uint4)));
   HIP_TRY(h, alloc_copy(h, (void**)&h->d_pe_info, pinf.data(), pinf.size() * sizeof(uint2)));
   HIP_TRY(h, alloc_copy(h, (void**)&h->d_pe_dir, pdir.data(), pdir.size() * 4));
-  if (ids) HIP_TRY(h, alloc_copy(h, (void**)&h->d_pe_ids, ids, (size_t)entry_off[K] * 4));
+  if (ids) {
+    HIP_TRY(h, alloc_copy(h, (void**)&h->d_pe_ids, ids, (size_t)entry_off[K] * 4));
+    HIP_TRY(h, alloc_copy(h, (void**)&h->d_pe_lrel, lrel.data(), lrel.size() * 4));
+    if (!cmap.empty()) HIP_TRY(h, alloc_copy(h, (void**)&h->d_pe_cmap, cmap.data(), cmap.size() * 4));
+  }
   HIP_TRY(h, hipStreamSynchronize(h->stream));  // (pageable sources)
   h->nparts = P;
   h->route_ok = true;
@@ -2380,6 +2416,8 @@ static int route_analyze_job(nmg_engine* h, const RouteJob& job) {
   lp.pe_info = h->d_pe_info;
   lp.pe_dir = h->d_pe_dir;
   lp.pe_ids = h->d_pe_ids;
+  lp.pe_lrel = h->d_pe_lrel;
+  lp.pe_cmap = h->d_pe_cmap;
   lp.rec16 = h->d_rec16;
   lp.cmeta = h->d_cmeta;
   lp.clist = h->d_clist;

@@ -98,7 +98,9 @@ struct PartInfo {
   uint32_t span;
   uint32_t dshift;     // directory slot j covers [first key + (j << dshift), + 2^dshift)
   uint32_t pages_lds;  // nb_threads * span <= kPartCells: page cells in LDS, else global atomics
-  uint32_t pad[3];
+  uint32_t cmap;       // ~0: cells [cb, cb + span); else (online table) span packed cells, the
+                       // histogram cell of packed cell j at pe_cmap[cmap + j]
+  uint32_t pad[2];
 };
 static_assert(sizeof(PartInfo) == 48, "PartInfo");
 
@@ -165,10 +167,12 @@ struct LocalParams {
   const PartInfo* parts;
   const uint64_t* pe_keys;   // [nparts][kPartSlots] keys, ascending
   const uint4* pe_nodes;     // [nparts][kPartSlots][2] (addr, end), (alloc, free) of each key's newest entry
-  const uint2* pe_info;      // [nparts][kPartSlots] (cell - cb or ~0, table position - e0 | older entries << 31)
+  const uint2* pe_info;      // [nparts][kPartSlots] (cell - cb, packed cell or ~0, table position - e0 | older entries << 31)
   const uint32_t* pe_dir;    // [nparts][kPartDir] largest key index <= slot start | keys inside the slot << 16
   const uint32_t* pe_ids;    // [table entries] entry id of each table position (an online table,
                              // nmg_update_objects), or null: the id is the position (nmg_set_objects)
+  const uint32_t* pe_lrel;   // [table entries] an entry's first packed cell (PartInfo::cmap != ~0)
+  const uint32_t* pe_cmap;   // packed cell -> histogram cell
   const uint4* rec16;
   const uint32_t* cmeta;
   const uint32_t* clist;     // chunk id | fill << kChunkIdBits, grouped by partition

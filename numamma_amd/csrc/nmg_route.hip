@@ -1580,7 +1580,9 @@ __device__ __forceinline__ int32_t match_older_pos(const Params& p, uint32_t fir
   return -1;
 }
 
-template <bool TIMING>
+// PACKED: an online table with packed page cells (LocalParams::pe_cmap; a
+// variant of its own, so that the offline table's flush carries none of it)
+template <bool TIMING, bool PACKED>
 __global__ __launch_bounds__(kLWG, 1) void local_kernel(LocalParams lp) {
   __shared__ uint64_t s_keys[kPartSlots];
   // node records split in two 16 B arrays (addr, end) and (alloc, free): a
@@ -1781,7 +1783,9 @@ __global__ __launch_bounds__(kLWG, 1) void local_kernel(LocalParams lp) {
           const int32_t pos = match_older_pos(p, d.y, d.x, addr[j], ts[j], baddr[j], hist);
           if (pos >= 0) {
             erel[j] = pos - (int32_t)pi.e0;
-            hrel[j] = hist == kHistSparse ? kEmpty32 : (uint32_t)(hist - pi.cb);
+            hrel[j] = hist == kHistSparse ? kEmpty32
+                      : PACKED && pi.cmap != ~0u ? lp.pe_lrel[pos]
+                                         : (uint32_t)(hist - pi.cb);
           }
         }
         vm_drain();
@@ -1915,6 +1919,7 @@ __global__ __launch_bounds__(kLWG, 1) void local_kernel(LocalParams lp) {
     // word), the row of a cell by a multiply-high (li * span < 2^32: exact)
     {
       const uint32_t nw = (ncell + 1) / 2, span = pi.span;
+      const uint32_t cmap = PACKED ? __builtin_amdgcn_readfirstlane(pi.cmap) : ~0u;
       const uint32_t smag = span ? 0xffffffffu / span + 1u : 0u;
       constexpr uint32_t kU = 4;
       for (uint32_t j0 = tid; j0 < nw; j0 += kU * kLWG) {
@@ -1929,7 +1934,9 @@ __global__ __launch_bounds__(kLWG, 1) void local_kernel(LocalParams lp) {
           for (uint32_t h = 0; h < 2; h++) {
             cnt[u][h] = (v >> (16 * h)) & 0xffffu;
             const uint32_t li = 2 * j + h, th = __umulhi(li, smag), rel = li - th * span;
-            pc[u][h] = p.hist + uint64_t(th) * p.hist_cells + pi.cb + rel;
+            uint64_t cell = pi.cb + rel;
+            if (cmap != ~0u) cell = cnt[u][h] ? lp.pe_cmap[cmap + rel] : 0u;  // (online: packed cells)
+            pc[u][h] = p.hist + uint64_t(th) * p.hist_cells + cell;
             old[u][h] = (excl && cnt[u][h]) ? l2_load(pc[u][h]) : 0u;
           }
         }
@@ -2030,8 +2037,14 @@ hipError_t launch_scatter(uint32_t grid, hipStream_t s, const ScatterParams& r) 
 }
 
 hipError_t launch_local(uint32_t grid, hipStream_t s, const LocalParams& r) {
-  if (r.p.flags & kDbgLocalTiming) hipLaunchKernelGGL(local_kernel<true>, dim3(grid), dim3(kLWG), 0, s, r);
-  else hipLaunchKernelGGL(local_kernel<false>, dim3(grid), dim3(kLWG), 0, s, r);
+  const bool timing = (r.p.flags & kDbgLocalTiming) != 0, packed = r.pe_cmap != nullptr;
+  if (packed) {
+    if (timing) hipLaunchKernelGGL((local_kernel<true, true>), dim3(grid), dim3(kLWG), 0, s, r);
+    else hipLaunchKernelGGL((local_kernel<false, true>), dim3(grid), dim3(kLWG), 0, s, r);
+  } else {
+    if (timing) hipLaunchKernelGGL((local_kernel<true, false>), dim3(grid), dim3(kLWG), 0, s, r);
+    else hipLaunchKernelGGL((local_kernel<false, false>), dim3(grid), dim3(kLWG), 0, s, r);
+  }
   return hipGetLastError();
 }
 
