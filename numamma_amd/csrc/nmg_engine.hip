@@ -165,6 +165,8 @@ struct nmg_engine {
   uint64_t* d_scratch = nullptr;          // [2] small device results (nmg_hist_pack / unpack)
   uint64_t* d_sparse_keys = nullptr;
   uint32_t* d_sparse_vals = nullptr;
+  uint64_t* d_objcw = nullptr;       // [objcw_cap][4] per-object counters laid out for the D2H
+  uint64_t objcw_cap = 0;
   uint64_t* d_sparse_ck = nullptr;  // [sparse_cap + 1] compacted (key, count) words + the count (sparse_download)
   uint32_t* d_sparse_dirty = nullptr;  // [2] parity flags (see reset_kernel)
   uint32_t* d_smatch = nullptr;        // NMG_F_SAMPLE_MATCHES: per 8 B of the arena span
@@ -347,6 +349,9 @@ static void free_counters(nmg_engine* h) {
   h->d_sparse_vals = nullptr;
   (void)hipFree(h->d_sparse_ck);
   h->d_sparse_ck = nullptr;
+  (void)hipFree(h->d_objcw);
+  h->d_objcw = nullptr;
+  h->objcw_cap = 0;
   (void)hipFree(h->d_sparse_dirty);
   h->d_sparse_dirty = nullptr;
   (void)hipFree(h->d_pk64);
@@ -2733,13 +2738,20 @@ extern "C" int nmg_get_object_counters(nmg_engine* h, uint64_t* first_ordinal, u
   if (rc) return rc;
   if (first_ordinal && h->E)
     HIP_TRY(h, hipMemcpy(first_ordinal, h->d_min64 + 36, (size_t)h->E * 8, hipMemcpyDeviceToHost));
-  if (count_weight && h->E) {
-    std::vector<uint64_t> soa((size_t)h->E * 4);
-    HIP_TRY(h, hipMemcpy(soa.data(), h->d_sum64 + 2 * kGlobalSums, soa.size() * 8, hipMemcpyDeviceToHost));
-    for (uint64_t e = 0; e < h->E; e++)
-      for (uint32_t a = 0; a < 2; a++)
-        for (uint32_t w = 0; w < 2; w++)
-          count_weight[e * 4 + a * 2 + w] = soa[objcw_index(e, a, w, h->E) - 2 * kGlobalSums];
+  if (count_weight && h->E) {  // the SoA rows laid out per entry on the device, then one copy
+    static_assert(objcw_index(1, 0, 0, 8) - objcw_index(0, 0, 0, 8) == 1 && objcw_index(0, 0, 1, 8) - objcw_index(0, 0, 0, 8) == 8 &&
+                      objcw_index(0, 1, 0, 8) - objcw_index(0, 0, 0, 8) == 16,
+                  "objcw_aos_kernel reads rows access * 2 + w");
+    if (h->E > h->objcw_cap) {
+      (void)hipFree(h->d_objcw);
+      h->d_objcw = nullptr;
+      h->objcw_cap = 0;
+      HIP_TRY(h, hipMalloc(&h->d_objcw, (size_t)h->E * 32));
+      h->objcw_cap = h->E;
+    }
+    HIP_TRY(h, launch_objcw_aos(h->stream, h->d_sum64 + 2 * kGlobalSums, h->E, h->d_objcw));
+    HIP_TRY(h, hipMemcpyAsync(count_weight, h->d_objcw, (size_t)h->E * 32, hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(h, hipStreamSynchronize(h->stream));
   }
   return NMG_OK;
 }

@@ -215,6 +215,8 @@ hipError_t launch_hist_pack(hipStream_t s, const uint32_t* hist, uint64_t ncells
                             uint64_t cap, unsigned long long* cnt, uint32_t* wgcnt);  // wgcnt: [1024] workspace
 hipError_t launch_hist_unpack(hipStream_t s, uint32_t* hist, uint64_t ncells, const void* u8, const void* ovf,
                               uint64_t n, unsigned long long* bad);
+// per-object counts and weights, SoA rows -> [E][access][w] (aos: E * 32 B)
+hipError_t launch_objcw_aos(hipStream_t s, const uint64_t* soa, uint64_t E, void* aos);
 // page-cell rows on the device (nmg_get_page_cells / nmg_report): per dense
 // entry the number of non-zero cells, then the (entry, thread, page, count)
 // rows at each entry's offset, in (thread, page) order

@@ -1096,6 +1096,26 @@ __global__ __launch_bounds__(kPackWG) void hist_pack_kernel(const uint32_t* hist
   }
 }
 
+// nmg_get_object_counters: the per-object counts and weights from their four
+// SoA rows (objcw_index: row access * 2 + w of E words) to [E][access][w],
+// one 32 B record per entry (a single contiguous D2H)
+__global__ __launch_bounds__(256) void objcw_aos_kernel(const uint64_t* soa, uint64_t E, uint4* aos) {
+  const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
+  for (uint64_t e = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; e < E; e += stride) {
+    const uint64_t r0 = soa[e], r1 = soa[E + e], r2 = soa[2 * E + e], r3 = soa[3 * E + e];
+    aos[2 * e] = make_uint4((uint32_t)r0, (uint32_t)(r0 >> 32), (uint32_t)r1, (uint32_t)(r1 >> 32));
+    aos[2 * e + 1] = make_uint4((uint32_t)r2, (uint32_t)(r2 >> 32), (uint32_t)r3, (uint32_t)(r3 >> 32));
+  }
+}
+
+hipError_t launch_objcw_aos(hipStream_t s, const uint64_t* soa, uint64_t E, void* aos) {
+  if (E) {
+    const uint32_t grid = (uint32_t)std::min<uint64_t>((E + 255) / 256, 4096);
+    hipLaunchKernelGGL(objcw_aos_kernel, dim3(grid), dim3(256), 0, s, soa, E, reinterpret_cast<uint4*>(aos));
+  }
+  return hipGetLastError();
+}
+
 // nmg_hist_unpack: hist = summed bytes, then += every overflow entry
 __global__ __launch_bounds__(256) void hist_unpack_kernel(uint32_t* hist, uint64_t ncells, const uint8_t* u8) {
   const uint64_t stride = uint64_t(gridDim.x) * blockDim.x, n4 = (ncells + 3) / 4;

@@ -120,6 +120,26 @@ class Engine:
                                        _ptr(acc, C.c_uint32)))
         self.buffer_bytes.extend(int(x) for x in lens if x)
 
+    def submit_arena(self, arena: np.ndarray, offs, lens, ranks, acc):
+        """nmg_submit_buffers over buffers laid out in one u8 host array:
+        buffer i = arena[offs[i] : offs[i] + lens[i]] (analysis order), its
+        pointers computed in numpy (no per-buffer Python objects; the arena
+        registered with register_host is read in place)."""
+        arena = np.ascontiguousarray(arena, dtype=np.uint8)
+        offs = np.ascontiguousarray(offs, dtype=np.uint64)
+        lens = np.ascontiguousarray(lens, dtype=np.uint64)
+        ranks = np.ascontiguousarray(ranks, dtype=np.uint32)
+        acc = np.ascontiguousarray(acc, dtype=np.uint32)
+        n = offs.shape[0]
+        if not (lens.shape[0] == ranks.shape[0] == acc.shape[0] == n):
+            raise ValueError("submit_arena: offs, lens, ranks and acc differ in length")
+        if n and int((offs + lens).max()) > arena.nbytes:
+            raise ValueError("submit_arena: a buffer ends past the arena")
+        ptrs = offs + np.uint64(arena.ctypes.data)
+        self._c(lib.nmg_submit_buffers(self.h, n, ptrs.ctypes.data_as(C.POINTER(C.c_void_p)),
+                                       _ptr(lens, C.c_uint64), _ptr(ranks, C.c_uint32), _ptr(acc, C.c_uint32)))
+        self.buffer_bytes.extend(lens[lens > 0].tolist())
+
     def register_host(self, arr: np.ndarray):
         """nmg_register_host over a host array the caller keeps alive (page
         aligned, its pages its own: page_aligned_empty): buffers submitted from

@@ -495,7 +495,8 @@ def test_zero_copy_bit_exact_vs_oracle(tmp_path, monkeypatch, cfg, mode):
 def test_register_host_api(tmp_path):
     """Registration rules: overlapping ranges are refused, a range holding
     submitted buffers cannot be unregistered before nmg_clear_buffers, and
-    a registered engine gives the same counters as a copying one."""
+    a registered engine gives the same counters as a copying one, its buffers
+    given as views or as (arena, offsets, lengths) arrays (Engine.submit_arena)."""
     from numamma_amd.engine import Engine
     from numamma_amd.replay import RECORD_DTYPE
 
@@ -515,7 +516,7 @@ def test_register_host_api(tmp_path):
         arena[off:off + b.shape[0]] = b
     views = [(r, a, arena[off:off + b.shape[0]]) for (r, a, b), off in zip(lins, offs)]
     out = []
-    for register in (False, True):
+    for register, as_arena in ((False, False), (True, False), (True, True)):
         eng = Engine(nb_threads=rp.nb_threads)
         eng.set_objects(rp.table)
         if register:
@@ -524,7 +525,17 @@ def test_register_host_api(tmp_path):
                 eng.register_host(arena[4096:])  # overlap
             with pytest.raises(_lib.NmgError):
                 eng.register_host(arena[100:])  # not page-aligned
-        eng.submit_buffers(views)
+        if as_arena:
+            lens = np.array([b.shape[0] for _, _, b in lins], dtype=np.uint64)
+            ranks = np.array([r for r, _, _ in lins], dtype=np.uint32)
+            accs = np.array([a for _, a, _ in lins], dtype=np.uint32)
+            with pytest.raises(ValueError):
+                eng.submit_arena(arena, offs, lens, ranks[:-1], accs)
+            with pytest.raises(ValueError):
+                eng.submit_arena(arena[:offs[-1]], offs, lens, ranks, accs)  # past the arena
+            eng.submit_arena(arena, offs, lens, ranks, accs)
+        else:
+            eng.submit_buffers(views)
         eng.analyze()
         eng.synchronize()
         g, ns, nf = eng.global_counters()
@@ -537,8 +548,9 @@ def test_register_host_api(tmp_path):
             eng.clear_buffers()
             eng.unregister_host(arena)
         eng.close()
-    for x, y in zip(*out):
-        assert np.array_equal(np.asarray(x), np.asarray(y))
+    for o in out[1:]:
+        for x, y in zip(out[0], o):
+            assert np.array_equal(np.asarray(x), np.asarray(y))
     assert out[0][1] == sum(int((b.view(RECORD_DTYPE)["type"] == 9).sum()) for _, _, b in lins)
 
 

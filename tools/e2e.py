@@ -79,7 +79,10 @@ def main():
             base = 0
             for (_, _, b), off in zip(lins, offs):
                 arena[base + off:base + off + b.shape[0]] = b
-            zc_views = [(r, acc, arena[base + off:base + off + b.shape[0]]) for (r, acc, b), off in zip(lins, offs)]
+            zc_views = (arena, np.array(offs, dtype=np.uint64) + base,
+                        np.array([b.shape[0] for _, _, b in lins], dtype=np.uint64),
+                        np.array([r for r, _, _ in lins], dtype=np.uint32),
+                        np.array([acc for _, acc, _ in lins], dtype=np.uint32))
             t = time.perf_counter()
             eng.register_host(arena)
             reg_s = time.perf_counter() - t
@@ -95,7 +98,7 @@ def main():
             elif mode == "batch":
                 eng.submit_buffers(lins)
             elif mode == "zerocopy":
-                eng.submit_buffers(zc_views)
+                eng.submit_arena(*zc_views)  # (pointers computed in numpy: no per-buffer list)
             else:
                 eng.stream_begin(chunk_bytes=a.chunk_mb << 20, copy_threads=a.threads)
                 for i in range(0, len(lins), a.batch):
