@@ -246,7 +246,7 @@ class Engine:
     def page_cells(self) -> np.ndarray:
         n = lib.nmg_count_page_cells(self.h)
         self._c(n)
-        rows = np.zeros((n, 4), dtype=np.uint32)
+        rows = np.empty((n, 4), dtype=np.uint32)  # (every row written by the engine)
         self._c(lib.nmg_get_page_cells(self.h, _ptr(rows, C.c_uint32), n))
         return rows
 
