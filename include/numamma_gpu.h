@@ -117,8 +117,10 @@ struct nmg_options {
    * nmg_create reads the whole current struct: zero-initialise it.  A
    * caller built against the first version passes its own struct size to
    * nmg_create_ex, which reads only that many bytes.  nb_gpus / devices are
-   * used only with abi_version == NMG_OPTIONS_ABI; nb_gpus > 1 without it is
-   * NMG_ERR_INVALID (not a silent one-GPU engine). */
+   * used only with abi_version == NMG_OPTIONS_ABI.  Without it they are
+   * ignored by nmg_create (a first-version binary's bytes past its struct),
+   * and nmg_create_ex(..., sizeof(struct nmg_options)) rejects nb_gpus > 1
+   * with NMG_ERR_INVALID (not a silent one-GPU engine). */
   uint32_t nb_gpus;
   uint32_t abi_version;      /* NMG_OPTIONS_ABI to use nb_gpus / devices */
   const int32_t *devices;
@@ -336,7 +338,8 @@ int nmg_import_array(nmg_engine *h, int which, const void *d_src);
  * padding): histogram = bytes + overflow, exactly the u32 sum. */
 int nmg_hist_pack(nmg_engine *h, uint32_t threshold, void *d_u8, void *d_ovf, uint64_t ovf_cap, uint64_t *n_ovf);
 int nmg_hist_unpack(nmg_engine *h, const void *d_u8, const void *d_ovf, uint64_t n_ovf);
-/* sparse (object, page, thread) cells: export as (key, count) pairs on host */
+/* sparse (object, page, thread) cells: export as (key, count) pairs on host,
+ * in ascending key order (keys are unique) */
 int64_t nmg_sparse_count(nmg_engine *h);
 int nmg_sparse_export(nmg_engine *h, uint64_t *keys, uint32_t *counts, int64_t n);
 int nmg_sparse_import(nmg_engine *h, const uint64_t *keys, const uint32_t *counts, int64_t n);

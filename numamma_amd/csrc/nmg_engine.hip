@@ -517,11 +517,23 @@ static bool internal_flags_allowed() {
   return e && *e && strcmp(e, "0") != 0;
 }
 
+static int create_impl(nmg_engine** out, const nmg_options* opt_in, size_t opt_size, bool v2_declared);
+
+// nmg_create reads the whole current struct, but a binary built against the
+// first version (32 bytes) may call it too: bytes 32..47 are then whatever
+// follows its struct.  So, as before the v2 fields existed, nb_gpus / devices
+// count only with abi_version == NMG_OPTIONS_ABI and are otherwise ignored;
+// the rejection of a v2 caller's nb_gpus > 1 without the ABI word is
+// nmg_create_ex's, whose opt_size says the caller declared those fields.
 extern "C" int nmg_create(nmg_engine** out, const nmg_options* opt) {
-  return nmg_create_ex(out, opt, sizeof(nmg_options));
+  return create_impl(out, opt, sizeof(nmg_options), false);
 }
 
 extern "C" int nmg_create_ex(nmg_engine** out, const nmg_options* opt_in, size_t opt_size) {
+  return create_impl(out, opt_in, opt_size, opt_size >= sizeof(nmg_options));
+}
+
+static int create_impl(nmg_engine** out, const nmg_options* opt_in, size_t opt_size, bool v2_declared) {
   if (!out) return NMG_ERR_INVALID;
   *out = nullptr;
   // only the caller's bytes of the struct are read (a first-version caller's
@@ -543,7 +555,7 @@ extern "C" int nmg_create_ex(nmg_engine** out, const nmg_options* opt_in, size_t
       return NMG_ERR_INVALID;
     }
     if (o2.abi_version != NMG_OPTIONS_ABI) {
-      if (o2.nb_gpus > 1) {  // (an older multi-GPU caller: not silently one GPU)
+      if (v2_declared && o2.nb_gpus > 1) {  // (a multi-GPU caller without the ABI word: not silently one GPU)
         g_create_error = "nmg_create: nb_gpus > 1 needs abi_version = NMG_OPTIONS_ABI";
         return NMG_ERR_INVALID;
       }
@@ -1419,11 +1431,13 @@ extern "C" int nmg_update_objects(nmg_engine* h, const uint64_t* keys, const uin
     // in id order, until a table lists every entry
     for (uint32_t id = (uint32_t)h->order.size(); id < h->E; id++) h->order.push_back(id);
   }
-  // the alarm table's partitions (a failure leaves attribute_kernel for it)
-  rc = build_partitions(h, keys, entry_off, nb_keys, chain, entry_ids);
-  if (rc) {
+  // the alarm table's partitions.  The new table is committed above, so a
+  // failure here is not the update's: the table stays on attribute_kernel
+  // (no partitions) and the update goes on to the workers, which must get
+  // the same table (a half-applied update would leave them on the old one).
+  if (build_partitions(h, keys, entry_off, nb_keys, chain, entry_ids) != NMG_OK) {
+    (void)hipGetLastError();
     free_route_table(h);
-    return rc;
   }
   for (nmg_engine* w : h->workers) {  // multi-GPU: the table on every device
     rc = nmg_update_objects(w, keys, entry_off, nb_keys, entry_ids, objects);
@@ -3060,8 +3074,15 @@ extern "C" int nmg_sparse_export(nmg_engine* h, uint64_t* keys, uint32_t* counts
   int rc = sparse_download(h, k, v);
   if (rc) return rc;
   if ((int64_t)k.size() != n) return fail(h, NMG_ERR_INVALID, "sparse count mismatch");
-  memcpy(keys, k.data(), n * 8);
-  memcpy(counts, v.data(), n * 4);
+  // in key order (the device compaction reserves its output slots per wave
+  // with an atomic, so its order varies from run to run; keys are unique)
+  std::vector<uint32_t> ord(k.size());
+  for (uint32_t i = 0; i < (uint32_t)ord.size(); i++) ord[i] = i;
+  std::sort(ord.begin(), ord.end(), [&](uint32_t a, uint32_t b) { return k[a] < k[b]; });
+  for (int64_t i = 0; i < n; i++) {
+    keys[i] = k[ord[i]];
+    counts[i] = v[ord[i]];
+  }
   return NMG_OK;
 }
 

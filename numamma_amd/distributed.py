@@ -100,7 +100,10 @@ class HistPacker:
         self.cells = eng.array_size(_lib.NMG_ARR_HIST32)
         self.cap = max(1024, int(self.cells * ovf_frac))
         self.u8 = torch.empty(max(self.cells, 4), dtype=torch.uint8, device=device)
-        self.ovf = torch.zeros(self.cap, dtype=torch.int64, device=device)
+        # (empty, not zeros: a fill on torch's stream is not ordered with
+        # nmg_hist_pack, which writes entries [0, n) on the engine's own
+        # non-blocking stream; merge() zeroes the padding [n, nmax) itself)
+        self.ovf = torch.empty(self.cap, dtype=torch.int64, device=device)
         self.n = torch.zeros(1, dtype=torch.int64, device=device)
         self.dense = None  # fallback: the u32 histogram (a list longer than cap)
 
@@ -192,7 +195,10 @@ def merge_engine(eng, dst: int = 0, group=None, device=None, packed_hist: bool =
             eng.import_array(which, t.data_ptr())
     n = eng.array_size(_lib.NMG_ARR_HIST32)
     if n and packed_hist:
-        HistPacker(eng, dev).merge(dst=dst, group=group)
+        hp = getattr(eng, "_hist_packer", None)  # one packer per engine, reused across merges
+        if hp is None or hp.cells != n:
+            hp = eng._hist_packer = HistPacker(eng, dev)
+        hp.merge(dst=dst, group=group)
     elif n:
         t = torch.empty(n, dtype=torch.int32, device=dev)
         eng.export_array(_lib.NMG_ARR_HIST32, t.data_ptr())

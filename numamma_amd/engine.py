@@ -126,15 +126,22 @@ class Engine:
         pointers computed in numpy (no per-buffer Python objects; the arena
         registered with register_host is read in place)."""
         arena = np.ascontiguousarray(arena, dtype=np.uint8)
-        offs = np.ascontiguousarray(offs, dtype=np.uint64)
-        lens = np.ascontiguousarray(lens, dtype=np.uint64)
+        # bounds in signed 64-bit before the conversion: a negative offset
+        # must not wrap to 2^64 - k and pass an unsigned check
+        o64 = np.asarray(offs, dtype=np.int64)
+        l64 = np.asarray(lens, dtype=np.int64)
+        if o64.shape != l64.shape:
+            raise ValueError("submit_arena: offs, lens, ranks and acc differ in length")
+        if o64.size and (int(o64.min()) < 0 or int(l64.min()) < 0 or bool(np.any(o64 > arena.nbytes))
+                         or bool(np.any(l64 > arena.nbytes - o64))):
+            raise ValueError("submit_arena: a buffer lies outside the arena")
+        offs = np.ascontiguousarray(o64, dtype=np.uint64)
+        lens = np.ascontiguousarray(l64, dtype=np.uint64)
         ranks = np.ascontiguousarray(ranks, dtype=np.uint32)
         acc = np.ascontiguousarray(acc, dtype=np.uint32)
         n = offs.shape[0]
         if not (lens.shape[0] == ranks.shape[0] == acc.shape[0] == n):
             raise ValueError("submit_arena: offs, lens, ranks and acc differ in length")
-        if n and int((offs + lens).max()) > arena.nbytes:
-            raise ValueError("submit_arena: a buffer ends past the arena")
         ptrs = offs + np.uint64(arena.ctypes.data)
         self._c(lib.nmg_submit_buffers(self.h, n, ptrs.ctypes.data_as(C.POINTER(C.c_void_p)),
                                        _ptr(lens, C.c_uint64), _ptr(ranks, C.c_uint32), _ptr(acc, C.c_uint32)))

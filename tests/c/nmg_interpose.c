@@ -30,7 +30,9 @@
  *    true (mem_intercept.h:68), so free() and realloc() take every pointer
  *    for one of theirs and read its header (mem_intercept.c:266-298,
  *    159-183) -- a block the interposer did not allocate (memalign & co,
- *    which it does not wrap either) hands a garbage pointer to libc.  With
+ *    which it does not wrap either) would hand a garbage pointer to libc;
+ *    this interposer stops at the first such block instead (exit code 86,
+ *    after its counters; see canary_ok).  With
  *    the check on (the default here, NumaMMa's --canary-check), free() passes
  *    such a block to libc, and realloc() aborts on it like the reference.
  *
@@ -146,10 +148,27 @@ static int ours(void *user) {
   return ((struct blk_head *)((unsigned char *)user - HEAD))->canary == CANARY;
 }
 
-/* CANARY_OK (mem_intercept.h:68): always true without the canary check */
+static void print_stats(void);
+
+/* CANARY_OK (mem_intercept.h:68): always true without the canary check, so
+ * NumaMMa would read this block's header from the bytes before it and hand
+ * libc a pointer taken from them.  The test interposer stops there instead:
+ * it counts the block, prints its counters and a line naming the pointer,
+ * and ends the process with NMG_INTERPOSE_FOREIGN_EXIT -- the outcome is
+ * asserted precisely and no process that holds the GPU frees garbage. */
+#define NMG_INTERPOSE_FOREIGN_EXIT 86
 static int canary_ok(void *user) {
   if (!canary_check) {
-    if (!ours(user)) __atomic_fetch_add(&n_foreign, 1, __ATOMIC_RELAXED); /* (counted, then trusted) */
+    if (!ours(user)) {
+      char line[160];
+      int n;
+      __atomic_fetch_add(&n_foreign, 1, __ATOMIC_RELAXED);
+      n = snprintf(line, sizeof line,
+                   "nmg_interpose: foreign block %p under canary_check=0 (its header would be trusted)\n", user);
+      if (n > 0) (void)!write(2, line, (size_t)n);
+      print_stats();
+      _exit(NMG_INTERPOSE_FOREIGN_EXIT);
+    }
     return 1;
   }
   return ours(user);
@@ -347,7 +366,9 @@ int pthread_create(pthread_t *th, const pthread_attr_t *attr, void *(*fn)(void *
   return real_pthread_create(th, attr, thread_start, t);
 }
 
-__attribute__((destructor)) static void report(void) {
+__attribute__((destructor)) static void report(void) { print_stats(); }
+
+static void print_stats(void) {
   char line[256];
   int n = snprintf(line, sizeof line,
                    "nmg_interpose: {\"recorded\": %lu, \"freed\": %lu, \"foreign_frees\": %lu, \"hand_made\": %lu, "

@@ -106,12 +106,18 @@ def test_internal_flag_bits_rejected(monkeypatch):
 
 
 def test_multi_gpu_without_abi_version_rejected(monkeypatch):
-    """nb_gpus > 1 is used only with abi_version = NMG_OPTIONS_ABI; without it
-    nmg_create fails instead of building a silent one-GPU engine."""
+    """nb_gpus > 1 is used only with abi_version = NMG_OPTIONS_ABI.  A caller
+    that declares the v2 fields (nmg_create_ex with the full struct size)
+    fails without it instead of building a silent one-GPU engine; nmg_create,
+    which a first-version binary may call with 32 bytes of struct, ignores
+    nb_gpus / devices without the ABI word (stray bytes past that struct)."""
     devs = (C.c_int32 * 2)(0, 1)
-    assert _create(_opts(nb_gpus=2, devices=devs)) == -1
-    assert _create(_opts(nb_gpus=2, abi_version=0x4E4D4701, devices=devs)) == -1
-    assert _create(_opts(nb_gpus=1)) in (0, -2)  # one GPU: nothing to gate
+    full = C.sizeof(_lib.nmg_options)
+    assert _create(_opts(nb_gpus=2, devices=devs), full) == -1
+    assert _create(_opts(nb_gpus=2, abi_version=0x4E4D4701, devices=devs), full) == -1
+    assert _create(_opts(nb_gpus=2, devices=devs)) in (0, -2)  # nmg_create: one GPU, as in version 1
+    assert _create(_opts(nb_gpus=0x7fffffff, abi_version=0x12345678)) in (0, -2)
+    assert _create(_opts(nb_gpus=1), full) in (0, -2)  # one GPU: nothing to gate
 
 
 def test_create_ex_reads_only_the_first_struct_version(tmp_path):

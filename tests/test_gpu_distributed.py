@@ -142,6 +142,7 @@ def test_hist_pack_round_trip(threshold, threads):
     ref = before.cpu().numpy().view(np.uint32)
     u8 = torch.empty(cells, dtype=torch.uint8, device=dev)
     ovf = torch.zeros(cells, dtype=torch.int64, device=dev)
+    torch.cuda.synchronize(dev)  # (the fill is on torch's stream; hist_pack writes on the engine's)
     n = eng.hist_pack(threshold, u8.data_ptr(), ovf.data_ptr(), cells)
     assert n == int((ref > threshold).sum())
     b = u8.cpu().numpy()

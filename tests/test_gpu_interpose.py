@@ -92,14 +92,22 @@ def test_bridge_without_canary_check(tmp_path):
     _compare(d, "o", "e")
 
 
+FOREIGN_EXIT = 86  # NMG_INTERPOSE_FOREIGN_EXIT (tests/c/nmg_interpose.c)
+
+
 def test_in_process_needs_canary_check(tmp_path):
-    """The engine in-process under canary_check = 0: the HIP runtime's first
-    free of a block the interposer did not allocate hands libc a pointer
-    read from garbage, and the process dies (the outcome INTEGRATION.md
-    section 2 states: in-process only with --canary-check)."""
+    """The engine in-process under canary_check = 0: the HIP runtime frees a
+    block the interposer did not allocate, whose header NumaMMa would trust
+    (the outcome INTEGRATION.md section 2 states: in-process only with
+    --canary-check).  The test interposer stops at that free, before libc
+    sees the bogus pointer, with its own exit code and counters: any other
+    failure (a missing binary, a HIP init error) fails this test."""
     d = str(tmp_path)
     path = _replay(d, 85)
     r = _run(d, [os.path.join(BIN, "nmg_c99_host"), path, os.path.join(d, "e"), os.path.join(d, "e.txt")],
              NMG_HOST_PROTECT="1", NMG_INTERPOSE_CANARY_CHECK="0")
     print("returncode", r.returncode, r.stderr[-500:])
-    assert r.returncode != 0
+    assert r.returncode == FOREIGN_EXIT, r.stderr[-3000:]
+    assert "foreign block" in r.stderr
+    st = interposer_stats(r.stderr)
+    assert st["foreign_frees"] >= 1

@@ -242,6 +242,9 @@ def test_two_shard_merge_matches_single(tmp_path):
         torch.cuda.synchronize()
         engines[0].import_array(which, m.data_ptr())
     parts = [e.sparse_export() for e in engines]
+    for k, _ in parts:  # (export order: ascending keys, reproducible)
+        assert np.all(k[1:] > k[:-1])
+    assert all(np.array_equal(a[0], b[0]) for a, b in zip(parts, [e.sparse_export() for e in engines]))
     engines[0].sparse_import(*merge_sparse(parts))
     cs = [e.buffer_counts() for e in engines]
     engines[0].set_buffer_counts(np.concatenate([c[0] for c in cs]), np.concatenate([c[1] for c in cs]),
@@ -533,6 +536,10 @@ def test_register_host_api(tmp_path):
                 eng.submit_arena(arena, offs, lens, ranks[:-1], accs)
             with pytest.raises(ValueError):
                 eng.submit_arena(arena[:offs[-1]], offs, lens, ranks, accs)  # past the arena
+            neg = np.asarray(offs, dtype=np.int64).copy()
+            neg[0] = -16  # (wraps to 2^64 - 16 unsigned: before the arena)
+            with pytest.raises(ValueError):
+                eng.submit_arena(arena, neg, lens, ranks, accs)
             eng.submit_arena(arena, offs, lens, ranks, accs)
         else:
             eng.submit_buffers(views)
