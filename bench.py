@@ -356,8 +356,7 @@ def result_line(args, w, world, steps, ms_per_step, value, attr_ms, total_ms, ph
     traffic, pmc, traffic_src = load_traffic(w.name)
     routed = rest_ms > 0.0  # the partition-first path ran (tables > 1023 keys)
     kernels = {}
-    # the route pass: route2_kernel, or route_kernel under the internal switch 0x20000000
-    route = "route_kernel" if int(os.environ.get("NMG_BENCH_DEBUG_FLAGS", "0"), 0) & 0x20000000 else "route2_kernel"
+    route = "route2_kernel"  # the route pass
     if routed:
         # the route pass reads every 40 B record and writes a 16 B compact
         # record per sample (nmg_route.h XLayout); the local pass reads them back

@@ -7,7 +7,7 @@
 // HBM lines per sample on a GPU.  This path first routes the samples by
 // address range, then attributes each range with its slice of the table in
 // LDS:
-//   1. route_kernel   streams the buffers in analysis order (the byte cursor of
+//   1. route2_kernel  streams the buffers in analysis order (the byte cursor of
 //                     __analyze_buffer, mem_sampling.c:815-927), counts the
 //                     SAMPLEs per buffer, and appends a 16 B compact record of
 //                     every SAMPLE to a chunk of its partition (partition = a run of
@@ -56,8 +56,6 @@ constexpr uint32_t kPartSlots = 1024;      // per-partition table stride
 constexpr uint32_t kPartDir = 1024;        // directory slots per partition (radix over its key span)
 constexpr uint32_t kPartEntries = 1536;    // entries per partition (LDS object counters)
 constexpr uint32_t kPartCells = 28672;     // u16 page cells per partition: nb_threads x cell span
-constexpr uint32_t kRouteWindows = 4;      // windows per LDS sort batch of the route pass
-constexpr uint32_t kRouteBatch = kRouteWindows * kWG;
 constexpr uint32_t kItemChunks = 1023;     // chunks per work item: < 2^16 records, so u16 page cells
                                            // and the packed object counters cannot overflow
 static_assert(kItemChunks * kChunk < 65536u, "u16 page cells per item");
@@ -72,22 +70,22 @@ constexpr uint32_t kDbgTinyPool = 0x20000; // route pass: private pools of 2 chu
 // ablation switches (tools/ablate.py; results are wrong with them)
 constexpr uint32_t kDbgTinyOvf = 0x80000;  // route pass: an overflow list of 64 records, the rest attributed directly
                                            // (tests, with kDbgTinyPool)
-constexpr uint32_t kDbgRouteNoWrite = 0x100000;  // route pass: batches sorted in LDS, no chunk stores
-constexpr uint32_t kDbgRouteNoBatch = 0x200000;  // route pass: no batch sort or stores at all
+constexpr uint32_t kDbgLapNoWait = 0x100000;   // route pass: a partition's LDS line is given up at the first
+                                                // record whose line is not the lap (tests: the given-up path)
 constexpr uint32_t kDbgLocalNoWork = 0x400000;   // local pass: chunk loads only
 constexpr uint32_t kDbgRouteTiming = 0x800000;   // route pass: per-wave phase cycles in Params::dbg
 constexpr uint32_t kDbgLocalNoObj = 0x1000000;   // local pass: no object counters / first ordinals
 constexpr uint32_t kDbgLocalNoPage = 0x2000000;  // local pass: no page cells
 constexpr uint32_t kDbgLocalNoGlobal = 0x4000000;  // local pass: no global counters
 constexpr uint32_t kDbgLocalNoSearch = 0x8000000;  // local pass: no lookup (nothing matches)
-constexpr uint32_t kDbgRouteV1 = 0x20000000;      // route pass: route_kernel (one workgroup-wide stream, batch
-                                                  // sort) instead of route2_kernel (A/B and tests)
+constexpr uint32_t kDbgNoLines = 0x20000000;      // route pass: no LDS line stage (every record stored to its
+                                                  // slot; tests and A/B)
 constexpr uint32_t kDbgLocalAtomics = 0x80000000u;  // local pass: every flush through atomics (A/B)
 constexpr uint32_t kDbgLocalTiming = 0x10000000;  // local pass: per-wave phase cycles in Params::dbg
                                                    // (wait, global, search, match, object, page per chunk;
                                                    // dequeue, setup, flush per item; chunks, items)
-constexpr int kRouteTimingWords = 12;            // wait+barrier, issue, global, search, rank, scan, alloc+stage, write,
-                                                 // state, windows, batches, -
+constexpr int kRouteTimingWords = 12;            // wait, check+loads, global, search, encode, claim+store, -, -,
+                                                 // -, windows, -, -
 
 // One partition: keys [k0, k0 + nk), entries [e0, e0 + ne) (entry ids of the
 // offline table are table positions, so a key range owns an id range), dense

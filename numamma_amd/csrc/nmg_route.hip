@@ -179,62 +179,12 @@ struct RDesc {
   __device__ __forceinline__ uint32_t access() const { return ta >> 16; }
 };
 
-// A lane's stride slot in window (cur of d0) [+ head of d1]: unlike
-// attribute_kernel's windows, d1 may belong to another stream (the route
-// pass keeps per-lane stream state), so windows stay full across buffer ends.
-struct RWin {
-  uint32_t pos;     // slot offset within its buffer
-  uint32_t n0, n1;  // slots in d0 / in d1 (uniform)
-  bool in1;
-  bool cand;
-};
-
-__device__ __forceinline__ RWin rwin_lane(int tid, uint32_t cur, const RDesc& d0, const RDesc& d1, bool has1) {
-  RWin w;
-  const uint32_t left = d0.len - cur;
-  w.n0 = min(left / kRecBytes + (left % kRecBytes != 0), (uint32_t)kWG);
-  w.n1 = 0;
-  if (has1 && w.n0 < (uint32_t)kWG) w.n1 = min(d1.len / kRecBytes + (d1.len % kRecBytes != 0), (uint32_t)kWG - w.n0);
-  w.in1 = (uint32_t)tid >= w.n0;
-  w.cand = (uint32_t)tid < w.n0 + w.n1;
-  w.pos = w.in1 ? (uint32_t(tid) - w.n0) * kRecBytes : cur + uint32_t(tid) * kRecBytes;
-  return w;
-}
-
-__device__ __forceinline__ void rload_slot(const uint8_t* data, const RWin& w, const RDesc& d0, const RDesc& d1,
-                                           RawRec& r) {
-  const uint64_t off = w.in1 ? d1.offset : d0.offset;
-  const uint32_t len = w.cand ? (w.in1 ? d1.len : d0.len) : 0;
-  load_rec(data + off, w.pos, len, r);
-}
-
-// The same loads without a branch: every lane issues its three loads (a lane
-// past its buffer reads the window's first record slot instead and gets
-// zeros), so that the number of memory ops per window is fixed and the
-// compiler's wait for a window's records can leave the next window's loads in
-// flight (route_kernel).
-__device__ __forceinline__ void rload_slot_nb(const uint8_t* data, const RWin& w, const RDesc& d0,
-                                              const RDesc& d1, RawRec& r) {
-  const uint64_t off = w.in1 ? d1.offset : d0.offset;
-  const uint32_t len = w.cand ? (w.in1 ? d1.len : d0.len) : 0;
-  const bool ok = uint64_t(w.pos) + kRecBytes <= len;
-  const uint64_t pos = ok ? w.pos : 0u;
-  const uint8_t* q = data + (ok ? off : d0.offset) + pos;
-  const uint32_t odd = uint32_t(pos >> 3) & 1;
-  const uint4 x = *reinterpret_cast<const uint4*>(q + (odd ? 8 : 0));
-  const uint4 y = *reinterpret_cast<const uint4*>(q + (odd ? 24 : 16));
-  const uint2 z = *reinterpret_cast<const uint2*>(q + (odd ? 0 : 32));
-  r.x = ok ? x : make_uint4(0, 0, 0, 0);
-  r.y = ok ? y : make_uint4(0, 0, 0, 0);
-  r.z = ok ? z : make_uint2(0, 0);
-}
-
 // update_counters(global_counters, ...) (mem_sampling.c:517-592) of both
 // access types in one per-lane accumulator, without a branch on the access:
 // counts of reads in the low and writes in the high 16 bits of a word,
 // weights summed per access.  The hit buckets of the first kDualGroups level
 // groups (L1, L2, L3, LFB, local RAM: the common PEBS levels) live here; the
-// other buckets, N/A... see dual_count.  Drained at least every
+// other buckets, N/A... see route_count.  Drained at least every
 // kDrainWindows records per lane (u16 counts; weights < 2^23, 256 x 2^23 <
 // 2^31).
 constexpr int kDualGroups = 5;
@@ -254,59 +204,10 @@ __device__ __forceinline__ void dual_clear(DualAcc& a) {
   a.tw[0] = a.tw[1] = 0;
 }
 
-// one SAMPLE of access `acc`: registers for the common buckets and
-// weights < 2^23; LDS (sums [2][kGlobalSums], mins / maxs [2][18]) for the rest
-__device__ __forceinline__ void dual_count(DualAcc& a, unsigned long long (*sums)[kGlobalSums],
-                                           unsigned long long (*mins)[18], unsigned long long (*maxs)[18],
-                                           uint32_t acc, uint32_t lvl, uint64_t w) {
-  const uint32_t bm = bucket_mask(lvl);
-  if (w < kLaneMaxWeight) {
-    const uint32_t w32 = (uint32_t)w, one = 1u << (16 * acc);
-    const uint32_t wr = acc ? 0u : w32, ww = acc ? w32 : 0u;
-    a.tc += one;
-    a.na += (lvl & LVL_NA) ? one : 0u;
-    a.tw[0] += wr;
-    a.tw[1] += ww;
-#pragma unroll
-    for (int g = 0; g < kDualGroups; g++) {
-      const bool in = (bm >> g) & 1;
-      a.cnt[g] += in ? one : 0u;
-      a.sum[0][g] += in ? wr : 0u;
-      a.sum[1][g] += in ? ww : 0u;
-    }
-    for (uint32_t m = bm >> kDualGroups; m; m &= m - 1) {  // rarer hit buckets, miss buckets
-      const uint32_t b = kDualGroups + (uint32_t)__builtin_ctz(m);
-      atomicAdd(&sums[acc][3 + 2 * b], 1ull);
-      if (w) atomicAdd(&sums[acc][4 + 2 * b], (unsigned long long)w);
-    }
-  } else {  // weights >= 2^23 cycles: straight to the LDS counters
-    atomicAdd(&sums[acc][0], 1ull);
-    atomicAdd(&sums[acc][1], (unsigned long long)w);
-    if (lvl & LVL_NA) atomicAdd(&sums[acc][2], 1ull);
-    for (uint32_t m = bm; m; m &= m - 1) {
-      const uint32_t b = (uint32_t)__builtin_ctz(m);
-      atomicAdd(&sums[acc][3 + 2 * b], 1ull);
-      atomicAdd(&sums[acc][4 + 2 * b], (unsigned long long)w);
-    }
-  }
-  // min / max only move monotonically: read first, atomic only on improvement
-  // (the first bucket's two reads issued together: one LDS round trip)
-  if (bm) {
-    const uint32_t b = (uint32_t)__builtin_ctz(bm);
-    const unsigned long long mn = mins[acc][b], mx = maxs[acc][b];
-    if (w < mn) atomicMin(&mins[acc][b], (unsigned long long)w);
-    if (w > mx) atomicMax(&maxs[acc][b], (unsigned long long)w);
-    for (uint32_t m = bm & (bm - 1); m; m &= m - 1) {  // (several level groups: rare)
-      const uint32_t b2 = (uint32_t)__builtin_ctz(m);
-      if (w < mins[acc][b2]) atomicMin(&mins[acc][b2], (unsigned long long)w);
-      if (w > maxs[acc][b2]) atomicMax(&maxs[acc][b2], (unsigned long long)w);
-    }
-  }
-}
-
-// dual_count for the route pass: the same register buckets, and every
-// minimum / maximum an LDS atomic that returns nothing (no round trip per
-// record; the route pass hides their LDS time behind its memory waits)
+// update_counters for the route pass: register buckets for the common
+// levels, LDS for the rest; READ_FIRST: a minimum / maximum is read first
+// and updated by an LDS atomic only when the record moves it, otherwise
+// every minimum / maximum is an LDS atomic that returns nothing
 template <bool READ_FIRST = false>
 __device__ __forceinline__ void route_count(DualAcc& a, unsigned long long (*sums)[kGlobalSums],
                                             unsigned long long (*mins)[18], unsigned long long (*maxs)[18],
@@ -341,7 +242,7 @@ __device__ __forceinline__ void route_count(DualAcc& a, unsigned long long (*sum
       atomicAdd(&sums[acc][4 + 2 * b], (unsigned long long)w);
     }
   }
-  if (READ_FIRST) {  // (dual_count's form: an atomic only when the record moves the bound)
+  if (READ_FIRST) {  // (an atomic only when the record moves the bound)
     if (bm) {
       const uint32_t b = (uint32_t)__builtin_ctz(bm);
       const unsigned long long mn = mins[acc][b], mx = maxs[acc][b];
@@ -405,164 +306,6 @@ __device__ __forceinline__ void rt_stamp(RTimer& t, int i) {
   }
 }
 
-// A window's record, held in registers from its processing until the next
-// window's barrier, then stored to its staging slot (so that the stores never
-// race with the delayed write phase of the previous batch, which reads the
-// staging area before that barrier)
-struct Held {
-  uint4 a;         // compact record
-  uint32_t q;      // partition | batch rank << 11, or kNoChunk (no record)
-};
-
-// The route pass's LDS state shared by the batch helpers.  Records are
-// staged unsorted, window b of the batch at slots [b * kWG, (b + 1) * kWG)
-// (lane-contiguous: conflict-free stores); the sort writes only a 16-bit
-// permutation, and the write phase gathers through it.
-struct RouteLds {
-  uint32_t* hist;     // [P] records of each partition in the batch (rank counters)
-  uint16_t* start;    // [P] first sorted position of each partition's run
-  uint32_t* cur;      // [2][kMaxParts + 1] open chunk id << 7 | fill, double-buffered by batch parity
-  uint32_t* nb;       // [P] first new chunk of the batch (kNoChunk: pool exhausted)
-  uint4* a16;         // [kRouteBatch] staging slot: compact record
-  const uint64_t* pb; // [P] partition starts (the overflow list keeps a record's)
-  uint32_t* uq;       // [kRouteBatch] partition | rank << 11, kNoChunk = empty slot
-  uint16_t* perm;     // [kRouteBatch] sorted position -> staging slot
-  uint32_t* wsum;     // [16] per-wave scan totals
-  uint32_t* misc;     // [0] records in the batch, [1] chunks taken, [2] first chunk never handed out
-};
-
-template <uint32_t WG = kWG>
-__device__ __forceinline__ void route_stage(const RouteLds& L, const Held& h, uint32_t b, int tid) {
-  const uint32_t slot = b * WG + (uint32_t)tid;
-  L.uq[slot] = h.q;
-  if (h.q != kNoChunk) L.a16[slot] = h.a;
-}
-
-// Sort batch `batch` (windows [0, nwin) staged) by partition -- the
-// permutation only -- and take chunks for the partitions that outgrow their
-// open chunk: three barriers (after the batch's ranks and stores, after the
-// scan, after the permutation).  Open-chunk state: batch b reads cur[b & 1]
-// and writes cur[(b + 1) & 1].
-template <bool TIMING>
-__device__ __forceinline__ void route_sort_batch(RTimer& rt, const RouteParams& rp, int tid, const RouteLds& L,
-                                                 uint32_t batch, uint32_t nwin, uint32_t c0, uint32_t cap) {
-  const uint32_t P = rp.nparts;
-  const int lane = tid & 63, wave = tid >> 6;
-  const uint32_t* cur_in = L.cur + (batch & 1) * (kMaxParts + 1);
-  uint32_t* cur_out = L.cur + ((batch + 1) & 1) * (kMaxParts + 1);
-  lds_sync();  // every rank and staging store of the batch done
-  // exclusive scan of the per-partition counts (two per thread, DPP within a wave)
-  const uint32_t i0 = 2 * (uint32_t)tid;
-  const uint32_t v0 = i0 < P ? L.hist[i0] : 0u, v1 = i0 + 1 < P ? L.hist[i0 + 1] : 0u;
-  const uint32_t s = v0 + v1;
-  const uint32_t inc = wave_incl_scan_u32(s);
-  if (lane == 63) L.wsum[wave] = inc;
-  lds_sync();
-  uint32_t wb = 0;
-  {
-    const uint4* ws = reinterpret_cast<const uint4*>(L.wsum);
-#pragma unroll
-    for (int k = 0; k < (int)(kWG / 64 / 4); k++) {
-      const uint4 x = ws[k];
-      wb += (4 * k + 0 < wave ? x.x : 0u) + (4 * k + 1 < wave ? x.y : 0u) + (4 * k + 2 < wave ? x.z : 0u) +
-            (4 * k + 3 < wave ? x.w : 0u);
-    }
-  }
-  const uint32_t ex = wb + inc - s;
-  rt_stamp<TIMING>(rt, 5);
-  // chunks for the partitions that outgrow their open chunk (private pool:
-  // workgroup-local atomics only), the next open-chunk state, counts cleared
-  for (uint32_t k = 0; k < 2; k++) {
-    const uint32_t q = i0 + k;
-    if (q >= P) break;
-    const uint32_t n = k ? v1 : v0;
-    L.start[q] = ex + (k ? v0 : 0u);
-    const uint32_t cur = cur_in[q];
-    if (!n) {
-      cur_out[q] = cur;
-      continue;
-    }
-    L.hist[q] = 0;
-    const uint32_t fill = cur & 127u, tot = fill + n;
-    if (tot <= kChunk) {
-      cur_out[q] = (cur & ~127u) | tot;
-      continue;
-    }
-    const uint32_t nn = (tot - kChunk + kChunk - 1) / kChunk;
-    const uint32_t base = atomicAdd(&L.misc[1], nn);
-    if (base + nn > cap) {
-      L.nb[q] = kNoChunk;  // pool exhausted: this batch's overflow of q goes to the overflow list
-      atomicMin(&L.misc[2], base);  // chunks from here on were never handed out
-      cur_out[q] = (cur & ~127u) | kChunk;
-      continue;
-    }
-    L.nb[q] = c0 + base;
-    for (uint32_t j = 0; j < nn; j++) rp.cmeta[c0 + base + j] = q | (kChunk << 24);
-    cur_out[q] = ((c0 + base + nn - 1) << 7) | (tot - kChunk - kChunk * (nn - 1));
-  }
-  if (tid == kWG - 1) L.misc[0] = wb + inc;  // records in the batch
-  lds_sync();
-  // the permutation: sorted position of every staged record (the reads of
-  // the batch's windows issued together)
-  uint32_t e[kRouteWindows], sp[kRouteWindows];
-#pragma unroll
-  for (uint32_t b = 0; b < kRouteWindows; b++) e[b] = b < nwin ? L.uq[b * kWG + (uint32_t)tid] : kNoChunk;
-#pragma unroll
-  for (uint32_t b = 0; b < kRouteWindows; b++) sp[b] = e[b] != kNoChunk ? L.start[e[b] & 2047u] : 0u;
-#pragma unroll
-  for (uint32_t b = 0; b < kRouteWindows; b++)
-    if (e[b] != kNoChunk) L.perm[sp[b] + (e[b] >> 11)] = (uint16_t)(b * kWG + (uint32_t)tid);
-  lds_sync();
-  rt_stamp<TIMING>(rt, 6);
-}
-
-// Each partition's run of sorted batch `batch` to its chunks: contiguous
-// slots, coalesced by run.  Run right after the next window's barrier and
-// before its loads are issued: a window waits for its loads with
-// vmcnt(0), which counts stores too, so stores issued behind the loads would
-// make the window wait for them.  (The staging slots it reads are rewritten
-// only after the next window's barrier.)
-template <bool TIMING>
-__device__ __forceinline__ void route_write_batch(RTimer& rt, const RouteParams& rp, int tid, const RouteLds& L,
-                                                  uint32_t batch) {
-  const Params& p = rp.p;
-  const uint32_t* cur_in = L.cur + (batch & 1) * (kMaxParts + 1);
-  const uint32_t total = L.misc[0];
-  for (uint32_t j = tid; j < total; j += kWG) {
-    const uint32_t src = L.perm[j];
-    const uint32_t q = L.uq[src] & 2047u;
-    const uint4 a = L.a16[src];
-    const uint32_t cur = cur_in[q];
-    const uint32_t pos = (cur & 127u) + (j - L.start[q]);
-    uint32_t chunk, slot;
-    if (pos < kChunk) {
-      chunk = cur >> 7;
-      slot = pos;
-    } else {
-      const uint32_t nb = L.nb[q];
-      if (nb == kNoChunk) {  // pool exhausted: to the overflow list (overflow_kernel)
-        const uint32_t o = atomicAdd(rp.ovf_cnt, 1u);
-        if (o < rp.ovf_cap) {
-          rp.ovf16[o] = a;
-          rp.ovfx[o] = L.pb[q];
-        } else {  // (only SAMPLE records shorter than 40 B get here) attributed at once, like
-                  // overflow_kernel does, so the default path accepts what the single-pass kernel does
-          XRec xr = x_decode(rp.xl, L.pb[q], a);
-          if (xr.esc) x_resolve(xr, p.data, p.sbufs);
-          direct_attribute(p, xr.addr, xr.ts, xr.w, xr.th, xr.acc, 0, rp.seq0 + xr.g, xr.off, xr.g);
-        }
-        continue;
-      }
-      chunk = nb + (pos - kChunk) / kChunk;
-      slot = (pos - kChunk) % kChunk;
-    }
-    if (p.flags & kDbgRouteNoWrite) continue;
-    const uint64_t k = uint64_t(chunk) * kChunk + slot;
-    rp.rec16[k] = a;
-  }
-  rt_stamp<TIMING>(rt, 7);
-}
-
 // Descriptors of the workgroup's range staged in LDS (offset, len,
 // thread | access << 16): a buffer transition reads LDS instead of waiting on
 // a global load.  Ranges longer than kDescLds read the rest from global
@@ -591,374 +334,52 @@ __device__ __forceinline__ RDesc route_desc(const RouteParams& rp, const uint4* 
   return d;
 }
 
-template <bool TIMING>
-__global__ __launch_bounds__(kWG, 1) void route_kernel(RouteParams rp) {
-  __shared__ uint64_t s_pb[kMaxParts + 1];
-  __shared__ uint16_t s_pdir[kRouteDir];
-  __shared__ uint32_t s_hist[kMaxParts + 1], s_cur[2][kMaxParts + 1], s_nb[kMaxParts + 1];
-  __shared__ uint16_t s_start[kMaxParts + 1];
-  __shared__ uint4 s_desc[kDescLds];
-  __shared__ uint4 s_a16[kRouteBatch];
-  __shared__ uint32_t s_uq[kRouteBatch];
-  __shared__ uint16_t s_perm[kRouteBatch];
-  __shared__ uint32_t s_list[kMaxList];
-  __shared__ uint32_t s_flags[3], s_nlist, s_next, s_err, s_wsum[kWG / 64], s_misc[3];
-  // the global mem_counters of the records this workgroup routes
-  __shared__ unsigned long long s_gsums[2][kGlobalSums], s_gmins[2][18], s_gmaxs[2][18];
-
-  Params& p = rp.p;
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const uint32_t P = rp.nparts;
-  const uint32_t c0 = rp.chunk0[blockIdx.x];
-  const uint32_t cap = rp.chunk0[blockIdx.x + 1] - c0;
-  for (uint32_t i = tid; i < kMaxParts + 1; i += kWG) s_pb[i] = rp.pbounds[i];
-  for (uint32_t i = tid; i < kRouteDir; i += kWG) s_pdir[i] = rp.pdir[i];
-  for (uint32_t i = tid; i < P; i += kWG) {
-    s_hist[i] = 0;
-    s_cur[0][i] = kChunk;  // no open chunk (full)
-  }
-  const uint32_t r0 = p.ranges[blockIdx.x], r1 = p.ranges[blockIdx.x + 1];
-  for (uint32_t i = r0 + tid; i < r1 && i - r0 < kDescLds; i += kWG) {
-    const BufDesc d = p.sbufs[i];
-    s_desc[i - r0] = make_uint4((uint32_t)d.offset, (uint32_t)(d.offset >> 32), d.len, d.thread_rank | (d.access << 16));
-  }
-  const RouteLds L{s_hist, s_start, &s_cur[0][0], s_nb, s_a16, s_pb, s_uq, s_perm, s_wsum, s_misc};
-  if (tid < 3) s_flags[tid] = 0;
-  if (tid == 0) {
-    s_misc[1] = 0;
-    s_misc[2] = kNoChunk;
-  }
-  if (tid < (int)kGlobalSums) s_gsums[0][tid] = s_gsums[1][tid] = 0;
-  if (tid < 18) {
-    s_gmins[0][tid] = s_gmins[1][tid] = ~0ull;  // INIT_COUNTER (mem_analyzer.c:415-420)
-    s_gmaxs[0][tid] = s_gmaxs[1][tid] = 0;
-  }
-  DualAcc gacc;  // per-lane update_counters, drained every kDrainWindows windows
-  dual_clear(gacc);
-  uint32_t gwin = 0;
-  lds_sync();
-
-  uint32_t nbatches = 0;  // (its parity picks the open-chunk state array)
-  if (r0 < r1) {
-    // Two windows' records are in flight: this window's (A) and the next's
-    // (B), loaded where the next window starts if this one holds only whole
-    // 40 B records -- the fast path; a slow-path window reloads B.  The loop
-    // is unrolled by two (window(A, B), window(B, A)) so that no register of a
-    // load in flight is ever copied.  A window's own chunk stores go out
-    // before the loads two windows ahead, and its wait is a vmcnt that leaves
-    // the next window's loads in flight.
-    uint32_t idx = r0;
-    uint32_t cur = 0;  // byte cursor (cur_cpt, mem_sampling.c:836)
-    RDesc d0 = route_desc(rp, s_desc, r0, idx);
-    RDesc d1 = idx + 1 < r1 ? route_desc(rp, s_desc, r0, idx + 1) : d0;
-    bool has1 = idx + 1 < r1;
-    // descriptor i of the range, given those of the window at idx (LDS reads otherwise)
-    auto desc_at = [&](uint32_t i, uint32_t at, const RDesc& a0, const RDesc& a1) -> RDesc {
-      return i == at ? a0 : i == at + 1 ? a1 : route_desc(rp, s_desc, r0, i);
-    };
-    // the next window's start if a window at (i, c) holds only whole records
-    // (the fast path's cursor update below)
-    auto advance = [&](uint32_t i, uint32_t c, const RDesc& e0, const RDesc& e1, bool h1, uint32_t& ni,
-                       uint32_t& nc) {
-      const uint32_t left = e0.len - c;
-      const uint32_t n0 = min(left / kRecBytes + (left % kRecBytes != 0), (uint32_t)kWG);
-      const uint32_t n1 = (h1 && n0 < (uint32_t)kWG) ? min(e1.len / kRecBytes + (e1.len % kRecBytes != 0),
-                                                            (uint32_t)kWG - n0) : 0u;
-      ni = i;
-      if (n1) {
-        ni = i + 1;
-        nc = n1 * kRecBytes;
-        if (nc >= e1.len) {
-          ni = i + 2;
-          nc = 0;
-        }
-      } else {
-        nc = c + n0 * kRecBytes;
-        if (nc >= e0.len) {
-          ni = i + 1;
-          nc = 0;
-        }
-      }
-    };
-    RawRec ra, rb;
-    uint32_t pidx, pcur;  // where rb was loaded
-    {
-      rload_slot_nb(p.data, rwin_lane(tid, 0, d0, d1, has1), d0, d1, ra);
-      advance(idx, 0, d0, d1, has1, pidx, pcur);
-      const bool pin = pidx < r1;  // (always three loads per lane, as in the loop)
-      const RDesc e0 = pin ? desc_at(pidx, idx, d0, d1) : d0;
-      const RDesc e1 = pin && pidx + 1 < r1 ? desc_at(pidx + 1, idx, d0, d1) : e0;
-      rload_slot_nb(p.data, rwin_lane(tid, pin ? pcur : 0u, e0, e1, pin && pidx + 1 < r1), e0, e1, rb);
-    }
-    uint32_t win = 0, bwin = 0;
-    uint32_t ns0 = 0, ns1 = 0;  // per-buffer SAMPLE tallies: buffer idx, idx + 1
-    RTimer rt;
-#pragma unroll
-    for (int k = 0; k < 9; k++) rt.acc[k] = 0;
-    rt.last = TIMING ? stamp() : 0;
-    bool wpending = false;  // a sorted batch waits for its chunk stores
-
-    // one window: A holds its records, B the next window's (in flight);
-    // returns true after the range's last window
-    auto window = [&](RawRec& A, RawRec& B) -> bool {
-      const RWin wl = rwin_lane(tid, cur, d0, d1, has1);
-      const Rec r = decode_rec(A, wl.pos);
-      // ---- fast-path check: every 40 B stride slot holds a whole 40 B record
-      const uint32_t wlen = wl.in1 ? d1.len : d0.len;
-      const bool bad =
-          (cur & 7) != 0 || (wl.cand && (uint64_t(wl.pos) + kRecBytes > wlen || (r.hdr >> 48) != kRecBytes));
-      const uint64_t badm = __ballot(bad);
-      if (badm && lane == 0) atomicOr(&s_flags[win % 3], 1u);
-      lds_sync();
-      const uint32_t f = __builtin_amdgcn_readfirstlane(s_flags[win % 3]);
-      if (tid == 0) s_flags[(win + 2) % 3] = 0;
-      win++;
-      if (TIMING) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");  // (timing: this window's loads count as wait)
-      rt_stamp<TIMING>(rt, 0);
-      uint32_t nidx = idx;
-      uint32_t ncur;
-      Rec rec = r;
-      bool valid, rin1;
-      uint32_t roff;
-      if (!(f & 1)) {
-        valid = wl.cand && uint32_t(r.hdr) == kSampleType;
-        rin1 = wl.in1;
-        roff = wl.pos;
-        advance(idx, cur, d0, d1, has1, nidx, ncur);
-      } else {
-        // ---- slow path (buffer idx only), as attribute_kernel: wave 0
-        // follows the header chain (non-SAMPLE records skipped by size,
-        // size 0 / truncation / misalignment flagged), listing SAMPLE offsets
-        const uint8_t* base = p.data + d0.offset;
-        const uint64_t len = d0.len;
-        if (tid < 64) {
-          uint64_t q0 = cur;
-          uint32_t n = 0, err = 0;
-          const uint64_t lim = min(uint64_t(cur) + kWinBytes, len);
-          while (q0 < lim && n + 65 <= kMaxList) {
-            const uint64_t q = q0 + uint64_t(lane) * kRecBytes;
-            const uint64_t hdr = (q + 8 <= len) ? *reinterpret_cast<const uint64_t*>(base + q) : 0;
-            const bool reg = q < lim && q + kRecBytes <= len && (hdr >> 48) == kRecBytes;
-            const uint64_t rm = __ballot(reg);
-            const uint32_t run = ~rm ? (uint32_t)__builtin_ctzll(~rm) : 64u;
-            const bool smp = (uint32_t)lane < run && uint32_t(hdr) == kSampleType;
-            const uint64_t sm = __ballot(smp);
-            if (smp) s_list[n + (uint32_t)__popcll(sm & ((1ull << lane) - 1))] = (uint32_t)q;
-            n += (uint32_t)__popcll(sm);
-            q0 += uint64_t(run) * kRecBytes;
-            if (run == 64 || q0 >= lim) continue;
-            if (q0 + 8 > len) {
-              err = kErrTruncated;
-              break;
-            }
-            const uint64_t h = (uint64_t)__shfl(hdr, (int)run, 64);
-            const uint32_t size = uint32_t(h >> 48);
-            if (size == 0) {  // mem_sampling.c:857-860
-              err = kErrZeroSize;
-              break;
-            }
-            if (size & 7) {
-              err = kErrUnaligned;
-              break;
-            }
-            if (uint32_t(h) == kSampleType) {
-              if (q0 + kRecBytes > len || q0 + size > len) {
-                err = kErrTruncated;
-                break;
-              }
-              if (lane == 0) s_list[n] = (uint32_t)q0;
-              n++;
-            }
-            q0 += size;  // non-SAMPLE records are skipped by their size (:918)
-          }
-          if (lane == 0) {
-            if (err) set_error(p, rp.seq0 + d0.pad, (uint32_t)q0, err);
-            s_err = err;
-            s_nlist = n;
-            s_next = (uint32_t)min(q0, len);
-          }
-        }
-        lds_sync();
-        const uint32_t n = __builtin_amdgcn_readfirstlane(s_nlist);
-        const uint32_t serr = __builtin_amdgcn_readfirstlane(s_err);
-        ncur = serr ? (uint32_t)len : __builtin_amdgcn_readfirstlane(s_next);
-        if (ncur >= len) {
-          nidx = idx + 1;
-          ncur = 0;
-        }
-        valid = (uint32_t)tid < n;
-        roff = valid ? s_list[tid] : 0;
-        rin1 = false;
-        RawRec rr;
-        load_rec(base, roff, valid ? len : 0, rr);
-        rec = decode_rec(rr, roff);
-        vm_drain();
-      }
-
-      // ---- descriptors of the next window
-      const RDesc nd0 = nidx < r1 ? desc_at(nidx, idx, d0, d1) : d0;
-      const RDesc nd1 = nidx + 1 < r1 ? desc_at(nidx + 1, idx, d0, d1) : nd0;
-      const bool nhas1 = nidx + 1 < r1;
-      // ---- the previous batch's chunk stores (before any later load: see
-      // route_write_batch), then a barrier: every wave has gathered that
-      // batch from the staging slots this window's records go to
-      if (wpending) {
-        route_write_batch<TIMING>(rt, rp, tid, L, nbatches - 1);
-        wpending = false;
-        lds_sync();
-      }
-      // ---- the next window's loads again if this window was not what B
-      // assumed (slow path), and the loads of the window after it
-      if (nidx < r1 && (nidx != pidx || ncur != pcur)) {
-        rload_slot(p.data, rwin_lane(tid, ncur, nd0, nd1, nhas1), nd0, nd1, B);
-        vm_drain();  // (rare: keeps the waits on the common path exact)
-      }
-      uint32_t qidx = nidx, qcur = 0;
-      if (nidx < r1) advance(nidx, ncur, nd0, nd1, nhas1, qidx, qcur);
-      {  // (always three loads per lane: past the range's end they reread this window's buffer)
-        const bool qin = qidx < r1;
-        const RDesc e0 = !qin ? d0 : desc_at(qidx, nidx, nd0, nd1);
-        const RDesc e1 = qin && qidx + 1 < r1 ? desc_at(qidx + 1, nidx, nd0, nd1) : e0;
-        rload_slot_nb(p.data, rwin_lane(tid, qin ? qcur : 0u, e0, e1, qin && qidx + 1 < r1), e0, e1, A);
-      }
-
-      // ---- this window's record: update_counters(global_counters, sample)
-      // (mem_sampling.c:882: every SAMPLE, matched or not), its partition, its
-      // batch rank, its slot
-      rt_stamp<TIMING>(rt, 1);
-      const uint32_t acc_l = rin1 ? d1.access() : d0.access();
-      if (valid) route_count(gacc, s_gsums, s_gmins, s_gmaxs, acc_l, uint32_t(rec.dsrc >> 5) & 0x3fff, rec.w);
-      if (++gwin == kDrainWindows) {  // keep the per-lane u16 counts / u32 sums bounded
-        dual_drain(gacc, s_gsums, lane);
-        gwin = 0;
-      }
-      rt_stamp<TIMING>(rt, 2);
-      // partition = the last partition whose first key <= addr.  Below the
-      // first key ht_lower_key finds no node and nothing can match: such a
-      // sample has been counted (global and per-buffer counters) and goes no
-      // further.
-      const bool routed = valid && rec.addr >= rp.seg[0].start;
-      const uint32_t q = routed ? route_partition(rp, s_pb, s_pdir, rec.addr) : 0u;
-      const uint64_t pbq = routed ? s_pb[q] : 0ull;
-      if (TIMING) (void)__builtin_amdgcn_readfirstlane(__ballot(pbq != 0));  // (the search ends here)
-      rt_stamp<TIMING>(rt, 3);
-      Held hr;
-      hr.q = kNoChunk;
-      if (routed) {
-        const uint32_t rk = atomicAdd(&s_hist[q], 1u);
-        hr.q = q | (rk << 11);
-        const uint32_t g = rin1 ? d1.pad : d0.pad;
-        const uint32_t th = rin1 ? d1.thread_rank() : d0.thread_rank();
-        hr.a = x_encode(rp.xl, pbq, rec.addr, rec.ts, rec.w, g, roff, th, acc_l);
-      }
-      {
-        // per-buffer SAMPLE tallies (mem_sampling.c:921-926): lanes of this
-        // wave in buffer idx + 1 are tid >= n0
-        const uint64_t vm = __ballot(valid);
-        const uint32_t w0 = uint32_t(tid) & ~63u;
-        const uint64_t m1 = ((f & 1) || wl.n0 >= w0 + 64) ? 0ull : (wl.n0 <= w0 ? ~0ull : (~0ull << (wl.n0 - w0)));
-        ns0 += (uint32_t)__popcll(vm & ~m1);
-        ns1 += (uint32_t)__popcll(vm & m1);
-      }
-      if (nidx != idx) {
-        if (lane == 0) {
-          if (ns0) atomicAdd(p.bufcnt + d0.pad, ns0);
-          if (nidx == idx + 2 && ns1) atomicAdd(p.bufcnt + d1.pad, ns1);
-        }
-        ns0 = nidx == idx + 1 ? ns1 : 0;
-        ns1 = 0;
-      }
-      const bool last = nidx >= r1;
-      rt_stamp<TIMING>(rt, 4);
-      if (p.flags & kDbgRouteNoBatch) {  // (ablation) forget the records
-        if (++bwin == kRouteWindows || last) {
-          lds_sync();
-          for (uint32_t q = tid; q < P; q += kWG) s_hist[q] = 0;
-          bwin = 0;
-        }
-      } else {
-        route_stage(L, hr, bwin, tid);  // (its batch's staging slot: no wave reads it now)
-        if (++bwin == kRouteWindows || last) {
-          route_sort_batch<TIMING>(rt, rp, tid, L, nbatches, bwin, c0, cap);
-          bwin = 0;
-          nbatches++;
-          if (last) route_write_batch<TIMING>(rt, rp, tid, L, nbatches - 1);
-          else wpending = true;
-        }
-      }
-      idx = nidx;
-      cur = ncur;
-      d0 = nd0;
-      d1 = nd1;
-      has1 = nhas1;
-      pidx = qidx;
-      pcur = qcur;
-      return last;
-    };
-    while (true) {
-      if (window(ra, rb)) break;
-      if (window(rb, ra)) break;
-    }
-    if (TIMING && lane == 0) {
-      unsigned long long* o = p.dbg + (uint64_t(blockIdx.x) * (kWG / 64) + tid / 64) * kRouteTimingWords;
-      for (int k = 0; k < 9; k++) o[k] = rt.acc[k];
-      o[9] = win;
-      o[10] = nbatches;
-    }
-  }
-  dual_drain(gacc, s_gsums, lane);
-  lds_sync();
-#pragma unroll
-  for (uint32_t a = 0; a < 2; a++) {  // the global mem_counters of both access types
-    if (tid < (int)kGlobalSums && s_gsums[a][tid])
-      atomicAdd(reinterpret_cast<unsigned long long*>(p.sum64 + gsum_index(a, tid)), s_gsums[a][tid]);
-    if (tid < 18 && s_gsums[a][3 + 2 * tid]) {
-      atomicMin(reinterpret_cast<unsigned long long*>(p.min64 + a * 18 + tid), s_gmins[a][tid]);
-      atomicMax(reinterpret_cast<unsigned long long*>(p.max64 + a * 18 + tid), s_gmaxs[a][tid]);
-    }
-  }
-  // open chunks' fill, chunk counts per partition, pool use
-  for (uint32_t q = tid; q < P; q += kWG) {
-    const uint32_t cur = s_cur[nbatches & 1][q];
-    if ((cur & 127u) < kChunk) rp.cmeta[cur >> 7] = q | ((cur & 127u) << 24);
-  }
-  if (tid == 0) rp.used[blockIdx.x] = min(min(s_misc[1], cap), s_misc[2]);
-}
-
 // ---------------------------------------------------------------------------
-// pass 1 with per-wave record streams and no batches (route2_kernel, the
-// default; kDbgRouteV1 selects route_kernel).
+// pass 1: route2_kernel, per-wave record streams.
 //
-// route_kernel moves one workgroup-wide byte cursor: every window of 1024
-// stride slots ends in a barrier (the fast-path check), and the batch sort
-// adds four more per four windows.  Here each wave owns whole buffers,
-// dequeued from the workgroup's range through an LDS counter, and walks them
-// with its own cursor in windows of 64 stride slots (__analyze_buffer's byte
-// cursor, mem_sampling.c:836-926, per buffer as the reference does it): the
-// fast-path check is a ballot, the slow path (LOST / short / irregular
-// records) is the wave's own header walk, and the per-buffer SAMPLE tally is
-// the wave's.  Nothing synchronises the workgroup between its first and last
-// barrier: each record claims a slot of its partition's open chunk with one
-// LDS atomic and is stored from its registers in the window that read it
-// (the chunk protocol is at the claim).  The next window's loads stay in
-// flight across the window.
+// Each wave owns whole buffers, dequeued from the workgroup's range through
+// an LDS counter, and walks them with its own cursor in windows of 64 stride
+// slots (__analyze_buffer's byte cursor, mem_sampling.c:836-926, per buffer
+// as the reference does it): the fast-path check is a ballot, the slow path
+// (LOST / short / irregular records) is the wave's own header walk, and the
+// per-buffer SAMPLE tally is the wave's.  Nothing synchronises the workgroup
+// between its first and last barrier: each record claims a slot of its
+// partition's open chunk with one LDS atomic (the chunk protocol is at the
+// claim) and goes to that slot through the partition's LDS line (below).
+// The next window's loads stay in flight across the window.
+//
+// The line stage.  A record stored straight to its chunk slot is a 16 B
+// store of its own: a wave-instruction of such stores touches 64 lines,
+// which costs the CU ~10x the issue time of 64 B runs at a 2 GB footprint
+// (tools/micro/vmem.hip), and a cold partition's line leaves L2 partly
+// written.  So every partition has a 64 B line in LDS, the four slots of a
+// chunk line (chunk slots 4l .. 4l + 3): a record whose line is the one the
+// partition's LDS line serves (its lap) is written there, and the record
+// that completes the line (the fourth write) has it written out whole, four
+// lanes of its wave per line, sixteen lines per store instruction.  The lap
+// then moves to the partition's next line.  A record whose line is not yet
+// the lap (the previous line still filling) re-reads the lap a few times;
+// past that the partition's LDS line is given up for the launch ("broken"):
+// its later records go straight to their slots, and a line left incomplete
+// -- broken, or a partition's last line -- is written out, the slots it
+// holds, after the workgroup's last barrier.  Hot partitions, whose lines
+// fill faster than a line's round trip through LDS, break early and store
+// directly; the consecutive slots their records claim in one wave-instruction
+// make those stores runs already.
 
-// route2_kernel's workgroup: 12 waves (three per SIMD); the kernel fits 128
-// VGPRs, so 16 waves are an A/B away (NMG_R2WG=1024)
-#ifndef NMG_R2WG
-#define NMG_R2WG 768
-#endif
-constexpr uint32_t kR2WG = NMG_R2WG;
-#ifndef NMG_R2MMREAD
-#define NMG_R2MMREAD 1
-#endif
-// (A/B builds only: route2 without its global counters (1), with a hash in
-// place of the partition search (2), without the record stores (4), without
-// the chunk claims (8: every lane stores to a fixed slot of its workgroup's
-// pool); results are wrong, and 4 / 8 hand the local pass no chunk)
-#ifndef NMG_R2_ABL
-#define NMG_R2_ABL 0
+// route2_kernel's workgroup: 12 waves (three per SIMD)
+constexpr uint32_t kR2WG = 768;
+// line stage: partitions q < kLineParts have an LDS line
+constexpr uint32_t kLineParts = 1280;
+constexpr uint32_t kLapSpins = 3;  // lap re-reads before a partition's line is given up
+// line word: fill (3 bits) | slots held (4) | broken (1) | lap (12: chunk
+// line number, mod 4096, of the line served)
+constexpr uint32_t kLwMaskShift = 3, kLwBroken = 0x80u, kLwLapShift = 8, kLwLapMask = 4095;
+// a write into slot j: fill + 1, slot bit; the release after a full line's
+// write-out: lap + 1, fill - 4, slots - 0xf
+constexpr uint32_t kLwRelease = (1u << kLwLapShift) - 4u - (0xfu << kLwMaskShift);
+#ifndef NMG_R2_LINES
+#define NMG_R2_LINES 1
 #endif
 constexpr uint32_t kWaves = kR2WG / 64;
 constexpr uint32_t kWaveWinBytes = 64 * kRecBytes;  // one wave window: 64 stride slots
@@ -1091,6 +512,11 @@ __global__ __launch_bounds__(kR2WG, 1) void route2_kernel(RouteParams rp) {
   __shared__ uint32_t s_taken, s_bnext;
   __shared__ unsigned long long s_gsums[2][kGlobalSums], s_gmins[2][18], s_gmaxs[2][18];
   __shared__ SegL s_seg[kRouteSegs];
+  // the line stage: per partition a line of four compact records, its line
+  // word and its chunk line (pool slot / 4); per wave the lines it writes out
+  __shared__ uint4 s_line[NMG_R2_LINES ? kLineParts * 4 : 1];
+  __shared__ uint32_t s_lw[NMG_R2_LINES ? kLineParts : 1], s_ldst[NMG_R2_LINES ? kLineParts : 1];
+  __shared__ uint2 s_tab[kWaves][64];
 
   Params& p = rp.p;
   const int tid = threadIdx.x;
@@ -1109,6 +535,10 @@ __global__ __launch_bounds__(kR2WG, 1) void route2_kernel(RouteParams rp) {
   for (uint32_t i = tid; i < kMaxParts + 1; i += kR2WG) s_pb[i] = rp.pbounds[i];
   for (uint32_t i = tid; i < kRouteDir; i += kR2WG) s_pdir[i] = rp.pdir[i];
   for (uint32_t i = tid; i < P; i += kR2WG) s_state[i] = st_pack(kStNone, kStNone, 0, 2 * kChunk);
+  // the first line of a partition: slot 0 of generation 1's open chunk
+  const uint32_t nlp = NMG_R2_LINES && !(p.flags & kDbgNoLines) ? min(P, kLineParts) : 0u;
+  const uint32_t spins = (p.flags & kDbgLapNoWait) ? 0u : kLapSpins;
+  for (uint32_t i = tid; i < nlp; i += kR2WG) s_lw[i] = (kChunk / 4) << kLwLapShift;
   const uint32_t r0 = p.ranges[blockIdx.x], r1 = p.ranges[blockIdx.x + 1];
   for (uint32_t i = r0 + tid; i < r1 && i - r0 < kDescLds; i += kR2WG) {
     const BufDesc d = p.sbufs[i];
@@ -1306,8 +736,7 @@ __global__ __launch_bounds__(kR2WG, 1) void route2_kernel(RouteParams rp) {
       // slot, store
       rt_stamp<TIMING>(rt, 1);
       const uint32_t acc_l = dw.access();
-      if (valid && !(NMG_R2_ABL & 1))
-        route_count<NMG_R2MMREAD != 0>(gacc, s_gsums, s_gmins, s_gmaxs, acc_l, uint32_t(rec.dsrc >> 5) & 0x3fff, rec.w);
+      if (valid) route_count<true>(gacc, s_gsums, s_gmins, s_gmaxs, acc_l, uint32_t(rec.dsrc >> 5) & 0x3fff, rec.w);
       if (++gwin == kDrainWindows) {
         dual_drain(gacc, s_gsums, lane);
         gwin = 0;
@@ -1315,9 +744,7 @@ __global__ __launch_bounds__(kR2WG, 1) void route2_kernel(RouteParams rp) {
       rt_stamp<TIMING>(rt, 2);
       // below the first key ht_lower_key finds no node: counted, not routed
       const bool routed = valid && rec.addr >= first_start;
-      const uint32_t q = !routed ? 0u
-                         : (NMG_R2_ABL & 2) ? uint32_t(rec.addr >> 12) % P
-                                            : route_partition_l(s_seg, nseg, s_pb, s_pdir, rec.addr);
+      const uint32_t q = routed ? route_partition_l(s_seg, nseg, s_pb, s_pdir, rec.addr) : 0u;
       if (TIMING) (void)__builtin_amdgcn_readfirstlane(__ballot(q != 0));  // (the search ends here)
       rt_stamp<TIMING>(rt, 3);
       uint4 a = make_uint4(0, 0, 0, 0);
@@ -1330,10 +757,15 @@ __global__ __launch_bounds__(kR2WG, 1) void route2_kernel(RouteParams rp) {
       // ---- a slot in q's open chunks: one LDS atomic on the partition's
       // state (route2_claim).  No barrier: the waves run on their own streams.
       uint64_t dst = ~0ull;  // rec16 slot, or ~0: no slot (not routed / overflow list)
+      uint32_t lid = 0;      // the slot's chunk line number (mod 4096): the lap that serves it
       bool ovf = false;
+      const bool lined = NMG_R2_LINES && routed && q < nlp;
+      // (the line word read beside the claim: a lap can only move on once this
+      // record's own line is written, so a lap that equals the record's line
+      // here still does after the claim)
+      uint32_t lw = lined ? s_lw[q] : 0u;
       {
-        bool todo = routed && !(NMG_R2_ABL & 8), spin = false;
-        if (NMG_R2_ABL & 8) dst = routed ? uint64_t(c0) * kChunk + (uint32_t)tid % max(cap * kChunk, 1u) : ~0ull;
+        bool todo = routed, spin = false;
         uint32_t waitg = 0;
         while (__ballot(todo)) {
           if (todo) {
@@ -1344,22 +776,22 @@ __global__ __launch_bounds__(kR2WG, 1) void route2_kernel(RouteParams rp) {
                 const uint32_t c = f < kChunk ? cu : nx;
                 if (c == kStOvf) ovf = true;
                 else dst = uint64_t(c0 + c) * kChunk + (f & (kChunk - 1));
+                lid = ((g << 6) + f) >> 2;  // (slot f - 64 of the next chunk = generation g + 1's slot)
                 todo = false;
                 if (f == kChunk + kChunk / 2) {  // half of the next chunk claimed: open the one after it
                   const uint32_t n2 = route2_take(s_taken, capl);
-                  if (n2 != kStOvf && !(NMG_R2_ABL & 12)) rp.cmeta[c0 + n2] = q | (kChunk << 24);
+                  if (n2 != kStOvf) rp.cmeta[c0 + n2] = q | (kChunk << 24);
                   route2_advance(&s_state[q], g, n2, n2, false, old + 1);
                 }
               } else if (cu == kStNone && f == 2 * kChunk) {  // q's first claim: open two chunks
                 const uint32_t n1 = route2_take(s_taken, capl);
                 const uint32_t n2 = n1 == kStOvf ? kStOvf : route2_take(s_taken, capl);
-                if (!(NMG_R2_ABL & 12)) {
-                  if (n1 != kStOvf) rp.cmeta[c0 + n1] = q | (kChunk << 24);
-                  if (n2 != kStOvf) rp.cmeta[c0 + n2] = q | (kChunk << 24);
-                }
+                if (n1 != kStOvf) rp.cmeta[c0 + n1] = q | (kChunk << 24);
+                if (n2 != kStOvf) rp.cmeta[c0 + n2] = q | (kChunk << 24);
                 route2_advance(&s_state[q], g, n1, n2, true, old + 1);
                 if (n1 == kStOvf) ovf = true;
                 else dst = uint64_t(c0 + n1) * kChunk;
+                lid = (g + 1) << 4;  // slot 0 of generation g + 1
                 todo = false;
               } else {  // void claim (past the next chunk): wait for the next generation
                 spin = true;
@@ -1372,7 +804,51 @@ __global__ __launch_bounds__(kR2WG, 1) void route2_kernel(RouteParams rp) {
           }
         }
       }
-      if (dst != ~0ull && !(NMG_R2_ABL & 4)) rp.rec16[dst] = a;
+      // ---- the line stage (see the comment above kR2WG)
+      bool staged = false;
+      if (NMG_R2_LINES && __ballot(lined && dst != ~0ull)) {
+        lid &= kLwLapMask;
+        bool wait = lined && dst != ~0ull && ((lw >> kLwLapShift) & kLwLapMask) != lid && !(lw & kLwBroken);
+        for (uint32_t k = 0; k < spins && __ballot(wait); k++) {  // (the previous line still filling)
+          if (wait) {
+            lw = __hip_atomic_load(&s_lw[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            wait = ((lw >> kLwLapShift) & kLwLapMask) != lid && !(lw & kLwBroken);
+          }
+        }
+        staged = lined && dst != ~0ull && ((lw >> kLwLapShift) & kLwLapMask) == lid;
+        if (wait) atomicOr(&s_lw[q], kLwBroken);  // given up: q's later records go straight to their slots
+        bool done = false;
+        const uint32_t j = (uint32_t)dst & 3u;
+        if (staged) {
+          s_line[q * 4 + j] = a;
+          s_ldst[q] = (uint32_t)(dst >> 2);
+          // (the record before the count that may complete the line)
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+          const uint32_t o = atomicAdd(&s_lw[q], 1u + (1u << (kLwMaskShift + j)));
+          done = (o & 7u) == 3u;
+        }
+        const uint64_t dm = __ballot(done);
+        if (dm) {  // the completed lines written out: four lanes per line, 16 lines per store
+          if (done) s_tab[wave][__popcll(dm & ((1ull << lane) - 1))] = make_uint2(q, (uint32_t)(dst >> 2));
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+          const uint32_t nd = (uint32_t)__popcll(dm);
+          for (uint32_t j0 = 0; j0 < nd; j0 += 16) {
+            const uint32_t jj = j0 + ((uint32_t)lane >> 2);
+            if (jj < nd) {
+              const uint2 t = s_tab[wave][jj];
+              const uint4 v = s_line[t.x * 4 + (lane & 3)];
+              rp.rec16[uint64_t(t.y) * 4 + (lane & 3)] = v;
+              // (the line read by all four lanes -- one instruction, waited
+              // for by the store -- before its slots are handed to the next line)
+              __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+              if ((lane & 3) == 0) atomicAdd(&s_lw[t.x], kLwRelease);
+            }
+          }
+        }
+      }
+      if (dst != ~0ull && !staged) rp.rec16[dst] = a;
       if (__ballot(ovf)) {  // (rare) a workgroup's pool outgrown: SAMPLEs shorter than 40 B
         if (ovf) {
           const uint32_t o = atomicAdd(rp.ovf_cnt, 1u);
@@ -1418,11 +894,18 @@ __global__ __launch_bounds__(kR2WG, 1) void route2_kernel(RouteParams rp) {
   for (uint32_t q = tid; q < P; q += kR2WG) {
     const unsigned long long st = s_state[q];
     const uint32_t f = st_cnt(st), cu = st_cur(st), nx = st_next(st);
-    if (cu == kStNone || (NMG_R2_ABL & 12)) continue;
+    if (cu == kStNone) continue;
     if (cu != kStOvf) rp.cmeta[c0 + cu] = q | (min(f, kChunk) << 24);
     if (nx != kStOvf) rp.cmeta[c0 + nx] = q | ((f > kChunk ? f - kChunk : 0u) << 24);
+    // a line the stage still holds (the partition's last, or one a given-up
+    // lap left incomplete): the slots it holds
+    if (q < nlp) {
+      const uint32_t lw = s_lw[q];
+      for (uint32_t j = 0; j < 4; j++)
+        if ((lw & 7u) && ((lw >> (kLwMaskShift + j)) & 1u)) rp.rec16[uint64_t(s_ldst[q]) * 4 + j] = s_line[q * 4 + j];
+    }
   }
-  if (tid == 0) rp.used[blockIdx.x] = (NMG_R2_ABL & 12) ? 0u : min(s_taken, capl);
+  if (tid == 0) rp.used[blockIdx.x] = min(s_taken, capl);
 }
 
 // ---------------------------------------------------------------------------
@@ -2008,11 +1491,8 @@ __global__ __launch_bounds__(kWG) void found_kernel(FoundParams r) {
 // launchers
 
 hipError_t launch_route(uint32_t grid, hipStream_t s, const RouteParams& r) {
-  if (!(r.p.flags & kDbgRouteV1) && (r.p.flags & kDbgRouteTiming))
-    hipLaunchKernelGGL(route2_kernel<true>, dim3(grid), dim3(kR2WG), 0, s, r);
-  else if (!(r.p.flags & kDbgRouteV1)) hipLaunchKernelGGL(route2_kernel<false>, dim3(grid), dim3(kR2WG), 0, s, r);
-  else if (r.p.flags & kDbgRouteTiming) hipLaunchKernelGGL(route_kernel<true>, dim3(grid), dim3(kWG), 0, s, r);
-  else hipLaunchKernelGGL(route_kernel<false>, dim3(grid), dim3(kWG), 0, s, r);
+  if (r.p.flags & kDbgRouteTiming) hipLaunchKernelGGL(route2_kernel<true>, dim3(grid), dim3(kR2WG), 0, s, r);
+  else hipLaunchKernelGGL(route2_kernel<false>, dim3(grid), dim3(kR2WG), 0, s, r);
   return hipGetLastError();
 }
 

@@ -172,10 +172,11 @@ def merge_sparse(parts) -> Tuple[np.ndarray, np.ndarray]:
     return u, (s & 0xFFFFFFFF).astype(np.uint32)
 
 
-def merge_engine(eng, dst: int = 0, group=None, device=None, packed_hist: bool = False) -> None:
+def merge_engine(eng, dst: int = 0, group=None, device=None, packed_hist: bool = False) -> int:
     """Merge every rank's partial counters into rank dst's engine (RCCL reduce
     of the dense arrays over xGMI; gathers of the small variable-length ones).
-    packed_hist: the page histogram through HistPacker (bytes + overflow)."""
+    packed_hist: the page histogram through HistPacker (bytes + overflow).
+    Returns the bytes this rank contributed to the dense collectives."""
     import torch
     import torch.distributed as dist
 
@@ -183,10 +184,12 @@ def merge_engine(eng, dst: int = 0, group=None, device=None, packed_hist: bool =
 
     rank = dist.get_rank(group)
     dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
+    nbytes = 0
     for which, op in ((_lib.NMG_ARR_SUM64, "sum"), (_lib.NMG_ARR_MIN64, "min"), (_lib.NMG_ARR_MAX64, "max")):
         n = eng.array_size(which)
         if n == 0:
             continue
+        nbytes += 8 * n
         t = torch.empty(n, dtype=torch.int64, device=dev)
         eng.export_array(which, t.data_ptr())
         reduce_u64(t, op, dst=dst, group=group)
@@ -198,8 +201,9 @@ def merge_engine(eng, dst: int = 0, group=None, device=None, packed_hist: bool =
         hp = getattr(eng, "_hist_packer", None)  # one packer per engine, reused across merges
         if hp is None or hp.cells != n:
             hp = eng._hist_packer = HistPacker(eng, dev)
-        hp.merge(dst=dst, group=group)
+        nbytes += hp.merge(dst=dst, group=group)
     elif n:
+        nbytes += 4 * n
         t = torch.empty(n, dtype=torch.int32, device=dev)
         eng.export_array(_lib.NMG_ARR_HIST32, t.data_ptr())
         reduce_u32_sum(t, dst=dst, group=group)
@@ -207,6 +211,7 @@ def merge_engine(eng, dst: int = 0, group=None, device=None, packed_hist: bool =
             torch.cuda.synchronize(dev)
             eng.import_array(_lib.NMG_ARR_HIST32, t.data_ptr())
     merge_host_side(eng, dst=dst, group=group)
+    return nbytes
 
 
 def merge_host_side(eng, dst: int = 0, group=None) -> None:

@@ -13,6 +13,10 @@ tests pin the parts the other parity tests do not reach on purpose:
 * partition shapes: many threads (page cells of a partition too many for
   LDS: global atomics), objects larger than a partition's LDS cells, heavily
   reused addresses (older entries), tiny buffers (more buffers than windows);
+* the route pass's LDS line stage: with it, without it (every record stored
+  to its slot), and with every partition's line given up at its first record
+  ahead of the lap (the given-up path and the end-of-launch write-out of
+  incomplete lines);
 * NMG_F_SINGLE_PASS gives the same results."""
 import os
 
@@ -29,7 +33,8 @@ pytestmark = pytest.mark.gpu
 NO_ROUTE = 0x10000
 TINY_POOL = 0x20000
 TINY_OVF = 0x80000  # (internal, with TINY_POOL) an overflow list of 64 records: the rest attributed in the route pass
-ROUTE_V1 = 0x20000000  # (internal) route_kernel instead of the default route2_kernel
+NO_LINES = 0x20000000  # (internal) route pass without the LDS line stage: every record stored to its slot
+LAP_NOWAIT = 0x100000  # (internal) a partition's LDS line given up at its first record ahead of the lap
 
 
 def _oracle(rp, d):
@@ -81,9 +86,10 @@ ROUTE_CASES = [
 
 
 @pytest.mark.parametrize("cfg", ROUTE_CASES, ids=[f"case{i}" for i in range(len(ROUTE_CASES))])
-@pytest.mark.parametrize("flags", [0, TINY_POOL, TINY_POOL | TINY_OVF, _lib.NMG_F_SINGLE_PASS, ROUTE_V1,
-                                   ROUTE_V1 | TINY_POOL, ROUTE_V1 | TINY_POOL | TINY_OVF],
-                         ids=["route", "tinypool", "tinyovf", "single", "v1", "v1tiny", "v1tinyovf"])
+@pytest.mark.parametrize("flags", [0, TINY_POOL, TINY_POOL | TINY_OVF, _lib.NMG_F_SINGLE_PASS, NO_LINES,
+                                   NO_LINES | TINY_POOL, LAP_NOWAIT, LAP_NOWAIT | TINY_POOL | TINY_OVF],
+                         ids=["route", "tinypool", "tinyovf", "single", "nolines", "nolinestiny", "lapnowait",
+                              "lapnowaittinyovf"])
 def test_route_bit_exact(tmp_path, cfg, flags):
     d = str(tmp_path)
     path, odir = _oracle(generate(cfg), d)
@@ -100,7 +106,7 @@ def _results(eng):
     return g, ns, nf, first, cw, bs, bf, eng.page_cells()
 
 
-@pytest.mark.parametrize("extra", [0, TINY_POOL, ROUTE_V1])
+@pytest.mark.parametrize("extra", [0, TINY_POOL, NO_LINES, LAP_NOWAIT])
 def test_route_accumulates_like_single_pass(extra):
     """analyze, analyze (no reset), synchronize, analyze: the route path and
     the single-pass kernel accumulate the same counters, per-buffer match
@@ -152,7 +158,7 @@ def test_route_escaped_records_bit_exact(tmp_path):
         rec["addr"][far] = np.uint64(0x600000000000) + rng.integers(0, 1 << 41, int(far.sum()), dtype=np.uint64)
         rec["weight"][heavy] = rng.integers(1 << 14, 1 << 20, int(heavy.sum()), dtype=np.uint64)
     path, odir = _oracle(rp, d)
-    for tag, flags in (("route", 0), ("tiny", TINY_POOL), ("v1", ROUTE_V1), ("v1tiny", ROUTE_V1 | TINY_POOL)):
+    for tag, flags in (("route", 0), ("tiny", TINY_POOL), ("nolines", NO_LINES), ("lapnowait", LAP_NOWAIT)):
         edir, raw = _engine(path, d, _lib.NMG_F_DEFAULT | flags, tag)
         _same(os.path.join(d, "oracle_raw.bin"), raw)
         _same(os.path.join(d, "oracle_stdout.txt"), os.path.join(d, f"engine_{tag}_stdout.txt"))

@@ -25,12 +25,11 @@ VARIANTS = {
     # large tables: the partition-first path (nmg_route.h) and its parts
     "legacy": 0x3 | 0x10000,            # attribute_kernel on a large table (kDbgNoRoute)
     "route": 0x3,                       # route2 + count + plan + scatter + local (default for > 1023 keys)
-    "route_v1": 0x3 | 0x20000000,       # ... with route_kernel (workgroup-wide stream, batch sort)
+    "route_nolines": 0x3 | 0x20000000,  # ... without the route pass's LDS line stage (every record stored to its slot)
     "route_atomics": 0x3 | 0x80000000,  # every local-pass flush through atomics
     "route_nopages": 0x1,               # ... without the page histogram
     "route_noloc": 0x3 | 0x400000,      # local pass loads its chunks only
-    "route_nowrite": 0x3 | 0x100000 | 0x400000,  # batches sorted in LDS, no chunk stores (local: loads only)
-    "route_nobatch": 0x3 | 0x200000,    # stream + partition search + batch ranks only
+    "route_lapnowait": 0x3 | 0x100000,  # ... every partition's line given up at its first record ahead of the lap
     "local_noobj": 0x3 | 0x1000000,     # local pass without object counters / first ordinals
     "local_nopage": 0x3 | 0x2000000,    # ... without page cells
     "local_noglobal": 0x3 | 0x4000000,  # ... without the global counters

@@ -28,9 +28,7 @@ sys.path.insert(0, ROOT)
 
 TIMING = 0x800000
 WORDS = 12
-# route_kernel (flag 0x20000000): per workgroup-wide window, then per batch
-PHASES = ["wait", "issue", "global", "search", "rank", "scan", "alloc", "write", "state"]
-# route2_kernel (the default): per wave window
+# route2_kernel: per wave window
 PHASES_V2 = ["wait", "check_loads", "global", "search", "encode", "claim_store"]
 WORKLOADS = {
     "c4": dict(nb_samples=125_000_000, nb_intervals=1_000_000, size_max=64 * 1024),
@@ -75,10 +73,8 @@ def main():
         win, bat = a[:, 9].sum(), a[:, 10].sum()
         out = {"workload": wname, "flags": hex(args.flags), "analyze_ms": float(np.median(ms)),
                "windows_per_wave": float(a[:, 9].mean()), "batches_per_wave": float(a[:, 10].mean())}
-        v1 = bool(args.flags & 0x20000000)
-        for k, name in enumerate(PHASES if v1 else PHASES_V2):
-            per = win if (k < 5 or not v1) else bat
-            out[f"{name}_cyc_per_{'window' if per is win else 'batch'}"] = float(a[:, k].sum() / per)
+        for k, name in enumerate(PHASES_V2):
+            out[f"{name}_cyc_per_window"] = float(a[:, k].sum() / win)
         out["total_cyc_per_wave"] = float(a[:, :9].sum(axis=1).mean())
         print(json.dumps(out), flush=True)
         e.close()
