@@ -371,7 +371,10 @@ __device__ __forceinline__ RDesc route_desc(const RouteParams& rp, const uint4* 
 constexpr uint32_t kR2WG = 768;
 // line stage: partitions q < kLineParts have an LDS line
 constexpr uint32_t kLineParts = 1280;
-constexpr uint32_t kLapSpins = 3;  // lap re-reads before a partition's line is given up
+#ifndef NMG_LAP_SPINS
+#define NMG_LAP_SPINS 3
+#endif
+constexpr uint32_t kLapSpins = NMG_LAP_SPINS;  // lap re-reads before a partition's line is given up
 // line word: fill (3 bits) | slots held (4) | broken (1) | lap (12: chunk
 // line number, mod 4096, of the line served)
 constexpr uint32_t kLwMaskShift = 3, kLwBroken = 0x80u, kLwLapShift = 8, kLwLapMask = 4095;
@@ -804,51 +807,62 @@ __global__ __launch_bounds__(kR2WG, 1) void route2_kernel(RouteParams rp) {
           }
         }
       }
-      // ---- the line stage (see the comment above kR2WG)
+      // ---- the line stage (see the comment above kR2WG).  In rounds: the
+      // records whose line is the lap go into it, the lines they complete are
+      // written out and their laps move on, then the records still ahead of
+      // their lap re-read it -- so a record waiting on a line that a record
+      // of its own wave completes gets in in the next round.  Past kLapSpins
+      // rounds (or on a given-up line) a record goes straight to its slot.
       bool staged = false;
       if (NMG_R2_LINES && __ballot(lined && dst != ~0ull)) {
         lid &= kLwLapMask;
-        bool wait = lined && dst != ~0ull && ((lw >> kLwLapShift) & kLwLapMask) != lid && !(lw & kLwBroken);
-        for (uint32_t k = 0; k < spins && __ballot(wait); k++) {  // (the previous line still filling)
-          if (wait) {
-            lw = __hip_atomic_load(&s_lw[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            wait = ((lw >> kLwLapShift) & kLwLapMask) != lid && !(lw & kLwBroken);
-          }
-        }
-        staged = lined && dst != ~0ull && ((lw >> kLwLapShift) & kLwLapMask) == lid;
-        if (wait) atomicOr(&s_lw[q], kLwBroken);  // given up: q's later records go straight to their slots
-        bool done = false;
         const uint32_t j = (uint32_t)dst & 3u;
-        if (staged) {
-          s_line[q * 4 + j] = a;
-          s_ldst[q] = (uint32_t)(dst >> 2);
-          // (the record before the count that may complete the line)
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-          const uint32_t o = atomicAdd(&s_lw[q], 1u + (1u << (kLwMaskShift + j)));
-          done = (o & 7u) == 3u;
-        }
-        const uint64_t dm = __ballot(done);
-        if (dm) {  // the completed lines written out: four lanes per line, 16 lines per store
-          if (done) s_tab[wave][__popcll(dm & ((1ull << lane) - 1))] = make_uint2(q, (uint32_t)(dst >> 2));
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
-          __builtin_amdgcn_wave_barrier();
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
-          const uint32_t nd = (uint32_t)__popcll(dm);
-          for (uint32_t j0 = 0; j0 < nd; j0 += 16) {
-            const uint32_t jj = j0 + ((uint32_t)lane >> 2);
-            if (jj < nd) {
-              const uint2 t = s_tab[wave][jj];
-              const uint4 v = s_line[t.x * 4 + (lane & 3)];
-              rp.rec16[uint64_t(t.y) * 4 + (lane & 3)] = v;
-              // (the line read by all four lanes -- one instruction, waited
-              // for by the store -- before its slots are handed to the next line)
-              __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-              if ((lane & 3) == 0) atomicAdd(&s_lw[t.x], kLwRelease);
+        bool pend = lined && dst != ~0ull;
+        if (TIMING) rt.acc[8] += (uint64_t)__popcll(__ballot(pend && ((lw >> kLwLapShift) & kLwLapMask) != lid));
+        for (uint32_t round = 0;; round++) {
+          const bool ready = pend && ((lw >> kLwLapShift) & kLwLapMask) == lid;
+          const bool give = pend && !ready && ((lw & kLwBroken) || round == spins);
+          if (give && !(lw & kLwBroken)) atomicOr(&s_lw[q], kLwBroken);  // q's later records: straight to their slots
+          pend = pend && !ready && !give;
+          bool done = false;
+          if (ready) {
+            s_line[q * 4 + j] = a;
+            s_ldst[q] = (uint32_t)(dst >> 2);
+            // (the record before the count that may complete the line)
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+            const uint32_t o = atomicAdd(&s_lw[q], 1u + (1u << (kLwMaskShift + j)));
+            done = (o & 7u) == 3u;
+            staged = true;
+          }
+          const uint64_t dm = __ballot(done);
+          if (dm) {  // the completed lines written out: four lanes per line, 16 lines per store
+            if (done) s_tab[wave][__popcll(dm & ((1ull << lane) - 1))] = make_uint2(q, (uint32_t)(dst >> 2));
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+            const uint32_t nd = (uint32_t)__popcll(dm);
+            for (uint32_t j0 = 0; j0 < nd; j0 += 16) {
+              const uint32_t jj = j0 + ((uint32_t)lane >> 2);
+              if (jj < nd) {
+                const uint2 t = s_tab[wave][jj];
+                const uint4 v = s_line[t.x * 4 + (lane & 3)];
+                rp.rec16[uint64_t(t.y) * 4 + (lane & 3)] = v;
+                // (the line read by all four lanes -- one instruction, waited
+                // for by the store -- before its slots are handed to the next line)
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+                if ((lane & 3) == 0) atomicAdd(&s_lw[t.x], kLwRelease);
+              }
             }
           }
+          if (!__ballot(pend)) break;
+          if (pend) lw = __hip_atomic_load(&s_lw[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
       }
       if (dst != ~0ull && !staged) rp.rec16[dst] = a;
+      if (TIMING) {  // (records staged / stored straight to their slot)
+        rt.acc[6] += (uint64_t)__popcll(__ballot(staged));
+        rt.acc[7] += (uint64_t)__popcll(__ballot(dst != ~0ull && !staged));
+      }
       if (__ballot(ovf)) {  // (rare) a workgroup's pool outgrown: SAMPLEs shorter than 40 B
         if (ovf) {
           const uint32_t o = atomicAdd(rp.ovf_cnt, 1u);
@@ -874,7 +888,10 @@ __global__ __launch_bounds__(kR2WG, 1) void route2_kernel(RouteParams rp) {
       unsigned long long* o = p.dbg + (uint64_t(blockIdx.x) * (kWG / 64) + tid / 64) * kRouteTimingWords;
       for (int k = 0; k < 9; k++) o[k] = rt.acc[k];
       o[9] = nwin;
-      o[10] = 0;
+      uint32_t nb = 0;  // (wave 0: the workgroup's partitions whose line was given up)
+      if (wave == 0)
+        for (uint32_t q = 0; q < nlp; q++) nb += (s_lw[q] & kLwBroken) ? 1u : 0u;
+      o[10] = nb;
     }
   }
   dual_drain(gacc, s_gsums, lane);

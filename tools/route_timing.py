@@ -75,7 +75,13 @@ def main():
                "windows_per_wave": float(a[:, 9].mean()), "batches_per_wave": float(a[:, 10].mean())}
         for k, name in enumerate(PHASES_V2):
             out[f"{name}_cyc_per_window"] = float(a[:, k].sum() / win)
-        out["total_cyc_per_wave"] = float(a[:, :9].sum(axis=1).mean())
+        # the line stage: records staged / stored straight to their slot, records
+        # that re-read the lap, partitions given up per workgroup
+        tot = a[:, 6].sum() + a[:, 7].sum()
+        out["staged_frac"] = float(a[:, 6].sum() / tot) if tot else 0.0
+        out["lap_wait_frac"] = float(a[:, 8].sum() / tot) if tot else 0.0
+        out["broken_parts_per_wg"] = float(a[:, 10].sum() / max(1.0, a.shape[0] / 12))
+        out["total_cyc_per_wave"] = float(a[:, :6].sum(axis=1).mean())
         print(json.dumps(out), flush=True)
         e.close()
         del d
