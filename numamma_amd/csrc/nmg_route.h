@@ -70,8 +70,8 @@ constexpr uint32_t kDbgTinyPool = 0x20000; // route pass: private pools of 2 chu
 // ablation switches (tools/ablate.py; results are wrong with them)
 constexpr uint32_t kDbgTinyOvf = 0x80000;  // route pass: an overflow list of 64 records, the rest attributed directly
                                            // (tests, with kDbgTinyPool)
-constexpr uint32_t kDbgLapNoWait = 0x100000;   // route pass: a partition's LDS line is given up at the first
-                                                // record whose line is not the lap (tests: the given-up path)
+constexpr uint32_t kDbgLapNoWait = 0x100000;   // route pass: a partition's LDS line is given up by a record one
+                                                // line ahead of the staged one (tests: the given-up path)
 constexpr uint32_t kDbgLocalNoWork = 0x400000;   // local pass: chunk loads only
 constexpr uint32_t kDbgRouteTiming = 0x800000;   // route pass: per-wave phase cycles in Params::dbg
 constexpr uint32_t kDbgLocalNoObj = 0x1000000;   // local pass: no object counters / first ordinals
@@ -84,7 +84,8 @@ constexpr uint32_t kDbgLocalAtomics = 0x80000000u;  // local pass: every flush t
 constexpr uint32_t kDbgLocalTiming = 0x10000000;  // local pass: per-wave phase cycles in Params::dbg
                                                    // (wait, global, search, match, object, page per chunk;
                                                    // dequeue, setup, flush per item; chunks, items)
-constexpr int kRouteTimingWords = 12;            // wait, check+loads, global, search, encode, claim+store, -, -,
+constexpr int kRouteTimingWords = 16;            // route2: wait, check+loads, global, search, encode, claim, staged,
+                                                 // direct, lap waits, windows, broken, line rounds, stores
                                                  // -, windows, -, -
 
 // One partition: keys [k0, k0 + nk), entries [e0, e0 + ne) (entry ids of the

@@ -204,62 +204,53 @@ __device__ __forceinline__ void dual_clear(DualAcc& a) {
   a.tw[0] = a.tw[1] = 0;
 }
 
-// update_counters for the route pass: register buckets for the common
-// levels, LDS for the rest; READ_FIRST: a minimum / maximum is read first
-// and updated by an LDS atomic only when the record moves it, otherwise
-// every minimum / maximum is an LDS atomic that returns nothing
-template <bool READ_FIRST = false>
+// update_counters(global_counters, sample) (mem_sampling.c:517-592) in the
+// route pass, for access type ACC (a wave window lies in one buffer, so its
+// access type is uniform and the caller branches on it once): register
+// buckets for the common levels, LDS for the rest; a minimum / maximum is
+// read first and updated by an LDS atomic only when the record moves it
+template <uint32_t ACC>
 __device__ __forceinline__ void route_count(DualAcc& a, unsigned long long (*sums)[kGlobalSums],
                                             unsigned long long (*mins)[18], unsigned long long (*maxs)[18],
-                                            uint32_t acc, uint32_t lvl, uint64_t w) {
+                                            uint32_t lvl, uint64_t w) {
   const uint32_t bm = bucket_mask(lvl);
   if (w < kLaneMaxWeight) {
-    const uint32_t w32 = (uint32_t)w, one = 1u << (16 * acc);
-    const uint32_t wr = acc ? 0u : w32, ww = acc ? w32 : 0u;
+    const uint32_t w32 = (uint32_t)w;
+    constexpr uint32_t one = 1u << (16 * ACC);
     a.tc += one;
     a.na += (lvl & LVL_NA) ? one : 0u;
-    a.tw[0] += wr;
-    a.tw[1] += ww;
+    a.tw[ACC] += w32;
 #pragma unroll
     for (int g = 0; g < kDualGroups; g++) {
       const bool in = (bm >> g) & 1;
       a.cnt[g] += in ? one : 0u;
-      a.sum[0][g] += in ? wr : 0u;
-      a.sum[1][g] += in ? ww : 0u;
+      a.sum[ACC][g] += in ? w32 : 0u;
     }
     for (uint32_t m = bm >> kDualGroups; m; m &= m - 1) {  // rarer hit buckets, miss buckets
       const uint32_t b = kDualGroups + (uint32_t)__builtin_ctz(m);
-      atomicAdd(&sums[acc][3 + 2 * b], 1ull);
-      if (w) atomicAdd(&sums[acc][4 + 2 * b], (unsigned long long)w);
+      atomicAdd(&sums[ACC][3 + 2 * b], 1ull);
+      if (w) atomicAdd(&sums[ACC][4 + 2 * b], (unsigned long long)w);
     }
   } else {  // weights >= 2^23 cycles: straight to the LDS counters
-    atomicAdd(&sums[acc][0], 1ull);
-    atomicAdd(&sums[acc][1], (unsigned long long)w);
-    if (lvl & LVL_NA) atomicAdd(&sums[acc][2], 1ull);
+    atomicAdd(&sums[ACC][0], 1ull);
+    atomicAdd(&sums[ACC][1], (unsigned long long)w);
+    if (lvl & LVL_NA) atomicAdd(&sums[ACC][2], 1ull);
     for (uint32_t m = bm; m; m &= m - 1) {
       const uint32_t b = (uint32_t)__builtin_ctz(m);
-      atomicAdd(&sums[acc][3 + 2 * b], 1ull);
-      atomicAdd(&sums[acc][4 + 2 * b], (unsigned long long)w);
+      atomicAdd(&sums[ACC][3 + 2 * b], 1ull);
+      atomicAdd(&sums[ACC][4 + 2 * b], (unsigned long long)w);
     }
   }
-  if (READ_FIRST) {  // (an atomic only when the record moves the bound)
-    if (bm) {
-      const uint32_t b = (uint32_t)__builtin_ctz(bm);
-      const unsigned long long mn = mins[acc][b], mx = maxs[acc][b];
-      if (w < mn) atomicMin(&mins[acc][b], (unsigned long long)w);
-      if (w > mx) atomicMax(&maxs[acc][b], (unsigned long long)w);
-      for (uint32_t m = bm & (bm - 1); m; m &= m - 1) {
-        const uint32_t b2 = (uint32_t)__builtin_ctz(m);
-        atomicMin(&mins[acc][b2], (unsigned long long)w);
-        atomicMax(&maxs[acc][b2], (unsigned long long)w);
-      }
+  if (bm) {  // (an atomic only when the record moves the bound)
+    const uint32_t b = (uint32_t)__builtin_ctz(bm);
+    const unsigned long long mn = mins[ACC][b], mx = maxs[ACC][b];
+    if (w < mn) atomicMin(&mins[ACC][b], (unsigned long long)w);
+    if (w > mx) atomicMax(&maxs[ACC][b], (unsigned long long)w);
+    for (uint32_t m = bm & (bm - 1); m; m &= m - 1) {
+      const uint32_t b2 = (uint32_t)__builtin_ctz(m);
+      atomicMin(&mins[ACC][b2], (unsigned long long)w);
+      atomicMax(&maxs[ACC][b2], (unsigned long long)w);
     }
-    return;
-  }
-  for (uint32_t m = bm; m; m &= m - 1) {
-    const uint32_t b = (uint32_t)__builtin_ctz(m);
-    atomicMin(&mins[acc][b], (unsigned long long)w);
-    atomicMax(&maxs[acc][b], (unsigned long long)w);
   }
 }
 
@@ -294,7 +285,7 @@ __device__ __forceinline__ void dual_drain(DualAcc& a, unsigned long long (*sums
 
 // kDbgRouteTiming: per-wave cycle accumulators of the route pass's phases
 struct RTimer {
-  uint64_t acc[10];
+  uint64_t acc[12];
   uint64_t last;
 };
 template <bool TIMING>
@@ -352,35 +343,35 @@ __device__ __forceinline__ RDesc route_desc(const RouteParams& rp, const uint4* 
 // store of its own: a wave-instruction of such stores touches 64 lines,
 // which costs the CU ~10x the issue time of 64 B runs at a 2 GB footprint
 // (tools/micro/vmem.hip), and a cold partition's line leaves L2 partly
-// written.  So every partition has a 64 B line in LDS, the four slots of a
-// chunk line (chunk slots 4l .. 4l + 3): a record whose line is the one the
-// partition's LDS line serves (its lap) is written there, and the record
-// that completes the line (the fourth write) has it written out whole, four
-// lanes of its wave per line, sixteen lines per store instruction.  The lap
-// then moves to the partition's next line.  A record whose line is not yet
-// the lap (the previous line still filling) re-reads the lap a few times;
-// past that the partition's LDS line is given up for the launch ("broken"):
-// its later records go straight to their slots, and a line left incomplete
-// -- broken, or a partition's last line -- is written out, the slots it
-// holds, after the workgroup's last barrier.  Hot partitions, whose lines
-// fill faster than a line's round trip through LDS, break early and store
-// directly; the consecutive slots their records claim in one wave-instruction
-// make those stores runs already.
+// written.  So every partition has a 64 B line in LDS for its chunk lines
+// (chunk slots 4l .. 4l + 3) in turn, and one 64-bit line word:
+//   the staged line S (its chunk-line number, mod 4096) and the slots it
+//   holds; for the lines S .. S + 7 the number of their records that are
+//   in place (written to the LDS line, or stored to their slot); a
+//   given-up bit.
+// A record whose line is S is written to the LDS line; a record of a line
+// ahead of S (a hot partition's records run ahead of its slowest writer) is
+// stored straight to its slot.  Either way it then counts itself for its
+// line with one LDS atomic; the record that brings S's count to 4 has the
+// staged slots written out -- a full line by four lanes of its wave,
+// sixteen lines per store instruction -- and moves S on, past any line
+// already complete.  Nothing ever waits: a record 8 lines or more ahead of
+// S gives the partition's line up (its later records are stored straight
+// to their slots and not counted), and a staged line left incomplete -- a
+// partition's last, or a given-up one -- is written out, the slots it
+// holds, after the workgroup's last barrier.
 
 // route2_kernel's workgroup: 12 waves (three per SIMD)
 constexpr uint32_t kR2WG = 768;
 // line stage: partitions q < kLineParts have an LDS line
 constexpr uint32_t kLineParts = 1280;
-#ifndef NMG_LAP_SPINS
-#define NMG_LAP_SPINS 3
-#endif
-constexpr uint32_t kLapSpins = NMG_LAP_SPINS;  // lap re-reads before a partition's line is given up
-// line word: fill (3 bits) | slots held (4) | broken (1) | lap (12: chunk
-// line number, mod 4096, of the line served)
-constexpr uint32_t kLwMaskShift = 3, kLwBroken = 0x80u, kLwLapShift = 8, kLwLapMask = 4095;
-// a write into slot j: fill + 1, slot bit; the release after a full line's
-// write-out: lap + 1, fill - 4, slots - 0xf
-constexpr uint32_t kLwRelease = (1u << kLwLapShift) - 4u - (0xfu << kLwMaskShift);
+// line word (u64): line l's count (3 bits) at 3 * (l mod 8), staged slots
+// (4) at 24, given up at 28, S at 52
+constexpr uint32_t kLwMaskShift = 24, kLwSShift = 52, kLwLineMask = 4095, kLwAhead = 8;
+constexpr unsigned long long kLwBroken = 1ull << 28;
+__device__ __forceinline__ uint32_t lw_count(unsigned long long w, uint32_t l) { return uint32_t(w >> (3 * (l & 7))) & 7u; }
+__device__ __forceinline__ uint32_t lw_s(unsigned long long w) { return uint32_t(w >> kLwSShift); }
+__device__ __forceinline__ uint32_t lw_mask(unsigned long long w) { return uint32_t(w >> kLwMaskShift) & 15u; }
 #ifndef NMG_R2_LINES
 #define NMG_R2_LINES 1
 #endif
@@ -518,7 +509,8 @@ __global__ __launch_bounds__(kR2WG, 1) void route2_kernel(RouteParams rp) {
   // the line stage: per partition a line of four compact records, its line
   // word and its chunk line (pool slot / 4); per wave the lines it writes out
   __shared__ uint4 s_line[NMG_R2_LINES ? kLineParts * 4 : 1];
-  __shared__ uint32_t s_lw[NMG_R2_LINES ? kLineParts : 1], s_ldst[NMG_R2_LINES ? kLineParts : 1];
+  __shared__ unsigned long long s_lw[NMG_R2_LINES ? kLineParts : 1];
+  __shared__ uint32_t s_ldst[NMG_R2_LINES ? kLineParts : 1];
   __shared__ uint2 s_tab[kWaves][64];
 
   Params& p = rp.p;
@@ -540,8 +532,9 @@ __global__ __launch_bounds__(kR2WG, 1) void route2_kernel(RouteParams rp) {
   for (uint32_t i = tid; i < P; i += kR2WG) s_state[i] = st_pack(kStNone, kStNone, 0, 2 * kChunk);
   // the first line of a partition: slot 0 of generation 1's open chunk
   const uint32_t nlp = NMG_R2_LINES && !(p.flags & kDbgNoLines) ? min(P, kLineParts) : 0u;
-  const uint32_t spins = (p.flags & kDbgLapNoWait) ? 0u : kLapSpins;
-  for (uint32_t i = tid; i < nlp; i += kR2WG) s_lw[i] = (kChunk / 4) << kLwLapShift;
+  for (uint32_t i = tid; i < nlp; i += kR2WG) s_lw[i] = (unsigned long long)(kChunk / 4) << kLwSShift;
+  // (kDbgLapNoWait: a record one line ahead of S already gives the line up -- tests)
+  const uint32_t ahead_max = (p.flags & kDbgLapNoWait) ? 1u : kLwAhead;
   const uint32_t r0 = p.ranges[blockIdx.x], r1 = p.ranges[blockIdx.x + 1];
   for (uint32_t i = r0 + tid; i < r1 && i - r0 < kDescLds; i += kR2WG) {
     const BufDesc d = p.sbufs[i];
@@ -613,7 +606,7 @@ __global__ __launch_bounds__(kR2WG, 1) void route2_kernel(RouteParams rp) {
 
     RTimer rt;  // (TIMING) per-wave phase cycles
 #pragma unroll
-    for (int k = 0; k < 9; k++) rt.acc[k] = 0;
+    for (int k = 0; k < 12; k++) rt.acc[k] = 0;
     rt.last = TIMING ? stamp() : 0;
     uint32_t nwin = 0;
 
@@ -739,7 +732,11 @@ __global__ __launch_bounds__(kR2WG, 1) void route2_kernel(RouteParams rp) {
       // slot, store
       rt_stamp<TIMING>(rt, 1);
       const uint32_t acc_l = dw.access();
-      if (valid) route_count<true>(gacc, s_gsums, s_gmins, s_gmaxs, acc_l, uint32_t(rec.dsrc >> 5) & 0x3fff, rec.w);
+      if (acc_l == 0) {  // (uniform)
+        if (valid) route_count<0>(gacc, s_gsums, s_gmins, s_gmaxs, uint32_t(rec.dsrc >> 5) & 0x3fff, rec.w);
+      } else {
+        if (valid) route_count<1>(gacc, s_gsums, s_gmins, s_gmaxs, uint32_t(rec.dsrc >> 5) & 0x3fff, rec.w);
+      }
       if (++gwin == kDrainWindows) {
         dual_drain(gacc, s_gsums, lane);
         gwin = 0;
@@ -766,7 +763,7 @@ __global__ __launch_bounds__(kR2WG, 1) void route2_kernel(RouteParams rp) {
       // (the line word read beside the claim: a lap can only move on once this
       // record's own line is written, so a lap that equals the record's line
       // here still does after the claim)
-      uint32_t lw = lined ? s_lw[q] : 0u;
+      unsigned long long lw = lined ? s_lw[q] : 0ull;
       {
         bool todo = routed, spin = false;
         uint32_t waitg = 0;
@@ -807,61 +804,74 @@ __global__ __launch_bounds__(kR2WG, 1) void route2_kernel(RouteParams rp) {
           }
         }
       }
-      // ---- the line stage (see the comment above kR2WG).  In rounds: the
-      // records whose line is the lap go into it, the lines they complete are
-      // written out and their laps move on, then the records still ahead of
-      // their lap re-read it -- so a record waiting on a line that a record
-      // of its own wave completes gets in in the next round.  Past kLapSpins
-      // rounds (or on a given-up line) a record goes straight to its slot.
+      rt_stamp<TIMING>(rt, 5);
+      // ---- the line stage (see the comment above kR2WG)
       bool staged = false;
-      if (NMG_R2_LINES && __ballot(lined && dst != ~0ull)) {
-        lid &= kLwLapMask;
-        const uint32_t j = (uint32_t)dst & 3u;
-        bool pend = lined && dst != ~0ull;
-        if (TIMING) rt.acc[8] += (uint64_t)__popcll(__ballot(pend && ((lw >> kLwLapShift) & kLwLapMask) != lid));
-        for (uint32_t round = 0;; round++) {
-          const bool ready = pend && ((lw >> kLwLapShift) & kLwLapMask) == lid;
-          const bool give = pend && !ready && ((lw & kLwBroken) || round == spins);
-          if (give && !(lw & kLwBroken)) atomicOr(&s_lw[q], kLwBroken);  // q's later records: straight to their slots
-          pend = pend && !ready && !give;
-          bool done = false;
-          if (ready) {
-            s_line[q * 4 + j] = a;
-            s_ldst[q] = (uint32_t)(dst >> 2);
-            // (the record before the count that may complete the line)
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-            const uint32_t o = atomicAdd(&s_lw[q], 1u + (1u << (kLwMaskShift + j)));
-            done = (o & 7u) == 3u;
-            staged = true;
-          }
-          const uint64_t dm = __ballot(done);
-          if (dm) {  // the completed lines written out: four lanes per line, 16 lines per store
-            if (done) s_tab[wave][__popcll(dm & ((1ull << lane) - 1))] = make_uint2(q, (uint32_t)(dst >> 2));
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
-            const uint32_t nd = (uint32_t)__popcll(dm);
-            for (uint32_t j0 = 0; j0 < nd; j0 += 16) {
-              const uint32_t jj = j0 + ((uint32_t)lane >> 2);
-              if (jj < nd) {
-                const uint2 t = s_tab[wave][jj];
-                const uint4 v = s_line[t.x * 4 + (lane & 3)];
-                rp.rec16[uint64_t(t.y) * 4 + (lane & 3)] = v;
-                // (the line read by all four lanes -- one instruction, waited
-                // for by the store -- before its slots are handed to the next line)
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-                if ((lane & 3) == 0) atomicAdd(&s_lw[t.x], kLwRelease);
+      if (NMG_R2_LINES && __ballot(lined)) {
+        lid &= kLwLineMask;
+        const uint32_t j = (uint32_t)dst & 3u, S = lw_s(lw), ahead = (lid - S) & kLwLineMask;
+        // (a record of the overflow list has no slot but counts for its line)
+        const bool counts = lined && !(lw & kLwBroken) && ahead < ahead_max;
+        staged = counts && ahead == 0 && dst != ~0ull;
+        if (lined && !(lw & kLwBroken) && ahead >= ahead_max) atomicOr(&s_lw[q], kLwBroken);
+        if (staged) {
+          s_line[q * 4 + j] = a;
+          s_ldst[q] = (uint32_t)(dst >> 2);
+          // (the record before the count that may complete the line)
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+        } else if (counts && dst != ~0ull) {
+          rp.rec16[dst] = a;
+        }
+        bool done = false;
+        uint32_t dmask = 0;
+        if (counts) {
+          const unsigned long long o =
+              atomicAdd(&s_lw[q], (1ull << (3 * (lid & 7))) + (staged ? 1ull << (kLwMaskShift + j) : 0ull));
+          // the line's fourth record, the line being S (S may have reached it
+          // since the read beside the claim)
+          done = lw_count(o, lid) == 3 && lw_s(o) == lid;
+          dmask = lw_mask(o) | (staged ? 1u << j : 0u);
+        }
+        if (TIMING) rt.acc[8] += (uint64_t)__popcll(__ballot(counts && !staged));
+        const uint64_t dm = __ballot(done);
+        if (dm) {  // the staged slots of the completed lines written out: four lanes per line
+          if (done)
+            s_tab[wave][__popcll(dm & ((1ull << lane) - 1))] = make_uint2(q | (dmask << 11) | (lid << 16), (uint32_t)(dst >> 2));
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+          const uint32_t nd = (uint32_t)__popcll(dm);
+          for (uint32_t j0 = 0; j0 < nd; j0 += 16) {
+            const uint32_t jj = j0 + ((uint32_t)lane >> 2);
+            if (jj < nd) {
+              const uint2 t = s_tab[wave][jj];
+              const uint32_t tq = t.x & 2047u, tm = (t.x >> 11) & 15u, k = lane & 3;
+              if ((tm >> k) & 1) rp.rec16[uint64_t(t.y) * 4 + k] = s_line[tq * 4 + k];
+              // (the line read by all four lanes -- one instruction, waited
+              // for by the stores -- before S moves on and its slots are reused)
+              __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+              if (k == 0) {  // S -> S + 1, past the lines already complete (all their records stored straight)
+                uint32_t l = t.x >> 16, m = tm;
+                while (true) {
+                  const unsigned long long o = atomicAdd(
+                      &s_lw[tq], (1ull << kLwSShift) - (4ull << (3 * (l & 7))) - ((unsigned long long)m << kLwMaskShift));
+                  l = (l + 1) & kLwLineMask;
+                  if (lw_count(o, l) != 4) break;
+                  m = 0;
+                }
               }
             }
           }
-          if (!__ballot(pend)) break;
-          if (pend) lw = __hip_atomic_load(&s_lw[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
       }
-      if (dst != ~0ull && !staged) rp.rec16[dst] = a;
+      if (!NMG_R2_LINES || !lined) staged = false;
+      rt_stamp<TIMING>(rt, 9);
+      // the records the line stage did not take: not lined, or given up
+      const bool straight = dst != ~0ull && !(lined && !(lw & kLwBroken) && ((lid - lw_s(lw)) & kLwLineMask) < ahead_max);
+      if (straight) rp.rec16[dst] = a;
       if (TIMING) {  // (records staged / stored straight to their slot)
         rt.acc[6] += (uint64_t)__popcll(__ballot(staged));
-        rt.acc[7] += (uint64_t)__popcll(__ballot(dst != ~0ull && !staged));
+        rt.acc[7] += (uint64_t)__popcll(__ballot(straight));
       }
       if (__ballot(ovf)) {  // (rare) a workgroup's pool outgrown: SAMPLEs shorter than 40 B
         if (ovf) {
@@ -877,7 +887,7 @@ __global__ __launch_bounds__(kR2WG, 1) void route2_kernel(RouteParams rp) {
         }
         vm_drain();  // (rare: nothing of this path stays pending where it joins the window)
       }
-      rt_stamp<TIMING>(rt, 5);
+      rt_stamp<TIMING>(rt, 10);
     };
 
     do {  // (d0: the wave's stream, uniform)
@@ -892,6 +902,8 @@ __global__ __launch_bounds__(kR2WG, 1) void route2_kernel(RouteParams rp) {
       if (wave == 0)
         for (uint32_t q = 0; q < nlp; q++) nb += (s_lw[q] & kLwBroken) ? 1u : 0u;
       o[10] = nb;
+      o[11] = rt.acc[9];
+      o[12] = rt.acc[10];
     }
   }
   dual_drain(gacc, s_gsums, lane);
@@ -917,9 +929,9 @@ __global__ __launch_bounds__(kR2WG, 1) void route2_kernel(RouteParams rp) {
     // a line the stage still holds (the partition's last, or one a given-up
     // lap left incomplete): the slots it holds
     if (q < nlp) {
-      const uint32_t lw = s_lw[q];
+      const uint32_t m = lw_mask(s_lw[q]);
       for (uint32_t j = 0; j < 4; j++)
-        if ((lw & 7u) && ((lw >> (kLwMaskShift + j)) & 1u)) rp.rec16[uint64_t(s_ldst[q]) * 4 + j] = s_line[q * 4 + j];
+        if ((m >> j) & 1u) rp.rec16[uint64_t(s_ldst[q]) * 4 + j] = s_line[q * 4 + j];
     }
   }
   if (tid == 0) rp.used[blockIdx.x] = min(s_taken, capl);

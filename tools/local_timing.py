@@ -28,7 +28,7 @@ os.environ.setdefault("NMG_INTERNAL_FLAGS", "1")  # (internal ablation / timing 
 sys.path.insert(0, ROOT)
 
 TIMING = 0x10000000
-WORDS = 12
+WORDS = 16
 PHASES = ["wait", "global", "search", "match", "object", "page", "dequeue", "setup", "flush"]
 WORKLOADS = {
     "c4": dict(nb_samples=125_000_000, nb_intervals=1_000_000, size_max=64 * 1024),

@@ -27,9 +27,9 @@ os.environ.setdefault("NMG_INTERNAL_FLAGS", "1")  # (internal ablation / timing 
 sys.path.insert(0, ROOT)
 
 TIMING = 0x800000
-WORDS = 12
+WORDS = 16
 # route2_kernel: per wave window
-PHASES_V2 = ["wait", "check_loads", "global", "search", "encode", "claim_store"]
+PHASES_V2 = ["wait", "check_loads", "global", "search", "encode", "claim"]
 WORKLOADS = {
     "c4": dict(nb_samples=125_000_000, nb_intervals=1_000_000, size_max=64 * 1024),
     "c3": dict(nb_samples=100_000_000, nb_intervals=100_000),
@@ -75,13 +75,15 @@ def main():
                "windows_per_wave": float(a[:, 9].mean()), "batches_per_wave": float(a[:, 10].mean())}
         for k, name in enumerate(PHASES_V2):
             out[f"{name}_cyc_per_window"] = float(a[:, k].sum() / win)
+        out["line_stage_cyc_per_window"] = float(a[:, 11].sum() / win)
+        out["store_cyc_per_window"] = float(a[:, 12].sum() / win)
         # the line stage: records staged / stored straight to their slot, records
         # that re-read the lap, partitions given up per workgroup
-        tot = a[:, 6].sum() + a[:, 7].sum()
+        tot = a[:, 6].sum() + a[:, 7].sum() + a[:, 8].sum()
         out["staged_frac"] = float(a[:, 6].sum() / tot) if tot else 0.0
-        out["lap_wait_frac"] = float(a[:, 8].sum() / tot) if tot else 0.0
+        out["counted_direct_frac"] = float(a[:, 8].sum() / tot) if tot else 0.0  # (staged_frac: staged; rest: given up)
         out["broken_parts_per_wg"] = float(a[:, 10].sum() / max(1.0, a.shape[0] / 12))
-        out["total_cyc_per_wave"] = float(a[:, :6].sum(axis=1).mean())
+        out["total_cyc_per_wave"] = float((a[:, :6].sum(axis=1) + a[:, 11] + a[:, 12]).mean())
         print(json.dumps(out), flush=True)
         e.close()
         del d
