@@ -86,20 +86,23 @@ class Workload:
         self.eng.set_device_buffers(self.d_arena.data_ptr(), offs, lens, ranks, acc, seq_base=rank * self.nb_buf)
         self.merge_bufs = []
         self.hist_packer = None
+        self.obj_packer = None
         if distributed:  # merge buffers for the timed RCCL reduces (dense arrays)
-            from numamma_amd.distributed import HistPacker
+            from numamma_amd.distributed import HistPacker, ObjPacker
 
             for which, dt in ((_lib.NMG_ARR_SUM64, torch.int64), (_lib.NMG_ARR_MIN64, torch.int64),
                               (_lib.NMG_ARR_MAX64, torch.int64)):
                 n = self.eng.array_size(which)
                 if n:
                     self.merge_bufs.append((which, torch.empty(n, dtype=dt, device=device)))
-            # the page histogram (70 % of the payload) packed: bytes + overflow list
+            # the page histogram (70 % of the payload) packed: bytes + overflow list;
+            # the per-object count / weight rows as u32 words + overflow list
             self.hist_packer = HistPacker(self.eng, device)
+            self.obj_packer = ObjPacker(self.eng, device)
 
     def step(self):
         from numamma_amd import _lib
-        from numamma_amd.distributed import reduce_u64
+        from numamma_amd.distributed import GLOBAL_SUM_WORDS, reduce_u64
 
         self.eng.reset()
         self.eng.analyze()
@@ -107,6 +110,10 @@ class Workload:
             self.eng.synchronize()
             for which, t in self.merge_bufs:
                 self.eng.export_array(which, t.data_ptr())
+                if which == _lib.NMG_ARR_SUM64 and self.obj_packer is not None:
+                    if self.obj_packer.merge(t, dst=0) is not None:
+                        reduce_u64(t[:GLOBAL_SUM_WORDS], "sum", dst=0)  # (the global sums as u64)
+                        continue
                 reduce_u64(t, {0: "sum", 1: "min", 2: "max"}[which], dst=0)
             if self.hist_packer is not None:
                 self.hist_packer.merge(dst=0)

@@ -338,6 +338,17 @@ int nmg_import_array(nmg_engine *h, int which, const void *d_src);
  * padding): histogram = bytes + overflow, exactly the u32 sum. */
 int nmg_hist_pack(nmg_engine *h, uint32_t threshold, void *d_u8, void *d_ovf, uint64_t ovf_cap, uint64_t *n_ovf);
 int nmg_hist_unpack(nmg_engine *h, const void *d_u8, const void *d_ovf, uint64_t n_ovf);
+/* Packed per-object counters for the merge: the count and
+ * weight rows of a sum64 image (nmg_export_array(NMG_ARR_SUM64) into d_sum64)
+ * as u32 words where a value is below `threshold` (2^32 / ranks: the sum over
+ * the ranks fits), 0 where it is not, and those values listed as (row word,
+ * value) u64 pairs in d_ovf (up to ovf_cap pairs; *n_ovf = the full length).
+ * d_u32 holds 4 * nb_entries words.  After a u32 SUM reduce of d_u32 and a
+ * gather of the lists, nmg_objcw_unpack writes the rows of d_sum64 (then
+ * nmg_import_array) from the summed words plus every listed value. */
+int nmg_objcw_pack(nmg_engine *h, const void *d_sum64, uint64_t threshold, void *d_u32, void *d_ovf,
+                   uint64_t ovf_cap, uint64_t *n_ovf);
+int nmg_objcw_unpack(nmg_engine *h, void *d_sum64, const void *d_u32, const void *d_ovf, uint64_t n_ovf);
 /* sparse (object, page, thread) cells: export as (key, count) pairs on host,
  * in ascending key order (keys are unique) */
 int64_t nmg_sparse_count(nmg_engine *h);

@@ -186,6 +186,8 @@ _SIGS = {
     "nmg_import_array": (C.c_int, [H, C.c_int, P]),
     "nmg_hist_pack": (C.c_int, [H, C.c_uint32, P, P, C.c_uint64, u64p]),
     "nmg_hist_unpack": (C.c_int, [H, P, P, C.c_uint64]),
+    "nmg_objcw_pack": (C.c_int, [H, P, C.c_uint64, P, P, C.c_uint64, u64p]),
+    "nmg_objcw_unpack": (C.c_int, [H, P, P, P, C.c_uint64]),
     "nmg_sparse_count": (C.c_int64, [H]),
     "nmg_sparse_export": (C.c_int, [H, u64p, u32p, C.c_int64]),
     "nmg_sparse_import": (C.c_int, [H, u64p, u32p, C.c_int64]),

@@ -103,6 +103,7 @@ void free_route_table(nmg_engine* h) {
   (void)hipFree(h->d_pe_keys);
   (void)hipFree(h->d_pe_nodes);
   (void)hipFree(h->d_pe_info);
+  (void)hipFree(h->d_pe_pnode);
   (void)hipFree(h->d_pe_dir);
   (void)hipFree(h->d_pe_ids);
   (void)hipFree(h->d_pe_lrel);
@@ -117,6 +118,7 @@ void free_route_table(nmg_engine* h) {
   h->d_pe_keys = nullptr;
   h->d_pe_nodes = nullptr;
   h->d_pe_info = nullptr;
+  h->d_pe_pnode = nullptr;
   h->route_ok = false;
   h->nparts = 0;
 }

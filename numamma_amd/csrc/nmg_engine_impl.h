@@ -259,8 +259,9 @@ struct nmg_engine {
   uint32_t nrsegs = 0;
   uint64_t* d_pe_keys = nullptr;  // [nparts][kPartSlots]
   uint4* d_pe_nodes = nullptr;    // [nparts][kPartSlots][2]
+  uint4* d_pe_pnode = nullptr;    // [nparts][kPartSlots] packed node records (PackedNode)
   uint2* d_pe_info = nullptr;     // [nparts][kPartSlots]
-  uint32_t* d_pe_dir = nullptr;   // [nparts][kPartDir]
+  uint4* d_pe_dir = nullptr;      // [nparts][kPartDir] (PartDir)
   uint32_t* d_pe_ids = nullptr;   // [table entries] entry id per table position (online tables; else null)
   uint32_t* d_pe_lrel = nullptr;  // [table entries] first packed LDS cell (online tables)
   uint32_t* d_pe_cmap = nullptr;  // packed cell -> histogram cell (online tables)

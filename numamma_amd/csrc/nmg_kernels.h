@@ -215,6 +215,11 @@ hipError_t launch_hist_pack(hipStream_t s, const uint32_t* hist, uint64_t ncells
                             uint64_t cap, unsigned long long* cnt, uint32_t* wgcnt);  // wgcnt: [1024] workspace
 hipError_t launch_hist_unpack(hipStream_t s, uint32_t* hist, uint64_t ncells, const void* u8, const void* ovf,
                               uint64_t n, unsigned long long* bad);
+// packed per-object counters (nmg_objcw_pack / nmg_objcw_unpack): n row words
+hipError_t launch_objcw_pack(hipStream_t s, const uint64_t* rows, uint64_t n, uint64_t thr, void* u32, void* ovf,
+                             uint64_t cap, unsigned long long* cnt);
+hipError_t launch_objcw_unpack(hipStream_t s, uint64_t* rows, uint64_t n, const void* u32, const void* ovf,
+                               uint64_t m, unsigned long long* bad);
 // per-object counts and weights, SoA rows -> [E][access][w] (aos: E * 32 B)
 hipError_t launch_objcw_aos(hipStream_t s, const uint64_t* soa, uint64_t E, void* aos);
 // page-cell rows on the device (nmg_get_page_cells / nmg_report): per dense

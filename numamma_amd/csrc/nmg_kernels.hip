@@ -1096,6 +1096,69 @@ __global__ __launch_bounds__(kPackWG) void hist_pack_kernel(const uint32_t* hist
   }
 }
 
+// Packed per-object counters for the multi-GPU merge (nmg_objcw_pack): the
+// four SoA rows [access][count, weight][E] of a sum64 image as u32 words where
+// a value is below thr (a rank's share of 2^32, so that the sum over the ranks
+// still fits), 0 there and a (row word, value) pair in the overflow list
+// where it is not.  The list's order does not matter: unpack adds.
+__global__ __launch_bounds__(256) void objcw_pack_kernel(const uint64_t* rows, uint64_t n, uint64_t thr,
+                                                         uint32_t* u32, unsigned long long* ovf, uint64_t cap,
+                                                         unsigned long long* cnt) {
+  const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
+  for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const uint64_t v = rows[i];
+    const bool big = v >= thr;
+    u32[i] = big ? 0u : (uint32_t)v;
+    if (big) {
+      const unsigned long long k = atomicAdd(cnt, 1ull);
+      if (k < cap) {
+        ovf[2 * k] = i;
+        ovf[2 * k + 1] = v;
+      }
+    }
+  }
+}
+
+// nmg_objcw_unpack: the rows = the summed u32 words, then += every listed value
+__global__ __launch_bounds__(256) void objcw_unpack_kernel(uint64_t* rows, uint64_t n, const uint32_t* u32) {
+  const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
+  for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) rows[i] = u32[i];
+}
+
+__global__ __launch_bounds__(256) void objcw_ovf_add_kernel(uint64_t* rows, uint64_t n, const unsigned long long* ovf,
+                                                            uint64_t m, unsigned long long* bad) {
+  const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
+  for (uint64_t k = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; k < m; k += stride) {
+    const uint64_t i = ovf[2 * k];
+    if (i < n) atomicAdd(reinterpret_cast<unsigned long long*>(rows + i), ovf[2 * k + 1]);
+    else atomicAdd(bad, 1ull);
+  }
+}
+
+hipError_t launch_objcw_pack(hipStream_t s, const uint64_t* rows, uint64_t n, uint64_t thr, void* u32, void* ovf,
+                             uint64_t cap, unsigned long long* cnt) {
+  if (n) {
+    const uint32_t grid = (uint32_t)std::min<uint64_t>((n + 255) / 256, 4096);
+    hipLaunchKernelGGL(objcw_pack_kernel, dim3(grid), dim3(256), 0, s, rows, n, thr, reinterpret_cast<uint32_t*>(u32),
+                       reinterpret_cast<unsigned long long*>(ovf), cap, cnt);
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_objcw_unpack(hipStream_t s, uint64_t* rows, uint64_t n, const void* u32, const void* ovf,
+                               uint64_t m, unsigned long long* bad) {
+  if (n) {
+    const uint32_t grid = (uint32_t)std::min<uint64_t>((n + 255) / 256, 4096);
+    hipLaunchKernelGGL(objcw_unpack_kernel, dim3(grid), dim3(256), 0, s, rows, n, reinterpret_cast<const uint32_t*>(u32));
+  }
+  if (m) {
+    const uint32_t grid = (uint32_t)std::min<uint64_t>((m + 255) / 256, 1024);
+    hipLaunchKernelGGL(objcw_ovf_add_kernel, dim3(grid), dim3(256), 0, s, rows, n,
+                       reinterpret_cast<const unsigned long long*>(ovf), m, bad);
+  }
+  return hipGetLastError();
+}
+
 // nmg_get_object_counters: the per-object counts and weights from their four
 // SoA rows (objcw_index: row access * 2 + w of E words) to [E][access][w],
 // one 32 B record per entry (a single contiguous D2H)

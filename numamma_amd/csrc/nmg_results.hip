@@ -383,6 +383,46 @@ extern "C" int nmg_hist_unpack(nmg_engine* h, const void* d_u8, const void* d_ov
   return NMG_OK;
 }
 
+extern "C" int nmg_objcw_pack(nmg_engine* h, const void* d_sum64, uint64_t threshold, void* d_u32, void* d_ovf,
+                              uint64_t ovf_cap, uint64_t* n_ovf) {
+  Range range("nmg_objcw_pack");
+  if (!h || !h->have_table || !n_ovf || !threshold) return NMG_ERR_INVALID;
+  const uint64_t n = 4ull * h->E;
+  *n_ovf = 0;
+  if (!n) return NMG_OK;
+  if (!d_sum64 || !d_u32 || (ovf_cap && !d_ovf)) return NMG_ERR_INVALID;
+  int rc = scratch_u64(h);
+  if (rc) return rc;
+  HIP_TRY(h, hipSetDevice(h->device));
+  HIP_TRY(h, hipMemsetAsync(h->d_scratch, 0, 8, h->stream));
+  const uint64_t* rows = reinterpret_cast<const uint64_t*>(d_sum64) + objcw_index(0, 0, 0, h->E);
+  HIP_TRY(h, launch_objcw_pack(h->stream, rows, n, threshold, d_u32, d_ovf, ovf_cap,
+                               reinterpret_cast<unsigned long long*>(h->d_scratch)));
+  HIP_TRY(h, hipMemcpyAsync(n_ovf, h->d_scratch, 8, hipMemcpyDeviceToHost, h->stream));
+  HIP_TRY(h, hipStreamSynchronize(h->stream));
+  return NMG_OK;
+}
+
+extern "C" int nmg_objcw_unpack(nmg_engine* h, void* d_sum64, const void* d_u32, const void* d_ovf, uint64_t n_ovf) {
+  Range range("nmg_objcw_unpack");
+  if (!h || !h->have_table || (n_ovf && !d_ovf)) return NMG_ERR_INVALID;
+  const uint64_t n = 4ull * h->E;
+  if (!n) return NMG_OK;
+  if (!d_sum64 || !d_u32) return NMG_ERR_INVALID;
+  int rc = scratch_u64(h);
+  if (rc) return rc;
+  HIP_TRY(h, hipSetDevice(h->device));
+  HIP_TRY(h, hipMemsetAsync(h->d_scratch + 1, 0, 8, h->stream));
+  uint64_t* rows = reinterpret_cast<uint64_t*>(d_sum64) + objcw_index(0, 0, 0, h->E);
+  HIP_TRY(h, launch_objcw_unpack(h->stream, rows, n, d_u32, d_ovf, n_ovf,
+                                 reinterpret_cast<unsigned long long*>(h->d_scratch + 1)));
+  uint64_t bad = 0;
+  HIP_TRY(h, hipMemcpyAsync(&bad, h->d_scratch + 1, 8, hipMemcpyDeviceToHost, h->stream));
+  HIP_TRY(h, hipStreamSynchronize(h->stream));
+  if (bad) return fail(h, NMG_ERR_RANGE, "nmg_objcw_unpack: overflow entries outside the rows");
+  return NMG_OK;
+}
+
 // The sparse cells can be non-empty only when something was inserted (or
 // imported) since the last reset: that reset cleared the table if it had been
 // written, and the flag of the analyses after it is d_sparse_dirty[nreset & 1]

@@ -41,7 +41,7 @@ constexpr uint32_t kMaxParts = (1u << kPartLevels) - 1;
 // arguments), its slot's entry (u16: last partition starting at or before the
 // slot start | starts inside the slot << 11, 31 = to the segment's end), then
 // a binary search over those few starts (sorted, in LDS)
-constexpr uint32_t kRouteDir = 2048;
+constexpr uint32_t kRouteDir = 4096;
 constexpr uint32_t kRouteSegs = 8;
 constexpr uint32_t kDirCntSat = 31;
 struct RSeg {
@@ -54,6 +54,22 @@ struct RSeg {
 constexpr uint32_t kPartKeys = 1023;       // local pass: keys per partition in LDS (sorted)
 constexpr uint32_t kPartSlots = 1024;      // per-partition table stride
 constexpr uint32_t kPartDir = 1024;        // directory slots per partition (radix over its key span)
+// PartDir, one directory slot (16 B): x = largest key index <= slot start
+// (10 bits) | keys inside the slot (11) << 10 | inline (1) << 21; y, z, w =
+// the first kDirInline inner keys' offsets from the slot start (u16 pairs,
+// 0xffff past the count), valid when `inline` (every listed offset < 2^16):
+// a lookup counts the offsets <= its own and reads keys only past them
+constexpr uint32_t kDirInline = 6;
+// PackedNode, a key's newest entry for the local pass's common path (16 B):
+//   end - first key (40 bits) | alloc_q (36) | free_q (36) | table position
+//   - e0 (11) | older entries (1) | exact (1)
+// with alloc_q / free_q = (date - tbase) >> kPnQShift, saturated (an entry
+// freed before tbase: alloc_q = max, free_q = 0).  A sample whose quantised
+// timestamp equals either bound, or a key marked exact (its object does not
+// start at the key, or its end or key offset does not fit), is decided on
+// the exact node record instead.
+constexpr uint32_t kPnQShift = 4;
+constexpr uint64_t kPnQMax = (1ull << 36) - 1;
 constexpr uint32_t kPartEntries = 1536;    // entries per partition (LDS object counters)
 constexpr uint32_t kPartCells = 28672;     // u16 page cells per partition: nb_threads x cell span
 constexpr uint32_t kItemChunks = 1023;     // chunks per work item: < 2^16 records, so u16 page cells
@@ -165,9 +181,10 @@ struct LocalParams {
   Params p;                  // table (nodes, chain, entries), counters, hist, sparse, flags
   const PartInfo* parts;
   const uint64_t* pe_keys;   // [nparts][kPartSlots] keys, ascending
-  const uint4* pe_nodes;     // [nparts][kPartSlots][2] (addr, end), (alloc, free) of each key's newest entry
-  const uint2* pe_info;      // [nparts][kPartSlots] (cell - cb, packed cell or ~0, table position - e0 | older entries << 31)
-  const uint32_t* pe_dir;    // [nparts][kPartDir] largest key index <= slot start | keys inside the slot << 16
+  const uint4* pe_nodes;     // [nparts][kPartSlots][2] (addr, end), (alloc, free) of each key's newest entry (exact)
+  const uint4* pe_pnode;     // [nparts][kPartSlots] the same, packed (PackedNode)
+  const uint2* pe_info;      // [nparts][kPartSlots] (cell - cb, or packed cell, or ~0 sparse; key - first key)
+  const uint4* pe_dir;       // [nparts][kPartDir] directory slots (PartDir)
   const uint32_t* pe_ids;    // [table entries] entry id of each table position (an online table,
                              // nmg_update_objects), or null: the id is the position (nmg_set_objects)
   const uint32_t* pe_lrel;   // [table entries] an entry's first packed cell (PartInfo::cmap != ~0)

@@ -103,6 +103,23 @@ __device__ __forceinline__ XRec x_decode(const XLayout& xl, uint64_t pb, uint4 v
   return r;
 }
 
+// x_decode without the bases: addr = the offset from the partition's first
+// key, ts = the offset from tbase (the local pass's common path)
+__device__ __forceinline__ XRec x_decode_rel(const XLayout& xl, uint4 v) {
+  XRec r;
+  r.addr = u64of(v.x, v.y & 0xffu);
+  r.ts = u64of(__builtin_amdgcn_alignbit(v.z, v.y, 8), (v.z >> 8) & 0xffu);
+  const uint32_t wesc = (uint32_t)xl.wesc;
+  r.w = __builtin_amdgcn_alignbit(v.w, v.z, 16) & wesc;
+  r.esc = r.w == wesc;
+  const uint32_t l0 = 16 + xl.wbits;
+  r.g = bits64(v.z, v.w, l0, (1u << xl.gbits) - 1);
+  r.off = bits64(v.z, v.w, l0 + xl.gbits, (1u << xl.obits) - 1) << 3;
+  r.th = bits64(v.z, v.w, l0 + xl.gbits + xl.obits, (1u << xl.tbits) - 1);
+  r.acc = bits64(v.z, v.w, l0 + xl.gbits + xl.obits + xl.tbits, 1u);
+  return r;
+}
+
 // an escaped record's address, timestamp and weight from the raw record
 // (struct mem_sample after the 8 B header: timestamp, addr, weight)
 __device__ __forceinline__ void x_resolve(XRec& r, const uint8_t* data, const BufDesc* descs) {
@@ -1097,12 +1114,9 @@ __device__ __forceinline__ int32_t match_older_pos(const Params& p, uint32_t fir
 template <bool TIMING, bool PACKED>
 __global__ __launch_bounds__(kLWG, 1) void local_kernel(LocalParams lp) {
   __shared__ uint64_t s_keys[kPartSlots];
-  // node records split in two 16 B arrays (addr, end) and (alloc, free): a
-  // 16 B stride spreads a wave's random reads over twice the bank groups of
-  // a 32 B one
-  __shared__ uint4 s_nodes[kPartSlots], s_dates[kPartSlots];
+  __shared__ uint4 s_pn[kPartSlots];  // packed node records (PackedNode)
   __shared__ uint2 s_info[kPartSlots];
-  __shared__ uint32_t s_dir[kPartDir];
+  __shared__ uint4 s_dir[kPartDir];   // directory slots (PartDir)
   __shared__ unsigned long long s_owt[2][kPartEntries];
   __shared__ unsigned long long s_first[kPartEntries];
   __shared__ uint32_t s_pg[kPartCells / 2];
@@ -1116,7 +1130,7 @@ __global__ __launch_bounds__(kLWG, 1) void local_kernel(LocalParams lp) {
   const bool pages = (p.flags & NMG_F_PAGE_HIST) != 0;
   RTimer rt;  // (kDbgLocalTiming) per-wave phase cycles
 #pragma unroll
-  for (int k = 0; k < 10; k++) rt.acc[k] = 0;
+  for (int k = 0; k < 12; k++) rt.acc[k] = 0;
   rt.last = TIMING ? stamp() : 0;
   uint32_t nchunks = 0, nit = 0;
   uint32_t nfound = 0;  // this wave's matched records (Params::found, added once per workgroup at the end)
@@ -1141,15 +1155,14 @@ __global__ __launch_bounds__(kLWG, 1) void local_kernel(LocalParams lp) {
     {
       const uint32_t nk = pi.nk;
       const uint64_t* gk = lp.pe_keys + uint64_t(q) * kPartSlots;
-      const uint4* gn = lp.pe_nodes + uint64_t(q) * kPartSlots * 2;
+      const uint4* gn = lp.pe_pnode + uint64_t(q) * kPartSlots;
       const uint2* gi = lp.pe_info + uint64_t(q) * kPartSlots;
       for (uint32_t i = tid; i < nk; i += kLWG) {
         s_keys[i] = gk[i];
-        s_nodes[i] = gn[2 * i];
-        s_dates[i] = gn[2 * i + 1];
+        s_pn[i] = gn[i];
         s_info[i] = gi[i];
       }
-      const uint32_t* gd = lp.pe_dir + uint64_t(q) * kPartDir;
+      const uint4* gd = lp.pe_dir + uint64_t(q) * kPartDir;
       for (uint32_t i = tid; i < kPartDir; i += kLWG) s_dir[i] = gd[i];
       for (uint32_t i = tid; i < item.z - item.y; i += kLWG) s_clist[i] = lp.clist[item.y + i];
     }
@@ -1202,50 +1215,74 @@ __global__ __launch_bounds__(kLWG, 1) void local_kernel(LocalParams lp) {
             lp.cmatch[s_clist[li[j]] & ((1u << kChunkIdBits) - 1)] = a16[j].x ^ a16[j].y ^ a16[j].z ^ a16[j].w;
         return;
       }
-      // (update_counters of every routed SAMPLE: the route pass)
+      // (update_counters of every routed SAMPLE: the route pass).  The common
+      // path works on the compact record's offsets: the address from the
+      // partition's first key (40 bits), the timestamp from tbase (40 bits).
+      // An escaped record (its address, timestamp or weight did not fit) is
+      // re-read from the raw record and decided on the exact node record.
       bool esc = false;
 #pragma unroll
       for (int j = 0; j < kLC; j++) {
-        xr[j] = x_decode(lp.xl, k0key, a16[j]);
+        xr[j] = x_decode_rel(lp.xl, a16[j]);
         esc |= valid[j] && xr[j].esc;
       }
       if (__ballot(esc)) {  // (rare) escaped records: address, timestamp and weight from the record
 #pragma unroll
         for (int j = 0; j < kLC; j++)
-          if (valid[j] && xr[j].esc) x_resolve(xr[j], p.data, lp.descs);
+          if (valid[j] && xr[j].esc) {
+            x_resolve(xr[j], p.data, lp.descs);
+            xr[j].addr -= k0key;  // (>= 0: routed to this partition); ts stays absolute
+          }
         vm_drain();
       }
 #pragma unroll
       for (int j = 0; j < kLC; j++) {
-        addr[j] = xr[j].addr;
-        ts[j] = xr[j].ts;
+        addr[j] = xr[j].addr;  // offset from the partition's first key
+        ts[j] = xr[j].ts;      // offset from tbase (escaped: absolute)
         w[j] = valid[j] ? xr[j].w : 0ull;
       }
       rt_stamp<TIMING>(rt, 1);
       // lower bound among the partition's keys (ht_lower_key, tools/hash.c:63-77):
-      // the record's address is < the next partition's first key; below the
-      // first key (partition 0 only) there is no node.  The directory slot
-      // gives the largest key <= the slot start and the keys inside the slot
-      // (usually 0 or 1; a binary search among them otherwise).
+      // the record's address is >= the partition's first key and < the next
+      // partition's.  The directory slot gives the largest key <= the slot
+      // start, the keys inside the slot and the first kDirInline of their
+      // offsets: the answer is that key plus the offsets <= the record's; keys
+      // are read only past them (or for a slot whose offsets do not fit).
       int32_t r[kLC];
       uint32_t sa[kLC], sn[kLC];
 #pragma unroll
       for (int j = 0; j < kLC; j++) {
         r[j] = -1;
         sa[j] = sn[j] = 0;
-        if (valid[j] && addr[j] >= k0key) {
-          const uint32_t de = s_dir[(uint32_t)min((addr[j] - k0key) >> dshift, (uint64_t)(kPartDir - 1))];
-          sa[j] = de & 0xffffu;  // answer in [a, a + n]: keys[a] <= addr
-          sn[j] = de >> 16;
+        if (valid[j]) {
+          const uint32_t slot = (uint32_t)min(addr[j] >> dshift, (uint64_t)(kPartDir - 1));
+          const uint4 de = s_dir[slot];
+          const uint32_t lo = de.x & 1023u, n = (de.x >> 10) & 2047u;
+          uint32_t a = lo, m = n;
+          if (n && ((de.x >> 21) & 1u)) {  // inline offsets
+            const uint64_t rs64 = addr[j] - (uint64_t(slot) << dshift);
+            const uint32_t rs = rs64 >> 16 ? 0x10000u : (uint32_t)rs64;
+            const uint32_t c = (uint32_t)((de.y & 0xffffu) <= rs) + (uint32_t)((de.y >> 16) <= rs) +
+                               (uint32_t)((de.z & 0xffffu) <= rs) + (uint32_t)((de.z >> 16) <= rs) +
+                               (uint32_t)((de.w & 0xffffu) <= rs) + (uint32_t)((de.w >> 16) <= rs);
+            a = lo + min(c, n);
+            m = (c == kDirInline && n > kDirInline) ? n - kDirInline : 0u;  // past the listed keys: search
+          }
+          sa[j] = a;  // answer in [a, a + m]: keys[a] <= addr
+          sn[j] = m;
           r[j] = 0;
         }
+      }
+      if (TIMING) {  // (records whose lookup reads keys)
+#pragma unroll
+        for (int j = 0; j < kLC; j++) rt.acc[11] += (uint64_t)__popcll(__ballot(sn[j] != 0));
       }
 #pragma unroll
       for (int j = 0; j < kLC; j++) {
         uint32_t a = sa[j], n = sn[j];
         while (n) {
           const uint32_t half = (n + 1) >> 1;
-          if (s_keys[a + half] <= addr[j]) {
+          if (s_keys[a + half] - k0key <= addr[j]) {
             a += half;
             n -= half;
           } else {
@@ -1261,27 +1298,62 @@ __global__ __launch_bounds__(kLWG, 1) void local_kernel(LocalParams lp) {
         (void)__builtin_amdgcn_readfirstlane(__ballot(any));
       }
       rt_stamp<TIMING>(rt, 2);
+      // is_sample_in_buffer (mem_analyzer.c:141-155) on the key's newest
+      // entry, from its packed node record: the object starts at the key, so
+      // key <= addr < end is addr - first key < end - first key; the dates
+      // compare quantised, a timestamp in the quantum of either bound (or an
+      // exact-marked key, or an escaped record) is decided on the exact node
       int32_t erel[kLC];
-      uint64_t baddr[kLC];
+      uint64_t pofs[kLC];  // a match: addr - buffer_addr
       uint32_t hrel[kLC];
-      bool older[kLC];
+      bool older[kLC], amb[kLC];
 #pragma unroll
       for (int j = 0; j < kLC; j++) {
         erel[j] = -1;
-        baddr[j] = 0;
+        pofs[j] = 0;
         hrel[j] = kEmpty32;
         older[j] = false;
+        amb[j] = false;
         if (r[j] >= 0 && !(p.flags & kDbgLocalNoSearch)) {
-          const uint4 na = s_nodes[r[j]], nb = s_dates[r[j]];
+          const uint4 pn = s_pn[r[j]];
           const uint2 inf = s_info[r[j]];
-          if (entry_match(na, nb, addr[j], ts[j])) {  // is_sample_in_buffer (mem_analyzer.c:141-155), newest entry
-            erel[j] = (int32_t)(inf.y & 0x7fffffffu);
-            baddr[j] = u64of(na.x, na.y);
+          const uint64_t end = u64of(pn.x, pn.y & 0xffu);
+          const uint64_t aq = u64of((pn.y >> 8) | (pn.z << 24), (pn.z >> 8) & 0xfu);
+          const uint64_t fq = u64of((pn.z >> 12) | (pn.w << 20), (pn.w >> 12) & 0xfu);
+          const uint64_t tq = ts[j] >> kPnQShift;
+          const bool in = addr[j] < end;
+          amb[j] = xr[j].esc || ((pn.w >> 28) & 1u) || (in && (tq == aq || tq == fq));
+          if (!amb[j] && in && tq > aq && tq < fq) {
+            erel[j] = (int32_t)((pn.w >> 16) & 2047u);
+            pofs[j] = addr[j] - inf.y;
             hrel[j] = inf.x;
-          } else {
-            older[j] = (inf.y >> 31) != 0;
+          } else if (!amb[j]) {
+            older[j] = ((pn.w >> 27) & 1u) != 0;
           }
         }
+      }
+      bool anyamb = false;
+#pragma unroll
+      for (int j = 0; j < kLC; j++) {
+        anyamb |= amb[j];
+        if (TIMING) rt.acc[10] += (uint64_t)__popcll(__ballot(amb[j]));  // (records decided on the exact node)
+      }
+      if (__ballot(anyamb)) {  // (rare) the exact node record, from global memory
+#pragma unroll
+        for (int j = 0; j < kLC; j++) {
+          if (!amb[j]) continue;
+          const uint64_t fa = k0key + addr[j], ft = xr[j].esc ? ts[j] : lp.xl.tbase + ts[j];
+          const uint4* gq = lp.pe_nodes + (uint64_t(q) * kPartSlots + (uint32_t)r[j]) * 2;
+          const uint4 na = gq[0], nb = gq[1];
+          if (entry_match(na, nb, fa, ft)) {
+            erel[j] = (int32_t)((s_pn[r[j]].w >> 16) & 2047u);
+            pofs[j] = fa - u64of(na.x, na.y);
+            hrel[j] = s_info[r[j]].x;
+          } else {
+            older[j] = ((s_pn[r[j]].w >> 27) & 1u) != 0;
+          }
+        }
+        vm_drain();
       }
       bool anyold = false;
 #pragma unroll
@@ -1290,11 +1362,13 @@ __global__ __launch_bounds__(kLWG, 1) void local_kernel(LocalParams lp) {
 #pragma unroll
         for (int j = 0; j < kLC; j++) {
           if (!older[j]) continue;
+          const uint64_t fa = k0key + addr[j], ft = xr[j].esc ? ts[j] : lp.xl.tbase + ts[j];
           const uint4 d = reinterpret_cast<const uint4*>(p.nodes + pi.k0 + (uint32_t)r[j])[3];  // (count, first)
-          uint64_t hist = kHistSparse;
-          const int32_t pos = match_older_pos(p, d.y, d.x, addr[j], ts[j], baddr[j], hist);
+          uint64_t hist = kHistSparse, baddr = 0;
+          const int32_t pos = match_older_pos(p, d.y, d.x, fa, ft, baddr, hist);
           if (pos >= 0) {
             erel[j] = pos - (int32_t)pi.e0;
+            pofs[j] = fa - baddr;
             hrel[j] = hist == kHistSparse ? kEmpty32
                       : PACKED && pi.cmap != ~0u ? lp.pe_lrel[pos]
                                          : (uint32_t)(hist - pi.cb);
@@ -1349,7 +1423,7 @@ __global__ __launch_bounds__(kLWG, 1) void local_kernel(LocalParams lp) {
         bool glob = false;
 #pragma unroll
         for (int j = 0; j < kLC; j++) {
-          page[j] = uint32_t(int(uint64_t(addr[j] - baddr[j]) / kPageSize));
+          page[j] = uint32_t(int(pofs[j] / kPageSize));
           if (erel[j] >= 0 && hrel[j] != kEmpty32 && ncell) {
             const uint32_t c = xr[j].th * pi.span + hrel[j] + page[j];
             atomicAdd(&s_pg[c >> 1], 1u << (16 * (c & 1)));
@@ -1474,6 +1548,8 @@ __global__ __launch_bounds__(kLWG, 1) void local_kernel(LocalParams lp) {
     o[9] = nchunks;
     o[10] = nit;
     o[11] = rt.acc[9];
+    o[12] = rt.acc[10];
+    o[13] = rt.acc[11];
   }
 }
 

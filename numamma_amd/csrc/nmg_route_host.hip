@@ -194,6 +194,7 @@ int route_analyze_job(nmg_engine* h, const RouteJob& job) {
   lp.pe_keys = h->d_pe_keys;
   lp.pe_nodes = h->d_pe_nodes;
   lp.pe_info = h->d_pe_info;
+  lp.pe_pnode = h->d_pe_pnode;
   lp.pe_dir = h->d_pe_dir;
   lp.pe_ids = h->d_pe_ids;
   lp.pe_lrel = h->d_pe_lrel;

@@ -277,16 +277,22 @@ int build_partitions(nmg_engine* h, const uint64_t* keys, const uint32_t* entry_
   for (const DevEntry& d : dev)
     if (d.alloc) h->route_tbase = std::min<uint64_t>(h->route_tbase, d.alloc);
   if (h->route_tbase == ~0ull) h->route_tbase = 0;
-  // per partition: keys ascending with their newest entry's node record and
-  // info, and a directory over the key span: slot j starts at first key + (j
-  // << dshift) and holds the index of the largest key <= that start and the
-  // number of keys inside the slot (the last slot: every key after its start)
+  // per partition: keys ascending with their newest entry's node record (the
+  // exact one, read by the local pass's rare paths), its packed form and
+  // info (the common path), and a directory over the key span: slot j starts
+  // at first key + (j << dshift) and holds the index of the largest key <=
+  // that start, the number of keys inside the slot (the last slot: every key
+  // after its start) and the first kDirInline of those keys' offsets from the
+  // slot start when they fit 16 bits (PartDir)
+  const uint64_t tb = h->route_tbase;
   std::vector<uint64_t> pk((size_t)P * kPartSlots, ~0ull);
   std::vector<uint4> pn((size_t)P * kPartSlots * 2, make_uint4(0, 0, 0, 0));
+  std::vector<uint4> ppn((size_t)P * kPartSlots, make_uint4(0, 0, 0, 0));
   std::vector<uint2> pinf((size_t)P * kPartSlots, make_uint2(kEmpty32, 0));
-  std::vector<uint32_t> pdir((size_t)P * kPartDir, 0);
+  std::vector<uint4> pdir((size_t)P * kPartDir, make_uint4(0, 0, 0, 0));
   for (uint32_t q = 0; q < P; q++) {
     const PartInfo& pi = parts[q];
+    const uint64_t f = keys[pi.k0];
     for (uint32_t r = 0; r < pi.nk; r++) {
       const uint32_t kk = pi.k0 + r;
       const DevEntry& d = dev[entry_off[kk]];
@@ -294,13 +300,29 @@ int build_partitions(nmg_engine* h, const uint64_t* keys, const uint32_t* entry_
       pk[o] = keys[kk];
       pn[2 * o] = make_uint4((uint32_t)d.addr, (uint32_t)(d.addr >> 32), (uint32_t)d.end, (uint32_t)(d.end >> 32));
       pn[2 * o + 1] = make_uint4((uint32_t)d.alloc, (uint32_t)(d.alloc >> 32), (uint32_t)d.free, (uint32_t)(d.free >> 32));
-      const uint32_t older = entry_off[kk + 1] - entry_off[kk] > 1 ? 0x80000000u : 0u;
+      const uint32_t older = entry_off[kk + 1] - entry_off[kk] > 1 ? 1u : 0u;
       const uint32_t hrel = d.hist == kHistSparse ? kEmpty32
                             : pi.cmap != ~0u         ? lrel[entry_off[kk]]
                                                      : (uint32_t)(d.hist - pi.cb);
-      pinf[o] = make_uint2(hrel, (entry_off[kk] - pi.e0) | older);
+      const uint64_t krel = keys[kk] - f;
+      // packed node (PackedNode): exact only where the object starts at its
+      // key and its end and key fit the relative fields
+      const uint64_t erel = d.end - f;
+      const bool exact = d.addr != keys[kk] || d.end < keys[kk] || (erel >> kAddrBits) != 0 || (krel >> 32) != 0;
+      uint64_t aq, fq;
+      if (d.free < tb) {  // (freed before the first allocation: no non-escaped sample can match)
+        aq = kPnQMax;
+        fq = 0;
+      } else {
+        aq = std::min<uint64_t>((d.alloc > tb ? d.alloc - tb : 0) >> kPnQShift, kPnQMax);
+        fq = std::min<uint64_t>((d.free - tb) >> kPnQShift, kPnQMax);
+      }
+      const uint64_t e40 = exact ? 0 : erel;
+      ppn[o] = make_uint4((uint32_t)e40, (uint32_t)(e40 >> 32) | ((uint32_t)aq << 8),
+                          (uint32_t)(aq >> 24) | ((uint32_t)fq << 12),
+                          (uint32_t)(fq >> 20) | ((entry_off[kk] - pi.e0) << 16) | (older << 27) | ((exact ? 1u : 0u) << 28));
+      pinf[o] = make_uint2(hrel, (uint32_t)krel);
     }
-    const uint64_t f = keys[pi.k0];
     uint32_t lo = 0;
     for (uint32_t j = 0; j < kPartDir; j++) {
       const uint64_t s0 = (uint64_t)j << pi.dshift;  // slot start relative to the first key
@@ -309,7 +331,19 @@ int build_partitions(nmg_engine* h, const uint64_t* keys, const uint32_t* entry_
       while (lo + 1 + c < pi.nk &&
              (j == kPartDir - 1 || keys[pi.k0 + lo + 1 + c] - f < s0 + (1ull << pi.dshift)))
         c++;
-      pdir[(size_t)q * kPartDir + j] = lo | (c << 16);
+      uint32_t off[kDirInline];
+      bool inl = true;
+      for (uint32_t i = 0; i < kDirInline; i++) {
+        off[i] = 0xffffu;
+        if (i < c) {
+          const uint64_t v = keys[pi.k0 + lo + 1 + i] - f - s0;
+          if (v >> 16) inl = false;
+          else off[i] = (uint32_t)v;
+        }
+      }
+      pdir[(size_t)q * kPartDir + j] =
+          make_uint4(lo | (c << 10) | ((inl && c ? 1u : 0u) << 21), off[0] | (off[1] << 16), off[2] | (off[3] << 16),
+                     off[4] | (off[5] << 16));
     }
   }
   // the route pass's partition search: the partitions' first keys ascending,
@@ -323,8 +357,9 @@ int build_partitions(nmg_engine* h, const uint64_t* keys, const uint32_t* entry_
   HIP_TRY(h, alloc_copy(h, (void**)&h->d_pdir, rdir.data(), rdir.size() * 2));
   HIP_TRY(h, alloc_copy(h, (void**)&h->d_pe_keys, pk.data(), pk.size() * 8));
   HIP_TRY(h, alloc_copy(h, (void**)&h->d_pe_nodes, pn.data(), pn.size() * sizeof(uint4)));
+  HIP_TRY(h, alloc_copy(h, (void**)&h->d_pe_pnode, ppn.data(), ppn.size() * sizeof(uint4)));
   HIP_TRY(h, alloc_copy(h, (void**)&h->d_pe_info, pinf.data(), pinf.size() * sizeof(uint2)));
-  HIP_TRY(h, alloc_copy(h, (void**)&h->d_pe_dir, pdir.data(), pdir.size() * 4));
+  HIP_TRY(h, alloc_copy(h, (void**)&h->d_pe_dir, pdir.data(), pdir.size() * sizeof(uint4)));
   if (ids) {
     HIP_TRY(h, alloc_copy(h, (void**)&h->d_pe_ids, ids, (size_t)entry_off[K] * 4));
     HIP_TRY(h, alloc_copy(h, (void**)&h->d_pe_lrel, lrel.data(), lrel.size() * 4));

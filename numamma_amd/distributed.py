@@ -151,6 +151,66 @@ class HistPacker:
         return self.cells + nmax * 8
 
 
+GLOBAL_SUM_WORDS = 2 * 39  # sum64's head: [2 access][39] global sums (nmg_internal.h kGlobalSums)
+
+
+class ObjPacker:
+    """Buffers of the packed per-object counter merge of one engine
+    (nmg_objcw_pack / nmg_objcw_unpack): sum64's four count / weight rows as
+    u32 words -- a value below 2^32 / world, so that the sum over the ranks
+    fits -- plus a list of the larger values as (row word, value) pairs
+    (allocated once; the list holds up to `ovf_frac` of the words)."""
+
+    def __init__(self, eng, device, ovf_frac: float = 1 / 64):
+        import torch
+
+        from . import _lib
+
+        self.eng = eng
+        n = eng.array_size(_lib.NMG_ARR_SUM64)
+        per = 78 if (eng.flags & _lib.NMG_F_OBJECT_LEVELS) else 4  # (levels: [E][2][37] after the rows)
+        self.E = (n - GLOBAL_SUM_WORDS) // per if n else 0
+        self.rows = 4 * self.E
+        self.cap = max(1024, int(self.rows * ovf_frac))
+        self.u32 = torch.empty(max(self.rows, 1), dtype=torch.int32, device=device)
+        self.ovf = torch.empty(2 * self.cap, dtype=torch.int64, device=device)
+        self.n = torch.zeros(1, dtype=torch.int64, device=device)
+
+    def merge(self, t, dst: int = 0, group=None):
+        """The rows of the sum64 image t (every rank's) summed into rank dst's
+        t; returns the bytes this rank contributed, or None when some rank's
+        list outgrew its buffer (the caller reduces the rows as u64)."""
+        import torch
+        import torch.distributed as dist
+
+        world = dist.get_world_size(group)
+        rank = dist.get_rank(group)
+        thr = (1 << 32) // world
+        n = self.eng.objcw_pack(t.data_ptr(), thr, self.u32.data_ptr(), self.ovf.data_ptr(), self.cap)
+        self.n.fill_(n)
+        _collective(self.n, dist.ReduceOp.MAX, None, group)
+        nmax = int(self.n.item())
+        if nmax > self.cap:
+            return None
+        if n < nmax:
+            self.ovf[2 * n:2 * nmax].zero_()  # (padding: row word 0 += 0)
+        _collective(self.u32[:self.rows], dist.ReduceOp.SUM, dst, group)  # (u32 sums as int32: the same bits)
+        part = self.ovf[:2 * nmax]
+        if dist.get_backend(group) == "nccl":
+            out = [torch.empty_like(part) for _ in range(world)] if rank == dst else None
+            dist.gather(part, out, dst=dst, group=group)
+        else:  # (gloo test runs: host staging)
+            cpu = part.cpu()
+            out = [torch.empty_like(cpu) for _ in range(world)] if rank == dst else None
+            dist.gather(cpu, out, dst=dst, group=group)
+        if rank == dst:
+            allovf = torch.cat([o.to(self.u32.device) for o in out]) if nmax else self.ovf[:0]
+            torch.cuda.synchronize(self.u32.device)
+            self.eng.objcw_unpack(t.data_ptr(), self.u32.data_ptr(), allovf.data_ptr() if nmax else 0,
+                                  allovf.numel() // 2)
+        return self.rows * 4 + nmax * 16
+
+
 def gather_arrays(a: np.ndarray, dst: int = 0, group=None):
     """Variable-length gather of a numpy array; returns the list on dst."""
     import torch.distributed as dist
@@ -175,7 +235,8 @@ def merge_sparse(parts) -> Tuple[np.ndarray, np.ndarray]:
 def merge_engine(eng, dst: int = 0, group=None, device=None, packed_hist: bool = False) -> int:
     """Merge every rank's partial counters into rank dst's engine (RCCL reduce
     of the dense arrays over xGMI; gathers of the small variable-length ones).
-    packed_hist: the page histogram through HistPacker (bytes + overflow).
+    packed_hist: the page histogram through HistPacker (bytes + overflow)
+    and the per-object counters through ObjPacker (u32 words + overflow).
     Returns the bytes this rank contributed to the dense collectives."""
     import torch
     import torch.distributed as dist
@@ -189,10 +250,23 @@ def merge_engine(eng, dst: int = 0, group=None, device=None, packed_hist: bool =
         n = eng.array_size(which)
         if n == 0:
             continue
-        nbytes += 8 * n
         t = torch.empty(n, dtype=torch.int64, device=dev)
         eng.export_array(which, t.data_ptr())
-        reduce_u64(t, op, dst=dst, group=group)
+        got = None
+        if packed_hist and which == _lib.NMG_ARR_SUM64:  # the per-object rows as u32 + a list
+            op_ = getattr(eng, "_obj_packer", None)
+            if op_ is None or op_.E * 4 + GLOBAL_SUM_WORDS > n:
+                op_ = eng._obj_packer = ObjPacker(eng, dev)
+            got = op_.merge(t, dst=dst, group=group)
+            if got is not None:
+                nbytes += got
+                rest = [t[:GLOBAL_SUM_WORDS]] + ([t[GLOBAL_SUM_WORDS + op_.rows:]] if n > GLOBAL_SUM_WORDS + op_.rows else [])
+                for part in rest:  # the global sums (and per-object levels) as u64
+                    nbytes += 8 * part.numel()
+                    reduce_u64(part, "sum", dst=dst, group=group)
+        if got is None:
+            nbytes += 8 * n
+            reduce_u64(t, op, dst=dst, group=group)
         if rank == dst:
             torch.cuda.synchronize(dev)
             eng.import_array(which, t.data_ptr())

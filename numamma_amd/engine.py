@@ -292,6 +292,17 @@ class Engine:
     def hist_unpack(self, d_u8: int, d_ovf: int, n_ovf: int):
         self._c(lib.nmg_hist_unpack(self.h, C.c_void_p(d_u8), C.c_void_p(d_ovf), n_ovf))
 
+    def objcw_pack(self, d_sum64: int, threshold: int, d_u32: int, d_ovf: int, ovf_cap: int) -> int:
+        """nmg_objcw_pack over a sum64 image: returns the number of (row word,
+        value) pairs (> ovf_cap: the list is incomplete)."""
+        n = C.c_uint64(0)
+        self._c(lib.nmg_objcw_pack(self.h, C.c_void_p(d_sum64), threshold, C.c_void_p(d_u32), C.c_void_p(d_ovf),
+                                   ovf_cap, C.byref(n)))
+        return n.value
+
+    def objcw_unpack(self, d_sum64: int, d_u32: int, d_ovf: int, n_ovf: int):
+        self._c(lib.nmg_objcw_unpack(self.h, C.c_void_p(d_sum64), C.c_void_p(d_u32), C.c_void_p(d_ovf), n_ovf))
+
     def sparse_export(self):
         n = lib.nmg_sparse_count(self.h)
         self._c(n)

@@ -158,3 +158,52 @@ def test_hist_pack_round_trip(threshold, threads):
     eng.export_array(_lib.NMG_ARR_HIST32, after.data_ptr())
     assert np.array_equal(after.cpu().numpy().view(np.uint32), ref)
     eng.close()
+
+
+@pytest.mark.parametrize("threshold", [1, 7, 1000, 1 << 32])
+def test_objcw_pack_round_trip(threshold):
+    """nmg_objcw_pack then nmg_objcw_unpack on one sum64 image gives back the
+    per-object count / weight rows: values below the threshold as u32 words,
+    the others as (row word, value) pairs; a list longer than its capacity
+    reports its full length; the global sums ahead of the rows are not
+    touched."""
+    import torch
+
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "oracle")]
+    from numamma_amd import _lib
+    from numamma_amd.distributed import GLOBAL_SUM_WORDS
+    from numamma_amd.engine import Engine
+    from numamma_amd.replay import SynthConfig, generate
+
+    rp = generate(SynthConfig(nb_samples=300_000, nb_intervals=20_000, seed=24))
+    eng = Engine(device=0, nb_threads=rp.nb_threads)
+    eng.set_objects(rp.table)
+    eng.submit_replay(rp)
+    eng.analyze()
+    eng.synchronize()
+    dev = torch.device("cuda", 0)
+    n = eng.array_size(_lib.NMG_ARR_SUM64)
+    t = torch.empty(n, dtype=torch.int64, device=dev)
+    eng.export_array(_lib.NMG_ARR_SUM64, t.data_ptr())
+    ref = t.cpu().numpy().view(np.uint64).copy()
+    E = (n - GLOBAL_SUM_WORDS) // 4
+    rows = ref[GLOBAL_SUM_WORDS:GLOBAL_SUM_WORDS + 4 * E]
+    u32 = torch.empty(4 * E, dtype=torch.int32, device=dev)
+    cap = 4 * E
+    ovf = torch.empty(2 * cap, dtype=torch.int64, device=dev)
+    nb = eng.objcw_pack(t.data_ptr(), threshold, u32.data_ptr(), ovf.data_ptr(), cap)
+    big = rows >= np.uint64(threshold)
+    assert nb == int(big.sum())
+    assert np.array_equal(u32.cpu().numpy().view(np.uint32), np.where(big, 0, rows).astype(np.uint32))
+    pairs = ovf[:2 * nb].cpu().numpy().view(np.uint64).reshape(-1, 2)
+    order = np.argsort(pairs[:, 0])
+    assert np.array_equal(pairs[order, 0], np.nonzero(big)[0].astype(np.uint64))
+    assert np.array_equal(pairs[order, 1], rows[big])
+    if nb > 1:
+        assert eng.objcw_pack(t.data_ptr(), threshold, u32.data_ptr(), ovf.data_ptr(), nb - 1) == nb  # (short)
+        eng.objcw_pack(t.data_ptr(), threshold, u32.data_ptr(), ovf.data_ptr(), cap)
+    t[GLOBAL_SUM_WORDS:].fill_(-1)  # the rows rebuilt from the words and the list alone
+    torch.cuda.synchronize(dev)
+    eng.objcw_unpack(t.data_ptr(), u32.data_ptr(), ovf.data_ptr(), nb)
+    assert np.array_equal(t.cpu().numpy().view(np.uint64), ref)
+    eng.close()

@@ -77,6 +77,9 @@ def main():
             per = ch if k < 6 else it
             out[f"{name}_cyc_per_{'chunk' if k < 6 else 'item'}"] = float(a[:, k].sum() / per)
         out["imbalance_cyc_per_item"] = float(a[:, 11].sum() / it)  # waiting for the item's slowest wave
+        recs = ch * 64
+        out["exact_node_frac"] = float(a[:, 12].sum() / recs)  # decided on the exact node record (global)
+        out["key_search_frac"] = float(a[:, 13].sum() / recs)  # lookups that read keys past the directory
         out["total_cyc_per_wave"] = float((a[:, :9].sum(axis=1) + a[:, 11]).mean())
         out["max_total_cyc_per_wave"] = float((a[:, :9].sum(axis=1) + a[:, 11]).max())
         print(json.dumps(out), flush=True)
