@@ -203,6 +203,8 @@ _SIGS = {
 }
 
 for _name, (_res, _args) in _SIGS.items():
+    if os.environ.get("NMG_LIB_PATH") and not hasattr(lib, _name):
+        continue  # (A/B timing of an older build: functions it predates stay unbound)
     _fn = getattr(lib, _name)  # AttributeError == missing export: fail loudly
     _fn.restype = _res
     _fn.argtypes = _args

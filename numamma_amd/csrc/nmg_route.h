@@ -61,15 +61,15 @@ constexpr uint32_t kPartDir = 1024;        // directory slots per partition (rad
 // a lookup counts the offsets <= its own and reads keys only past them
 constexpr uint32_t kDirInline = 6;
 // PackedNode, a key's newest entry for the local pass's common path (16 B):
-//   end - first key (40 bits) | alloc_q (36) | free_q (36) | table position
-//   - e0 (11) | older entries (1) | exact (1)
-// with alloc_q / free_q = (date - tbase) >> kPnQShift, saturated (an entry
-// freed before tbase: alloc_q = max, free_q = 0).  A sample whose quantised
-// timestamp equals either bound, or a key marked exact (its object does not
-// start at the key, or its end or key offset does not fit), is decided on
-// the exact node record instead.
-constexpr uint32_t kPnQShift = 4;
-constexpr uint64_t kPnQMax = (1ull << 36) - 1;
+//   x = end - first key, y = alloc_q, z = free_q, w = table position - e0
+//   (11 bits) | kPnOlder | kPnExact
+// with alloc_q / free_q = (date - tbase) >> kPnQShift, saturated to 32 bits
+// (an entry freed before tbase: alloc_q = ~0, free_q = 0, no sample
+// matches).  A sample whose quantised timestamp equals either bound, or a
+// key marked exact (its object does not start at the key, or its end or key
+// offset needs more than 32 bits), is decided on the exact node record.
+constexpr uint32_t kPnQShift = 8;
+constexpr uint32_t kPnOlder = 1u << 11, kPnExact = 1u << 12;
 constexpr uint32_t kPartEntries = 1536;    // entries per partition (LDS object counters)
 constexpr uint32_t kPartCells = 28672;     // u16 page cells per partition: nb_threads x cell span
 constexpr uint32_t kItemChunks = 1023;     // chunks per work item: < 2^16 records, so u16 page cells
@@ -123,8 +123,10 @@ static_assert(sizeof(PartInfo) == 48, "PartInfo");
 // global counters were done by the route pass)
 //   lo = addr - partition start (kAddrBits) | (ts - tbase) << kAddrBits (low 24 bits)
 //   hi = (ts - tbase) >> 24 (16 bits) | min(weight, wesc) << 16 (wbits)
-//        | location << (16 + wbits): buffer index g (gbits), byte offset / 8
-//        (obits), thread rank (tbits), access type (1)
+//        | location << (16 + wbits): byte offset / 8 (obits), then buffer
+//          index g (gbits) -- ordered as the analysis position, so the local
+//          pass keeps first matches as locations --
+//        | thread rank << (63 - tbits) | access type << 63
 // A record whose address, timestamp or weight does not fit carries wesc: the
 // local pass re-reads all three from the raw record (rare).
 constexpr uint32_t kAddrBits = 40;

@@ -64,8 +64,13 @@ __device__ __forceinline__ uint32_t route_partition(const RouteParams& rp, const
 
 struct XRec {
   uint64_t addr, ts, w;
-  uint32_t g, off, th, acc;
+  uint64_t loc;  // byte offset / 8 | buffer index << obits: ordered as the analysis position
+  uint32_t th, acc;
   bool esc;  // addr, ts and w are still to be re-read from the raw record (x_resolve)
+  __device__ __forceinline__ uint32_t g(const XLayout& xl) const { return uint32_t(loc >> xl.obits); }
+  __device__ __forceinline__ uint32_t off(const XLayout& xl) const {
+    return uint32_t(loc & ((1ull << xl.obits) - 1)) << 3;
+  }
 };
 
 // the record of a SAMPLE routed to the partition starting at pb (addr >= pb)
@@ -74,33 +79,11 @@ __device__ __forceinline__ uint4 x_encode(const XLayout& xl, uint64_t pb, uint64
   const uint64_t ar = addr - pb, tr = ts - xl.tbase;
   const bool fit = (ar >> kAddrBits) == 0 && ts >= xl.tbase && (tr >> kTsBits) == 0 && w < xl.wesc;
   const uint64_t a = fit ? ar : 0ull, t = fit ? tr : 0ull, wq = fit ? w : xl.wesc;
-  const uint64_t loc = uint64_t(g) | (uint64_t(off >> 3) << xl.gbits) | (uint64_t(th) << (xl.gbits + xl.obits)) |
-                       (uint64_t(acc) << (xl.gbits + xl.obits + xl.tbits));
+  const uint64_t loc = uint64_t(off >> 3) | (uint64_t(g) << xl.obits);
   const uint64_t lo = a | (t << kAddrBits);
-  const uint64_t hi = (t >> (64 - kAddrBits)) | (wq << 16) | (loc << (16 + xl.wbits));
+  const uint64_t hi = (t >> (64 - kAddrBits)) | (wq << 16) | (loc << (16 + xl.wbits)) |
+                      (uint64_t(th) << (63 - xl.tbits)) | (uint64_t(acc) << 63);
   return make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
-}
-
-// bits [start, start + width) of the 64-bit value hi:lo, width <= 32 (32-bit
-// funnel shifts: the local pass decodes two records per lane per step)
-__device__ __forceinline__ uint32_t bits64(uint32_t lo, uint32_t hi, uint32_t start, uint32_t mask) {
-  return (start < 32 ? __builtin_amdgcn_alignbit(hi, lo, start) : hi >> (start - 32)) & mask;
-}
-
-__device__ __forceinline__ XRec x_decode(const XLayout& xl, uint64_t pb, uint4 v) {
-  XRec r;
-  r.addr = pb + u64of(v.x, v.y & 0xffu);
-  r.ts = xl.tbase + u64of(__builtin_amdgcn_alignbit(v.z, v.y, 8), (v.z >> 8) & 0xffu);
-  const uint32_t wesc = (uint32_t)xl.wesc;
-  r.w = __builtin_amdgcn_alignbit(v.w, v.z, 16) & wesc;
-  r.esc = r.w == wesc;
-  // the location from bit 16 + wbits of hi = v.w:v.z
-  const uint32_t l0 = 16 + xl.wbits;
-  r.g = bits64(v.z, v.w, l0, (1u << xl.gbits) - 1);
-  r.off = bits64(v.z, v.w, l0 + xl.gbits, (1u << xl.obits) - 1) << 3;
-  r.th = bits64(v.z, v.w, l0 + xl.gbits + xl.obits, (1u << xl.tbits) - 1);
-  r.acc = bits64(v.z, v.w, l0 + xl.gbits + xl.obits + xl.tbits, 1u);
-  return r;
 }
 
 // x_decode without the bases: addr = the offset from the partition's first
@@ -112,18 +95,23 @@ __device__ __forceinline__ XRec x_decode_rel(const XLayout& xl, uint4 v) {
   const uint32_t wesc = (uint32_t)xl.wesc;
   r.w = __builtin_amdgcn_alignbit(v.w, v.z, 16) & wesc;
   r.esc = r.w == wesc;
-  const uint32_t l0 = 16 + xl.wbits;
-  r.g = bits64(v.z, v.w, l0, (1u << xl.gbits) - 1);
-  r.off = bits64(v.z, v.w, l0 + xl.gbits, (1u << xl.obits) - 1) << 3;
-  r.th = bits64(v.z, v.w, l0 + xl.gbits + xl.obits, (1u << xl.tbits) - 1);
-  r.acc = bits64(v.z, v.w, l0 + xl.gbits + xl.obits + xl.tbits, 1u);
+  r.loc = (u64of(v.z, v.w) >> (16 + xl.wbits)) & ((1ull << (xl.obits + xl.gbits)) - 1);
+  r.th = (v.w >> (31 - xl.tbits)) & ((1u << xl.tbits) - 1);
+  r.acc = v.w >> 31;
+  return r;
+}
+
+__device__ __forceinline__ XRec x_decode(const XLayout& xl, uint64_t pb, uint4 v) {
+  XRec r = x_decode_rel(xl, v);
+  r.addr += pb;
+  r.ts += xl.tbase;
   return r;
 }
 
 // an escaped record's address, timestamp and weight from the raw record
 // (struct mem_sample after the 8 B header: timestamp, addr, weight)
-__device__ __forceinline__ void x_resolve(XRec& r, const uint8_t* data, const BufDesc* descs) {
-  const uint64_t* q = reinterpret_cast<const uint64_t*>(data + descs[r.g].offset + r.off);
+__device__ __forceinline__ void x_resolve(XRec& r, const XLayout& xl, const uint8_t* data, const BufDesc* descs) {
+  const uint64_t* q = reinterpret_cast<const uint64_t*>(data + descs[r.g(xl)].offset + r.off(xl));
   r.ts = q[1];
   r.addr = q[2];
   r.w = q[3];
@@ -898,8 +886,9 @@ __global__ __launch_bounds__(kR2WG, 1) void route2_kernel(RouteParams rp) {
             rp.ovfx[o] = pbq;
           } else {  // attributed at once
             XRec xr = x_decode(rp.xl, pbq, a);
-            if (xr.esc) x_resolve(xr, p.data, p.sbufs);
-            direct_attribute(p, xr.addr, xr.ts, xr.w, xr.th, xr.acc, 0, rp.seq0 + xr.g, xr.off, xr.g);
+            if (xr.esc) x_resolve(xr, rp.xl, p.data, p.sbufs);
+            direct_attribute(p, xr.addr, xr.ts, xr.w, xr.th, xr.acc, 0, rp.seq0 + xr.g(rp.xl), xr.off(rp.xl),
+                             xr.g(rp.xl));
           }
         }
         vm_drain();  // (rare: nothing of this path stays pending where it joins the window)
@@ -963,8 +952,9 @@ __global__ __launch_bounds__(256) void overflow_kernel(RouteParams rp) {
   const uint32_t n = min(*rp.ovf_cnt, rp.ovf_cap);
   for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
     XRec xr = x_decode(rp.xl, rp.ovfx[i], rp.ovf16[i]);
-    if (xr.esc) x_resolve(xr, rp.p.data, rp.p.sbufs);
-    direct_attribute(rp.p, xr.addr, xr.ts, xr.w, xr.th, xr.acc, 0, rp.seq0 + xr.g, xr.off, xr.g);
+    if (xr.esc) x_resolve(xr, rp.xl, rp.p.data, rp.p.sbufs);
+    direct_attribute(rp.p, xr.addr, xr.ts, xr.w, xr.th, xr.acc, 0, rp.seq0 + xr.g(rp.xl), xr.off(rp.xl),
+                     xr.g(rp.xl));
   }
 }
 
@@ -1230,7 +1220,7 @@ __global__ __launch_bounds__(kLWG, 1) void local_kernel(LocalParams lp) {
 #pragma unroll
         for (int j = 0; j < kLC; j++)
           if (valid[j] && xr[j].esc) {
-            x_resolve(xr[j], p.data, lp.descs);
+            x_resolve(xr[j], lp.xl, p.data, lp.descs);
             xr[j].addr -= k0key;  // (>= 0: routed to this partition); ts stays absolute
           }
         vm_drain();
@@ -1317,18 +1307,16 @@ __global__ __launch_bounds__(kLWG, 1) void local_kernel(LocalParams lp) {
         if (r[j] >= 0 && !(p.flags & kDbgLocalNoSearch)) {
           const uint4 pn = s_pn[r[j]];
           const uint2 inf = s_info[r[j]];
-          const uint64_t end = u64of(pn.x, pn.y & 0xffu);
-          const uint64_t aq = u64of((pn.y >> 8) | (pn.z << 24), (pn.z >> 8) & 0xfu);
-          const uint64_t fq = u64of((pn.z >> 12) | (pn.w << 20), (pn.w >> 12) & 0xfu);
-          const uint64_t tq = ts[j] >> kPnQShift;
-          const bool in = addr[j] < end;
-          amb[j] = xr[j].esc || ((pn.w >> 28) & 1u) || (in && (tq == aq || tq == fq));
-          if (!amb[j] && in && tq > aq && tq < fq) {
-            erel[j] = (int32_t)((pn.w >> 16) & 2047u);
+          // (the offsets are < 2^40: the timestamp's quantum fits 32 bits)
+          const uint32_t tq = __builtin_amdgcn_alignbit((uint32_t)(ts[j] >> 32), (uint32_t)ts[j], kPnQShift);
+          const bool in = addr[j] < (uint64_t)pn.x;
+          amb[j] = xr[j].esc || (pn.w & kPnExact) || (in && (tq == pn.y || tq == pn.z));
+          if (!amb[j] && in && tq > pn.y && tq < pn.z) {
+            erel[j] = (int32_t)(pn.w & 2047u);
             pofs[j] = addr[j] - inf.y;
             hrel[j] = inf.x;
           } else if (!amb[j]) {
-            older[j] = ((pn.w >> 27) & 1u) != 0;
+            older[j] = (pn.w & kPnOlder) != 0;
           }
         }
       }
@@ -1346,11 +1334,11 @@ __global__ __launch_bounds__(kLWG, 1) void local_kernel(LocalParams lp) {
           const uint4* gq = lp.pe_nodes + (uint64_t(q) * kPartSlots + (uint32_t)r[j]) * 2;
           const uint4 na = gq[0], nb = gq[1];
           if (entry_match(na, nb, fa, ft)) {
-            erel[j] = (int32_t)((s_pn[r[j]].w >> 16) & 2047u);
+            erel[j] = (int32_t)(s_pn[r[j]].w & 2047u);
             pofs[j] = fa - u64of(na.x, na.y);
             hrel[j] = s_info[r[j]].x;
           } else {
-            older[j] = ((s_pn[r[j]].w >> 27) & 1u) != 0;
+            older[j] = (s_pn[r[j]].w & kPnOlder) != 0;
           }
         }
         vm_drain();
@@ -1404,17 +1392,16 @@ __global__ __launch_bounds__(kLWG, 1) void local_kernel(LocalParams lp) {
         }
         vm_drain();
       }
-      // first match in analysis order (quirk Q7)
+      // first match in analysis order (quirk Q7): the compact record's
+      // location (buffer index, byte offset) orders as the ordinal does; the
+      // flush turns the minimum into (seq << 32) | offset
       if (!noobj) {  // (read first: an unconditional LDS min per match was 9 % slower, hot entries)
-        unsigned long long ord[kLC], cur[kLC];
+        unsigned long long cur[kLC];
 #pragma unroll
-        for (int j = 0; j < kLC; j++) {
-          ord[j] = ((lp.seq0 + xr[j].g) << 32) | xr[j].off;
-          cur[j] = erel[j] >= 0 ? s_first[erel[j]] : 0ull;
-        }
+        for (int j = 0; j < kLC; j++) cur[j] = erel[j] >= 0 ? s_first[erel[j]] : 0ull;
 #pragma unroll
         for (int j = 0; j < kLC; j++)
-          if (erel[j] >= 0 && ord[j] < cur[j]) atomicMin(&s_first[erel[j]], ord[j]);
+          if (erel[j] >= 0 && xr[j].loc < cur[j]) atomicMin(&s_first[erel[j]], (unsigned long long)xr[j].loc);
       }
       rt_stamp<TIMING>(rt, 4);
       if (pages && !(p.flags & kDbgLocalNoPage)) {
@@ -1438,7 +1425,8 @@ __global__ __launch_bounds__(kLWG, 1) void local_kernel(LocalParams lp) {
               atomicAdd(p.hist + uint64_t(xr[j].th) * p.hist_cells + pi.cb + hrel[j] + page[j], 1u);
             } else if (hrel[j] == kEmpty32) {
               const uint32_t sidx = p.entries[entry_id(lp, pi.e0 + (uint32_t)erel[j])].sidx;
-              if (sidx != ~0u) sparse_add(p, sparse_key(sidx, xr[j].th, page[j]), lp.seq0 + xr[j].g, xr[j].off, 1u);
+              if (sidx != ~0u)
+                sparse_add(p, sparse_key(sidx, xr[j].th, page[j]), lp.seq0 + xr[j].g(lp.xl), xr[j].off(lp.xl), 1u);
             }
           }
           vm_drain();
@@ -1492,9 +1480,10 @@ __global__ __launch_bounds__(kLWG, 1) void local_kernel(LocalParams lp) {
           if (wt) atomicAdd(reinterpret_cast<unsigned long long*>(pw), (unsigned long long)wt);
         }
       }
-      const uint64_t fo = s_first[i];
-      if (fo != ~0ull) {
+      const uint64_t floc = s_first[i];
+      if (floc != ~0ull) {
         s_first[i] = ~0ull;
+        const uint64_t fo = ((lp.seq0 + (floc >> lp.xl.obits)) << 32) | ((floc & ((1ull << lp.xl.obits) - 1)) << 3);
         uint64_t* pf = p.min64 + 36 + e;
         if (excl) *pf = min(l2_load(pf), fo);
         else atomicMin(reinterpret_cast<unsigned long long*>(pf), (unsigned long long)fo);

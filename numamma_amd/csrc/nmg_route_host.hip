@@ -236,7 +236,7 @@ int route_analyze_job(nmg_engine* h, const RouteJob& job) {
     f.bufcnt = h->d_bufcnt + job.index_base;
     f.nb_bufs = (uint32_t)h->bufcnt_stride;
     f.gbits = xl.gbits;
-    f.gshift = 16 + xl.wbits;
+    f.gshift = 16 + xl.wbits + xl.obits;
     HIP_TRY(h, launch_found(grid, h->stream, f));
     return NMG_OK;
   }
@@ -262,7 +262,7 @@ int route_settle(nmg_engine* h) {
   f.bufcnt = h->d_bufcnt;
   f.nb_bufs = (uint32_t)h->bufcnt_stride;
   f.gbits = h->route_xl.gbits;
-  f.gshift = 16 + h->route_xl.wbits;
+  f.gshift = 16 + h->route_xl.wbits + h->route_xl.obits;
   HIP_TRY(h, hipSetDevice(h->device));
   HIP_TRY(h, launch_found(h->route_grid, h->stream, f));
   return NMG_OK;

@@ -305,22 +305,24 @@ int build_partitions(nmg_engine* h, const uint64_t* keys, const uint32_t* entry_
                             : pi.cmap != ~0u         ? lrel[entry_off[kk]]
                                                      : (uint32_t)(d.hist - pi.cb);
       const uint64_t krel = keys[kk] - f;
-      // packed node (PackedNode): exact only where the object starts at its
-      // key and its end and key fit the relative fields
+      // packed node (PackedNode): exact where the object does not start at
+      // its key or its end or key offset needs more than 32 bits -- unless
+      // it was freed before the first allocation (the [stack], Q4): no
+      // non-escaped sample can match it, whatever its bounds
       const uint64_t erel = d.end - f;
-      const bool exact = d.addr != keys[kk] || d.end < keys[kk] || (erel >> kAddrBits) != 0 || (krel >> 32) != 0;
+      const bool never = d.free < tb;
+      const bool exact =
+          !never && (d.addr != keys[kk] || d.end < keys[kk] || (erel >> 32) != 0 || (krel >> 32) != 0);
       uint64_t aq, fq;
-      if (d.free < tb) {  // (freed before the first allocation: no non-escaped sample can match)
-        aq = kPnQMax;
+      if (never) {
+        aq = 0xffffffffull;
         fq = 0;
       } else {
-        aq = std::min<uint64_t>((d.alloc > tb ? d.alloc - tb : 0) >> kPnQShift, kPnQMax);
-        fq = std::min<uint64_t>((d.free - tb) >> kPnQShift, kPnQMax);
+        aq = std::min<uint64_t>((d.alloc > tb ? d.alloc - tb : 0) >> kPnQShift, 0xffffffffull);
+        fq = std::min<uint64_t>((d.free - tb) >> kPnQShift, 0xffffffffull);
       }
-      const uint64_t e40 = exact ? 0 : erel;
-      ppn[o] = make_uint4((uint32_t)e40, (uint32_t)(e40 >> 32) | ((uint32_t)aq << 8),
-                          (uint32_t)(aq >> 24) | ((uint32_t)fq << 12),
-                          (uint32_t)(fq >> 20) | ((entry_off[kk] - pi.e0) << 16) | (older << 27) | ((exact ? 1u : 0u) << 28));
+      ppn[o] = make_uint4(exact || never ? 0u : (uint32_t)erel, (uint32_t)aq, (uint32_t)fq,
+                          (entry_off[kk] - pi.e0) | (older ? kPnOlder : 0u) | (exact ? kPnExact : 0u));
       pinf[o] = make_uint2(hrel, (uint32_t)krel);
     }
     uint32_t lo = 0;
