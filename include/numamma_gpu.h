@@ -289,7 +289,9 @@ int nmg_set_device_buffers(nmg_engine *h, const void *d_data, const uint64_t *of
  * first).  Asynchronous; counters accumulate across calls. */
 int nmg_analyze(nmg_engine *h);
 int nmg_synchronize(nmg_engine *h);
-/* Zero every counter (global, per buffer, per object, page histogram). */
+/* Zero every counter (global, per buffer, per object, page histogram); per
+ * buffer counts replaced by nmg_set_buffer_counts are dropped (the engine's own
+ * buffers again). */
 int nmg_reset_counters(nmg_engine *h);
 /* Drop every submitted buffer (staging memory is kept for reuse). */
 int nmg_clear_buffers(nmg_engine *h);

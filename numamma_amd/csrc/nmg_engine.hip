@@ -380,6 +380,11 @@ extern "C" int nmg_reset_counters(nmg_engine* h) {
   if (h->multi && h->counts_override) {  // merged per-buffer counts (multi_finish)
     std::fill(h->ov_samples.begin(), h->ov_samples.end(), 0u);
     std::fill(h->ov_found.begin(), h->ov_found.end(), 0u);
+  } else if (h->counts_override) {  // a job's counts (nmg_set_buffer_counts): back to this engine's buffers
+    h->counts_override = false;
+    h->ov_samples.clear();
+    h->ov_found.clear();
+    h->ov_bytes.clear();
   }
   h->multi_found = 0;
   HIP_TRY(h, hipSetDevice(h->device));

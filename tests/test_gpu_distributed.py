@@ -55,9 +55,12 @@ def _worker(rank, world, port, workdir, cfg_name, ret, packed=False):
         eng.set_objects(rp.table)
         eng.set_device_buffers(d_arena.data_ptr(), offs[lo:hi] - base, lens[lo:hi], ranks[lo:hi], acc[lo:hi],
                                seq_base=lo)
-        eng.analyze()
-        eng.synchronize()
-        merge_engine(eng, dst=0, device=dev, packed_hist=packed)
+        for rep in range(2 if packed else 1):  # (packed: a second job on the same engines, reset in between --
+            if rep:                             # rank 0 drops the first merge's per-buffer counts)
+                eng.reset()
+            eng.analyze()
+            eng.synchronize()
+            merge_engine(eng, dst=0, device=dev, packed_hist=packed)
         if rank == 0:
             edir = os.path.join(workdir, "engine")
             eng.report(edir, os.path.join(workdir, "e.txt"))

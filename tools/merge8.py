@@ -63,6 +63,7 @@ def _worker(rank, world, port, shm, args, ret):
         dist.all_gather_object(nbuf, len(lens))
         seq_base = int(sum(nbuf[:rank]))
         t_gen = time.time() - t0
+        _log(f"rank {rank}: shard generated in {t_gen:.0f}s ({len(lens)} buffers)")
         # the bit-exact restatement of this shard (its own analysis order: seq
         # 0..), one rank at a time (host memory: a replay file in shm each)
         path = os.path.join(shm, f"shard{rank}.bin")
@@ -73,6 +74,7 @@ def _worker(rank, world, port, shm, args, ret):
                 rp.write(path)
                 tm = pyoracle.run_mt(path, raw, threads=args.mt_threads, levels=False)
                 os.remove(path)
+                _log(f"rank {rank}: restatement {tm['analysis_s']:.1f}s")
             dist.barrier()
         dev = torch.device("cuda", 0)
         d_arena = torch.from_numpy(arena).to(dev)
@@ -96,6 +98,7 @@ def _worker(rank, world, port, shm, args, ret):
             dist.barrier()
             tc = time.perf_counter()
             steps.append((tb - ta, tc - tb))
+            _log(f"rank {rank}: rep {rep} analyze {tb - ta:.3f}s merge {tc - tb:.3f}s")
         out = {"rank": rank, "seq_base": seq_base, "nb_buffers": len(lens), "gen_s": t_gen,
                "restatement_s": tm["analysis_s"], "payload_bytes": nbytes,
                "analyze_s": [s[0] for s in steps], "merge_s": [s[1] for s in steps]}
