@@ -184,108 +184,109 @@ struct RDesc {
   __device__ __forceinline__ uint32_t access() const { return ta >> 16; }
 };
 
-// update_counters(global_counters, ...) (mem_sampling.c:517-592) of both
-// access types in one per-lane accumulator, without a branch on the access:
-// counts of reads in the low and writes in the high 16 bits of a word,
-// weights summed per access.  The hit buckets of the first kDualGroups level
-// groups (L1, L2, L3, LFB, local RAM: the common PEBS levels) live here; the
-// other buckets, N/A... see route_count.  Drained at least every
-// kDrainWindows records per lane (u16 counts; weights < 2^23, 256 x 2^23 <
-// 2^31).
-constexpr int kDualGroups = 5;
-struct DualAcc {
-  uint32_t tc, na;                  // total count, N/A count: read | write << 16
-  uint32_t cnt[kDualGroups];        // hit bucket g counts: read | write << 16
-  uint32_t tw[2], sum[2][kDualGroups];  // weights per access
+// update_counters(global_counters, ...) (mem_sampling.c:517-592) in the
+// route pass: per lane and access type, one u32 per counter pair, count << 24
+// | weight sum, for the total and for kRtGroups buckets (the common PEBS
+// levels: hits in L1, LFB, L2, L3, local RAM and remote RAM, L3 misses); the
+// NA count.  A record whose weight reaches 2^16, or that falls in another
+// bucket, or in two, is counted -- those parts -- by LDS atomics.  Drained
+// every kRouteDrain windows (255 records of < 2^16 fit 24 bits).
+//
+// A record's level class: the hit levels x = lvl >> 3 (11 bits) when HIT,
+// else the miss levels at bit 11 when MISS (HIT beats MISS, quirk Q12).
+// Group g covers class bits kRtMask[g] and is bucket nibble g of kRtBucketNib.
+constexpr int kRtGroups = 7;
+__device__ __forceinline__ uint32_t rt_class(uint32_t lvl) {
+  const uint32_t x = lvl >> 3;
+  return (lvl & LVL_HIT) ? x : (lvl & LVL_MISS) ? x << 11 : 0u;
+}
+// groups: x0 L1 (bucket 0), x1 LFB (3), x2 L2 (1), x3 L3 (2), x4 local RAM
+// (4), x5|x6 remote RAM (5), miss x3 L3 (9 + 2)
+constexpr uint32_t kRtMask[kRtGroups] = {1u, 2u, 4u, 8u, 16u, 0x60u, 8u << 11};
+constexpr uint32_t kRtBucketNib = 0xB542130u;  // group g -> bucket (nibble g)
+constexpr uint32_t kRtKnown = 0x7fu | (8u << 11);
+constexpr uint32_t kRouteDrain = 128;
+constexpr uint32_t kRtOne = 1u << 24;
+struct RouteAcc {
+  uint32_t tot, na, g[kRtGroups];
 };
-
-__device__ __forceinline__ void dual_clear(DualAcc& a) {
-  a.tc = a.na = 0;
+__device__ __forceinline__ void racc_clear(RouteAcc& a) {
+  a.tot = a.na = 0;
 #pragma unroll
-  for (int g = 0; g < kDualGroups; g++) {
-    a.cnt[g] = 0;
-    a.sum[0][g] = a.sum[1][g] = 0;
-  }
-  a.tw[0] = a.tw[1] = 0;
+  for (int g = 0; g < kRtGroups; g++) a.g[g] = 0;
 }
 
-// update_counters(global_counters, sample) (mem_sampling.c:517-592) in the
-// route pass, for access type ACC (a wave window lies in one buffer, so its
-// access type is uniform and the caller branches on it once): register
-// buckets for the common levels, LDS for the rest; a minimum / maximum is
-// read first and updated by an LDS atomic only when the record moves it
+// the counting of one SAMPLE of access type ACC (a wave window lies in one
+// buffer: the caller branches on the access once); every lane of the wave
+// calls it, `valid` the ones with a SAMPLE.  The minimum / maximum of the
+// record's register bucket is read first and updated by an LDS atomic only
+// when the record moves it.
 template <uint32_t ACC>
-__device__ __forceinline__ void route_count(DualAcc& a, unsigned long long (*sums)[kGlobalSums],
+__device__ __forceinline__ void route_count(RouteAcc& a, unsigned long long (*sums)[kGlobalSums],
                                             unsigned long long (*mins)[18], unsigned long long (*maxs)[18],
-                                            uint32_t lvl, uint64_t w) {
-  const uint32_t bm = bucket_mask(lvl);
-  if (w < kLaneMaxWeight) {
-    const uint32_t w32 = (uint32_t)w;
-    constexpr uint32_t one = 1u << (16 * ACC);
-    a.tc += one;
-    a.na += (lvl & LVL_NA) ? one : 0u;
-    a.tw[ACC] += w32;
+                                            bool valid, uint32_t lvl, uint64_t w) {
+  const uint32_t cls = rt_class(lvl);
+  const bool big = w >= (1u << 16);
+  const uint32_t term = (valid && !big) ? (uint32_t)w + kRtOne : 0u;
+  a.tot += term;
+  a.na += (valid && !big) ? (lvl & LVL_NA) : 0u;
+  uint32_t gm = 0;  // the record's groups, one bit each
 #pragma unroll
-    for (int g = 0; g < kDualGroups; g++) {
-      const bool in = (bm >> g) & 1;
-      a.cnt[g] += in ? one : 0u;
-      a.sum[ACC][g] += in ? w32 : 0u;
-    }
-    for (uint32_t m = bm >> kDualGroups; m; m &= m - 1) {  // rarer hit buckets, miss buckets
-      const uint32_t b = kDualGroups + (uint32_t)__builtin_ctz(m);
-      atomicAdd(&sums[ACC][3 + 2 * b], 1ull);
-      if (w) atomicAdd(&sums[ACC][4 + 2 * b], (unsigned long long)w);
-    }
-  } else {  // weights >= 2^23 cycles: straight to the LDS counters
-    atomicAdd(&sums[ACC][0], 1ull);
-    atomicAdd(&sums[ACC][1], (unsigned long long)w);
-    if (lvl & LVL_NA) atomicAdd(&sums[ACC][2], 1ull);
-    for (uint32_t m = bm; m; m &= m - 1) {
-      const uint32_t b = (uint32_t)__builtin_ctz(m);
-      atomicAdd(&sums[ACC][3 + 2 * b], 1ull);
-      atomicAdd(&sums[ACC][4 + 2 * b], (unsigned long long)w);
-    }
+  for (int g = 0; g < kRtGroups; g++) {
+    const bool in = (cls & kRtMask[g]) != 0;
+    a.g[g] += in ? term : 0u;
+    gm |= in ? 1u << g : 0u;
   }
-  if (bm) {  // (an atomic only when the record moves the bound)
-    const uint32_t b = (uint32_t)__builtin_ctz(bm);
-    const unsigned long long mn = mins[ACC][b], mx = maxs[ACC][b];
-    if (w < mn) atomicMin(&mins[ACC][b], (unsigned long long)w);
-    if (w > mx) atomicMax(&maxs[ACC][b], (unsigned long long)w);
-    for (uint32_t m = bm & (bm - 1); m; m &= m - 1) {
-      const uint32_t b2 = (uint32_t)__builtin_ctz(m);
-      atomicMin(&mins[ACC][b2], (unsigned long long)w);
-      atomicMax(&maxs[ACC][b2], (unsigned long long)w);
+  const uint32_t fb = gm ? (kRtBucketNib >> (4 * __builtin_ctz(gm))) & 15u : 0xffu;
+  if (valid && gm) {
+    const unsigned long long mn = mins[ACC][fb], mx = maxs[ACC][fb];
+    if (w < mn) atomicMin(&mins[ACC][fb], (unsigned long long)w);
+    if (w > mx) atomicMax(&maxs[ACC][fb], (unsigned long long)w);
+  }
+  // (rare) every other bucket, and the whole record when its weight is big
+  const bool rare = valid && (big || (cls & ~kRtKnown) || (gm & (gm - 1)));
+  if (__ballot(rare)) {
+    if (rare) {
+      if (big) {
+        atomicAdd(&sums[ACC][0], 1ull);
+        atomicAdd(&sums[ACC][1], (unsigned long long)w);
+        if (lvl & LVL_NA) atomicAdd(&sums[ACC][2], 1ull);
+      }
+      for (uint32_t m = bucket_mask(lvl); m; m &= m - 1) {
+        const uint32_t bk = (uint32_t)__builtin_ctz(m);
+        bool reg = false;  // (counted in registers unless big)
+#pragma unroll
+        for (int g = 0; g < kRtGroups; g++) reg |= ((gm >> g) & 1u) && ((kRtBucketNib >> (4 * g)) & 15u) == bk;
+        if (big || !reg) {
+          atomicAdd(&sums[ACC][3 + 2 * bk], 1ull);
+          if (w) atomicAdd(&sums[ACC][4 + 2 * bk], (unsigned long long)w);
+        }
+        if (bk != fb) {
+          atomicMin(&mins[ACC][bk], (unsigned long long)w);
+          atomicMax(&maxs[ACC][bk], (unsigned long long)w);
+        }
+      }
     }
   }
 }
 
 // lanes -> the workgroup's LDS counters (every lane of the wave calls this)
-__device__ __forceinline__ void dual_drain(DualAcc& a, unsigned long long (*sums)[kGlobalSums], int lane) {
-  if (__ballot(a.tc != 0) == 0) return;
-  auto add2 = [&](uint32_t packed, int word) {  // read | write << 16 counts
-    if (__ballot(packed != 0) == 0) return;
-    const uint32_t r = wave_sum_u32(packed & 0xffffu), wv = wave_sum_u32(packed >> 16);
+__device__ __forceinline__ void racc_drain(RouteAcc& a, unsigned long long* sums, int lane) {
+  if (__ballot(a.tot != 0) == 0) return;  // (every register count comes with the total's)
+  auto add = [&](uint32_t v, int word) {  // count << 24 | weight -> words word, word + 1
+    if (__ballot(v != 0) == 0) return;
+    const uint32_t c = wave_sum_u32(v >> 24), wt = wave_sum_u32(v & (kRtOne - 1));
     if (lane == 0) {
-      if (r) atomicAdd(&sums[0][word], (unsigned long long)r);
-      if (wv) atomicAdd(&sums[1][word], (unsigned long long)wv);
+      atomicAdd(&sums[word], (unsigned long long)c);
+      if (wt) atomicAdd(&sums[word + 1], (unsigned long long)wt);
     }
   };
-  auto addw = [&](uint32_t v, int acc, int word) {
-    if (__ballot(v != 0) == 0) return;
-    const uint64_t t = wave_sum_u32x(v);
-    if (lane == 0) atomicAdd(&sums[acc][word], (unsigned long long)t);
-  };
-  add2(a.tc, 0);
-  add2(a.na, 2);
-  addw(a.tw[0], 0, 1);
-  addw(a.tw[1], 1, 1);
+  add(a.tot, 0);
+  const uint32_t na = wave_sum_u32(a.na);
+  if (lane == 0 && na) atomicAdd(&sums[2], (unsigned long long)na);
 #pragma unroll
-  for (int g = 0; g < kDualGroups; g++) {
-    add2(a.cnt[g], 3 + 2 * g);
-    addw(a.sum[0][g], 0, 4 + 2 * g);
-    addw(a.sum[1][g], 1, 4 + 2 * g);
-  }
-  dual_clear(a);
+  for (int g = 0; g < kRtGroups; g++) add(a.g[g], 3 + 2 * int((kRtBucketNib >> (4 * g)) & 15u));
+  racc_clear(a);
 }
 
 // kDbgRouteTiming: per-wave cycle accumulators of the route pass's phases
@@ -367,7 +368,10 @@ __device__ __forceinline__ RDesc route_desc(const RouteParams& rp, const uint4* 
 // holds, after the workgroup's last barrier.
 
 // route2_kernel's workgroup: 12 waves (three per SIMD)
-constexpr uint32_t kR2WG = 768;
+#ifndef NMG_R2WG
+#define NMG_R2WG 768
+#endif
+constexpr uint32_t kR2WG = NMG_R2WG;
 // line stage: partitions q < kLineParts have an LDS line
 constexpr uint32_t kLineParts = 1280;
 // line word (u64): line l's count (3 bits) at 3 * (l mod 8), staged slots
@@ -377,6 +381,9 @@ constexpr unsigned long long kLwBroken = 1ull << 28;
 __device__ __forceinline__ uint32_t lw_count(unsigned long long w, uint32_t l) { return uint32_t(w >> (3 * (l & 7))) & 7u; }
 __device__ __forceinline__ uint32_t lw_s(unsigned long long w) { return uint32_t(w >> kLwSShift); }
 __device__ __forceinline__ uint32_t lw_mask(unsigned long long w) { return uint32_t(w >> kLwMaskShift) & 15u; }
+#ifndef NMG_R2_UNALIGNED
+#define NMG_R2_UNALIGNED 0
+#endif
 #ifndef NMG_R2_LINES
 #define NMG_R2_LINES 1
 #endif
@@ -411,37 +418,42 @@ __device__ __forceinline__ void wload(const uint8_t* data, uint64_t off, uint32_
   const __amdgpu_buffer_rsrc_t rs =
       __builtin_amdgcn_make_buffer_rsrc((void*)(data + off), (short)0, (int)len, 0x00020000);
   const uint32_t pos = c + uint32_t(lane) * kRecBytes;
+#if NMG_R2_UNALIGNED
+  // (8 B aligned 16 B loads: hdr ts | addr w | dsrc, no per-lane select)
+  const auto x = __builtin_amdgcn_raw_buffer_load_b128(rs, pos, 0, 0);
+  const auto y = __builtin_amdgcn_raw_buffer_load_b128(rs, pos + 16, 0, 0);
+  const auto z = __builtin_amdgcn_raw_buffer_load_b64(rs, pos + 32, 0, 0);
+#else
   const uint32_t odd = (pos >> 3) & 1;  // 16 B aligned pieces, as load_rec
   const auto x = __builtin_amdgcn_raw_buffer_load_b128(rs, pos + (odd ? 8 : 0), 0, 0);
   const auto y = __builtin_amdgcn_raw_buffer_load_b128(rs, pos + (odd ? 24 : 16), 0, 0);
   const auto z = __builtin_amdgcn_raw_buffer_load_b64(rs, pos + (odd ? 0 : 32), 0, 0);
+#endif
   r.x = make_uint4(x[0], x[1], x[2], x[3]);
   r.y = make_uint4(y[0], y[1], y[2], y[3]);
   r.z = make_uint2(z[0], z[1]);
 }
 
-// route_partition with the segment table in LDS (uniform reads) instead of
-// kernel arguments, which the compiler would keep in scalar registers
+// route_partition with the segment table in LDS instead of kernel arguments
+// (which the compiler would keep in scalar registers): the segment is the
+// number of segment starts <= addr past the first (the starts in one group
+// of broadcast reads, the unused ones ~0), then one read of its parameters
 struct SegL {
   uint4 a;  // start lo, start hi, base, nslots
   uint4 b;  // shift, qlast
 };
-__device__ __forceinline__ uint32_t route_partition_l(const SegL* s_seg, uint32_t nseg, const uint64_t* s_pb,
-                                                      const uint16_t* s_pdir, uint64_t addr) {
-  // (field by field: a select of whole structs goes through scratch memory)
-  const uint4 a0 = s_seg[0].a, b0 = s_seg[0].b;
-  uint64_t s0 = u64of(a0.x, a0.y);
-  uint32_t base = a0.z, ns = a0.w, sh = b0.x, ql = b0.y;
-  for (uint32_t k = 1; k < nseg; k++) {
-    const uint4 ak = s_seg[k].a, bk = s_seg[k].b;
-    const uint64_t sk = u64of(ak.x, ak.y);
-    const bool in = addr >= sk;
-    s0 = in ? sk : s0;
-    base = in ? ak.z : base;
-    ns = in ? ak.w : ns;
-    sh = in ? bk.x : sh;
-    ql = in ? bk.y : ql;
-  }
+__device__ __forceinline__ uint32_t route_partition_l(const SegL* s_seg, const uint64_t* s_segst, uint32_t nseg,
+                                                      const uint64_t* s_pb, const uint16_t* s_pdir, uint64_t addr) {
+  uint32_t k = 0;
+  uint64_t st[kRouteSegs];
+#pragma unroll
+  for (uint32_t j = 1; j < kRouteSegs; j++) st[j] = s_segst[j];
+#pragma unroll
+  for (uint32_t j = 1; j < kRouteSegs; j++) k += (uint32_t)(addr >= st[j]);
+  k = min(k, nseg - 1);  // (addr = ~0 passes the unused starts too)
+  const uint4 ak = s_seg[k].a, bk = s_seg[k].b;
+  const uint64_t s0 = u64of(ak.x, ak.y);
+  const uint32_t base = ak.z, ns = ak.w, sh = bk.x, ql = bk.y;
   const uint64_t rel = (addr - s0) >> sh;
   const uint32_t e = s_pdir[base + (rel < ns ? (uint32_t)rel : ns - 1)];
   uint32_t q = e & 2047u;
@@ -511,6 +523,7 @@ __global__ __launch_bounds__(kR2WG, 1) void route2_kernel(RouteParams rp) {
   __shared__ uint32_t s_taken, s_bnext;
   __shared__ unsigned long long s_gsums[2][kGlobalSums], s_gmins[2][18], s_gmaxs[2][18];
   __shared__ SegL s_seg[kRouteSegs];
+  __shared__ uint64_t s_segst[kRouteSegs];
   // the line stage: per partition a line of four compact records, its line
   // word and its chunk line (pool slot / 4); per wave the lines it writes out
   __shared__ uint4 s_line[NMG_R2_LINES ? kLineParts * 4 : 1];
@@ -525,6 +538,7 @@ __global__ __launch_bounds__(kR2WG, 1) void route2_kernel(RouteParams rp) {
     const RSeg g = rp.seg[tid];
     s_seg[tid].a = make_uint4((uint32_t)g.start, (uint32_t)(g.start >> 32), g.base, g.nslots);
     s_seg[tid].b = make_uint4(g.shift, g.qlast, 0, 0);
+    s_segst[tid] = tid < rp.nseg ? g.start : ~0ull;
   }
   const uint32_t nseg = rp.nseg;
   const uint64_t first_start = rp.seg[0].start;
@@ -554,8 +568,9 @@ __global__ __launch_bounds__(kR2WG, 1) void route2_kernel(RouteParams rp) {
     s_gmins[0][tid] = s_gmins[1][tid] = ~0ull;  // INIT_COUNTER (mem_analyzer.c:415-420)
     s_gmaxs[0][tid] = s_gmaxs[1][tid] = 0;
   }
-  DualAcc gacc;  // per-lane update_counters, drained every kDrainWindows windows
-  dual_clear(gacc);
+  RouteAcc gacc[2];  // per-lane update_counters per access type, drained every kRouteDrain windows
+  racc_clear(gacc[0]);
+  racc_clear(gacc[1]);
   uint32_t gwin = 0;
   lds_sync();
 
@@ -640,7 +655,16 @@ __global__ __launch_bounds__(kR2WG, 1) void route2_kernel(RouteParams rp) {
         nwin++;
       }
       rt_stamp<TIMING>(rt, 0);
+#if NMG_R2_UNALIGNED
+      Rec rec;
+      rec.hdr = u64of(A.x.x, A.x.y);
+      rec.ts = u64of(A.x.z, A.x.w);
+      rec.addr = u64of(A.y.x, A.y.y);
+      rec.w = u64of(A.y.z, A.y.w);
+      rec.dsrc = u64of(A.z.x, A.z.y);
+#else
       Rec rec = decode_rec(A, pos);
+#endif
       const bool bad = cand && (uint64_t(pos) + kRecBytes > dw.len || (rec.hdr >> 48) != kRecBytes);
       bool valid;
       uint32_t roff = pos, ncur;
@@ -738,18 +762,19 @@ __global__ __launch_bounds__(kR2WG, 1) void route2_kernel(RouteParams rp) {
       rt_stamp<TIMING>(rt, 1);
       const uint32_t acc_l = dw.access();
       if (acc_l == 0) {  // (uniform)
-        if (valid) route_count<0>(gacc, s_gsums, s_gmins, s_gmaxs, uint32_t(rec.dsrc >> 5) & 0x3fff, rec.w);
+        route_count<0>(gacc[0], s_gsums, s_gmins, s_gmaxs, valid, uint32_t(rec.dsrc >> 5) & 0x3fff, rec.w);
       } else {
-        if (valid) route_count<1>(gacc, s_gsums, s_gmins, s_gmaxs, uint32_t(rec.dsrc >> 5) & 0x3fff, rec.w);
+        route_count<1>(gacc[1], s_gsums, s_gmins, s_gmaxs, valid, uint32_t(rec.dsrc >> 5) & 0x3fff, rec.w);
       }
-      if (++gwin == kDrainWindows) {
-        dual_drain(gacc, s_gsums, lane);
+      if (++gwin == kRouteDrain) {
+        racc_drain(gacc[0], s_gsums[0], lane);
+        racc_drain(gacc[1], s_gsums[1], lane);
         gwin = 0;
       }
       rt_stamp<TIMING>(rt, 2);
       // below the first key ht_lower_key finds no node: counted, not routed
       const bool routed = valid && rec.addr >= first_start;
-      const uint32_t q = routed ? route_partition_l(s_seg, nseg, s_pb, s_pdir, rec.addr) : 0u;
+      const uint32_t q = routed ? route_partition_l(s_seg, s_segst, nseg, s_pb, s_pdir, rec.addr) : 0u;
       if (TIMING) (void)__builtin_amdgcn_readfirstlane(__ballot(q != 0));  // (the search ends here)
       rt_stamp<TIMING>(rt, 3);
       uint4 a = make_uint4(0, 0, 0, 0);
@@ -912,7 +937,8 @@ __global__ __launch_bounds__(kR2WG, 1) void route2_kernel(RouteParams rp) {
       o[12] = rt.acc[10];
     }
   }
-  dual_drain(gacc, s_gsums, lane);
+  racc_drain(gacc[0], s_gsums[0], lane);
+  racc_drain(gacc[1], s_gsums[1], lane);
   lds_sync();
 #pragma unroll
   for (uint32_t a = 0; a < 2; a++) {  // the global mem_counters of both access types
