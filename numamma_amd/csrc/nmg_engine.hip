@@ -104,6 +104,8 @@ void free_route_table(nmg_engine* h) {
   (void)hipFree(h->d_pe_nodes);
   (void)hipFree(h->d_pe_info);
   (void)hipFree(h->d_pe_pnode);
+  (void)hipFree(h->d_pe_old);
+  (void)hipFree(h->d_pe_oinf);
   (void)hipFree(h->d_pe_dir);
   (void)hipFree(h->d_pe_ids);
   (void)hipFree(h->d_pe_lrel);
@@ -119,6 +121,8 @@ void free_route_table(nmg_engine* h) {
   h->d_pe_nodes = nullptr;
   h->d_pe_info = nullptr;
   h->d_pe_pnode = nullptr;
+  h->d_pe_old = nullptr;
+  h->d_pe_oinf = nullptr;
   h->route_ok = false;
   h->nparts = 0;
 }

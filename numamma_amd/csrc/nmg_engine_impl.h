@@ -260,6 +260,8 @@ struct nmg_engine {
   uint64_t* d_pe_keys = nullptr;  // [nparts][kPartSlots]
   uint4* d_pe_nodes = nullptr;    // [nparts][kPartSlots][2]
   uint4* d_pe_pnode = nullptr;    // [nparts][kPartSlots] packed node records (PackedNode)
+  uint4* d_pe_old = nullptr;      // [nparts][kOldLds] older entries, packed
+  uint32_t* d_pe_oinf = nullptr;  // [nparts][kOldLds]
   uint2* d_pe_info = nullptr;     // [nparts][kPartSlots]
   uint4* d_pe_dir = nullptr;      // [nparts][kPartDir] (PartDir)
   uint32_t* d_pe_ids = nullptr;   // [table entries] entry id per table position (online tables; else null)

@@ -62,14 +62,24 @@ constexpr uint32_t kPartDir = 1024;        // directory slots per partition (rad
 constexpr uint32_t kDirInline = 6;
 // PackedNode, a key's newest entry for the local pass's common path (16 B):
 //   x = end - first key, y = alloc_q, z = free_q, w = table position - e0
-//   (11 bits) | kPnOlder | kPnExact
+//   (11 bits) | kPnOlder | kPnExact | kPnOldLds | older entries << kPnOldShift
 // with alloc_q / free_q = (date - tbase) >> kPnQShift, saturated to 32 bits
 // (an entry freed before tbase: alloc_q = ~0, free_q = 0, no sample
-// matches).  A sample whose quantised timestamp equals either bound, or a
-// key marked exact (its object does not start at the key, or its end or key
-// offset needs more than 32 bits), is decided on the exact node record.
+// matches); pe_info.y = buffer_addr - first key.  A sample whose quantised
+// timestamp equals either bound, or a key marked exact (its object's start or
+// end offset needs more than 32 bits), is decided on the exact node record.
 constexpr uint32_t kPnQShift = 8;
 constexpr uint32_t kPnOlder = 1u << 11, kPnExact = 1u << 12;
+// The older entries of a partition's reused keys (the LIFO chain past the
+// newest, tools/hash.c:108-114), in table order, up to kOldLds per partition:
+// x = end - first key, y = alloc_q, z = free_q, w = buffer_addr - first key
+// (an entry freed before tbase: all zero but y = ~0), and per entry its page
+// cell (pe_oinf, as PartInfo's info.x).  A key has them in the list
+// (kPnOldLds) when all fit: the list index of its i-th older entry is its
+// table position - e0 - key index + i - 1.  Otherwise, or when a quantised
+// date is ambiguous, the lookup walks the chain in global memory.
+constexpr uint32_t kOldLds = 512;
+constexpr uint32_t kPnOldLds = 1u << 13, kPnOldShift = 16;
 constexpr uint32_t kPartEntries = 1536;    // entries per partition (LDS object counters)
 constexpr uint32_t kPartCells = 28672;     // u16 page cells per partition: nb_threads x cell span
 constexpr uint32_t kItemChunks = 1023;     // chunks per work item: < 2^16 records, so u16 page cells
@@ -185,7 +195,9 @@ struct LocalParams {
   const uint64_t* pe_keys;   // [nparts][kPartSlots] keys, ascending
   const uint4* pe_nodes;     // [nparts][kPartSlots][2] (addr, end), (alloc, free) of each key's newest entry (exact)
   const uint4* pe_pnode;     // [nparts][kPartSlots] the same, packed (PackedNode)
-  const uint2* pe_info;      // [nparts][kPartSlots] (cell - cb, or packed cell, or ~0 sparse; key - first key)
+  const uint4* pe_old;       // [nparts][kOldLds] older entries, packed (kOldLds)
+  const uint32_t* pe_oinf;   // [nparts][kOldLds] their page cells
+  const uint2* pe_info;      // [nparts][kPartSlots] (cell - cb, or packed cell, or ~0 sparse; buffer_addr - first key)
   const uint4* pe_dir;       // [nparts][kPartDir] directory slots (PartDir)
   const uint32_t* pe_ids;    // [table entries] entry id of each table position (an online table,
                              // nmg_update_objects), or null: the id is the position (nmg_set_objects)

@@ -376,11 +376,26 @@ constexpr uint32_t kR2WG = NMG_R2WG;
 constexpr uint32_t kLineParts = 1280;
 // line word (u64): line l's count (3 bits) at 3 * (l mod 8), staged slots
 // (4) at 24, given up at 28, S at 52
+#ifndef NMG_R2_LW32
+#define NMG_R2_LW32 0
+#endif
+#if NMG_R2_LW32
+// (32-bit variant: four lines' counts, S mod 1024)
+typedef uint32_t LineWord;
+constexpr uint32_t kLwMaskShift = 12, kLwSShift = 22, kLwLineMask = 1023, kLwAhead = 4;
+constexpr LineWord kLwBroken = 1u << 16;
+#else
+typedef unsigned long long LineWord;
 constexpr uint32_t kLwMaskShift = 24, kLwSShift = 52, kLwLineMask = 4095, kLwAhead = 8;
-constexpr unsigned long long kLwBroken = 1ull << 28;
-__device__ __forceinline__ uint32_t lw_count(unsigned long long w, uint32_t l) { return uint32_t(w >> (3 * (l & 7))) & 7u; }
-__device__ __forceinline__ uint32_t lw_s(unsigned long long w) { return uint32_t(w >> kLwSShift); }
-__device__ __forceinline__ uint32_t lw_mask(unsigned long long w) { return uint32_t(w >> kLwMaskShift) & 15u; }
+constexpr LineWord kLwBroken = 1ull << 28;
+#endif
+constexpr LineWord kLwOne = 1;
+__device__ __forceinline__ uint32_t lw_count(LineWord w, uint32_t l) { return uint32_t(w >> (3 * (l & (kLwAhead - 1)))) & 7u; }
+__device__ __forceinline__ uint32_t lw_s(LineWord w) { return uint32_t(w >> kLwSShift); }
+__device__ __forceinline__ uint32_t lw_mask(LineWord w) { return uint32_t(w >> kLwMaskShift) & 15u; }
+#ifndef NMG_R2_ABL
+#define NMG_R2_ABL 0
+#endif
 #ifndef NMG_R2_UNALIGNED
 #define NMG_R2_UNALIGNED 0
 #endif
@@ -527,7 +542,7 @@ __global__ __launch_bounds__(kR2WG, 1) void route2_kernel(RouteParams rp) {
   // the line stage: per partition a line of four compact records, its line
   // word and its chunk line (pool slot / 4); per wave the lines it writes out
   __shared__ uint4 s_line[NMG_R2_LINES ? kLineParts * 4 : 1];
-  __shared__ unsigned long long s_lw[NMG_R2_LINES ? kLineParts : 1];
+  __shared__ LineWord s_lw[NMG_R2_LINES ? kLineParts : 1];
   __shared__ uint32_t s_ldst[NMG_R2_LINES ? kLineParts : 1];
   __shared__ uint2 s_tab[kWaves][64];
 
@@ -551,7 +566,7 @@ __global__ __launch_bounds__(kR2WG, 1) void route2_kernel(RouteParams rp) {
   for (uint32_t i = tid; i < P; i += kR2WG) s_state[i] = st_pack(kStNone, kStNone, 0, 2 * kChunk);
   // the first line of a partition: slot 0 of generation 1's open chunk
   const uint32_t nlp = NMG_R2_LINES && !(p.flags & kDbgNoLines) ? min(P, kLineParts) : 0u;
-  for (uint32_t i = tid; i < nlp; i += kR2WG) s_lw[i] = (unsigned long long)(kChunk / 4) << kLwSShift;
+  for (uint32_t i = tid; i < nlp; i += kR2WG) s_lw[i] = LineWord(kChunk / 4) << kLwSShift;
   // (kDbgLapNoWait: a record one line ahead of S already gives the line up -- tests)
   const uint32_t ahead_max = (p.flags & kDbgLapNoWait) ? 1u : kLwAhead;
   const uint32_t r0 = p.ranges[blockIdx.x], r1 = p.ranges[blockIdx.x + 1];
@@ -642,6 +657,7 @@ __global__ __launch_bounds__(kR2WG, 1) void route2_kernel(RouteParams rp) {
       d.ta = __builtin_amdgcn_readfirstlane(d.ta);
       d.pad = __builtin_amdgcn_readfirstlane(d.pad);
     };
+    uint32_t sink = 0;  // (NMG_R2_ABL ablations: what the skipped stages would have consumed)
     auto window = [&](RawRec& A, RawRec& B) {
       uni(d0);
       uni(d1);
@@ -760,6 +776,10 @@ __global__ __launch_bounds__(kR2WG, 1) void route2_kernel(RouteParams rp) {
       // (mem_sampling.c:882: every SAMPLE, matched or not), partition, chunk
       // slot, store
       rt_stamp<TIMING>(rt, 1);
+#if NMG_R2_ABL >= 5
+      sink ^= (uint32_t)rec.addr ^ (uint32_t)rec.dsrc ^ (uint32_t)rec.w ^ (uint32_t)rec.ts;
+      return;
+#endif
       const uint32_t acc_l = dw.access();
       if (acc_l == 0) {  // (uniform)
         route_count<0>(gacc[0], s_gsums, s_gmins, s_gmaxs, valid, uint32_t(rec.dsrc >> 5) & 0x3fff, rec.w);
@@ -772,6 +792,10 @@ __global__ __launch_bounds__(kR2WG, 1) void route2_kernel(RouteParams rp) {
         gwin = 0;
       }
       rt_stamp<TIMING>(rt, 2);
+#if NMG_R2_ABL >= 4
+      sink ^= (uint32_t)rec.addr ^ (uint32_t)rec.ts;
+      return;
+#endif
       // below the first key ht_lower_key finds no node: counted, not routed
       const bool routed = valid && rec.addr >= first_start;
       const uint32_t q = routed ? route_partition_l(s_seg, s_segst, nseg, s_pb, s_pdir, rec.addr) : 0u;
@@ -784,6 +808,10 @@ __global__ __launch_bounds__(kR2WG, 1) void route2_kernel(RouteParams rp) {
         a = x_encode(rp.xl, pbq, rec.addr, rec.ts, rec.w, dw.pad, roff, dw.thread_rank(), acc_l);
       }
       rt_stamp<TIMING>(rt, 4);
+#if NMG_R2_ABL >= 3
+      sink ^= a.x ^ a.y ^ a.z ^ a.w ^ q;
+      return;
+#endif
       // ---- a slot in q's open chunks: one LDS atomic on the partition's
       // state (route2_claim).  No barrier: the waves run on their own streams.
       uint64_t dst = ~0ull;  // rec16 slot, or ~0: no slot (not routed / overflow list)
@@ -793,7 +821,7 @@ __global__ __launch_bounds__(kR2WG, 1) void route2_kernel(RouteParams rp) {
       // (the line word read beside the claim: a lap can only move on once this
       // record's own line is written, so a lap that equals the record's line
       // here still does after the claim)
-      unsigned long long lw = lined ? s_lw[q] : 0ull;
+      LineWord lw = lined ? s_lw[q] : LineWord(0);
       {
         bool todo = routed, spin = false;
         uint32_t waitg = 0;
@@ -835,6 +863,10 @@ __global__ __launch_bounds__(kR2WG, 1) void route2_kernel(RouteParams rp) {
         }
       }
       rt_stamp<TIMING>(rt, 5);
+#if NMG_R2_ABL >= 2
+      sink ^= a.x ^ a.y ^ a.z ^ a.w ^ (uint32_t)dst ^ lid ^ (uint32_t)lw;
+      return;
+#endif
       // ---- the line stage (see the comment above kR2WG)
       bool staged = false;
       if (NMG_R2_LINES && __ballot(lined)) {
@@ -850,13 +882,17 @@ __global__ __launch_bounds__(kR2WG, 1) void route2_kernel(RouteParams rp) {
           // (the record before the count that may complete the line)
           __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
         } else if (counts && dst != ~0ull) {
+#if NMG_R2_ABL >= 1
+          sink ^= a.x ^ (uint32_t)dst;
+#else
           rp.rec16[dst] = a;
+#endif
         }
         bool done = false;
         uint32_t dmask = 0;
         if (counts) {
-          const unsigned long long o =
-              atomicAdd(&s_lw[q], (1ull << (3 * (lid & 7))) + (staged ? 1ull << (kLwMaskShift + j) : 0ull));
+          const LineWord o =
+              atomicAdd(&s_lw[q], (kLwOne << (3 * (lid & (kLwAhead - 1)))) + (staged ? kLwOne << (kLwMaskShift + j) : LineWord(0)));
           // the line's fourth record, the line being S (S may have reached it
           // since the read beside the claim)
           done = lw_count(o, lid) == 3 && lw_s(o) == lid;
@@ -876,15 +912,19 @@ __global__ __launch_bounds__(kR2WG, 1) void route2_kernel(RouteParams rp) {
             if (jj < nd) {
               const uint2 t = s_tab[wave][jj];
               const uint32_t tq = t.x & 2047u, tm = (t.x >> 11) & 15u, k = lane & 3;
+#if NMG_R2_ABL >= 1
+              if ((tm >> k) & 1) sink ^= s_line[tq * 4 + k].x ^ t.y;
+#else
               if ((tm >> k) & 1) rp.rec16[uint64_t(t.y) * 4 + k] = s_line[tq * 4 + k];
+#endif
               // (the line read by all four lanes -- one instruction, waited
               // for by the stores -- before S moves on and its slots are reused)
               __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
               if (k == 0) {  // S -> S + 1, past the lines already complete (all their records stored straight)
                 uint32_t l = t.x >> 16, m = tm;
                 while (true) {
-                  const unsigned long long o = atomicAdd(
-                      &s_lw[tq], (1ull << kLwSShift) - (4ull << (3 * (l & 7))) - ((unsigned long long)m << kLwMaskShift));
+                  const LineWord o = atomicAdd(&s_lw[tq], (kLwOne << kLwSShift) - (LineWord(4) << (3 * (l & (kLwAhead - 1)))) -
+                                                            (LineWord(m) << kLwMaskShift));
                   l = (l + 1) & kLwLineMask;
                   if (lw_count(o, l) != 4) break;
                   m = 0;
@@ -898,7 +938,11 @@ __global__ __launch_bounds__(kR2WG, 1) void route2_kernel(RouteParams rp) {
       rt_stamp<TIMING>(rt, 9);
       // the records the line stage did not take: not lined, or given up
       const bool straight = dst != ~0ull && !(lined && !(lw & kLwBroken) && ((lid - lw_s(lw)) & kLwLineMask) < ahead_max);
+#if NMG_R2_ABL >= 1
+      if (straight) sink ^= a.y ^ (uint32_t)dst;
+#else
       if (straight) rp.rec16[dst] = a;
+#endif
       if (TIMING) {  // (records staged / stored straight to their slot)
         rt.acc[6] += (uint64_t)__popcll(__ballot(staged));
         rt.acc[7] += (uint64_t)__popcll(__ballot(straight));
@@ -925,6 +969,7 @@ __global__ __launch_bounds__(kR2WG, 1) void route2_kernel(RouteParams rp) {
       window(ra, rb);
       window(rb, ra);
     } while (d0.pad != kNoBuf);
+    if (sink == 0x9e3779b9u) rp.used[blockIdx.x] = sink;  // (never: keeps the ablated stages' inputs live)
     if (TIMING && lane == 0) {
       unsigned long long* o = p.dbg + (uint64_t(blockIdx.x) * (kWG / 64) + tid / 64) * kRouteTimingWords;
       for (int k = 0; k < 9; k++) o[k] = rt.acc[k];
@@ -1133,6 +1178,8 @@ __global__ __launch_bounds__(kLWG, 1) void local_kernel(LocalParams lp) {
   __shared__ uint4 s_pn[kPartSlots];  // packed node records (PackedNode)
   __shared__ uint2 s_info[kPartSlots];
   __shared__ uint4 s_dir[kPartDir];   // directory slots (PartDir)
+  __shared__ uint4 s_old[kOldLds];    // older entries of reused keys (kOldLds)
+  __shared__ uint32_t s_oinf[kOldLds];
   __shared__ unsigned long long s_owt[2][kPartEntries];
   __shared__ unsigned long long s_first[kPartEntries];
   __shared__ uint32_t s_pg[kPartCells / 2];
@@ -1180,6 +1227,13 @@ __global__ __launch_bounds__(kLWG, 1) void local_kernel(LocalParams lp) {
       }
       const uint4* gd = lp.pe_dir + uint64_t(q) * kPartDir;
       for (uint32_t i = tid; i < kPartDir; i += kLWG) s_dir[i] = gd[i];
+      const uint32_t nold = min(pi.ne - nk, kOldLds);
+      const uint4* go = lp.pe_old + uint64_t(q) * kOldLds;
+      const uint32_t* goi = lp.pe_oinf + uint64_t(q) * kOldLds;
+      for (uint32_t i = tid; i < nold; i += kLWG) {
+        s_old[i] = go[i];
+        s_oinf[i] = goi[i];
+      }
       for (uint32_t i = tid; i < item.z - item.y; i += kLWG) s_clist[i] = lp.clist[item.y + i];
     }
     if (tid == 0) s_cnext = 0;
@@ -1321,7 +1375,7 @@ __global__ __launch_bounds__(kLWG, 1) void local_kernel(LocalParams lp) {
       // exact-marked key, or an escaped record) is decided on the exact node
       int32_t erel[kLC];
       uint64_t pofs[kLC];  // a match: addr - buffer_addr
-      uint32_t hrel[kLC];
+      uint32_t hrel[kLC], pnw[kLC], tq[kLC];
       bool older[kLC], amb[kLC];
 #pragma unroll
       for (int j = 0; j < kLC; j++) {
@@ -1330,14 +1384,16 @@ __global__ __launch_bounds__(kLWG, 1) void local_kernel(LocalParams lp) {
         hrel[j] = kEmpty32;
         older[j] = false;
         amb[j] = false;
+        pnw[j] = 0;
+        // (the offsets are < 2^40: the timestamp's quantum fits 32 bits)
+        tq[j] = __builtin_amdgcn_alignbit((uint32_t)(ts[j] >> 32), (uint32_t)ts[j], kPnQShift);
         if (r[j] >= 0 && !(p.flags & kDbgLocalNoSearch)) {
           const uint4 pn = s_pn[r[j]];
           const uint2 inf = s_info[r[j]];
-          // (the offsets are < 2^40: the timestamp's quantum fits 32 bits)
-          const uint32_t tq = __builtin_amdgcn_alignbit((uint32_t)(ts[j] >> 32), (uint32_t)ts[j], kPnQShift);
-          const bool in = addr[j] < (uint64_t)pn.x;
-          amb[j] = xr[j].esc || (pn.w & kPnExact) || (in && (tq == pn.y || tq == pn.z));
-          if (!amb[j] && in && tq > pn.y && tq < pn.z) {
+          pnw[j] = pn.w;
+          const bool in = addr[j] >= (uint64_t)inf.y && addr[j] < (uint64_t)pn.x;
+          amb[j] = xr[j].esc || (pn.w & kPnExact) || (in && (tq[j] == pn.y || tq[j] == pn.z));
+          if (!amb[j] && in && tq[j] > pn.y && tq[j] < pn.z) {
             erel[j] = (int32_t)(pn.w & 2047u);
             pofs[j] = addr[j] - inf.y;
             hrel[j] = inf.x;
@@ -1372,7 +1428,33 @@ __global__ __launch_bounds__(kLWG, 1) void local_kernel(LocalParams lp) {
       bool anyold = false;
 #pragma unroll
       for (int j = 0; j < kLC; j++) anyold |= older[j];
-      if (__ballot(anyold)) {  // (rare) older entries of a reused address (LIFO, tools/hash.c:108-114)
+      if (__ballot(anyold)) {  // older entries of a reused address (LIFO, tools/hash.c:108-114): the LDS list
+#pragma unroll
+        for (int j = 0; j < kLC; j++) {
+          if (!older[j] || xr[j].esc || !(pnw[j] & kPnOldLds)) continue;
+          const uint32_t e = pnw[j] & 2047u, base = e - (uint32_t)r[j], c = (pnw[j] >> kPnOldShift) & 2047u;
+          bool glob = false;
+          for (uint32_t i = 0; i < c; i++) {
+            const uint4 o = s_old[base + i];
+            const bool in = addr[j] >= (uint64_t)o.w && addr[j] < (uint64_t)o.x;
+            if (in && (tq[j] == o.y || tq[j] == o.z)) {  // (a quantum of either date: the chain decides)
+              glob = true;
+              break;
+            }
+            if (in && tq[j] > o.y && tq[j] < o.z) {
+              erel[j] = (int32_t)(e + 1 + i);
+              pofs[j] = addr[j] - o.w;
+              hrel[j] = s_oinf[base + i];
+              break;
+            }
+          }
+          older[j] = glob;
+        }
+        anyold = false;
+#pragma unroll
+        for (int j = 0; j < kLC; j++) anyold |= older[j];
+      }
+      if (__ballot(anyold)) {  // (rare) the chain in global memory: escaped records, keys past the list
 #pragma unroll
         for (int j = 0; j < kLC; j++) {
           if (!older[j]) continue;

@@ -165,6 +165,13 @@ int route_analyze_job(nmg_engine* h, const RouteJob& job) {
   }
   HIP_TRY(h, launch_route(grid, h->stream, rp));
   HIP_TRY(h, hipEventRecord(h->ringr[slot], h->stream));
+#if NMG_R2_ABL  // (ablation builds, tools/ab_build.sh: the route pass alone, its output unused)
+  HIP_TRY(h, hipEventRecord(h->ringm[slot], h->stream));
+  HIP_TRY(h, hipEventRecord(h->ring1[slot], h->stream));
+  h->nlaunch++;
+  h->launched = true;
+  return NMG_OK;
+#endif
   HIP_TRY(h, launch_overflow(h->stream, rp));
   ScatterParams sc;
   sc.cmeta = h->d_cmeta;
@@ -195,6 +202,8 @@ int route_analyze_job(nmg_engine* h, const RouteJob& job) {
   lp.pe_nodes = h->d_pe_nodes;
   lp.pe_info = h->d_pe_info;
   lp.pe_pnode = h->d_pe_pnode;
+  lp.pe_old = h->d_pe_old;
+  lp.pe_oinf = h->d_pe_oinf;
   lp.pe_dir = h->d_pe_dir;
   lp.pe_ids = h->d_pe_ids;
   lp.pe_lrel = h->d_pe_lrel;

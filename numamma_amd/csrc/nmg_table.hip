@@ -290,6 +290,23 @@ int build_partitions(nmg_engine* h, const uint64_t* keys, const uint32_t* entry_
   std::vector<uint4> ppn((size_t)P * kPartSlots, make_uint4(0, 0, 0, 0));
   std::vector<uint2> pinf((size_t)P * kPartSlots, make_uint2(kEmpty32, 0));
   std::vector<uint4> pdir((size_t)P * kPartDir, make_uint4(0, 0, 0, 0));
+  std::vector<uint4> pold((size_t)P * kOldLds, make_uint4(0, 0, 0, 0));
+  std::vector<uint32_t> poinf((size_t)P * kOldLds, kEmpty32);
+  // an entry's page cell relative to its partition (as pe_info.x)
+  auto cell_rel = [&](const PartInfo& pi, uint32_t e) -> uint32_t {
+    const DevEntry& d = dev[e];
+    return d.hist == kHistSparse ? kEmpty32 : pi.cmap != ~0u ? lrel[e] : (uint32_t)(d.hist - pi.cb);
+  };
+  // the quantised dates of an entry (never matching: ~0, 0)
+  auto qdates = [&](const DevEntry& d, uint64_t tb, uint32_t& aq, uint32_t& fq) {
+    if (d.free < tb) {
+      aq = 0xffffffffu;
+      fq = 0;
+    } else {
+      aq = (uint32_t)std::min<uint64_t>((d.alloc > tb ? d.alloc - tb : 0) >> kPnQShift, 0xffffffffull);
+      fq = (uint32_t)std::min<uint64_t>((d.free - tb) >> kPnQShift, 0xffffffffull);
+    }
+  };
   for (uint32_t q = 0; q < P; q++) {
     const PartInfo& pi = parts[q];
     const uint64_t f = keys[pi.k0];
@@ -301,29 +318,40 @@ int build_partitions(nmg_engine* h, const uint64_t* keys, const uint32_t* entry_
       pn[2 * o] = make_uint4((uint32_t)d.addr, (uint32_t)(d.addr >> 32), (uint32_t)d.end, (uint32_t)(d.end >> 32));
       pn[2 * o + 1] = make_uint4((uint32_t)d.alloc, (uint32_t)(d.alloc >> 32), (uint32_t)d.free, (uint32_t)(d.free >> 32));
       const uint32_t older = entry_off[kk + 1] - entry_off[kk] > 1 ? 1u : 0u;
-      const uint32_t hrel = d.hist == kHistSparse ? kEmpty32
-                            : pi.cmap != ~0u         ? lrel[entry_off[kk]]
-                                                     : (uint32_t)(d.hist - pi.cb);
-      const uint64_t krel = keys[kk] - f;
-      // packed node (PackedNode): exact where the object does not start at
-      // its key or its end or key offset needs more than 32 bits -- unless
-      // it was freed before the first allocation (the [stack], Q4): no
-      // non-escaped sample can match it, whatever its bounds
-      const uint64_t erel = d.end - f;
+      const uint32_t hrel = cell_rel(pi, entry_off[kk]);
+      // packed node (PackedNode): exact where the object's start or end
+      // offset from the first key needs more than 32 bits -- unless it was
+      // freed before the first allocation (the [stack], Q4): no non-escaped
+      // sample can match it, whatever its bounds
+      const uint64_t erel = d.end - f, brel = d.addr - f;
       const bool never = d.free < tb;
-      const bool exact =
-          !never && (d.addr != keys[kk] || d.end < keys[kk] || (erel >> 32) != 0 || (krel >> 32) != 0);
-      uint64_t aq, fq;
-      if (never) {
-        aq = 0xffffffffull;
-        fq = 0;
-      } else {
-        aq = std::min<uint64_t>((d.alloc > tb ? d.alloc - tb : 0) >> kPnQShift, 0xffffffffull);
-        fq = std::min<uint64_t>((d.free - tb) >> kPnQShift, 0xffffffffull);
+      const bool exact = !never && (d.addr < f || d.end < d.addr || (erel >> 32) != 0 || (brel >> 32) != 0);
+      uint32_t aq, fq;
+      qdates(d, tb, aq, fq);
+      // the key's older entries in the partition's list (kOldLds) when they fit
+      const uint32_t nold = entry_off[kk + 1] - entry_off[kk] - 1, lbase = entry_off[kk] - pi.e0 - r;
+      bool old_lds = nold > 0 && nold < 2048 && lbase + nold <= kOldLds;
+      for (uint32_t i = 1; old_lds && i <= nold; i++) {
+        const uint32_t e = entry_off[kk] + i;
+        const DevEntry& od = dev[e];
+        uint32_t oa, of;
+        qdates(od, tb, oa, of);
+        uint4 v = make_uint4(0, oa, of, 0);
+        if (od.free >= tb) {  // (else: never matches, bounds irrelevant)
+          if (od.addr < f || od.end < od.addr || ((od.end - f) >> 32) != 0) {
+            old_lds = false;
+            break;
+          }
+          v.x = (uint32_t)(od.end - f);
+          v.w = (uint32_t)(od.addr - f);
+        }
+        pold[(size_t)q * kOldLds + lbase + i - 1] = v;
+        poinf[(size_t)q * kOldLds + lbase + i - 1] = cell_rel(pi, e);
       }
-      ppn[o] = make_uint4(exact || never ? 0u : (uint32_t)erel, (uint32_t)aq, (uint32_t)fq,
-                          (entry_off[kk] - pi.e0) | (older ? kPnOlder : 0u) | (exact ? kPnExact : 0u));
-      pinf[o] = make_uint2(hrel, (uint32_t)krel);
+      ppn[o] = make_uint4(exact || never ? 0u : (uint32_t)erel, aq, fq,
+                          (entry_off[kk] - pi.e0) | (older ? kPnOlder : 0u) | (exact ? kPnExact : 0u) |
+                              (old_lds ? kPnOldLds | (nold << kPnOldShift) : 0u));
+      pinf[o] = make_uint2(hrel, exact || never ? 0u : (uint32_t)brel);
     }
     uint32_t lo = 0;
     for (uint32_t j = 0; j < kPartDir; j++) {
@@ -360,6 +388,8 @@ int build_partitions(nmg_engine* h, const uint64_t* keys, const uint32_t* entry_
   HIP_TRY(h, alloc_copy(h, (void**)&h->d_pe_keys, pk.data(), pk.size() * 8));
   HIP_TRY(h, alloc_copy(h, (void**)&h->d_pe_nodes, pn.data(), pn.size() * sizeof(uint4)));
   HIP_TRY(h, alloc_copy(h, (void**)&h->d_pe_pnode, ppn.data(), ppn.size() * sizeof(uint4)));
+  HIP_TRY(h, alloc_copy(h, (void**)&h->d_pe_old, pold.data(), pold.size() * sizeof(uint4)));
+  HIP_TRY(h, alloc_copy(h, (void**)&h->d_pe_oinf, poinf.data(), poinf.size() * 4));
   HIP_TRY(h, alloc_copy(h, (void**)&h->d_pe_info, pinf.data(), pinf.size() * sizeof(uint2)));
   HIP_TRY(h, alloc_copy(h, (void**)&h->d_pe_dir, pdir.data(), pdir.size() * sizeof(uint4)));
   if (ids) {

@@ -323,6 +323,7 @@ class SynthConfig:
     size_min: int = 64
     size_max: int = 256 * 1024
     reuse_frac: float = 0.03
+    reuse_depth: int = 2  # entries per reused key (LIFO chain, disjoint lifetimes)
     realloc_frac: float = 0.005
     nb_globals: int = 8
     global_size: int = 8192
@@ -404,14 +405,14 @@ def make_table(cfg: SynthConfig, rng: np.random.Generator) -> ObjectTable:
         strings += f"app.c:{100 + g}(func_{g % 97})".encode() + b"\0"
     g_tail = [rng.integers(0x400000, 0x500000, int(gdepth[g]) - 3, dtype=np.uint64) for g in range(G)]
 
-    nent = K + int(reused.sum())
+    nper = np.where(reused, max(2, int(cfg.reuse_depth)), 1)
+    nent = int(nper.sum())
     ent = np.zeros(nent, dtype=ENTRY_DTYPE)
     head_frames = rng.integers(0x7F0000000000, 0x7F0000100000, (nent, 3), dtype=np.uint64)
     alloc_jit = rng.integers(0, HORIZON // 100, (K, 2))
     # entries in key order, newest first (vectorised; the only random draws
     # inside the per-key walk are the realloc'd keys' offsets, taken in key
     # order as the scalar walk did)
-    nper = np.where(reused, 2, 1)
     entry_off = np.zeros(K + 1, dtype=np.uint32)
     entry_off[1:] = np.cumsum(nper)
     ek = np.repeat(np.arange(K), nper)               # entry -> key
@@ -425,10 +426,13 @@ def make_table(cfg: SynthConfig, rng: np.random.Generator) -> ObjectTable:
         ent["buffer_addr"][e] = keys[k] + np.uint64(16 * int(rng.integers(1, 64)))
         ent["buffer_size"][e] = size[k] + np.uint64(16 * int(rng.integers(0, 512)))
     j0, j1 = alloc_jit[ek, 0].astype(np.uint64), alloc_jit[ek, 1].astype(np.uint64)
-    two = nper[ek] == 2
-    half = np.uint64(HORIZON // 2)
-    ent["alloc_date"] = np.uint64(T0) + j0 + np.where(two & (ej == 0), half, np.uint64(0))
-    ent["free_date"] = np.uint64(T0) + np.where(two & (ej == 1), half, np.uint64(HORIZON)) - j1
+    # a key's d entries split the horizon: entry ej (0 = newest) lives in
+    # slice d - 1 - ej (d = 1: the whole horizon)
+    d = nper[ek].astype(np.uint64)
+    seg = np.uint64(HORIZON) // d
+    sl = d - np.uint64(1) - ej.astype(np.uint64)
+    ent["alloc_date"] = np.uint64(T0) + j0 + sl * seg
+    ent["free_date"] = np.uint64(T0) + (sl + np.uint64(1)) * seg - j1
     ent["caller_rip"] = grip[eg]
     ent["mem_type"] = MEM_DYNAMIC
     ent["caller_off"] = g_caller_off[eg]
@@ -527,11 +531,13 @@ def _records(n: int, rng: np.random.Generator, cfg: SynthConfig, table: ObjectTa
         e0 = table.entry_off[heap_first + k].astype(np.int64)
         e1 = table.entry_off[heap_first + k + 1].astype(np.int64)
         tso = ts[cat_obj]
-        # newest entry whose lifetime has started (entries are newest-first)
+        # newest entry whose lifetime has started (entries are newest-first,
+        # allocations descending along the chain)
         e = e0.copy()
-        two = (e1 - e0) == 2
-        older = two & (tso < ent["alloc_date"][e0])
-        e[older] += 1
+        ne = e1 - e0
+        for i in range(1, int(ne.max()) if ne.shape[0] else 1):
+            past = (ne > i) & (tso < ent["alloc_date"][np.minimum(e0 + i - 1, ent.shape[0] - 1)])
+            e += past.astype(np.int64)
         base = ent["buffer_addr"][e]
         sz = ent["buffer_size"][e]
         addr[cat_obj] = base + (rng.random(no) * sz).astype(np.uint64)

@@ -82,6 +82,10 @@ ROUTE_CASES = [
     SynthConfig(nb_samples=400_000, nb_intervals=400_000, size_max=4096, heap_clusters=10, seed=77),
     # 3 arenas: a segment each, dense slots
     SynthConfig(nb_samples=300_000, nb_intervals=60_000, heap_clusters=3, cluster_gap=1 << 36, seed=78),
+    # chains of 4 entries on 30 % of the keys: up to ~900 older entries per
+    # partition, so keys past the local pass's LDS list (kOldLds) walk the
+    # chain in global memory
+    SynthConfig(nb_samples=300_000, nb_intervals=20_000, reuse_frac=0.3, reuse_depth=4, seed=80),
 ]
 
 
