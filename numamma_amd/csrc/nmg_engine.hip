@@ -426,6 +426,7 @@ extern "C" int nmg_reset_counters(nmg_engine* h) {
   const uint32_t rgrid = (uint32_t)std::min<uint64_t>((longest + 256 * 16 - 1) / (256 * 16), (uint64_t)h->num_cus * 4);
   HIP_TRY(h, launch_reset(rgrid, h->stream, r));
   h->nreset++;
+  h->counters_fresh = true;
   return NMG_OK;
 }
 

@@ -120,6 +120,9 @@ struct nmg_engine {
   // cells counted by nmg_count_page_cells stay on the device (cells_*) until
   // nmg_get_page_cells of the same epoch copies them out
   uint64_t epoch = 1, cells_epoch = 0;
+  // the counter arrays hold what the last reset wrote (no analysis, import or
+  // table update since): the local pass may store instead of adding
+  bool counters_fresh = false;
   // host memory registered with nmg_register_host (device-visible, pinned):
   // a submitted buffer inside it is read by the kernels in place over PCIe
   // (zc_dev[i] = its device address, 0 = staged)

@@ -325,6 +325,7 @@ extern "C" int nmg_export_array(nmg_engine* h, int which, void* d_dst) {
 
 extern "C" int nmg_import_array(nmg_engine* h, int which, const void* d_src) {
   if (h) h->epoch++;
+  if (h) h->counters_fresh = false;
   Range range("nmg_import_array");
   if (!h || !h->have_table) return NMG_ERR_INVALID;
   size_t bytes = 0;
@@ -365,6 +366,7 @@ extern "C" int nmg_hist_pack(nmg_engine* h, uint32_t threshold, void* d_u8, void
 
 extern "C" int nmg_hist_unpack(nmg_engine* h, const void* d_u8, const void* d_ovf, uint64_t n_ovf) {
   if (h) h->epoch++;
+  if (h) h->counters_fresh = false;
   Range range("nmg_hist_unpack");
   if (!h || !h->have_table || (n_ovf && !d_ovf)) return NMG_ERR_INVALID;
   const uint64_t cells = h->hist_cells * h->T;

@@ -175,7 +175,7 @@ struct PlanParams {
   uint32_t* pcnt;        // in: [grid][nparts] chunk counts; out: exclusive prefix over workgroups
   uint32_t* pbase;       // out: [nparts] first list slot of each partition
   uint4* items;          // out: {partition, list begin, list end, 0}
-  uint32_t* ctl;         // out: [0] number of items, [1] dequeue head (zeroed), [2] overflow records (zeroed)
+  uint32_t* ctl;         // out: [0] number of items, [1] dequeue head (zeroed), [2] overflow records (zeroed), [3] their number for local_kernel
   uint32_t grid, nparts;
 };
 
@@ -207,11 +207,14 @@ struct LocalParams {
   const uint32_t* cmeta;
   const uint32_t* clist;     // chunk id | fill << kChunkIdBits, grouped by partition
   const uint4* items;
-  uint32_t* ctl;             // [0] items, [1] dequeue head
+  uint32_t* ctl;             // [0] items, [1] dequeue head, [3] records of the overflow path (plan_kernel)
   unsigned long long* cmatch;  // [chunks] match bit per record
   const BufDesc* descs;      // analysis order (escaped weights are re-read from the record)
   XLayout xl;
   uint64_t seq0;
+  uint32_t fresh;            // the counters are as the last reset left them (no analysis since): an
+                             // item alone on its partition stores its counters without reading them,
+                             // unless the overflow path or a large weight wrote to them
 };
 
 struct FoundParams {

@@ -368,40 +368,18 @@ __device__ __forceinline__ RDesc route_desc(const RouteParams& rp, const uint4* 
 // holds, after the workgroup's last barrier.
 
 // route2_kernel's workgroup: 12 waves (three per SIMD)
-#ifndef NMG_R2WG
-#define NMG_R2WG 768
-#endif
-constexpr uint32_t kR2WG = NMG_R2WG;
+constexpr uint32_t kR2WG = 768;
 // line stage: partitions q < kLineParts have an LDS line
 constexpr uint32_t kLineParts = 1280;
 // line word (u64): line l's count (3 bits) at 3 * (l mod 8), staged slots
 // (4) at 24, given up at 28, S at 52
-#ifndef NMG_R2_LW32
-#define NMG_R2_LW32 0
-#endif
-#if NMG_R2_LW32
-// (32-bit variant: four lines' counts, S mod 1024)
-typedef uint32_t LineWord;
-constexpr uint32_t kLwMaskShift = 12, kLwSShift = 22, kLwLineMask = 1023, kLwAhead = 4;
-constexpr LineWord kLwBroken = 1u << 16;
-#else
 typedef unsigned long long LineWord;
 constexpr uint32_t kLwMaskShift = 24, kLwSShift = 52, kLwLineMask = 4095, kLwAhead = 8;
 constexpr LineWord kLwBroken = 1ull << 28;
-#endif
 constexpr LineWord kLwOne = 1;
 __device__ __forceinline__ uint32_t lw_count(LineWord w, uint32_t l) { return uint32_t(w >> (3 * (l & (kLwAhead - 1)))) & 7u; }
 __device__ __forceinline__ uint32_t lw_s(LineWord w) { return uint32_t(w >> kLwSShift); }
 __device__ __forceinline__ uint32_t lw_mask(LineWord w) { return uint32_t(w >> kLwMaskShift) & 15u; }
-#ifndef NMG_R2_ABL
-#define NMG_R2_ABL 0
-#endif
-#ifndef NMG_R2_UNALIGNED
-#define NMG_R2_UNALIGNED 0
-#endif
-#ifndef NMG_R2_LINES
-#define NMG_R2_LINES 1
-#endif
 constexpr uint32_t kWaves = kR2WG / 64;
 constexpr uint32_t kWaveWinBytes = 64 * kRecBytes;  // one wave window: 64 stride slots
 constexpr uint32_t kNoBuf = 0xffffffffu;            // RDesc::pad of "no buffer"
@@ -433,17 +411,10 @@ __device__ __forceinline__ void wload(const uint8_t* data, uint64_t off, uint32_
   const __amdgpu_buffer_rsrc_t rs =
       __builtin_amdgcn_make_buffer_rsrc((void*)(data + off), (short)0, (int)len, 0x00020000);
   const uint32_t pos = c + uint32_t(lane) * kRecBytes;
-#if NMG_R2_UNALIGNED
-  // (8 B aligned 16 B loads: hdr ts | addr w | dsrc, no per-lane select)
-  const auto x = __builtin_amdgcn_raw_buffer_load_b128(rs, pos, 0, 0);
-  const auto y = __builtin_amdgcn_raw_buffer_load_b128(rs, pos + 16, 0, 0);
-  const auto z = __builtin_amdgcn_raw_buffer_load_b64(rs, pos + 32, 0, 0);
-#else
   const uint32_t odd = (pos >> 3) & 1;  // 16 B aligned pieces, as load_rec
   const auto x = __builtin_amdgcn_raw_buffer_load_b128(rs, pos + (odd ? 8 : 0), 0, 0);
   const auto y = __builtin_amdgcn_raw_buffer_load_b128(rs, pos + (odd ? 24 : 16), 0, 0);
   const auto z = __builtin_amdgcn_raw_buffer_load_b64(rs, pos + (odd ? 0 : 32), 0, 0);
-#endif
   r.x = make_uint4(x[0], x[1], x[2], x[3]);
   r.y = make_uint4(y[0], y[1], y[2], y[3]);
   r.z = make_uint2(z[0], z[1]);
@@ -541,9 +512,9 @@ __global__ __launch_bounds__(kR2WG, 1) void route2_kernel(RouteParams rp) {
   __shared__ uint64_t s_segst[kRouteSegs];
   // the line stage: per partition a line of four compact records, its line
   // word and its chunk line (pool slot / 4); per wave the lines it writes out
-  __shared__ uint4 s_line[NMG_R2_LINES ? kLineParts * 4 : 1];
-  __shared__ LineWord s_lw[NMG_R2_LINES ? kLineParts : 1];
-  __shared__ uint32_t s_ldst[NMG_R2_LINES ? kLineParts : 1];
+  __shared__ uint4 s_line[kLineParts * 4];
+  __shared__ LineWord s_lw[kLineParts];
+  __shared__ uint32_t s_ldst[kLineParts];
   __shared__ uint2 s_tab[kWaves][64];
 
   Params& p = rp.p;
@@ -565,7 +536,7 @@ __global__ __launch_bounds__(kR2WG, 1) void route2_kernel(RouteParams rp) {
   for (uint32_t i = tid; i < kRouteDir; i += kR2WG) s_pdir[i] = rp.pdir[i];
   for (uint32_t i = tid; i < P; i += kR2WG) s_state[i] = st_pack(kStNone, kStNone, 0, 2 * kChunk);
   // the first line of a partition: slot 0 of generation 1's open chunk
-  const uint32_t nlp = NMG_R2_LINES && !(p.flags & kDbgNoLines) ? min(P, kLineParts) : 0u;
+  const uint32_t nlp = !(p.flags & kDbgNoLines) ? min(P, kLineParts) : 0u;
   for (uint32_t i = tid; i < nlp; i += kR2WG) s_lw[i] = LineWord(kChunk / 4) << kLwSShift;
   // (kDbgLapNoWait: a record one line ahead of S already gives the line up -- tests)
   const uint32_t ahead_max = (p.flags & kDbgLapNoWait) ? 1u : kLwAhead;
@@ -657,7 +628,6 @@ __global__ __launch_bounds__(kR2WG, 1) void route2_kernel(RouteParams rp) {
       d.ta = __builtin_amdgcn_readfirstlane(d.ta);
       d.pad = __builtin_amdgcn_readfirstlane(d.pad);
     };
-    uint32_t sink = 0;  // (NMG_R2_ABL ablations: what the skipped stages would have consumed)
     auto window = [&](RawRec& A, RawRec& B) {
       uni(d0);
       uni(d1);
@@ -671,16 +641,7 @@ __global__ __launch_bounds__(kR2WG, 1) void route2_kernel(RouteParams rp) {
         nwin++;
       }
       rt_stamp<TIMING>(rt, 0);
-#if NMG_R2_UNALIGNED
-      Rec rec;
-      rec.hdr = u64of(A.x.x, A.x.y);
-      rec.ts = u64of(A.x.z, A.x.w);
-      rec.addr = u64of(A.y.x, A.y.y);
-      rec.w = u64of(A.y.z, A.y.w);
-      rec.dsrc = u64of(A.z.x, A.z.y);
-#else
       Rec rec = decode_rec(A, pos);
-#endif
       const bool bad = cand && (uint64_t(pos) + kRecBytes > dw.len || (rec.hdr >> 48) != kRecBytes);
       bool valid;
       uint32_t roff = pos, ncur;
@@ -776,10 +737,6 @@ __global__ __launch_bounds__(kR2WG, 1) void route2_kernel(RouteParams rp) {
       // (mem_sampling.c:882: every SAMPLE, matched or not), partition, chunk
       // slot, store
       rt_stamp<TIMING>(rt, 1);
-#if NMG_R2_ABL >= 5
-      sink ^= (uint32_t)rec.addr ^ (uint32_t)rec.dsrc ^ (uint32_t)rec.w ^ (uint32_t)rec.ts;
-      return;
-#endif
       const uint32_t acc_l = dw.access();
       if (acc_l == 0) {  // (uniform)
         route_count<0>(gacc[0], s_gsums, s_gmins, s_gmaxs, valid, uint32_t(rec.dsrc >> 5) & 0x3fff, rec.w);
@@ -792,10 +749,6 @@ __global__ __launch_bounds__(kR2WG, 1) void route2_kernel(RouteParams rp) {
         gwin = 0;
       }
       rt_stamp<TIMING>(rt, 2);
-#if NMG_R2_ABL >= 4
-      sink ^= (uint32_t)rec.addr ^ (uint32_t)rec.ts;
-      return;
-#endif
       // below the first key ht_lower_key finds no node: counted, not routed
       const bool routed = valid && rec.addr >= first_start;
       const uint32_t q = routed ? route_partition_l(s_seg, s_segst, nseg, s_pb, s_pdir, rec.addr) : 0u;
@@ -808,16 +761,12 @@ __global__ __launch_bounds__(kR2WG, 1) void route2_kernel(RouteParams rp) {
         a = x_encode(rp.xl, pbq, rec.addr, rec.ts, rec.w, dw.pad, roff, dw.thread_rank(), acc_l);
       }
       rt_stamp<TIMING>(rt, 4);
-#if NMG_R2_ABL >= 3
-      sink ^= a.x ^ a.y ^ a.z ^ a.w ^ q;
-      return;
-#endif
       // ---- a slot in q's open chunks: one LDS atomic on the partition's
       // state (route2_claim).  No barrier: the waves run on their own streams.
       uint64_t dst = ~0ull;  // rec16 slot, or ~0: no slot (not routed / overflow list)
       uint32_t lid = 0;      // the slot's chunk line number (mod 4096): the lap that serves it
       bool ovf = false;
-      const bool lined = NMG_R2_LINES && routed && q < nlp;
+      const bool lined = routed && q < nlp;
       // (the line word read beside the claim: a lap can only move on once this
       // record's own line is written, so a lap that equals the record's line
       // here still does after the claim)
@@ -863,13 +812,9 @@ __global__ __launch_bounds__(kR2WG, 1) void route2_kernel(RouteParams rp) {
         }
       }
       rt_stamp<TIMING>(rt, 5);
-#if NMG_R2_ABL >= 2
-      sink ^= a.x ^ a.y ^ a.z ^ a.w ^ (uint32_t)dst ^ lid ^ (uint32_t)lw;
-      return;
-#endif
       // ---- the line stage (see the comment above kR2WG)
       bool staged = false;
-      if (NMG_R2_LINES && __ballot(lined)) {
+      if (__ballot(lined)) {
         lid &= kLwLineMask;
         const uint32_t j = (uint32_t)dst & 3u, S = lw_s(lw), ahead = (lid - S) & kLwLineMask;
         // (a record of the overflow list has no slot but counts for its line)
@@ -882,11 +827,7 @@ __global__ __launch_bounds__(kR2WG, 1) void route2_kernel(RouteParams rp) {
           // (the record before the count that may complete the line)
           __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
         } else if (counts && dst != ~0ull) {
-#if NMG_R2_ABL >= 1
-          sink ^= a.x ^ (uint32_t)dst;
-#else
           rp.rec16[dst] = a;
-#endif
         }
         bool done = false;
         uint32_t dmask = 0;
@@ -912,11 +853,7 @@ __global__ __launch_bounds__(kR2WG, 1) void route2_kernel(RouteParams rp) {
             if (jj < nd) {
               const uint2 t = s_tab[wave][jj];
               const uint32_t tq = t.x & 2047u, tm = (t.x >> 11) & 15u, k = lane & 3;
-#if NMG_R2_ABL >= 1
-              if ((tm >> k) & 1) sink ^= s_line[tq * 4 + k].x ^ t.y;
-#else
               if ((tm >> k) & 1) rp.rec16[uint64_t(t.y) * 4 + k] = s_line[tq * 4 + k];
-#endif
               // (the line read by all four lanes -- one instruction, waited
               // for by the stores -- before S moves on and its slots are reused)
               __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
@@ -934,15 +871,11 @@ __global__ __launch_bounds__(kR2WG, 1) void route2_kernel(RouteParams rp) {
           }
         }
       }
-      if (!NMG_R2_LINES || !lined) staged = false;
+      if (!lined) staged = false;
       rt_stamp<TIMING>(rt, 9);
       // the records the line stage did not take: not lined, or given up
       const bool straight = dst != ~0ull && !(lined && !(lw & kLwBroken) && ((lid - lw_s(lw)) & kLwLineMask) < ahead_max);
-#if NMG_R2_ABL >= 1
-      if (straight) sink ^= a.y ^ (uint32_t)dst;
-#else
       if (straight) rp.rec16[dst] = a;
-#endif
       if (TIMING) {  // (records staged / stored straight to their slot)
         rt.acc[6] += (uint64_t)__popcll(__ballot(staged));
         rt.acc[7] += (uint64_t)__popcll(__ballot(straight));
@@ -969,7 +902,6 @@ __global__ __launch_bounds__(kR2WG, 1) void route2_kernel(RouteParams rp) {
       window(ra, rb);
       window(rb, ra);
     } while (d0.pad != kNoBuf);
-    if (sink == 0x9e3779b9u) rp.used[blockIdx.x] = sink;  // (never: keeps the ablated stages' inputs live)
     if (TIMING && lane == 0) {
       unsigned long long* o = p.dbg + (uint64_t(blockIdx.x) * (kWG / 64) + tid / 64) * kRouteTimingWords;
       for (int k = 0; k < 9; k++) o[k] = rt.acc[k];
@@ -1106,6 +1038,7 @@ __global__ __launch_bounds__(kWG) void plan_kernel(PlanParams r) {
   if (tid == kWG - 1) {
     r.ctl[0] = wn + in;
     r.ctl[1] = 0;
+    r.ctl[3] = r.ctl[2];  // this launch's overflow-path records (read by local_kernel)
     r.ctl[2] = 0;  // overflow list (read by overflow_kernel before this launch)
   }
 }
@@ -1128,19 +1061,12 @@ __global__ __launch_bounds__(kWG) void scatter_kernel(ScatterParams r) {
 // ---------------------------------------------------------------------------
 // pass 3: attribute one partition per workgroup at a time
 
-// a load served by L2, never by this CU's L1 (global_load ... sc1)
 // local pass: workgroup size and chunks per interleaved group (a wave holds
 // two groups: one being attributed, the other's records in flight)
-#ifndef NMG_LWG
-#define NMG_LWG 1024
-#endif
-#ifndef NMG_LC
-#define NMG_LC 2
-#endif
-#define NMG_STR2(x) #x
-#define NMG_STR(x) NMG_STR2(x)
-constexpr uint32_t kLWG = NMG_LWG;
-constexpr int kLC = NMG_LC;
+constexpr uint32_t kLWG = 1024;
+constexpr int kLC = 2;  // (the timing wait below counts on it)
+
+// a load served by L2, never by this CU's L1 (global_load ... sc1)
 template <typename T>
 __device__ __forceinline__ T l2_load(const T* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1184,7 +1110,7 @@ __global__ __launch_bounds__(kLWG, 1) void local_kernel(LocalParams lp) {
   __shared__ unsigned long long s_first[kPartEntries];
   __shared__ uint32_t s_pg[kPartCells / 2];
   __shared__ uint32_t s_clist[kItemChunks];  // the item's chunk list entries
-  __shared__ uint32_t s_item, s_cnext, s_nfound;
+  __shared__ uint32_t s_item, s_cnext, s_nfound, s_big;
 
   Params& p = lp.p;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -1240,6 +1166,7 @@ __global__ __launch_bounds__(kLWG, 1) void local_kernel(LocalParams lp) {
     const uint32_t ncell = (pages && pi.pages_lds) ? T * pi.span : 0u;
     const bool excl = item.w != 0 && !(p.flags & kDbgLocalAtomics);  // no other workgroup writes this partition's
                                                                      // counters
+    if (tid == 0) s_big = 0;
     lds_sync();
     const uint64_t k0key = u64of(__builtin_amdgcn_readfirstlane((uint32_t)s_keys[0]),
                                  __builtin_amdgcn_readfirstlane((uint32_t)(s_keys[0] >> 32)));
@@ -1274,7 +1201,7 @@ __global__ __launch_bounds__(kLWG, 1) void local_kernel(LocalParams lp) {
         valid[j] = (uint32_t)lane < fill;
       }
       if (TIMING) {  // (timing: these chunks' loads count as wait; the other group's kLC loads are younger)
-        asm volatile("s_waitcnt vmcnt(" NMG_STR(NMG_LC) ")" ::: "memory");
+        asm volatile("s_waitcnt vmcnt(2)" ::: "memory");  // (kLC)
         nchunks += kLC;
       }
       rt_stamp<TIMING>(rt, 0);
@@ -1490,6 +1417,7 @@ __global__ __launch_bounds__(kLWG, 1) void local_kernel(LocalParams lp) {
 #pragma unroll
       for (int j = 0; j < kLC; j++) anybig |= erel[j] >= 0 && w[j] >= kLaneMaxWeight;
       if (__ballot(anybig) && !noobj) {  // (rare) large weights
+        if (lane == 0) s_big = 1;  // (this item's counters are no longer fresh)
 #pragma unroll
         for (int j = 0; j < kLC; j++) {
           if (erel[j] < 0 || w[j] < kLaneMaxWeight) continue;
@@ -1565,6 +1493,12 @@ __global__ __launch_bounds__(kLWG, 1) void local_kernel(LocalParams lp) {
     }
     lds_sync();
     rt_stamp<TIMING>(rt, 9);  // (waiting for the item's slowest wave)
+    // an item alone on its partition whose counters nothing else wrote since
+    // the reset (no overflow-path record in this launch, no large weight in
+    // this item) stores them without reading: counts and weights from zero,
+    // first ordinals from ~0, page cells from zero
+    const bool clean = excl && lp.fresh && __builtin_amdgcn_readfirstlane(lp.ctl[3]) == 0;
+    const bool clean_obj = clean && __builtin_amdgcn_readfirstlane(s_big) == 0;
     // the item's counters to global memory, consecutive lanes on consecutive
     // words, each LDS word zeroed for the next item as it is read; the only
     // item of its partition adds with plain loads and stores (no other
@@ -1580,7 +1514,10 @@ __global__ __launch_bounds__(kLWG, 1) void local_kernel(LocalParams lp) {
         const uint64_t cnt = v >> kPackShift, wt = v & ((1ull << kPackShift) - 1);
         uint64_t* pc = p.sum64 + objcw_index(e, a, 0, p.nb_entries);
         uint64_t* pw = p.sum64 + objcw_index(e, a, 1, p.nb_entries);
-        if (excl) {  // (loads past L1: this workgroup's own large-weight atomics went to L2)
+        if (clean_obj) {
+          *pc = cnt;
+          if (wt) *pw = wt;
+        } else if (excl) {  // (loads past L1: this workgroup's own large-weight atomics went to L2)
           *pc = l2_load(pc) + cnt;
           if (wt) *pw = l2_load(pw) + wt;
         } else {
@@ -1593,7 +1530,8 @@ __global__ __launch_bounds__(kLWG, 1) void local_kernel(LocalParams lp) {
         s_first[i] = ~0ull;
         const uint64_t fo = ((lp.seq0 + (floc >> lp.xl.obits)) << 32) | ((floc & ((1ull << lp.xl.obits) - 1)) << 3);
         uint64_t* pf = p.min64 + 36 + e;
-        if (excl) *pf = min(l2_load(pf), fo);
+        if (clean) *pf = fo;
+        else if (excl) *pf = min(l2_load(pf), fo);
         else atomicMin(reinterpret_cast<unsigned long long*>(pf), (unsigned long long)fo);
       }
     }
@@ -1620,7 +1558,7 @@ __global__ __launch_bounds__(kLWG, 1) void local_kernel(LocalParams lp) {
             uint64_t cell = pi.cb + rel;
             if (cmap != ~0u) cell = cnt[u][h] ? lp.pe_cmap[cmap + rel] : 0u;  // (online: packed cells)
             pc[u][h] = p.hist + uint64_t(th) * p.hist_cells + cell;
-            old[u][h] = (excl && cnt[u][h]) ? l2_load(pc[u][h]) : 0u;
+            old[u][h] = (excl && !clean && cnt[u][h]) ? l2_load(pc[u][h]) : 0u;
           }
         }
 #pragma unroll

@@ -89,8 +89,8 @@ int route_pool(nmg_engine* h, const std::vector<BufDesc>& descs, uint32_t grid, 
     HIP_TRY(h, hipMalloc(&h->d_used, grid * 4));
     HIP_TRY(h, hipMalloc(&h->d_pcnt, (size_t)grid * (kMaxParts + 1) * 4));
     HIP_TRY(h, hipMalloc(&h->d_pbase, (kMaxParts + 1) * 4));
-    HIP_TRY(h, hipMalloc(&h->d_ctl, 3 * 4));
-    HIP_TRY(h, hipMemset(h->d_ctl, 0, 3 * 4));
+    HIP_TRY(h, hipMalloc(&h->d_ctl, 4 * 4));
+    HIP_TRY(h, hipMemset(h->d_ctl, 0, 4 * 4));
     HIP_TRY(h, hipMalloc(&h->d_ovf16, ovf * sizeof(uint4)));
     HIP_TRY(h, hipMalloc(&h->d_ovfx, ovf * 8));
     h->ovf_cap = ovf;
@@ -165,13 +165,6 @@ int route_analyze_job(nmg_engine* h, const RouteJob& job) {
   }
   HIP_TRY(h, launch_route(grid, h->stream, rp));
   HIP_TRY(h, hipEventRecord(h->ringr[slot], h->stream));
-#if NMG_R2_ABL  // (ablation builds, tools/ab_build.sh: the route pass alone, its output unused)
-  HIP_TRY(h, hipEventRecord(h->ringm[slot], h->stream));
-  HIP_TRY(h, hipEventRecord(h->ring1[slot], h->stream));
-  h->nlaunch++;
-  h->launched = true;
-  return NMG_OK;
-#endif
   HIP_TRY(h, launch_overflow(h->stream, rp));
   ScatterParams sc;
   sc.cmeta = h->d_cmeta;
@@ -217,6 +210,8 @@ int route_analyze_job(nmg_engine* h, const RouteJob& job) {
   lp.descs = job.sdescs;
   lp.xl = xl;
   lp.seq0 = seq0;
+  lp.fresh = h->counters_fresh ? 1u : 0u;
+  h->counters_fresh = false;
   if ((h->flags & kDbgLocalTiming) && !(h->flags & kDbgRouteTiming)) {  // (internal) per-wave phase cycles
     const size_t n = (size_t)h->num_cus * (kWG / 64) * kRouteTimingWords;
     if (n > h->dbg_cap) {

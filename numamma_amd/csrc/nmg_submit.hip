@@ -728,8 +728,10 @@ int launch_attribution(nmg_engine* h, const uint8_t* data, const BufDesc* sdescs
       HIP_TRY(h, hipMemsetAsync(h->d_dbg, 0, n * 8, h->stream));
       h->dbg_len = n;
       p.dbg = reinterpret_cast<unsigned long long*>(h->d_dbg);
+      h->counters_fresh = false;
       HIP_TRY(h, launch_attribute(true, mode, grid, h->stream, p));
     } else {
+      h->counters_fresh = false;
       HIP_TRY(h, launch_attribute(false, mode, grid, h->stream, p));
     }
     HIP_TRY(h, hipEventRecord(h->ringr[slot], h->stream));
