@@ -499,6 +499,49 @@ __device__ __forceinline__ void route2_advance(unsigned long long* st, uint32_t 
   }
 }
 
+// a claim's outcome: the rec16 slot (~0: none), its chunk line, the
+// overflow list; !ok: a void claim, past the next chunk -- wait for
+// generation waitg to end and claim again
+struct Claim {
+  uint64_t dst;
+  uint32_t lid, waitg;
+  bool ovf, ok;
+};
+__device__ __forceinline__ Claim route2_settle(uint64_t old, uint32_t q, unsigned long long* s_state, uint32_t& taken,
+                                               uint32_t capl, uint32_t* cmeta, uint32_t c0) {
+  Claim r;
+  r.dst = ~0ull;
+  r.lid = 0;
+  r.waitg = 0;
+  r.ovf = false;
+  r.ok = true;
+  const uint32_t f = st_cnt(old), g = st_gen(old), cu = st_cur(old), nx = st_next(old);
+  if (cu != kStNone && f < 2 * kChunk) {  // a slot of the open chunk or of the next one
+    const uint32_t c = f < kChunk ? cu : nx;
+    if (c == kStOvf) r.ovf = true;
+    else r.dst = uint64_t(c0 + c) * kChunk + (f & (kChunk - 1));
+    r.lid = ((g << 6) + f) >> 2;  // (slot f - 64 of the next chunk = generation g + 1's slot)
+    if (f == kChunk + kChunk / 2) {  // half of the next chunk claimed: open the one after it
+      const uint32_t n2 = route2_take(taken, capl);
+      if (n2 != kStOvf) cmeta[c0 + n2] = q | (kChunk << 24);
+      route2_advance(&s_state[q], g, n2, n2, false, old + 1);
+    }
+  } else if (cu == kStNone && f == 2 * kChunk) {  // q's first claim: open two chunks
+    const uint32_t n1 = route2_take(taken, capl);
+    const uint32_t n2 = n1 == kStOvf ? kStOvf : route2_take(taken, capl);
+    if (n1 != kStOvf) cmeta[c0 + n1] = q | (kChunk << 24);
+    if (n2 != kStOvf) cmeta[c0 + n2] = q | (kChunk << 24);
+    route2_advance(&s_state[q], g, n1, n2, true, old + 1);
+    if (n1 == kStOvf) r.ovf = true;
+    else r.dst = uint64_t(c0 + n1) * kChunk;
+    r.lid = (g + 1) << 4;  // slot 0 of generation g + 1
+  } else {
+    r.waitg = g;
+    r.ok = false;
+  }
+  return r;
+}
+
 template <bool TIMING>
 __global__ __launch_bounds__(kR2WG, 1) void route2_kernel(RouteParams rp) {
   __shared__ uint64_t s_pb[kMaxParts + 1];
@@ -772,38 +815,27 @@ __global__ __launch_bounds__(kR2WG, 1) void route2_kernel(RouteParams rp) {
       // here still does after the claim)
       LineWord lw = lined ? s_lw[q] : LineWord(0);
       {
-        bool todo = routed, spin = false;
         uint32_t waitg = 0;
-        while (__ballot(todo)) {
+        bool todo = false;
+        if (routed) {
+          const Claim c = route2_settle(atomicAdd(&s_state[q], 1ull), q, s_state, s_taken, capl, rp.cmeta, c0);
+          dst = c.dst;
+          lid = c.lid;
+          ovf = c.ovf;
+          waitg = c.waitg;
+          todo = !c.ok;
+        }
+        bool spin = todo;
+        while (__ballot(todo)) {  // (rare) void claims
           if (todo) {
             if (!spin) {
-              const uint64_t old = atomicAdd(&s_state[q], 1ull);
-              const uint32_t f = st_cnt(old), g = st_gen(old), cu = st_cur(old), nx = st_next(old);
-              if (cu != kStNone && f < 2 * kChunk) {  // a slot of the open chunk or of the next one
-                const uint32_t c = f < kChunk ? cu : nx;
-                if (c == kStOvf) ovf = true;
-                else dst = uint64_t(c0 + c) * kChunk + (f & (kChunk - 1));
-                lid = ((g << 6) + f) >> 2;  // (slot f - 64 of the next chunk = generation g + 1's slot)
-                todo = false;
-                if (f == kChunk + kChunk / 2) {  // half of the next chunk claimed: open the one after it
-                  const uint32_t n2 = route2_take(s_taken, capl);
-                  if (n2 != kStOvf) rp.cmeta[c0 + n2] = q | (kChunk << 24);
-                  route2_advance(&s_state[q], g, n2, n2, false, old + 1);
-                }
-              } else if (cu == kStNone && f == 2 * kChunk) {  // q's first claim: open two chunks
-                const uint32_t n1 = route2_take(s_taken, capl);
-                const uint32_t n2 = n1 == kStOvf ? kStOvf : route2_take(s_taken, capl);
-                if (n1 != kStOvf) rp.cmeta[c0 + n1] = q | (kChunk << 24);
-                if (n2 != kStOvf) rp.cmeta[c0 + n2] = q | (kChunk << 24);
-                route2_advance(&s_state[q], g, n1, n2, true, old + 1);
-                if (n1 == kStOvf) ovf = true;
-                else dst = uint64_t(c0 + n1) * kChunk;
-                lid = (g + 1) << 4;  // slot 0 of generation g + 1
-                todo = false;
-              } else {  // void claim (past the next chunk): wait for the next generation
-                spin = true;
-                waitg = g;
-              }
+              const Claim c = route2_settle(atomicAdd(&s_state[q], 1ull), q, s_state, s_taken, capl, rp.cmeta, c0);
+              dst = c.dst;
+              lid = c.lid;
+              ovf = c.ovf;
+              waitg = c.waitg;
+              todo = !c.ok;
+              spin = todo;
             } else {
               const uint64_t st = __hip_atomic_load(&s_state[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
               spin = st_gen(st) == waitg;
