@@ -154,7 +154,9 @@ def main():
                     help="records in the reference-loop oracle's sample (its linear call-site list is quadratic)")
     ap.add_argument("--cpu-st-records", type=int, default=2_000_000,
                     help="records in the one-thread run of the multi-threaded restatement")
-    ap.add_argument("--cpu-mt-records", type=int, default=25_000_000, help="records in the multi-threaded baseline's sample")
+    ap.add_argument("--cpu-mt-records", type=int, default=62_500_000,
+                    help="records in the multi-threaded baseline's sample (about 0.8 s a run on 16 threads: long "
+                         "enough that the shared host's noise averages out within a run)")
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)),
                     help="host threads of the multi-threaded CPU baseline (default: this job's CPU share, "
                          "OMP_NUM_THREADS, else every CPU)")
@@ -522,6 +524,8 @@ def cpu_baseline(rp, max_records, mt_records, threads, st_records, target_s=20.0
                       f"{threads} threads ({secs:.1f}s of analysis + merge), median run; {host}",
             "runs": rates,
             "spread": [float(min(rates)), float(max(rates))],
+            # interquartile range relative to the median (the runs' spread without the outliers)
+            "iqr_pct": float(100.0 * (np.percentile(rates, 75) - np.percentile(rates, 25)) / v),
         }
         os.remove(path)
         sub, n = _sample_replay(rp, st_records)

@@ -173,7 +173,7 @@ struct RouteParams {
 
 struct PlanParams {
   uint32_t* pcnt;        // in: [grid][nparts] chunk counts; out: exclusive prefix over workgroups
-  uint32_t* pbase;       // out: [nparts] first list slot of each partition
+  uint32_t* pbase;       // out: [nparts] first list slot of each partition (plan_cols_kernel: the totals)
   uint4* items;          // out: {partition, list begin, list end, 0}
   uint32_t* ctl;         // out: [0] number of items, [1] dequeue head (zeroed), [2] overflow records (zeroed), [3] their number for local_kernel
   uint32_t grid, nparts;

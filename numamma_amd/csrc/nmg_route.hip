@@ -1013,23 +1013,58 @@ __global__ __launch_bounds__(kWG) void count_kernel(CountParams cp) {
   for (uint32_t q = tid; q < P; q += kWG) out[q] = s_cnt[q];
 }
 
+// pass 2a: per partition, the exclusive prefix of its chunk counts over the
+// route workgroups (a column of pcnt), and the partition's total into pbase.
+// 64 partitions per workgroup, the rows in 16 groups of consecutive
+// workgroups: every count of a thread in flight at once, the groups' sums
+// combined in LDS.
+constexpr uint32_t kPlanRowGroups = kWG / 64;
+__global__ __launch_bounds__(kWG) void plan_cols_kernel(PlanParams r) {
+  __shared__ uint32_t s_sum[kPlanRowGroups][64];
+  const uint32_t tid = threadIdx.x, c = tid & 63, rg = tid >> 6;
+  const uint32_t P = r.nparts, q = blockIdx.x * 64 + c;
+  const uint32_t per = (r.grid + kPlanRowGroups - 1) / kPlanRowGroups, w0 = rg * per;
+  constexpr uint32_t kU = 16;  // counts in registers (groups of more rows: in steps of kU)
+  uint32_t sum = 0;
+  for (uint32_t b = 0; b < per; b += kU) {
+    uint32_t v[kU];
+#pragma unroll
+    for (uint32_t u = 0; u < kU; u++) {
+      const uint32_t w = w0 + b + u;
+      v[u] = (q < P && b + u < per && w < r.grid) ? r.pcnt[uint64_t(w) * P + q] : 0u;
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < kU; u++) sum += v[u];
+  }
+  s_sum[rg][c] = sum;
+  __syncthreads();
+  uint32_t run = 0;
+  for (uint32_t g = 0; g < rg; g++) run += s_sum[g][c];
+  for (uint32_t b = 0; b < per; b += kU) {
+    uint32_t v[kU];
+#pragma unroll
+    for (uint32_t u = 0; u < kU; u++) {
+      const uint32_t w = w0 + b + u;
+      v[u] = (q < P && b + u < per && w < r.grid) ? r.pcnt[uint64_t(w) * P + q] : 0u;
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < kU; u++) {
+      const uint32_t w = w0 + b + u;
+      if (q < P && b + u < per && w < r.grid) r.pcnt[uint64_t(w) * P + q] = run;
+      run += v[u];
+    }
+  }
+  if (q < P && rg == kPlanRowGroups - 1) r.pbase[q] = run;  // (the last group: the column's total)
+}
+
+// pass 2b (one workgroup): the partitions' first list slots and work items
+// from their totals (plan_cols_kernel)
 __global__ __launch_bounds__(kWG) void plan_kernel(PlanParams r) {
   __shared__ uint32_t s_tot[kMaxParts + 1], s_nit[kMaxParts + 1], s_wsum[2][kWG / 64];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const uint32_t P = r.nparts;
-  for (uint32_t q = tid; q < P; q += kWG) {  // per partition: exclusive prefix over the workgroups
-    uint32_t run = 0;
-    constexpr uint32_t kU = 32;  // loads of kU workgroups in flight before their prefixes are stored
-    for (uint32_t w0 = 0; w0 < r.grid; w0 += kU) {
-      uint32_t v[kU];
-#pragma unroll
-      for (uint32_t u = 0; u < kU; u++) v[u] = w0 + u < r.grid ? r.pcnt[uint64_t(w0 + u) * P + q] : 0u;
-#pragma unroll
-      for (uint32_t u = 0; u < kU; u++) {
-        if (w0 + u < r.grid) r.pcnt[uint64_t(w0 + u) * P + q] = run;
-        run += v[u];
-      }
-    }
+  for (uint32_t q = tid; q < P; q += kWG) {
+    const uint32_t run = r.pbase[q];
     s_tot[q] = run;
     s_nit[q] = (run + kItemChunks - 1) / kItemChunks;
   }
@@ -1669,6 +1704,7 @@ hipError_t launch_route(uint32_t grid, hipStream_t s, const RouteParams& r) {
 }
 
 hipError_t launch_plan(hipStream_t s, const PlanParams& r) {
+  if (r.nparts) hipLaunchKernelGGL(plan_cols_kernel, dim3((r.nparts + 63) / 64), dim3(kWG), 0, s, r);
   hipLaunchKernelGGL(plan_kernel, dim3(1), dim3(kWG), 0, s, r);
   return hipGetLastError();
 }
