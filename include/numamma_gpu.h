@@ -312,6 +312,31 @@ int64_t nmg_count_page_cells(nmg_engine *h);
 /* non-zero cells as (entry, thread, page, count) rows in (entry, thread, page) order */
 int nmg_get_page_cells(nmg_engine *h, uint32_t *rows /* [n][4] */, int64_t n);
 
+/* ---- results snapshot: the getters' results copied to host memory while
+ * the next analysis runs (one engine of one GPU; not a multi-GPU handle, not
+ * after nmg_set_buffer_counts).
+ * nmg_results_begin enqueues, behind the analyses already enqueued, a device
+ * copy of every result (the per-buffer matched counts and the page-cell rows
+ * built there) and their copy to pinned host memory on a stream of their
+ * own, and returns: the engine may be reset and analyse again at once.
+ * nmg_results_end waits for that copy and describes it; the arrays are the
+ * engine's and stay valid until the next nmg_results_begin or
+ * nmg_destroy.  Their content equals what nmg_get_global_counters,
+ * nmg_get_buffer_counts, nmg_get_object_counters and nmg_get_page_cells
+ * returned at the time of nmg_results_begin. */
+struct nmg_results_view {
+  struct nmg_mem_counters global[2];
+  uint64_t nb_samples, nb_found;
+  uint32_t nb_buffers, nb_entries;
+  const uint32_t *buffer_samples, *buffer_found; /* [nb_buffers] */
+  const uint64_t *first_ordinal;                 /* [nb_entries] */
+  const uint64_t *count_weight;                  /* [nb_entries][2][2] */
+  int64_t nb_cells;
+  const uint32_t *cells;                         /* [nb_cells][4] as nmg_get_page_cells */
+};
+int nmg_results_begin(nmg_engine *h);
+int nmg_results_end(nmg_engine *h, struct nmg_results_view *out);
+
 /* ---- multi-GPU merge (sharded buffer lists, one engine per rank) ----
  * Arrays are exposed as flat u64 / u32 vectors so a caller can reduce them
  * with RCCL (torch.distributed) over xGMI:

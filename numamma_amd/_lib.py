@@ -140,6 +140,22 @@ class nmg_host_results(C.Structure):
     ]
 
 
+class nmg_results_view(C.Structure):
+    _fields_ = [
+        ("global_", nmg_mem_counters * 2),
+        ("nb_samples", C.c_uint64),
+        ("nb_found", C.c_uint64),
+        ("nb_buffers", C.c_uint32),
+        ("nb_entries", C.c_uint32),
+        ("buffer_samples", C.POINTER(C.c_uint32)),
+        ("buffer_found", C.POINTER(C.c_uint32)),
+        ("first_ordinal", C.POINTER(C.c_uint64)),
+        ("count_weight", C.POINTER(C.c_uint64)),
+        ("nb_cells", C.c_int64),
+        ("cells", C.POINTER(C.c_uint32)),
+    ]
+
+
 assert C.sizeof(nmg_mem_counters) == 600
 assert C.sizeof(nmg_object) == 32
 
@@ -181,6 +197,8 @@ _SIGS = {
     "nmg_get_object_levels": (C.c_int, [H, u64p]),
     "nmg_count_page_cells": (C.c_int64, [H]),
     "nmg_get_page_cells": (C.c_int, [H, u32p, C.c_int64]),
+    "nmg_results_begin": (C.c_int, [H]),
+    "nmg_results_end": (C.c_int, [H, C.POINTER(nmg_results_view)]),
     "nmg_array_size": (C.c_uint64, [H, C.c_int]),
     "nmg_export_array": (C.c_int, [H, C.c_int, P]),
     "nmg_import_array": (C.c_int, [H, C.c_int, P]),

@@ -340,6 +340,7 @@ extern "C" void nmg_destroy(nmg_engine* h) {
   (void)hipFree(h->d_dbg);
   (void)hipFree(h->d_smatch);
   if (h->h_stage) (void)hipHostFree(h->h_stage);
+  snap_free(h);
   if (h->copy_stream) (void)hipStreamSynchronize(h->copy_stream);
   for (auto& sl : h->slots) {
     if (sl.h_stage) (void)hipHostFree(sl.h_stage);

@@ -142,6 +142,27 @@ struct nmg_engine {
     std::vector<std::pair<uint64_t, uint32_t>> cells;  // ((thread << 32 | page), count)
   };
   std::vector<SparseRows> cells_sparse;
+  // results snapshot (nmg_results_begin / nmg_results_end, nmg_results.hip)
+  struct ResSnap {
+    hipStream_t stream = nullptr;
+    hipEvent_t ready = nullptr, copied = nullptr;
+    bool pending = false;
+    bool meta_dirty = true;            // hist_base / npages / sparse entries changed: re-upload
+    uint64_t E = 0, nb = 0, nsent = 0, rows_dev = 0, rows_host = 0, sparse_cap = 0;
+    uint64_t *d_base = nullptr, *d_off = nullptr, *d_part = nullptr, *d_soff = nullptr;
+    uint32_t *d_np = nullptr, *d_cnt = nullptr, *d_sent = nullptr;
+    uint64_t *d_sum = nullptr, *d_min = nullptr, *d_max = nullptr, *d_objcw = nullptr, *d_found = nullptr;
+    uint32_t* d_bufcnt = nullptr;
+    uint64_t* d_ck = nullptr;          // the sparse table's used slots, compacted (+ their count)
+    void* d_rows = nullptr;            // uint4 rows
+    // pinned host copies
+    uint64_t *h_sum = nullptr, *h_min = nullptr, *h_max = nullptr, *h_objcw = nullptr, *h_small = nullptr,
+             *h_soff = nullptr;        // h_small: [0] matched total, [1] rows, [2] sparse cells
+    uint32_t* h_bufcnt = nullptr;
+    uint32_t* h_rows = nullptr;        // mapped: copy_rows_kernel writes it
+    uint64_t h_cap_E = 0, h_cap_nb = 0, h_cap_sent = 0;
+  } snap;
+  uint64_t snap_nb = 0;  // buffers of the snapshot in flight
   uint32_t K = 0, E = 0;
   uint64_t* d_keys = nullptr;
   DevEntry* d_nodes = nullptr;
@@ -349,6 +370,7 @@ int fail(nmg_engine* h, int code, const std::string& msg);
 void free_counters(nmg_engine* h);
 void free_lookup(nmg_engine* h);
 void free_route_table(nmg_engine* h);
+void snap_free(nmg_engine* h);  // the results snapshot's buffers and stream
 void free_route_pool(nmg_engine* h);
 LookupSet take_lookup(nmg_engine* h);
 void put_lookup(nmg_engine* h, const LookupSet& l);

@@ -225,6 +225,12 @@ hipError_t launch_objcw_aos(hipStream_t s, const uint64_t* soa, uint64_t E, void
 // page-cell rows on the device (nmg_get_page_cells / nmg_report): per dense
 // entry the number of non-zero cells, then the (entry, thread, page, count)
 // rows at each entry's offset, in (thread, page) order
+hipError_t launch_cells_sparse_count(hipStream_t s, const uint64_t* ck, const unsigned long long* n_ptr, uint64_t cap,
+                                     const uint32_t* sent, uint32_t nsent, const uint64_t* base, uint32_t* cnt);
+uint32_t scan_parts(uint64_t n);  // partial sums launch_scan_u32 needs (+ 1)
+hipError_t launch_scan_u32(hipStream_t s, const uint32_t* in, uint64_t n, uint64_t* out /* [n + 1] */, uint64_t* part);
+hipError_t launch_gather_off(hipStream_t s, const uint64_t* off, const uint32_t* sent, uint32_t nsent, uint64_t* out);
+hipError_t launch_copy_rows(hipStream_t s, const void* src, const uint64_t* n_ptr, uint64_t cap, void* dst);
 hipError_t launch_cells_count(hipStream_t s, const uint32_t* hist, uint64_t hist_cells, uint32_t T,
                               const uint64_t* base, const uint32_t* np, uint32_t E, uint32_t* cnt);
 hipError_t launch_cells_emit(hipStream_t s, const uint32_t* hist, uint64_t hist_cells, uint32_t T,

@@ -1326,6 +1326,122 @@ __global__ __launch_bounds__(256) void cells_emit_kernel(const uint32_t* hist, u
   }
 }
 
+// The results snapshot's cell rows (nmg_results_begin) without a host round
+// trip: the sparse table's compacted cells counted per entry, an exclusive
+// scan of the per-entry counts into row offsets on the device, the sparse
+// entries' offsets gathered, and the rows copied into mapped host memory by
+// a kernel that reads their number on the device.
+__global__ __launch_bounds__(256) void cells_sparse_count_kernel(const uint64_t* ck, const unsigned long long* n_ptr,
+                                                                 const uint32_t* sent, uint32_t nsent,
+                                                                 const uint64_t* base, uint32_t* cnt) {
+  const uint64_t n = *n_ptr;
+  for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += gridDim.x * 256ull) {
+    const uint64_t key = ck[2 * i];
+    const uint32_t s = uint32_t(key >> 42);  // (sparse_key_idx)
+    // (an entry's sparse cells count only where it has no dense cells, as cells_prepare)
+    if (key != ~0ull && ck[2 * i + 1] && s < nsent && base[sent[s]] == ~0ull) atomicAdd(&cnt[sent[s]], 1u);
+  }
+}
+
+constexpr uint32_t kScanItems = 16, kScanBlock = 256 * kScanItems;
+__device__ __forceinline__ uint32_t scan_thread_sum(const uint32_t* in, uint64_t n, uint64_t i0) {
+  uint32_t t = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < kScanItems; k++) t += i0 + k < n ? in[i0 + k] : 0u;
+  return t;
+}
+// the block's exclusive prefix of per-thread values (256 threads) and its total
+__device__ __forceinline__ uint64_t block_excl_scan(uint64_t v, uint64_t* s_w, uint64_t& total) {
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint64_t x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint64_t y = __shfl_up(x, o, 64);
+    if ((int)lane >= o) x += y;
+  }
+  if (lane == 63) s_w[wave] = x;
+  __syncthreads();
+  uint64_t base = 0;
+  total = 0;
+  for (uint32_t w = 0; w < 4; w++) {
+    if (w < wave) base += s_w[w];
+    total += s_w[w];
+  }
+  __syncthreads();
+  return base + x - v;
+}
+__global__ __launch_bounds__(256) void scan_sums_kernel(const uint32_t* in, uint64_t n, uint64_t* part) {
+  __shared__ uint64_t s_w[4];
+  const uint64_t i0 = uint64_t(blockIdx.x) * kScanBlock + threadIdx.x * kScanItems;
+  uint64_t total;
+  (void)block_excl_scan(scan_thread_sum(in, n, i0), s_w, total);
+  if (threadIdx.x == 0) part[blockIdx.x] = total;
+}
+__global__ __launch_bounds__(256) void scan_parts_kernel(uint64_t* part, uint32_t nb) {
+  __shared__ uint64_t s_w[4];
+  uint64_t carry = 0;
+  for (uint32_t b0 = 0; b0 < nb; b0 += 256) {
+    const uint32_t b = b0 + threadIdx.x;
+    const uint64_t v = b < nb ? part[b] : 0ull;
+    uint64_t total;
+    const uint64_t pre = block_excl_scan(v, s_w, total);
+    if (b < nb) part[b] = carry + pre;
+    carry += total;
+  }
+  if (threadIdx.x == 0) part[nb] = carry;
+}
+__global__ __launch_bounds__(256) void scan_apply_kernel(const uint32_t* in, uint64_t n, const uint64_t* part,
+                                                         uint64_t* out) {
+  __shared__ uint64_t s_w[4];
+  const uint64_t i0 = uint64_t(blockIdx.x) * kScanBlock + threadIdx.x * kScanItems;
+  uint64_t total;
+  uint64_t o = part[blockIdx.x] + block_excl_scan(scan_thread_sum(in, n, i0), s_w, total);
+#pragma unroll
+  for (uint32_t k = 0; k < kScanItems; k++)
+    if (i0 + k < n) {
+      out[i0 + k] = o;
+      o += in[i0 + k];
+    }
+  if (blockIdx.x == 0 && threadIdx.x == 0) out[n] = part[gridDim.x];  // (the grand total)
+}
+__global__ __launch_bounds__(256) void gather_off_kernel(const uint64_t* off, const uint32_t* sent, uint32_t nsent,
+                                                         uint64_t* out) {
+  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < nsent; i += gridDim.x * 256) out[i] = off[sent[i]];
+}
+__global__ __launch_bounds__(256) void copy_rows_kernel(const uint4* src, const uint64_t* n_ptr, uint64_t cap,
+                                                        uint4* dst) {
+  const uint64_t n = min(*n_ptr, cap);
+  for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += gridDim.x * 256ull) dst[i] = src[i];
+}
+
+hipError_t launch_cells_sparse_count(hipStream_t s, const uint64_t* ck, const unsigned long long* n_ptr, uint64_t cap,
+                                     const uint32_t* sent, uint32_t nsent, const uint64_t* base, uint32_t* cnt) {
+  const uint32_t grid = (uint32_t)std::min<uint64_t>((cap + 255) / 256, 1024);
+  hipLaunchKernelGGL(cells_sparse_count_kernel, dim3(std::max<uint32_t>(grid, 1)), dim3(256), 0, s, ck, n_ptr, sent,
+                     nsent, base, cnt);
+  return hipGetLastError();
+}
+uint32_t scan_parts(uint64_t n) { return (uint32_t)((n + kScanBlock - 1) / kScanBlock); }
+hipError_t launch_scan_u32(hipStream_t s, const uint32_t* in, uint64_t n, uint64_t* out, uint64_t* part) {
+  const uint32_t nb = scan_parts(n);
+  if (nb) hipLaunchKernelGGL(scan_sums_kernel, dim3(nb), dim3(256), 0, s, in, n, part);
+  hipLaunchKernelGGL(scan_parts_kernel, dim3(1), dim3(256), 0, s, part, nb);
+  if (nb) hipLaunchKernelGGL(scan_apply_kernel, dim3(nb), dim3(256), 0, s, in, n, part, out);
+  return hipGetLastError();
+}
+hipError_t launch_gather_off(hipStream_t s, const uint64_t* off, const uint32_t* sent, uint32_t nsent, uint64_t* out) {
+  if (nsent)
+    hipLaunchKernelGGL(gather_off_kernel, dim3(std::min<uint32_t>((nsent + 255) / 256, 1024)), dim3(256), 0, s, off,
+                       sent, nsent, out);
+  return hipGetLastError();
+}
+hipError_t launch_copy_rows(hipStream_t s, const void* src, const uint64_t* n_ptr, uint64_t cap, void* dst) {
+  const uint32_t grid = (uint32_t)std::min<uint64_t>((cap + 255) / 256, 4096);
+  hipLaunchKernelGGL(copy_rows_kernel, dim3(std::max<uint32_t>(grid, 1)), dim3(256), 0, s,
+                     reinterpret_cast<const uint4*>(src), n_ptr, cap, reinterpret_cast<uint4*>(dst));
+  return hipGetLastError();
+}
+
 hipError_t launch_cells_count(hipStream_t s, const uint32_t* hist, uint64_t hist_cells, uint32_t T,
                               const uint64_t* base, const uint32_t* np, uint32_t E, uint32_t* cnt) {
   const uint32_t grid = (uint32_t)std::min<uint64_t>((E + 3) / 4, 8192);

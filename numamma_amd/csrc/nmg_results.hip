@@ -1,6 +1,7 @@
 // nmg_results.hip -- result getters (global and per-object counters, page
 // cells), the merge arrays of the multi-GPU chain (export / import, packed page
 // histogram, sparse cells, per-buffer counts).
+#include <chrono>
 #include "nmg_engine_impl.h"
 
 namespace nmg {
@@ -163,8 +164,17 @@ extern "C" int nmg_get_object_levels(nmg_engine* h, uint64_t* levels) {
 // once.
 int cells_prepare(nmg_engine* h) {
   if (h->cells_epoch == h->epoch) return NMG_OK;
+  const bool timing = getenv("NMG_CELLS_TIMING") != nullptr;  // (phase times on stderr)
+  auto tp = std::chrono::steady_clock::now();
+  auto lap = [&](const char* what) {
+    if (!timing) return;
+    const auto now = std::chrono::steady_clock::now();
+    fprintf(stderr, "cells_prepare: %-10s %.3f ms\n", what, std::chrono::duration<double, std::milli>(now - tp).count());
+    tp = now;
+  };
   int rc = nmg_synchronize(h);
   if (rc) return rc;
+  lap("sync");
   const uint32_t E = h->E;
   // sparse cells grouped per entry
   std::vector<std::vector<std::pair<uint64_t, uint32_t>>> sparse(h->sparse_entries.size());
@@ -184,6 +194,7 @@ int cells_prepare(nmg_engine* h) {
       }
     for (auto& l : sparse) std::sort(l.begin(), l.end());
   }
+  lap("sparse");
   std::vector<int64_t> sidx_of(E, -1);
   for (size_t s = 0; s < h->sparse_entries.size(); s++) sidx_of[h->sparse_entries[s]] = (int64_t)s;
   std::vector<uint32_t> cnt(E, 0);
@@ -213,6 +224,7 @@ int cells_prepare(nmg_engine* h) {
         (rc = hip(hipStreamSynchronize(h->stream), "count")))
       return rc;
   }
+  lap("count");
   std::vector<uint64_t> off(E);
   uint64_t n = 0;
   h->cells_sparse.clear();
@@ -227,6 +239,7 @@ int cells_prepare(nmg_engine* h) {
       n += cnt[e];
     }
   }
+  lap("prefix");
   if (dense && n) {
     if (n > h->cells_rows_cap) {
       (void)hipFree(h->d_cells_rows);
@@ -242,7 +255,10 @@ int cells_prepare(nmg_engine* h) {
         (rc = hip(hipStreamSynchronize(h->stream), "emit")))
       return rc;
   }
+  lap("emit");
   cleanup();
+  lap("free");
+  if (timing) fprintf(stderr, "cells_prepare: %llu rows\n", (unsigned long long)n);
   h->cells_n = (int64_t)n;
   h->cells_epoch = h->epoch;
   return NMG_OK;
@@ -251,8 +267,12 @@ int cells_prepare(nmg_engine* h) {
 // the prepared rows into rows[cells_n * 4]: dense rows D2H, sparse rows placed
 int cells_fill(nmg_engine* h, uint32_t* rows) {
   const bool dense = h->hist_cells && h->E;
+  const auto t0 = std::chrono::steady_clock::now();
   if (dense && h->cells_n)
     HIP_TRY(h, hipMemcpy(rows, h->d_cells_rows, (size_t)h->cells_n * 16, hipMemcpyDeviceToHost));
+  if (getenv("NMG_CELLS_TIMING"))
+    fprintf(stderr, "cells_fill: rows D2H %.3f ms\n",
+            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
   for (const auto& g : h->cells_sparse) {
     uint32_t* r = rows + g.off * 4;
     for (const auto& kv : g.cells) {
@@ -535,5 +555,274 @@ extern "C" int nmg_set_buffer_counts(nmg_engine* h, uint32_t nb_buffers, const u
   h->ov_samples.assign(nb_samples, nb_samples + nb_buffers);
   h->ov_found.assign(nb_found, nb_found + nb_buffers);
   h->ov_bytes.assign(buffer_bytes, buffer_bytes + nb_buffers);
+  return NMG_OK;
+}
+
+// ---- results snapshot (include/numamma_gpu.h: nmg_results_begin / end)
+
+namespace nmg {
+// device and pinned buffers of the snapshot, (re)allocated when the table or
+// the buffer list outgrows them
+static int snap_alloc(nmg_engine* h) {
+  auto& S = h->snap;
+  const uint64_t E = h->E, nb = h->descs.size(), nsent = h->sparse_entries.size();
+  const uint64_t rows = h->hist_cells * h->T + (h->d_sparse_keys ? h->sparse_cap : 0);
+  if (!S.stream) {
+    HIP_TRY(h, hipStreamCreateWithFlags(&S.stream, hipStreamNonBlocking));
+    HIP_TRY(h, hipEventCreateWithFlags(&S.ready, hipEventDisableTiming));
+    HIP_TRY(h, hipEventCreateWithFlags(&S.copied, hipEventDisableTiming));
+  }
+  if (E != S.E || !S.d_min) {
+    for (void* q : {(void*)S.d_base, (void*)S.d_off, (void*)S.d_np, (void*)S.d_cnt, (void*)S.d_min, (void*)S.d_objcw,
+                    (void*)S.d_part})
+      (void)hipFree(q);
+    S.d_base = S.d_off = S.d_part = S.d_min = S.d_objcw = nullptr;
+    S.d_np = S.d_cnt = nullptr;
+    HIP_TRY(h, hipMalloc(&S.d_base, (E + 1) * 8));
+    HIP_TRY(h, hipMalloc(&S.d_off, (E + 1) * 8));
+    HIP_TRY(h, hipMalloc(&S.d_part, (scan_parts(E) + 1) * 8));
+    HIP_TRY(h, hipMalloc(&S.d_np, (E + 1) * 4));
+    HIP_TRY(h, hipMalloc(&S.d_cnt, (E + 1) * 4));
+    HIP_TRY(h, hipMalloc(&S.d_min, (36 + E + 1) * 8));
+    HIP_TRY(h, hipMalloc(&S.d_objcw, (E + 1) * 32));
+    S.E = E;
+    S.meta_dirty = true;
+  }
+  if (!S.d_sum) {
+    HIP_TRY(h, hipMalloc(&S.d_sum, 2 * kGlobalSums * 8));
+    HIP_TRY(h, hipMalloc(&S.d_max, 36 * 8));
+    HIP_TRY(h, hipMalloc(&S.d_found, 8));
+    HIP_TRY(h, hipHostMalloc((void**)&S.h_sum, 2 * kGlobalSums * 8, 0));
+    HIP_TRY(h, hipHostMalloc((void**)&S.h_max, 36 * 8, 0));
+    HIP_TRY(h, hipHostMalloc((void**)&S.h_small, 4 * 8, 0));
+  }
+  if (nb > S.nb || !S.d_bufcnt) {
+    (void)hipFree(S.d_bufcnt);
+    S.d_bufcnt = nullptr;
+    HIP_TRY(h, hipMalloc(&S.d_bufcnt, (2 * nb + 1) * 4));
+    S.nb = nb;
+  }
+  if (nsent > S.nsent || !S.d_sent) {
+    (void)hipFree(S.d_sent);
+    (void)hipFree(S.d_soff);
+    S.d_sent = nullptr;
+    S.d_soff = nullptr;
+    HIP_TRY(h, hipMalloc(&S.d_sent, (nsent + 1) * 4));
+    HIP_TRY(h, hipMalloc(&S.d_soff, (nsent + 1) * 8));
+    S.nsent = nsent;
+    S.meta_dirty = true;
+  }
+  if (rows > S.rows_dev || !S.d_rows) {
+    (void)hipFree(S.d_rows);
+    S.d_rows = nullptr;
+    HIP_TRY(h, hipMalloc(&S.d_rows, (rows + 1) * 16));
+    S.rows_dev = rows;
+  }
+  if (h->d_sparse_keys && (S.sparse_cap != h->sparse_cap || !S.d_ck)) {
+    (void)hipFree(S.d_ck);
+    S.d_ck = nullptr;
+    HIP_TRY(h, hipMalloc(&S.d_ck, (2 * h->sparse_cap + 1) * 8));
+    S.sparse_cap = h->sparse_cap;
+  }
+  // pinned host copies (the rows grow on demand in nmg_results_end)
+  if (E > S.h_cap_E || !S.h_min) {
+    (void)hipHostFree(S.h_min);
+    (void)hipHostFree(S.h_objcw);
+    S.h_min = S.h_objcw = nullptr;
+    HIP_TRY(h, hipHostMalloc((void**)&S.h_min, (36 + E + 1) * 8, 0));
+    HIP_TRY(h, hipHostMalloc((void**)&S.h_objcw, (E + 1) * 32, 0));
+    S.h_cap_E = E;
+  }
+  if (nb > S.h_cap_nb || !S.h_bufcnt) {
+    (void)hipHostFree(S.h_bufcnt);
+    S.h_bufcnt = nullptr;
+    HIP_TRY(h, hipHostMalloc((void**)&S.h_bufcnt, (2 * nb + 1) * 4, 0));
+    S.h_cap_nb = nb;
+  }
+  if (nsent > S.h_cap_sent || !S.h_soff) {
+    (void)hipHostFree(S.h_soff);
+    S.h_soff = nullptr;
+    HIP_TRY(h, hipHostMalloc((void**)&S.h_soff, (nsent + 1) * 8, 0));
+    S.h_cap_sent = nsent;
+  }
+  return NMG_OK;
+}
+
+}  // namespace nmg
+
+void snap_free(nmg_engine* h) {
+  auto& S = h->snap;
+  if (S.stream) (void)hipStreamSynchronize(S.stream);
+  for (void* q : {(void*)S.d_base, (void*)S.d_off, (void*)S.d_part, (void*)S.d_soff, (void*)S.d_np, (void*)S.d_cnt,
+                  (void*)S.d_sent, (void*)S.d_sum, (void*)S.d_min, (void*)S.d_max, (void*)S.d_objcw, (void*)S.d_found,
+                  (void*)S.d_bufcnt, (void*)S.d_ck, S.d_rows})
+    (void)hipFree(q);
+  for (void* q : {(void*)S.h_sum, (void*)S.h_min, (void*)S.h_max, (void*)S.h_objcw, (void*)S.h_small, (void*)S.h_soff,
+                  (void*)S.h_bufcnt, (void*)S.h_rows})
+    (void)hipHostFree(q);
+  if (S.ready) (void)hipEventDestroy(S.ready);
+  if (S.copied) (void)hipEventDestroy(S.copied);
+  if (S.stream) (void)hipStreamDestroy(S.stream);
+  S = nmg_engine::ResSnap();
+}
+
+extern "C" int nmg_results_begin(nmg_engine* h) {
+  Range range("nmg_results_begin");
+  if (!h) return NMG_ERR_INVALID;
+  if (!h->have_table) return fail(h, NMG_ERR_STATE, "nmg_results_begin before nmg_set_objects");
+  if (h->multi || h->counts_override)
+    return fail(h, NMG_ERR_STATE, "nmg_results_begin: a multi-GPU handle or merged per-buffer counts");
+  if (h->streaming) return fail(h, NMG_ERR_STATE, "nmg_results_begin while streaming");
+  auto& S = h->snap;
+  HIP_TRY(h, hipSetDevice(h->device));
+  if (S.pending) {  // (a snapshot nobody ended: its copy must finish before the buffers are reused)
+    HIP_TRY(h, hipStreamSynchronize(S.stream));
+    S.pending = false;
+  }
+  int rc = route_settle(h);  // (the per-buffer matched counts of the last route analysis, enqueued)
+  if (rc) return rc;
+  rc = snap_alloc(h);
+  if (rc) return rc;
+  const uint64_t E = h->E, nb = h->descs.size(), nsent = h->sparse_entries.size();
+  hipStream_t st = h->stream;
+  if (S.meta_dirty) {  // (the table's cell layout: uploaded once per table)
+    std::vector<uint32_t> np(E);
+    for (uint64_t e = 0; e < E; e++) np[e] = h->hist_base[e] == kHistSparse ? 0u : (uint32_t)h->npages[e];
+    if (E) {
+      HIP_TRY(h, hipMemcpyAsync(S.d_base, h->hist_base.data(), E * 8, hipMemcpyHostToDevice, st));
+      HIP_TRY(h, hipMemcpyAsync(S.d_np, np.data(), E * 4, hipMemcpyHostToDevice, st));
+    }
+    if (nsent) HIP_TRY(h, hipMemcpyAsync(S.d_sent, h->sparse_entries.data(), nsent * 4, hipMemcpyHostToDevice, st));
+    HIP_TRY(h, hipStreamSynchronize(st));  // (pageable sources)
+    S.meta_dirty = false;
+  }
+  // the device snapshot, behind the enqueued analyses
+  HIP_TRY(h, hipMemcpyAsync(S.d_sum, h->d_sum64, 2 * kGlobalSums * 8, hipMemcpyDeviceToDevice, st));
+  HIP_TRY(h, hipMemcpyAsync(S.d_min, h->d_min64, (36 + E) * 8, hipMemcpyDeviceToDevice, st));
+  HIP_TRY(h, hipMemcpyAsync(S.d_max, h->d_max64, 36 * 8, hipMemcpyDeviceToDevice, st));
+  if (nb) {
+    HIP_TRY(h, hipMemcpyAsync(S.d_bufcnt, h->d_bufcnt, nb * 4, hipMemcpyDeviceToDevice, st));
+    HIP_TRY(h, hipMemcpyAsync(S.d_bufcnt + nb, h->d_bufcnt + h->bufcnt_stride, nb * 4, hipMemcpyDeviceToDevice, st));
+  }
+  if (h->d_found) HIP_TRY(h, hipMemcpyAsync(S.d_found, h->d_found, 8, hipMemcpyDeviceToDevice, st));
+  else HIP_TRY(h, hipMemsetAsync(S.d_found, 0, 8, st));
+  if (E) HIP_TRY(h, launch_objcw_aos(st, h->d_sum64 + 2 * kGlobalSums, E, S.d_objcw));
+  // page-cell rows: per-entry counts (dense, then the sparse table's), their
+  // exclusive scan, the dense rows; the sparse ones are placed by the host
+  unsigned long long* nsp = S.d_ck ? reinterpret_cast<unsigned long long*>(S.d_ck + 2 * S.sparse_cap) : nullptr;
+  if (E) {
+    if (h->hist_cells)
+      HIP_TRY(h, launch_cells_count(st, h->d_hist, h->hist_cells, h->T, S.d_base, S.d_np, (uint32_t)E, S.d_cnt));
+    else
+      HIP_TRY(h, hipMemsetAsync(S.d_cnt, 0, E * 4, st));
+    if (nsp) {
+      HIP_TRY(h, hipMemsetAsync(nsp, 0, 8, st));
+      HIP_TRY(h, launch_sparse_compact(st, h->d_sparse_keys, h->d_sparse_vals, h->sparse_cap, S.d_ck, nsp));
+      HIP_TRY(h, launch_cells_sparse_count(st, S.d_ck, nsp, h->sparse_cap, S.d_sent, (uint32_t)nsent, S.d_base,
+                                           S.d_cnt));
+    }
+    HIP_TRY(h, launch_scan_u32(st, S.d_cnt, E, S.d_off, S.d_part));
+    if (h->hist_cells)
+      HIP_TRY(h, launch_cells_emit(st, h->d_hist, h->hist_cells, h->T, S.d_base, S.d_np, (uint32_t)E, S.d_off,
+                                   (uint4*)S.d_rows));
+    HIP_TRY(h, launch_gather_off(st, S.d_off, S.d_sent, (uint32_t)nsent, S.d_soff));
+  } else {
+    HIP_TRY(h, hipMemsetAsync(S.d_off, 0, 8, st));
+  }
+  HIP_TRY(h, hipEventRecord(S.ready, st));
+  // the copy to pinned host memory, on the snapshot's own stream
+  hipStream_t cs = S.stream;
+  HIP_TRY(h, hipStreamWaitEvent(cs, S.ready, 0));
+  HIP_TRY(h, hipMemcpyAsync(S.h_sum, S.d_sum, 2 * kGlobalSums * 8, hipMemcpyDeviceToHost, cs));
+  HIP_TRY(h, hipMemcpyAsync(S.h_min, S.d_min, (36 + E) * 8, hipMemcpyDeviceToHost, cs));
+  HIP_TRY(h, hipMemcpyAsync(S.h_max, S.d_max, 36 * 8, hipMemcpyDeviceToHost, cs));
+  if (nb) HIP_TRY(h, hipMemcpyAsync(S.h_bufcnt, S.d_bufcnt, 2 * nb * 4, hipMemcpyDeviceToHost, cs));
+  HIP_TRY(h, hipMemcpyAsync(S.h_small, S.d_found, 8, hipMemcpyDeviceToHost, cs));
+  HIP_TRY(h, hipMemcpyAsync(S.h_small + 1, S.d_off + E, 8, hipMemcpyDeviceToHost, cs));
+  if (nsp) HIP_TRY(h, hipMemcpyAsync(S.h_small + 2, nsp, 8, hipMemcpyDeviceToHost, cs));
+  else S.h_small[2] = 0;
+  if (E) HIP_TRY(h, hipMemcpyAsync(S.h_objcw, S.d_objcw, E * 32, hipMemcpyDeviceToHost, cs));
+  if (nsent) HIP_TRY(h, hipMemcpyAsync(S.h_soff, S.d_soff, nsent * 8, hipMemcpyDeviceToHost, cs));
+  if (S.h_rows && S.rows_host) {  // (the rows' number is on the device: a kernel copies them)
+    void* dst = nullptr;
+    HIP_TRY(h, hipHostGetDevicePointer(&dst, S.h_rows, 0));
+    HIP_TRY(h, launch_copy_rows(cs, S.d_rows, S.d_off + E, S.rows_host, dst));
+  }
+  HIP_TRY(h, hipEventRecord(S.copied, cs));
+  S.pending = true;
+  h->snap_nb = nb;
+  return NMG_OK;
+}
+
+extern "C" int nmg_results_end(nmg_engine* h, nmg_results_view* out) {
+  Range range("nmg_results_end");
+  if (!h || !out) return NMG_ERR_INVALID;
+  auto& S = h->snap;
+  if (!S.pending) return fail(h, NMG_ERR_STATE, "nmg_results_end without nmg_results_begin");
+  HIP_TRY(h, hipSetDevice(h->device));
+  HIP_TRY(h, hipEventSynchronize(S.copied));
+  S.pending = false;
+  const uint64_t E = S.E, nb = h->snap_nb, nsent = h->sparse_entries.size();
+  const uint64_t nrows = S.h_small[1], nspc = S.h_small[2];
+  if (nrows > S.rows_host) {  // (the pinned rows outgrown: grown, and this time copied here)
+    (void)hipHostFree(S.h_rows);
+    S.h_rows = nullptr;
+    S.rows_host = 0;
+    const uint64_t cap = nrows + nrows / 4 + 1024;
+    HIP_TRY(h, hipHostMalloc((void**)&S.h_rows, cap * 16, 0));
+    S.rows_host = cap;
+    HIP_TRY(h, hipMemcpy(S.h_rows, S.d_rows, nrows * 16, hipMemcpyDeviceToHost));
+  }
+  if (nspc) {  // the sparse cells, each entry's in (thread, page) order at its rows
+    std::vector<uint64_t> kv(2 * nspc);
+    HIP_TRY(h, hipMemcpy(kv.data(), S.d_ck, 2 * nspc * 8, hipMemcpyDeviceToHost));
+    std::vector<std::vector<std::pair<uint64_t, uint32_t>>> per(nsent);
+    for (uint64_t i = 0; i < nspc; i++) {
+      const uint64_t k = kv[2 * i];
+      const uint32_t v = (uint32_t)kv[2 * i + 1];
+      const uint32_t s = sparse_key_idx(k);
+      if (k == ~0ull || !v || s >= nsent || h->hist_base[h->sparse_entries[s]] != kHistSparse) continue;
+      per[s].push_back({(uint64_t(sparse_key_thread(k)) << 32) | sparse_key_page(k), v});
+    }
+    for (uint64_t s = 0; s < nsent; s++) {
+      auto& l = per[s];
+      if (l.empty()) continue;
+      std::sort(l.begin(), l.end());
+      uint32_t* r = S.h_rows + S.h_soff[s] * 4;
+      for (const auto& c : l) {
+        r[0] = h->sparse_entries[s];
+        r[1] = (uint32_t)(c.first >> 32);
+        r[2] = (uint32_t)c.first;
+        r[3] = c.second;
+        r += 4;
+      }
+    }
+  }
+  memset(out, 0, sizeof(*out));
+  for (int a = 0; a < 2; a++) {  // (as engine_download)
+    nmg_mem_counters& c = out->global[a];
+    const uint64_t* s = S.h_sum + gsum_index(a, 0);
+    c.total_count = s[0];
+    c.total_weight = s[1];
+    c.na_miss_count = s[2];
+    for (int k = 0; k < 18; k++) {
+      c.b[k].count = s[3 + 2 * k];
+      c.b[k].sum_weight = s[4 + 2 * k];
+      c.b[k].min_weight = S.h_min[a * 18 + k];
+      c.b[k].max_weight = S.h_max[a * 18 + k];
+    }
+  }
+  uint64_t ns = 0;
+  for (uint64_t b = 0; b < nb; b++) ns += (uint64_t)(int64_t)(int32_t)S.h_bufcnt[b];
+  out->nb_samples = ns;
+  out->nb_found = S.h_small[0];
+  out->nb_buffers = (uint32_t)nb;
+  out->nb_entries = (uint32_t)E;
+  out->buffer_samples = S.h_bufcnt;
+  out->buffer_found = S.h_bufcnt + nb;
+  out->first_ordinal = S.h_min + 36;
+  out->count_weight = S.h_objcw;
+  out->nb_cells = (int64_t)nrows;
+  out->cells = S.h_rows;
   return NMG_OK;
 }

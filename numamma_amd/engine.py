@@ -257,6 +257,31 @@ class Engine:
         self._c(lib.nmg_get_page_cells(self.h, _ptr(rows, C.c_uint32), n))
         return rows
 
+    def results_begin(self):
+        """nmg_results_begin: the results so far snapshotted on the device and
+        copied to pinned host memory on a stream of their own; the engine may
+        be reset and analyse again at once."""
+        self._c(lib.nmg_results_begin(self.h))
+
+    def results_end(self):
+        """nmg_results_end: wait for the snapshot's copy; (global counters,
+        nb_samples, nb_found, buffer samples, buffer found, first ordinals,
+        count_weight [E, 2, 2], page-cell rows [n, 4]).  The arrays are views
+        of the engine's pinned memory, valid until the next results_begin."""
+        v = _lib.nmg_results_view()
+        self._c(lib.nmg_results_end(self.h, C.byref(v)))
+
+        def arr(ptr, n, shape=None):
+            if not n:
+                return np.zeros(shape or (0,), dtype=np.dtype(ptr._type_))
+            a = np.ctypeslib.as_array(ptr, shape=(n,))
+            return a.reshape(shape) if shape else a
+
+        g = np.stack([counters_to_numpy(v.global_[0]), counters_to_numpy(v.global_[1])])
+        nb, E, nc = v.nb_buffers, v.nb_entries, v.nb_cells
+        return (g, int(v.nb_samples), int(v.nb_found), arr(v.buffer_samples, nb), arr(v.buffer_found, nb),
+                arr(v.first_ordinal, E), arr(v.count_weight, 4 * E, (E, 2, 2)), arr(v.cells, 4 * nc, (nc, 4)))
+
     # ------------------------------------------------------------------
     def report(self, output_dir: str, stdout_path: Optional[str] = None, dump_single_items: int = 1,
                dump_flags: int = 0, maps_path: Optional[str] = None, maps_text: Optional[str] = None,

@@ -1,0 +1,64 @@
+"""nmg_results_begin / nmg_results_end: the results snapshot copied to host
+memory while the next analysis runs.  Its view must equal the synchronous
+getters (themselves bit-exact against the oracle in the parity tests) at the
+time of nmg_results_begin, even though the engine is reset and analyses
+another workload before nmg_results_end."""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from numamma_amd.replay import SynthConfig, generate  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+CASES = {
+    # attribute_kernel (small table)
+    "k700": dict(nb_samples=200_000, nb_intervals=700, seed=21),
+    # partition-first path, sparse cells of large objects and the [stack]
+    "k60k": dict(nb_samples=300_000, nb_intervals=60_000, size_max=4 << 20, seed=22),
+}
+
+
+def _sync_results(eng):
+    g, ns, nf = eng.global_counters()
+    bs, bf = eng.buffer_counts()
+    first, cw = eng.object_counters()
+    return g, ns, nf, bs, bf, first, cw, eng.page_cells()
+
+
+@pytest.mark.parametrize("case", sorted(CASES))
+def test_results_snapshot_equals_getters(case):
+    import torch
+    from numamma_amd.engine import Engine
+
+    rp = generate(SynthConfig(**CASES[case]))
+    rp2 = generate(SynthConfig(**dict(CASES[case], seed=CASES[case]["seed"] + 100)))
+    arena, offs, lens, ranks, acc = rp.packed()
+    arena2, offs2, lens2, ranks2, acc2 = rp2.packed()
+    d1 = torch.from_numpy(arena).cuda()
+    d2 = torch.from_numpy(arena2).cuda()
+    eng = Engine(nb_threads=rp.nb_threads)
+    eng.set_objects(rp.table)
+    for rep in range(3):  # (the second and third snapshots reuse the pinned buffers)
+        eng.reset()
+        eng.set_device_buffers(d1.data_ptr(), offs, lens, ranks, acc)
+        eng.analyze()
+        want = _sync_results(eng)
+        eng.results_begin()
+        # the next analysis at once: another workload on the same table
+        eng.reset()
+        eng.set_device_buffers(d2.data_ptr(), offs2, lens2, ranks2, acc2)
+        eng.analyze()
+        got = eng.results_end()
+        names = ("global", "nb_samples", "nb_found", "buffer_samples", "buffer_found", "first_ordinal",
+                 "count_weight", "cells")
+        for name, x, y in zip(names, want, got):
+            assert np.array_equal(np.asarray(x), np.asarray(y)), (rep, name)
+        assert want[7].shape[0] > 0
+    eng.synchronize()
+    eng.close()

@@ -17,6 +17,10 @@ everything nmg_report reads).  Modes (one JSON line each):
               nmg_register_host (like perf rings pinned at thread start; the
               registration is timed apart, register_s): one nmg_submit_buffers
               call copies nothing, the kernels read the arena over PCIe
+  zerocopy_pipe  zerocopy analyses back to back, each one's results taken with
+              nmg_results_begin / nmg_results_end: its copy to host memory
+              runs while the next analysis reads its records over PCIe;
+              e2e_s = the median interval between consecutive results
 
     python tools/e2e.py [c2|c4shard] [--threads 16] [--chunk-mb 64] [--batch 256]
 """
@@ -68,7 +72,7 @@ def main():
 
     zc_views, reg_s = None, None
     for mode in a.modes.split(","):
-        if mode == "zerocopy" and zc_views is None:
+        if mode in ("zerocopy", "zerocopy_pipe") and zc_views is None:
             offs, o = [], 0
             for _, _, b in lins:
                 offs.append(o)
@@ -86,6 +90,44 @@ def main():
             t = time.perf_counter()
             eng.register_host(arena)
             reg_s = time.perf_counter() - t
+        if mode == "zerocopy_pipe":
+            ends, cells = [], 0
+            eng.synchronize()
+            t_start = time.perf_counter()
+            calls = {}
+            for r in range(a.reps + 2):
+                tc = [time.perf_counter()]
+                eng.clear_buffers()
+                tc.append(time.perf_counter())
+                eng.reset()
+                tc.append(time.perf_counter())
+                eng.submit_arena(*zc_views)
+                tc.append(time.perf_counter())
+                eng.analyze()
+                tc.append(time.perf_counter())
+                if r:
+                    res = eng.results_end()
+                    cells = res[7].shape[0]
+                    ends.append(time.perf_counter())
+                tc.append(time.perf_counter())
+                eng.results_begin()
+                tc.append(time.perf_counter())
+                for k, name in enumerate(("clear", "reset", "submit", "analyze", "end", "begin")):
+                    calls.setdefault(name, []).append(tc[k + 1] - tc[k])
+            res = eng.results_end()
+            ends.append(time.perf_counter())
+            iv = np.diff(np.array(ends))
+            e2e = float(np.median(iv))
+            print(json.dumps({
+                "workload": a.workload, "mode": mode, "records": int(nsamples), "bytes": int(nbytes),
+                "copy_threads": 0, "analyses": a.reps + 2, "intervals_s": iv.tolist(), "e2e_s": e2e,
+                "e2e_samples_per_s": nsamples / e2e, "total_s": ends[-1] - t_start,
+                "total_samples_per_s": (a.reps + 2) * nsamples / (ends[-1] - t_start), "cells": int(cells),
+                "register_s": reg_s, "host_call_s": {k: float(np.median(v[1:])) for k, v in calls.items()},
+                "note": "steady state: each interval is one analysis (PCIe read of the records) with the previous "
+                        "analysis' results copied to pinned host memory meanwhile (counters, per-buffer counts, "
+                        "object counters, page-cell rows)"}), flush=True)
+            continue
         reps = []
         for r in range(a.reps + 1):
             eng.clear_buffers()
