@@ -340,6 +340,9 @@ extern "C" void nmg_destroy(nmg_engine* h) {
   (void)hipFree(h->d_dbg);
   (void)hipFree(h->d_smatch);
   if (h->h_stage) (void)hipHostFree(h->h_stage);
+  if (h->up_recorded) (void)hipEventSynchronize(h->up_ev);
+  if (h->up_ev) (void)hipEventDestroy(h->up_ev);
+  (void)hipHostFree(h->up_pin);
   snap_free(h);
   if (h->copy_stream) (void)hipStreamSynchronize(h->copy_stream);
   for (auto& sl : h->slots) {

@@ -221,6 +221,13 @@ struct nmg_engine {
   size_t descs_cap = 0;
   BufDesc* d_sdescs = nullptr;   // descriptors in stream-sorted schedule order
   uint32_t* d_ranges = nullptr;  // per-workgroup [begin, end) in d_order
+  size_t sdescs_cap = 0, ranges_cap = 0;
+  // pinned staging of an analysis' small uploads (descriptors, schedule,
+  // chunk pools): copied on the engine stream without a host wait
+  uint8_t* up_pin = nullptr;
+  size_t up_cap = 0, up_off = 0;
+  hipEvent_t up_ev = nullptr;
+  bool up_recorded = false;
   uint32_t sched_grid = 0;       // grid the current schedule was built for
   bool descs_dirty = false;
   bool multi_staged = false;  // the workers' arenas hold the current buffers (multi_analyze)
@@ -371,6 +378,10 @@ void free_counters(nmg_engine* h);
 void free_lookup(nmg_engine* h);
 void free_route_table(nmg_engine* h);
 void snap_free(nmg_engine* h);  // the results snapshot's buffers and stream
+// an H2D copy of n bytes from host memory the caller may reuse at once:
+// through the pinned staging, on the engine stream, no host wait
+int stage_h2d(nmg_engine* h, void* d_dst, const void* src, size_t n);
+void stage_reset(nmg_engine* h);  // (an analysis' first upload: the staging from its start again)
 void free_route_pool(nmg_engine* h);
 LookupSet take_lookup(nmg_engine* h);
 void put_lookup(nmg_engine* h, const LookupSet& l);

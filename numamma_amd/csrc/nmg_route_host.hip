@@ -105,7 +105,8 @@ int route_prepare(nmg_engine* h, uint32_t grid, const std::vector<uint32_t>& ran
   std::vector<uint32_t> c0;
   const int rc = route_pool(h, h->descs, grid, ranges.data(), c0);
   if (rc) return rc;
-  HIP_TRY(h, hipMemcpy(h->d_chunk0, c0.data(), (grid + 1) * 4, hipMemcpyHostToDevice));
+  const int rc2 = stage_h2d(h, h->d_chunk0, c0.data(), (grid + 1) * 4);
+  if (rc2) return rc2;
   h->route_sched_key = h->nparts | ((h->flags & kDbgTinyPool) ? 0x80000000u : 0u);
   return NMG_OK;
 }

@@ -495,6 +495,38 @@ extern "C" int nmg_clear_buffers(nmg_engine* h) {
   return NMG_OK;
 }
 
+int stage_h2d(nmg_engine* h, void* d_dst, const void* src, size_t n) {
+  if (!n) return NMG_OK;
+  const size_t need = (n + 255) & ~size_t(255);
+  if (h->up_off + need > h->up_cap) {  // full: every copy from it done first, then from its start
+    if (h->up_recorded) HIP_TRY(h, hipEventSynchronize(h->up_ev));
+    h->up_off = 0;
+    if (need > h->up_cap) {
+      (void)hipHostFree(h->up_pin);
+      h->up_pin = nullptr;
+      h->up_cap = 0;
+      const size_t cap = std::max<size_t>(need * 2, 4u << 20);
+      HIP_TRY(h, hipHostMalloc((void**)&h->up_pin, cap, 0));
+      h->up_cap = cap;
+    }
+  }
+  if (!h->up_ev) HIP_TRY(h, hipEventCreateWithFlags(&h->up_ev, hipEventDisableTiming));
+  uint8_t* p = h->up_pin + h->up_off;
+  memcpy(p, src, n);
+  HIP_TRY(h, hipMemcpyAsync(d_dst, p, n, hipMemcpyHostToDevice, h->stream));
+  HIP_TRY(h, hipEventRecord(h->up_ev, h->stream));
+  h->up_recorded = true;
+  h->up_off += need;
+  return NMG_OK;
+}
+
+void stage_reset(nmg_engine* h) {
+  // the previous analysis' copies ran before its kernels, so this wait is
+  // normally already satisfied
+  if (h->up_recorded) (void)hipEventSynchronize(h->up_ev);
+  h->up_off = 0;
+}
+
 int upload_buffers(nmg_engine* h) {
   Range range("nmg_stage_h2d");
   if (!h->external && h->staged_dirty) {
@@ -527,9 +559,10 @@ int upload_buffers(nmg_engine* h) {
     }
     h->bufcnt_stride = n;
     if (n) {
-      HIP_TRY(h, hipMemcpyAsync(h->d_descs, h->descs.data(), n * sizeof(BufDesc), hipMemcpyHostToDevice, h->stream));
+      stage_reset(h);
+      const int rc = stage_h2d(h, h->d_descs, h->descs.data(), n * sizeof(BufDesc));
+      if (rc) return rc;
       HIP_TRY(h, hipMemsetAsync(h->d_bufcnt, 0, n * 2 * 4, h->stream));
-      HIP_TRY(h, hipStreamSynchronize(h->stream));  // descs come from pageable memory
     }
     h->descs_dirty = false;
   }
@@ -575,14 +608,20 @@ int build_schedule(nmg_engine* h, uint32_t grid, bool by_stream) {
   std::vector<uint32_t> ranges(grid + 1, 0);
   std::vector<BufDesc> sorted(nb);
   make_schedule(h->descs, grid, 0, sorted.data(), ranges.data(), by_stream);
-  (void)hipFree(h->d_sdescs);
-  (void)hipFree(h->d_ranges);
-  h->d_sdescs = nullptr;
-  h->d_ranges = nullptr;
-  HIP_TRY(h, hipMalloc(&h->d_sdescs, std::max<size_t>(nb, 1) * sizeof(BufDesc)));
-  HIP_TRY(h, hipMalloc(&h->d_ranges, (grid + 1) * 4));
-  if (nb) HIP_TRY(h, hipMemcpy(h->d_sdescs, sorted.data(), nb * sizeof(BufDesc), hipMemcpyHostToDevice));
-  HIP_TRY(h, hipMemcpy(h->d_ranges, ranges.data(), (grid + 1) * 4, hipMemcpyHostToDevice));
+  if (nb > h->sdescs_cap || grid + 1 > h->ranges_cap || !h->d_sdescs) {  // (grown only: a free waits for the device)
+    HIP_TRY(h, hipStreamSynchronize(h->stream));
+    (void)hipFree(h->d_sdescs);
+    (void)hipFree(h->d_ranges);
+    h->d_sdescs = nullptr;
+    h->d_ranges = nullptr;
+    h->sdescs_cap = std::max<size_t>(nb, 1);
+    h->ranges_cap = grid + 1;
+    HIP_TRY(h, hipMalloc(&h->d_sdescs, h->sdescs_cap * sizeof(BufDesc)));
+    HIP_TRY(h, hipMalloc(&h->d_ranges, h->ranges_cap * 4));
+  }
+  int rc = stage_h2d(h, h->d_sdescs, sorted.data(), nb * sizeof(BufDesc));
+  if (!rc) rc = stage_h2d(h, h->d_ranges, ranges.data(), (grid + 1) * 4);
+  if (rc) return rc;
   h->sched_grid = grid;
   h->sched_route = !by_stream;
   if (!by_stream) return route_prepare(h, grid, ranges);
