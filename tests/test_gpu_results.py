@@ -62,3 +62,34 @@ def test_results_snapshot_equals_getters(case):
         assert want[7].shape[0] > 0
     eng.synchronize()
     eng.close()
+
+
+def test_results_snapshot_errors_and_restart():
+    """end without begin is a state error; a begin nobody ended is waited for
+    by the next begin; a snapshot after set_buffer_counts (merged counts) is
+    refused."""
+    import torch
+    from numamma_amd._lib import NmgError
+    from numamma_amd.engine import Engine
+
+    rp = generate(SynthConfig(**CASES["k700"]))
+    arena, offs, lens, ranks, acc = rp.packed()
+    d = torch.from_numpy(arena).cuda()
+    eng = Engine(nb_threads=rp.nb_threads)
+    eng.set_objects(rp.table)
+    eng.set_device_buffers(d.data_ptr(), offs, lens, ranks, acc)
+    with pytest.raises(NmgError):
+        eng.results_end()
+    eng.analyze()
+    eng.results_begin()
+    eng.results_begin()  # (the first one's copy waited for, its view dropped)
+    got = eng.results_end()
+    want = _sync_results(eng)
+    assert all(np.array_equal(np.asarray(x), np.asarray(y)) for x, y in zip(want, got))
+    with pytest.raises(NmgError):
+        eng.results_end()
+    s, f = eng.buffer_counts()
+    eng.set_buffer_counts(s, f, np.asarray(eng.buffer_bytes, dtype=np.uint64))
+    with pytest.raises(NmgError):
+        eng.results_begin()
+    eng.close()
