@@ -1004,9 +1004,17 @@ __global__ __launch_bounds__(kWG) void count_kernel(CountParams cp) {
   for (uint32_t q = tid; q < P; q += kWG) s_cnt[q] = 0;
   __syncthreads();
   const uint32_t c0 = r.chunk0[w], n = r.used[w];
-  for (uint32_t c = c0 + tid; c < c0 + n; c += kWG) {
-    const uint32_t m = r.cmeta[c];
-    if (m >> 24) atomicAdd(&s_cnt[m & 0xffffffu], 1u);  // (fill 0: a chunk route2 opened and nothing reached)
+  constexpr uint32_t kU = 8;  // chunk tags in flight per thread
+  for (uint32_t b = 0; b < n; b += kU * kWG) {
+    uint32_t m[kU];
+#pragma unroll
+    for (uint32_t u = 0; u < kU; u++) {
+      const uint32_t i = b + u * kWG + tid;
+      m[u] = i < n ? r.cmeta[c0 + i] : 0u;
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < kU; u++)
+      if (m[u] >> 24) atomicAdd(&s_cnt[m[u] & 0xffffffu], 1u);  // (fill 0: a chunk route2 opened and nothing reached)
   }
   __syncthreads();
   uint32_t* out = const_cast<uint32_t*>(r.pcnt) + uint64_t(w) * P;
@@ -1111,17 +1119,26 @@ __global__ __launch_bounds__(kWG) void plan_kernel(PlanParams r) {
 }
 
 __global__ __launch_bounds__(kWG) void scatter_kernel(ScatterParams r) {
-  __shared__ uint32_t s_cnt[kMaxParts + 1];
+  __shared__ uint32_t s_cnt[kMaxParts + 1];  // this workgroup's next list slot per partition
   const uint32_t tid = threadIdx.x, w = blockIdx.x, P = r.nparts;
-  for (uint32_t q = tid; q < P; q += kWG) s_cnt[q] = 0;
+  const uint32_t* off = r.pcnt + uint64_t(w) * P;
+  for (uint32_t q = tid; q < P; q += kWG) s_cnt[q] = r.pbase[q] + off[q];
   __syncthreads();
   const uint32_t c0 = r.chunk0[w], n = r.used[w];
-  const uint32_t* off = r.pcnt + uint64_t(w) * P;
-  for (uint32_t c = c0 + tid; c < c0 + n; c += kWG) {
-    const uint32_t m = r.cmeta[c], q = m & 0xffffffu;
-    if (!(m >> 24)) continue;
-    const uint32_t k = atomicAdd(&s_cnt[q], 1u);
-    r.clist[r.pbase[q] + off[q] + k] = c | ((m >> 24) << kChunkIdBits);  // chunk id | fill
+  constexpr uint32_t kU = 8;  // chunk tags in flight per thread
+  for (uint32_t b = 0; b < n; b += kU * kWG) {
+    uint32_t m[kU];
+#pragma unroll
+    for (uint32_t u = 0; u < kU; u++) {
+      const uint32_t i = b + u * kWG + tid;
+      m[u] = i < n ? r.cmeta[c0 + i] : 0u;
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < kU; u++) {
+      if (!(m[u] >> 24)) continue;
+      const uint32_t k = atomicAdd(&s_cnt[m[u] & 0xffffffu], 1u);
+      r.clist[k] = (c0 + b + u * kWG + tid) | ((m[u] >> 24) << kChunkIdBits);  // chunk id | fill
+    }
   }
 }
 
@@ -1177,7 +1194,7 @@ __global__ __launch_bounds__(kLWG, 1) void local_kernel(LocalParams lp) {
   __shared__ unsigned long long s_first[kPartEntries];
   __shared__ uint32_t s_pg[kPartCells / 2];
   __shared__ uint32_t s_clist[kItemChunks];  // the item's chunk list entries
-  __shared__ uint32_t s_item, s_cnext, s_nfound, s_big;
+  __shared__ uint32_t s_item, s_cnext, s_nfound, s_big, s_took;
 
   Params& p = lp.p;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -1197,8 +1214,13 @@ __global__ __launch_bounds__(kLWG, 1) void local_kernel(LocalParams lp) {
     s_first[i] = ~0ull;
   }
   for (uint32_t i = tid; i < kPartCells / 2; i += kLWG) s_pg[i] = 0;
+  // the next item is taken by the first wave done with the current one's
+  // chunks (its dequeue latency hidden behind the others' chunks and the flush)
+  if (tid == 0) {
+    s_item = atomicAdd(lp.ctl + 1, 1u);
+    s_took = 0;
+  }
   while (true) {
-    if (tid == 0) s_item = atomicAdd(lp.ctl + 1, 1u);
     lds_sync();
     const uint32_t it = __builtin_amdgcn_readfirstlane(s_item);
     rt_stamp<TIMING>(rt, 6);
@@ -1209,27 +1231,42 @@ __global__ __launch_bounds__(kLWG, 1) void local_kernel(LocalParams lp) {
     const PartInfo pi = lp.parts[q];
     const uint32_t dshift = __builtin_amdgcn_readfirstlane(pi.dshift);
     {
-      const uint32_t nk = pi.nk;
-      const uint64_t* gk = lp.pe_keys + uint64_t(q) * kPartSlots;
-      const uint4* gn = lp.pe_pnode + uint64_t(q) * kPartSlots;
-      const uint2* gi = lp.pe_info + uint64_t(q) * kPartSlots;
-      for (uint32_t i = tid; i < nk; i += kLWG) {
-        s_keys[i] = gk[i];
-        s_pn[i] = gn[i];
-        s_info[i] = gi[i];
+      // the partition's tables and the item's chunk list: at most one element
+      // of each per thread, every load in flight before the first LDS store
+      static_assert(kPartKeys <= kLWG && kPartDir == kLWG && kOldLds <= kLWG && kItemChunks <= kLWG,
+                    "one table element per thread");
+      const uint32_t nk = pi.nk, nold = min(pi.ne - nk, kOldLds), ncl = item.z - item.y;
+      uint64_t key = 0;
+      uint4 pn = make_uint4(0, 0, 0, 0), od = pn;
+      uint2 inf = make_uint2(0, 0);
+      uint32_t oi = 0, cl = 0;
+      if (tid < nk) {
+        key = lp.pe_keys[uint64_t(q) * kPartSlots + tid];
+        pn = lp.pe_pnode[uint64_t(q) * kPartSlots + tid];
+        inf = lp.pe_info[uint64_t(q) * kPartSlots + tid];
       }
-      const uint4* gd = lp.pe_dir + uint64_t(q) * kPartDir;
-      for (uint32_t i = tid; i < kPartDir; i += kLWG) s_dir[i] = gd[i];
-      const uint32_t nold = min(pi.ne - nk, kOldLds);
-      const uint4* go = lp.pe_old + uint64_t(q) * kOldLds;
-      const uint32_t* goi = lp.pe_oinf + uint64_t(q) * kOldLds;
-      for (uint32_t i = tid; i < nold; i += kLWG) {
-        s_old[i] = go[i];
-        s_oinf[i] = goi[i];
+      const uint4 dd = lp.pe_dir[uint64_t(q) * kPartDir + tid];
+      if (tid < nold) {
+        od = lp.pe_old[uint64_t(q) * kOldLds + tid];
+        oi = lp.pe_oinf[uint64_t(q) * kOldLds + tid];
       }
-      for (uint32_t i = tid; i < item.z - item.y; i += kLWG) s_clist[i] = lp.clist[item.y + i];
+      if (tid < ncl) cl = lp.clist[item.y + tid];
+      if (tid < nk) {
+        s_keys[tid] = key;
+        s_pn[tid] = pn;
+        s_info[tid] = inf;
+      }
+      s_dir[tid] = dd;
+      if (tid < nold) {
+        s_old[tid] = od;
+        s_oinf[tid] = oi;
+      }
+      if (tid < ncl) s_clist[tid] = cl;
     }
-    if (tid == 0) s_cnext = 0;
+    if (tid == 0) {
+      s_cnext = 0;
+      s_took = 0;
+    }
     const uint32_t ncell = (pages && pi.pages_lds) ? T * pi.span : 0u;
     const bool excl = item.w != 0 && !(p.flags & kDbgLocalAtomics);  // no other workgroup writes this partition's
                                                                      // counters
@@ -1558,6 +1595,8 @@ __global__ __launch_bounds__(kLWG, 1) void local_kernel(LocalParams lp) {
 #pragma unroll
       for (int j = 0; j < kLC; j++) chunk_load(lb + j, B[j]);
     }
+    // (every wave read this item's index before the setup's barrier)
+    if (lane == 0 && atomicExch(&s_took, 1u) == 0) s_item = atomicAdd(lp.ctl + 1, 1u);
     lds_sync();
     rt_stamp<TIMING>(rt, 9);  // (waiting for the item's slowest wave)
     // an item alone on its partition whose counters nothing else wrote since
