@@ -1195,6 +1195,7 @@ __global__ __launch_bounds__(kLWG, 1) void local_kernel(LocalParams lp) {
   __shared__ uint32_t s_pg[kPartCells / 2];
   __shared__ uint32_t s_clist[kItemChunks];  // the item's chunk list entries
   __shared__ uint32_t s_item, s_cnext, s_nfound, s_big, s_took;
+  __shared__ uint4 s_nx[4];  // the next item's work item and PartInfo (take_next)
 
   Params& p = lp.p;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -1214,21 +1215,40 @@ __global__ __launch_bounds__(kLWG, 1) void local_kernel(LocalParams lp) {
     s_first[i] = ~0ull;
   }
   for (uint32_t i = tid; i < kPartCells / 2; i += kLWG) s_pg[i] = 0;
-  // the next item is taken by the first wave done with the current one's
-  // chunks (its dequeue latency hidden behind the others' chunks and the flush)
-  if (tid == 0) {
-    s_item = atomicAdd(lp.ctl + 1, 1u);
-    s_took = 0;
-  }
+  // the next item -- its index, work item and partition descriptor, into
+  // LDS -- is taken by the first wave done with the current one's chunks:
+  // those three dependent round trips hide behind the other waves' chunks and
+  // the flush (one whole wave calls this)
+  static_assert(sizeof(PartInfo) == 48, "PartInfo: three uint4");
+  auto take_next = [&]() {
+    uint32_t idx = 0;
+    if (lane == 0) idx = atomicAdd(lp.ctl + 1, 1u);
+    idx = __builtin_amdgcn_readfirstlane(idx);
+    if (lane == 0) s_item = idx;
+    if (idx < nitems) {
+      const uint4 nx = lp.items[idx];
+      const uint32_t nq = __builtin_amdgcn_readfirstlane(nx.x);
+      if (lane == 0) s_nx[0] = nx;
+      if (lane < 3) s_nx[1 + lane] = reinterpret_cast<const uint4*>(lp.parts + nq)[lane];
+    }
+  };
+  if (tid < 64) take_next();
+  if (tid == 0) s_took = 0;
   while (true) {
     lds_sync();
     const uint32_t it = __builtin_amdgcn_readfirstlane(s_item);
     rt_stamp<TIMING>(rt, 6);
     if (it >= nitems) break;
     nit++;
-    const uint4 item = lp.items[it];
+    const uint4 item = s_nx[0];
     const uint32_t q = __builtin_amdgcn_readfirstlane(item.x);
-    const PartInfo pi = lp.parts[q];
+    PartInfo pi;
+    {
+      uint4* pw = reinterpret_cast<uint4*>(&pi);
+      pw[0] = s_nx[1];
+      pw[1] = s_nx[2];
+      pw[2] = s_nx[3];
+    }
     const uint32_t dshift = __builtin_amdgcn_readfirstlane(pi.dshift);
     {
       // the partition's tables and the item's chunk list: at most one element
@@ -1595,8 +1615,10 @@ __global__ __launch_bounds__(kLWG, 1) void local_kernel(LocalParams lp) {
 #pragma unroll
       for (int j = 0; j < kLC; j++) chunk_load(lb + j, B[j]);
     }
-    // (every wave read this item's index before the setup's barrier)
-    if (lane == 0 && atomicExch(&s_took, 1u) == 0) s_item = atomicAdd(lp.ctl + 1, 1u);
+    // (every wave read this item's index and descriptors before the setup's barrier)
+    uint32_t won = 0;
+    if (lane == 0) won = atomicExch(&s_took, 1u) == 0 ? 1u : 0u;
+    if (__builtin_amdgcn_readfirstlane(won)) take_next();
     lds_sync();
     rt_stamp<TIMING>(rt, 9);  // (waiting for the item's slowest wave)
     // an item alone on its partition whose counters nothing else wrote since
