@@ -343,6 +343,9 @@ extern "C" void nmg_destroy(nmg_engine* h) {
   if (h->up_recorded) (void)hipEventSynchronize(h->up_ev);
   if (h->up_ev) (void)hipEventDestroy(h->up_ev);
   (void)hipHostFree(h->up_pin);
+  for (void* q : {(void*)h->cprep.d_base, (void*)h->cprep.d_off, (void*)h->cprep.d_part, (void*)h->cprep.d_np,
+                  (void*)h->cprep.d_cnt, (void*)h->cprep.d_sent, (void*)h->cprep.d_soff})
+    (void)hipFree(q);
   snap_free(h);
   if (h->copy_stream) (void)hipStreamSynchronize(h->copy_stream);
   for (auto& sl : h->slots) {

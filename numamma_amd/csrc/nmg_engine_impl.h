@@ -163,6 +163,13 @@ struct nmg_engine {
     uint64_t h_cap_E = 0, h_cap_nb = 0, h_cap_sent = 0;
   } snap;
   uint64_t snap_nb = 0;  // buffers of the snapshot in flight
+  // the synchronous page-cell getters' device buffers (cells_prepare), kept across calls
+  struct CellsPrep {
+    uint64_t E = 0, nsent = 0;
+    bool meta_dirty = true;
+    uint64_t *d_base = nullptr, *d_off = nullptr, *d_part = nullptr, *d_soff = nullptr;
+    uint32_t *d_np = nullptr, *d_cnt = nullptr, *d_sent = nullptr;
+  } cprep;
   uint32_t K = 0, E = 0;
   uint64_t* d_keys = nullptr;
   DevEntry* d_nodes = nullptr;

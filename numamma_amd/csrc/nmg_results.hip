@@ -155,13 +155,15 @@ extern "C" int nmg_get_object_levels(nmg_engine* h, uint64_t* levels) {
 
 
 // Every non-zero (entry, thread, page) cell, entries in id order, each
-// entry's cells in (thread, page) order.  Dense cells are counted and
-// compacted into rows on the device (cells_count / cells_emit); the rows stay
-// there (d_cells_rows) until copied out, so only they cross PCIe, once.  The
-// sparse table's cells (entries past the dense budget, e.g. [stack]) are
-// grouped on the host and placed at their entries' offsets.  Cached per
-// results epoch: nmg_count_page_cells then nmg_get_page_cells does the work
-// once.
+// entry's cells in (thread, page) order.  On the device, in buffers kept
+// across calls (the table's cell layout uploaded once per table): dense cells
+// counted per entry (cells_count), the sparse table's cells (entries past the
+// dense budget, e.g. [stack]) counted per entry from its compacted slots, an
+// exclusive scan into row offsets, the dense rows emitted (cells_emit).  The
+// rows stay on the device (d_cells_rows) until copied out, so only they cross
+// PCIe, once; the sparse rows are sorted on the host and placed at their
+// entries' offsets.  Cached per results epoch: nmg_count_page_cells then
+// nmg_get_page_cells does the work once.
 int cells_prepare(nmg_engine* h) {
   if (h->cells_epoch == h->epoch) return NMG_OK;
   const bool timing = getenv("NMG_CELLS_TIMING") != nullptr;  // (phase times on stderr)
@@ -175,89 +177,88 @@ int cells_prepare(nmg_engine* h) {
   int rc = nmg_synchronize(h);
   if (rc) return rc;
   lap("sync");
-  const uint32_t E = h->E;
-  // sparse cells grouped per entry
-  std::vector<std::vector<std::pair<uint64_t, uint32_t>>> sparse(h->sparse_entries.size());
-  bool any_sparse = false;
-  rc = sparse_nonempty(h, &any_sparse);
-  if (rc) return rc;
-  if (any_sparse) {
-    std::vector<uint64_t> k;
-    std::vector<uint32_t> v;
-    rc = sparse_download(h, k, v);
-    if (rc) return rc;
-    for (size_t i = 0; i < k.size(); i++)
-      if (k[i] != ~0ull && v[i]) {
-        uint32_t s = sparse_key_idx(k[i]);
-        // order within an entry: (thread, page)
-        sparse[s].push_back({(uint64_t(sparse_key_thread(k[i])) << 32) | sparse_key_page(k[i]), v[i]});
-      }
-    for (auto& l : sparse) std::sort(l.begin(), l.end());
+  const uint64_t E = h->E, nsent = h->sparse_entries.size();
+  auto& C = h->cprep;
+  if (E != C.E || !C.d_off || nsent > C.nsent) {  // (grown only with the table)
+    for (void* q : {(void*)C.d_base, (void*)C.d_off, (void*)C.d_part, (void*)C.d_np, (void*)C.d_cnt,
+                    (void*)C.d_sent, (void*)C.d_soff})
+      (void)hipFree(q);
+    C = nmg_engine::CellsPrep();
+    HIP_TRY(h, hipMalloc(&C.d_base, (E + 1) * 8));
+    HIP_TRY(h, hipMalloc(&C.d_off, (E + 1) * 8));
+    HIP_TRY(h, hipMalloc(&C.d_part, (scan_parts(E) + 1) * 8));
+    HIP_TRY(h, hipMalloc(&C.d_np, (E + 1) * 4));
+    HIP_TRY(h, hipMalloc(&C.d_cnt, (E + 1) * 4));
+    HIP_TRY(h, hipMalloc(&C.d_sent, (nsent + 1) * 4));
+    HIP_TRY(h, hipMalloc(&C.d_soff, (nsent + 1) * 8));
+    C.E = E;
+    C.nsent = nsent;
+    C.meta_dirty = true;
   }
-  lap("sparse");
-  std::vector<int64_t> sidx_of(E, -1);
-  for (size_t s = 0; s < h->sparse_entries.size(); s++) sidx_of[h->sparse_entries[s]] = (int64_t)s;
-  std::vector<uint32_t> cnt(E, 0);
-  uint64_t *d_base = nullptr, *d_off = nullptr;
-  uint32_t *d_np = nullptr, *d_cnt = nullptr;
-  auto cleanup = [&]() {
-    (void)hipFree(d_base);
-    (void)hipFree(d_off);
-    (void)hipFree(d_np);
-    (void)hipFree(d_cnt);
-  };
-  auto hip = [&](hipError_t e, const char* what) {
-    if (e == hipSuccess) return NMG_OK;
-    cleanup();
-    return fail(h, NMG_ERR_HIP, std::string("page cells: ") + what + ": " + hipGetErrorString(e));
-  };
-  const bool dense = h->hist_cells && E;
-  if (dense) {
+  if (C.meta_dirty) {  // (the table's cell layout)
     std::vector<uint32_t> np(E);
-    for (uint32_t e = 0; e < E; e++) np[e] = h->hist_base[e] == kHistSparse ? 0u : (uint32_t)h->npages[e];
-    if ((rc = hip(hipMalloc(&d_base, (size_t)E * 8), "alloc")) || (rc = hip(hipMalloc(&d_np, (size_t)E * 4), "alloc")) ||
-        (rc = hip(hipMalloc(&d_cnt, (size_t)E * 4), "alloc")) ||
-        (rc = hip(hipMemcpyAsync(d_base, h->hist_base.data(), (size_t)E * 8, hipMemcpyHostToDevice, h->stream), "upload")) ||
-        (rc = hip(hipMemcpyAsync(d_np, np.data(), (size_t)E * 4, hipMemcpyHostToDevice, h->stream), "upload")) ||
-        (rc = hip(launch_cells_count(h->stream, h->d_hist, h->hist_cells, h->T, d_base, d_np, E, d_cnt), "count")) ||
-        (rc = hip(hipMemcpyAsync(cnt.data(), d_cnt, (size_t)E * 4, hipMemcpyDeviceToHost, h->stream), "counts")) ||
-        (rc = hip(hipStreamSynchronize(h->stream), "count")))
-      return rc;
+    for (uint64_t e = 0; e < E; e++) np[e] = h->hist_base[e] == kHistSparse ? 0u : (uint32_t)h->npages[e];
+    if (E) {
+      HIP_TRY(h, hipMemcpy(C.d_base, h->hist_base.data(), E * 8, hipMemcpyHostToDevice));
+      HIP_TRY(h, hipMemcpy(C.d_np, np.data(), E * 4, hipMemcpyHostToDevice));
+    }
+    if (nsent) HIP_TRY(h, hipMemcpy(C.d_sent, h->sparse_entries.data(), nsent * 4, hipMemcpyHostToDevice));
+    C.meta_dirty = false;
   }
-  lap("count");
-  std::vector<uint64_t> off(E);
+  lap("meta");
+  // sparse cells: compacted on the device (sparse_download, which leaves
+  // them in d_sparse_ck) and grouped per entry here
+  std::vector<uint64_t> k;
+  std::vector<uint32_t> v;
+  rc = sparse_download(h, k, v);
+  if (rc) return rc;
+  std::vector<std::vector<std::pair<uint64_t, uint32_t>>> sparse(nsent);
+  for (size_t i = 0; i < k.size(); i++) {
+    const uint32_t s = sparse_key_idx(k[i]);
+    if (k[i] == ~0ull || !v[i] || s >= nsent || h->hist_base[h->sparse_entries[s]] != kHistSparse) continue;
+    // order within an entry: (thread, page)
+    sparse[s].push_back({(uint64_t(sparse_key_thread(k[i])) << 32) | sparse_key_page(k[i]), v[i]});
+  }
+  for (auto& l : sparse) std::sort(l.begin(), l.end());
+  lap("sparse");
+  const bool dense = h->hist_cells && E;
   uint64_t n = 0;
+  std::vector<uint64_t> soff(nsent, 0);
+  if (E) {
+    hipStream_t st = h->stream;
+    if (dense)
+      HIP_TRY(h, launch_cells_count(st, h->d_hist, h->hist_cells, h->T, C.d_base, C.d_np, (uint32_t)E, C.d_cnt));
+    else
+      HIP_TRY(h, hipMemsetAsync(C.d_cnt, 0, E * 4, st));
+    if (!k.empty())
+      HIP_TRY(h, launch_cells_sparse_count(st, h->d_sparse_ck,
+                                           reinterpret_cast<const unsigned long long*>(h->d_sparse_ck + 2 * h->sparse_cap),
+                                           h->sparse_cap, C.d_sent, (uint32_t)nsent, C.d_base, C.d_cnt));
+    HIP_TRY(h, launch_scan_u32(st, C.d_cnt, E, C.d_off, C.d_part));
+    HIP_TRY(h, hipMemcpyAsync(&n, C.d_off + E, 8, hipMemcpyDeviceToHost, st));
+    if (!k.empty()) {
+      HIP_TRY(h, launch_gather_off(st, C.d_off, C.d_sent, (uint32_t)nsent, C.d_soff));
+      HIP_TRY(h, hipMemcpyAsync(soff.data(), C.d_soff, nsent * 8, hipMemcpyDeviceToHost, st));
+    }
+    HIP_TRY(h, hipStreamSynchronize(st));
+    lap("count");
+    if (dense && n) {
+      if (n > h->cells_rows_cap) {
+        (void)hipFree(h->d_cells_rows);
+        h->d_cells_rows = nullptr;
+        h->cells_rows_cap = 0;
+        HIP_TRY(h, hipMalloc(&h->d_cells_rows, n * 16));
+        h->cells_rows_cap = n;
+      }
+      HIP_TRY(h, launch_cells_emit(st, h->d_hist, h->hist_cells, h->T, C.d_base, C.d_np, (uint32_t)E, C.d_off,
+                                   (uint4*)h->d_cells_rows));
+      HIP_TRY(h, hipStreamSynchronize(st));
+    }
+    lap("emit");
+  }
   h->cells_sparse.clear();
-  for (uint32_t e = 0; e < E; e++) {
-    off[e] = n;
-    if (sidx_of[e] >= 0 && h->hist_base[e] == kHistSparse) {
-      auto& l = sparse[sidx_of[e]];
-      const uint64_t k = l.size();
-      if (k) h->cells_sparse.push_back({n, e, std::move(l)});
-      n += k;
-    } else {
-      n += cnt[e];
-    }
-  }
-  lap("prefix");
-  if (dense && n) {
-    if (n > h->cells_rows_cap) {
-      (void)hipFree(h->d_cells_rows);
-      h->d_cells_rows = nullptr;
-      h->cells_rows_cap = 0;
-      if ((rc = hip(hipMalloc(&h->d_cells_rows, n * 16), "alloc"))) return rc;
-      h->cells_rows_cap = n;
-    }
-    if ((rc = hip(hipMalloc(&d_off, (size_t)E * 8), "alloc")) ||
-        (rc = hip(hipMemcpyAsync(d_off, off.data(), (size_t)E * 8, hipMemcpyHostToDevice, h->stream), "upload")) ||
-        (rc = hip(launch_cells_emit(h->stream, h->d_hist, h->hist_cells, h->T, d_base, d_np, E, d_off,
-                                    (uint4*)h->d_cells_rows), "emit")) ||
-        (rc = hip(hipStreamSynchronize(h->stream), "emit")))
-      return rc;
-  }
-  lap("emit");
-  cleanup();
-  lap("free");
+  for (uint64_t s = 0; s < nsent; s++)
+    if (!sparse[s].empty()) h->cells_sparse.push_back({soff[s], h->sparse_entries[s], std::move(sparse[s])});
   if (timing) fprintf(stderr, "cells_prepare: %llu rows\n", (unsigned long long)n);
   h->cells_n = (int64_t)n;
   h->cells_epoch = h->epoch;

@@ -407,7 +407,7 @@ extern "C" int nmg_set_objects(nmg_engine* h, const uint64_t* keys, const uint32
                                uint32_t nb_keys, const nmg_object* entries, uint32_t nb_entries) {
   if (h) h->epoch++;
   if (h) h->counters_fresh = false;
-  if (h) h->snap.meta_dirty = true;
+  if (h) h->snap.meta_dirty = h->cprep.meta_dirty = true;
   Range range("nmg_set_objects");
   if (!h || (nb_keys && (!keys || !entry_off)) || (nb_entries && !entries))
     return NMG_ERR_INVALID;
@@ -691,7 +691,7 @@ extern "C" int nmg_update_objects(nmg_engine* h, const uint64_t* keys, const uin
                                   uint32_t nb_keys, const uint32_t* entry_ids, const nmg_object* objects) {
   if (h) h->epoch++;
   if (h) h->counters_fresh = false;  // (grown objects' page cells move)
-  if (h) h->snap.meta_dirty = true;
+  if (h) h->snap.meta_dirty = h->cprep.meta_dirty = true;
   Range range("nmg_update_objects");
   if (!h || (nb_keys && (!keys || !entry_off || !entry_ids || !objects))) return NMG_ERR_INVALID;
   if (!h->have_table) return fail(h, NMG_ERR_STATE, "nmg_update_objects before nmg_set_objects");
