@@ -64,6 +64,40 @@ def test_results_snapshot_equals_getters(case):
     eng.close()
 
 
+def test_page_cells_kept_buffers_across_tables():
+    """The page-cell preparation keeps its device buffers across calls and
+    tables (they only grow): one engine switched between a large and a small
+    table must give the rows a fresh engine gives for each, and a repeated
+    getter call the same rows again."""
+    import torch
+    from numamma_amd.engine import Engine
+
+    rps = [generate(SynthConfig(**CASES[c])) for c in ("k60k", "k700", "k60k")]
+    rps[2] = generate(SynthConfig(**dict(CASES["k60k"], seed=CASES["k60k"]["seed"] + 7)))
+    nthr = max(rp.nb_threads for rp in rps)
+    eng = Engine(nb_threads=nthr)
+    for i, rp in enumerate(rps):
+        arena, offs, lens, ranks, acc = rp.packed()
+        d = torch.from_numpy(arena).cuda()
+        eng.set_objects(rp.table)
+        eng.reset()
+        eng.set_device_buffers(d.data_ptr(), offs, lens, ranks, acc)
+        eng.analyze()
+        got = eng.page_cells()
+        again = eng.page_cells()
+        fresh = Engine(nb_threads=nthr)
+        fresh.set_objects(rp.table)
+        fresh.set_device_buffers(d.data_ptr(), offs, lens, ranks, acc)
+        fresh.analyze()
+        want = fresh.page_cells()
+        fresh.close()
+        assert want.shape[0] > 0, i
+        assert np.array_equal(np.asarray(got), np.asarray(want)), i
+        assert np.array_equal(np.asarray(again), np.asarray(want)), i
+        eng.synchronize()
+    eng.close()
+
+
 def test_results_snapshot_errors_and_restart():
     """end without begin is a state error; a begin nobody ended is waited for
     by the next begin; a snapshot after set_buffer_counts (merged counts) is
