@@ -11,7 +11,8 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # (NMG_LIB_PATH: another in-tree build of the same library, for A/B timing
-# of two kernel versions on one box; tools/ab_lib.sh)
+# of two kernel versions on one box; tools/ab_lib.sh.  Every export must still
+# be there unless NMG_LIB_AB=1 says the build is an older A/B side.)
 LIB_PATH = os.environ.get("NMG_LIB_PATH") or os.path.join(_HERE, "libnumamma_gpu.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "numamma_gpu.h")
 
@@ -220,12 +221,18 @@ _SIGS = {
     "nmg_run_replay": (C.c_int, [C.c_char_p, C.c_char_p, C.c_char_p, C.c_char_p, C.c_int, C.c_uint32]),
 }
 
+_SKIPPED = []
 for _name, (_res, _args) in _SIGS.items():
-    if os.environ.get("NMG_LIB_PATH") and not hasattr(lib, _name):
-        continue  # (A/B timing of an older build: functions it predates stay unbound)
+    if os.environ.get("NMG_LIB_AB") == "1" and not hasattr(lib, _name):
+        _SKIPPED.append(_name)  # (A/B timing of an older build: functions it predates stay unbound)
+        continue
     _fn = getattr(lib, _name)  # AttributeError == missing export: fail loudly
     _fn.restype = _res
     _fn.argtypes = _args
+if _SKIPPED:
+    import sys as _sys
+
+    print(f"numamma_amd: NMG_LIB_AB=1, {LIB_PATH} lacks {', '.join(_SKIPPED)}", file=_sys.stderr)
 
 
 def declared_symbols():

@@ -161,6 +161,7 @@ struct nmg_engine {
     uint32_t* h_bufcnt = nullptr;
     uint32_t* h_rows = nullptr;        // mapped: copy_rows_kernel writes it
     uint64_t h_cap_E = 0, h_cap_nb = 0, h_cap_sent = 0;
+    std::vector<uint32_t> sent_entry;  // begin-time table: sparse idx -> entry (~0: no longer sparse)
   } snap;
   uint64_t snap_nb = 0;  // buffers of the snapshot in flight
   // the synchronous page-cell getters' device buffers (cells_prepare), kept across calls

@@ -686,16 +686,22 @@ extern "C" int nmg_results_begin(nmg_engine* h) {
   if (rc) return rc;
   const uint64_t E = h->E, nb = h->descs.size(), nsent = h->sparse_entries.size();
   hipStream_t st = h->stream;
-  if (S.meta_dirty) {  // (the table's cell layout: uploaded once per table)
+  if (S.meta_dirty) {  // (the table's cell layout: uploaded once per table, through the
+                       // pinned staging on the engine stream -- begin never waits for it)
     std::vector<uint32_t> np(E);
     for (uint64_t e = 0; e < E; e++) np[e] = h->hist_base[e] == kHistSparse ? 0u : (uint32_t)h->npages[e];
-    if (E) {
-      HIP_TRY(h, hipMemcpyAsync(S.d_base, h->hist_base.data(), E * 8, hipMemcpyHostToDevice, st));
-      HIP_TRY(h, hipMemcpyAsync(S.d_np, np.data(), E * 4, hipMemcpyHostToDevice, st));
-    }
-    if (nsent) HIP_TRY(h, hipMemcpyAsync(S.d_sent, h->sparse_entries.data(), nsent * 4, hipMemcpyHostToDevice, st));
-    HIP_TRY(h, hipStreamSynchronize(st));  // (pageable sources)
+    rc = stage_h2d(h, S.d_base, h->hist_base.data(), E * 8);
+    if (!rc) rc = stage_h2d(h, S.d_np, np.data(), E * 4);
+    if (!rc) rc = stage_h2d(h, S.d_sent, h->sparse_entries.data(), nsent * 4);
+    if (rc) return rc;
     S.meta_dirty = false;
+  }
+  // the sparse entries as this table has them: nmg_results_end places the
+  // sparse rows with these, whatever table the engine holds by then
+  S.sent_entry.resize(nsent);
+  for (uint64_t s = 0; s < nsent; s++) {
+    const uint32_t e = h->sparse_entries[s];
+    S.sent_entry[s] = h->hist_base[e] == kHistSparse ? e : ~0u;
   }
   // the device snapshot, behind the enqueued analyses
   HIP_TRY(h, hipMemcpyAsync(S.d_sum, h->d_sum64, 2 * kGlobalSums * 8, hipMemcpyDeviceToDevice, st));
@@ -763,7 +769,7 @@ extern "C" int nmg_results_end(nmg_engine* h, nmg_results_view* out) {
   HIP_TRY(h, hipSetDevice(h->device));
   HIP_TRY(h, hipEventSynchronize(S.copied));
   S.pending = false;
-  const uint64_t E = S.E, nb = h->snap_nb, nsent = h->sparse_entries.size();
+  const uint64_t E = S.E, nb = h->snap_nb, nsent = S.sent_entry.size();  // (the begin-time table's)
   const uint64_t nrows = S.h_small[1], nspc = S.h_small[2];
   if (nrows > S.rows_host) {  // (the pinned rows outgrown: grown, and this time copied here)
     (void)hipHostFree(S.h_rows);
@@ -782,7 +788,7 @@ extern "C" int nmg_results_end(nmg_engine* h, nmg_results_view* out) {
       const uint64_t k = kv[2 * i];
       const uint32_t v = (uint32_t)kv[2 * i + 1];
       const uint32_t s = sparse_key_idx(k);
-      if (k == ~0ull || !v || s >= nsent || h->hist_base[h->sparse_entries[s]] != kHistSparse) continue;
+      if (k == ~0ull || !v || s >= nsent || S.sent_entry[s] == ~0u) continue;
       per[s].push_back({(uint64_t(sparse_key_thread(k)) << 32) | sparse_key_page(k), v});
     }
     for (uint64_t s = 0; s < nsent; s++) {
@@ -791,7 +797,7 @@ extern "C" int nmg_results_end(nmg_engine* h, nmg_results_view* out) {
       std::sort(l.begin(), l.end());
       uint32_t* r = S.h_rows + S.h_soff[s] * 4;
       for (const auto& c : l) {
-        r[0] = h->sparse_entries[s];
+        r[0] = S.sent_entry[s];
         r[1] = (uint32_t)(c.first >> 32);
         r[2] = (uint32_t)c.first;
         r[3] = c.second;

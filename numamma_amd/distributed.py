@@ -152,6 +152,8 @@ class HistPacker:
 
 
 GLOBAL_SUM_WORDS = 2 * 39  # sum64's head: [2 access][39] global sums (nmg_internal.h kGlobalSums)
+LEVEL_WORDS = 37           # per entry and access: na, 18 x (count, sum) (nmg_internal.h kLevelWords)
+GLOBAL_MIN_WORDS = 2 * 18  # min64's head: [2][18] bucket minima, then [E] ordinals and the error word
 
 
 class ObjPacker:
@@ -168,8 +170,15 @@ class ObjPacker:
 
         self.eng = eng
         n = eng.array_size(_lib.NMG_ARR_SUM64)
-        per = 78 if (eng.flags & _lib.NMG_F_OBJECT_LEVELS) else 4  # (levels: [E][2][37] after the rows)
-        self.E = (n - GLOBAL_SUM_WORDS) // per if n else 0
+        levels = bool(eng.flags & _lib.NMG_F_OBJECT_LEVELS)
+        per = 4 + (2 * LEVEL_WORDS if levels else 0)  # (levels: [E][2][37] after the rows)
+        # the entry count from min64 ([2][18] minima, [E] ordinals, error word), checked
+        # against sum64's size: a layout change in nmg_internal.h fails here, not silently
+        self.E = eng.array_size(_lib.NMG_ARR_MIN64) - GLOBAL_MIN_WORDS - 1 if n else 0
+        if n and self.E * per + GLOBAL_SUM_WORDS != n:
+            raise RuntimeError(f"ObjPacker: sum64 holds {n} words, not {GLOBAL_SUM_WORDS} + {per} x {self.E} entries")
+        self.n_sum64 = n  # the engine's sum64 size this packer was built for
+        self.levels = levels
         self.rows = 4 * self.E
         self.cap = max(1024, int(self.rows * ovf_frac))
         self.u32 = torch.empty(max(self.rows, 1), dtype=torch.int32, device=device)
@@ -254,8 +263,8 @@ def merge_engine(eng, dst: int = 0, group=None, device=None, packed_hist: bool =
         eng.export_array(which, t.data_ptr())
         got = None
         if packed_hist and which == _lib.NMG_ARR_SUM64:  # the per-object rows as u32 + a list
-            op_ = getattr(eng, "_obj_packer", None)
-            if op_ is None or op_.E * 4 + GLOBAL_SUM_WORDS > n:
+            op_ = getattr(eng, "_obj_packer", None)  # rebuilt whenever the table's size changed
+            if op_ is None or op_.n_sum64 != n or op_.levels != bool(eng.flags & _lib.NMG_F_OBJECT_LEVELS):
                 op_ = eng._obj_packer = ObjPacker(eng, dev)
             got = op_.merge(t, dst=dst, group=group)
             if got is not None:

@@ -33,7 +33,10 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, workdir, cfg_name, ret, packed=False):
+def _worker(rank, world, port, workdir, cfg_name, ret, packed=False, before=None):
+    """before: a configuration analysed and merged first on the same engines,
+    whose table is then replaced by cfg_name's (a larger one: the merge's
+    cached packers must be rebuilt for the new entry count)."""
     sys.path[:0] = [ROOT, os.path.join(ROOT, "oracle")]
     try:
         import torch
@@ -44,23 +47,32 @@ def _worker(rank, world, port, workdir, cfg_name, ret, packed=False):
         from numamma_amd.replay import SynthConfig, generate
 
         dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
-        rp = generate(SynthConfig(**CFGS[cfg_name]))
-        arena, offs, lens, ranks, acc = rp.packed()
-        lo, hi = shard_ranges(lens, world)[rank]
         dev = torch.device("cuda", 0)
-        base = int(offs[lo]) if hi > lo else 0
-        end = int(offs[hi - 1] + lens[hi - 1]) if hi > lo else 0
-        d_arena = torch.from_numpy(arena[base:end].copy()).to(dev)
-        eng = Engine(device=0, nb_threads=rp.nb_threads)
-        eng.set_objects(rp.table)
-        eng.set_device_buffers(d_arena.data_ptr(), offs[lo:hi] - base, lens[lo:hi], ranks[lo:hi], acc[lo:hi],
-                               seq_base=lo)
-        for rep in range(2 if packed else 1):  # (packed: a second job on the same engines, reset in between --
-            if rep:                             # rank 0 drops the first merge's per-buffer counts)
+        eng = None
+        keep = []
+        for name in ([before] if before else []) + [cfg_name]:
+            rp = generate(SynthConfig(**CFGS[name]))
+            arena, offs, lens, ranks, acc = rp.packed()
+            lo, hi = shard_ranges(lens, world)[rank]
+            base = int(offs[lo]) if hi > lo else 0
+            end = int(offs[hi - 1] + lens[hi - 1]) if hi > lo else 0
+            d_arena = torch.from_numpy(arena[base:end].copy()).to(dev)
+            keep.append(d_arena)
+            if eng is None:
+                eng = Engine(device=0, nb_threads=rp.nb_threads)
+            else:
+                eng.clear_buffers()
+            eng.set_objects(rp.table)
+            eng.set_device_buffers(d_arena.data_ptr(), offs[lo:hi] - base, lens[lo:hi], ranks[lo:hi], acc[lo:hi],
+                                   seq_base=lo)
+            for rep in range(2 if packed else 1):  # (packed: a second job on the same engines, reset in between
+                if rep:                             # -- rank 0 drops the first merge's per-buffer counts)
+                    eng.reset()
+                eng.analyze()
+                eng.synchronize()
+                merge_engine(eng, dst=0, device=dev, packed_hist=packed)
+            if name != cfg_name:
                 eng.reset()
-            eng.analyze()
-            eng.synchronize()
-            merge_engine(eng, dst=0, device=dev, packed_hist=packed)
         if rank == 0:
             edir = os.path.join(workdir, "engine")
             eng.report(edir, os.path.join(workdir, "e.txt"))
@@ -82,6 +94,17 @@ def _worker(rank, world, port, workdir, cfg_name, ret, packed=False):
 @pytest.mark.parametrize("packed", [False, True], ids=["dense", "packed"])
 @pytest.mark.parametrize("cfg_name", sorted(CFGS))
 def test_two_rank_engine_merge_matches_oracle(cfg_name, packed):
+    _two_rank(cfg_name, packed)
+
+
+def test_two_rank_packed_merge_after_table_grew():
+    """Two packed merges on the same engines, the table grown from 700 to
+    60k intervals in between (the per-object packer must follow
+    the entry count, not write past its buffer)."""
+    _two_rank("k60k", True, before="k700")
+
+
+def _two_rank(cfg_name, packed, before=None):
     import multiprocessing as mp
 
     sys.path[:0] = [ROOT, os.path.join(ROOT, "oracle")]
@@ -93,7 +116,7 @@ def test_two_rank_engine_merge_matches_oracle(cfg_name, packed):
     ret = ctx.Queue()
     with tempfile.TemporaryDirectory() as d:
         port = _free_port()
-        procs = [ctx.Process(target=_worker, args=(r, 2, port, d, cfg_name, ret, packed)) for r in range(2)]
+        procs = [ctx.Process(target=_worker, args=(r, 2, port, d, cfg_name, ret, packed, before)) for r in range(2)]
         for p in procs:
             p.start()
         msgs = [ret.get(timeout=240) for _ in procs]

@@ -127,3 +127,37 @@ def test_results_snapshot_errors_and_restart():
     with pytest.raises(NmgError):
         eng.results_begin()
     eng.close()
+
+
+def test_results_snapshot_survives_table_switch():
+    """A table switch between nmg_results_begin and nmg_results_end (ADVICE
+    r5): the view is the begin-time analysis, its sparse rows placed with the
+    begin-time table's sparse entries, even though nmg_set_objects replaced
+    the table (different entry count and sparse entries) in between."""
+    import torch
+    from numamma_amd.engine import Engine
+
+    rp = generate(SynthConfig(**CASES["k60k"]))
+    rp2 = generate(SynthConfig(**dict(CASES["k60k"], nb_intervals=20_000, seed=123)))
+    arena, offs, lens, ranks, acc = rp.packed()
+    arena2, offs2, lens2, ranks2, acc2 = rp2.packed()
+    d1 = torch.from_numpy(arena).cuda()
+    d2 = torch.from_numpy(arena2).cuda()
+    eng = Engine(nb_threads=max(rp.nb_threads, rp2.nb_threads))
+    eng.set_objects(rp.table)
+    eng.set_device_buffers(d1.data_ptr(), offs, lens, ranks, acc)
+    eng.analyze()
+    want = _sync_results(eng)
+    assert want[7].shape[0] > 0
+    eng.results_begin()
+    eng.clear_buffers()
+    eng.set_objects(rp2.table)
+    eng.set_device_buffers(d2.data_ptr(), offs2, lens2, ranks2, acc2)
+    eng.analyze()
+    got = eng.results_end()
+    names = ("global", "nb_samples", "nb_found", "buffer_samples", "buffer_found", "first_ordinal", "count_weight",
+             "cells")
+    for name, x, y in zip(names, want, got):
+        assert np.array_equal(np.asarray(x), np.asarray(y)), name
+    eng.synchronize()
+    eng.close()

@@ -5,7 +5,7 @@ cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 TAG=$1; LIB=${2:-}
-[ -n "$LIB" ] && export NMG_LIB_PATH=$PWD/$LIB
+[ -n "$LIB" ] && export NMG_LIB_PATH=$PWD/$LIB NMG_LIB_AB=1
 i=0
 for set in "TA_TA_BUSY_sum TA_BUFFER_WRITE_WAVEFRONTS_sum GRBM_GUI_ACTIVE" "TD_TD_BUSY_sum TCP_TCP_TA_DATA_STALL_CYCLES_sum GRBM_GUI_ACTIVE" "TA_BUFFER_TOTAL_CYCLES_sum TA_ADDR_STALLED_BY_TC_CYCLES_sum GRBM_GUI_ACTIVE"; do
   i=$((i+1))
