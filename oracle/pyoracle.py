@@ -11,7 +11,9 @@ import os
 import subprocess
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-ORACLE_SO = os.path.join(HERE, "liboracle.so")
+# (NMG_ORACLE_DIR: the sanitizer build of the oracle libraries, tools/sanitize.sh)
+SO_DIR = os.environ.get("NMG_ORACLE_DIR") or HERE
+ORACLE_SO = os.path.join(SO_DIR, "liboracle.so")
 REF_SO = os.path.join(HERE, "_ref", "libref_hash.so")
 REF_HASH_TEST = os.path.join(HERE, "_ref", "hash_test")
 
@@ -142,7 +144,7 @@ def run_mt(replay_path: str, raw_path: str | None = None, threads: int = 16, lev
     returns the timings: load, parallel analysis, merge."""
     global _mt
     if _mt is None:
-        so = os.path.join(HERE, "liboracle_mt.so")
+        so = os.path.join(SO_DIR, "liboracle_mt.so")
         if not os.path.exists(so):
             build()
         _mt = C.CDLL(so)

@@ -17,7 +17,8 @@ from numamma_amd.replay import SynthConfig, generate
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 BIN = os.path.join(ROOT, "numamma_amd", "bin")
-INTERPOSER = os.path.join(BIN, "libnmg_interpose.so")
+# (NMG_INTERPOSER: the UBSan build of the interposer, tools/sanitize.sh)
+INTERPOSER = os.environ.get("NMG_INTERPOSER") or os.path.join(BIN, "libnmg_interpose.so")
 
 
 def interposed_env(**extra):
