@@ -87,6 +87,10 @@ class Workload:
         self.merge_bufs = []
         self.hist_packer = None
         self.obj_packer = None
+        # per-step split of a distributed step (host clock): analysis (reset +
+        # analyze + synchronize) and merge (exports, RCCL reduces / gathers,
+        # imports, synchronized), and the counter bytes this rank contributes
+        self.split = {"analysis_s": 0.0, "merge_s": 0.0, "steps": 0, "payload_bytes": 0}
         if distributed:  # merge buffers for the timed RCCL reduces (dense arrays)
             from numamma_amd.distributed import HistPacker, ObjPacker
 
@@ -101,22 +105,36 @@ class Workload:
             self.obj_packer = ObjPacker(self.eng, device)
 
     def step(self):
+        import torch
+
         from numamma_amd import _lib
         from numamma_amd.distributed import GLOBAL_SUM_WORDS, reduce_u64
 
+        t0 = time.perf_counter()
         self.eng.reset()
         self.eng.analyze()
         if self.merge_bufs:
             self.eng.synchronize()
+            t1 = time.perf_counter()
+            nbytes = 0
             for which, t in self.merge_bufs:
                 self.eng.export_array(which, t.data_ptr())
                 if which == _lib.NMG_ARR_SUM64 and self.obj_packer is not None:
-                    if self.obj_packer.merge(t, dst=0) is not None:
+                    got = self.obj_packer.merge(t, dst=0)
+                    if got is not None:
                         reduce_u64(t[:GLOBAL_SUM_WORDS], "sum", dst=0)  # (the global sums as u64)
+                        nbytes += got + 8 * GLOBAL_SUM_WORDS
                         continue
                 reduce_u64(t, {0: "sum", 1: "min", 2: "max"}[which], dst=0)
+                nbytes += 8 * t.numel()
             if self.hist_packer is not None:
-                self.hist_packer.merge(dst=0)
+                nbytes += self.hist_packer.merge(dst=0)
+            torch.cuda.synchronize(self.d_arena.device)  # (the reduces ran on the collectives' stream)
+            t2 = time.perf_counter()
+            self.split["analysis_s"] += t1 - t0
+            self.split["merge_s"] += t2 - t1
+            self.split["steps"] += 1
+            self.split["payload_bytes"] = nbytes
 
 
 def timed_run(w, steps, warmup, barrier, agree=None):
@@ -131,6 +149,8 @@ def timed_run(w, steps, warmup, barrier, agree=None):
         steps = int(min(2000, max(20, math.ceil(MIN_TIMED_S / max(one, 1e-6)))))
         if agree:  # every rank runs rank 0's count (the steps hold collectives)
             steps = agree(steps)
+    if hasattr(w, "split"):  # (the timed steps only)
+        w.split.update(analysis_s=0.0, merge_s=0.0, steps=0)
     t_start = time.perf_counter()
     for _ in range(steps):
         w.step()
@@ -222,8 +242,19 @@ def main():
     if distributed:
         merge_engine(w.eng, dst=0)  # full merge once (dense + gathers) for the report
 
+    split = None
+    if distributed and w.split["steps"]:  # the slowest rank's analysis / merge split per step
+        sp = torch.tensor([w.split["analysis_s"], w.split["merge_s"]], dtype=torch.float64,
+                          device=device if backend == "nccl" else "cpu")
+        dist.all_reduce(sp, op=dist.ReduceOp.MAX)
+        split = {"analysis_ms": float(sp[0]) * 1e3 / w.split["steps"], "merge_ms": float(sp[1]) * 1e3 / w.split["steps"],
+                 "payload_bytes_per_rank": int(w.split["payload_bytes"]),
+                 "note": "host clock per timed step, maximum over ranks: analysis = reset + analyze + synchronize; "
+                         "merge = exports + RCCL reduces / gathers + imports, synchronized"}
     if rank == 0:
         out = result_line(args, w, world, steps, ms_per_step, value, attr_ms, total_ms, phases)
+        if split:
+            out["merge"] = split
         if world == 1 and args.secondary:
             out["secondary"] = {}
             for name in args.secondary.split(","):
@@ -271,7 +302,8 @@ def main_one_process(args):
 
     n = args.gpus
     visible = torch.cuda.device_count()
-    if visible < n:
+    same = os.environ.get("NMG_BENCH_SAME_GPU") == "1"  # (test hook: every worker on GPU 0, device merges)
+    if visible < n and not same:
         log(f"error: --gpus {n} but {visible} GPU(s) visible")
         sys.exit(2)
     wl = WORKLOADS[args.workload]
@@ -282,7 +314,7 @@ def main_one_process(args):
     shard = sum(x.nbytes for x in bufs) // RECORD_BYTES
     log(f"[1 process, {n} GPUs] {args.workload}: shard of {shard} records in {len(bufs)} buffers, generated in "
         f"{time.time() - t0:.1f}s; every GPU analyses one copy of it")
-    eng = Engine(devices=list(range(n)), nb_threads=rp.nb_threads, copy_threads=16)
+    eng = Engine(devices=[0] * n if same else list(range(n)), nb_threads=rp.nb_threads, copy_threads=16)
     eng.set_objects(rp.table)
     subs = [(b.thread_rank, b.access_type, x) for b, x in zip(rp.buffers, bufs) if x.shape[0]]
     for _ in range(n):  # N shards in analysis order; the handle cuts them into N byte-balanced ranges
@@ -299,6 +331,7 @@ def main_one_process(args):
             torch.cuda.synchronize(d)
 
     elapsed, steps = timed_run(W(), args.steps, args.warmup, barrier)
+    merge_ms, payload = eng.merge_stats()  # (the last step's merge, GPU events on the root device)
     g, ns, nf = eng.global_counters()
     assert ns == n * shard, (ns, n * shard)
     ms_per_step = elapsed * 1e3 / steps
@@ -321,6 +354,11 @@ def main_one_process(args):
                                    "RCCL reduce of the counters" if n > 1 else
                                    "one process, one engine handle over host-staged buffers (the --gpus N path at N=1)")},
     }
+    out["merge"] = {"merge_ms": merge_ms, "analysis_ms": ms_per_step - merge_ms, "payload_bytes_per_gpu": payload,
+                    "note": ("GPU events on the root device around the last step's counter merge (end of worker 0's "
+                             "analysis to the end of the reduces, waiting for the other workers included); analysis_ms "
+                             "= ms_per_step - merge_ms" if n > 1 else "one GPU: no merge")
+                            + ("; workers share GPU 0 (NMG_BENCH_SAME_GPU=1): device merges, not RCCL" if same else "")}
     # per GPU: its shard's 40 B records over the whole step (analysis, the
     # RCCL reduce of the counters into GPU 0's handle, the handle's gathers)
     achieved = shard * RECORD_BYTES / (ms_per_step * 1e-3) / 1e9

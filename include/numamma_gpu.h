@@ -392,6 +392,12 @@ int nmg_get_launch_times(nmg_engine *h, float *ms, int n);
 /* the same launches split: the attribution kernel alone (attribute_ms) and the
  * whole launch including the long-tail reduce (total_ms); returns the count */
 int nmg_get_kernel_times(nmg_engine *h, float *attribute_ms, float *total_ms, int n);
+/* a multi-GPU handle's last nmg_analyze: GPU time of the counter merge on the
+ * root device (from the end of worker 0's analysis to the end of the reduces
+ * into the handle, waiting for the other workers included) and the counter
+ * bytes each worker contributes to it (sum64, min64, max64, page histogram);
+ * 0 and 0 for a single-GPU engine */
+int nmg_get_merge_stats(nmg_engine *h, float *merge_ms, uint64_t *payload_bytes);
 
 /*
  * Report: the stdout text of mem_sampling_finalize + ma_finalize from

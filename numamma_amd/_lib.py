@@ -212,6 +212,7 @@ _SIGS = {
     "nmg_sparse_import": (C.c_int, [H, u64p, u32p, C.c_int64]),
     "nmg_set_buffer_counts": (C.c_int, [H, C.c_uint32, u32p, u32p, u64p]),
     "nmg_last_analyze_ms": (C.c_int, [H, C.POINTER(C.c_float)]),
+    "nmg_get_merge_stats": (C.c_int, [H, C.POINTER(C.c_float), C.POINTER(C.c_uint64)]),
     "nmg_get_launch_times": (C.c_int, [H, C.POINTER(C.c_float), C.c_int]),
     "nmg_get_kernel_times": (C.c_int, [H, C.POINTER(C.c_float), C.POINTER(C.c_float), C.c_int]),
     "nmg_debug_phase_times": (C.c_int, [H, C.POINTER(C.c_float), C.POINTER(C.c_float), C.c_int]),

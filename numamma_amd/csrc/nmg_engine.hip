@@ -100,6 +100,7 @@ void free_route_table(nmg_engine* h) {
   (void)hipFree(h->d_parts);
   (void)hipFree(h->d_pbounds);
   (void)hipFree(h->d_pdir);
+  (void)hipFree(h->d_pdead);
   (void)hipFree(h->d_pe_keys);
   (void)hipFree(h->d_pe_nodes);
   (void)hipFree(h->d_pe_info);
@@ -117,6 +118,7 @@ void free_route_table(nmg_engine* h) {
   h->d_parts = nullptr;
   h->d_pbounds = nullptr;
   h->d_pdir = nullptr;
+  h->d_pdead = nullptr;
   h->d_pe_keys = nullptr;
   h->d_pe_nodes = nullptr;
   h->d_pe_info = nullptr;
@@ -545,6 +547,18 @@ extern "C" int nmg_get_kernel_times(nmg_engine* h, float* attribute_ms, float* t
     HIP_TRY(h, hipEventElapsedTime(&total_ms[i], h->ring0[slot], h->ring1[slot]));
   }
   return cnt;
+}
+
+extern "C" int nmg_get_merge_stats(nmg_engine* h, float* merge_ms, uint64_t* payload_bytes) {
+  if (!h || !merge_ms || !payload_bytes) return NMG_ERR_INVALID;
+  *merge_ms = 0.f;
+  *payload_bytes = 0;
+  if (!h->multi || !h->merge_timed) return NMG_OK;
+  HIP_TRY(h, hipSetDevice(h->device));
+  HIP_TRY(h, hipEventSynchronize(h->merge_ev1));
+  HIP_TRY(h, hipEventElapsedTime(merge_ms, h->merge_ev0, h->merge_ev1));
+  *payload_bytes = h->merge_bytes;
+  return NMG_OK;
 }
 
 extern "C" int nmg_last_analyze_ms(nmg_engine* h, float* ms) {

@@ -281,6 +281,12 @@ struct nmg_engine {
   std::vector<int> devices;
   bool multi = false, multi_distinct = false, multi_pending = false;
   uint64_t multi_found = 0;  // matched SAMPLEs of the workers (multi_finish)
+  // the merge of the last multi_analyze, timed on the root device's stream that
+  // carries it (worker 0's for RCCL, this handle's for device merges): from
+  // the end of worker 0's analysis to the end of the merges (nmg_get_merge_stats)
+  hipEvent_t merge_ev0 = nullptr, merge_ev1 = nullptr;
+  bool merge_timed = false;
+  uint64_t merge_bytes = 0;  // counter bytes each worker contributes per merge
   std::vector<void*> comms;  // ncclComm_t per worker (distinct devices)
   std::vector<uint8_t*> warena;
   std::vector<size_t> warena_cap;
@@ -293,6 +299,7 @@ struct nmg_engine {
   PartInfo* d_parts = nullptr;
   uint64_t* d_pbounds = nullptr;  // [kMaxParts + 1] partition starts, ascending
   uint16_t* d_pdir = nullptr;     // [kRouteDir] the route pass's directory over them
+  uint32_t* d_pdead = nullptr;    // [(kMaxParts + 1) / 32] partitions no sample with ts != 0 can match
   RSeg rsegs[kRouteSegs];         // its segments
   uint64_t route_tbase = 0;       // compact records: timestamps relative to this (XLayout)
   uint32_t nrsegs = 0;

@@ -82,6 +82,10 @@ void multi_destroy(nmg_engine* h) {
   }
   if (Rccl* r = rccl())
     for (void* c : h->comms) r->destroy((ncclComm_t)c);
+  (void)hipSetDevice(h->device);
+  if (h->merge_ev0) (void)hipEventDestroy(h->merge_ev0);
+  if (h->merge_ev1) (void)hipEventDestroy(h->merge_ev1);
+  h->merge_ev0 = h->merge_ev1 = nullptr;
   for (nmg_engine* w : h->workers) nmg_destroy(w);
   h->workers.clear();
   h->comms.clear();
@@ -143,6 +147,27 @@ int multi_analyze(nmg_engine* h) {
     int which, op;
   };
   const Arr arrs[4] = {{NMG_ARR_SUM64, 0}, {NMG_ARR_MIN64, 1}, {NMG_ARR_MAX64, 2}, {NMG_ARR_HIST32, 3}};
+  // merge timing (nmg_get_merge_stats): worker 0 shares this handle's device
+  HIP_TRY(h, hipSetDevice(h->device));
+  if (!h->merge_ev0) {
+    HIP_TRY(h, hipEventCreate(&h->merge_ev0));
+    HIP_TRY(h, hipEventCreate(&h->merge_ev1));
+  }
+  hipStream_t mst = h->multi_distinct ? h->workers[0]->stream : h->stream;
+  if (!h->multi_distinct) {  // (the device merges run on this handle's stream after worker 0's analysis)
+    hipEvent_t ev;
+    HIP_TRY(h, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    HIP_TRY(h, hipEventRecord(ev, h->workers[0]->stream));
+    HIP_TRY(h, hipStreamWaitEvent(h->stream, ev, 0));
+    (void)hipEventDestroy(ev);
+  }
+  HIP_TRY(h, hipEventRecord(h->merge_ev0, mst));
+  h->merge_bytes = 0;
+  for (const Arr& x : arrs) {
+    size_t bytes = 0;
+    (void)array_ptr(h->workers[0], x.which, &bytes);
+    h->merge_bytes += bytes;
+  }
   // The workers' counters accumulate like this handle's would (they are
   // reset only with it), so the handle's arrays are rebuilt as the merge of
   // the workers' -- no pass of its own over the old values.
@@ -197,6 +222,9 @@ int multi_analyze(nmg_engine* h) {
       }
     }
   }
+  HIP_TRY(h, hipSetDevice(h->device));
+  HIP_TRY(h, hipEventRecord(h->merge_ev1, mst));
+  h->merge_timed = true;
   h->multi_staged = true;
   h->multi_pending = true;
   h->launched = false;

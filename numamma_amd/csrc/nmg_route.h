@@ -156,6 +156,10 @@ struct RouteParams {
                              // global counters, per-buffer counts, and the table for direct attribution
   const uint64_t* pbounds;   // [kMaxParts + 1] partition start keys, ascending, ~0 padding
   const uint16_t* pdir;      // [kRouteDir] directory slots of every segment
+  const uint32_t* pdead;     // [(kMaxParts + 1) / 32] bit q: every entry of partition q has free_date 0,
+                             // so only a sample with timestamp 0 can match one (alloc <= ts <= free,
+                             // is_sample_in_buffer, mem_analyzer.c:148-149): the [stack] range after
+                             // warn_non_freed_buffers (Q4), an online table's live objects (Q3)
   RSeg seg[kRouteSegs];      // segments of the partition starts, ascending
   uint32_t nseg;
   uint32_t nparts;

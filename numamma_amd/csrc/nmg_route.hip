@@ -14,6 +14,22 @@
 #include "nmg_device.h"
 #include "nmg_route.h"
 
+// build-time A/B switches of route2_kernel (tools/ab_build.sh -D...; the
+// defaults are the shipped kernel): workgroup size, the back stage of two
+// windows at a time, the global minimum / maximum read from LDS per record
+#ifndef NMG_R2WG
+#define NMG_R2WG 768
+#endif
+#ifndef NMG_R2PAIR
+#define NMG_R2PAIR 0
+#endif
+#ifndef NMG_R2LDSMM  // (1: the shipped way; 0: per-lane register minima / maxima, measured no faster)
+#define NMG_R2LDSMM 1
+#endif
+#ifndef NMG_ABL_NOSCATTER  // (ablation only, results wrong: no record stored outside the line stage)
+#define NMG_ABL_NOSCATTER 0
+#endif
+
 namespace nmg {
 
 static_assert((uint64_t)kItemChunks * kChunk * kLaneMaxWeight < (1ull << kPackShift), "packed weight per item");
@@ -188,7 +204,10 @@ struct RDesc {
 // route pass: per lane and access type, one u32 per counter pair, count << 24
 // | weight sum, for the total and for kRtGroups buckets (the common PEBS
 // levels: hits in L1, LFB, L2, L3, local RAM and remote RAM, L3 misses); the
-// NA count.  A record whose weight reaches 2^16, or that falls in another
+// NA count; and per group the minimum and maximum weight of the records whose
+// first group it is, as one u32 of two u16 fields, max << 16 | (0xffff -
+// min) (0: no record; every record makes it non-zero), kept with one packed
+// u16 max.  A record whose weight reaches 2^16, or that falls in another
 // bucket, or in two, is counted -- those parts -- by LDS atomics.  Drained
 // every kRouteDrain windows (255 records of < 2^16 fit 24 bits).
 //
@@ -208,19 +227,36 @@ constexpr uint32_t kRtKnown = 0x7fu | (8u << 11);
 constexpr uint32_t kRouteDrain = 128;
 constexpr uint32_t kRtOne = 1u << 24;
 struct RouteAcc {
-  uint32_t tot, na, g[kRtGroups];
+  uint32_t tot, na, g[kRtGroups], mm[kRtGroups];
 };
 __device__ __forceinline__ void racc_clear(RouteAcc& a) {
   a.tot = a.na = 0;
 #pragma unroll
-  for (int g = 0; g < kRtGroups; g++) a.g[g] = 0;
+  for (int g = 0; g < kRtGroups; g++) a.g[g] = a.mm[g] = 0;
+}
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+// both u16 fields' maxima (v_pk_max_u16)
+__device__ __forceinline__ uint32_t pk_max_u16(uint32_t a, uint32_t b) {
+  const u16x2 r = __builtin_elementwise_max(__builtin_bit_cast(u16x2, a), __builtin_bit_cast(u16x2, b));
+  return __builtin_bit_cast(uint32_t, r);
+}
+// full-wave u32 maximum (DPP, as wave_sum_u32; lanes past a row's edge read 0)
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+  v = max(v, dpp0<0x111, 0xf>(v));
+  v = max(v, dpp0<0x112, 0xf>(v));
+  v = max(v, dpp0<0x114, 0xf>(v));
+  v = max(v, dpp0<0x118, 0xf>(v));
+  v = max(v, dpp0<0x142, 0xa>(v));
+  v = max(v, dpp0<0x143, 0xc>(v));
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
 }
 
 // the counting of one SAMPLE of access type ACC (a wave window lies in one
 // buffer: the caller branches on the access once); every lane of the wave
 // calls it, `valid` the ones with a SAMPLE.  The minimum / maximum of the
-// record's register bucket is read first and updated by an LDS atomic only
-// when the record moves it.
+// record's first group is read from LDS and updated by an LDS atomic only when
+// the record moves it (NMG_R2LDSMM=0: kept in the lane's registers until the
+// drain instead -- measured no faster).
 template <uint32_t ACC>
 __device__ __forceinline__ void route_count(RouteAcc& a, unsigned long long (*sums)[kGlobalSums],
                                             unsigned long long (*mins)[18], unsigned long long (*maxs)[18],
@@ -238,11 +274,18 @@ __device__ __forceinline__ void route_count(RouteAcc& a, unsigned long long (*su
     gm |= in ? 1u << g : 0u;
   }
   const uint32_t fb = gm ? (kRtBucketNib >> (4 * __builtin_ctz(gm))) & 15u : 0xffu;
-  if (valid && gm) {
+#if NMG_R2LDSMM  // read the LDS minimum / maximum, an atomic when the record moves it
+  if (valid && gm && !big) {
     const unsigned long long mn = mins[ACC][fb], mx = maxs[ACC][fb];
     if (w < mn) atomicMin(&mins[ACC][fb], (unsigned long long)w);
     if (w > mx) atomicMax(&maxs[ACC][fb], (unsigned long long)w);
   }
+#else  // (A/B, round 6) the lane's registers, drained with the counts
+  const uint32_t pw = (valid && !big) ? ((uint32_t)w << 16) | (0xffffu - (uint32_t)w) : 0u;
+  const uint32_t first = gm & (0u - gm);  // the record's first group
+#pragma unroll
+  for (int g = 0; g < kRtGroups; g++) a.mm[g] = first == (1u << g) ? pk_max_u16(a.mm[g], pw) : a.mm[g];
+#endif
   // (rare) every other bucket, and the whole record when its weight is big
   const bool rare = valid && (big || (cls & ~kRtKnown) || (gm & (gm - 1)));
   if (__ballot(rare)) {
@@ -261,7 +304,7 @@ __device__ __forceinline__ void route_count(RouteAcc& a, unsigned long long (*su
           atomicAdd(&sums[ACC][3 + 2 * bk], 1ull);
           if (w) atomicAdd(&sums[ACC][4 + 2 * bk], (unsigned long long)w);
         }
-        if (bk != fb) {
+        if (bk != fb || big) {  // (the first group's, in registers unless big)
           atomicMin(&mins[ACC][bk], (unsigned long long)w);
           atomicMax(&maxs[ACC][bk], (unsigned long long)w);
         }
@@ -271,8 +314,22 @@ __device__ __forceinline__ void route_count(RouteAcc& a, unsigned long long (*su
 }
 
 // lanes -> the workgroup's LDS counters (every lane of the wave calls this)
-__device__ __forceinline__ void racc_drain(RouteAcc& a, unsigned long long* sums, int lane) {
-  if (__ballot(a.tot != 0) == 0) return;  // (every register count comes with the total's)
+__device__ __forceinline__ void racc_drain(RouteAcc& a, unsigned long long* sums, unsigned long long* mins,
+                                           unsigned long long* maxs, int lane) {
+#pragma unroll
+  for (int g = 0; g < kRtGroups; g++) {  // the groups' minimum / maximum weights
+    if (__ballot(a.mm[g] != 0) == 0) continue;
+    const uint32_t hi = wave_max_u32(a.mm[g] >> 16), lo = wave_max_u32(a.mm[g] & 0xffffu);
+    const uint32_t bk = (kRtBucketNib >> (4 * g)) & 15u;
+    if (lane == 0) {
+      atomicMin(&mins[bk], (unsigned long long)(0xffffu - lo));
+      atomicMax(&maxs[bk], (unsigned long long)hi);
+    }
+  }
+  if (__ballot(a.tot != 0) == 0) {
+    racc_clear(a);
+    return;
+  }  // (every register count comes with the total's)
   auto add = [&](uint32_t v, int word) {  // count << 24 | weight -> words word, word + 1
     if (__ballot(v != 0) == 0) return;
     const uint32_t c = wave_sum_u32(v >> 24), wt = wave_sum_u32(v & (kRtOne - 1));
@@ -368,7 +425,7 @@ __device__ __forceinline__ RDesc route_desc(const RouteParams& rp, const uint4* 
 // holds, after the workgroup's last barrier.
 
 // route2_kernel's workgroup: 12 waves (three per SIMD)
-constexpr uint32_t kR2WG = 768;
+constexpr uint32_t kR2WG = NMG_R2WG;
 // line stage: partitions q < kLineParts have an LDS line
 constexpr uint32_t kLineParts = 1280;
 // line word (u64): line l's count (3 bits) at 3 * (l mod 8), staged slots
@@ -542,10 +599,27 @@ __device__ __forceinline__ Claim route2_settle(uint64_t old, uint32_t q, unsigne
   return r;
 }
 
+template <int N>
+__device__ __forceinline__ bool any_of(const bool (&b)[N]) {
+  bool r = false;
+#pragma unroll
+  for (int i = 0; i < N; i++) r |= b[i];
+  return r;
+}
+
+// a routed record between route2_kernel's front (stream, counters, partition,
+// encode) and its back (claim, line stage, store)
+struct XF {
+  uint4 a;     // the compact record
+  uint32_t q;  // its partition
+  bool routed;
+};
+
 template <bool TIMING>
 __global__ __launch_bounds__(kR2WG, 1) void route2_kernel(RouteParams rp) {
   __shared__ uint64_t s_pb[kMaxParts + 1];
   __shared__ uint16_t s_pdir[kRouteDir];
+  __shared__ uint32_t s_dead[(kMaxParts + 1) / 32];
   __shared__ unsigned long long s_state[kMaxParts + 1];  // open chunk << 32 | slots claimed in it
   __shared__ uint4 s_desc[kDescLds];
   __shared__ uint32_t s_wlist[kWaves][64];  // slow path: the wave window's SAMPLE offsets
@@ -577,6 +651,7 @@ __global__ __launch_bounds__(kR2WG, 1) void route2_kernel(RouteParams rp) {
   const uint32_t capl = min(cap, kStMaxLocal + 1);  // (pool indices fit the state's 20-bit fields)
   for (uint32_t i = tid; i < kMaxParts + 1; i += kR2WG) s_pb[i] = rp.pbounds[i];
   for (uint32_t i = tid; i < kRouteDir; i += kR2WG) s_pdir[i] = rp.pdir[i];
+  if (tid < (int)((kMaxParts + 1) / 32)) s_dead[tid] = rp.pdead[tid];
   for (uint32_t i = tid; i < P; i += kR2WG) s_state[i] = st_pack(kStNone, kStNone, 0, 2 * kChunk);
   // the first line of a partition: slot 0 of generation 1's open chunk
   const uint32_t nlp = !(p.flags & kDbgNoLines) ? min(P, kLineParts) : 0u;
@@ -671,7 +746,7 @@ __global__ __launch_bounds__(kR2WG, 1) void route2_kernel(RouteParams rp) {
       d.ta = __builtin_amdgcn_readfirstlane(d.ta);
       d.pad = __builtin_amdgcn_readfirstlane(d.pad);
     };
-    auto window = [&](RawRec& A, RawRec& B) {
+    auto front = [&](RawRec& A, RawRec& B, XF& X) {
       uni(d0);
       uni(d1);
       cur = __builtin_amdgcn_readfirstlane(cur);
@@ -787,95 +862,142 @@ __global__ __launch_bounds__(kR2WG, 1) void route2_kernel(RouteParams rp) {
         route_count<1>(gacc[1], s_gsums, s_gmins, s_gmaxs, valid, uint32_t(rec.dsrc >> 5) & 0x3fff, rec.w);
       }
       if (++gwin == kRouteDrain) {
-        racc_drain(gacc[0], s_gsums[0], lane);
-        racc_drain(gacc[1], s_gsums[1], lane);
+        racc_drain(gacc[0], s_gsums[0], s_gmins[0], s_gmaxs[0], lane);
+        racc_drain(gacc[1], s_gsums[1], s_gmins[1], s_gmaxs[1], lane);
         gwin = 0;
       }
       rt_stamp<TIMING>(rt, 2);
       // below the first key ht_lower_key finds no node: counted, not routed
-      const bool routed = valid && rec.addr >= first_start;
+      bool routed = valid && rec.addr >= first_start;
       const uint32_t q = routed ? route_partition_l(s_seg, s_segst, nseg, s_pb, s_pdir, rec.addr) : 0u;
+      // a partition whose entries all have free_date 0 matches only timestamp-0
+      // samples (RouteParams::pdead): the others are done (unmatched), not routed
+      routed = routed && (rec.ts == 0 || !((s_dead[q >> 5] >> (q & 31)) & 1u));
       if (TIMING) (void)__builtin_amdgcn_readfirstlane(__ballot(q != 0));  // (the search ends here)
       rt_stamp<TIMING>(rt, 3);
-      uint4 a = make_uint4(0, 0, 0, 0);
-      uint64_t pbq = 0;
-      if (routed) {
-        pbq = s_pb[q];
-        a = x_encode(rp.xl, pbq, rec.addr, rec.ts, rec.w, dw.pad, roff, dw.thread_rank(), acc_l);
-      }
+      X.a = make_uint4(0, 0, 0, 0);
+      X.q = q;
+      X.routed = routed;
+      if (routed) X.a = x_encode(rp.xl, s_pb[q], rec.addr, rec.ts, rec.w, dw.pad, roff, dw.thread_rank(), acc_l);
       rt_stamp<TIMING>(rt, 4);
-      // ---- a slot in q's open chunks: one LDS atomic on the partition's
-      // state (route2_claim).  No barrier: the waves run on their own streams.
-      uint64_t dst = ~0ull;  // rec16 slot, or ~0: no slot (not routed / overflow list)
-      uint32_t lid = 0;      // the slot's chunk line number (mod 4096): the lap that serves it
-      bool ovf = false;
-      const bool lined = routed && q < nlp;
-      // (the line word read beside the claim: a lap can only move on once this
-      // record's own line is written, so a lap that equals the record's line
-      // here still does after the claim)
-      LineWord lw = lined ? s_lw[q] : LineWord(0);
-      {
-        uint32_t waitg = 0;
-        bool todo = false;
-        if (routed) {
-          const Claim c = route2_settle(atomicAdd(&s_state[q], 1ull), q, s_state, s_taken, capl, rp.cmeta, c0);
-          dst = c.dst;
-          lid = c.lid;
-          ovf = c.ovf;
-          waitg = c.waitg;
-          todo = !c.ok;
+    };
+
+    // ---- the records of N windows (one; two in the NMG_R2PAIR A/B build,
+    // their LDS round trips issued together): a slot in each record's
+    // partition's open chunks (one LDS atomic on the partition's state,
+    // route2_settle), the line stage, the stores.  (Two records of one lane
+    // behave as the records of two lanes: every step below is correct for any
+    // number of records of one partition.)  No barrier: the waves run on
+    // their own streams.
+    auto back = [&](const auto& X) {
+      constexpr int N = (int)(sizeof(X) / sizeof(X[0]));
+      uint64_t dst[N];   // rec16 slot, or ~0: no slot (not routed / overflow list)
+      uint32_t lid[N];   // the slot's chunk line number (mod 4096): the lap that serves it
+      bool ovf[N], lined[N];
+      LineWord lw[N];
+      uint32_t waitg[N];
+      bool todo[N];
+      unsigned long long old[N];
+#pragma unroll
+      for (int r = 0; r < N; r++) {
+        dst[r] = ~0ull;
+        lid[r] = 0;
+        ovf[r] = false;
+        waitg[r] = 0;
+        todo[r] = false;
+        lined[r] = X[r].routed && X[r].q < nlp;
+        // (the line word read beside the claim: a lap can only move on once
+        // this record's own line is written, so a lap that equals the
+        // record's line here still does after the claim)
+        lw[r] = lined[r] ? s_lw[X[r].q] : LineWord(0);
+      }
+#pragma unroll
+      for (int r = 0; r < N; r++) old[r] = X[r].routed ? atomicAdd(&s_state[X[r].q], 1ull) : 0ull;
+#pragma unroll
+      for (int r = 0; r < N; r++) {
+        if (X[r].routed) {
+          const Claim c = route2_settle(old[r], X[r].q, s_state, s_taken, capl, rp.cmeta, c0);
+          dst[r] = c.dst;
+          lid[r] = c.lid;
+          ovf[r] = c.ovf;
+          waitg[r] = c.waitg;
+          todo[r] = !c.ok;
         }
-        bool spin = todo;
-        while (__ballot(todo)) {  // (rare) void claims
-          if (todo) {
-            if (!spin) {
-              const Claim c = route2_settle(atomicAdd(&s_state[q], 1ull), q, s_state, s_taken, capl, rp.cmeta, c0);
-              dst = c.dst;
-              lid = c.lid;
-              ovf = c.ovf;
-              waitg = c.waitg;
-              todo = !c.ok;
-              spin = todo;
+      }
+      {
+        bool spin[N];
+#pragma unroll
+        for (int r = 0; r < N; r++) spin[r] = todo[r];
+        while (__ballot(any_of(todo))) {  // (rare) void claims
+#pragma unroll
+          for (int r = 0; r < N; r++) {
+            if (!todo[r]) continue;
+            if (!spin[r]) {
+              const Claim c = route2_settle(atomicAdd(&s_state[X[r].q], 1ull), X[r].q, s_state, s_taken, capl, rp.cmeta, c0);
+              dst[r] = c.dst;
+              lid[r] = c.lid;
+              ovf[r] = c.ovf;
+              waitg[r] = c.waitg;
+              todo[r] = !c.ok;
+              spin[r] = todo[r];
             } else {
-              const uint64_t st = __hip_atomic_load(&s_state[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-              spin = st_gen(st) == waitg;
+              const uint64_t st = __hip_atomic_load(&s_state[X[r].q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+              spin[r] = st_gen(st) == waitg[r];
             }
           }
         }
       }
       rt_stamp<TIMING>(rt, 5);
       // ---- the line stage (see the comment above kR2WG)
-      bool staged = false;
-      if (__ballot(lined)) {
-        lid &= kLwLineMask;
-        const uint32_t j = (uint32_t)dst & 3u, S = lw_s(lw), ahead = (lid - S) & kLwLineMask;
-        // (a record of the overflow list has no slot but counts for its line)
-        const bool counts = lined && !(lw & kLwBroken) && ahead < ahead_max;
-        staged = counts && ahead == 0 && dst != ~0ull;
-        if (lined && !(lw & kLwBroken) && ahead >= ahead_max) atomicOr(&s_lw[q], kLwBroken);
-        if (staged) {
-          s_line[q * 4 + j] = a;
-          s_ldst[q] = (uint32_t)(dst >> 2);
-          // (the record before the count that may complete the line)
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-        } else if (counts && dst != ~0ull) {
-          rp.rec16[dst] = a;
+      bool staged[N], counts[N];
+#pragma unroll
+      for (int r = 0; r < N; r++) staged[r] = counts[r] = false;
+      if (__ballot(any_of(lined))) {
+        bool done[N];
+        uint32_t dmask[N];
+#pragma unroll
+        for (int r = 0; r < N; r++) {
+          lid[r] &= kLwLineMask;
+          const uint32_t j = (uint32_t)dst[r] & 3u, S = lw_s(lw[r]), ahead = (lid[r] - S) & kLwLineMask;
+          // (a record of the overflow list has no slot but counts for its line)
+          counts[r] = lined[r] && !(lw[r] & kLwBroken) && ahead < ahead_max;
+          staged[r] = counts[r] && ahead == 0 && dst[r] != ~0ull;
+          if (lined[r] && !(lw[r] & kLwBroken) && ahead >= ahead_max) atomicOr(&s_lw[X[r].q], kLwBroken);
+          if (staged[r]) {
+            s_line[X[r].q * 4 + j] = X[r].a;
+            s_ldst[X[r].q] = (uint32_t)(dst[r] >> 2);
+          } else if (counts[r] && dst[r] != ~0ull) {
+            if (!NMG_ABL_NOSCATTER) rp.rec16[dst[r]] = X[r].a;
+          }
         }
-        bool done = false;
-        uint32_t dmask = 0;
-        if (counts) {
-          const LineWord o =
-              atomicAdd(&s_lw[q], (kLwOne << (3 * (lid & (kLwAhead - 1)))) + (staged ? kLwOne << (kLwMaskShift + j) : LineWord(0)));
+        // (the staged records before the counts that may complete their lines)
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+        LineWord o[N];
+#pragma unroll
+        for (int r = 0; r < N; r++) {
+          o[r] = 0;
+          if (counts[r]) {
+            const uint32_t j = (uint32_t)dst[r] & 3u;
+            o[r] = atomicAdd(&s_lw[X[r].q], (kLwOne << (3 * (lid[r] & (kLwAhead - 1)))) +
+                                                (staged[r] ? kLwOne << (kLwMaskShift + j) : LineWord(0)));
+          }
+        }
+#pragma unroll
+        for (int r = 0; r < N; r++) {
           // the line's fourth record, the line being S (S may have reached it
           // since the read beside the claim)
-          done = lw_count(o, lid) == 3 && lw_s(o) == lid;
-          dmask = lw_mask(o) | (staged ? 1u << j : 0u);
+          done[r] = counts[r] && lw_count(o[r], lid[r]) == 3 && lw_s(o[r]) == lid[r];
+          dmask[r] = counts[r] ? lw_mask(o[r]) | (staged[r] ? 1u << ((uint32_t)dst[r] & 3u) : 0u) : 0u;
+          if (TIMING) rt.acc[8] += (uint64_t)__popcll(__ballot(counts[r] && !staged[r]));
         }
-        if (TIMING) rt.acc[8] += (uint64_t)__popcll(__ballot(counts && !staged));
-        const uint64_t dm = __ballot(done);
-        if (dm) {  // the staged slots of the completed lines written out: four lanes per line
-          if (done)
-            s_tab[wave][__popcll(dm & ((1ull << lane) - 1))] = make_uint2(q | (dmask << 11) | (lid << 16), (uint32_t)(dst >> 2));
+#pragma unroll
+        for (int r = 0; r < N; r++) {
+          const uint64_t dm = __ballot(done[r]);
+          if (!dm) continue;
+          // the staged slots of the completed lines written out: four lanes per line
+          if (done[r])
+            s_tab[wave][__popcll(dm & ((1ull << lane) - 1))] =
+                make_uint2(X[r].q | (dmask[r] << 11) | (lid[r] << 16), (uint32_t)(dst[r] >> 2));
           __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
           __builtin_amdgcn_wave_barrier();
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
@@ -892,34 +1014,43 @@ __global__ __launch_bounds__(kR2WG, 1) void route2_kernel(RouteParams rp) {
               if (k == 0) {  // S -> S + 1, past the lines already complete (all their records stored straight)
                 uint32_t l = t.x >> 16, m = tm;
                 while (true) {
-                  const LineWord o = atomicAdd(&s_lw[tq], (kLwOne << kLwSShift) - (LineWord(4) << (3 * (l & (kLwAhead - 1)))) -
-                                                            (LineWord(m) << kLwMaskShift));
+                  const LineWord ow = atomicAdd(&s_lw[tq], (kLwOne << kLwSShift) - (LineWord(4) << (3 * (l & (kLwAhead - 1)))) -
+                                                              (LineWord(m) << kLwMaskShift));
                   l = (l + 1) & kLwLineMask;
-                  if (lw_count(o, l) != 4) break;
+                  if (lw_count(ow, l) != 4) break;
                   m = 0;
                 }
               }
             }
           }
+          // (s_tab reused by the second record's lines: every lane read its entry above)
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
         }
       }
-      if (!lined) staged = false;
       rt_stamp<TIMING>(rt, 9);
-      // the records the line stage did not take: not lined, or given up
-      const bool straight = dst != ~0ull && !(lined && !(lw & kLwBroken) && ((lid - lw_s(lw)) & kLwLineMask) < ahead_max);
-      if (straight) rp.rec16[dst] = a;
-      if (TIMING) {  // (records staged / stored straight to their slot)
-        rt.acc[6] += (uint64_t)__popcll(__ballot(staged));
-        rt.acc[7] += (uint64_t)__popcll(__ballot(straight));
+#pragma unroll
+      for (int r = 0; r < N; r++) {
+        // the records the line stage did not take: not lined, or given up
+        const bool straight = dst[r] != ~0ull && !counts[r];
+        if (straight && !NMG_ABL_NOSCATTER) rp.rec16[dst[r]] = X[r].a;
+        if (TIMING) {  // (records staged / stored straight to their slot)
+          rt.acc[6] += (uint64_t)__popcll(__ballot(staged[r]));
+          rt.acc[7] += (uint64_t)__popcll(__ballot(straight));
+        }
       }
-      if (__ballot(ovf)) {  // (rare) a workgroup's pool outgrown: SAMPLEs shorter than 40 B
-        if (ovf) {
+      if (__ballot(any_of(ovf))) {  // (rare) a workgroup's pool outgrown: SAMPLEs shorter than 40 B
+#pragma unroll
+        for (int r = 0; r < N; r++) {
+          if (!ovf[r]) continue;
+          const uint64_t pbq = s_pb[X[r].q];
           const uint32_t o = atomicAdd(rp.ovf_cnt, 1u);
           if (o < rp.ovf_cap) {
-            rp.ovf16[o] = a;
+            rp.ovf16[o] = X[r].a;
             rp.ovfx[o] = pbq;
           } else {  // attributed at once
-            XRec xr = x_decode(rp.xl, pbq, a);
+            XRec xr = x_decode(rp.xl, pbq, X[r].a);
             if (xr.esc) x_resolve(xr, rp.xl, p.data, p.sbufs);
             direct_attribute(p, xr.addr, xr.ts, xr.w, xr.th, xr.acc, 0, rp.seq0 + xr.g(rp.xl), xr.off(rp.xl),
                              xr.g(rp.xl));
@@ -930,10 +1061,22 @@ __global__ __launch_bounds__(kR2WG, 1) void route2_kernel(RouteParams rp) {
       rt_stamp<TIMING>(rt, 10);
     };
 
+#if NMG_R2PAIR
+    XF X[2];  // (A/B: the back of two windows at a time -- measured slower, round 6)
     do {  // (d0: the wave's stream, uniform)
-      window(ra, rb);
-      window(rb, ra);
+      front(ra, rb, X[0]);
+      front(rb, ra, X[1]);
+      back(X);
     } while (d0.pad != kNoBuf);
+#else
+    XF X[1];
+    do {  // (d0: the wave's stream, uniform)
+      front(ra, rb, X[0]);
+      back(X);
+      front(rb, ra, X[0]);
+      back(X);
+    } while (d0.pad != kNoBuf);
+#endif
     if (TIMING && lane == 0) {
       unsigned long long* o = p.dbg + (uint64_t(blockIdx.x) * (kWG / 64) + tid / 64) * kRouteTimingWords;
       for (int k = 0; k < 9; k++) o[k] = rt.acc[k];
@@ -946,8 +1089,8 @@ __global__ __launch_bounds__(kR2WG, 1) void route2_kernel(RouteParams rp) {
       o[12] = rt.acc[10];
     }
   }
-  racc_drain(gacc[0], s_gsums[0], lane);
-  racc_drain(gacc[1], s_gsums[1], lane);
+  racc_drain(gacc[0], s_gsums[0], s_gmins[0], s_gmaxs[0], lane);
+  racc_drain(gacc[1], s_gsums[1], s_gmins[1], s_gmaxs[1], lane);
   lds_sync();
 #pragma unroll
   for (uint32_t a = 0; a < 2; a++) {  // the global mem_counters of both access types

@@ -138,6 +138,7 @@ int route_analyze_job(nmg_engine* h, const RouteJob& job) {
   rp.p = base;
   rp.pbounds = h->d_pbounds;
   rp.pdir = h->d_pdir;
+  rp.pdead = h->d_pdead;
   for (uint32_t k = 0; k < kRouteSegs; k++) rp.seg[k] = h->rsegs[k];
   rp.nseg = h->nrsegs;
   rp.nparts = h->nparts;

@@ -382,6 +382,15 @@ int build_partitions(nmg_engine* h, const uint64_t* keys, const uint32_t* entry_
   for (uint32_t q = 0; q < P; q++) pb[q] = keys[parts[q].k0];
   std::vector<uint16_t> rdir;
   route_segments(pb.data(), P, h->rsegs, &h->nrsegs, rdir);
+  // partitions whose entries all have free_date 0 (RouteParams::pdead): the
+  // route pass keeps only their timestamp-0 samples, the others cannot match
+  std::vector<uint32_t> dead((kMaxParts + 1) / 32, 0u);
+  for (uint32_t q = 0; q < P; q++) {
+    bool d = true;
+    for (uint32_t e = parts[q].e0; d && e < parts[q].e0 + parts[q].ne; e++) d = dev[e].free == 0;
+    if (d) dead[q >> 5] |= 1u << (q & 31);
+  }
+  HIP_TRY(h, alloc_copy(h, (void**)&h->d_pdead, dead.data(), dead.size() * 4));
   HIP_TRY(h, alloc_copy(h, (void**)&h->d_parts, parts.data(), parts.size() * sizeof(PartInfo)));
   HIP_TRY(h, alloc_copy(h, (void**)&h->d_pbounds, pb.data(), pb.size() * 8));
   HIP_TRY(h, alloc_copy(h, (void**)&h->d_pdir, rdir.data(), rdir.size() * 2));

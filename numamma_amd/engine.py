@@ -223,6 +223,13 @@ class Engine:
         self._c(lib.nmg_last_analyze_ms(self.h, C.byref(ms)))
         return ms.value
 
+    def merge_stats(self):
+        """(merge ms, counter bytes per GPU) of a multi-GPU handle's last
+        analysis (nmg_get_merge_stats); (0, 0) for a single-GPU engine."""
+        ms, nb = C.c_float(), C.c_uint64()
+        self._c(lib.nmg_get_merge_stats(self.h, C.byref(ms), C.byref(nb)))
+        return ms.value, nb.value
+
     # ------------------------------------------------------------------
     def global_counters(self):
         out = (_lib.nmg_mem_counters * 2)()

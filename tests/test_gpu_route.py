@@ -167,3 +167,45 @@ def test_route_escaped_records_bit_exact(tmp_path):
         _same(os.path.join(d, "oracle_raw.bin"), raw)
         _same(os.path.join(d, "oracle_stdout.txt"), os.path.join(d, f"engine_{tag}_stdout.txt"))
         _same_dirs(odir, edir)
+
+
+def test_route_settled_partitions_keep_timestamp_zero(tmp_path):
+    """Partitions whose entries all have free_date 0 (the [stack] range after
+    warn_non_freed_buffers, quirk Q4; RouteParams::pdead) are matched only by
+    timestamp-0 samples (alloc <= ts <= free, mem_analyzer.c:148-149): the route
+    pass drops their other samples and keeps those.  Here 20 % of the [stack]
+    samples carry timestamp 0 and must match the stack entry (a call site of
+    their own, page cells in the sparse table), and a cluster of objects
+    allocated at 0 and never freed (free_date 0) forms partitions of its own,
+    hit by timestamp-0 samples too."""
+    from numamma_amd.replay import RECORD_DTYPE, STACK_BASE
+
+    d = str(tmp_path)
+    rp = generate(SynthConfig(nb_samples=300_000, nb_intervals=30_000, heap_clusters=3, cluster_gap=1 << 36,
+                              seed=81))
+    t = rp.table
+    # the highest heap cluster's objects: allocated at 0, never freed
+    keys = np.asarray(t.keys, dtype=np.uint64)
+    heap = keys[keys < np.uint64(STACK_BASE)]
+    hi = heap[-1] - np.uint64(1 << 35)
+    ent = t.entries
+    live = (ent["buffer_addr"] >= hi) & (ent["buffer_addr"] < np.uint64(STACK_BASE)) & (ent["alloc_date"] > 0)
+    ent["alloc_date"][live] = 0
+    ent["free_date"][live] = 0
+    assert live.sum() > 3000  # (several partitions of them)
+    rng = np.random.default_rng(81)
+    nz = 0
+    for b in rp.buffers:
+        rec = b.ring.view(RECORD_DTYPE)  # pure 40 B SAMPLE streams
+        sel = ((rec["addr"] >= np.uint64(STACK_BASE)) | (rec["addr"] >= hi)) & (rng.random(rec.shape[0]) < 0.2)
+        rec["timestamp"][sel] = 0
+        nz += int(sel.sum())
+    assert nz > 1000
+    path, odir = _oracle(rp, d)
+    raw = RawResults.read(os.path.join(d, "oracle_raw.bin"))
+    assert raw.nb_found > 0
+    for tag, flags in (("route", 0), ("tiny", TINY_POOL), ("single", _lib.NMG_F_SINGLE_PASS)):
+        edir, eraw = _engine(path, d, _lib.NMG_F_DEFAULT | flags, tag)
+        _same(os.path.join(d, "oracle_raw.bin"), eraw)
+        _same(os.path.join(d, "oracle_stdout.txt"), os.path.join(d, f"engine_{tag}_stdout.txt"))
+        _same_dirs(odir, edir)

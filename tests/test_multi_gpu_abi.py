@@ -57,7 +57,17 @@ def test_multi_gpu_handle_bit_exact(tmp_path, nb_gpus, cfg):
     eng.analyze()
     eng.synchronize()
     _check(d, eng, rp, "second")
+    # the merge of that analysis: timed on the root device, every counter array's bytes per worker
+    from numamma_amd import _lib
+
+    ms, payload = eng.merge_stats()
+    assert ms > 0.0
+    assert payload == 8 * sum(eng.array_size(a) for a in (_lib.NMG_ARR_SUM64, _lib.NMG_ARR_MIN64,
+                                                         _lib.NMG_ARR_MAX64)) + 4 * eng.array_size(_lib.NMG_ARR_HIST32)
     eng.close()
+    one = Engine(nb_threads=rp.nb_threads)  # a single-GPU engine merges nothing
+    assert one.merge_stats() == (0.0, 0)
+    one.close()
 
 
 def test_multi_gpu_rejects_device_buffers():
