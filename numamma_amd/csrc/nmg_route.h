@@ -82,10 +82,14 @@ constexpr uint32_t kOldLds = 512;
 constexpr uint32_t kPnOldLds = 1u << 13, kPnOldShift = 16;
 constexpr uint32_t kPartEntries = 1536;    // entries per partition (LDS object counters)
 constexpr uint32_t kPartCells = 28672;     // u16 page cells per partition: nb_threads x cell span
-constexpr uint32_t kItemChunks = 1023;     // chunks per work item: < 2^16 records, so u16 page cells
-                                           // and the packed object counters cannot overflow
-static_assert(kItemChunks * kChunk < 65536u, "u16 page cells per item");
+#ifndef NMG_ITEM_CHUNKS
+#define NMG_ITEM_CHUNKS 1023
+#endif
+constexpr uint32_t kItemChunks = NMG_ITEM_CHUNKS;  // chunks per work item (one workgroup): the packed object
+                                                   // counters cannot overflow; past 2^16 records a u16 page
+                                                   // cell can, and the local pass carries it (kPageCarry)
 static_assert((uint64_t)kItemChunks * kChunk < (1ull << (64 - kPackShift)), "packed count per item");
+constexpr bool kPageCarry = (uint64_t)kItemChunks * kChunk >= 65536u;
 constexpr uint32_t kChunkIdBits = 25;      // route pass LDS: chunk id << 7 | fill
 constexpr uint32_t kNoChunk = 0xffffffffu;
 constexpr uint32_t kFoundLds = 16384;      // found_kernel: per-buffer LDS counters of one workgroup

@@ -26,6 +26,9 @@
 #ifndef NMG_R2LDSMM  // (1: the shipped way; 0: per-lane register minima / maxima, measured no faster)
 #define NMG_R2LDSMM 1
 #endif
+#ifndef NMG_R2COAL  // route pass: whole-line record loads, dealt to the lanes through LDS (A/B)
+#define NMG_R2COAL 0
+#endif
 #ifndef NMG_ABL_NOSCATTER  // (ablation only, results wrong: no record stored outside the line stage)
 #define NMG_ABL_NOSCATTER 0
 #endif
@@ -365,7 +368,7 @@ __device__ __forceinline__ void rt_stamp(RTimer& t, int i) {
 // a global load.  Ranges longer than kDescLds read the rest from global
 // memory.  In the analysis-order schedule the count slot (.pad) is the
 // index and seq = seq0 + index.
-constexpr uint32_t kDescLds = 512;
+constexpr uint32_t kDescLds = NMG_R2COAL ? 160 : 512;
 
 __device__ __forceinline__ RDesc route_desc(const RouteParams& rp, const uint4* s_desc, uint32_t r0, uint32_t i) {
   RDesc d;
@@ -427,7 +430,7 @@ __device__ __forceinline__ RDesc route_desc(const RouteParams& rp, const uint4* 
 // route2_kernel's workgroup: 12 waves (three per SIMD)
 constexpr uint32_t kR2WG = NMG_R2WG;
 // line stage: partitions q < kLineParts have an LDS line
-constexpr uint32_t kLineParts = 1280;
+constexpr uint32_t kLineParts = NMG_R2COAL ? 1152 : 1280;
 // line word (u64): line l's count (3 bits) at 3 * (l mod 8), staged slots
 // (4) at 24, given up at 28, S at 52
 typedef unsigned long long LineWord;
@@ -476,6 +479,51 @@ __device__ __forceinline__ void wload(const uint8_t* data, uint64_t off, uint32_
   r.y = make_uint4(y[0], y[1], y[2], y[3]);
   r.z = make_uint2(z[0], z[1]);
 }
+
+// NMG_R2COAL: the wave window's bytes as three whole-line loads (lane l:
+// bytes 16 l, 1024 + 16 l, 2048 + 16 l of the window; the third only for
+// lanes < 32), dealt to the lanes' 40 B records through the wave's LDS stage
+struct CRec {
+  uint4 a, b, c;
+};
+__device__ __forceinline__ void cload(const uint8_t* data, uint64_t off, uint32_t len, uint32_t c, int lane,
+                                      CRec& r) {
+  off = u64of(__builtin_amdgcn_readfirstlane((uint32_t)off), __builtin_amdgcn_readfirstlane((uint32_t)(off >> 32)));
+  len = __builtin_amdgcn_readfirstlane(len);
+  c = __builtin_amdgcn_readfirstlane(c);
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(data + off), (short)0, (int)len, 0x00020000);
+  const uint32_t pos = c + uint32_t(lane) * 16u;
+  const auto x = __builtin_amdgcn_raw_buffer_load_b128(rs, pos, 0, 0);
+  const auto y = __builtin_amdgcn_raw_buffer_load_b128(rs, pos + 1024u, 0, 0);
+  const auto z = __builtin_amdgcn_raw_buffer_load_b128(rs, pos + 2048u, 0, 0);
+  r.a = make_uint4(x[0], x[1], x[2], x[3]);
+  r.b = make_uint4(y[0], y[1], y[2], y[3]);
+  r.c = make_uint4(z[0], z[1], z[2], z[3]);
+}
+__device__ __forceinline__ Rec stage_rec(uint4* st, const CRec& r, int lane) {
+  st[lane] = r.a;
+  st[64 + lane] = r.b;
+  if (lane < 32) st[128 + lane] = r.c;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+  const uint64_t* q = reinterpret_cast<const uint64_t*>(st) + 5 * lane;
+  Rec d;
+  d.hdr = q[0];
+  d.ts = q[1];
+  d.addr = q[2];
+  d.w = q[3];
+  d.dsrc = q[4];
+  return d;
+}
+#if NMG_R2COAL
+typedef CRec WRec;
+#define NMG_WLOAD(d, o, l, c, ln, r) cload(d, o, l, c, ln, r)
+#else
+typedef RawRec WRec;
+#define NMG_WLOAD(d, o, l, c, ln, r) wload(d, o, l, c, ln, r)
+#endif
 
 // route_partition with the segment table in LDS instead of kernel arguments
 // (which the compiler would keep in scalar registers): the segment is the
@@ -622,7 +670,15 @@ __global__ __launch_bounds__(kR2WG, 1) void route2_kernel(RouteParams rp) {
   __shared__ uint32_t s_dead[(kMaxParts + 1) / 32];
   __shared__ unsigned long long s_state[kMaxParts + 1];  // open chunk << 32 | slots claimed in it
   __shared__ uint4 s_desc[kDescLds];
+#if NMG_R2COAL
+  // per wave, used in turn: the window's bytes (front start), the slow path's
+  // SAMPLE offsets, the line write-out table (back) -- one wave's LDS ops run in order
+  __shared__ uint4 s_stage[kWaves][kWaveWinBytes / 16];
+  uint32_t(*s_wlist)[kWaveWinBytes / 4] = reinterpret_cast<uint32_t(*)[kWaveWinBytes / 4]>(s_stage);
+  uint2(*s_tab)[kWaveWinBytes / 8] = reinterpret_cast<uint2(*)[kWaveWinBytes / 8]>(s_stage);
+#else
   __shared__ uint32_t s_wlist[kWaves][64];  // slow path: the wave window's SAMPLE offsets
+#endif
   __shared__ uint32_t s_taken, s_bnext;
   __shared__ unsigned long long s_gsums[2][kGlobalSums], s_gmins[2][18], s_gmaxs[2][18];
   __shared__ SegL s_seg[kRouteSegs];
@@ -632,7 +688,9 @@ __global__ __launch_bounds__(kR2WG, 1) void route2_kernel(RouteParams rp) {
   __shared__ uint4 s_line[kLineParts * 4];
   __shared__ LineWord s_lw[kLineParts];
   __shared__ uint32_t s_ldst[kLineParts];
+#if !NMG_R2COAL
   __shared__ uint2 s_tab[kWaves][64];
+#endif
 
   Params& p = rp.p;
   const int tid = threadIdx.x;
@@ -723,10 +781,10 @@ __global__ __launch_bounds__(kR2WG, 1) void route2_kernel(RouteParams rp) {
         elen = d1.len;
       }
     };
-    RawRec ra, rb;
-    wload(p.data, d0.offset, d0.len, 0, lane, ra);
+    WRec ra, rb;
+    NMG_WLOAD(p.data, d0.offset, d0.len, 0, lane, ra);
     predict();
-    wload(p.data, eoff, elen, pcur, lane, rb);
+    NMG_WLOAD(p.data, eoff, elen, pcur, lane, rb);
 
     RTimer rt;  // (TIMING) per-wave phase cycles
 #pragma unroll
@@ -746,7 +804,7 @@ __global__ __launch_bounds__(kR2WG, 1) void route2_kernel(RouteParams rp) {
       d.ta = __builtin_amdgcn_readfirstlane(d.ta);
       d.pad = __builtin_amdgcn_readfirstlane(d.pad);
     };
-    auto front = [&](RawRec& A, RawRec& B, XF& X) {
+    auto front = [&](WRec& A, WRec& B, XF& X) {
       uni(d0);
       uni(d1);
       cur = __builtin_amdgcn_readfirstlane(cur);
@@ -759,7 +817,11 @@ __global__ __launch_bounds__(kR2WG, 1) void route2_kernel(RouteParams rp) {
         nwin++;
       }
       rt_stamp<TIMING>(rt, 0);
+#if NMG_R2COAL
+      Rec rec = stage_rec(s_stage[wave], A, lane);
+#else
       Rec rec = decode_rec(A, pos);
+#endif
       const bool bad = cand && (uint64_t(pos) + kRecBytes > dw.len || (rec.hdr >> 48) != kRecBytes);
       bool valid;
       uint32_t roff = pos, ncur;
@@ -845,11 +907,11 @@ __global__ __launch_bounds__(kR2WG, 1) void route2_kernel(RouteParams rp) {
       // ---- the next window's loads again if it is not where B was loaded
       // (after a slow-path window), then the loads of the window after it
       if (d0.pad != pidx || (d0.pad != kNoBuf && cur != pcur)) {
-        wload(p.data, d0.offset, d0.len, cur, lane, B);
+        NMG_WLOAD(p.data, d0.offset, d0.len, cur, lane, B);
         vm_drain();  // (rare: keeps the waits on the common path exact)
       }
       predict();
-      wload(p.data, eoff, elen, pcur, lane, A);
+      NMG_WLOAD(p.data, eoff, elen, pcur, lane, A);
 
       // ---- this window's records: update_counters(global_counters, sample)
       // (mem_sampling.c:882: every SAMPLE, matched or not), partition, chunk
@@ -1291,6 +1353,11 @@ __global__ __launch_bounds__(kWG) void scatter_kernel(ScatterParams r) {
 // local pass: workgroup size and chunks per interleaved group (a wave holds
 // two groups: one being attributed, the other's records in flight)
 constexpr uint32_t kLWG = 1024;
+// u16 page cells of items past 2^16 records (kPageCarry): at kCarryAt a
+// cell moves kCarryMove of its count to global memory (at most kLWG * 2
+// adds are in flight, far fewer than 2^16 - kCarryAt)
+constexpr uint32_t kCarryAt = 0xf000u, kCarryMove = 0x8000u;
+static_assert(2 * kLWG < 0x10000u - kCarryAt && kCarryMove < kCarryAt, "page cell carry margin");
 constexpr int kLC = 2;  // (the timing wait below counts on it)
 
 // a load served by L2, never by this CU's L1 (global_load ... sc1)
@@ -1337,7 +1404,7 @@ __global__ __launch_bounds__(kLWG, 1) void local_kernel(LocalParams lp) {
   __shared__ unsigned long long s_first[kPartEntries];
   __shared__ uint32_t s_pg[kPartCells / 2];
   __shared__ uint32_t s_clist[kItemChunks];  // the item's chunk list entries
-  __shared__ uint32_t s_item, s_cnext, s_nfound, s_big, s_took;
+  __shared__ uint32_t s_item, s_cnext, s_nfound, s_big, s_took, s_carry;
   __shared__ uint4 s_nx[4];  // the next item's work item and PartInfo (take_next)
 
   Params& p = lp.p;
@@ -1395,14 +1462,15 @@ __global__ __launch_bounds__(kLWG, 1) void local_kernel(LocalParams lp) {
     const uint32_t dshift = __builtin_amdgcn_readfirstlane(pi.dshift);
     {
       // the partition's tables and the item's chunk list: at most one element
-      // of each per thread, every load in flight before the first LDS store
-      static_assert(kPartKeys <= kLWG && kPartDir == kLWG && kOldLds <= kLWG && kItemChunks <= kLWG,
-                    "one table element per thread");
+      // of each table per thread (kClPer of the list), every load in flight
+      // before the first LDS store
+      static_assert(kPartKeys <= kLWG && kPartDir == kLWG && kOldLds <= kLWG, "one table element per thread");
+      constexpr uint32_t kClPer = (kItemChunks + kLWG - 1) / kLWG;
       const uint32_t nk = pi.nk, nold = min(pi.ne - nk, kOldLds), ncl = item.z - item.y;
       uint64_t key = 0;
       uint4 pn = make_uint4(0, 0, 0, 0), od = pn;
       uint2 inf = make_uint2(0, 0);
-      uint32_t oi = 0, cl = 0;
+      uint32_t oi = 0, cl[kClPer];
       if (tid < nk) {
         key = lp.pe_keys[uint64_t(q) * kPartSlots + tid];
         pn = lp.pe_pnode[uint64_t(q) * kPartSlots + tid];
@@ -1413,7 +1481,8 @@ __global__ __launch_bounds__(kLWG, 1) void local_kernel(LocalParams lp) {
         od = lp.pe_old[uint64_t(q) * kOldLds + tid];
         oi = lp.pe_oinf[uint64_t(q) * kOldLds + tid];
       }
-      if (tid < ncl) cl = lp.clist[item.y + tid];
+#pragma unroll
+      for (uint32_t u = 0; u < kClPer; u++) cl[u] = tid + u * kLWG < ncl ? lp.clist[item.y + tid + u * kLWG] : 0u;
       if (tid < nk) {
         s_keys[tid] = key;
         s_pn[tid] = pn;
@@ -1424,7 +1493,9 @@ __global__ __launch_bounds__(kLWG, 1) void local_kernel(LocalParams lp) {
         s_old[tid] = od;
         s_oinf[tid] = oi;
       }
-      if (tid < ncl) s_clist[tid] = cl;
+#pragma unroll
+      for (uint32_t u = 0; u < kClPer; u++)
+        if (tid + u * kLWG < ncl) s_clist[tid + u * kLWG] = cl[u];
     }
     if (tid == 0) {
       s_cnext = 0;
@@ -1433,7 +1504,7 @@ __global__ __launch_bounds__(kLWG, 1) void local_kernel(LocalParams lp) {
     const uint32_t ncell = (pages && pi.pages_lds) ? T * pi.span : 0u;
     const bool excl = item.w != 0 && !(p.flags & kDbgLocalAtomics);  // no other workgroup writes this partition's
                                                                      // counters
-    if (tid == 0) s_big = 0;
+    if (tid == 0) s_big = s_carry = 0;
     lds_sync();
     const uint64_t k0key = u64of(__builtin_amdgcn_readfirstlane((uint32_t)s_keys[0]),
                                  __builtin_amdgcn_readfirstlane((uint32_t)(s_keys[0] >> 32)));
@@ -1677,9 +1748,10 @@ __global__ __launch_bounds__(kLWG, 1) void local_kernel(LocalParams lp) {
       rt_stamp<TIMING>(rt, 3);
       const bool noobj = (p.flags & kDbgLocalNoObj) != 0;
 #pragma unroll
-      for (int j = 0; j < kLC; j++)
-        if (erel[j] >= 0 && !noobj && w[j] < kLaneMaxWeight)
-          atomicAdd(&s_owt[xr[j].acc][erel[j]], (1ull << kPackShift) | w[j]);
+      for (int j = 0; j < kLC; j++) {
+        bool ok = erel[j] >= 0 && !noobj && w[j] < kLaneMaxWeight;
+        if (ok) atomicAdd(&s_owt[xr[j].acc][erel[j]], (1ull << kPackShift) | w[j]);
+      }
       bool anybig = false;
 #pragma unroll
       for (int j = 0; j < kLC; j++) anybig |= erel[j] >= 0 && w[j] >= kLaneMaxWeight;
@@ -1710,15 +1782,44 @@ __global__ __launch_bounds__(kLWG, 1) void local_kernel(LocalParams lp) {
       if (pages && !(p.flags & kDbgLocalNoPage)) {
         // ma_get_block: page_no = (int)((addr - buffer_addr) / 4096) (mem_analyzer.c:530-531)
         uint32_t page[kLC];
-        bool glob = false;
+        bool glob = false, carry[kLC];
 #pragma unroll
         for (int j = 0; j < kLC; j++) {
           page[j] = uint32_t(int(pofs[j] / kPageSize));
+          carry[j] = false;
           if (erel[j] >= 0 && hrel[j] != kEmpty32 && ncell) {
-            const uint32_t c = xr[j].th * pi.span + hrel[j] + page[j];
-            atomicAdd(&s_pg[c >> 1], 1u << (16 * (c & 1)));
+            const uint32_t c = xr[j].th * pi.span + hrel[j] + page[j], sh = 16 * (c & 1);
+            if (kPageCarry) {  // (an item past 2^16 records: a cell could wrap its u16)
+              const uint32_t o = atomicAdd(&s_pg[c >> 1], 1u << sh);
+              carry[j] = ((o >> sh) & 0xffffu) == kCarryAt - 1;
+            } else {
+              atomicAdd(&s_pg[c >> 1], 1u << sh);
+            }
           }
           glob |= erel[j] >= 0 && (hrel[j] == kEmpty32 || !ncell);
+        }
+        if (kPageCarry) {
+          bool anyc = false;
+#pragma unroll
+          for (int j = 0; j < kLC; j++) anyc |= carry[j];
+          // (rare) a cell reached kCarryAt: kCarryMove of its count go to the
+          // histogram in global memory.  Exactly one add brings a cell from
+          // kCarryAt - 1 to kCarryAt (only adds raise it, and the move takes it
+          // far below), and fewer adds than 2^16 - kCarryAt can be in flight
+          // in the workgroup before the move lands: no u16 wraps, no borrow
+          // crosses into the neighbouring cell.
+          if (__ballot(anyc)) {
+            if (lane == 0) s_carry = 1;  // (the flush then adds to the cells instead of storing them)
+#pragma unroll
+            for (int j = 0; j < kLC; j++) {
+              if (!carry[j]) continue;
+              const uint32_t rel = hrel[j] + page[j], c = xr[j].th * pi.span + rel;
+              atomicSub(&s_pg[c >> 1], kCarryMove << (16 * (c & 1)));
+              const uint64_t cell = (PACKED && pi.cmap != ~0u) ? (uint64_t)lp.pe_cmap[pi.cmap + rel] : pi.cb + rel;
+              atomicAdd(p.hist + uint64_t(xr[j].th) * p.hist_cells + cell, kCarryMove);
+            }
+            vm_drain();
+          }
         }
         if (__ballot(glob)) {  // (rare) cells in global memory: dense or sparse
 #pragma unroll
@@ -1770,6 +1871,7 @@ __global__ __launch_bounds__(kLWG, 1) void local_kernel(LocalParams lp) {
     // first ordinals from ~0, page cells from zero
     const bool clean = excl && lp.fresh && __builtin_amdgcn_readfirstlane(lp.ctl[3]) == 0;
     const bool clean_obj = clean && __builtin_amdgcn_readfirstlane(s_big) == 0;
+    const bool clean_pg = clean && __builtin_amdgcn_readfirstlane(s_carry) == 0;
     // the item's counters to global memory, consecutive lanes on consecutive
     // words, each LDS word zeroed for the next item as it is read; the only
     // item of its partition adds with plain loads and stores (no other
@@ -1829,7 +1931,7 @@ __global__ __launch_bounds__(kLWG, 1) void local_kernel(LocalParams lp) {
             uint64_t cell = pi.cb + rel;
             if (cmap != ~0u) cell = cnt[u][h] ? lp.pe_cmap[cmap + rel] : 0u;  // (online: packed cells)
             pc[u][h] = p.hist + uint64_t(th) * p.hist_cells + cell;
-            old[u][h] = (excl && !clean && cnt[u][h]) ? l2_load(pc[u][h]) : 0u;
+            old[u][h] = (excl && !clean_pg && cnt[u][h]) ? l2_load(pc[u][h]) : 0u;
           }
         }
 #pragma unroll

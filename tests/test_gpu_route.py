@@ -209,3 +209,23 @@ def test_route_settled_partitions_keep_timestamp_zero(tmp_path):
         _same(os.path.join(d, "oracle_raw.bin"), eraw)
         _same(os.path.join(d, "oracle_stdout.txt"), os.path.join(d, f"engine_{tag}_stdout.txt"))
         _same_dirs(odir, edir)
+
+
+def test_route_hot_page_cell_past_u16(tmp_path):
+    """One cell taking most of an item's records: a Zipf(3) hot object of one
+    page, one thread, so a work item of the local pass puts far more than
+    2^16 samples on one u16 LDS page cell when items hold more than 2^16
+    records (kPageCarry: the cell moves kCarryMove to global memory at
+    kCarryAt); the counts must still equal the oracle's, and the hot cell
+    must be past 2^16."""
+    d = str(tmp_path)
+    cfg = SynthConfig(nb_samples=600_000, nb_intervals=3_000, nb_threads=1, size_min=64, size_max=4000, zipf_s=3.0,
+                      frac_gap=0.0, frac_stack=0.0, frac_global=0.0, reuse_frac=0.0, realloc_frac=0.0, seed=82)
+    path, odir = _oracle(generate(cfg), d)
+    raw = RawResults.read(os.path.join(d, "oracle_raw.bin"))
+    assert int(raw.cells[:, 3].max()) > 3 * 65536
+    for tag, flags in (("route", 0), ("nolines", NO_LINES)):
+        edir, eraw = _engine(path, d, _lib.NMG_F_DEFAULT | flags, tag)
+        _same(os.path.join(d, "oracle_raw.bin"), eraw)
+        _same(os.path.join(d, "oracle_stdout.txt"), os.path.join(d, f"engine_{tag}_stdout.txt"))
+        _same_dirs(odir, edir)
