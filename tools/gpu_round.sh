@@ -63,6 +63,16 @@ for s in $STAGES; do
         --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 5 --warmup 1 > $OUT/bench2g_$TAG.json 2> $OUT/bench2g_$TAG.err \
         || { echo "bench2g failed"; tail -40 $OUT/bench2g_$TAG.err; exit 1; }
       cat $OUT/bench2g_$TAG.json ;;
+    handle)
+      # the one-process multi-GPU path on this box: one engine handle over 1 GPU, and 2
+      # workers sharing GPU 0 (device merges): each line carries its merge split
+      echo "== bench --handle (1 GPU; 2 workers on GPU 0)"
+      timeout -k 10 600 python bench.py --handle --steps 10 --warmup 2 --no-cpu-baseline > $OUT/bench_handle1_$TAG.json 2> $OUT/bench_handle1_$TAG.err \
+        || { echo "bench handle1 failed"; tail -30 $OUT/bench_handle1_$TAG.err; exit 1; }
+      cat $OUT/bench_handle1_$TAG.json
+      timeout -k 10 600 env NMG_BENCH_SAME_GPU=1 python bench.py --handle --gpus 2 --steps 10 --warmup 2 --no-cpu-baseline > $OUT/bench_handle2_$TAG.json 2> $OUT/bench_handle2_$TAG.err \
+        || { echo "bench handle2 failed"; tail -30 $OUT/bench_handle2_$TAG.err; exit 1; }
+      cat $OUT/bench_handle2_$TAG.json ;;
     pmcsq)
       echo "== rocprofv3 -L + SQ counter passes"
       timeout -k 10 120 rocprofv3 -L > $OUT/counters_list.txt 2>&1 || true
