@@ -29,6 +29,12 @@
 #ifndef NMG_R2COAL  // route pass: whole-line record loads, dealt to the lanes through LDS (A/B)
 #define NMG_R2COAL 0
 #endif
+#ifndef NMG_R2ONESTORE  // route pass: one store instruction for every record stored alone (shipped: 1)
+#define NMG_R2ONESTORE 1
+#endif
+#ifndef NMG_LOCAL_ONEMATCH  // local pass: one store instruction for a chunk group's match bits (shipped: 1)
+#define NMG_LOCAL_ONEMATCH 1
+#endif
 #ifndef NMG_ABL_NOSCATTER  // (ablation only, results wrong: no record stored outside the line stage)
 #define NMG_ABL_NOSCATTER 0
 #endif
@@ -1028,7 +1034,7 @@ __global__ __launch_bounds__(kR2WG, 1) void route2_kernel(RouteParams rp) {
           if (staged[r]) {
             s_line[X[r].q * 4 + j] = X[r].a;
             s_ldst[X[r].q] = (uint32_t)(dst[r] >> 2);
-          } else if (counts[r] && dst[r] != ~0ull) {
+          } else if (counts[r] && dst[r] != ~0ull && !NMG_R2ONESTORE) {
             if (!NMG_ABL_NOSCATTER) rp.rec16[dst[r]] = X[r].a;
           }
         }
@@ -1096,7 +1102,11 @@ __global__ __launch_bounds__(kR2WG, 1) void route2_kernel(RouteParams rp) {
       for (int r = 0; r < N; r++) {
         // the records the line stage did not take: not lined, or given up
         const bool straight = dst[r] != ~0ull && !counts[r];
-        if (straight && !NMG_ABL_NOSCATTER) rp.rec16[dst[r]] = X[r].a;
+        // (NMG_R2ONESTORE: the records counted for a line ahead of the staged one
+        // stored here too -- one store instruction for every record stored
+        // alone; nothing reads the slots before the local pass)
+        const bool alone = straight || (NMG_R2ONESTORE && counts[r] && !staged[r] && dst[r] != ~0ull);
+        if (alone && !NMG_ABL_NOSCATTER) rp.rec16[dst[r]] = X[r].a;
         if (TIMING) {  // (records staged / stored straight to their slot)
           rt.acc[6] += (uint64_t)__popcll(__ballot(staged[r]));
           rt.acc[7] += (uint64_t)__popcll(__ballot(straight));
@@ -1739,12 +1749,27 @@ __global__ __launch_bounds__(kLWG, 1) void local_kernel(LocalParams lp) {
       }
       // the chunks' match bits (per-buffer counts, found_kernel) straight to
       // global memory, and this wave's matched total
+#if NMG_LOCAL_ONEMATCH  // (lane j stores chunk j's bits: one store instruction for the group)
+      {
+        uint64_t mine = 0;
+        uint32_t ml = 0;
+#pragma unroll
+        for (int j = 0; j < kLC; j++) {
+          const uint64_t fm = __ballot(erel[j] >= 0);
+          nfound += (uint32_t)__popcll(fm);
+          mine = lane == j ? fm : mine;
+          ml = lane == j ? li[j] : ml;
+        }
+        if (lane < kLC && ml < nl) lp.cmatch[s_clist[ml] & ((1u << kChunkIdBits) - 1)] = mine;
+      }
+#else
 #pragma unroll
       for (int j = 0; j < kLC; j++) {
         const uint64_t fm = __ballot(erel[j] >= 0);
         nfound += (uint32_t)__popcll(fm);
         if (lane == 0 && li[j] < nl) lp.cmatch[s_clist[li[j]] & ((1u << kChunkIdBits) - 1)] = fm;
       }
+#endif
       rt_stamp<TIMING>(rt, 3);
       const bool noobj = (p.flags & kDbgLocalNoObj) != 0;
 #pragma unroll
