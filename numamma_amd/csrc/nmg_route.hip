@@ -35,12 +35,6 @@
 #ifndef NMG_LOCAL_ONEMATCH  // local pass: one store instruction for a chunk group's match bits (shipped: 1)
 #define NMG_LOCAL_ONEMATCH 1
 #endif
-#ifndef NMG_R2CMLIST  // route pass: chunk tags queued per wave, stored 40+ at a time (A/B)
-#define NMG_R2CMLIST 0
-#endif
-#ifndef NMG_R2MERGEOUT  // route pass: records stored alone share the line write-out's store (A/B)
-#define NMG_R2MERGEOUT 0
-#endif
 #ifndef NMG_ABL_NOSCATTER  // (ablation only, results wrong: no record stored outside the line stage)
 #define NMG_ABL_NOSCATTER 0
 #endif
@@ -624,41 +618,8 @@ struct Claim {
   uint32_t lid, waitg;
   bool ovf, ok;
 };
-// A chunk's tag (cmeta: partition | fill << 24), written when it is opened:
-// NMG_R2CMLIST queues it in the wave's LDS list (pool index << 11 |
-// partition), which the wave stores kCmList at a time -- one store
-// instruction instead of one per window that opens a chunk; a full list
-// stores the tag at once.
-constexpr uint32_t kCmList = 64, kCmFlush = 40;
-struct CmList {
-  uint32_t* l;  // the wave's list (kCmList)
-  uint32_t* n;  // its length
-};
-__device__ __forceinline__ void cm_put(uint32_t n, uint32_t q, const CmList& cl, uint32_t* cmeta, uint32_t c0) {
-  if (NMG_R2CMLIST) {
-    const uint32_t i = atomicAdd(cl.n, 1u);
-    if (i < kCmList) {
-      cl.l[i] = (n << 11) | q;
-      return;
-    }
-  }
-  cmeta[c0 + n] = q | (kChunk << 24);
-}
-// the wave's queued tags to cmeta (every lane of the wave calls this)
-__device__ __forceinline__ void cm_flush(const CmList& cl, uint32_t* cmeta, uint32_t c0, int lane, uint32_t at) {
-  const uint32_t n = __builtin_amdgcn_readfirstlane(*cl.n);
-  if (n < at) return;
-  if ((uint32_t)lane < min(n, kCmList)) {
-    const uint32_t v = cl.l[lane];
-    cmeta[c0 + (v >> 11)] = (v & 2047u) | (kChunk << 24);
-  }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
-  if (lane == 0) *cl.n = 0;
-}
 __device__ __forceinline__ Claim route2_settle(uint64_t old, uint32_t q, unsigned long long* s_state, uint32_t& taken,
-                                               uint32_t capl, uint32_t* cmeta, uint32_t c0, const CmList& cl) {
+                                               uint32_t capl, uint32_t* cmeta, uint32_t c0) {
   Claim r;
   r.dst = ~0ull;
   r.lid = 0;
@@ -673,14 +634,14 @@ __device__ __forceinline__ Claim route2_settle(uint64_t old, uint32_t q, unsigne
     r.lid = ((g << 6) + f) >> 2;  // (slot f - 64 of the next chunk = generation g + 1's slot)
     if (f == kChunk + kChunk / 2) {  // half of the next chunk claimed: open the one after it
       const uint32_t n2 = route2_take(taken, capl);
-      if (n2 != kStOvf) cm_put(n2, q, cl, cmeta, c0);
+      if (n2 != kStOvf) cmeta[c0 + n2] = q | (kChunk << 24);
       route2_advance(&s_state[q], g, n2, n2, false, old + 1);
     }
   } else if (cu == kStNone && f == 2 * kChunk) {  // q's first claim: open two chunks
     const uint32_t n1 = route2_take(taken, capl);
     const uint32_t n2 = n1 == kStOvf ? kStOvf : route2_take(taken, capl);
-    if (n1 != kStOvf) cm_put(n1, q, cl, cmeta, c0);
-    if (n2 != kStOvf) cm_put(n2, q, cl, cmeta, c0);
+    if (n1 != kStOvf) cmeta[c0 + n1] = q | (kChunk << 24);
+    if (n2 != kStOvf) cmeta[c0 + n2] = q | (kChunk << 24);
     route2_advance(&s_state[q], g, n1, n2, true, old + 1);
     if (n1 == kStOvf) r.ovf = true;
     else r.dst = uint64_t(c0 + n1) * kChunk;
@@ -736,19 +697,10 @@ __global__ __launch_bounds__(kR2WG, 1) void route2_kernel(RouteParams rp) {
 #if !NMG_R2COAL
   __shared__ uint2 s_tab[kWaves][64];
 #endif
-#if NMG_R2CMLIST
-  __shared__ uint32_t s_cml[kWaves][kCmList], s_cmn[kWaves];  // queued chunk tags (cm_put)
-#endif
 
   Params& p = rp.p;
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
-#if NMG_R2CMLIST
-  const CmList cml{s_cml[wave], &s_cmn[wave]};
-  if (lane == 0) s_cmn[wave] = 0;
-#else
-  const CmList cml{nullptr, nullptr};
-#endif
   if (tid < (int)kRouteSegs) {
     const RSeg g = rp.seg[tid];
     s_seg[tid].a = make_uint4((uint32_t)g.start, (uint32_t)(g.start >> 32), g.base, g.nslots);
@@ -1032,7 +984,7 @@ __global__ __launch_bounds__(kR2WG, 1) void route2_kernel(RouteParams rp) {
 #pragma unroll
       for (int r = 0; r < N; r++) {
         if (X[r].routed) {
-          const Claim c = route2_settle(old[r], X[r].q, s_state, s_taken, capl, rp.cmeta, c0, cml);
+          const Claim c = route2_settle(old[r], X[r].q, s_state, s_taken, capl, rp.cmeta, c0);
           dst[r] = c.dst;
           lid[r] = c.lid;
           ovf[r] = c.ovf;
@@ -1049,7 +1001,7 @@ __global__ __launch_bounds__(kR2WG, 1) void route2_kernel(RouteParams rp) {
           for (int r = 0; r < N; r++) {
             if (!todo[r]) continue;
             if (!spin[r]) {
-              const Claim c = route2_settle(atomicAdd(&s_state[X[r].q], 1ull), X[r].q, s_state, s_taken, capl, rp.cmeta, c0, cml);
+              const Claim c = route2_settle(atomicAdd(&s_state[X[r].q], 1ull), X[r].q, s_state, s_taken, capl, rp.cmeta, c0);
               dst[r] = c.dst;
               lid[r] = c.lid;
               ovf[r] = c.ovf;
@@ -1066,7 +1018,6 @@ __global__ __launch_bounds__(kR2WG, 1) void route2_kernel(RouteParams rp) {
       rt_stamp<TIMING>(rt, 5);
       // ---- the line stage (see the comment above kR2WG)
       bool staged[N], counts[N];
-      bool merged_any = false;  // the records stored alone went out with the line write-out
 #pragma unroll
       for (int r = 0; r < N; r++) staged[r] = counts[r] = false;
       if (__ballot(any_of(lined))) {
@@ -1107,7 +1058,6 @@ __global__ __launch_bounds__(kR2WG, 1) void route2_kernel(RouteParams rp) {
           dmask[r] = counts[r] ? lw_mask(o[r]) | (staged[r] ? 1u << ((uint32_t)dst[r] & 3u) : 0u) : 0u;
           if (TIMING) rt.acc[8] += (uint64_t)__popcll(__ballot(counts[r] && !staged[r]));
         }
-        bool merged = false;  // (N == 1, NMG_R2MERGEOUT) the records stored alone went with the write-out
 #pragma unroll
         for (int r = 0; r < N; r++) {
           const uint64_t dm = __ballot(done[r]);
@@ -1137,32 +1087,7 @@ __global__ __launch_bounds__(kR2WG, 1) void route2_kernel(RouteParams rp) {
               }
             }
           };
-          uint32_t j0 = 0;
-          if constexpr (N == 1 && NMG_R2MERGEOUT) {
-            // the lanes that store no record of their own take the first lines'
-            // pieces (whole lines only), and one store instruction carries both
-            const bool al = dst[0] != ~0ull && !(counts[0] && staged[0]) && !(counts[0] && !NMG_R2ONESTORE);
-            const uint64_t am = __ballot(al);
-            const uint32_t rk = (uint32_t)__popcll(~am & ((1ull << lane) - 1));
-            const uint32_t nfit = min(nd, (64u - (uint32_t)__popcll(am)) / 4u);
-            const bool pc = !al && rk < 4 * nfit;
-            uint64_t sa = dst[0];
-            uint4 sd = X[0].a;
-            bool act = al && !NMG_ABL_NOSCATTER;
-            uint2 t = make_uint2(0, 0);
-            if (pc) {
-              t = s_tab[wave][rk >> 2];
-              const uint32_t tq = t.x & 2047u, tm = (t.x >> 11) & 15u, k = rk & 3;
-              sa = uint64_t(t.y) * 4 + k;
-              sd = s_line[tq * 4 + k];
-              act = (tm >> k) & 1;
-            }
-            if (act) rp.rec16[sa] = sd;
-            if (pc) piece_done(t, rk & 3);
-            j0 = nfit;
-            merged = true;
-          }
-          for (; j0 < nd; j0 += 16) {
+          for (uint32_t j0 = 0; j0 < nd; j0 += 16) {
             const uint32_t jj = j0 + ((uint32_t)lane >> 2);
             if (jj < nd) {
               const uint2 t = s_tab[wave][jj];
@@ -1176,7 +1101,6 @@ __global__ __launch_bounds__(kR2WG, 1) void route2_kernel(RouteParams rp) {
           __builtin_amdgcn_wave_barrier();
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
         }
-        merged_any = merged;
       }
       rt_stamp<TIMING>(rt, 9);
 #pragma unroll
@@ -1187,7 +1111,7 @@ __global__ __launch_bounds__(kR2WG, 1) void route2_kernel(RouteParams rp) {
         // stored here too -- one store instruction for every record stored
         // alone; nothing reads the slots before the local pass)
         const bool alone = straight || (NMG_R2ONESTORE && counts[r] && !staged[r] && dst[r] != ~0ull);
-        if (alone && !merged_any && !NMG_ABL_NOSCATTER) rp.rec16[dst[r]] = X[r].a;
+        if (alone && !NMG_ABL_NOSCATTER) rp.rec16[dst[r]] = X[r].a;
         if (TIMING) {  // (records staged / stored straight to their slot)
           rt.acc[6] += (uint64_t)__popcll(__ballot(staged[r]));
           rt.acc[7] += (uint64_t)__popcll(__ballot(straight));
@@ -1211,7 +1135,6 @@ __global__ __launch_bounds__(kR2WG, 1) void route2_kernel(RouteParams rp) {
         }
         vm_drain();  // (rare: nothing of this path stays pending where it joins the window)
       }
-      if (NMG_R2CMLIST) cm_flush(cml, rp.cmeta, c0, lane, kCmFlush);
       rt_stamp<TIMING>(rt, 10);
     };
 
@@ -1231,10 +1154,7 @@ __global__ __launch_bounds__(kR2WG, 1) void route2_kernel(RouteParams rp) {
       back(X);
     } while (d0.pad != kNoBuf);
 #endif
-    if (NMG_R2CMLIST) {  // the tags still queued, stored before the fills below overwrite some of them
-      cm_flush(cml, rp.cmeta, c0, lane, 1);
-      vm_drain();
-    }
+
     if (TIMING && lane == 0) {
       unsigned long long* o = p.dbg + (uint64_t(blockIdx.x) * (kWG / 64) + tid / 64) * kRouteTimingWords;
       for (int k = 0; k < 9; k++) o[k] = rt.acc[k];
