@@ -314,7 +314,8 @@ def main_one_process(args):
     shard = sum(x.nbytes for x in bufs) // RECORD_BYTES
     log(f"[1 process, {n} GPUs] {args.workload}: shard of {shard} records in {len(bufs)} buffers, generated in "
         f"{time.time() - t0:.1f}s; every GPU analyses one copy of it")
-    eng = Engine(devices=[0] * n if same else list(range(n)), nb_threads=rp.nb_threads, copy_threads=16)
+    devices = [0] * n if same else list(range(n))
+    eng = Engine(devices=devices, nb_threads=rp.nb_threads, copy_threads=16)
     eng.set_objects(rp.table)
     subs = [(b.thread_rank, b.access_type, x) for b, x in zip(rp.buffers, bufs) if x.shape[0]]
     for _ in range(n):  # N shards in analysis order; the handle cuts them into N byte-balanced ranges
@@ -327,7 +328,7 @@ def main_one_process(args):
 
     def barrier():
         eng.synchronize()
-        for d in range(n):
+        for d in sorted(set(devices)):
             torch.cuda.synchronize(d)
 
     elapsed, steps = timed_run(W(), args.steps, args.warmup, barrier)
