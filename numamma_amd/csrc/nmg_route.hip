@@ -50,6 +50,12 @@
 #ifndef NMG_R2FSV  // route pass: the table's first key held in vector registers (A/B)
 #define NMG_R2FSV 0
 #endif
+#ifndef NMG_ABL_VNOP  // (ablation only: v_nop / dependent s_add_u32 instructions inserted per window)
+#define NMG_ABL_VNOP 0
+#endif
+#ifndef NMG_ABL_SNOP
+#define NMG_ABL_SNOP 0
+#endif
 #ifndef NMG_ABL_NOSCATTER  // (ablation only, results wrong: no record stored outside the line stage)
 #define NMG_ABL_NOSCATTER 0
 #endif
@@ -983,6 +989,14 @@ __global__ __launch_bounds__(kR2WG, 1) void route2_kernel(RouteParams rp) {
       // (mem_sampling.c:882: every SAMPLE, matched or not), partition, chunk
       // slot, store
       rt_stamp<TIMING>(rt, 1);
+#pragma unroll
+      for (int k = 0; k < NMG_ABL_VNOP; k++) asm volatile("v_nop");
+      if (NMG_ABL_SNOP) {
+        uint32_t dmy = __builtin_amdgcn_readfirstlane(cur);
+#pragma unroll
+        for (int k = 0; k < NMG_ABL_SNOP; k++) asm volatile("s_add_u32 %0, %0, 1" : "+s"(dmy));
+        asm volatile("" ::"s"(dmy));
+      }
       const uint32_t acc_l = dw.access();
       MmPend mmp;
       if (acc_l == 0) {  // (uniform)
