@@ -35,27 +35,6 @@
 #ifndef NMG_LOCAL_ONEMATCH  // local pass: one store instruction for a chunk group's match bits (shipped: 1)
 #define NMG_LOCAL_ONEMATCH 1
 #endif
-#ifndef NMG_R2SEG4  // route pass: three segment-start compares when the table has <= 4 segments (A/B)
-#define NMG_R2SEG4 0
-#endif
-#ifndef NMG_R2PBDEAD  // route pass: the partition's start and settled bit read together (A/B)
-#define NMG_R2PBDEAD 0
-#endif
-#ifndef NMG_R2NOFENCE  // route pass: no wait between the LDS line write and the line-word count (A/B)
-#define NMG_R2NOFENCE 0
-#endif
-#ifndef NMG_R2MMEARLY  // route pass: the counters' LDS minimum / maximum read before the search (A/B)
-#define NMG_R2MMEARLY 0
-#endif
-#ifndef NMG_R2FSV  // route pass: the table's first key held in vector registers (A/B)
-#define NMG_R2FSV 0
-#endif
-#ifndef NMG_ABL_VNOP  // (ablation only: v_nop / dependent s_add_u32 instructions inserted per window)
-#define NMG_ABL_VNOP 0
-#endif
-#ifndef NMG_ABL_SNOP
-#define NMG_ABL_SNOP 0
-#endif
 #ifndef NMG_ABL_NOSCATTER  // (ablation only, results wrong: no record stored outside the line stage)
 #define NMG_ABL_NOSCATTER 0
 #endif
@@ -287,26 +266,10 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
 // record's first group is read from LDS and updated by an LDS atomic only when
 // the record moves it (NMG_R2LDSMM=0: kept in the lane's registers until the
 // drain instead -- measured no faster).
-// (NMG_R2MMEARLY) the LDS minimum / maximum of a record's first group, read
-// in the counting and compared after the partition search: the two reads
-// share the search's first wait
-struct MmPend {
-  unsigned long long mn, mx;
-  uint32_t fb;
-  bool on;
-};
-template <uint32_t ACC>
-__device__ __forceinline__ void route_mm_finish(const MmPend& m, unsigned long long (*mins)[18],
-                                                unsigned long long (*maxs)[18], uint64_t w) {
-  if (m.on) {
-    if (w < m.mn) atomicMin(&mins[ACC][m.fb], (unsigned long long)w);
-    if (w > m.mx) atomicMax(&maxs[ACC][m.fb], (unsigned long long)w);
-  }
-}
 template <uint32_t ACC>
 __device__ __forceinline__ void route_count(RouteAcc& a, unsigned long long (*sums)[kGlobalSums],
                                             unsigned long long (*mins)[18], unsigned long long (*maxs)[18],
-                                            bool valid, uint32_t lvl, uint64_t w, MmPend& pend) {
+                                            bool valid, uint32_t lvl, uint64_t w) {
   const uint32_t cls = rt_class(lvl);
   const bool big = w >= (1u << 16);
   const uint32_t term = (valid && !big) ? (uint32_t)w + kRtOne : 0u;
@@ -320,13 +283,7 @@ __device__ __forceinline__ void route_count(RouteAcc& a, unsigned long long (*su
     gm |= in ? 1u << g : 0u;
   }
   const uint32_t fb = gm ? (kRtBucketNib >> (4 * __builtin_ctz(gm))) & 15u : 0xffu;
-  pend.on = false;
-#if NMG_R2MMEARLY
-  pend.on = valid && gm && !big;
-  pend.fb = fb;
-  pend.mn = pend.on ? mins[ACC][fb] : 0ull;
-  pend.mx = pend.on ? maxs[ACC][fb] : 0ull;
-#elif NMG_R2LDSMM  // read the LDS minimum / maximum, an atomic when the record moves it
+#if NMG_R2LDSMM  // read the LDS minimum / maximum, an atomic when the record moves it
   if (valid && gm && !big) {
     const unsigned long long mn = mins[ACC][fb], mx = maxs[ACC][fb];
     if (w < mn) atomicMin(&mins[ACC][fb], (unsigned long long)w);
@@ -585,22 +542,11 @@ struct SegL {
 __device__ __forceinline__ uint32_t route_partition_l(const SegL* s_seg, const uint64_t* s_segst, uint32_t nseg,
                                                       const uint64_t* s_pb, const uint16_t* s_pdir, uint64_t addr) {
   uint32_t k = 0;
-#if NMG_R2SEG4
-  if (nseg <= 4) {  // (uniform) the common case: globals, heap, mmap'd regions, stack
-    uint64_t st[4];
+  uint64_t st[kRouteSegs];
 #pragma unroll
-    for (uint32_t j = 1; j < 4; j++) st[j] = s_segst[j];
+  for (uint32_t j = 1; j < kRouteSegs; j++) st[j] = s_segst[j];
 #pragma unroll
-    for (uint32_t j = 1; j < 4; j++) k += (uint32_t)(addr >= st[j]);
-  } else
-#endif
-  {
-    uint64_t st[kRouteSegs];
-#pragma unroll
-    for (uint32_t j = 1; j < kRouteSegs; j++) st[j] = s_segst[j];
-#pragma unroll
-    for (uint32_t j = 1; j < kRouteSegs; j++) k += (uint32_t)(addr >= st[j]);
-  }
+  for (uint32_t j = 1; j < kRouteSegs; j++) k += (uint32_t)(addr >= st[j]);
   k = min(k, nseg - 1);  // (addr = ~0 passes the unused starts too)
   const uint4 ak = s_seg[k].a, bk = s_seg[k].b;
   const uint64_t s0 = u64of(ak.x, ak.y);
@@ -762,19 +708,7 @@ __global__ __launch_bounds__(kR2WG, 1) void route2_kernel(RouteParams rp) {
     s_segst[tid] = tid < rp.nseg ? g.start : ~0ull;
   }
   const uint32_t nseg = rp.nseg;
-#if NMG_R2FSV
-  // (in vector registers: as a scalar kernel argument the compiler reloads it
-  // every window, and that load's wait drains the LDS operations in flight)
-  uint64_t first_start;
-  {
-    uint32_t lo, hi;
-    asm volatile("v_mov_b32 %0, %1" : "=v"(lo) : "s"((uint32_t)rp.seg[0].start));
-    asm volatile("v_mov_b32 %0, %1" : "=v"(hi) : "s"((uint32_t)(rp.seg[0].start >> 32)));
-    first_start = u64of(lo, hi);
-  }
-#else
   const uint64_t first_start = rp.seg[0].start;
-#endif
   const uint32_t P = rp.nparts;
   const uint32_t c0 = rp.chunk0[blockIdx.x];
   const uint32_t cap = rp.chunk0[blockIdx.x + 1] - c0;
@@ -989,20 +923,11 @@ __global__ __launch_bounds__(kR2WG, 1) void route2_kernel(RouteParams rp) {
       // (mem_sampling.c:882: every SAMPLE, matched or not), partition, chunk
       // slot, store
       rt_stamp<TIMING>(rt, 1);
-#pragma unroll
-      for (int k = 0; k < NMG_ABL_VNOP; k++) asm volatile("v_nop");
-      if (NMG_ABL_SNOP) {
-        uint32_t dmy = __builtin_amdgcn_readfirstlane(cur);
-#pragma unroll
-        for (int k = 0; k < NMG_ABL_SNOP; k++) asm volatile("s_add_u32 %0, %0, 1" : "+s"(dmy));
-        asm volatile("" ::"s"(dmy));
-      }
       const uint32_t acc_l = dw.access();
-      MmPend mmp;
       if (acc_l == 0) {  // (uniform)
-        route_count<0>(gacc[0], s_gsums, s_gmins, s_gmaxs, valid, uint32_t(rec.dsrc >> 5) & 0x3fff, rec.w, mmp);
+        route_count<0>(gacc[0], s_gsums, s_gmins, s_gmaxs, valid, uint32_t(rec.dsrc >> 5) & 0x3fff, rec.w);
       } else {
-        route_count<1>(gacc[1], s_gsums, s_gmins, s_gmaxs, valid, uint32_t(rec.dsrc >> 5) & 0x3fff, rec.w, mmp);
+        route_count<1>(gacc[1], s_gsums, s_gmins, s_gmaxs, valid, uint32_t(rec.dsrc >> 5) & 0x3fff, rec.w);
       }
       if (++gwin == kRouteDrain) {
         racc_drain(gacc[0], s_gsums[0], s_gmins[0], s_gmaxs[0], lane);
@@ -1013,31 +938,15 @@ __global__ __launch_bounds__(kR2WG, 1) void route2_kernel(RouteParams rp) {
       // below the first key ht_lower_key finds no node: counted, not routed
       bool routed = valid && rec.addr >= first_start;
       const uint32_t q = routed ? route_partition_l(s_seg, s_segst, nseg, s_pb, s_pdir, rec.addr) : 0u;
-#if NMG_R2PBDEAD
-      const uint64_t pbq = s_pb[q];  // (q = 0 when not routed: a valid index)
-      const uint32_t dword = s_dead[q >> 5];
-#endif
-#if NMG_R2MMEARLY
-      if (acc_l == 0) route_mm_finish<0>(mmp, s_gmins, s_gmaxs, rec.w);
-      else route_mm_finish<1>(mmp, s_gmins, s_gmaxs, rec.w);
-#endif
       // a partition whose entries all have free_date 0 matches only timestamp-0
       // samples (RouteParams::pdead): the others are done (unmatched), not routed
-#if NMG_R2PBDEAD
-      routed = routed && (rec.ts == 0 || !((dword >> (q & 31)) & 1u));
-#else
       routed = routed && (rec.ts == 0 || !((s_dead[q >> 5] >> (q & 31)) & 1u));
-#endif
       if (TIMING) (void)__builtin_amdgcn_readfirstlane(__ballot(q != 0));  // (the search ends here)
       rt_stamp<TIMING>(rt, 3);
       X.a = make_uint4(0, 0, 0, 0);
       X.q = q;
       X.routed = routed;
-#if NMG_R2PBDEAD
-      if (routed) X.a = x_encode(rp.xl, pbq, rec.addr, rec.ts, rec.w, dw.pad, roff, dw.thread_rank(), acc_l);
-#else
       if (routed) X.a = x_encode(rp.xl, s_pb[q], rec.addr, rec.ts, rec.w, dw.pad, roff, dw.thread_rank(), acc_l);
-#endif
       rt_stamp<TIMING>(rt, 4);
     };
 
@@ -1129,9 +1038,8 @@ __global__ __launch_bounds__(kR2WG, 1) void route2_kernel(RouteParams rp) {
             if (!NMG_ABL_NOSCATTER) rp.rec16[dst[r]] = X[r].a;
           }
         }
-        // (the staged records before the counts that may complete their lines;
-        // NMG_R2NOFENCE: a wave's LDS operations are performed in order)
-        if (!NMG_R2NOFENCE) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+        // (the staged records before the counts that may complete their lines)
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
         LineWord o[N];
 #pragma unroll
         for (int r = 0; r < N; r++) {
