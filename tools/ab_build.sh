@@ -10,6 +10,7 @@ for f in nmg_kernels nmg_route nmg_engine nmg_table nmg_submit nmg_route_host nm
     -x hip -c csrc/$f.hip -o ../build_ab/obj_$NAME/$f.o &
 done
 wait
+for f in nmg_kernels nmg_route nmg_engine nmg_table nmg_submit nmg_route_host nmg_results nmg_multi; do [ -f ../build_ab/obj_$NAME/$f.o ] || { echo "compile of $f failed"; exit 1; }; done
 /opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o ../build_ab/lib_$NAME.so ../build_ab/obj_$NAME/*.o build/nmg_report.o \
   build/nmg_replay.o -L/opt/rocm/lib -lrocprofiler-sdk-roctx
 rm -rf ../build_ab/obj_$NAME
