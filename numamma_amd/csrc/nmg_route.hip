@@ -35,15 +35,6 @@
 #ifndef NMG_LOCAL_ONEMATCH  // local pass: one store instruction for a chunk group's match bits (shipped: 1)
 #define NMG_LOCAL_ONEMATCH 1
 #endif
-#ifndef NMG_R2LDPOL  // route pass: cache policy bits of the record loads (A/B: 2 = nt, 16 = sc1)
-#define NMG_R2LDPOL 0
-#endif
-#ifndef NMG_R2NTST  // route pass: compact records stored non-temporal (A/B)
-#define NMG_R2NTST 0
-#endif
-#ifndef NMG_LNTLD  // local pass: chunk loads non-temporal (A/B)
-#define NMG_LNTLD 0
-#endif
 #ifndef NMG_ABL_NOSCATTER  // (ablation only, results wrong: no record stored outside the line stage)
 #define NMG_ABL_NOSCATTER 0
 #endif
@@ -442,16 +433,6 @@ __device__ __forceinline__ RDesc route_desc(const RouteParams& rp, const uint4* 
 // partition's last, or a given-up one -- is written out, the slots it
 // holds, after the workgroup's last barrier.
 
-// a compact record to its chunk slot
-__device__ __forceinline__ void rec_store(uint4* p, uint4 v) {
-#if NMG_R2NTST
-  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-  __builtin_nontemporal_store(__builtin_bit_cast(u32x4, v), reinterpret_cast<u32x4*>(p));
-#else
-  *p = v;
-#endif
-}
-
 // route2_kernel's workgroup: 12 waves (three per SIMD)
 constexpr uint32_t kR2WG = NMG_R2WG;
 // line stage: partitions q < kLineParts have an LDS line
@@ -497,9 +478,9 @@ __device__ __forceinline__ void wload(const uint8_t* data, uint64_t off, uint32_
       __builtin_amdgcn_make_buffer_rsrc((void*)(data + off), (short)0, (int)len, 0x00020000);
   const uint32_t pos = c + uint32_t(lane) * kRecBytes;
   const uint32_t odd = (pos >> 3) & 1;  // 16 B aligned pieces, as load_rec
-  const auto x = __builtin_amdgcn_raw_buffer_load_b128(rs, pos + (odd ? 8 : 0), 0, NMG_R2LDPOL);
-  const auto y = __builtin_amdgcn_raw_buffer_load_b128(rs, pos + (odd ? 24 : 16), 0, NMG_R2LDPOL);
-  const auto z = __builtin_amdgcn_raw_buffer_load_b64(rs, pos + (odd ? 0 : 32), 0, NMG_R2LDPOL);
+  const auto x = __builtin_amdgcn_raw_buffer_load_b128(rs, pos + (odd ? 8 : 0), 0, 0);
+  const auto y = __builtin_amdgcn_raw_buffer_load_b128(rs, pos + (odd ? 24 : 16), 0, 0);
+  const auto z = __builtin_amdgcn_raw_buffer_load_b64(rs, pos + (odd ? 0 : 32), 0, 0);
   r.x = make_uint4(x[0], x[1], x[2], x[3]);
   r.y = make_uint4(y[0], y[1], y[2], y[3]);
   r.z = make_uint2(z[0], z[1]);
@@ -1111,7 +1092,7 @@ __global__ __launch_bounds__(kR2WG, 1) void route2_kernel(RouteParams rp) {
             if (jj < nd) {
               const uint2 t = s_tab[wave][jj];
               const uint32_t tq = t.x & 2047u, tm = (t.x >> 11) & 15u, k = lane & 3;
-              if ((tm >> k) & 1) rec_store(rp.rec16 + uint64_t(t.y) * 4 + k, s_line[tq * 4 + k]);
+              if ((tm >> k) & 1) rp.rec16[uint64_t(t.y) * 4 + k] = s_line[tq * 4 + k];
               piece_done(t, k);
             }
           }
@@ -1130,7 +1111,7 @@ __global__ __launch_bounds__(kR2WG, 1) void route2_kernel(RouteParams rp) {
         // stored here too -- one store instruction for every record stored
         // alone; nothing reads the slots before the local pass)
         const bool alone = straight || (NMG_R2ONESTORE && counts[r] && !staged[r] && dst[r] != ~0ull);
-        if (alone && !NMG_ABL_NOSCATTER) rec_store(rp.rec16 + dst[r], X[r].a);
+        if (alone && !NMG_ABL_NOSCATTER) rp.rec16[dst[r]] = X[r].a;
         if (TIMING) {  // (records staged / stored straight to their slot)
           rt.acc[6] += (uint64_t)__popcll(__ballot(staged[r]));
           rt.acc[7] += (uint64_t)__popcll(__ballot(straight));
@@ -1559,13 +1540,7 @@ __global__ __launch_bounds__(kLWG, 1) void local_kernel(LocalParams lp) {
     const uint32_t nl = item.z - item.y;
     auto chunk_load = [&](uint32_t l, uint4& a) {  // the chunk at list position l (l >= nl: none; no branch)
       const uint32_t e = l < nl ? s_clist[l] : 0u;
-#if NMG_LNTLD
-      typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-      a = __builtin_bit_cast(uint4, __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(
-                                        lp.rec16 + uint64_t(e & ((1u << kChunkIdBits) - 1)) * kChunk + lane)));
-#else
       a = lp.rec16[uint64_t(e & ((1u << kChunkIdBits) - 1)) * kChunk + lane];
-#endif
     };
     // the kLC chunks at list positions l0, l0 + 1, ... (past the list: no valid lane)
     auto process = [&](uint32_t l0, const uint4 (&a16)[kLC]) {
