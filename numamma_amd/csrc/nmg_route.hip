@@ -35,9 +35,6 @@
 #ifndef NMG_LOCAL_ONEMATCH  // local pass: one store instruction for a chunk group's match bits (shipped: 1)
 #define NMG_LOCAL_ONEMATCH 1
 #endif
-#ifndef NMG_LPT  // plan pass: work items queued largest first (A/B)
-#define NMG_LPT 0
-#endif
 #ifndef NMG_ABL_NOSCATTER  // (ablation only, results wrong: no record stored outside the line stage)
 #define NMG_ABL_NOSCATTER 0
 #endif
@@ -1325,48 +1322,14 @@ __global__ __launch_bounds__(kWG) void plan_kernel(PlanParams r) {
     wn += s_wsum[1][w2];
   }
   const uint32_t tb = wt + it - (t0 + t1), nb = wn + in - (n0 + n1);
-#if NMG_LPT
-  // the items queued largest first (the local pass's workgroups take them in
-  // queue order: the last ones taken are the smallest, so the workgroups end
-  // close together): a counting sort over 64 size classes, largest class
-  // first, any order inside a class
-  constexpr uint32_t kLptBk = 64;
-  __shared__ uint32_t s_bk[kLptBk];
-  auto bucket = [](uint32_t size) { return (kItemChunks - size) * kLptBk / (kItemChunks + 1); };
-  if (tid < (int)kLptBk) s_bk[tid] = 0;
-  __syncthreads();
-  for (uint32_t k = 0; k < 2; k++) {
-    const uint32_t q = i0 + k, tot = k ? t1 : t0;
-    if (q >= P) break;
-    for (uint32_t j = 0; j * kItemChunks < tot; j++)
-      atomicAdd(&s_bk[bucket(min(tot, (j + 1) * kItemChunks) - j * kItemChunks)], 1u);
-  }
-  __syncthreads();
-  if (tid == 0) {
-    uint32_t run = 0;
-    for (uint32_t b = 0; b < kLptBk; b++) {
-      const uint32_t c = s_bk[b];
-      s_bk[b] = run;
-      run += c;
-    }
-  }
-  __syncthreads();
-#endif
   for (uint32_t k = 0; k < 2; k++) {
     const uint32_t q = i0 + k;
     if (q >= P) break;
     const uint32_t base = tb + (k ? t0 : 0u), ibase = nb + (k ? n0 : 0u), tot = k ? t1 : t0;
     r.pbase[q] = base;
-    for (uint32_t j = 0; j * kItemChunks < tot; j++) {
-      const uint32_t e = min(tot, (j + 1) * kItemChunks);
-#if NMG_LPT
-      const uint32_t slot = atomicAdd(&s_bk[bucket(e - j * kItemChunks)], 1u);
-#else
-      const uint32_t slot = ibase + j;
-#endif
-      r.items[slot] = make_uint4(q, base + j * kItemChunks, base + e,
-                                 tot <= kItemChunks ? 1u : 0u);  // .w: the partition's only item
-    }
+    for (uint32_t j = 0; j * kItemChunks < tot; j++)
+      r.items[ibase + j] = make_uint4(q, base + j * kItemChunks, base + min(tot, (j + 1) * kItemChunks),
+                                      tot <= kItemChunks ? 1u : 0u);  // .w: the partition's only item
   }
   if (tid == kWG - 1) {
     r.ctl[0] = wn + in;
