@@ -80,17 +80,7 @@ int route_pool(nmg_engine* h, const std::vector<BufDesc>& descs, uint32_t grid, 
     free_route_pool(h);
     h->route_pending = pending;
     const size_t cap = std::max<size_t>(tot, 1);
-#if NMG_REC16_CONTIG  // (A/B) the chunk pool physically contiguous when the driver can give it
-    if (hipExtMallocWithFlags(reinterpret_cast<void**>(&h->d_rec16), cap * kChunk * sizeof(uint4), hipDeviceMallocContiguous) != hipSuccess) {
-      (void)hipGetLastError();
-      fprintf(stderr, "nmg: contiguous chunk pool refused, plain hipMalloc\n");
-      HIP_TRY(h, hipMalloc(&h->d_rec16, cap * kChunk * sizeof(uint4)));
-    } else {
-      fprintf(stderr, "nmg: contiguous chunk pool of %zu bytes\n", (size_t)(cap * kChunk * sizeof(uint4)));
-    }
-#else
     HIP_TRY(h, hipMalloc(&h->d_rec16, cap * kChunk * sizeof(uint4)));
-#endif
     HIP_TRY(h, hipMalloc(&h->d_cmeta, cap * 4));
     HIP_TRY(h, hipMalloc(&h->d_cmatch, cap * 8));
     HIP_TRY(h, hipMalloc(&h->d_clist, cap * 4));
