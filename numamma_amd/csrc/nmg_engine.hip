@@ -129,70 +129,9 @@ void free_route_table(nmg_engine* h) {
   h->nparts = 0;
 }
 
-// Device memory for the chunk pool: a reserved address range mapped from
-// physical pieces of 2 MiB (pools up to 128 MiB) or 64 MiB (hipMemCreate +
-// hipMemMap), not hipMalloc.  The route pass scatters 64 B line writes over
-// every workgroup's open chunks; over such a mapping it ran 1.653 ms at the
-// c4 shard against 1.804 from hipMalloc (-8 %, both piece sizes; a physically
-// contiguous hipExtMallocWithFlags pool: 2.075), DESIGN.md §7.0r6.  Falls
-// back to hipMalloc where the driver refuses the mapping.
-hipError_t map_alloc(nmg_engine* h, void** dptr, size_t bytes, size_t* mapped) {
-  *mapped = 0;
-  *dptr = nullptr;
-  hipMemAllocationProp prop = {};
-  prop.type = hipMemAllocationTypePinned;
-  prop.location.type = hipMemLocationTypeDevice;
-  prop.location.id = h->device;
-  size_t gran = 0;
-  if (hipMemGetAllocationGranularity(&gran, &prop, hipMemAllocationGranularityRecommended) == hipSuccess && gran) {
-    const size_t want = bytes <= (128u << 20) ? (2u << 20) : (64u << 20);
-    const size_t piece = (std::max(want, gran) + gran - 1) / gran * gran;
-    const size_t total = (std::max<size_t>(bytes, 1) + piece - 1) / piece * piece;
-    void* va = nullptr;
-    if (hipMemAddressReserve(&va, total, piece, nullptr, 0) == hipSuccess) {
-      size_t done = 0;
-      bool ok = true;
-      for (; done < total && ok; done += piece) {
-        hipMemGenericAllocationHandle_t hd;
-        if (hipMemCreate(&hd, piece, &prop, 0) != hipSuccess) {
-          ok = false;
-          break;
-        }
-        ok = hipMemMap((char*)va + done, piece, 0, hd, 0) == hipSuccess;
-        (void)hipMemRelease(hd);  // (the mapping keeps the piece)
-        if (!ok) break;
-      }
-      hipMemAccessDesc acc = {};
-      acc.location = prop.location;
-      acc.flags = hipMemAccessFlagsProtReadWrite;
-      if (ok && hipMemSetAccess(va, total, &acc, 1) == hipSuccess) {
-        *dptr = va;
-        *mapped = total;
-        return hipSuccess;
-      }
-      if (done) (void)hipMemUnmap(va, done);
-      (void)hipMemAddressFree(va, total);
-    }
-  }
-  (void)hipGetLastError();
-  return hipMalloc(dptr, bytes ? bytes : 16);
-}
-
-void map_free(void* ptr, size_t mapped) {
-  if (!ptr) return;
-  if (!mapped) {
-    (void)hipFree(ptr);
-    return;
-  }
-  (void)hipMemUnmap(ptr, mapped);
-  (void)hipMemAddressFree(ptr, mapped);
-}
-
 // the per-analysis buffers of the partition-first path
 void free_route_pool(nmg_engine* h) {
-  map_free(h->d_rec16, h->rec16_mapped);
-  h->rec16_mapped = 0;
-  for (void* q : {(void*)h->d_cmeta, (void*)h->d_cmatch, (void*)h->d_clist,
+  for (void* q : {(void*)h->d_rec16, (void*)h->d_cmeta, (void*)h->d_cmatch, (void*)h->d_clist,
                   (void*)h->d_items, (void*)h->d_chunk0, (void*)h->d_used, (void*)h->d_pcnt, (void*)h->d_pbase,
                   (void*)h->d_ctl, (void*)h->d_ovf16, (void*)h->d_ovfx})
     (void)hipFree(q);

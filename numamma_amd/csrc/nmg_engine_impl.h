@@ -314,7 +314,6 @@ struct nmg_engine {
   uint32_t* d_pe_lrel = nullptr;  // [table entries] first packed LDS cell (online tables)
   uint32_t* d_pe_cmap = nullptr;  // packed cell -> histogram cell (online tables)
   uint4* d_rec16 = nullptr;       // chunk pool: [chunks][kChunk] (addr, ts) and X words
-  size_t rec16_mapped = 0;        // its mapped bytes (map_alloc); 0: from hipMalloc
   uint32_t* d_cmeta = nullptr;
   unsigned long long* d_cmatch = nullptr;
   uint32_t* d_clist = nullptr;
@@ -403,10 +402,6 @@ LookupSet take_lookup(nmg_engine* h);
 void put_lookup(nmg_engine* h, const LookupSet& l);
 void free_table(nmg_engine* h);
 hipError_t alloc_copy(nmg_engine* h, void** dptr, const void* src, size_t bytes);
-// device memory mapped from large physical pieces (see nmg_engine.hip); *mapped = the
-// bytes to pass to map_free, 0 when it fell back to hipMalloc (free with hipFree)
-hipError_t map_alloc(nmg_engine* h, void** dptr, size_t bytes, size_t* mapped);
-void map_free(void* ptr, size_t mapped);
 int check_table(nmg_engine* h, const uint64_t* keys, const uint32_t* entry_off, uint32_t nb_keys,
                        uint32_t n);
 int build_lookup(nmg_engine* h, const uint64_t* keys, const uint32_t* entry_off, uint32_t nb_keys,

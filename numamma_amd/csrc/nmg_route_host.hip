@@ -80,7 +80,7 @@ int route_pool(nmg_engine* h, const std::vector<BufDesc>& descs, uint32_t grid, 
     free_route_pool(h);
     h->route_pending = pending;
     const size_t cap = std::max<size_t>(tot, 1);
-    HIP_TRY(h, map_alloc(h, reinterpret_cast<void**>(&h->d_rec16), cap * kChunk * sizeof(uint4), &h->rec16_mapped));
+    HIP_TRY(h, hipMalloc(&h->d_rec16, cap * kChunk * sizeof(uint4)));
     HIP_TRY(h, hipMalloc(&h->d_cmeta, cap * 4));
     HIP_TRY(h, hipMalloc(&h->d_cmatch, cap * 8));
     HIP_TRY(h, hipMalloc(&h->d_clist, cap * 4));
